@@ -1,0 +1,234 @@
+"""Model abstraction (SURVEY §2.2 M1–M4, §2.3 G1–G3).
+
+* ``Model`` / ``RichModel`` — ``LIB/models/Model.scala:15-44``: a serializable descriptor;
+  ``open()`` loads the graph and opens a session on the subtask's device before the first
+  call, ``close()`` releases it.  Runtime fields are not pickled (the reference marks
+  them ``@transient``), so models can be shipped to worker processes as descriptors.
+* ``GraphMethod`` — ``LIB/graphs/GraphMethod.scala:8-36``: a typed method contract with a
+  ``name`` that must equal the SignatureDef ``method_name``.
+* ``ModelFunction`` — ``LIB/models/ModelFunction.scala:18-79``: binds (session, signature,
+  method) into a callable.  Calling it returns a context manager over the outputs
+  (``with model.fn(x) as y:``), the equivalent of the reference's lazy
+  ``ManagedResource``; ``fn.apply(x)`` returns outputs directly.
+* ``GraphLoader`` / ``DefaultGraphLoader`` / ``GraphDefGraphLoader`` — ``LIB/graphs/*``.
+* ``GenericModel`` — ``LIB/models/generic/GenericModel.scala:12-44``.
+"""
+from __future__ import annotations
+
+import abc
+import contextlib
+import logging
+from typing import Any, Callable, Mapping
+
+import torch
+
+from ..graph.graph import Graph
+from ..graph.session import Session
+from ..proto.messages import GraphDef, SignatureDef
+from ..types.codecs import to_graph_tensor
+from ..types.names import TensorName
+from ..utils import fs
+
+LOG = logging.getLogger("flink_tensorflow_amd.models")
+
+
+class Model(abc.ABC):
+    """Marker base for model descriptors (``Model[Self]``)."""
+
+    _TRANSIENT: tuple[str, ...] = ()
+
+    def __getstate__(self):
+        st = dict(self.__dict__)
+        for k in self._TRANSIENT:
+            st[k] = None
+        return st
+
+
+class RichModel(Model):
+    """A model with a lifecycle (``RichModel.open/close``)."""
+
+    def open(self) -> None:  # noqa: B027 - optional hook
+        pass
+
+    def close(self) -> None:  # noqa: B027 - optional hook
+        pass
+
+    @property
+    def is_open(self) -> bool:
+        return True
+
+    def __enter__(self):
+        self.open()
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+# ------------------------------------------------------------------ methods
+class GraphMethod(abc.ABC):
+    """Typed method: ``name`` + ``inputs(x) -> {signature key: tensor}`` +
+    ``outputs({key: tensor}) -> result``."""
+
+    name: str = ""
+
+    @abc.abstractmethod
+    def inputs(self, value) -> Mapping[str, Any]:
+        ...
+
+    @abc.abstractmethod
+    def outputs(self, tensors: Mapping[str, Any]):
+        ...
+
+
+class _Outputs(contextlib.AbstractContextManager):
+    """Holds a call's outputs; closing releases them (arena slots / HBM references)."""
+
+    def __init__(self, value):
+        self.value = value
+        self.closed = False
+
+    def __enter__(self):
+        return self.value
+
+    def __exit__(self, *a):
+        self.close()
+
+    def close(self):
+        self.value = None
+        self.closed = True
+
+
+class ModelFunction:
+    """``ModelFunction(session, signature_def, method)`` → callable."""
+
+    def __init__(self, session_provider: Callable[[], Session] | Session, signature_def: SignatureDef,
+                 method: GraphMethod, check_method_name: bool = True):
+        if check_method_name and method.name and signature_def.method_name != method.name:
+            raise ValueError(f"signature method name {signature_def.method_name!r} does not match "
+                             f"method {method.name!r}")
+        self._session = session_provider
+        self.signature_def = signature_def
+        self.method = method
+        self._fetch_keys = sorted(signature_def.outputs)
+        self._fetch_names = [str(TensorName.parse(signature_def.outputs[k].name)) for k in self._fetch_keys]
+
+    @property
+    def session(self) -> Session:
+        s = self._session
+        return s() if callable(s) and not isinstance(s, Session) else s
+
+    def feeds(self, value) -> dict[str, Any]:
+        sess = self.session
+        mapped = self.method.inputs(value)
+        feeds = {}
+        for key, info in self.signature_def.inputs.items():
+            if key not in mapped:
+                raise ValueError(f"missing input {key!r} for signature (expected {sorted(self.signature_def.inputs)})")
+            feeds[str(TensorName.parse(info.name))] = to_graph_tensor(mapped[key], device=sess.device)
+        return feeds
+
+    def run(self, value, run_metadata: bool = False):
+        sess = self.session
+        res = sess.run(self._fetch_names, self.feeds(value), run_metadata=run_metadata)
+        outs = res.outputs if run_metadata else res
+        out = self.method.outputs(dict(zip(self._fetch_keys, outs)))
+        if run_metadata:
+            return out, res.metadata
+        return out
+
+    def apply(self, value):
+        return self.run(value)
+
+    def __call__(self, value) -> _Outputs:
+        return _Outputs(self.run(value))
+
+
+# ------------------------------------------------------------------ graph loaders
+class GraphLoader(abc.ABC):
+    @abc.abstractmethod
+    def load(self) -> Graph:
+        ...
+
+
+class DefaultGraphLoader(GraphLoader):
+    """Reads a binary GraphDef from a (URI) path, with an optional import prefix."""
+
+    def __init__(self, path: str, prefix: str = ""):
+        self.path = path
+        self.prefix = prefix
+
+    def load(self) -> Graph:
+        data = fs.read_bytes(self.path)
+        g = Graph.from_graph_def(data, self.prefix)
+        LOG.info("loaded %s", self.path)
+        return g
+
+
+class GraphDefGraphLoader(GraphLoader):
+    """Loads an in-memory GraphDef; the prefix IS applied (reference ignores it, B4)."""
+
+    def __init__(self, graph_def: GraphDef | bytes, prefix: str = ""):
+        self.graph_def_bytes = graph_def if isinstance(graph_def, bytes) else graph_def.encode()
+        self.prefix = prefix
+
+    def load(self) -> Graph:
+        return Graph.from_graph_def(self.graph_def_bytes, self.prefix)
+
+
+# ------------------------------------------------------------------ generic model
+class GenericModel(RichModel):
+    """A model over an ad-hoc graph.  Subclasses provide ``graph_loader``."""
+
+    _TRANSIENT = ("_graph", "_session")
+
+    def __init__(self, device: str | torch.device | None = None):
+        self.device = device
+        self._graph: Graph | None = None
+        self._session: Session | None = None
+
+    @property
+    @abc.abstractmethod
+    def graph_loader(self) -> GraphLoader:
+        ...
+
+    def open(self) -> None:
+        if self._session is not None:
+            return
+        g = self.graph_loader.load()
+        try:
+            self._session = Session(g, device=self.device or default_device())
+            self._graph = g
+        except Exception:
+            self._graph = None
+            raise
+
+    def close(self) -> None:
+        if self._session is not None:
+            self._session.close()
+        self._session = None
+        self._graph = None
+
+    @property
+    def is_open(self) -> bool:
+        return self._session is not None
+
+    def session(self) -> Session:
+        if self._session is None:
+            raise RuntimeError(f"{type(self).__name__} is not open")
+        return self._session
+
+    @property
+    def graph(self) -> Graph:
+        if self._graph is None:
+            raise RuntimeError(f"{type(self).__name__} is not open")
+        return self._graph
+
+
+def default_device() -> torch.device:
+    """The subtask's device: ``cuda:LOCAL_RANK`` when a GPU is visible, else CPU."""
+    import os
+
+    if torch.cuda.is_available():
+        return torch.device("cuda", int(os.environ.get("LOCAL_RANK", torch.cuda.current_device())))
+    return torch.device("cpu")

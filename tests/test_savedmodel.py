@@ -1,0 +1,197 @@
+"""SavedModel / bundle / executor conformance on the half_plus_two fixture.
+
+Acceptance from SURVEY §7.2 step 1-2: the §2.9 facts (5 signatures, SaverDef, variables
+a/b/c = 0.5/2/3), a byte-identical bundle round trip, all 5 signatures executing, and the
+``DefaultSaverITCase`` save → mutate → restore sequence
+(``TST/.../io/DefaultSaverITCase.scala:21-53``).
+"""
+import os
+import shutil
+
+import pytest
+import torch
+
+from flink_tensorflow_amd.io import bundle
+from flink_tensorflow_amd.io.saver import DefaultSaver, Saver, VariableSaver
+from flink_tensorflow_amd.models import (ClassificationMethod, PredictMethod, RegressionMethod, SavedModelModel,
+                                         SignatureConstants, TensorFlowModel)
+from flink_tensorflow_amd.types import example, feature
+
+
+def test_metagraph_facts(half_plus_two):
+    m = SavedModelModel(half_plus_two)
+    mg = m.metagraph
+    assert list(mg.meta_info_def.tags) == ["serve"]
+    assert sorted(mg.signature_def) == ["classify_x_to_y", "regress_x2_to_y3", "regress_x_to_y", "regress_x_to_y2",
+                                        "serving_default"]
+    sd = mg.saver_def
+    assert (sd.filename_tensor_name, sd.save_tensor_name, sd.restore_op_name) == (
+        "save/Const:0", "save/Identity:0", "save/restore_all")
+    assert sd.max_to_keep == 5 and sd.sharded and sd.version == 2
+    assert mg.signature_def["regress_x_to_y"].method_name == SignatureConstants.REGRESS_METHOD_NAME
+    assert not m.is_open  # metagraph did not load the bundle (B7)
+
+
+def test_bundle_reads_variables(half_plus_two):
+    r = bundle.BundleReader(os.path.join(half_plus_two, "variables", "variables"))
+    vals = {k: float(v) for k, v in r.read_all().items()}
+    assert vals == {"a": 0.5, "b": 2.0, "c": 3.0}
+
+
+def test_bundle_roundtrip_byte_identical(half_plus_two, tmp_path):
+    src = os.path.join(half_plus_two, "variables", "variables")
+    t = bundle.BundleReader(src).read_all()
+    dst = str(tmp_path / "v")
+    bundle.save_tensors(dst, t)
+    for suffix in (".index", ".data-00000-of-00001"):
+        assert open(src + suffix, "rb").read() == open(dst + suffix, "rb").read()
+
+
+def test_bundle_detects_corruption(tmp_path):
+    p = str(tmp_path / "ck")
+    bundle.save_tensors(p, {"w": torch.arange(16, dtype=torch.float32), "s": __import__(
+        "flink_tensorflow_amd").types.StringTensor([b"ab", b"c"], (2,))})
+    assert bundle.BundleReader(p).read("s").tolist() == [b"ab", b"c"]
+    data = bytearray(open(p + ".data-00000-of-00001", "rb").read())
+    data[3] ^= 0xFF
+    open(p + ".data-00000-of-00001", "wb").write(bytes(data))
+    with pytest.raises(bundle.DataLossError):
+        bundle.BundleReader(p).read_all()
+    idx = bytearray(open(p + ".index", "rb").read())
+    idx[2] ^= 0xFF
+    open(p + ".index", "wb").write(bytes(idx))
+    with pytest.raises(bundle.DataLossError):
+        bundle.BundleReader(p)
+
+
+class HalfPlusTwo(TensorFlowModel):
+    """``TST/.../ml/HalfPlusTwo.scala:14-28``."""
+
+    def __init__(self, path):
+        super().__init__(device="cpu")
+        self._loader = TensorFlowModel.load(path, "serve")
+
+    @property
+    def loader(self):
+        return self._loader
+
+    def regress_x_to_y(self, x):
+        return self.function("regress_x_to_y", RegressionMethod()).apply(x)
+
+    def regress_x_to_y2(self, x):
+        return self.function("regress_x_to_y2", RegressionMethod()).apply(x)
+
+
+@pytest.fixture
+def model(half_plus_two):
+    m = HalfPlusTwo(half_plus_two)
+    m.open()
+    yield m
+    m.close()
+
+
+def test_all_five_signatures(model):
+    exs = [example(("x", feature(float(v))), ("x2", feature(float(v) * 10))) for v in range(4)]
+    y = model.regress_x_to_y(exs)
+    assert y.reshape(-1).tolist() == [2.0, 2.5, 3.0, 3.5]
+    assert model.regress_x_to_y2(exs).reshape(-1).tolist() == [3.0, 3.5, 4.0, 4.5]
+    y3 = model.function("regress_x2_to_y3", RegressionMethod()).apply(torch.tensor([[2.0], [4.0]]))
+    assert y3.reshape(-1).tolist() == [4.0, 5.0]
+    classes, scores = model.function("classify_x_to_y", ClassificationMethod()).apply(exs)
+    assert classes is None and scores.reshape(-1).tolist() == [2.0, 2.5, 3.0, 3.5]
+    out = model.function("serving_default", PredictMethod()).apply({"x": torch.tensor([[1.0]])})
+    assert out["y"].item() == 2.5
+    # x2 default (0.0) is applied when the feature is absent
+    exs_no_x2 = [example(("x", feature(1.0)))]
+    y3b = model.session().run("y3:0", {"tf_example:0": __import__("flink_tensorflow_amd").types.messages_to_tensor(exs_no_x2)})
+    assert y3b.item() == 3.0
+
+
+def test_model_function_context_manager_and_metadata(model):
+    fn = model.function("regress_x_to_y", RegressionMethod())
+    with fn([example(("x", feature(2.0)))]) as y:
+        assert y.item() == 3.0
+    out, md = fn.run([example(("x", feature(2.0)))], run_metadata=True)
+    names = [s.node_name for s in md.step_stats.dev_stats[0].node_stats]
+    assert "ParseExample/ParseExample" in names and "y" in names
+
+
+def test_method_name_mismatch_rejected(model):
+    with pytest.raises(ValueError):
+        model.function("serving_default", RegressionMethod())
+
+
+def test_double_open_rejected(model):
+    with pytest.raises(RuntimeError):
+        model.open()
+
+
+def _get_a(sess):
+    return sess.run("a:0").item()
+
+
+def _set_a(sess, v):
+    sess.run(targets=["a/Assign"], feed_dict={"a/initial_value:0": torch.tensor(v)})
+
+
+def test_default_saver_itcase(model, tmp_path):
+    """save(a=1) → set a=2 → restore → a == 1."""
+    sess = model.session()
+    saver = Saver.create(model.metagraph.saver_def)
+    assert isinstance(saver, DefaultSaver)
+    _set_a(sess, 1.0)
+    path = saver.save(sess, str(tmp_path / "model-0"))
+    assert path == str(tmp_path / "model-0")
+    assert os.path.exists(path + ".index") and os.path.exists(path + ".data-00000-of-00001")
+    _set_a(sess, 2.0)
+    assert _get_a(sess) == 2.0
+    saver.restore(sess, path)
+    assert _get_a(sess) == 1.0
+    # the temp shard dir of the sharded saver was merged away
+    assert not [d for d in os.listdir(tmp_path) if "_temp_" in d]
+
+
+def test_variable_saver(model, tmp_path):
+    sess = model.session()
+    vs = VariableSaver()
+    p = vs.save(sess, str(tmp_path / "vars"))
+    _set_a(sess, 9.0)
+    vs.restore(sess, p)
+    assert _get_a(sess) == 0.5
+
+
+def test_remote_fs_model_copy(half_plus_two):
+    from flink_tensorflow_amd.utils import fs
+
+    memfs = fs.get_fs("mem://x")[0]
+    for root, _, files in os.walk(half_plus_two):
+        for f in files:
+            full = os.path.join(root, f)
+            memfs.write_bytes("mem://models/hp2/" + os.path.relpath(full, half_plus_two), open(full, "rb").read())
+    m = SavedModelModel("mem://models/hp2", device="cpu")
+    assert "regress_x_to_y" in m.metagraph.signature_def
+    m.open()
+    try:
+        y = m.function("regress_x_to_y", RegressionMethod()).apply([example(("x", feature(4.0)))])
+        assert y.item() == 4.0
+    finally:
+        m.close()
+
+
+def test_pickled_model_is_a_descriptor(model):
+    import pickle
+
+    m2 = pickle.loads(pickle.dumps(model))
+    assert not m2.is_open
+    m2.open()
+    assert m2.regress_x_to_y([example(("x", feature(0.0)))]).item() == 2.0
+    m2.close()
+
+
+def test_asset_init_op_ran(model):
+    v = model.session().variables["filename_tensor"]
+    assert v.item() == b"foo.txt"
+
+
+def teardown_module(module):
+    shutil.rmtree("/tmp/ftm-none", ignore_errors=True)
