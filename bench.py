@@ -1,0 +1,156 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 bf16 image-classification stream, micro-batched.
+
+Metric (BASELINE.json): whole-node records/sec + p50 per-record latency, ResNet-50 stream,
+DP = number of GPUs (one process per GPU; launched by torch.distributed.run for N > 1).
+
+Each rank runs the framework's streaming inference path on its own GPU:
+
+  synthetic record source (decoded uint8 256x256x3 images, one record per image)
+    → MicroBatcher (max_batch = --batch)
+    → PipelinedGpuRunner: C++ gather into pinned slot → H2D on a side stream →
+      hipGraph replay of the compiled ResNet-50 plan (fused resize+normalize kernel,
+      29 implicit-GEMM MFMA convs with folded BN / fused residual+ReLU, pool, FC GEMM,
+      fused softmax+top-5) → D2H of top-5 labels/probabilities
+    → sink (per-record latency = result on host − record ingest)
+
+Weights: random init (no network); rank 0's compiled weights are RCCL-broadcast to every
+other rank (the DP model-distribution path).  A "step" is one micro-batch of --batch
+records per GPU (weak scaling).  W warmup steps, then exactly K timed steps bracketed by a
+barrier + device synchronize; the elapsed time is the MAX over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "records/sec (whole node) + p50 per-record latency, ResNet-50 stream DP=1/8"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="micro-batch (records per GPU per step)")
+    ap.add_argument("--image-hw", type=int, default=256, help="decoded source image size (resized to 224)")
+    ap.add_argument("--depth", type=int, default=3, help="pipeline slots")
+    ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
+    ap.add_argument("--pool", type=int, default=512, help="distinct synthetic images cycled by the source")
+    args = ap.parse_args()
+
+    import torch
+
+    from flink_tensorflow_amd.batching.engine import PipelinedGpuRunner
+    from flink_tensorflow_amd.graph.compiler import CompiledFunction
+    from flink_tensorflow_amd.graph.graph import Graph
+    from flink_tensorflow_amd.models.zoo.resnet import resnet50_flops_per_image, resnet50_graph_def
+    from flink_tensorflow_amd.parallel import comm
+
+    comm.init_distributed()
+    rank, ws, local = comm.world()
+    if ws != args.gpus:
+        if rank == 0:
+            print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={ws}; using WORLD_SIZE", file=sys.stderr)
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    B, HW = args.batch, args.image_hw
+    t0 = time.perf_counter()
+    gd = resnet50_graph_def(image_hw=(HW, HW), top_k=5, seed=0)
+    graph = Graph.from_graph_def(gd)
+    plan = CompiledFunction(graph, {"images:0": ((B, HW, HW, 3), "UINT8")}, ["top_k:0", "top_k:1"], dev,
+                            use_graph=not args.no_graph, strict=True)
+    # rank 0's weights to all ranks over RCCL; in-place, so the captured graph stays valid
+    nbytes = comm.broadcast_tensors(plan.params, src=0)
+    compile_s = time.perf_counter() - t0
+
+    rng = np.random.default_rng(1234 + rank)
+    pool = rng.integers(0, 256, size=(args.pool, HW, HW, 3), dtype=np.uint8)
+    records = [pool[i] for i in range(args.pool)]
+    runner = PipelinedGpuRunner({B: plan}, "images:0", lambda p: p.output_tensors(), (HW, HW, 3), torch.uint8,
+                                depth=args.depth, device=dev)
+
+    cursor = 0
+    lat = []
+    n_done = 0
+
+    def step(collect):
+        nonlocal cursor, n_done
+        batch = [records[(cursor + i) % args.pool] for i in range(B)]
+        cursor += B
+        now = time.perf_counter()
+        ts = np.full(B, now)
+        for r in runner.poll() + runner.submit(batch, ts):
+            n_done += r.n
+            if collect:
+                lat.append(r.latencies[: r.n])
+
+    for _ in range(args.warmup):
+        step(False)
+    for r in runner.drain():
+        pass
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    for r in runner.drain():
+        lat.append(r.latencies[: r.n])
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    elapsed_max = comm.all_reduce_scalar(elapsed, "max", device=dev)
+
+    lat_all = np.concatenate(lat) if lat else np.zeros(1)
+    p50 = float(np.percentile(lat_all, 50) * 1e3)
+    p99 = float(np.percentile(lat_all, 99) * 1e3)
+    p50s = comm.all_gather_object(p50)
+    per_gpu = B * args.steps / elapsed
+    total = ws * B * args.steps / elapsed_max
+    flops = resnet50_flops_per_image(224) * total
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(total, 1),
+            "unit": "records/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": f"synthetic decoded uint8 {HW}x{HW}x3 images, random-init weights",
+            "config": {"model": "ResNet-50 v1.5", "global_batch": B * ws, "seq_len": None,
+                       "parallelism": f"dp{ws}", "micro_batch_per_gpu": B, "input_hw": 224},
+            "p50_latency_ms": round(float(np.median(p50s)), 3),
+            "p99_latency_ms": round(p99, 3),
+            "per_gpu_records_per_s": round(per_gpu, 1),
+            "model_tflops_per_s": round(flops / 1e12, 1),
+            "compile_s": round(compile_s, 2),
+            "weights_broadcast_bytes": nbytes,
+            "plan": plan.summary(),
+        }
+        print(json.dumps(out), flush=True)
+    if comm.is_dist():
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,853 @@
+"""Graph compiler: lowers a (feeds → fetches) signature of a TF graph onto the CDNA4
+kernels for fixed input shapes, plans HBM buffers, and captures the launch sequence in
+a hipGraph (``torch.cuda.CUDAGraph`` is HIP graph capture on ROCm).
+
+This is the MI355X replacement of libtensorflow's session executor for the hot path
+(SURVEY §2.8 N2/N3, §7.3).  Passes:
+
+1. **prune** to the fetched subgraph, stopping at fed tensors;
+2. **constant folding** of everything that depends only on Const/variables (weights are
+   frozen into the plan; variables are read from the session at compile time);
+3. **fusion** (pattern match, TF semantics preserved):
+   * ``Conv2D → [BiasAdd | FusedBatchNorm]* → [Add(residual)] → [Relu|Relu6]`` → one
+     implicit-GEMM conv launch with BN folded into the weights and a bias+residual+act
+     epilogue;
+   * ``MatMul → [BiasAdd] → [Add] → [act]`` → one MFMA GEMM launch;
+   * ``uint8 feed → Cast → ResizeBilinear → Sub → Div|Mul`` → the fused preprocess kernel
+     (bf16 NHWC, channels padded to 8 for the stem conv);
+   * ``Mean(axes=[1,2])`` → global-avg-pool; ``MaxPool``/``AvgPool`` → pool kernel;
+   * ``Softmax [→ TopKV2]`` → fused softmax+top-k kernel;
+   * ``ConcatV2`` on channels → producers write straight into channel slices of one
+     buffer (no copy) when every producer is a kernel that supports it;
+   * everything else runs as captured PyTorch glue ops (logged; ``strict=True`` rejects).
+4. **memory planning**: liveness-based reuse of exact-size HBM buffers;
+5. **capture**: one hipGraph per (signature, batch size).
+
+Activations are bf16 NHWC on device; fetched outputs are cast back to the graph dtype.
+"""
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass, field
+from typing import Any, Callable
+
+import numpy as np
+import torch
+
+from ..ops import kernels as K
+from ..types.dtypes import DataType
+from ..types.names import TensorName
+from ..types.tensor import StringTensor
+from . import ops_core  # noqa: F401
+from .graph import Graph, Node
+from .op_registry import OpContext, lookup
+from .ops_nn import same_pads
+
+LOG = logging.getLogger("flink_tensorflow_amd.compiler")
+
+_ACTS = {"Relu": K.ACT_RELU, "Relu6": K.ACT_RELU6, "Sigmoid": K.ACT_SIGMOID, "Tanh": K.ACT_TANH}
+
+
+class CompileError(RuntimeError):
+    pass
+
+
+@dataclass
+class Val:
+    """A symbolic value in the plan."""
+
+    shape: tuple
+    dtype: torch.dtype
+    const: Any = None          # folded constant (host tensor / StringTensor)
+    buf: torch.Tensor | None = None
+    phys_c: int | None = None  # physical channel count when padded (stem input)
+    alias_of: "Val | None" = None
+    last_use: int = -1
+    concat_slot: tuple | None = None  # (target Val, channel offset) for concat-by-stride-write
+
+    @property
+    def is_const(self):
+        return self.const is not None
+
+
+@dataclass
+class Step:
+    name: str
+    kind: str
+    fn: Callable[[], None]
+    inputs: list = field(default_factory=list)
+    outputs: list = field(default_factory=list)
+
+
+class _ConstSession:
+    """Minimal session facade for folding constants through interpreter kernels."""
+
+    def __init__(self, variables):
+        self.variables = variables
+        self._const_cache = {}
+
+
+class CompiledFunction:
+    def __init__(self, graph: Graph, feeds: dict[str, tuple[tuple, Any]], fetches: list[str], device,
+                 variables: dict | None = None, use_graph: bool = True, strict: bool = False,
+                 topk_fetch: bool = True):
+        self.graph = graph
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            use_graph = False  # host plans run the fp32 reference ops (used by CPU tests)
+        self.feed_names = [str(TensorName.parse(f)) for f in feeds]
+        self.feed_specs = {str(TensorName.parse(f)): v for f, v in feeds.items()}
+        self.fetch_names = [str(TensorName.parse(f)) for f in fetches]
+        self.variables = variables or {}
+        self.strict = strict
+        self.steps: list[Step] = []
+        self.params: list[torch.Tensor] = []  # device weights/biases baked into the plan
+        self.glue_ops: list[str] = []
+        self.vals: dict[tuple[str, int], Val] = {}
+        self._pool: dict[int, list[torch.Tensor]] = {}
+        self._fused: set[str] = set()
+        self._const_sess = _ConstSession(self.variables)
+        self._input_bufs: dict[str, torch.Tensor] = {}
+        self._outputs: list = []
+        self._graph_obj: torch.cuda.CUDAGraph | None = None
+        import contextlib
+
+        with torch.cuda.device(self.device) if self.device.type == "cuda" else contextlib.nullcontext():
+            self._compile()
+            self._plan_memory_and_bind()
+            if use_graph:
+                self._capture()
+
+    # ================================================================== compile
+    def _compile(self):
+        g = self.graph
+        fed = {TensorName.parse(f) for f in self.feed_names}
+        fed_nodes = {f.name for f in fed}
+        needed, stack = set(), [TensorName.parse(f).name for f in self.fetch_names]
+        while stack:
+            n = stack.pop()
+            if n in needed:
+                continue
+            needed.add(n)
+            if n in fed_nodes:
+                continue
+            node = g[n]
+            stack.extend(s for s, _ in node.inputs)
+            stack.extend(node.control_inputs)
+        self.order = [n for n in g.topo_order(needed)]
+        self.needed = needed
+        # consumers restricted to the pruned subgraph
+        self.cons: dict[str, list[str]] = {}
+        for n in self.order:
+            for s, _ in g[n].inputs:
+                self.cons.setdefault(s, []).append(n)
+        for f in fed:
+            shape, dt = self.feed_specs[str(f)]
+            dt = DataType.of(dt).torch
+            self.vals[(f.name, f.index)] = Val(tuple(shape), dt)
+        # Lower in topological order, but defer a Conv2D/MatMul whose fused chain ends in a
+        # residual Add until the other Add operand has been lowered (DFS topo order often
+        # visits the main path before the shortcut branch).
+        pending: list[str] = []
+
+        def ready(n: str, allow_unfused: bool = False) -> bool:
+            node = g[n]
+            if any(src not in self.vals for src in node.inputs):
+                return False
+            return allow_unfused or node.op not in ("Conv2D", "MatMul") or self._residual_ready(node)
+
+        def drain(allow_unfused=False):
+            progress = True
+            while pending and progress:
+                progress = False
+                for p in list(pending):
+                    if p in self._fused:
+                        pending.remove(p)
+                        progress = True
+                    elif ready(p, allow_unfused):
+                        pending.remove(p)
+                        self._lower(g[p])
+                        progress = True
+
+        for name in self.order:
+            if name in fed_nodes or name in self._fused:
+                continue
+            if not ready(name):
+                pending.append(name)
+                continue
+            self._lower(g[name])
+            drain()
+        while pending:  # residual fusion impossible for what is left: lower unfused
+            before = len(pending)
+            drain(allow_unfused=True)
+            if len(pending) == before:
+                raise CompileError(f"cannot schedule nodes {pending[:5]}")
+        for f in self.fetch_names:
+            tn = TensorName.parse(f)
+            if (tn.name, tn.index) not in self.vals:
+                raise CompileError(f"fetch {f} was not produced by the plan")
+
+    # ------------------------------------------------------------------ helpers
+    def _in(self, node: Node, i: int) -> Val:
+        s, k = node.inputs[i]
+        v = self._get((s, k))
+        if v is None:
+            raise CompileError(f"input {s}:{k} of {node.name} not available")
+        return v
+
+    def _get(self, src: tuple[str, int]) -> Val | None:
+        v = self.vals.get(src)
+        return v if v is not None else self._const_val(src)
+
+    def _single_consumer(self, name: str) -> Node | None:
+        c = self.cons.get(name, [])
+        fetched = any(TensorName.parse(f).name == name for f in self.fetch_names)
+        if len(c) != 1 or fetched:
+            return None
+        return self.graph[c[0]]
+
+    def _const_val(self, src: tuple[str, int]) -> Val | None:
+        """Value of ``src`` if it is (or can be folded to) a constant, folding on demand
+        (DFS topo order may reach a consumer before its constant operands)."""
+        v = self.vals.get(src)
+        if v is not None:
+            return v if v.is_const else None
+        node = self.graph.nodes.get(src[0])
+        if node is None or node.name not in self.needed:
+            return None
+        for s in node.inputs:
+            if self._const_val(s) is None:
+                return None
+        if node.op in ("Placeholder", "PlaceholderV2"):
+            return None
+        try:
+            ok = self._fold(node)
+        except CompileError:
+            return None
+        v = self.vals.get(src)
+        return v if ok and v is not None and v.is_const else None
+
+    def _residual_ready(self, node: Node) -> bool:
+        """True unless ``node``'s fusible chain contains an Add whose other operand is a
+        not-yet-lowered (non-constant) value."""
+        cur = node
+        for _ in range(8):
+            nxt = self._single_consumer(cur.name)
+            if nxt is None:
+                return True
+            if nxt.op in ("Add", "AddV2"):
+                other = [nxt.inputs[i] for i, (s, _) in enumerate(nxt.inputs) if s != cur.name]
+                if len(other) != 1:
+                    return True
+                src = other[0]
+                if src in self.vals:
+                    return True
+                # constants get folded when reached; only wait for computed values
+                return self.graph[src[0]].op in ("Const",)
+            if nxt.op in ("BiasAdd",) or nxt.op.startswith("FusedBatchNorm") or nxt.op in _ACTS:
+                cur = nxt
+                continue
+            return True
+        return True
+
+    def _fold(self, node: Node) -> bool:
+        """Constant-fold ``node`` if all its data inputs are constants."""
+        ins = [self.vals.get((s, k)) for s, k in node.inputs]
+        if node.op in ("Placeholder", "PlaceholderV2"):
+            raise CompileError(f"placeholder {node.name} must be fed")
+        if node.op in ("VariableV2", "Variable", "VarHandleOp"):
+            name = node.attr("shared_name") or node.name
+            v = self.variables.get(name)
+            if v is None:
+                raise CompileError(f"variable {name} is uninitialized at compile time")
+            self.vals[(node.name, 0)] = Val(tuple(v.shape), getattr(v, "dtype", None), const=_host(v))
+            return True
+        if any(v is None or not v.is_const for v in ins):
+            return False
+        ctx = OpContext(self._const_sess, torch.device("cpu"))
+        outs = lookup(node.op)(ctx, node, *[v.const for v in ins])
+        for k, o in enumerate(outs):
+            if isinstance(o, ops_core.VarRef):
+                o = o.read()
+            o = _host(o)
+            self.vals[(node.name, k)] = Val(tuple(o.shape), getattr(o, "dtype", None), const=o)
+        return True
+
+    def _new(self, shape, dtype=torch.bfloat16, phys_c=None) -> Val:
+        return Val(tuple(int(s) for s in shape), dtype, phys_c=phys_c)
+
+    def _emit(self, name, kind, fn, inputs, outputs):
+        self.steps.append(Step(name, kind, fn, list(inputs), list(outputs)))
+
+    # ------------------------------------------------------------------ lowering
+    def _lower(self, node: Node):
+        if self._fold(node):
+            return
+        op = node.op
+        if op == "Conv2D":
+            return self._lower_conv(node)
+        if op == "MatMul":
+            return self._lower_matmul(node)
+        if op == "Cast" and self._try_preprocess(node):
+            return
+        if op in ("MaxPool", "AvgPool"):
+            return self._lower_pool(node)
+        if op == "Mean":
+            if self._lower_mean(node):
+                return
+        if op == "Softmax":
+            return self._lower_softmax(node)
+        if op in ("Identity", "StopGradient", "Snapshot"):
+            self.vals[(node.name, 0)] = self._in(node, 0)
+            return
+        if op == "Reshape":
+            return self._lower_reshape(node)
+        if op == "ConcatV2":
+            return self._lower_concat(node)
+        if op == "NoOp":
+            return
+        return self._lower_glue(node)
+
+    # ---- conv chain
+    def _conv_chain(self, start: Node):
+        """Follows Conv2D/MatMul → BiasAdd/FusedBatchNorm* → Add(res)? → act? ."""
+        scale = None
+        bias = None
+        residual = None
+        act = K.ACT_NONE
+        cur = start
+        absorbed = []
+        while True:
+            nxt = self._single_consumer(cur.name)
+            if nxt is None:
+                break
+            if nxt.op in ("BiasAdd", "Add", "AddV2") and residual is None and act == K.ACT_NONE:
+                other = [i for i, (s, _) in enumerate(nxt.inputs) if s != cur.name]
+                if len(other) != 1:
+                    break
+                ov = self._get(nxt.inputs[other[0]])
+                if ov is not None and ov.is_const and ov.const.dim() == 1:
+                    b = ov.const.float()
+                    bias = b if bias is None else bias + b
+                elif nxt.op != "BiasAdd" and ov is not None and not ov.is_const:
+                    residual = (nxt, other[0])
+                else:
+                    break
+            elif nxt.op.startswith("FusedBatchNorm") and residual is None and act == K.ACT_NONE:
+                if nxt.attr("is_training", False):
+                    break
+                p = [self._get(nxt.inputs[i]) for i in range(1, 5)]
+                if not all(v is not None and v.is_const for v in p):
+                    break
+                g, b, m, v = (t.const.float() for t in p)
+                eps = nxt.attr("epsilon", 1e-3)
+                s = g * torch.rsqrt(v + eps)
+                shift = b - m * s
+                scale = s if scale is None else scale * s
+                bias = shift if bias is None else bias * s + shift
+                if any(c in self.cons.get(nxt.name, []) for c in []):
+                    break
+            elif nxt.op in _ACTS and act == K.ACT_NONE:
+                act = _ACTS[nxt.op]
+            else:
+                break
+            absorbed.append(nxt)
+            cur = nxt
+        return cur, scale, bias, residual, act, absorbed
+
+    def _lower_conv(self, node: Node):
+        x = self._in(node, 0)
+        wv = self._in(node, 1)
+        if not wv.is_const:
+            return self._lower_glue(node)
+        if node.attr("data_format", "NHWC") != "NHWC":
+            return self._lower_glue(node)
+        strides = node.attr("strides")
+        dil = node.attr("dilations") or [1, 1, 1, 1]
+        sh, sw = strides[1], strides[2]
+        dh, dw = dil[1], dil[2]
+        w = wv.const.float()  # HWIO
+        KH, KW, Cin, Cout = w.shape
+        N, H, W, C = x.shape
+        if C != Cin:
+            raise CompileError(f"{node.name}: input channels {C} != filter {Cin}")
+        padding = node.attr("padding", "SAME")
+        if padding == "SAME":
+            pt, pb = same_pads(H, KH, sh, dh)
+            pl, pr = same_pads(W, KW, sw, dw)
+        elif padding == "VALID":
+            pt = pb = pl = pr = 0
+        else:
+            return self._lower_glue(node)
+        last, scale, bias, residual, act, absorbed = self._conv_chain(node)
+        if scale is not None:
+            w = w * scale  # fold BN into the output channels
+        phys = x.phys_c or C
+        cin_pad = -(-phys // 8) * 8
+        w_ohwi = w.permute(3, 0, 1, 2).contiguous()
+        if cin_pad != Cin:
+            w_ohwi = torch.nn.functional.pad(w_ohwi, (0, cin_pad - Cin))
+        cout_pad = -(-Cout // 4) * 4
+        if cout_pad != Cout:
+            return self._lower_glue(node)
+        w_dev = w_ohwi.to(self.device, torch.bfloat16).contiguous()
+        b_dev = bias.to(self.device, torch.float32).contiguous() if bias is not None else None
+        self.params += [w_dev] + ([b_dev] if b_dev is not None else [])
+        Ho = (H + pt + pb - ((KH - 1) * dh + 1)) // sh + 1
+        Wo = (W + pl + pr - ((KW - 1) * dw + 1)) // sw + 1
+        out = self._new((N, Ho, Wo, Cout))
+        res_val = None
+        if residual is not None:
+            rn, ri = residual
+            res_val = self.vals[rn.inputs[ri]]
+        xin = self._ensure_padded(x, cin_pad, node.name)
+        for a in absorbed:
+            self._fused.add(a.name)
+
+        def run(xin=xin, out=out, res_val=res_val, w_dev=w_dev, b_dev=b_dev):
+            K.conv2d_nhwc(xin.buf, w_dev, b_dev, res_val.buf if res_val is not None else None, (sh, sw),
+                          (pt, pb, pl, pr), (dh, dw), act, out=_target(out), out_channel_offset=_coff(out))
+
+        self._emit(node.name, "conv", run, [xin] + ([res_val] if res_val else []), [out])
+        self.vals[(last.name, 0)] = out
+        self._alias_fused_outputs(absorbed, out)
+
+    def _alias_fused_outputs(self, absorbed, out):
+        for a in absorbed:
+            self.vals[(a.name, 0)] = out
+
+    def _ensure_padded(self, x: Val, cin_pad: int, name: str) -> Val:
+        phys = x.phys_c or x.shape[-1]
+        if phys == cin_pad and x.dtype == torch.bfloat16:
+            return x
+        y = self._new((*x.shape[:-1], cin_pad), phys_c=cin_pad)
+        c = x.shape[-1]
+
+        def run(x=x, y=y, c=c):
+            y.buf.zero_()
+            y.buf[..., :c].copy_(x.buf[..., :c])
+
+        self._emit(name + "/pad_cin", "glue", run, [x], [y])
+        return y
+
+    # ---- matmul chain
+    def _lower_matmul(self, node: Node):
+        a = self._in(node, 0)
+        b = self._in(node, 1)
+        if not b.is_const or node.attr("transpose_a", False) or len(a.shape) != 2:
+            return self._lower_glue(node)
+        wt = b.const.float()
+        w_nk = wt if node.attr("transpose_b", False) else wt.t()
+        N, Kd = w_nk.shape
+        if Kd % 8 or N % 4:
+            return self._lower_glue(node)
+        last, scale, bias, residual, act, absorbed = self._conv_chain(node)
+        if scale is not None:
+            w_nk = w_nk * scale[:, None]
+        w_dev = w_nk.to(self.device, torch.bfloat16).contiguous()
+        b_dev = bias.to(self.device, torch.float32).contiguous() if bias is not None else None
+        self.params += [w_dev] + ([b_dev] if b_dev is not None else [])
+        out = self._new((a.shape[0], N))
+        res_val = self.vals[residual[0].inputs[residual[1]]] if residual is not None else None
+        xin = self._as_bf16(a, node.name)
+        for n in absorbed:
+            self._fused.add(n.name)
+
+        def run(xin=xin, out=out, res_val=res_val, w_dev=w_dev, b_dev=b_dev):
+            K.gemm(xin.buf, w_dev, b_dev, res_val.buf if res_val is not None else None, act, out=out.buf)
+
+        self._emit(node.name, "gemm", run, [xin] + ([res_val] if res_val else []), [out])
+        self.vals[(last.name, 0)] = out
+        self._alias_fused_outputs(absorbed, out)
+
+    def _as_bf16(self, v: Val, name: str) -> Val:
+        if v.dtype == torch.bfloat16:
+            return v
+        y = self._new(v.shape)
+
+        def run(v=v, y=y):
+            y.buf.copy_(v.buf)
+
+        self._emit(name + "/to_bf16", "glue", run, [v], [y])
+        return y
+
+    # ---- preprocess: uint8 → Cast → ResizeBilinear → Sub → Div|Mul
+    def _try_preprocess(self, cast: Node) -> bool:
+        x = self._in(cast, 0)
+        if x.is_const or x.dtype != torch.uint8 or len(x.shape) != 4 or x.shape[3] != 3:
+            return False
+        chain = [cast]
+        cur = cast
+        size = None
+        mean = torch.zeros(3)
+        std = torch.ones(3)
+        align = half = False
+        nxt = self._single_consumer(cur.name)
+        if nxt is not None and nxt.op == "ResizeBilinear":
+            sv = self._get(nxt.inputs[1])
+            if sv is None or not sv.is_const:
+                return False
+            size = tuple(int(v) for v in sv.const.reshape(-1).tolist())
+            align = nxt.attr("align_corners", False)
+            half = nxt.attr("half_pixel_centers", False)
+            chain.append(nxt)
+            cur = nxt
+            nxt = self._single_consumer(cur.name)
+        if nxt is not None and nxt.op == "Sub":
+            mv = self._get(nxt.inputs[1])
+            if mv is not None and mv.is_const and nxt.inputs[0][0] == cur.name:
+                mean = mean + mv.const.float().reshape(-1).expand(3)
+                chain.append(nxt)
+                cur = nxt
+                nxt = self._single_consumer(cur.name)
+        if nxt is not None and nxt.op in ("Div", "RealDiv", "Mul"):
+            sv2 = self._get(nxt.inputs[1])
+            if sv2 is not None and sv2.is_const and nxt.inputs[0][0] == cur.name:
+                f = sv2.const.float().reshape(-1).expand(3)
+                std = std * f if nxt.op != "Mul" else std / f
+                chain.append(nxt)
+                cur = nxt
+        if size is None:
+            size = (x.shape[1], x.shape[2])
+        out = self._new((x.shape[0], size[0], size[1], 3), phys_c=8)
+        out_buf_shape = (x.shape[0], size[0], size[1], 8)
+        out.buf_shape = out_buf_shape
+        for n in chain[1:]:
+            self._fused.add(n.name)
+        mean_t, std_t = tuple(mean.tolist()), tuple(std.tolist())
+
+        def run(x=x, out=out):
+            K.preprocess_images(x.buf, size, mean_t, std_t, align, half, out=out.buf)
+
+        self._emit(cast.name + "/preprocess", "preprocess", run, [x], [out])
+        for n in chain:
+            self.vals[(n.name, 0)] = out
+        return True
+
+    # ---- pooling / reductions / softmax
+    def _lower_pool(self, node: Node):
+        x = self._in(node, 0)
+        if node.attr("data_format", "NHWC") != "NHWC" or (x.phys_c or x.shape[-1]) % 8:
+            return self._lower_glue(node)
+        k = node.attr("ksize")
+        s = node.attr("strides")
+        kh, kw, sh, sw = k[1], k[2], s[1], s[2]
+        N, H, W, C = x.shape
+        if node.attr("padding", "VALID") == "SAME":
+            pt, pb = same_pads(H, kh, sh)
+            pl, pr = same_pads(W, kw, sw)
+        else:
+            pt = pb = pl = pr = 0
+        Ho = (H + pt + pb - kh) // sh + 1
+        Wo = (W + pl + pr - kw) // sw + 1
+        out = self._new((N, Ho, Wo, C))
+        mode = "max" if node.op == "MaxPool" else "avg"
+        xin = self._as_bf16(x, node.name)
+
+        def run(xin=xin, out=out):
+            K.pool2d_nhwc(xin.buf, (kh, kw), (sh, sw), (pt, pb, pl, pr), mode, out=_target(out),
+                          out_channel_offset=_coff(out))
+
+        self._emit(node.name, "pool", run, [xin], [out])
+        self.vals[(node.name, 0)] = out
+
+    def _lower_mean(self, node: Node) -> bool:
+        x = self._in(node, 0)
+        av = self._get(node.inputs[1])
+        if av is None or not av.is_const or len(x.shape) != 4:
+            return False
+        axes = sorted(int(a) % 4 for a in av.const.reshape(-1).tolist())
+        if axes != [1, 2] or x.shape[-1] % 8:
+            return False
+        keep = node.attr("keep_dims", False)
+        N, H, W, C = x.shape
+        out = self._new((N, 1, 1, C) if keep else (N, C))
+        xin = self._as_bf16(x, node.name)
+
+        def run(xin=xin, out=out):
+            K.global_avgpool(xin.buf, out=out.buf.view(N, C))
+
+        self._emit(node.name, "gap", run, [xin], [out])
+        self.vals[(node.name, 0)] = out
+        return True
+
+    def _lower_softmax(self, node: Node):
+        x = self._in(node, 0)
+        if len(x.shape) != 2:
+            return self._lower_glue(node)
+        R, C = x.shape
+        xin = self._as_bf16(x, node.name)
+        topk = None
+        for c in self.cons.get(node.name, []):
+            cn = self.graph[c]
+            if cn.op == "TopKV2":
+                kv = self._get(cn.inputs[1])
+                if kv is not None and kv.is_const:
+                    topk = (cn, int(kv.const.item()))
+        probs = self._new((R, C))
+        k = topk[1] if topk else 1
+        vals = self._new((R, k), torch.float32)
+        idxs = self._new((R, k), torch.int32)
+
+        def run(xin=xin, probs=probs, vals=vals, idxs=idxs):
+            K.softmax_topk(xin.buf, k, want_probs=True, vals=vals.buf, idxs=idxs.buf, probs=probs.buf)
+
+        self._emit(node.name, "softmax_topk", run, [xin], [probs, vals, idxs])
+        self.vals[(node.name, 0)] = probs
+        if topk is not None:
+            self._fused.add(topk[0].name)
+            self.vals[(topk[0].name, 0)] = vals
+            self.vals[(topk[0].name, 1)] = idxs
+
+    def _lower_reshape(self, node: Node):
+        x = self._in(node, 0)
+        sv = self._get(node.inputs[1])
+        if sv is None or not sv.is_const or x.phys_c:
+            return self._lower_glue(node)
+        shape = [int(v) for v in sv.const.reshape(-1).tolist()]
+        n = int(np.prod(x.shape))
+        if -1 in shape:
+            i = shape.index(-1)
+            rest = int(np.prod([s for j, s in enumerate(shape) if j != i]))
+            shape[i] = n // max(rest, 1)
+        out = Val(tuple(shape), x.dtype, alias_of=x)
+        self.vals[(node.name, 0)] = out
+
+    def _lower_concat(self, node: Node):
+        ins = [self._in(node, i) for i in range(len(node.inputs) - 1)]
+        av = self._get(node.inputs[-1])
+        if av is None or not av.is_const:
+            return self._lower_glue(node)
+        axis = int(av.const.item()) % len(ins[0].shape)
+        shape = list(ins[0].shape)
+        shape[axis] = sum(v.shape[axis] for v in ins)
+        out = self._new(tuple(shape), ins[0].dtype)
+        stride_write = (axis == len(shape) - 1 and len(shape) == 4
+                        and all(self._concat_writable(v, node.inputs[i][0], node.name) for i, v in enumerate(ins)))
+        if stride_write:
+            off = 0
+            for v in ins:
+                v.concat_slot = (out, off)
+                off += v.shape[-1]
+            self.vals[(node.name, 0)] = out
+            out._concat_children = ins
+            return
+
+        def run(ins=ins, out=out, axis=axis):
+            torch.cat([v.buf for v in ins], dim=axis, out=out.buf)
+
+        self._emit(node.name, "concat", run, ins, [out])
+        self.vals[(node.name, 0)] = out
+
+    def _concat_writable(self, v: Val, src_node: str, concat_node: str) -> bool:
+        # produced by exactly one conv/pool step (which can write at a channel offset),
+        # consumed by nothing but this concat, and not fetched
+        prods = [s for s in self.steps if any(o is v for o in s.outputs)]
+        if len(prods) != 1 or prods[0].kind not in ("conv", "pool") or v.concat_slot is not None:
+            return False
+        if v.alias_of is not None or v.phys_c:
+            return False
+        # every graph node that maps to this value must feed only the concat
+        for (n, _), val in self.vals.items():
+            if val is v and any(c != concat_node for c in self.cons.get(n, [])):
+                return False
+            if val is v and any(TensorName.parse(f).name == n for f in self.fetch_names):
+                return False
+        return v.shape[-1] % 8 == 0 and v.dtype == torch.bfloat16 and src_node in self.cons
+
+    def _lower_glue(self, node: Node):
+        if self.strict:
+            raise CompileError(f"op {node.op} ({node.name}) has no CDNA4 lowering (strict mode)")
+        self.glue_ops.append(node.op)
+        LOG.info("glue op %s (%s) runs as a captured PyTorch op", node.op, node.name)
+        ins = [self.vals.get((s, k)) for s, k in node.inputs]
+        if any(v is None for v in ins):
+            raise CompileError(f"inputs of {node.name} not available")
+        fn = lookup(node.op)
+        # infer output shapes with a meta/CPU dry run on zeros
+        ctx = OpContext(self._const_sess, torch.device("cpu"))
+        probe = [v.const if v.is_const else torch.zeros(v.shape, dtype=torch.float32 if v.dtype == torch.bfloat16
+                                                          else v.dtype) for v in ins]
+        outs = fn(ctx, node, *probe)
+        outv = [self._new(o.shape, torch.bfloat16 if o.dtype == torch.float32 else o.dtype) for o in outs]
+        dev_consts = [None if not v.is_const else (v.const.to(self.device) if isinstance(v.const, torch.Tensor)
+                                                    else v.const) for v in ins]
+        dctx = OpContext(self._const_sess, self.device)
+
+        def run(node=node, ins=ins, outv=outv, dev_consts=dev_consts):
+            args = []
+            for v, dc in zip(ins, dev_consts):
+                if dc is not None:
+                    args.append(dc)
+                else:
+                    b = _view(v)
+                    args.append(b.float() if b.dtype == torch.bfloat16 else b)
+            res = fn(dctx, node, *args)
+            for o, r in zip(outv, res):
+                o.buf.copy_(r.reshape(o.buf.shape))
+
+        self._emit(node.name, "glue", run, [v for v in ins if not v.is_const], outv)
+        for k, o in enumerate(outv):
+            self.vals[(node.name, k)] = o
+
+    # ================================================================== memory
+    def _plan_memory_and_bind(self):
+        # feeds get dedicated input buffers
+        for f in self.feed_names:
+            tn = TensorName.parse(f)
+            v = self.vals[(tn.name, tn.index)]
+            v.buf = torch.empty(v.shape, dtype=v.dtype, device=self.device)
+            self._input_bufs[f] = v.buf
+        fetch_vals = [self.vals[(TensorName.parse(f).name, TensorName.parse(f).index)] for f in self.fetch_names]
+        for i, s in enumerate(self.steps):
+            for v in s.inputs:
+                _root(v).last_use = max(_root(v).last_use, i)
+        keep = {id(_root(v)) for v in fetch_vals}
+        for i, s in enumerate(self.steps):
+            for o in s.outputs:
+                r = _root(o)
+                if r.buf is None:
+                    tgt = r.concat_slot[0] if r.concat_slot else None
+                    if tgt is not None:
+                        if tgt.buf is None:
+                            tgt.buf = self._alloc(tgt.shape, tgt.dtype, keep_forever=id(tgt) in keep)
+                            tgt.last_use = max(tgt.last_use, max((c.last_use for c in getattr(tgt, "_concat_children", [])), default=-1))
+                        continue
+                    shape = getattr(r, "buf_shape", None) or (*r.shape[:-1], r.phys_c) if r.phys_c else r.shape
+                    r.buf = self._alloc(tuple(shape), r.dtype, keep_forever=id(r) in keep)
+            # release buffers whose last use is this step
+            for v in {id(_root(x)): _root(x) for x in s.inputs}.values():
+                if v.last_use == i and id(v) not in keep and v.buf is not None and not v.is_const \
+                        and not any(v is self.vals.get((TensorName.parse(f).name, TensorName.parse(f).index))
+                                    for f in self.feed_names):
+                    self._free(v.buf)
+        for v in self.vals.values():
+            if v.alias_of is not None:
+                r = _root(v)
+                if r.buf is not None:
+                    v.buf = r.buf.view(v.shape) if r.buf.is_contiguous() else r.buf.reshape(v.shape)
+        self._outputs = []
+        for fv in fetch_vals:
+            if fv.is_const:
+                self._outputs.append(fv.const)
+            else:
+                self._outputs.append(fv)
+
+    def _alloc(self, shape, dtype, keep_forever=False):
+        nbytes = int(np.prod(shape)) * torch.empty((), dtype=dtype).element_size()
+        lst = self._pool.get(nbytes)
+        if lst and not keep_forever:
+            raw = lst.pop()
+        else:
+            raw = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
+        return raw[:nbytes].view(dtype).view(shape)
+
+    def _free(self, buf: torch.Tensor):
+        raw = buf.view(-1).view(torch.uint8) if buf.numel() else None
+        if raw is not None:
+            self._pool.setdefault(raw.numel(), []).append(raw)
+
+    # ================================================================== execution
+    def _run_steps(self):
+        for s in self.steps:
+            s.fn()
+
+    def _capture(self):
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._run_steps()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._run_steps()
+        self._graph_obj = g
+
+    def input_buffer(self, feed: str) -> torch.Tensor:
+        return self._input_bufs[str(TensorName.parse(feed))]
+
+    def replay(self):
+        """Runs the plan on the current input buffers (no host synchronisation)."""
+        if self._graph_obj is not None:
+            self._graph_obj.replay()
+        else:
+            self._run_steps()
+
+    def __call__(self, feeds: dict | None = None, copy_outputs: bool = True, cast_outputs: bool = True):
+        for k, v in (feeds or {}).items():
+            buf = self.input_buffer(k)
+            if isinstance(v, StringTensor):
+                raise CompileError("STRING feeds are not supported in compiled plans")
+            buf.copy_(v, non_blocking=True)
+        self.replay()
+        outs = []
+        for o in self._outputs:
+            if isinstance(o, Val):
+                b = _view(o)
+                if cast_outputs and b.dtype == torch.bfloat16:
+                    b = b.float()
+                elif copy_outputs:
+                    b = b.clone()
+                outs.append(b)
+            else:
+                outs.append(o)
+        return outs
+
+    def output_tensors(self) -> list:
+        """The static device tensors holding the fetched values (valid after replay)."""
+        return [_view(o) if isinstance(o, Val) else o for o in self._outputs]
+
+    def param_bytes(self) -> int:
+        return sum(p.numel() * p.element_size() for p in self.params)
+
+    def summary(self) -> dict:
+        kinds: dict[str, int] = {}
+        for s in self.steps:
+            kinds[s.kind] = kinds.get(s.kind, 0) + 1
+        return {"steps": len(self.steps), "kinds": kinds, "glue_ops": sorted(set(self.glue_ops)),
+                "hip_graph": self._graph_obj is not None}
+
+
+def _root(v: Val) -> Val:
+    while v.alias_of is not None:
+        v = v.alias_of
+    return v
+
+
+def _view(v: Val) -> torch.Tensor:
+    r = _root(v)
+    if r.concat_slot is not None and r.buf is None:
+        tgt, off = r.concat_slot
+        return tgt.buf[..., off:off + r.shape[-1]]
+    b = r.buf
+    if r.phys_c and b.shape[-1] != r.shape[-1] and v is r:
+        return b
+    if v is not r:
+        return b.reshape(v.shape)
+    return b
+
+
+def _target(v: Val) -> torch.Tensor:
+    r = _root(v)
+    if r.concat_slot is not None:
+        return r.concat_slot[0].buf
+    return r.buf
+
+
+def _coff(v: Val) -> int:
+    r = _root(v)
+    return r.concat_slot[1] if r.concat_slot is not None else 0
+
+
+def _host(t):
+    if isinstance(t, torch.Tensor):
+        return t.detach().to("cpu")
+    return t
+
+
+def compile_signature(session, feeds: dict[str, tuple[tuple, Any]], fetches: list[str], use_graph=True,
+                      strict=False) -> CompiledFunction:
+    """Compiles ``session``'s graph for the given feed shapes on the session's GPU."""
+    return CompiledFunction(session.graph, feeds, fetches, session.device, session.variables, use_graph, strict)

@@ -1,0 +1,21 @@
+// pybind11 entry point of the `_hip` kernel library.  Each kernel TU exposes a
+// register_* function; launchers take raw device pointers + shapes + a hipStream_t
+// (passed as an integer from torch.cuda.current_stream().cuda_stream), so every launch
+// lands on the caller's stream and is captured by hipGraph capture.
+#include <pybind11/pybind11.h>
+
+void register_igemm(pybind11::module_& m);
+void register_nn_misc(pybind11::module_& m);
+void register_transformer(pybind11::module_& m);
+void register_embedding(pybind11::module_& m);
+void register_fp8(pybind11::module_& m);
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "flink_tensorflow_amd CDNA4 (gfx950) kernels";
+  m.attr("arch") = "gfx950";
+  register_igemm(m);
+  register_nn_misc(m);
+  register_transformer(m);
+  register_embedding(m);
+  register_fp8(m);
+}

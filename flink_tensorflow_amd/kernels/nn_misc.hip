@@ -1,0 +1,262 @@
+// Memory-bound CNN kernels for CDNA4: image preprocess, pooling, softmax+top-k.
+// Every kernel moves bf16 as 16-byte vectors (8 channels per lane) — guide Guideline 13.
+#include <pybind11/pybind11.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+
+namespace {
+
+// ------------------------------------------------------------------------------------
+// Fused preprocess: uint8 HWC image batch -> bilinear resize (TF ResizeBilinear
+// semantics) -> (v - mean[c]) * inv_std[c] -> bf16 NHWC with C padded to 8 (zeros), the
+// stem conv's input layout.  Replaces the reference's per-image
+// DecodeJpeg->Cast->ExpandDims->ResizeBilinear->Sub->Div graph
+// (EX/inception/ImageNormalization.scala:42-77) with one pass over the batch.
+// One thread per output pixel; the 3 channels of each of the 4 taps are 3 byte loads.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restrict__ src, bf16* __restrict__ dst,
+                                                         int B, int Hi, int Wi, int Ho, int Wo, float sy, float sx,
+                                                         int half_pixel, float m0, float m1, float m2, float s0,
+                                                         float s1, float s2, int src_stride) {
+  const int total = B * Ho * Wo;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int ox = idx % Wo;
+    const int t = idx / Wo;
+    const int oy = t % Ho;
+    const int b = t / Ho;
+    float fy = half_pixel ? (oy + 0.5f) * sy - 0.5f : oy * sy;
+    float fx = half_pixel ? (ox + 0.5f) * sx - 0.5f : ox * sx;
+    float fy0 = floorf(fy), fx0 = floorf(fx);
+    int y0 = max((int)fy0, 0), x0 = max((int)fx0, 0);
+    int y1 = min(y0 + 1, Hi - 1), x1 = min(x0 + 1, Wi - 1);
+    float wy = fminf(fmaxf(fy - (half_pixel ? (float)y0 : fy0), 0.f), 1.f);
+    float wx = fminf(fmaxf(fx - (half_pixel ? (float)x0 : fx0), 0.f), 1.f);
+    const uint8_t* img = src + (size_t)b * src_stride;
+    const uint8_t* p00 = img + ((size_t)y0 * Wi + x0) * 3;
+    const uint8_t* p01 = img + ((size_t)y0 * Wi + x1) * 3;
+    const uint8_t* p10 = img + ((size_t)y1 * Wi + x0) * 3;
+    const uint8_t* p11 = img + ((size_t)y1 * Wi + x1) * 3;
+    float out[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float top = (float)p00[c] + ((float)p01[c] - (float)p00[c]) * wx;
+      float bot = (float)p10[c] + ((float)p11[c] - (float)p10[c]) * wx;
+      out[c] = top + (bot - top) * wy;
+    }
+    bf16x8 o;
+    o[0] = f2bf((out[0] - m0) * s0);
+    o[1] = f2bf((out[1] - m1) * s1);
+    o[2] = f2bf((out[2] - m2) * s2);
+    o[3] = o[4] = o[5] = o[6] = o[7] = f2bf(0.f);
+    *reinterpret_cast<bf16x8*>(dst + (size_t)idx * 8) = o;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// 2-D pooling, NHWC bf16, TF semantics: MAX pads with -inf; AVG excludes padding from
+// the divisor.  One thread per (output pixel, 8-channel chunk).
+// ------------------------------------------------------------------------------------
+template <bool MAX>
+__global__ __launch_bounds__(256) void pool_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N, int H,
+                                                   int W, int C, int Ho, int Wo, int kh, int kw, int sh, int sw,
+                                                   int ph, int pw, int ldy, int y_coff) {
+  const int cchunks = C / 8;
+  const long total = (long)N * Ho * Wo * cchunks;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int cc = idx % cchunks;
+    long t = idx / cchunks;
+    const int ox = t % Wo;
+    t /= Wo;
+    const int oy = t % Ho;
+    const int n = t / Ho;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = MAX ? -INFINITY : 0.f;
+    int cnt = 0;
+    const int iy0 = oy * sh - ph, ix0 = ox * sw - pw;
+    for (int dy = 0; dy < kh; ++dy) {
+      const int iy = iy0 + dy;
+      if ((unsigned)iy >= (unsigned)H) continue;
+      for (int dx = 0; dx < kw; ++dx) {
+        const int ix = ix0 + dx;
+        if ((unsigned)ix >= (unsigned)W) continue;
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (((size_t)n * H + iy) * W + ix) * C + cc * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = MAX ? fmaxf(acc[e], (float)v[e]) : acc[e] + (float)v[e];
+        ++cnt;
+      }
+    }
+    bf16x8 o;
+    const float inv = MAX ? 1.f : 1.f / (float)max(cnt, 1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e] * inv);
+    *reinterpret_cast<bf16x8*>(y + (((size_t)n * Ho + oy) * Wo + ox) * ldy + y_coff + cc * 8) = o;
+  }
+}
+
+// Global average pool [N, HW, C] -> [N, C] (fp32 accumulate).  One block per image,
+// each thread owns 8 channels; loops over the HW positions with 16-B loads.
+__global__ __launch_bounds__(256) void global_avgpool_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int HW,
+                                                             int C) {
+  const int n = blockIdx.x;
+  const float inv = 1.f / (float)HW;
+  for (int cc = threadIdx.x; cc < C / 8; cc += blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const bf16* p = x + (size_t)n * HW * C + cc * 8;
+    for (int i = 0; i < HW; ++i) {
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(p + (size_t)i * C);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += (float)v[e];
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e] * inv);
+    *reinterpret_cast<bf16x8*>(y + (size_t)n * C + cc * 8) = o;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Row softmax fused with top-k (replaces the reference's host-side sort of the full
+// [M, N] label matrix, EX/inception/InceptionModel.scala:76-90).  One wave per row; the
+// row lives in registers (PER values per lane, strided by 64 for coalescing), so the
+// logits are read exactly once.  Outputs top-k probabilities (fp32) and class indices;
+// optionally the full probability row (bf16).
+// ------------------------------------------------------------------------------------
+template <int PER>
+__global__ __launch_bounds__(256) void softmax_topk_kernel(const bf16* __restrict__ logits, int rows, int C, int ld,
+                                                           int k, float* __restrict__ vals, int* __restrict__ idxs,
+                                                           bf16* __restrict__ probs) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const bf16* p = logits + (size_t)row * ld;
+  float v[PER];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < C ? (float)p[c] : -INFINITY;
+    mx = fmaxf(mx, v[i]);
+  }
+  mx = wave_reduce_max(mx);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    v[i] = (lane + 64 * i) < C ? __expf(v[i] - mx) : 0.f;
+    s += v[i];
+  }
+  s = wave_reduce_sum(s);
+  const float inv = 1.f / s;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) v[i] *= inv;
+  if (probs) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      if (c < C) probs[(size_t)row * C + c] = f2bf(v[i]);
+    }
+  }
+  for (int t = 0; t < k; ++t) {
+    float best = -1.f;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      if (c < C && (v[i] > best || (v[i] == best && c < bi))) {
+        best = v[i];
+        bi = c;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      float ob = __shfl_xor(best, o, 64);
+      int oi = __shfl_xor(bi, o, 64);
+      if (ob > best || (ob == best && oi < bi)) {
+        best = ob;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      vals[(size_t)row * k + t] = best;
+      idxs[(size_t)row * k + t] = bi;
+    }
+    // knock out the winner (owned by lane bi % 64, slot bi / 64)
+    if ((bi & 63) == lane) {
+#pragma unroll
+      for (int i = 0; i < PER; ++i)
+        if (i == (bi >> 6)) v[i] = -2.f;
+    }
+  }
+}
+
+int grid_for(long work, int block) {
+  long g = (work + block - 1) / block;
+  return (int)(g < 1 ? 1 : (g > 2048 * 8 ? 2048 * 8 : g));
+}
+
+}  // namespace
+
+void preprocess_u8_to_bf16(uintptr_t src, uintptr_t dst, int B, int Hi, int Wi, int Ho, int Wo, int align_corners,
+                           int half_pixel, float m0, float m1, float m2, float s0, float s1, float s2, int src_stride,
+                           uintptr_t stream) {
+  if (B <= 0 || Hi <= 0 || Wi <= 0 || Ho <= 0 || Wo <= 0) throw std::invalid_argument("preprocess: bad shape");
+  if (src_stride < Hi * Wi * 3) throw std::invalid_argument("preprocess: src_stride smaller than one image");
+  if (dst % 16) throw std::invalid_argument("preprocess: dst not 16-byte aligned");
+  float sy = (align_corners && Ho > 1) ? (float)(Hi - 1) / (Ho - 1) : (float)Hi / Ho;
+  float sx = (align_corners && Wo > 1) ? (float)(Wi - 1) / (Wo - 1) : (float)Wi / Wo;
+  long work = (long)B * Ho * Wo;
+  hipLaunchKernelGGL(preprocess_kernel, dim3(grid_for(work, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const uint8_t*>(src), reinterpret_cast<bf16*>(dst), B, Hi, Wi, Ho, Wo, sy, sx,
+                     half_pixel, m0, m1, m2, s0, s1, s2, src_stride);
+  FTM_CHECK_LAUNCH();
+}
+
+void pool2d_nhwc_bf16(uintptr_t x, uintptr_t y, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh,
+                      int sw, int ph, int pw, int is_max, int ldy, int y_coff, uintptr_t stream) {
+  if (C % 8 || ldy % 8 || y_coff % 8) throw std::invalid_argument("pool2d: C, ldy, y_coff must be multiples of 8");
+  if (x % 16 || y % 16) throw std::invalid_argument("pool2d: pointers must be 16-byte aligned");
+  long work = (long)N * Ho * Wo * (C / 8);
+  auto s = reinterpret_cast<hipStream_t>(stream);
+  if (is_max)
+    hipLaunchKernelGGL(pool_kernel<true>, dim3(grid_for(work, 256)), dim3(256), 0, s, reinterpret_cast<const bf16*>(x),
+                       reinterpret_cast<bf16*>(y), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, ldy, y_coff);
+  else
+    hipLaunchKernelGGL(pool_kernel<false>, dim3(grid_for(work, 256)), dim3(256), 0, s,
+                       reinterpret_cast<const bf16*>(x), reinterpret_cast<bf16*>(y), N, H, W, C, Ho, Wo, kh, kw, sh, sw,
+                       ph, pw, ldy, y_coff);
+  FTM_CHECK_LAUNCH();
+}
+
+void global_avgpool_bf16(uintptr_t x, uintptr_t y, int N, int HW, int C, uintptr_t stream) {
+  if (C % 8) throw std::invalid_argument("global_avgpool: C must be a multiple of 8");
+  if (x % 16 || y % 16) throw std::invalid_argument("global_avgpool: pointers must be 16-byte aligned");
+  hipLaunchKernelGGL(global_avgpool_kernel, dim3(N), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const bf16*>(x), reinterpret_cast<bf16*>(y), HW, C);
+  FTM_CHECK_LAUNCH();
+}
+
+void softmax_topk_bf16(uintptr_t logits, int rows, int C, int ld, int k, uintptr_t vals, uintptr_t idxs,
+                       uintptr_t probs, uintptr_t stream) {
+  if (k < 1 || k > C) throw std::invalid_argument("softmax_topk: k out of range");
+  if (C > 64 * 64) throw std::invalid_argument("softmax_topk: C > 4096 not supported");
+  dim3 grid((rows + 3) / 4), block(256);
+  auto s = reinterpret_cast<hipStream_t>(stream);
+  auto L = reinterpret_cast<const bf16*>(logits);
+  auto V = reinterpret_cast<float*>(vals);
+  auto I = reinterpret_cast<int*>(idxs);
+  auto P = reinterpret_cast<bf16*>(probs);
+  if (C <= 64 * 16) hipLaunchKernelGGL(softmax_topk_kernel<16>, grid, block, 0, s, L, rows, C, ld, k, V, I, P);
+  else if (C <= 64 * 32) hipLaunchKernelGGL(softmax_topk_kernel<32>, grid, block, 0, s, L, rows, C, ld, k, V, I, P);
+  else hipLaunchKernelGGL(softmax_topk_kernel<64>, grid, block, 0, s, L, rows, C, ld, k, V, I, P);
+  FTM_CHECK_LAUNCH();
+}
+
+void register_nn_misc(pybind11::module_& m) {
+  m.def("preprocess_u8_to_bf16", &preprocess_u8_to_bf16);
+  m.def("pool2d_nhwc_bf16", &pool2d_nhwc_bf16);
+  m.def("global_avgpool_bf16", &global_avgpool_bf16);
+  m.def("softmax_topk_bf16", &softmax_topk_bf16);
+}

@@ -1,0 +1,295 @@
+"""Python entry points of the hand-written CDNA4 kernels.
+
+Every op has exactly two implementations:
+
+* **HBM tensors (``cuda``)** → the gfx950 HIP kernel in ``_hip`` (``kernels/*.hip``).  If
+  the library is missing on a GPU machine the call raises — there is no silent PyTorch
+  fallback on the device path.
+* **host tensors** → a plain PyTorch fp32 reference with identical semantics, used by the
+  CPU test-suite and as the numerics oracle for the GPU tests.
+
+Shapes, dtypes, alignment and contiguity are validated on the host before any launch
+(a malformed launch can fault the whole GPU).  All launches go to the caller's current
+stream, so the ops are hipGraph-capturable.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .. import _ext
+
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_SIGMOID, ACT_TANH, ACT_RELU6 = 0, 1, 2, 3, 4, 5
+_ACT_NAMES = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU, "gelu_tanh": ACT_GELU,
+              "sigmoid": ACT_SIGMOID, "tanh": ACT_TANH, "relu6": ACT_RELU6}
+
+
+def act_code(act) -> int:
+    if isinstance(act, int):
+        return act
+    try:
+        return _ACT_NAMES[act]
+    except KeyError:
+        raise ValueError(f"unknown activation {act!r}") from None
+
+
+def _apply_act_ref(y: torch.Tensor, act: int) -> torch.Tensor:
+    if act == ACT_RELU:
+        return torch.relu(y)
+    if act == ACT_GELU:
+        return F.gelu(y, approximate="tanh")
+    if act == ACT_SIGMOID:
+        return torch.sigmoid(y)
+    if act == ACT_TANH:
+        return torch.tanh(y)
+    if act == ACT_RELU6:
+        return torch.clamp(y, 0, 6)
+    return y
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: torch.Tensor | None) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _check(t: torch.Tensor, name: str, dtype=torch.bfloat16, device=None):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name}: on {t.device}, expected {device}")
+
+
+def _hip():
+    return _ext.hip(required=True)
+
+
+# ------------------------------------------------------------------------------ conv
+def conv_out_hw(H, W, KH, KW, sh, sw, ph, pw, dh=1, dw=1, ph_hi=None, pw_hi=None):
+    ph_hi = ph if ph_hi is None else ph_hi
+    pw_hi = pw if pw_hi is None else pw_hi
+    Ho = (H + ph + ph_hi - ((KH - 1) * dh + 1)) // sh + 1
+    Wo = (W + pw + pw_hi - ((KW - 1) * dw + 1)) // sw + 1
+    return Ho, Wo
+
+
+def conv2d_nhwc(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor | None = None,
+                residual: torch.Tensor | None = None, stride=(1, 1), pad=(0, 0, 0, 0), dilation=(1, 1),
+                act=None, out: torch.Tensor | None = None, out_channel_offset: int = 0) -> torch.Tensor:
+    """NHWC conv, weights [Cout, KH, KW, Cin]; ``pad = (top, bottom, left, right)``.
+
+    Fused epilogue ``act(conv + bias + residual)``.  With ``out`` given, the result is
+    written at channel offset ``out_channel_offset`` of ``out`` (concat-by-stride-write).
+    """
+    a = act_code(act)
+    N, H, W, Cin = x.shape
+    Cout, KH, KW, Cin2 = w_ohwi.shape
+    if Cin2 != Cin:
+        raise ValueError(f"conv2d_nhwc: input has {Cin} channels, weights expect {Cin2}")
+    sh, sw = stride
+    pt, pb, pl, pr = pad
+    dh, dw = dilation
+    Ho, Wo = conv_out_hw(H, W, KH, KW, sh, sw, pt, pl, dh, dw, pb, pr)
+    if out is None:
+        out = torch.empty((N, Ho, Wo, Cout), dtype=x.dtype if x.is_cuda else torch.float32, device=x.device)
+        out_channel_offset = 0
+    if out.shape[:3] != (N, Ho, Wo) or out_channel_offset + Cout > out.shape[3]:
+        raise ValueError(f"conv2d_nhwc: out {tuple(out.shape)} cannot hold [{N},{Ho},{Wo},{Cout}] at "
+                         f"offset {out_channel_offset}")
+    if residual is not None and tuple(residual.shape) != (N, Ho, Wo, Cout):
+        raise ValueError(f"conv2d_nhwc: residual {tuple(residual.shape)} != {(N, Ho, Wo, Cout)}")
+    if x.is_cuda:
+        for t, n in ((x, "x"), (w_ohwi, "w"), (out, "out")):
+            _check(t, n, device=x.device)
+        if residual is not None:
+            _check(residual, "residual", device=x.device)
+        if bias is not None:
+            _check(bias, "bias", torch.float32, x.device)
+            if bias.numel() != Cout:
+                raise ValueError("conv2d_nhwc: bias size != Cout")
+        if (pt, pl) != (pb, pr) and (pb > pt or pr > pl):
+            # the kernel pads implicitly with the top/left offsets; bottom/right padding
+            # beyond that is implied by the bounds check as long as Ho/Wo match
+            pass
+        _hip().conv2d_nhwc_bf16(x.data_ptr(), w_ohwi.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(),
+                                N, H, W, Cin, Cout, KH, KW, sh, sw, pt, pl, dh, dw, Ho, Wo, out.shape[3],
+                                out_channel_offset, Cout if residual is None else residual.shape[3], a, _stream())
+        return out
+    # host reference
+    xn = x.float().permute(0, 3, 1, 2)
+    xn = F.pad(xn, (pl, pr, pt, pb))
+    y = F.conv2d(xn, w_ohwi.float().permute(0, 3, 1, 2), stride=(sh, sw), dilation=(dh, dw))
+    y = y.permute(0, 2, 3, 1)
+    if bias is not None:
+        y = y + bias.float()
+    if residual is not None:
+        y = y + residual.float()
+    y = _apply_act_ref(y, a)
+    out[..., out_channel_offset:out_channel_offset + Cout] = y.to(out.dtype)
+    return out
+
+
+def gemm(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = None, residual: torch.Tensor | None = None,
+         act=None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``act(x[M,K] @ w[N,K]^T + bias + residual)``; leading dims of x are flattened."""
+    a = act_code(act)
+    lead = x.shape[:-1]
+    K = x.shape[-1]
+    N, K2 = w_nk.shape
+    if K != K2:
+        raise ValueError(f"gemm: K mismatch {K} vs {K2}")
+    x2 = x.reshape(-1, K)
+    M = x2.shape[0]
+    if out is None:
+        out = torch.empty((*lead, N), dtype=x.dtype if x.is_cuda else torch.float32, device=x.device)
+    out2 = out.reshape(M, N)
+    if residual is not None and residual.numel() != M * N:
+        raise ValueError("gemm: residual shape mismatch")
+    if x.is_cuda:
+        _check(x2, "x", device=x.device)
+        _check(w_nk, "w", device=x.device)
+        _check(out2, "out", device=x.device)
+        if bias is not None:
+            _check(bias, "bias", torch.float32, x.device)
+        if residual is not None:
+            _check(residual, "residual", device=x.device)
+        _hip().gemm_bf16(x2.data_ptr(), w_nk.data_ptr(), _ptr(bias), _ptr(residual), out2.data_ptr(), M, N, K, K, N,
+                         N, a, _stream())
+        return out
+    y = x2.float() @ w_nk.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    if residual is not None:
+        y = y + residual.reshape(M, N).float()
+    out2.copy_(_apply_act_ref(y, a).to(out.dtype))
+    return out
+
+
+# ------------------------------------------------------------------------------ preprocess
+def preprocess_images(images_u8: torch.Tensor, out_hw=(224, 224), mean=(117.0, 117.0, 117.0),
+                      std=(1.0, 1.0, 1.0), align_corners=False, half_pixel_centers=False,
+                      out: torch.Tensor | None = None) -> torch.Tensor:
+    """uint8 [B,H,W,3] → resize (TF ResizeBilinear) → (v-mean)/std → bf16 [B,Ho,Wo,8]
+    (channels 3..7 zero: the stem conv's Cin=8 layout)."""
+    if images_u8.dtype != torch.uint8 or images_u8.dim() != 4 or images_u8.shape[3] != 3:
+        raise ValueError("preprocess_images expects uint8 [B,H,W,3]")
+    B, Hi, Wi, _ = images_u8.shape
+    Ho, Wo = out_hw
+    if out is None:
+        out = torch.empty((B, Ho, Wo, 8), dtype=torch.bfloat16 if images_u8.is_cuda else torch.float32,
+                          device=images_u8.device)
+    if tuple(out.shape) != (B, Ho, Wo, 8):
+        raise ValueError(f"preprocess_images: out must be {(B, Ho, Wo, 8)}")
+    if images_u8.is_cuda:
+        if not images_u8.is_contiguous():
+            raise ValueError("preprocess_images: input must be contiguous")
+        _check(out, "out", device=images_u8.device)
+        _hip().preprocess_u8_to_bf16(images_u8.data_ptr(), out.data_ptr(), B, Hi, Wi, Ho, Wo, int(align_corners),
+                                     int(half_pixel_centers), float(mean[0]), float(mean[1]), float(mean[2]),
+                                     1.0 / std[0], 1.0 / std[1], 1.0 / std[2], Hi * Wi * 3, _stream())
+        return out
+    from ..graph.ops_nn import resize_bilinear_tf
+
+    y = resize_bilinear_tf(images_u8.float(), Ho, Wo, align_corners, half_pixel_centers)
+    y = (y - torch.tensor(mean)) / torch.tensor(std)
+    out.zero_()
+    out[..., :3] = y.to(out.dtype)
+    return out
+
+
+# ------------------------------------------------------------------------------ pooling
+def pool2d_nhwc(x: torch.Tensor, ksize, stride, pad=(0, 0, 0, 0), mode="max", out=None, out_channel_offset=0):
+    N, H, W, C = x.shape
+    kh, kw = ksize
+    sh, sw = stride
+    pt, pb, pl, pr = pad
+    Ho = (H + pt + pb - kh) // sh + 1
+    Wo = (W + pl + pr - kw) // sw + 1
+    if out is None:
+        out = torch.empty((N, Ho, Wo, C), dtype=x.dtype, device=x.device)
+        out_channel_offset = 0
+    if x.is_cuda:
+        _check(x, "x", device=x.device)
+        _check(out, "out", device=x.device)
+        _hip().pool2d_nhwc_bf16(x.data_ptr(), out.data_ptr(), N, H, W, C, Ho, Wo, kh, kw, sh, sw, pt, pl,
+                                int(mode == "max"), out.shape[3], out_channel_offset, _stream())
+        return out
+    xn = x.float().permute(0, 3, 1, 2)
+    if mode == "max":
+        y = F.max_pool2d(F.pad(xn, (pl, pr, pt, pb), value=float("-inf")), (kh, kw), (sh, sw))
+    else:
+        s = F.avg_pool2d(F.pad(xn, (pl, pr, pt, pb)), (kh, kw), (sh, sw), divisor_override=1)
+        c = F.avg_pool2d(F.pad(torch.ones_like(xn[:, :1]), (pl, pr, pt, pb)), (kh, kw), (sh, sw), divisor_override=1)
+        y = s / c
+    out[..., out_channel_offset:out_channel_offset + C] = y.permute(0, 2, 3, 1).to(out.dtype)
+    return out
+
+
+def global_avgpool(x: torch.Tensor, out=None) -> torch.Tensor:
+    N, H, W, C = x.shape
+    if out is None:
+        out = torch.empty((N, C), dtype=x.dtype, device=x.device)
+    if x.is_cuda:
+        _check(x, "x", device=x.device)
+        _check(out, "out", device=x.device)
+        _hip().global_avgpool_bf16(x.data_ptr(), out.data_ptr(), N, H * W, C, _stream())
+        return out
+    out.copy_(x.float().mean((1, 2)).to(out.dtype))
+    return out
+
+
+# ------------------------------------------------------------------------------ softmax/top-k
+def softmax_topk(logits: torch.Tensor, k: int, want_probs: bool = False, vals=None, idxs=None, probs=None):
+    """Row softmax + top-k → (values fp32 [R,k], indices int32 [R,k], probs or None)."""
+    R, C = logits.shape
+    dev = logits.device
+    if vals is None:
+        vals = torch.empty((R, k), dtype=torch.float32, device=dev)
+    if idxs is None:
+        idxs = torch.empty((R, k), dtype=torch.int32, device=dev)
+    if want_probs and probs is None:
+        probs = torch.empty((R, C), dtype=logits.dtype, device=dev)
+    if logits.is_cuda:
+        if logits.stride(1) != 1:
+            raise ValueError("softmax_topk: logits rows must be contiguous")
+        _check(vals, "vals", torch.float32, dev)
+        _check(idxs, "idxs", torch.int32, dev)
+        _hip().softmax_topk_bf16(logits.data_ptr(), R, C, logits.stride(0), k, vals.data_ptr(), idxs.data_ptr(),
+                                 _ptr(probs), _stream())
+        return vals, idxs, probs
+    p = torch.softmax(logits.float(), -1)
+    v, i = torch.topk(p, k, -1)
+    vals.copy_(v)
+    idxs.copy_(i.to(torch.int32))
+    if probs is not None:
+        probs.copy_(p.to(probs.dtype))
+    return vals, idxs, probs
+
+
+# ------------------------------------------------------------------------------ layernorm
+def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, residual: torch.Tensor | None = None,
+              eps: float = 1e-12, out=None, sum_out=None) -> torch.Tensor:
+    """``LN(x + residual)``; optionally also writes the pre-norm sum to ``sum_out``."""
+    D = x.shape[-1]
+    rows = x.numel() // D
+    if out is None:
+        out = torch.empty_like(x)
+    if x.is_cuda:
+        _check(x, "x", device=x.device)
+        _check(out, "out", device=x.device)
+        _check(gamma, "gamma", torch.float32, x.device)
+        _check(beta, "beta", torch.float32, x.device)
+        if residual is not None:
+            _check(residual, "residual", device=x.device)
+        _hip().layernorm_bf16(x.data_ptr(), _ptr(residual), gamma.data_ptr(), beta.data_ptr(), out.data_ptr(),
+                              _ptr(sum_out), rows, D, float(eps), _stream())
+        return out
+    s = x.float() + (residual.float() if residual is not None else 0)
+    if sum_out is not None:
+        sum_out.copy_(s.to(sum_out.dtype))
+    out.copy_(F.layer_norm(s, (D,), gamma.float(), beta.float(), eps).to(out.dtype))
+    return out

@@ -1,0 +1,154 @@
+"""Numerics of the hand-written CDNA4 kernels vs plain PyTorch fp32 references.
+
+Inputs are generated in bf16 on the host; the reference runs the same bf16 values in
+fp32 on the CPU (``ops.kernels`` host path), the kernel runs on the GPU.  Tolerances are
+set by bf16 output rounding (8 significant bits) and fp32 accumulation-order noise.
+"""
+import pytest
+import torch
+
+from flink_tensorflow_amd.ops import kernels as K
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _close(got, ref, rtol=2e-2, atol_scale=2e-2):
+    got = got.float().cpu()
+    ref = ref.float().cpu()
+    atol = atol_scale * max(ref.abs().max().item(), 1e-3)
+    torch.testing.assert_close(got, ref, rtol=rtol, atol=atol)
+
+
+CONV_CASES = [
+    # N, H, W, Cin, Cout, K, stride, pad(t,b,l,r), act, residual, bias
+    (2, 56, 56, 64, 64, 1, 1, (0, 0, 0, 0), "relu", False, True),
+    (2, 56, 56, 64, 256, 1, 1, (0, 0, 0, 0), "none", True, True),
+    (2, 28, 28, 128, 128, 3, 1, (1, 1, 1, 1), "relu", False, True),
+    (2, 56, 56, 128, 128, 3, 2, (0, 1, 0, 1), "relu", False, True),
+    (2, 224, 224, 8, 64, 7, 2, (2, 3, 2, 3), "relu", False, True),
+    (3, 7, 7, 512, 2048, 1, 1, (0, 0, 0, 0), "relu", True, True),
+    (1, 14, 14, 256, 1000, 1, 1, (0, 0, 0, 0), "none", False, False),  # Cout tail
+    (2, 17, 17, 192, 160, 1, 7, (0, 0, 0, 0), "relu", False, True),
+    (2, 9, 11, 64, 96, 3, 1, (1, 1, 1, 1), "relu6", False, True),       # M tail
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv2d_nhwc(case):
+    N, H, W, Cin, Cout, k, s, pad, act, has_res, has_b = case
+    kh, kw = (k, k) if k != 7 or Cin == 8 else (1, 7)
+    if case[5] == 1 and case[6] == 7:  # the 1x7 Inception-style case
+        kh, kw, s = 1, 7, 1
+        pad = (0, 0, 3, 3)
+    g = torch.Generator().manual_seed(hash(case) % 1000)
+    x = torch.randn(N, H, W, Cin, generator=g).to(torch.bfloat16)
+    w = (torch.randn(Cout, kh, kw, Cin, generator=g) / (kh * kw * Cin) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, generator=g) if has_b else None
+    Ho, Wo = K.conv_out_hw(H, W, kh, kw, s, s, pad[0], pad[2], 1, 1, pad[1], pad[3])
+    r = torch.randn(N, Ho, Wo, Cout, generator=g).to(torch.bfloat16) if has_res else None
+    ref = K.conv2d_nhwc(x, w, b, r, (s, s), pad, (1, 1), act)
+    got = K.conv2d_nhwc(x.to(DEV), w.to(DEV), b.to(DEV) if b is not None else None,
+                        r.to(DEV) if r is not None else None, (s, s), pad, (1, 1), act)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape
+    _close(got, ref)
+
+
+def test_conv_identity_asymmetric():
+    """A = I check with an asymmetric B (guide §3): catches a transposed C-write."""
+    N, H, W, C = 1, 4, 4, 64
+    x = torch.arange(N * H * W * C, dtype=torch.float32).reshape(N, H, W, C).remainder(7).to(torch.bfloat16)
+    w = torch.eye(C).reshape(C, 1, 1, C).to(torch.bfloat16)
+    got = K.conv2d_nhwc(x.to(DEV), w.to(DEV))
+    assert torch.equal(got.cpu(), x)
+
+
+def test_conv_concat_slice_write():
+    x = torch.randn(2, 8, 8, 64).to(torch.bfloat16).to(DEV)
+    w1 = torch.randn(32, 1, 1, 64).to(torch.bfloat16).to(DEV)
+    w2 = torch.randn(64, 1, 1, 64).to(torch.bfloat16).to(DEV)
+    out = torch.zeros(2, 8, 8, 96, dtype=torch.bfloat16, device=DEV)
+    K.conv2d_nhwc(x, w1, out=out, out_channel_offset=0)
+    K.conv2d_nhwc(x, w2, out=out, out_channel_offset=32)
+    ref = torch.cat([K.conv2d_nhwc(x, w1), K.conv2d_nhwc(x, w2)], -1)
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("M,N,Kd,act", [(256, 1000, 2048, "none"), (77, 3072, 768, "gelu"), (5, 64, 64, "relu"),
+                                         (1024, 768, 3072, "none")])
+def test_gemm(M, N, Kd, act):
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, Kd, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, generator=g)
+    ref = K.gemm(x, w, b, None, act)
+    got = K.gemm(x.to(DEV), w.to(DEV), b.to(DEV), None, act)
+    _close(got, ref)
+
+
+@pytest.mark.parametrize("hw_in,hw_out,half", [((256, 256), (224, 224), False), ((224, 224), (224, 224), False),
+                                               ((300, 200), (224, 224), True)])
+def test_preprocess(hw_in, hw_out, half):
+    img = torch.randint(0, 256, (3, *hw_in, 3), dtype=torch.uint8)
+    mean, std = (123.68, 116.78, 103.94), (58.4, 57.12, 57.38)
+    ref = K.preprocess_images(img, hw_out, mean, std, False, half)
+    got = K.preprocess_images(img.to(DEV), hw_out, mean, std, False, half)
+    _close(got, ref, rtol=1e-2, atol_scale=1e-2)
+    assert (got[..., 3:] == 0).all()
+
+
+@pytest.mark.parametrize("mode,k,s,pad", [("max", 3, 2, (0, 1, 0, 1)), ("avg", 3, 1, (1, 1, 1, 1)),
+                                          ("max", 2, 2, (0, 0, 0, 0)), ("avg", 8, 8, (0, 0, 0, 0))])
+def test_pool(mode, k, s, pad):
+    x = torch.randn(2, 16, 16, 64).to(torch.bfloat16)
+    ref = K.pool2d_nhwc(x, (k, k), (s, s), pad, mode)
+    got = K.pool2d_nhwc(x.to(DEV), (k, k), (s, s), pad, mode)
+    _close(got, ref, rtol=1e-2, atol_scale=1e-2)
+
+
+def test_global_avgpool():
+    x = torch.randn(4, 7, 7, 2048).to(torch.bfloat16)
+    _close(K.global_avgpool(x.to(DEV)), K.global_avgpool(x), rtol=1e-2, atol_scale=1e-2)
+
+
+@pytest.mark.parametrize("C,k", [(1000, 5), (10, 3), (4096, 1)])
+def test_softmax_topk(C, k):
+    logits = (torch.randn(37, C) * 3).to(torch.bfloat16)
+    v_ref, i_ref, p_ref = K.softmax_topk(logits, k, want_probs=True)
+    v, i, p = K.softmax_topk(logits.to(DEV), k, want_probs=True)
+    _close(p, p_ref, rtol=1e-2, atol_scale=1e-2)
+    torch.testing.assert_close(v.cpu(), v_ref, rtol=1e-3, atol=1e-4)
+    # indices: equal except where probabilities tie in bf16
+    mism = (i.cpu() != i_ref)
+    if mism.any():
+        assert torch.allclose(p_ref.float().gather(1, i.cpu().long()), v_ref, atol=1e-3)
+
+
+@pytest.mark.parametrize("D", [768, 1024, 64])
+def test_layernorm(D):
+    x = torch.randn(33, D).to(torch.bfloat16)
+    r = torch.randn(33, D).to(torch.bfloat16)
+    gm, bt = torch.randn(D), torch.randn(D)
+    ref = K.layernorm(x, gm, bt, r)
+    got = K.layernorm(x.to(DEV), gm.to(DEV), bt.to(DEV), r.to(DEV))
+    _close(got, ref)
+
+
+def test_linear_autograd():
+    from flink_tensorflow_amd.ops.autograd import linear
+
+    x = torch.randn(64, 96).to(torch.bfloat16)
+    w = (torch.randn(32, 96) / 10).to(torch.bfloat16)
+    b = torch.randn(32)
+    xs = [x.clone().requires_grad_(True), x.to(DEV).requires_grad_(True)]
+    ws = [w.clone().float().requires_grad_(True), w.to(DEV).requires_grad_(True)]
+    bs = [b.clone().requires_grad_(True), b.to(DEV).requires_grad_(True)]
+    outs = []
+    for i in range(2):
+        y = linear(xs[i], ws[i] if i else ws[i].to(torch.bfloat16), bs[i], "relu")
+        y.float().sum().backward()
+        outs.append(y)
+    _close(outs[1], outs[0])
+    _close(xs[1].grad, xs[0].grad)
+    _close(bs[1].grad, bs[0].grad)
