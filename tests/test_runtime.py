@@ -1,0 +1,239 @@
+"""Streaming runtime: the reference's ITCases ported onto the local executor, plus the
+function kinds, windows, keyed state, co-processing, checkpoints and restarts that the
+reference declares but never tests."""
+import os
+import time
+
+import pytest
+import torch
+
+from flink_tensorflow_amd.models import RegressionMethod, TensorFlowModel
+from flink_tensorflow_amd.runtime import (PROCESS_ONCE, BytesInputFormat, CheckpointedFunction, CountWindows,
+                                          ListStateDescriptor, MemorySink, ModelAllWindowFunction,
+                                          ModelCoProcessFunction, ModelFlatMapFunction, ModelProcessFunction,
+                                          ModelWindowFunction, OutputTag, ProcessFunction, RestartStrategy,
+                                          RichFlatMapFunction, StreamExecutionEnvironment, ValueStateDescriptor,
+                                          register_types)
+from flink_tensorflow_amd.types import example, feature
+from flink_tensorflow_amd.utils.fault import FailAfter
+
+
+class HalfPlusTwo(TensorFlowModel):
+    def __init__(self, path):
+        super().__init__(device="cpu")
+        self._loader = TensorFlowModel.load(path, "serve")
+
+    @property
+    def loader(self):
+        return self._loader
+
+    def regress_x_to_y(self, exs):
+        return self.function("regress_x_to_y", RegressionMethod()).apply(exs)
+
+
+def examples():
+    return [(example(("x", feature(float(v)))), 0.5 * v + 2.0) for v in range(4)]
+
+
+class _RegressFlatMap(RichFlatMapFunction):
+    """RegressITCase's in-operator check (``TST/.../ml/RegressITCase.scala:46-62``)."""
+
+    def __init__(self, model):
+        super().__init__()
+        self.model = model
+
+    def open(self, config=None):
+        self.model.open()
+
+    def close(self):
+        self.model.close()
+
+    def flat_map(self, value, out):
+        ex, expected = value
+        y = self.model.regress_x_to_y([ex]).reshape(-1).tolist()
+        assert y == [expected], (y, expected)
+        out.collect(y[0])
+
+
+@pytest.mark.parametrize("parallelism", [1, 4])
+def test_regress_itcase(half_plus_two, parallelism):
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(parallelism)
+    register_types(env.get_config())
+    sink = env.from_collection(examples()).rebalance().flat_map(_RegressFlatMap(HalfPlusTwo(half_plus_two))) \
+        .collect_into()
+    res = env.execute("regress")
+    assert sorted(sink.results()) == [2.0, 2.5, 3.0, 3.5]
+    assert res.attempts == 0
+
+
+def test_map_with_model(half_plus_two):
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    out = env.from_collection(examples()).rebalance() \
+        .map_with_model(HalfPlusTwo(half_plus_two), lambda v, m: m.regress_x_to_y([v[0]]).item()) \
+        .execute_and_collect()
+    assert sorted(out) == [2.0, 2.5, 3.0, 3.5]
+    with pytest.raises(ValueError):
+        env.from_collection([1]).map_with_model(None, lambda v, m: v)
+
+
+class _Proc(ModelProcessFunction):
+    def process_element(self, value, ctx, out):
+        out.collect(self.model.regress_x_to_y([value[0]]).item())
+
+
+class _Co(ModelCoProcessFunction):
+    def process_element1(self, value, ctx, out):
+        out.collect(("data", self.model.regress_x_to_y([value[0]]).item()))
+
+    def process_element2(self, value, ctx, out):
+        out.collect(("control", value))
+
+
+class _Win(ModelWindowFunction):
+    def apply(self, key, window, inputs, out):
+        ys = self.model.regress_x_to_y([v[0] for v in inputs]).reshape(-1).tolist()
+        out.collect((key, sorted(ys)))
+
+
+class _AllWin(ModelAllWindowFunction):
+    def apply(self, window, inputs, out):
+        out.collect(sorted(self.model.regress_x_to_y([v[0] for v in inputs]).reshape(-1).tolist()))
+
+
+class _FM(ModelFlatMapFunction):
+    def flat_map(self, value, out):
+        out.collect(self.model.regress_x_to_y([value[0]]).item())
+
+
+def test_all_six_model_function_kinds(half_plus_two):
+    """The reference's Abstract{Process,CoProcess,Window,AllWindow}Function crash with
+    MatchError for non-CheckpointedModels (B6); here all six kinds run."""
+    m = HalfPlusTwo(half_plus_two)
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    s = env.from_collection(examples())
+    checkpoint_dir = None
+    del checkpoint_dir
+    r_map = s.map_with_model(m, lambda v, mm: mm.regress_x_to_y([v[0]]).item()).collect_into()
+    r_fm = s.flat_map(_FM(m)).collect_into()
+    r_proc = s.process(_Proc(m)).collect_into()
+    r_co = s.connect(env.from_collection(["reload"])).process(_Co(m)).collect_into()
+    r_win = s.key_by(lambda v: int(v[1] * 2) % 2).count_window(2).apply(_Win(m)).collect_into()
+    r_all = s.count_window_all(4).apply(_AllWin(m)).collect_into()
+    env.execute("six-kinds")
+    want = [2.0, 2.5, 3.0, 3.5]
+    assert sorted(r_map.results()) == want
+    assert sorted(r_fm.results()) == want
+    assert sorted(r_proc.results()) == want
+    co = r_co.results()
+    assert sorted(v for k, v in co if k == "data") == want and ("control", "reload") in co
+    assert sorted(r_win.results()) == [(0, [2.0, 3.0]), (1, [2.5, 3.5])]
+    assert r_all.results() == [want]
+
+
+class _CountPerKey(ProcessFunction):
+    def open(self, config=None):
+        self.count = self.get_runtime_context().get_state(ValueStateDescriptor("n", 0))
+
+    def process_element(self, value, ctx, out):
+        self.count.update(self.count.value() + 1)
+        out.collect((ctx.get_current_key(), self.count.value()))
+        if value % 5 == 0:
+            ctx.output(OutputTag("fives"), value)
+
+
+def test_keyed_state_and_side_output():
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(3)
+    main = env.from_collection(list(range(30))).key_by(lambda v: v % 3).process(_CountPerKey())
+    side = main.get_side_output(OutputTag("fives")).collect_into()
+    res = main.collect_into()
+    env.execute("keyed")
+    last = {}
+    for k, c in res.results():
+        last[k] = max(last.get(k, 0), c)
+    assert last == {0: 10, 1: 10, 2: 10}
+    assert sorted(side.results()) == [0, 5, 10, 15, 20, 25]
+
+
+def test_event_time_windows_and_watermarks():
+    from flink_tensorflow_amd.runtime import WindowFunction
+
+    class Sum(WindowFunction):
+        def apply(self, key, window, inputs, out):
+            out.collect((key, window.start, sum(v[1] for v in inputs)))
+
+    data = [("a", 1, 0.5), ("a", 2, 1.5), ("b", 3, 0.7), ("a", 4, 2.2), ("b", 5, 2.9), ("a", 6, 1.9)]
+    env = StreamExecutionEnvironment.get_execution_environment()
+    res = (env.from_collection(data).assign_timestamps_and_watermarks(lambda v: v[2], 1.0)
+           .key_by(lambda v: v[0]).time_window(1.0, event_time=True).apply(Sum()).execute_and_collect())
+    assert sorted(res) == [("a", 0.0, 1), ("a", 1.0, 8), ("a", 2.0, 4), ("b", 0.0, 3), ("b", 2.0, 5)]
+
+
+def test_file_source_zero_length_and_filters(tmp_path):
+    for name, data in [("a.jpg", b"x" * 10), ("b.jpeg", b""), ("c.crdownload", b"y"), ("d.txt", b"z")]:
+        (tmp_path / name).write_bytes(data)
+    fmt = BytesInputFormat(include=["*.jpg"]).configure(include=["*.jpeg"], exclude=["*.crdownload"])
+    env = StreamExecutionEnvironment.get_execution_environment()
+    out = env.read_file(fmt, str(tmp_path), PROCESS_ONCE).map(lambda v: (os.path.basename(v[0]), len(v[1]))) \
+        .execute_and_collect()
+    assert sorted(out) == [("a.jpg", 10), ("b.jpeg", 0)]  # zero-length file emitted exactly once (B5)
+
+
+class _Summer(ProcessFunction, CheckpointedFunction):
+    def __init__(self):
+        super().__init__()
+        self.total = 0
+
+    def initialize_state(self, ctx):
+        self.st = ctx.operator_state.get_list_state(ListStateDescriptor("total"))
+        if ctx.is_restored():
+            self.total = sum(self.st.get())
+
+    def snapshot_state(self, ctx):
+        self.st.update([self.total])
+
+    def process_element(self, value, ctx, out):
+        self.total += value
+        out.collect(self.total)
+
+
+def test_checkpoint_and_restart_from_latest(tmp_path):
+    """Fail on the first attempt after a checkpoint completed; the restarted job rewinds
+    the source to the checkpointed offset and restores operator state."""
+    env = StreamExecutionEnvironment.get_execution_environment()
+    env.enable_checkpointing(0.05, str(tmp_path / "chk"))
+    env.set_restart_strategy(RestartStrategy.fixed_delay(2, 0.0))
+    from flink_tensorflow_amd.runtime.sources import CollectionSource
+
+    src = env.add_source(CollectionSource(list(range(1, 201)), delay_s=0.002), "numbers")
+    sink = src.map(FailAfter(150, attempts=(0,))).process(_Summer()).collect_into()
+    res = env.execute("recover")
+    assert res.attempts == 1
+    assert len(res.checkpoints) >= 1
+    assert max(sink.results()) == sum(range(1, 201))  # state + offsets restored consistently
+    from flink_tensorflow_amd.runtime.checkpoint import CheckpointStorage
+
+    assert CheckpointStorage(str(tmp_path / "chk")).latest() is not None
+
+
+def test_failure_without_restart_raises():
+    from flink_tensorflow_amd.runtime import JobExecutionException
+
+    env = StreamExecutionEnvironment.get_execution_environment()
+    env.from_collection(list(range(10))).map(FailAfter(3)).collect_into()
+    with pytest.raises(JobExecutionException):
+        env.execute("boom")
+
+
+def test_batched_model_operator(half_plus_two):
+    env = StreamExecutionEnvironment.get_execution_environment()
+
+    def run_batch(model, values):
+        return model.regress_x_to_y([v[0] for v in values]).reshape(-1).tolist()
+
+    sink = env.from_collection(examples() * 25).map_with_model_batched(HalfPlusTwo(half_plus_two), run_batch,
+                                                                       max_batch=16, max_delay_ms=2).collect_into()
+    res = env.execute("batched")
+    out = sink.results()
+    assert len(out) == 100 and sorted(set(out)) == [2.0, 2.5, 3.0, 3.5]
+    hist = [m for k, m in res.metrics.items() if k.startswith("batched-model")][0]["histograms"]["batch_size"]
+    assert hist["max"] == 16
