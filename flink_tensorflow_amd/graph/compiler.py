@@ -379,28 +379,39 @@ class CompiledFunction:
             pt = pb = pl = pr = 0
         else:
             return self._lower_glue(node)
+        if Cout % 8:
+            return self._lower_glue(node)
         last, scale, bias, residual, act, absorbed = self._conv_chain(node)
         if scale is not None:
             w = w * scale  # fold BN into the output channels
-        phys = x.phys_c or C
-        cin_pad = -(-phys // 8) * 8
-        w_ohwi = w.permute(3, 0, 1, 2).contiguous()
-        if cin_pad != Cin:
-            w_ohwi = torch.nn.functional.pad(w_ohwi, (0, cin_pad - Cin))
-        cout_pad = -(-Cout // 4) * 4
-        if cout_pad != Cout:
-            return self._lower_glue(node)
+        Ho = (H + pt + pb - ((KH - 1) * dh + 1)) // sh + 1
+        Wo = (W + pl + pr - ((KW - 1) * dw + 1)) // sw + 1
+        if self._s2d_ok(x, node, C, sh, sw, dh, dw, pt, pl, H, W):
+            # stride-2 RGB stem over the space-to-depth preprocess output (K 392 -> 256)
+            w_ohwi, (pt, pb, pl, pr) = K.s2d_stem_weights(w, H, W, (pt, pb, pl, pr))
+            x.pre_cfg["s2d"] = True
+            x.buf_shape = (N, H // 2, W // 2, 16)
+            x.phys_c = 16
+            xin_shape_override = (N, H // 2, W // 2, 16)
+            KH, KW = w_ohwi.shape[1], w_ohwi.shape[2]
+            sh = sw = 1
+            cin_pad = 16
+        else:
+            xin_shape_override = None
+            phys = x.phys_c or C
+            cin_pad = -(-phys // 8) * 8
+            w_ohwi = w.permute(3, 0, 1, 2).contiguous()
+            if cin_pad != Cin:
+                w_ohwi = torch.nn.functional.pad(w_ohwi, (0, cin_pad - Cin))
         w_dev = w_ohwi.to(self.device, torch.bfloat16).contiguous()
         b_dev = bias.to(self.device, torch.float32).contiguous() if bias is not None else None
         self.params += [w_dev] + ([b_dev] if b_dev is not None else [])
-        Ho = (H + pt + pb - ((KH - 1) * dh + 1)) // sh + 1
-        Wo = (W + pl + pr - ((KW - 1) * dw + 1)) // sw + 1
         out = self._new((N, Ho, Wo, Cout))
         res_val = None
         if residual is not None:
             rn, ri = residual
             res_val = self.vals[rn.inputs[ri]]
-        xin = self._ensure_padded(x, cin_pad, node.name)
+        xin = x if xin_shape_override is not None else self._ensure_padded(x, cin_pad, node.name)
         for a in absorbed:
             self._fused.add(a.name)
 
@@ -411,6 +422,19 @@ class CompiledFunction:
         self._emit(node.name, "conv", run, [xin] + ([res_val] if res_val else []), [out])
         self.vals[(last.name, 0)] = out
         self._alias_fused_outputs(absorbed, out)
+
+    def _s2d_ok(self, x: Val, node: Node, C, sh, sw, dh, dw, pt, pl, H, W) -> bool:
+        cfg = getattr(x, "pre_cfg", None)
+        if cfg is None or C != 3 or (sh, sw) != (2, 2) or (dh, dw) != (1, 1) or pt % 2 or pl % 2 or H % 2 or W % 2:
+            return False
+        chain = x.pre_chain
+        users = set()
+        for (n, _), v in self.vals.items():
+            if v is x:
+                if any(TensorName.parse(f).name == n for f in self.fetch_names):
+                    return False
+                users.update(c for c in self.cons.get(n, []) if c not in chain)
+        return users == {node.name}
 
     def _alias_fused_outputs(self, absorbed, out):
         for a in absorbed:
@@ -439,7 +463,7 @@ class CompiledFunction:
         wt = b.const.float()
         w_nk = wt if node.attr("transpose_b", False) else wt.t()
         N, Kd = w_nk.shape
-        if Kd % 8 or N % 4:
+        if Kd % 8 or N % 8:
             return self._lower_glue(node)
         last, scale, bias, residual, act, absorbed = self._conv_chain(node)
         if scale is not None:
@@ -512,12 +536,15 @@ class CompiledFunction:
         out = self._new((x.shape[0], size[0], size[1], 3), phys_c=8)
         out_buf_shape = (x.shape[0], size[0], size[1], 8)
         out.buf_shape = out_buf_shape
+        out.pre_cfg = {"s2d": False}
+        out.pre_chain = {n.name for n in chain}
         for n in chain[1:]:
             self._fused.add(n.name)
         mean_t, std_t = tuple(mean.tolist()), tuple(std.tolist())
+        cfg = out.pre_cfg
 
         def run(x=x, out=out):
-            K.preprocess_images(x.buf, size, mean_t, std_t, align, half, out=out.buf)
+            K.preprocess_images(x.buf, size, mean_t, std_t, align, half, out=out.buf, s2d=cfg["s2d"])
 
         self._emit(cast.name + "/preprocess", "preprocess", run, [x], [out])
         for n in chain:

@@ -85,16 +85,27 @@ class Graph:
         g.import_graph_def(gd, prefix)
         return g
 
-    def import_graph_def(self, gd: GraphDef | bytes, prefix: str = "") -> None:
+    def import_graph_def(self, gd: GraphDef | bytes, prefix: str = "",
+                         input_map: dict[str, str] | None = None) -> None:
+        """Imports ``gd`` under ``prefix``.  ``input_map`` rewires references to tensors of
+        the imported graph (``"input:0"``) onto existing tensors of this graph
+        (``"normalized:0"``), like ``tf.import_graph_def(input_map=...)``."""
         if isinstance(gd, (bytes, bytearray, memoryview)):
             gd = GraphDef.decode(bytes(gd))
         pfx = (prefix.rstrip("/") + "/") if prefix else ""
+        imap = {}
+        for k, v in (input_map or {}).items():
+            kn, ki, _ = parse_input(k)
+            vn, vi, _ = parse_input(v)
+            imap[(kn, ki)] = (vn, vi)
         for nd in gd.node:
             data, ctrl = [], []
             for s in nd.input:
                 n, k, is_ctrl = parse_input(s)
                 if is_ctrl:
                     ctrl.append(pfx + n)
+                elif (n, k) in imap:
+                    data.append(imap[(n, k)])
                 else:
                     data.append((pfx + n, k))
             name = pfx + nd.name

@@ -3,20 +3,25 @@
 //
 // Used for every Conv2D / MatMul of the compiled GPU plan (ResNet-50, Inception-v3,
 // BERT projections, Wide&Deep towers).  Layouts (TF-native NHWC):
-//   x  [N, H, W, Cin]  bf16, Cin % 8 == 0 (the stem pads 3 -> 8 in the preprocess kernel)
+//   x  [N, H, W, Cin]  bf16, Cin % 8 == 0 (the stem input comes from the preprocess kernel
+//      already padded / space-to-depth packed)
 //   w  [Cout, KH, KW, Cin] bf16  ("OHWI", K-contiguous rows; BN folded in at load time)
 //   y  [N, Ho, Wo, ldy] bf16, written at channel offset y_coff (concat-by-stride-write)
 // GEMM view: C^T[Cout, M] = W[Cout, K] . X^T[K, M]; M = N*Ho*Wo pixels, K = KH*KW*Cin.
-// MFMA operand A = weight rows (output channels), operand B = im2col pixel rows, so an
-// accumulator lane holds 4 consecutive channels of one pixel (8-byte bf16 stores).
+// MFMA operand A = weight rows (output channels), operand B = im2col pixel rows.
 //
-// Tiling: 128 pixels x 128 channels x BK=64 per 256-thread workgroup (4 waves, 2x2, each
-// 64x64 = 4x4 tiles of v_mfma_f32_16x16x32_bf16).  Register-staged global->LDS double
-// buffer (issue the next tile's 16-B loads before the MFMAs, write them to the other
-// LDS buffer after: guide T14), one barrier per K-tile.  LDS rows are 128 B, chunk-XOR
-// swizzled (chunk ^ (row & 7)) so the ds_read_b128 fragment reads are conflict-free
-// (guide T2).  Blocks are remapped XCD-aware so the channel tiles of one pixel tile
-// share an L2 (guide T1).
+// Tile configurations (4 waves = 256 threads, each wave 64 channels x TM pixels of
+// v_mfma_f32_16x16x32_bf16 fragments):
+//   <BM=128, BN=128>  wide layers            (2 x 2 waves, 64 x 64 per wave)
+//   <BM=256, BN=64>   Cout <= 64 layers      (4 x 1 waves, 64 x 64 per wave; no wasted MFMA)
+// K is staged 64 deep per step.  Register-staged global->LDS double buffer: the next
+// tile's 16-B loads are issued before the MFMAs and written to the other LDS buffer after
+// (guide T14); one barrier per K-tile.  LDS rows are 128 B, chunk-XOR swizzled
+// (chunk ^ (row & 7)) so every ds_read_b128 fragment read is conflict-free (guide T2).
+// Epilogue: acc + bias is rounded to bf16 into an LDS tile (padded rows), then each
+// thread streams 16-B row segments: residual loads, activation and output stores are all
+// fully coalesced 16-B accesses (the memory-bound 1x1 layers live on this).  Blocks are
+// remapped XCD-aware so the channel tiles of one pixel tile share an L2 (guide T1).
 #include <pybind11/pybind11.h>
 
 #include <stdexcept>
@@ -26,8 +31,6 @@
 
 namespace {
 
-constexpr int BM = 128;  // pixels per tile
-constexpr int BN = 128;  // output channels per tile
 constexpr int BK = 64;   // K per stage
 constexpr int NT = 256;  // threads
 
@@ -47,11 +50,21 @@ struct IgemmParams {
 
 FTM_DEVICE int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
 
-template <bool CONV, int ACT, bool HAS_BIAS, bool HAS_RES>
+template <int BM, int BN, int STAGES, bool CONV, int ACT, bool HAS_BIAS, bool HAS_RES>
 __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (BM + BN) * BK];  // 64 KiB
-  bf16* Xs = smem;                 // [2][BM][BK]
-  bf16* Ws = smem + 2 * BM * BK;   // [2][BN][BK]
+  constexpr int WAVES_N = BN / 64;
+  constexpr int WAVES_M = 4 / WAVES_N;
+  constexpr int TM = BM / WAVES_M;     // pixels per wave
+  constexpr int J = TM / 16;           // pixel fragments per wave
+  constexpr int XR = BM / 32;          // X chunks staged per thread
+  constexpr int WR = BN / 32;          // W chunks staged per thread
+  constexpr int OPAD = 8;              // epilogue row padding (bf16)
+  constexpr int STAGE_ELEMS = STAGES * (BM + BN) * BK;
+  constexpr int EPI_ELEMS = BM * (BN + OPAD);
+  constexpr int LDS_ELEMS = STAGE_ELEMS > EPI_ELEMS ? STAGE_ELEMS : EPI_ELEMS;
+  __shared__ __attribute__((aligned(16))) bf16 smem[LDS_ELEMS];
+  bf16* Xs = smem;                      // [STAGES][BM][BK]
+  bf16* Ws = smem + STAGES * BM * BK;   // [STAGES][BN][BK]
 
   const int nwg = p.tiles_m * p.tiles_n;
   const int tile = xcd_remap(blockIdx.x, nwg);
@@ -63,18 +76,17 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wp = wave & 1;   // pixel half of the tile
-  const int wc = wave >> 1;  // channel half
+  const int wp = wave % WAVES_M;  // pixel slab of the tile
+  const int wc = wave / WAVES_M;  // channel slab
 
-  // ---- per-thread staging assignment: fixed k-chunk, 4 rows (r0 + 32 i)
+  // ---- per-thread staging assignment: fixed k-chunk, rows r0 + 32 i
   const int kc = tid & 7;
   const int r0 = tid >> 3;
 
-  // pixel-row precompute (conv): base offset of image n, top-left input coords
-  int xbase[4], hb[4], wb[4];
-  bool mvalid[4];
+  int xbase[XR], hb[XR], wb[XR];
+  bool mvalid[XR];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < XR; ++i) {
     int m = m0 + r0 + 32 * i;
     mvalid[i] = m < p.M;
     int mm = mvalid[i] ? m : 0;
@@ -92,16 +104,16 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
       wb[i] = 0;
     }
   }
-  const bf16* wrow[4];
-  bool nvalid[4];
+  const bf16* wrow[WR];
+  bool nvalid[WR];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < WR; ++i) {
     int co = n0 + r0 + 32 * i;
     nvalid[i] = co < p.Cout;
     wrow[i] = p.w + (size_t)(nvalid[i] ? co : 0) * p.K;
   }
 
-  u32x4 xr[4], wr[4];
+  u32x4 xr[XR], wr[WR];
   const u32x4 zero4 = {0u, 0u, 0u, 0u};
 
   auto load_tile = [&](int k0) {
@@ -113,7 +125,7 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
       int kh = kidx / p.KW;
       int kw = kidx - kh * p.KW;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < XR; ++i) {
         int hi = hb[i] + kh * p.dh;
         int wi = wb[i] + kw * p.dw;
         bool ok = kvalid && mvalid[i] && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
@@ -121,13 +133,13 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < XR; ++i) {
         bool ok = kvalid && mvalid[i];
         xr[i] = ok ? *reinterpret_cast<const u32x4*>(p.x + (size_t)xbase[i] + k) : zero4;
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < WR; ++i) {
       bool ok = kvalid && nvalid[i];
       wr[i] = ok ? *reinterpret_cast<const u32x4*>(wrow[i] + k) : zero4;
     }
@@ -136,18 +148,16 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
     bf16* xs = Xs + buf * BM * BK;
     bf16* ws = Ws + buf * BN * BK;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int row = r0 + 32 * i;
-      *reinterpret_cast<u32x4*>(xs + swz(row, kc)) = xr[i];
-      *reinterpret_cast<u32x4*>(ws + swz(row, kc)) = wr[i];
-    }
+    for (int i = 0; i < XR; ++i) *reinterpret_cast<u32x4*>(xs + swz(r0 + 32 * i, kc)) = xr[i];
+#pragma unroll
+    for (int i = 0; i < WR; ++i) *reinterpret_cast<u32x4*>(ws + swz(r0 + 32 * i, kc)) = wr[i];
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][J];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (p.K + BK - 1) / BK;
   load_tile(0);
@@ -158,78 +168,140 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
   const int fchunk = lane >> 4;  // 0..3 -> k offset 8*fchunk within a 32-deep substep
 
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
+    const int buf = STAGES == 2 ? (kt & 1) : 0;
     if (kt + 1 < nk) load_tile((kt + 1) * BK);
     const bf16* xs = Xs + buf * BM * BK;
     const bf16* ws = Ws + buf * BN * BK;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 a[4], b[4];
+      bf16x8 a[4], b[J];
       const int chunk = ks * 4 + fchunk;
 #pragma unroll
       for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ws + swz(wc * 64 + i * 16 + frow, chunk));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(xs + swz(wp * 64 + j * 16 + frow, chunk));
+      for (int j = 0; j < J; ++j) b[j] = *reinterpret_cast<const bf16x8*>(xs + swz(wp * TM + j * 16 + frow, chunk));
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_tile(buf ^ 1);
+    if (kt + 1 < nk) {
+      if constexpr (STAGES == 1) __syncthreads();  // single buffer: everyone done reading
+      store_tile(STAGES == 2 ? (buf ^ 1) : 0);
+    }
     __syncthreads();
   }
 
-  // ---- epilogue: lane holds channels c..c+3 of pixel m for each (i, j) fragment
+  // ---- epilogue phase 1: (acc + bias) -> bf16 LDS tile [BM][BN + OPAD]
+  constexpr int OLD = BN + OPAD;
+  bf16* Os = smem;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int c = n0 + wc * 64 + i * 16 + (lane >> 4) * 4;
-    if (c >= p.Cout) continue;
+    const int cl = wc * 64 + i * 16 + (lane >> 4) * 4;  // local channel of this lane's 4 rows
     f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (HAS_BIAS) bv = *reinterpret_cast<const f32x4*>(p.bias + c);
+    if constexpr (HAS_BIAS) {
+      if (n0 + cl < p.Cout) bv = *reinterpret_cast<const f32x4*>(p.bias + n0 + cl);
+    }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = m0 + wp * 64 + j * 16 + (lane & 15);
-      if (m >= p.M) continue;
+    for (int j = 0; j < J; ++j) {
+      const int pl = wp * TM + j * 16 + (lane & 15);
       f32x4 v = acc[i][j] + bv;
-      if constexpr (HAS_RES) {
-        bf16x4 r = *reinterpret_cast<const bf16x4*>(p.res + (size_t)m * p.ldr + c);
-        v[0] += (float)r[0];
-        v[1] += (float)r[1];
-        v[2] += (float)r[2];
-        v[3] += (float)r[3];
-      }
       bf16x4 o;
-      o[0] = f2bf(apply_act<ACT>(v[0]));
-      o[1] = f2bf(apply_act<ACT>(v[1]));
-      o[2] = f2bf(apply_act<ACT>(v[2]));
-      o[3] = f2bf(apply_act<ACT>(v[3]));
-      *reinterpret_cast<bf16x4*>(p.y + (size_t)m * p.ldy + p.y_coff + c) = o;
+      if constexpr (HAS_RES) {
+        o[0] = f2bf(v[0]); o[1] = f2bf(v[1]); o[2] = f2bf(v[2]); o[3] = f2bf(v[3]);
+      } else {
+        o[0] = f2bf(apply_act<ACT>(v[0]));
+        o[1] = f2bf(apply_act<ACT>(v[1]));
+        o[2] = f2bf(apply_act<ACT>(v[2]));
+        o[3] = f2bf(apply_act<ACT>(v[3]));
+      }
+      *reinterpret_cast<bf16x4*>(Os + pl * OLD + cl) = o;
     }
   }
+  __syncthreads();
+
+  // ---- epilogue phase 2: coalesced 16-B row segments (+ residual, activation)
+  constexpr int CPR = BN / 8;  // 16-B chunks per tile row
+#pragma unroll
+  for (int q = tid; q < BM * CPR; q += NT) {
+    const int pl = q / CPR;
+    const int cc = q % CPR;
+    const int m = m0 + pl;
+    const int c = n0 + cc * 8;
+    if (m >= p.M || c >= p.Cout) continue;
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(Os + pl * OLD + cc * 8);
+    if constexpr (HAS_RES) {
+      bf16x8 r = *reinterpret_cast<const bf16x8*>(p.res + (size_t)m * p.ldr + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(apply_act<ACT>((float)v[e] + (float)r[e]));
+    }
+    *reinterpret_cast<bf16x8*>(p.y + (size_t)m * p.ldy + p.y_coff + c) = v;
+  }
+}
+
+// The bias pointer is always set (the launcher substitutes a zero vector).
+template <int BM, int BN, int STAGES, bool CONV, int ACT>
+void launch_act(const IgemmParams& p0, hipStream_t s) {
+  IgemmParams p = p0;
+  p.tiles_m = (p.M + BM - 1) / BM;
+  p.tiles_n = (p.Cout + BN - 1) / BN;
+  dim3 grid(p.tiles_m * p.tiles_n), block(NT);
+  if (p.res) hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, STAGES, CONV, ACT, true, true>), grid, block, 0, s, p);
+  else hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, STAGES, CONV, ACT, true, false>), grid, block, 0, s, p);
+}
+
+// Tile configurations: 0 = 128x128 double-buffered, 1 = 256x64 double-buffered,
+// 2 = 128x128 single-buffered (more blocks/CU), 3 = 256x64 single-buffered, 4 = 64x128.
+constexpr int NCFG = 5;
+
+// Measured on the ResNet-50 layer set (bench/conv_tune.py, profiles/r01_tune): the
+// single-buffered tiles win almost everywhere — 4 blocks/CU of occupancy hide the
+// global-load latency better than a second LDS stage at 2 blocks/CU.
+int auto_config(const IgemmParams& p) {
+  if (p.Cout <= 64) return 3;
+  return 2;
 }
 
 template <bool CONV, int ACT>
-void launch_act(const IgemmParams& p, hipStream_t s) {
-  dim3 grid(p.tiles_m * p.tiles_n), block(NT);
-  const bool hb = p.bias != nullptr, hr = p.res != nullptr;
-  if (hb && hr) hipLaunchKernelGGL((igemm_bf16_kernel<CONV, ACT, true, true>), grid, block, 0, s, p);
-  else if (hb) hipLaunchKernelGGL((igemm_bf16_kernel<CONV, ACT, true, false>), grid, block, 0, s, p);
-  else if (hr) hipLaunchKernelGGL((igemm_bf16_kernel<CONV, ACT, false, true>), grid, block, 0, s, p);
-  else hipLaunchKernelGGL((igemm_bf16_kernel<CONV, ACT, false, false>), grid, block, 0, s, p);
+void launch_tile(const IgemmParams& p, int cfg, hipStream_t s) {
+  if (cfg < 0) cfg = auto_config(p);
+  switch (cfg) {
+    case 0: launch_act<128, 128, 2, CONV, ACT>(p, s); break;
+    case 1: launch_act<256, 64, 2, CONV, ACT>(p, s); break;
+    case 2: launch_act<128, 128, 1, CONV, ACT>(p, s); break;
+    case 3: launch_act<256, 64, 1, CONV, ACT>(p, s); break;
+    case 4: launch_act<64, 128, 2, CONV, ACT>(p, s); break;
+    default: throw std::invalid_argument("unknown igemm config " + std::to_string(cfg));
+  }
 }
 
 template <bool CONV>
-void launch(const IgemmParams& p, int act, hipStream_t s) {
-  switch (act) {
-    case ACT_NONE: launch_act<CONV, ACT_NONE>(p, s); break;
-    case ACT_RELU: launch_act<CONV, ACT_RELU>(p, s); break;
-    case ACT_GELU_TANH: launch_act<CONV, ACT_GELU_TANH>(p, s); break;
-    case ACT_SIGMOID: launch_act<CONV, ACT_SIGMOID>(p, s); break;
-    case ACT_TANH: launch_act<CONV, ACT_TANH>(p, s); break;
-    case ACT_RELU6: launch_act<CONV, ACT_RELU6>(p, s); break;
-    default: throw std::invalid_argument("unknown activation " + std::to_string(act));
+void launch(const IgemmParams& p, int act, int cfg, hipStream_t s) {
+  if constexpr (CONV) {
+    switch (act) {
+      case ACT_NONE: launch_tile<CONV, ACT_NONE>(p, cfg, s); break;
+      case ACT_RELU: launch_tile<CONV, ACT_RELU>(p, cfg, s); break;
+      case ACT_RELU6: launch_tile<CONV, ACT_RELU6>(p, cfg, s); break;
+      default: throw std::invalid_argument("conv activation must be none/relu/relu6");
+    }
+  } else {
+    switch (act) {
+      case ACT_NONE: launch_tile<CONV, ACT_NONE>(p, cfg, s); break;
+      case ACT_RELU: launch_tile<CONV, ACT_RELU>(p, cfg, s); break;
+      case ACT_GELU_TANH: launch_tile<CONV, ACT_GELU_TANH>(p, cfg, s); break;
+      case ACT_SIGMOID: launch_tile<CONV, ACT_SIGMOID>(p, cfg, s); break;
+      case ACT_TANH: launch_tile<CONV, ACT_TANH>(p, cfg, s); break;
+      case ACT_RELU6: launch_tile<CONV, ACT_RELU6>(p, cfg, s); break;
+      default: throw std::invalid_argument("unknown activation " + std::to_string(act));
+    }
   }
   FTM_CHECK_LAUNCH();
+}
+
+// No allocation in the launch path (it may be captured into a hipGraph): a layer without
+// bias passes a zero vector owned by the caller.
+void require_bias(const float* b) {
+  if (!b) throw std::invalid_argument("igemm: bias pointer is required (pass zeros for no bias)");
 }
 
 void check_align(uintptr_t ptr, int bytes, const char* what) {
@@ -241,16 +313,18 @@ void check_align(uintptr_t ptr, int bytes, const char* what) {
 // Conv2D NHWC implicit GEMM.  Shapes are validated here (host side) before any launch.
 void conv2d_nhwc_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int N, int H, int W,
                       int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw, int Ho, int Wo,
-                      int ldy, int y_coff, int ldr, int act, uintptr_t stream) {
+                      int ldy, int y_coff, int ldr, int act, uintptr_t stream, int cfg) {
   if (Cin % 8) throw std::invalid_argument("conv2d_nhwc_bf16: Cin must be a multiple of 8");
-  if (Cout % 4 || ldy % 4 || y_coff % 4) throw std::invalid_argument("conv2d_nhwc_bf16: Cout/ldy/y_coff % 4 != 0");
-  if (res && ldr % 4) throw std::invalid_argument("conv2d_nhwc_bf16: residual stride % 4 != 0");
+  if (Cout % 8 || ldy % 8 || y_coff % 8) throw std::invalid_argument("conv2d_nhwc_bf16: Cout/ldy/y_coff % 8 != 0");
+  if (res && ldr % 8) throw std::invalid_argument("conv2d_nhwc_bf16: residual stride % 8 != 0");
   if (N <= 0 || Ho <= 0 || Wo <= 0 || Cout <= 0) throw std::invalid_argument("conv2d_nhwc_bf16: empty problem");
+  if ((long)N * H * W * Cin >= (1L << 31) || (long)N * Ho * Wo >= (1L << 31))
+    throw std::invalid_argument("conv2d_nhwc_bf16: tensor too large for 32-bit indexing");
   check_align(x, 16, "x");
   check_align(w, 16, "w");
-  check_align(y, 8, "y");
+  check_align(y, 16, "y");
   if (bias) check_align(bias, 16, "bias");
-  if (res) check_align(res, 8, "residual");
+  if (res) check_align(res, 16, "residual");
   IgemmParams p{};
   p.x = reinterpret_cast<const bf16*>(x);
   p.w = reinterpret_cast<const bf16*>(w);
@@ -263,28 +337,25 @@ void conv2d_nhwc_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, u
   p.K = KH * KW * Cin;
   p.ldx = Cin;
   p.ldy = ldy; p.y_coff = y_coff; p.ldr = ldr;
-  p.tiles_m = (p.M + BM - 1) / BM;
-  p.tiles_n = (Cout + BN - 1) / BN;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  require_bias(p.bias);
   const bool pointwise = KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
-  if (pointwise) {
-    p.ldx = Cin;
-    launch<false>(p, act, s);  // 1x1/s1: the input IS the [M, Cin] matrix
-  } else {
-    launch<true>(p, act, s);
-  }
+  if (pointwise) launch<false>(p, act, cfg, s);  // 1x1/s1: the input IS the [M, Cin] matrix
+  else launch<true>(p, act, cfg, s);
 }
 
 // Y[M, N] = act(X[M, K] . W[N, K]^T + bias + res).  X row stride ldx, Y row stride ldy.
 void gemm_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int M, int N, int K, int ldx,
-               int ldy, int ldr, int act, uintptr_t stream) {
+               int ldy, int ldr, int act, uintptr_t stream, int cfg) {
   if (K % 8 || ldx % 8) throw std::invalid_argument("gemm_bf16: K and ldx must be multiples of 8");
-  if (N % 4 || ldy % 4) throw std::invalid_argument("gemm_bf16: N and ldy must be multiples of 4");
+  if (N % 8 || ldy % 8) throw std::invalid_argument("gemm_bf16: N and ldy must be multiples of 8");
+  if (res && ldr % 8) throw std::invalid_argument("gemm_bf16: residual stride % 8 != 0");
   if (M <= 0 || N <= 0) throw std::invalid_argument("gemm_bf16: empty problem");
   check_align(x, 16, "x");
   check_align(w, 16, "w");
-  check_align(y, 8, "y");
+  check_align(y, 16, "y");
   if (bias) check_align(bias, 16, "bias");
+  if (res) check_align(res, 16, "residual");
   IgemmParams p{};
   p.x = reinterpret_cast<const bf16*>(x);
   p.w = reinterpret_cast<const bf16*>(w);
@@ -292,12 +363,13 @@ void gemm_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_
   p.res = reinterpret_cast<const bf16*>(res);
   p.y = reinterpret_cast<bf16*>(y);
   p.M = M; p.Cout = N; p.K = K; p.ldx = ldx; p.ldy = ldy; p.y_coff = 0; p.ldr = ldr;
-  p.tiles_m = (M + BM - 1) / BM;
-  p.tiles_n = (N + BN - 1) / BN;
-  launch<false>(p, act, reinterpret_cast<hipStream_t>(stream));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  require_bias(p.bias);
+  launch<false>(p, act, cfg, s);
 }
 
 void register_igemm(pybind11::module_& m) {
   m.def("conv2d_nhwc_bf16", &conv2d_nhwc_bf16);
   m.def("gemm_bf16", &gemm_bf16);
+  m.attr("igemm_num_configs") = NCFG;
 }

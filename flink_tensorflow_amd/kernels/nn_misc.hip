@@ -17,41 +17,73 @@ namespace {
 // (EX/inception/ImageNormalization.scala:42-77) with one pass over the batch.
 // One thread per output pixel; the 3 channels of each of the 4 taps are 3 byte loads.
 // ------------------------------------------------------------------------------------
+struct PreParams {
+  int Hi, Wi, Ho, Wo;
+  float sy, sx;
+  int half_pixel;
+  float m[3], s[3];
+  int src_stride;
+};
+
+// One resized + normalized RGB pixel (TF ResizeBilinear coordinates).
+FTM_DEVICE void resize_pixel(const uint8_t* img, const PreParams& q, int oy, int ox, float out[3]) {
+  float fy = q.half_pixel ? (oy + 0.5f) * q.sy - 0.5f : oy * q.sy;
+  float fx = q.half_pixel ? (ox + 0.5f) * q.sx - 0.5f : ox * q.sx;
+  float fy0 = floorf(fy), fx0 = floorf(fx);
+  int y0 = max((int)fy0, 0), x0 = max((int)fx0, 0);
+  int y1 = min(y0 + 1, q.Hi - 1), x1 = min(x0 + 1, q.Wi - 1);
+  float wy = fminf(fmaxf(fy - (q.half_pixel ? (float)y0 : fy0), 0.f), 1.f);
+  float wx = fminf(fmaxf(fx - (q.half_pixel ? (float)x0 : fx0), 0.f), 1.f);
+  const uint8_t* p00 = img + ((size_t)y0 * q.Wi + x0) * 3;
+  const uint8_t* p01 = img + ((size_t)y0 * q.Wi + x1) * 3;
+  const uint8_t* p10 = img + ((size_t)y1 * q.Wi + x0) * 3;
+  const uint8_t* p11 = img + ((size_t)y1 * q.Wi + x1) * 3;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float top = (float)p00[c] + ((float)p01[c] - (float)p00[c]) * wx;
+    float bot = (float)p10[c] + ((float)p11[c] - (float)p10[c]) * wx;
+    out[c] = (top + (bot - top) * wy - q.m[c]) * q.s[c];
+  }
+}
+
+// Layout 0: [B, Ho, Wo, 8] (RGB + 5 zero channels).
+// Layout 1 (space-to-depth 2x2, for the stride-2 stem conv): [B, Ho/2, Wo/2, 16] with
+// channel (dy*2+dx)*3 + c = pixel (2*oy2+dy, 2*ox2+dx) channel c, channels 12..15 zero.
+template <int S2D>
 __global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restrict__ src, bf16* __restrict__ dst,
-                                                         int B, int Hi, int Wi, int Ho, int Wo, float sy, float sx,
-                                                         int half_pixel, float m0, float m1, float m2, float s0,
-                                                         float s1, float s2, int src_stride) {
+                                                         int B, PreParams q) {
+  const int Wo = S2D ? q.Wo / 2 : q.Wo, Ho = S2D ? q.Ho / 2 : q.Ho;
   const int total = B * Ho * Wo;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
     const int ox = idx % Wo;
     const int t = idx / Wo;
     const int oy = t % Ho;
     const int b = t / Ho;
-    float fy = half_pixel ? (oy + 0.5f) * sy - 0.5f : oy * sy;
-    float fx = half_pixel ? (ox + 0.5f) * sx - 0.5f : ox * sx;
-    float fy0 = floorf(fy), fx0 = floorf(fx);
-    int y0 = max((int)fy0, 0), x0 = max((int)fx0, 0);
-    int y1 = min(y0 + 1, Hi - 1), x1 = min(x0 + 1, Wi - 1);
-    float wy = fminf(fmaxf(fy - (half_pixel ? (float)y0 : fy0), 0.f), 1.f);
-    float wx = fminf(fmaxf(fx - (half_pixel ? (float)x0 : fx0), 0.f), 1.f);
-    const uint8_t* img = src + (size_t)b * src_stride;
-    const uint8_t* p00 = img + ((size_t)y0 * Wi + x0) * 3;
-    const uint8_t* p01 = img + ((size_t)y0 * Wi + x1) * 3;
-    const uint8_t* p10 = img + ((size_t)y1 * Wi + x0) * 3;
-    const uint8_t* p11 = img + ((size_t)y1 * Wi + x1) * 3;
-    float out[3];
+    const uint8_t* img = src + (size_t)b * q.src_stride;
+    float v[3];
+    if constexpr (S2D) {
+      bf16x8 o0, o1;
+      float pix[4][3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      float top = (float)p00[c] + ((float)p01[c] - (float)p00[c]) * wx;
-      float bot = (float)p10[c] + ((float)p11[c] - (float)p10[c]) * wx;
-      out[c] = top + (bot - top) * wy;
+      for (int d = 0; d < 4; ++d) resize_pixel(img, q, 2 * oy + (d >> 1), 2 * ox + (d & 1), pix[d]);
+      o0[0] = f2bf(pix[0][0]); o0[1] = f2bf(pix[0][1]); o0[2] = f2bf(pix[0][2]);
+      o0[3] = f2bf(pix[1][0]); o0[4] = f2bf(pix[1][1]); o0[5] = f2bf(pix[1][2]);
+      o0[6] = f2bf(pix[2][0]); o0[7] = f2bf(pix[2][1]);
+      o1[0] = f2bf(pix[2][2]);
+      o1[1] = f2bf(pix[3][0]); o1[2] = f2bf(pix[3][1]); o1[3] = f2bf(pix[3][2]);
+      o1[4] = o1[5] = o1[6] = o1[7] = f2bf(0.f);
+      bf16x8* d = reinterpret_cast<bf16x8*>(dst + (size_t)idx * 16);
+      d[0] = o0;
+      d[1] = o1;
+    } else {
+      resize_pixel(img, q, oy, ox, v);
+      bf16x8 o;
+      o[0] = f2bf(v[0]);
+      o[1] = f2bf(v[1]);
+      o[2] = f2bf(v[2]);
+      o[3] = o[4] = o[5] = o[6] = o[7] = f2bf(0.f);
+      *reinterpret_cast<bf16x8*>(dst + (size_t)idx * 8) = o;
     }
-    bf16x8 o;
-    o[0] = f2bf((out[0] - m0) * s0);
-    o[1] = f2bf((out[1] - m1) * s1);
-    o[2] = f2bf((out[2] - m2) * s2);
-    o[3] = o[4] = o[5] = o[6] = o[7] = f2bf(0.f);
-    *reinterpret_cast<bf16x8*>(dst + (size_t)idx * 8) = o;
   }
 }
 
@@ -201,16 +233,25 @@ int grid_for(long work, int block) {
 
 void preprocess_u8_to_bf16(uintptr_t src, uintptr_t dst, int B, int Hi, int Wi, int Ho, int Wo, int align_corners,
                            int half_pixel, float m0, float m1, float m2, float s0, float s1, float s2, int src_stride,
-                           uintptr_t stream) {
+                           int s2d, uintptr_t stream) {
   if (B <= 0 || Hi <= 0 || Wi <= 0 || Ho <= 0 || Wo <= 0) throw std::invalid_argument("preprocess: bad shape");
   if (src_stride < Hi * Wi * 3) throw std::invalid_argument("preprocess: src_stride smaller than one image");
   if (dst % 16) throw std::invalid_argument("preprocess: dst not 16-byte aligned");
-  float sy = (align_corners && Ho > 1) ? (float)(Hi - 1) / (Ho - 1) : (float)Hi / Ho;
-  float sx = (align_corners && Wo > 1) ? (float)(Wi - 1) / (Wo - 1) : (float)Wi / Wo;
-  long work = (long)B * Ho * Wo;
-  hipLaunchKernelGGL(preprocess_kernel, dim3(grid_for(work, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     reinterpret_cast<const uint8_t*>(src), reinterpret_cast<bf16*>(dst), B, Hi, Wi, Ho, Wo, sy, sx,
-                     half_pixel, m0, m1, m2, s0, s1, s2, src_stride);
+  if (s2d && (Ho % 2 || Wo % 2)) throw std::invalid_argument("preprocess: space-to-depth needs even output size");
+  PreParams q;
+  q.Hi = Hi; q.Wi = Wi; q.Ho = Ho; q.Wo = Wo;
+  q.sy = (align_corners && Ho > 1) ? (float)(Hi - 1) / (Ho - 1) : (float)Hi / Ho;
+  q.sx = (align_corners && Wo > 1) ? (float)(Wi - 1) / (Wo - 1) : (float)Wi / Wo;
+  q.half_pixel = half_pixel;
+  q.m[0] = m0; q.m[1] = m1; q.m[2] = m2;
+  q.s[0] = s0; q.s[1] = s1; q.s[2] = s2;
+  q.src_stride = src_stride;
+  long work = s2d ? (long)B * (Ho / 2) * (Wo / 2) : (long)B * Ho * Wo;
+  auto s = reinterpret_cast<hipStream_t>(stream);
+  auto S = reinterpret_cast<const uint8_t*>(src);
+  auto D = reinterpret_cast<bf16*>(dst);
+  if (s2d) hipLaunchKernelGGL(preprocess_kernel<1>, dim3(grid_for(work, 256)), dim3(256), 0, s, S, D, B, q);
+  else hipLaunchKernelGGL(preprocess_kernel<0>, dim3(grid_for(work, 256)), dim3(256), 0, s, S, D, B, q);
   FTM_CHECK_LAUNCH();
 }
 

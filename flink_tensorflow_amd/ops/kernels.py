@@ -68,6 +68,18 @@ def _hip():
     return _ext.hip(required=True)
 
 
+_ZERO_BIAS: dict = {}
+
+
+def _zeros_bias(n: int, device) -> torch.Tensor:
+    """Cached zero bias for bias-less layers (no allocation inside captured launches)."""
+    key = (device, n)
+    t = _ZERO_BIAS.get(key)
+    if t is None:
+        t = _ZERO_BIAS[key] = torch.zeros(n, dtype=torch.float32, device=device)
+    return t
+
+
 # ------------------------------------------------------------------------------ conv
 def conv_out_hw(H, W, KH, KW, sh, sw, ph, pw, dh=1, dw=1, ph_hi=None, pw_hi=None):
     ph_hi = ph if ph_hi is None else ph_hi
@@ -79,7 +91,7 @@ def conv_out_hw(H, W, KH, KW, sh, sw, ph, pw, dh=1, dw=1, ph_hi=None, pw_hi=None
 
 def conv2d_nhwc(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor | None = None,
                 residual: torch.Tensor | None = None, stride=(1, 1), pad=(0, 0, 0, 0), dilation=(1, 1),
-                act=None, out: torch.Tensor | None = None, out_channel_offset: int = 0) -> torch.Tensor:
+                act=None, out: torch.Tensor | None = None, out_channel_offset: int = 0, cfg: int = -1) -> torch.Tensor:
     """NHWC conv, weights [Cout, KH, KW, Cin]; ``pad = (top, bottom, left, right)``.
 
     Fused epilogue ``act(conv + bias + residual)``.  With ``out`` given, the result is
@@ -111,13 +123,12 @@ def conv2d_nhwc(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor | None
             _check(bias, "bias", torch.float32, x.device)
             if bias.numel() != Cout:
                 raise ValueError("conv2d_nhwc: bias size != Cout")
-        if (pt, pl) != (pb, pr) and (pb > pt or pr > pl):
-            # the kernel pads implicitly with the top/left offsets; bottom/right padding
-            # beyond that is implied by the bounds check as long as Ho/Wo match
-            pass
-        _hip().conv2d_nhwc_bf16(x.data_ptr(), w_ohwi.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(),
+        else:
+            bias = _zeros_bias(Cout, x.device)
+        # bottom/right padding is implied by the kernel's bounds check (Ho/Wo carry it)
+        _hip().conv2d_nhwc_bf16(x.data_ptr(), w_ohwi.data_ptr(), bias.data_ptr(), _ptr(residual), out.data_ptr(),
                                 N, H, W, Cin, Cout, KH, KW, sh, sw, pt, pl, dh, dw, Ho, Wo, out.shape[3],
-                                out_channel_offset, Cout if residual is None else residual.shape[3], a, _stream())
+                                out_channel_offset, Cout if residual is None else residual.shape[3], a, _stream(), cfg)
         return out
     # host reference
     xn = x.float().permute(0, 3, 1, 2)
@@ -134,7 +145,7 @@ def conv2d_nhwc(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor | None
 
 
 def gemm(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = None, residual: torch.Tensor | None = None,
-         act=None, out: torch.Tensor | None = None) -> torch.Tensor:
+         act=None, out: torch.Tensor | None = None, cfg: int = -1) -> torch.Tensor:
     """``act(x[M,K] @ w[N,K]^T + bias + residual)``; leading dims of x are flattened."""
     a = act_code(act)
     lead = x.shape[:-1]
@@ -155,10 +166,12 @@ def gemm(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = None, 
         _check(out2, "out", device=x.device)
         if bias is not None:
             _check(bias, "bias", torch.float32, x.device)
+        else:
+            bias = _zeros_bias(N, x.device)
         if residual is not None:
             _check(residual, "residual", device=x.device)
-        _hip().gemm_bf16(x2.data_ptr(), w_nk.data_ptr(), _ptr(bias), _ptr(residual), out2.data_ptr(), M, N, K, K, N,
-                         N, a, _stream())
+        _hip().gemm_bf16(x2.data_ptr(), w_nk.data_ptr(), bias.data_ptr(), _ptr(residual), out2.data_ptr(), M, N, K, K,
+                         N, N, a, _stream(), cfg)
         return out
     y = x2.float() @ w_nk.float().t()
     if bias is not None:
@@ -172,33 +185,71 @@ def gemm(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = None, 
 # ------------------------------------------------------------------------------ preprocess
 def preprocess_images(images_u8: torch.Tensor, out_hw=(224, 224), mean=(117.0, 117.0, 117.0),
                       std=(1.0, 1.0, 1.0), align_corners=False, half_pixel_centers=False,
-                      out: torch.Tensor | None = None) -> torch.Tensor:
-    """uint8 [B,H,W,3] → resize (TF ResizeBilinear) → (v-mean)/std → bf16 [B,Ho,Wo,8]
-    (channels 3..7 zero: the stem conv's Cin=8 layout)."""
+                      out: torch.Tensor | None = None, s2d: bool = False) -> torch.Tensor:
+    """uint8 [B,H,W,3] → resize (TF ResizeBilinear) → (v-mean)/std → bf16.
+
+    Layout ``[B,Ho,Wo,8]`` (channels 3..7 zero), or with ``s2d`` the 2x2 space-to-depth
+    layout ``[B,Ho/2,Wo/2,16]`` consumed by the stride-2 stem conv (``s2d_stem_weights``)."""
     if images_u8.dtype != torch.uint8 or images_u8.dim() != 4 or images_u8.shape[3] != 3:
         raise ValueError("preprocess_images expects uint8 [B,H,W,3]")
     B, Hi, Wi, _ = images_u8.shape
     Ho, Wo = out_hw
+    oshape = (B, Ho // 2, Wo // 2, 16) if s2d else (B, Ho, Wo, 8)
+    if s2d and (Ho % 2 or Wo % 2):
+        raise ValueError("space-to-depth preprocess needs an even output size")
     if out is None:
-        out = torch.empty((B, Ho, Wo, 8), dtype=torch.bfloat16 if images_u8.is_cuda else torch.float32,
+        out = torch.empty(oshape, dtype=torch.bfloat16 if images_u8.is_cuda else torch.float32,
                           device=images_u8.device)
-    if tuple(out.shape) != (B, Ho, Wo, 8):
-        raise ValueError(f"preprocess_images: out must be {(B, Ho, Wo, 8)}")
+    if tuple(out.shape) != oshape:
+        raise ValueError(f"preprocess_images: out must be {oshape}, got {tuple(out.shape)}")
     if images_u8.is_cuda:
         if not images_u8.is_contiguous():
             raise ValueError("preprocess_images: input must be contiguous")
         _check(out, "out", device=images_u8.device)
         _hip().preprocess_u8_to_bf16(images_u8.data_ptr(), out.data_ptr(), B, Hi, Wi, Ho, Wo, int(align_corners),
                                      int(half_pixel_centers), float(mean[0]), float(mean[1]), float(mean[2]),
-                                     1.0 / std[0], 1.0 / std[1], 1.0 / std[2], Hi * Wi * 3, _stream())
+                                     1.0 / std[0], 1.0 / std[1], 1.0 / std[2], Hi * Wi * 3, int(s2d), _stream())
         return out
     from ..graph.ops_nn import resize_bilinear_tf
 
     y = resize_bilinear_tf(images_u8.float(), Ho, Wo, align_corners, half_pixel_centers)
     y = (y - torch.tensor(mean)) / torch.tensor(std)
     out.zero_()
-    out[..., :3] = y.to(out.dtype)
+    if s2d:
+        blk = y.reshape(B, Ho // 2, 2, Wo // 2, 2, 3).permute(0, 1, 3, 2, 4, 5).reshape(B, Ho // 2, Wo // 2, 12)
+        out[..., :12] = blk.to(out.dtype)
+    else:
+        out[..., :3] = y.to(out.dtype)
     return out
+
+
+def s2d_stem_weights(w_hwio: torch.Tensor, H: int, W: int, pads):
+    """Rewrites a stride-2 KxK conv over RGB (pads top/left even) as a stride-1
+    ceil(K/2)² conv over the 2x2 space-to-depth input (16 channels, 12 used).
+
+    Returns ``(w_ohwi [Cout, KBH, KBW, 16], block_pads (t, b, l, r))``.  Cuts the stem's
+    MFMA work from K = 7·7·8 = 392 to 4·4·16 = 256 and makes every 16-B im2col load useful.
+    """
+    KH, KW, C, Cout = w_hwio.shape
+    pt, pb, pl, pr = pads
+    if C != 3 or pt % 2 or pl % 2 or H % 2 or W % 2:
+        raise ValueError("s2d stem needs RGB input, even top/left padding and even H/W")
+    KBH, KBW = (KH + 1) // 2, (KW + 1) // 2
+    w2 = torch.zeros(Cout, KBH, KBW, 16, dtype=torch.float32)
+    wf = w_hwio.float()
+    for kh in range(KH):
+        for kw in range(KW):
+            ch = ((kh % 2) * 2 + (kw % 2)) * 3
+            w2[:, kh // 2, kw // 2, ch:ch + 3] = wf[kh, kw].t()
+    Ho = (H + pt + pb - KH) // 2 + 1
+    Wo = (W + pl + pr - KW) // 2 + 1
+    Hb, Wb = H // 2, W // 2
+    pt_b, pl_b = pt // 2, pl // 2
+    pb_b = Ho - 1 + KBH - Hb - pt_b
+    pr_b = Wo - 1 + KBW - Wb - pl_b
+    if pb_b < 0 or pr_b < 0:
+        raise ValueError("s2d stem: negative block padding")
+    return w2, (pt_b, pb_b, pl_b, pr_b)
 
 
 # ------------------------------------------------------------------------------ pooling

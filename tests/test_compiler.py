@@ -50,3 +50,20 @@ def test_memory_reuse(small_resnet):
     plan = CompiledFunction(small_resnet, {"images:0": ((1, 72, 72, 3), "UINT8")}, ["probs:0"], "cpu")
     distinct = {s.outputs[0].buf.untyped_storage().data_ptr() for s in plan.steps if s.outputs[0].buf is not None}
     assert len(distinct) < len(plan.steps)  # buffers are recycled between layers
+
+
+def test_s2d_stem_equivalence():
+    """Stride-2 7x7 RGB stem == stride-1 4x4 conv over the space-to-depth input."""
+    from flink_tensorflow_amd.graph.ops_nn import conv2d_tf, same_pads
+    from flink_tensorflow_amd.ops import kernels as K
+
+    img = torch.randint(0, 256, (2, 100, 90, 3), dtype=torch.uint8)
+    w = torch.randn(7, 7, 3, 64)
+    a = K.preprocess_images(img, (224, 224))
+    ref = conv2d_tf(a[..., :3].float(), w, (2, 2), "SAME")
+    pt, pb = same_pads(224, 7, 2)
+    w2, pads = K.s2d_stem_weights(w, 224, 224, (pt, pb, pt, pb))
+    b = K.preprocess_images(img, (224, 224), s2d=True)
+    got = K.conv2d_nhwc(b, w2, pad=pads)
+    assert pads == (1, 2, 1, 2)
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-2)
