@@ -76,7 +76,11 @@ class CEPOperator(Operator):
     def _now(self, ts):
         return ts if ts is not None else time.time()
 
+    _evt = False  # event-time mode: records carry timestamps
+
     def process(self, rec, input_index=0):
+        if rec.ts is not None:
+            self._evt = True
         now = self._now(rec.ts)
         key = self.key_selector(rec.value) if self.key_selector else None
         self._expire(now, key)
@@ -117,9 +121,19 @@ class CEPOperator(Operator):
             self.partials[k] = keep
 
     def on_idle(self, now):
-        self._expire(time.time())
+        if not self._event_time():
+            self._expire(time.time())
+
+    def on_watermark(self, ts):
+        if self._event_time():
+            self._expire(ts)
+
+    def _event_time(self) -> bool:
+        return self._evt or self.current_watermark > float("-inf")
 
     def next_deadline(self):
+        if self._event_time():
+            return None
         w = self.pattern.window
         starts = [p.start for ps in self.partials.values() for p in ps]
         return (min(starts) + w) if (w is not None and starts) else None

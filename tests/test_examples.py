@@ -1,0 +1,82 @@
+"""The reference's example applications (Inception labelling, Johnny CEP) on the runtime."""
+import io
+import os
+
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+from flink_tensorflow_amd.models.zoo.inception import (ImageInputFormat, ImageNormalization, InceptionModel,
+                                                        googlenet_like_graph_def)
+from flink_tensorflow_amd.runtime import PROCESS_ONCE, StreamExecutionEnvironment
+from flink_tensorflow_amd.runtime.cep import CEP, Pattern
+
+
+def _jpeg(h=64, w=48, seed=0) -> bytes:
+    rng = np.random.default_rng(seed)
+    buf = io.BytesIO()
+    Image.fromarray(rng.integers(0, 256, (h, w, 3), dtype=np.uint8)).save(buf, format="JPEG")
+    return buf.getvalue()
+
+
+def test_image_normalization_graph():
+    m = ImageNormalization()
+    m.open()
+    out = m.normalize(_jpeg())
+    m.close()
+    assert tuple(out.shape) == (1, 224, 224, 3) and out.dtype == torch.float32
+    assert -118 <= out.min().item() and out.max().item() <= 139
+
+
+def test_inception_stream_labels(tmp_path):
+    for i in range(3):
+        (tmp_path / f"img{i}.jpg").write_bytes(_jpeg(seed=i))
+    (tmp_path / "partial.crdownload").write_bytes(b"junk")
+    model = InceptionModel(str(tmp_path), image_hw=(64, 48), device="cpu")
+    env = StreamExecutionEnvironment.get_execution_environment()
+    out = (env.read_file(ImageInputFormat(), str(tmp_path), PROCESS_ONCE)
+           .map_with_model(model, lambda rec, m: (rec[0], m.label([rec[1]])[0][0]))
+           .execute_and_collect())
+    assert sorted(n for n, _ in out) == ["img0.jpg", "img1.jpg", "img2.jpg"]
+    for _, (p, label) in out:
+        assert 0.0 <= p <= 1.0 and label.startswith("class_")
+
+
+def test_inception_host_normalized_records(tmp_path):
+    (tmp_path / "a.jpeg").write_bytes(_jpeg())
+    env = StreamExecutionEnvironment.get_execution_environment()
+    out = env.read_file(ImageInputFormat(normalize_on_host=True), str(tmp_path)).execute_and_collect()
+    name, tv = out[0]
+    assert name == "a.jpeg" and tv.shape() == (1, 224, 224, 3)
+
+
+def test_googlenet_graph_runs():
+    from flink_tensorflow_amd.graph.graph import Graph
+    from flink_tensorflow_amd.graph.session import Session
+
+    g = Graph.from_graph_def(googlenet_like_graph_def(num_classes=16, width=0.25))
+    y = Session(g).run("output:0", {"input:0": torch.randn(2, 224, 224, 3)})
+    assert tuple(y.shape) == (2, 16)
+    torch.testing.assert_close(y.sum(-1), torch.ones(2))
+
+
+def test_johnny_cep():
+    """cheeseburger → ladybug → llama within 60 s → AccessGranted; else AccessDenied
+    (``EX/inception/johnny.scala:52-62``)."""
+    def conf(lbl):
+        return lambda v: v[1] == lbl and v[0] >= 0.5
+
+    pattern = (Pattern.begin("first").where(conf("cheeseburger"))
+               .followed_by("second").where(conf("ladybug"))
+               .followed_by("third").where(conf("llama")).within(60))
+    events = [(0.9, "cheeseburger", 0.0), (0.3, "ladybug", 1.0), (0.8, "ladybug", 2.0), (0.7, "cat", 3.0),
+              (0.95, "llama", 4.0),                                  # granted (t=0..4)
+              (0.9, "cheeseburger", 100.0), (0.9, "ladybug", 110.0),  # times out at 160
+              (0.9, "llama", 170.0)]
+    env = StreamExecutionEnvironment.get_execution_environment()
+    stream = env.from_collection(events).assign_timestamps_and_watermarks(lambda e: e[2])
+    out = CEP.pattern(stream, pattern).select(lambda m: ("AccessGranted", m["third"][2]),
+                                              lambda partial, ts: ("AccessDenied", ts)).execute_and_collect()
+    assert ("AccessGranted", 4.0) in out
+    assert ("AccessDenied", 160.0) in out
