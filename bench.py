@@ -33,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "records/sec (whole node) + p50 per-record latency, ResNet-50 stream DP=1/8"
+METRIC_BERT = "records/sec (whole node) + p50 per-record latency, BERT-base text-classification stream"
 
 
 def main():
@@ -44,7 +45,10 @@ def main():
     ap.add_argument("--image-hw", type=int, default=256, help="decoded source image size (resized to 224)")
     ap.add_argument("--depth", type=int, default=3, help="pipeline slots")
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
-    ap.add_argument("--pool", type=int, default=512, help="distinct synthetic images cycled by the source")
+    ap.add_argument("--pool", type=int, default=512, help="distinct synthetic records cycled by the source")
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert"],
+                    help="resnet50 = BASELINE headline; bert = BERT-base text-classification stream")
+    ap.add_argument("--seq-len", type=int, default=128)
     args = ap.parse_args()
 
     import torch
@@ -67,18 +71,43 @@ def main():
 
     B, HW = args.batch, args.image_hw
     t0 = time.perf_counter()
-    gd = resnet50_graph_def(image_hw=(HW, HW), top_k=5, seed=0)
-    graph = Graph.from_graph_def(gd)
-    plan = CompiledFunction(graph, {"images:0": ((B, HW, HW, 3), "UINT8")}, ["top_k:0", "top_k:1"], dev,
-                            use_graph=not args.no_graph, strict=True)
-    # rank 0's weights to all ranks over RCCL; in-place, so the captured graph stays valid
-    nbytes = comm.broadcast_tensors(plan.params, src=0)
+    if args.model == "resnet50":
+        gd = resnet50_graph_def(image_hw=(HW, HW), top_k=5, seed=0)
+        graph = Graph.from_graph_def(gd)
+        plan = CompiledFunction(graph, {"images:0": ((B, HW, HW, 3), "UINT8")}, ["top_k:0", "top_k:1"], dev,
+                                use_graph=not args.no_graph, strict=True)
+        params = plan.params
+        feed, rec_shape, rec_dtype = "images:0", (HW, HW, 3), torch.uint8
+        flops_per_record = resnet50_flops_per_image(224)
+        rng = np.random.default_rng(1234 + rank)
+        pool = rng.integers(0, 256, size=(args.pool, HW, HW, 3), dtype=np.uint8)
+        model_name, data = "ResNet-50 v1.5", f"synthetic decoded uint8 {HW}x{HW}x3 images, random-init weights"
+        seq = None
+    else:
+        from flink_tensorflow_amd.models.zoo.bert import (BertConfig, BertDeviceWeights, BertEncoderPlan,
+                                                          init_bert_weights)
+
+        cfg = BertConfig.base()
+        seq = args.seq_len
+        w = BertDeviceWeights(init_bert_weights(cfg, seed=rank), cfg, dev)  # rank-local init, then broadcast
+        plan = BertEncoderPlan(w, B, seq, use_graph=not args.no_graph)
+        params = w.tensors()
+        feed, rec_shape, rec_dtype = "ids", (seq,), torch.int32
+        flops_per_record = plan.flops() / B
+        rng = np.random.default_rng(1234 + rank)
+        pool = rng.integers(1000, cfg.vocab_size, size=(args.pool, seq), dtype=np.int32)
+        lens = rng.integers(seq // 2, seq + 1, size=args.pool)
+        for i, n in enumerate(lens):
+            pool[i, n:] = 0
+        pool[:, 0] = 101
+        model_name, data = "BERT-base (seq classification)", f"synthetic token ids, seq {seq}, random-init weights"
+    # rank 0's weights to all ranks over RCCL (one flattened buffer per dtype); in place,
+    # so the captured hipGraph stays valid
+    nbytes = comm.broadcast_tensors(params, src=0)
     compile_s = time.perf_counter() - t0
 
-    rng = np.random.default_rng(1234 + rank)
-    pool = rng.integers(0, 256, size=(args.pool, HW, HW, 3), dtype=np.uint8)
     records = [pool[i] for i in range(args.pool)]
-    runner = PipelinedGpuRunner({B: plan}, "images:0", lambda p: p.output_tensors(), (HW, HW, 3), torch.uint8,
+    runner = PipelinedGpuRunner({B: plan}, feed, lambda p: p.output_tensors(), rec_shape, rec_dtype,
                                 depth=args.depth, device=dev)
 
     cursor = 0
@@ -120,10 +149,10 @@ def main():
     p50s = comm.all_gather_object(p50)
     per_gpu = B * args.steps / elapsed
     total = ws * B * args.steps / elapsed_max
-    flops = resnet50_flops_per_image(224) * total
+    flops = flops_per_record * total
     if rank == 0:
         out = {
-            "metric": METRIC,
+            "metric": METRIC if args.model == "resnet50" else METRIC_BERT,
             "value": round(total, 1),
             "unit": "records/s",
             "n_gpus": ws,
@@ -134,16 +163,17 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": f"synthetic decoded uint8 {HW}x{HW}x3 images, random-init weights",
-            "config": {"model": "ResNet-50 v1.5", "global_batch": B * ws, "seq_len": None,
-                       "parallelism": f"dp{ws}", "micro_batch_per_gpu": B, "input_hw": 224},
+            "data": data,
+            "config": {"model": model_name, "global_batch": B * ws, "seq_len": seq,
+                       "parallelism": f"dp{ws}", "micro_batch_per_gpu": B,
+                       "input_hw": 224 if seq is None else None},
             "p50_latency_ms": round(float(np.median(p50s)), 3),
             "p99_latency_ms": round(p99, 3),
             "per_gpu_records_per_s": round(per_gpu, 1),
             "model_tflops_per_s": round(flops / 1e12, 1),
             "compile_s": round(compile_s, 2),
             "weights_broadcast_bytes": nbytes,
-            "plan": plan.summary(),
+            "plan": plan.summary() if hasattr(plan, "summary") else {"hip_graph": plan.graph is not None},
         }
         print(json.dumps(out), flush=True)
     if comm.is_dist():

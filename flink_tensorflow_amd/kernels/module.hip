@@ -9,6 +9,7 @@ void register_nn_misc(pybind11::module_& m);
 void register_transformer(pybind11::module_& m);
 void register_embedding(pybind11::module_& m);
 void register_fp8(pybind11::module_& m);
+void register_attention(pybind11::module_& m);
 
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "flink_tensorflow_amd CDNA4 (gfx950) kernels";
@@ -18,4 +19,5 @@ PYBIND11_MODULE(_hip, m) {
   register_transformer(m);
   register_embedding(m);
   register_fp8(m);
+  register_attention(m);
 }

@@ -1,0 +1,372 @@
+"""BERT-base text classification (BASELINE config 3: BERT stream, DP over xGMI).
+
+The encoder runs entirely on the CDNA4 kernels, one hipGraph per (batch bucket, seq):
+
+    embed_ln (gather word/pos/type + LayerNorm, one pass)
+    12 x [ gemm(x, Wqkv) + b          -> qkv [T, 2304]     (fused Q|K|V projection)
+           attention(qkv, ids)        -> ctx [T, 768]      (flash-style, key-padding mask)
+           gemm(ctx, Wo) + b + x      -> y                 (residual fused in the epilogue)
+           layernorm(y)               -> x
+           gemm(x, W1) + b -> GELU    -> h [T, 3072]       (activation fused)
+           gemm(h, W2) + b + x        -> y ; layernorm(y) -> x ]
+    pooler: gemm(x[:, 0], Wp) + b -> tanh ; classifier gemm -> softmax (host: 2 logits)
+
+Weights are random-init (no checkpoint download) but use the TF BERT checkpoint variable
+names, so ``load_tf_checkpoint`` can read a real ``bert_model.ckpt`` bundle through the
+native TensorBundle reader.  Text records are tokenized on the host by a hashing
+WordPiece-free tokenizer (no vocab file offline); token-id records bypass it.
+"""
+from __future__ import annotations
+
+import re
+import zlib
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ...ops import kernels as K
+from ...runtime.model_functions import BatchedGpuModel
+from ..core import RichModel, default_device
+
+
+@dataclass
+class BertConfig:
+    vocab_size: int = 30522
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    intermediate: int = 3072
+    max_position: int = 512
+    type_vocab: int = 2
+    num_labels: int = 2
+    eps: float = 1e-12
+
+    @staticmethod
+    def base(**kw) -> "BertConfig":
+        return BertConfig(**kw)
+
+    @staticmethod
+    def tiny(**kw) -> "BertConfig":
+        d = dict(vocab_size=1000, hidden=128, layers=2, heads=2, intermediate=256, max_position=128)
+        d.update(kw)
+        return BertConfig(**d)
+
+    def params(self) -> int:
+        h, i = self.hidden, self.intermediate
+        emb = (self.vocab_size + self.max_position + self.type_vocab) * h + 2 * h
+        layer = 4 * h * h + 4 * h + 2 * h * i + i + h + 4 * h
+        return emb + self.layers * layer + h * h + h + h * self.num_labels + self.num_labels
+
+
+class HashingTokenizer:
+    """Lower-case word split, crc32-hashed into the vocab; [CLS] ... [SEP], pad 0."""
+
+    CLS, SEP, PAD = 101, 102, 0
+
+    def __init__(self, vocab_size: int, max_len: int):
+        self.vocab_size = vocab_size
+        self.max_len = max_len
+
+    def __call__(self, text: str) -> np.ndarray:
+        ids = [self.CLS]
+        lo = min(1000, self.vocab_size // 2)  # ids below `lo` are reserved (special tokens)
+        for w in re.findall(r"[a-z0-9]+|[^\sa-z0-9]", text.lower()):
+            ids.append(lo + zlib.crc32(w.encode()) % (self.vocab_size - lo))
+            if len(ids) >= self.max_len - 1:
+                break
+        ids.append(self.SEP)
+        out = np.zeros(self.max_len, dtype=np.int32)
+        out[: len(ids)] = ids
+        return out
+
+
+def init_bert_weights(cfg: BertConfig, seed: int = 0) -> dict[str, torch.Tensor]:
+    """Random-init fp32 host weights named like the TF BERT checkpoint."""
+    g = torch.Generator().manual_seed(seed)
+
+    def n(*shape):
+        return torch.randn(*shape, generator=g) * 0.02
+
+    h, i = cfg.hidden, cfg.intermediate
+    w = {
+        "bert/embeddings/word_embeddings": n(cfg.vocab_size, h),
+        "bert/embeddings/position_embeddings": n(cfg.max_position, h),
+        "bert/embeddings/token_type_embeddings": n(cfg.type_vocab, h),
+        "bert/embeddings/LayerNorm/gamma": torch.ones(h),
+        "bert/embeddings/LayerNorm/beta": torch.zeros(h),
+        "bert/pooler/dense/kernel": n(h, h),
+        "bert/pooler/dense/bias": torch.zeros(h),
+        "output_weights": n(cfg.num_labels, h),
+        "output_bias": torch.zeros(cfg.num_labels),
+    }
+    for l in range(cfg.layers):
+        p = f"bert/encoder/layer_{l}/"
+        for nm in ("query", "key", "value"):
+            w[p + f"attention/self/{nm}/kernel"] = n(h, h)
+            w[p + f"attention/self/{nm}/bias"] = torch.zeros(h)
+        w[p + "attention/output/dense/kernel"] = n(h, h)
+        w[p + "attention/output/dense/bias"] = torch.zeros(h)
+        w[p + "attention/output/LayerNorm/gamma"] = torch.ones(h)
+        w[p + "attention/output/LayerNorm/beta"] = torch.zeros(h)
+        w[p + "intermediate/dense/kernel"] = n(h, i)
+        w[p + "intermediate/dense/bias"] = torch.zeros(i)
+        w[p + "output/dense/kernel"] = n(i, h)
+        w[p + "output/dense/bias"] = torch.zeros(h)
+        w[p + "output/LayerNorm/gamma"] = torch.ones(h)
+        w[p + "output/LayerNorm/beta"] = torch.zeros(h)
+    return w
+
+
+def load_tf_checkpoint(prefix: str, cfg: BertConfig) -> dict[str, torch.Tensor]:
+    """Reads a TF BERT checkpoint (TensorBundle V2) with the native bundle reader."""
+    from ...io.bundle import BundleReader
+
+    ref = init_bert_weights(cfg)
+    with BundleReader(prefix) as r:
+        return {k: r.read(k).float() if k in r else v for k, v in ref.items()}
+
+
+class BertDeviceWeights:
+    """Kernel-layout device weights: bf16 [N, K] matrices (QKV fused), fp32 biases/LN."""
+
+    def __init__(self, host: dict[str, torch.Tensor], cfg: BertConfig, device):
+        d = torch.device(device)
+        bf = torch.bfloat16 if d.type == "cuda" else torch.float32
+
+        def mat(kernel):  # TF kernels are [in, out]; the GEMM wants [out, in]
+            return kernel.t().contiguous().to(d, bf)
+
+        def vec(v):
+            return v.float().contiguous().to(d)
+
+        self.cfg = cfg
+        self.word = host["bert/embeddings/word_embeddings"].to(d, bf).contiguous()
+        self.pos = host["bert/embeddings/position_embeddings"].to(d, bf).contiguous()
+        self.type = host["bert/embeddings/token_type_embeddings"].to(d, bf).contiguous()
+        self.emb_g = vec(host["bert/embeddings/LayerNorm/gamma"])
+        self.emb_b = vec(host["bert/embeddings/LayerNorm/beta"])
+        self.layers = []
+        for l in range(cfg.layers):
+            p = f"bert/encoder/layer_{l}/"
+            qkv_w = torch.cat([host[p + f"attention/self/{nm}/kernel"] for nm in ("query", "key", "value")], 1)
+            qkv_b = torch.cat([host[p + f"attention/self/{nm}/bias"] for nm in ("query", "key", "value")])
+            self.layers.append({
+                "qkv_w": mat(qkv_w), "qkv_b": vec(qkv_b),
+                "o_w": mat(host[p + "attention/output/dense/kernel"]), "o_b": vec(host[p + "attention/output/dense/bias"]),
+                "ln1_g": vec(host[p + "attention/output/LayerNorm/gamma"]),
+                "ln1_b": vec(host[p + "attention/output/LayerNorm/beta"]),
+                "i_w": mat(host[p + "intermediate/dense/kernel"]), "i_b": vec(host[p + "intermediate/dense/bias"]),
+                "f_w": mat(host[p + "output/dense/kernel"]), "f_b": vec(host[p + "output/dense/bias"]),
+                "ln2_g": vec(host[p + "output/LayerNorm/gamma"]), "ln2_b": vec(host[p + "output/LayerNorm/beta"]),
+            })
+        self.pool_w = mat(host["bert/pooler/dense/kernel"])
+        self.pool_b = vec(host["bert/pooler/dense/bias"])
+        nl = cfg.num_labels
+        npad = -(-nl // 8) * 8  # GEMM N must be a multiple of 8: pad the classifier
+        cw = torch.zeros(npad, cfg.hidden)
+        cw[:nl] = host["output_weights"]
+        cb = torch.zeros(npad)
+        cb[:nl] = host["output_bias"]
+        self.cls_w = cw.to(d, bf).contiguous()
+        self.cls_b = cb.to(d)
+
+    def tensors(self) -> list[torch.Tensor]:
+        out = [self.word, self.pos, self.type, self.emb_g, self.emb_b, self.pool_w, self.pool_b, self.cls_w, self.cls_b]
+        for L in self.layers:
+            out += list(L.values())
+        return out
+
+
+class BertEncoderPlan:
+    """Preallocated buffers + launch sequence for one (batch, seq); hipGraph-captured."""
+
+    def __init__(self, w: BertDeviceWeights, batch: int, seq: int, use_graph: bool = True):
+        cfg = w.cfg
+        self.w, self.B, self.S = w, batch, seq
+        d = w.word.device
+        dt = w.word.dtype
+        T = batch * seq
+        h = cfg.hidden
+        self.ids = torch.zeros(T, dtype=torch.int32, device=d)
+        self.x = torch.empty(T, h, dtype=dt, device=d)
+        self.y = torch.empty(T, h, dtype=dt, device=d)
+        self.qkv = torch.empty(T, 3 * h, dtype=dt, device=d)
+        self.ctx = torch.empty(T, h, dtype=dt, device=d)
+        self.ffn = torch.empty(T, cfg.intermediate, dtype=dt, device=d)
+        self.cls_in = torch.empty(batch, h, dtype=dt, device=d)
+        self.pooled = torch.empty(batch, h, dtype=dt, device=d)
+        self.logits = torch.empty(batch, w.cls_w.shape[0], dtype=dt, device=d)
+        self.graph = None
+        if use_graph and d.type == "cuda":
+            self._capture()
+
+    def _run(self):
+        w, cfg, B, S = self.w, self.w.cfg, self.B, self.S
+        K.embed_layernorm(self.ids, None, w.word, w.pos, w.type, w.emb_g, w.emb_b, S, cfg.eps, out=self.x)
+        for L in w.layers:
+            K.gemm(self.x, L["qkv_w"], L["qkv_b"], out=self.qkv)
+            K.attention(self.qkv, self.ids, B, S, cfg.heads, out=self.ctx)
+            K.gemm(self.ctx, L["o_w"], L["o_b"], residual=self.x, out=self.y)
+            K.layernorm(self.y, L["ln1_g"], L["ln1_b"], eps=cfg.eps, out=self.x)
+            K.gemm(self.x, L["i_w"], L["i_b"], act="gelu", out=self.ffn)
+            K.gemm(self.ffn, L["f_w"], L["f_b"], residual=self.x, out=self.y)
+            K.layernorm(self.y, L["ln2_g"], L["ln2_b"], eps=cfg.eps, out=self.x)
+        self.cls_in.copy_(self.x.view(B, S, -1)[:, 0])
+        K.gemm(self.cls_in, w.pool_w, w.pool_b, act="tanh", out=self.pooled)
+        K.gemm(self.pooled, w.cls_w, w.cls_b, out=self.logits)
+
+    def _capture(self):
+        s = torch.cuda.Stream(self.ids.device)
+        s.wait_stream(torch.cuda.current_stream(self.ids.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._run()
+        torch.cuda.current_stream(self.ids.device).wait_stream(s)
+        torch.cuda.synchronize(self.ids.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._run()
+        self.graph = g
+
+    # plan protocol used by PipelinedGpuRunner
+    def input_buffer(self, feed: str) -> torch.Tensor:
+        return self.ids.view(self.B, self.S)
+
+    def replay(self):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._run()
+
+    def output_tensors(self):
+        return [self.logits[:, : self.w.cfg.num_labels]]
+
+    def __call__(self, ids: torch.Tensor) -> torch.Tensor:
+        self.ids.view(self.B, self.S).copy_(ids)
+        self.replay()
+        return torch.softmax(self.logits[:, : self.w.cfg.num_labels].float(), -1)
+
+    def flops(self) -> float:
+        cfg, T = self.w.cfg, self.B * self.S
+        h, i = cfg.hidden, cfg.intermediate
+        per_layer = 2 * T * (3 * h * h + h * h + 2 * h * i) + 4 * self.B * cfg.heads * self.S * self.S * (h // cfg.heads)
+        return cfg.layers * per_layer
+
+
+class BertClassifierModel(RichModel, BatchedGpuModel):
+    """Text (or token-id) records → class probabilities; micro-batched on the GPU."""
+
+    _TRANSIENT = ("_w", "_plans", "_runner")
+
+    def __init__(self, cfg: BertConfig | None = None, seq_len: int = 128, buckets=(64, 256), seed: int = 0,
+                 device=None, checkpoint: str | None = None, depth: int = 3, use_graph: bool = True):
+        self.cfg = cfg or BertConfig.base()
+        self.seq_len = seq_len
+        self.buckets = tuple(sorted(buckets))
+        self.seed = seed
+        self.device = device
+        self.checkpoint = checkpoint
+        self.depth = depth
+        self.use_graph = use_graph
+        self.tokenizer = HashingTokenizer(self.cfg.vocab_size, seq_len)
+        self._w = self._plans = self._runner = None
+
+    def open(self):
+        dev = torch.device(self.device) if self.device is not None else default_device()
+        host = load_tf_checkpoint(self.checkpoint, self.cfg) if self.checkpoint else init_bert_weights(self.cfg, self.seed)
+        self._w = BertDeviceWeights(host, self.cfg, dev)
+        self._plans = {b: BertEncoderPlan(self._w, b, self.seq_len, self.use_graph) for b in self.buckets}
+        if dev.type == "cuda":
+            from ...batching.engine import PipelinedGpuRunner
+
+            self._runner = PipelinedGpuRunner(self._plans, "ids", lambda p: p.output_tensors(), (self.seq_len,),
+                                              torch.int32, depth=self.depth, device=dev)
+
+    def close(self):
+        if self._runner is not None:
+            self._runner.drain()
+        self._w = self._plans = self._runner = None
+
+    @property
+    def is_open(self):
+        return self._w is not None
+
+    def weights(self) -> BertDeviceWeights:
+        return self._w
+
+    def encode(self, record) -> np.ndarray:
+        if isinstance(record, str):
+            return self.tokenizer(record)
+        a = np.asarray(record, dtype=np.int32).reshape(-1)
+        out = np.zeros(self.seq_len, dtype=np.int32)
+        out[: min(len(a), self.seq_len)] = a[: self.seq_len]
+        return out
+
+    def predict(self, records) -> torch.Tensor:
+        """Synchronous class probabilities [N, num_labels]."""
+        ids = np.stack([self.encode(r) for r in records])
+        n = len(ids)
+        b = next((bk for bk in self.buckets if bk >= n), None)
+        if b is None:
+            return torch.cat([self.predict(records[i:i + self.buckets[-1]]) for i in range(0, n, self.buckets[-1])])
+        buf = np.zeros((b, self.seq_len), dtype=np.int32)
+        buf[:n] = ids
+        plan = self._plans[b]
+        return plan(torch.from_numpy(buf).to(plan.ids.device))[:n].cpu()
+
+    # BatchedGpuModel
+    def _res(self, br):
+        probs = torch.softmax(br.outputs[0][: br.n].float(), -1)
+        return probs.tolist(), br.tags, br.latencies
+
+    def submit(self, records, ingest_ts, tags):
+        if self._runner is None:
+            import time
+
+            return [(self.predict(records).tolist(), tags, time.perf_counter() - np.asarray(ingest_ts))]
+        arrs = [self.encode(r) for r in records]
+        cap = self.buckets[-1]
+        out = []
+        for s in range(0, len(arrs), cap):
+            for br in self._runner.submit(arrs[s:s + cap], np.asarray(ingest_ts[s:s + cap]), list(tags[s:s + cap])):
+                out.append(self._res(br))
+        return out
+
+    def poll(self):
+        return [self._res(b) for b in self._runner.poll()] if self._runner is not None else []
+
+    def drain(self):
+        return [self._res(b) for b in self._runner.drain()] if self._runner is not None else []
+
+
+def reference_forward(host: dict[str, torch.Tensor], cfg: BertConfig, ids: torch.Tensor) -> torch.Tensor:
+    """Plain PyTorch fp32 BERT (numerics oracle): ids [B, S] → logits [B, num_labels]."""
+    import torch.nn.functional as F
+
+    B, S = ids.shape
+    h = cfg.hidden
+    x = host["bert/embeddings/word_embeddings"][ids.long()] + host["bert/embeddings/position_embeddings"][:S]
+    x = x + host["bert/embeddings/token_type_embeddings"][0]
+    x = F.layer_norm(x, (h,), host["bert/embeddings/LayerNorm/gamma"], host["bert/embeddings/LayerNorm/beta"], cfg.eps)
+    mask = (ids == 0)[:, None, None, :]
+    dh = h // cfg.heads
+    for l in range(cfg.layers):
+        p = f"bert/encoder/layer_{l}/"
+
+        def lin(t, nm):
+            return t @ host[p + nm + "/kernel"] + host[p + nm + "/bias"]
+
+        q = lin(x, "attention/self/query").view(B, S, cfg.heads, dh).transpose(1, 2)
+        k = lin(x, "attention/self/key").view(B, S, cfg.heads, dh).transpose(1, 2)
+        v = lin(x, "attention/self/value").view(B, S, cfg.heads, dh).transpose(1, 2)
+        a = (q @ k.transpose(-1, -2)) / dh ** 0.5
+        a = torch.softmax(a.masked_fill(mask, float("-inf")), -1).nan_to_num(0.0)
+        ctx = (a @ v).transpose(1, 2).reshape(B, S, h)
+        x = F.layer_norm(lin(ctx, "attention/output/dense") + x, (h,), host[p + "attention/output/LayerNorm/gamma"],
+                         host[p + "attention/output/LayerNorm/beta"], cfg.eps)
+        f = F.gelu(lin(x, "intermediate/dense"), approximate="tanh")
+        x = F.layer_norm(lin(f, "output/dense") + x, (h,), host[p + "output/LayerNorm/gamma"],
+                         host[p + "output/LayerNorm/beta"], cfg.eps)
+    pooled = torch.tanh(x[:, 0] @ host["bert/pooler/dense/kernel"] + host["bert/pooler/dense/bias"])
+    return pooled @ host["output_weights"].t() + host["output_bias"]

@@ -321,6 +321,65 @@ def softmax_topk(logits: torch.Tensor, k: int, want_probs: bool = False, vals=No
     return vals, idxs, probs
 
 
+# ------------------------------------------------------------------------------ attention
+def attention(qkv: torch.Tensor, ids: torch.Tensor, batch: int, seq: int, heads: int, pad_id: int = 0,
+              scale: float | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Multi-head self-attention over the fused QKV projection output.
+
+    ``qkv`` [B*S, 3*H*64] bf16 (Q|K|V blocks, head h at h*64), ``ids`` [B*S] int32 token
+    ids (keys whose id == ``pad_id`` are masked).  Returns ctx [B*S, H*64]."""
+    T = batch * seq
+    Dh = qkv.shape[1] // (3 * heads)
+    if qkv.shape != (T, 3 * heads * Dh):
+        raise ValueError(f"attention: qkv shape {tuple(qkv.shape)} != {(T, 3 * heads * Dh)}")
+    if ids.numel() != T:
+        raise ValueError("attention: ids must have B*S entries")
+    scale = (1.0 / Dh ** 0.5) if scale is None else scale
+    if out is None:
+        out = torch.empty((T, heads * Dh), dtype=qkv.dtype, device=qkv.device)
+    if qkv.is_cuda:
+        _check(qkv, "qkv", device=qkv.device)
+        _check(out, "out", device=qkv.device)
+        _check(ids, "ids", torch.int32, qkv.device)
+        _hip().attention_fwd_bf16(qkv.data_ptr(), ids.data_ptr(), out.data_ptr(), batch, seq, heads, Dh, pad_id,
+                                  float(scale), _stream())
+        return out
+    q, k, v = qkv.float().reshape(batch, seq, 3, heads, Dh).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * scale
+    mask = (ids.reshape(batch, 1, 1, seq) == pad_id)
+    s = s.masked_fill(mask, float("-inf"))
+    p = torch.softmax(s, -1).nan_to_num(0.0)
+    o = (p @ v).permute(0, 2, 1, 3).reshape(T, heads * Dh)
+    out.copy_(o.to(out.dtype))
+    return out
+
+
+def embed_layernorm(ids: torch.Tensor, type_ids: torch.Tensor | None, word: torch.Tensor, pos: torch.Tensor,
+                    type_emb: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, seq: int, eps: float = 1e-12,
+                    out: torch.Tensor | None = None) -> torch.Tensor:
+    """``LN(word[ids] + pos[t % S] + type[type_ids])`` → [T, D] bf16 (one fused pass)."""
+    T = ids.numel()
+    V, D = word.shape
+    if out is None:
+        out = torch.empty((T, D), dtype=word.dtype, device=word.device)
+    if ids.is_cuda:
+        _check(ids, "ids", torch.int32, ids.device)
+        for t, n in ((word, "word"), (pos, "pos"), (type_emb, "type"), (out, "out")):
+            _check(t, n, device=ids.device)
+        if type_ids is not None:
+            _check(type_ids, "type_ids", torch.int32, ids.device)
+        if pos.shape[0] < seq:
+            raise ValueError("embed_layernorm: position table shorter than the sequence")
+        _hip().embed_ln_bf16(ids.data_ptr(), _ptr(type_ids), word.data_ptr(), pos.data_ptr(), type_emb.data_ptr(),
+                             gamma.data_ptr(), beta.data_ptr(), out.data_ptr(), T, seq, D, V, float(eps), _stream())
+        return out
+    idx = ids.long().clamp(0, V - 1)
+    x = word.float()[idx] + pos.float()[torch.arange(T) % seq]
+    x = x + type_emb.float()[type_ids.long() if type_ids is not None else torch.zeros(T, dtype=torch.long)]
+    out.copy_(F.layer_norm(x, (D,), gamma.float(), beta.float(), eps).to(out.dtype))
+    return out
+
+
 # ------------------------------------------------------------------------------ layernorm
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, residual: torch.Tensor | None = None,
               eps: float = 1e-12, out=None, sum_out=None) -> torch.Tensor:

@@ -1,0 +1,81 @@
+"""BERT encoder on the kernel path vs a plain PyTorch fp32 BERT."""
+import numpy as np
+import pytest
+import torch
+
+from flink_tensorflow_amd.models.zoo.bert import (BertClassifierModel, BertConfig, BertDeviceWeights,
+                                                  BertEncoderPlan, HashingTokenizer, init_bert_weights,
+                                                  reference_forward)
+
+
+def _ids(B, S, vocab, seed=0):
+    rng = np.random.default_rng(seed)
+    ids = rng.integers(1000, vocab, (B, S)).astype(np.int32)
+    lens = rng.integers(S // 2, S + 1, B)
+    for b, n in enumerate(lens):
+        ids[b, n:] = 0  # padding masked in attention
+    ids[:, 0] = 101
+    return torch.from_numpy(ids)
+
+
+def test_bert_plan_host_matches_reference():
+    cfg = BertConfig.tiny(vocab_size=2000)
+    host = init_bert_weights(cfg, seed=1)
+    plan = BertEncoderPlan(BertDeviceWeights(host, cfg, "cpu"), batch=3, seq=24)
+    ids = _ids(3, 24, cfg.vocab_size)
+    got = plan(ids)
+    ref = torch.softmax(reference_forward(host, cfg, ids), -1)
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_tokenizer_and_model_host():
+    tok = HashingTokenizer(30522, 16)
+    a = tok("Hello, world!")
+    assert a[0] == 101 and a[5] == 102 and (a[6:] == 0).all() and a.dtype == np.int32  # hello , world !
+    m = BertClassifierModel(BertConfig.tiny(), seq_len=16, buckets=(4,), device="cpu")
+    m.open()
+    p = m.predict(["good movie", "bad movie", "meh"])
+    assert p.shape == (3, 2)
+    torch.testing.assert_close(p.sum(-1), torch.ones(3))
+    m.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [128, 77])
+def test_bert_base_gpu_vs_fp32_reference(S):
+    cfg = BertConfig.base()
+    host = init_bert_weights(cfg, seed=2)
+    dev = torch.device("cuda", 0)
+    plan = BertEncoderPlan(BertDeviceWeights(host, cfg, dev), batch=4, seq=S)
+    ids = _ids(4, S, cfg.vocab_size, seed=S)
+    got = plan(ids.to(dev)).cpu()
+    ref = torch.softmax(reference_forward(host, cfg, ids), -1)
+    torch.testing.assert_close(got, ref, rtol=0, atol=3e-2)
+    assert plan.graph is not None
+
+
+@pytest.mark.gpu
+def test_attention_kernel_vs_reference():
+    from flink_tensorflow_amd.ops import kernels as K
+
+    B, S, H = 3, 100, 12
+    g = torch.Generator().manual_seed(0)
+    qkv = torch.randn(B * S, 3 * H * 64, generator=g).to(torch.bfloat16)
+    ids = _ids(B, S, 30000).reshape(-1)
+    ref = K.attention(qkv, ids, B, S, H)
+    got = K.attention(qkv.cuda(), ids.cuda(), B, S, H)
+    torch.testing.assert_close(got.float().cpu(), ref.float(), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+def test_embed_ln_kernel():
+    from flink_tensorflow_amd.ops import kernels as K
+
+    V, D, S = 500, 768, 32
+    word, pos, typ = (torch.randn(V, D) * 0.02).to(torch.bfloat16), (torch.randn(64, D) * 0.02).to(torch.bfloat16), \
+        (torch.randn(2, D) * 0.02).to(torch.bfloat16)
+    gm, bt = torch.randn(D), torch.randn(D)
+    ids = torch.randint(0, V, (4 * S,), dtype=torch.int32)
+    ref = K.embed_layernorm(ids, None, word, pos, typ, gm, bt, S)
+    got = K.embed_layernorm(ids.cuda(), None, word.cuda(), pos.cuda(), typ.cuda(), gm.cuda(), bt.cuda(), S)
+    torch.testing.assert_close(got.float().cpu(), ref.float(), rtol=2e-2, atol=5e-2)

@@ -1,0 +1,114 @@
+"""Collective layer on CPU processes (gloo, world_size 2): weight broadcast, bucketed
+overlapped gradient all-reduce, metric reduction, and a distributed stream whose sources
+are partitioned by rank (the one-process-per-GPU DP layout, rehearsed on the host)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    try:
+        from flink_tensorflow_amd.parallel import comm
+
+        comm.init_distributed(backend="gloo")
+        q.put((rank, fn(rank, world)))
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, f"ERROR {e}\n{traceback.format_exc()}"))
+
+
+def _run(fn, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for r, v in out.items():
+        assert not (isinstance(v, str) and v.startswith("ERROR")), v
+    return out
+
+
+def _broadcast(rank, world):
+    from flink_tensorflow_amd.parallel import comm
+
+    ts = [torch.full((3, 4), float(rank)), torch.arange(5, dtype=torch.int64) * (rank + 1),
+          torch.full((7,), float(rank + 10))]
+    n = comm.broadcast_tensors(ts, src=0)
+    return [t.tolist() for t in ts], n
+
+
+def test_broadcast_tensors():
+    out = _run(_broadcast)
+    assert out[0][0] == out[1][0]
+    assert out[1][0][0] == [[0.0] * 4] * 3 and out[1][0][1] == [0, 1, 2, 3, 4]
+    assert out[1][1] == (12 + 7) * 4 + 5 * 8
+
+
+def _grads(rank, world):
+    from flink_tensorflow_amd.parallel import comm
+
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 3))
+    bucketer = comm.GradBucketer(list(model.parameters()), bucket_bytes=256)
+    x = torch.randn(4, 8) + rank
+    model(x).pow(2).sum().backward()
+    bucketer.synchronize()
+    total = comm.all_reduce_scalar(float(rank + 1), "sum")
+    return [p.grad.clone() for p in model.parameters()], len(bucketer.buckets), total
+
+
+def test_grad_bucketer_averages():
+    out = _run(_grads)
+    g0, nb, total = out[0]
+    g1, _, _ = out[1]
+    assert nb > 1 and total == 3.0
+    for a, b in zip(g0, g1):
+        torch.testing.assert_close(a, b)
+    # compare with the single-process average of both ranks' gradients
+    ref = None
+    for r in range(2):  # replay each rank's RNG sequence: seed → model init → input
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 3))
+        x = torch.randn(4, 8) + r
+        model(x).pow(2).sum().backward()
+        if ref is None:
+            ref = [torch.zeros_like(p) for p in model.parameters()]
+        for acc, p in zip(ref, model.parameters()):
+            acc += p.grad / 2
+    for a, b in zip(g0, ref):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def _stream(rank, world):
+    from flink_tensorflow_amd.runtime import StreamExecutionEnvironment
+
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    return sorted(env.from_collection(list(range(40)), parallelism=2).map(lambda v: v * 10).execute_and_collect())
+
+
+def test_distributed_stream_partitions_sources():
+    out = _run(_stream)
+    allv = sorted(out[0] + out[1])
+    assert allv == [v * 10 for v in range(40)]
+    assert set(out[0]).isdisjoint(out[1])
