@@ -1,0 +1,130 @@
+"""Embedding ops for online training: bag lookup (fwd), row-sparse gradient (bwd) and a
+sparse Adagrad update, on the HIP kernels for HBM tensors and PyTorch fp32 references on
+the host.  The backward is deterministic: gradient rows are sorted by destination on the
+GPU (``torch.sort``) and every destination row is summed by one wave in a fixed order."""
+from __future__ import annotations
+
+import torch
+
+from .kernels import _check, _hip, _stream
+
+
+def embedding_bag(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``ids`` [R, L] int32 (−1 = empty slot), ``table`` fp32 [V, D] → bf16 [R, D] (sum over L)."""
+    R, L = ids.shape
+    V, D = table.shape
+    if out is None:
+        out = torch.empty((R, D), dtype=torch.bfloat16 if table.is_cuda else torch.float32, device=table.device)
+    if table.is_cuda:
+        _check(ids, "ids", torch.int32, table.device)
+        _check(table, "table", torch.float32, table.device)
+        _check(out, "out", device=table.device)
+        _hip().embedding_bag_fwd(ids.data_ptr(), table.data_ptr(), out.data_ptr(), R, L, D, V, _stream())
+        return out
+    idx = ids.long()
+    valid = (idx >= 0) & (idx < V)
+    rows = table[idx.clamp(0, V - 1)] * valid.unsqueeze(-1)
+    out.copy_(rows.sum(1).to(out.dtype))
+    return out
+
+
+def segment_sum(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L: int = 1):
+    """Deterministic sum of ``rows[i // L]`` grouped by ``keys[i]`` (keys outside
+    ``[0, num_rows)`` dropped).  Returns ``(unique keys int32 [U], sums fp32 [U, D])``."""
+    D = rows.shape[1]
+    flat = keys.reshape(-1).long()
+    valid = (flat >= 0) & (flat < num_rows)
+    key = torch.where(valid, flat, torch.full_like(flat, num_rows))
+    sorted_ids, perm = torch.sort(key, stable=True)
+    uids, counts = torch.unique_consecutive(sorted_ids, return_counts=True)
+    if uids.numel() and uids[-1].item() == num_rows:  # drop the invalid bucket
+        uids, counts = uids[:-1], counts[:-1]
+    U = uids.numel()
+    seg = torch.zeros(U + 1, dtype=torch.int64, device=keys.device)
+    seg[1:] = torch.cumsum(counts, 0)
+    out = torch.empty((U, D), dtype=torch.float32, device=rows.device)
+    if rows.is_cuda:
+        g = rows.contiguous()
+        fp32 = g.dtype == torch.float32
+        if not fp32 and g.dtype != torch.bfloat16:
+            g = g.to(torch.bfloat16)
+        _hip().segment_sum_rows(g.data_ptr(), perm.to(torch.int32).data_ptr(), seg.to(torch.int32).data_ptr(),
+                                out.data_ptr(), U, D, L, int(fp32), _stream())
+        return uids.to(torch.int32), out
+    src = perm[: int(seg[-1])] // L
+    dst = torch.repeat_interleave(torch.arange(U), counts)
+    out.zero_()
+    out.index_add_(0, dst, rows.float()[src])
+    return uids.to(torch.int32), out
+
+
+def embedding_bag_backward(ids: torch.Tensor, grad_out: torch.Tensor, num_rows: int):
+    """Row-sparse gradient of ``embedding_bag``: returns ``(uids int32 [U], rows fp32 [U, D])``."""
+    return segment_sum(ids, grad_out, num_rows, ids.shape[1])
+
+
+def sparse_adagrad(table: torch.Tensor, accum: torch.Tensor, uids: torch.Tensor, grads: torch.Tensor, lr: float,
+                   eps: float = 1e-8) -> None:
+    U, D = grads.shape
+    if table.is_cuda:
+        _check(table, "table", torch.float32, table.device)
+        _check(accum, "accum", torch.float32, table.device)
+        _check(grads, "grads", torch.float32, table.device)
+        _check(uids, "uids", torch.int32, table.device)
+        _hip().sparse_adagrad(table.data_ptr(), accum.data_ptr(), uids.data_ptr(), grads.data_ptr(), U, D, float(lr),
+                              float(eps), _stream())
+        return
+    idx = uids.long()
+    a = accum[idx] + grads * grads
+    accum[idx] = a
+    table[idx] -= lr * grads / (a.sqrt() + eps)
+
+
+class EmbeddingBagFunction(torch.autograd.Function):
+    """Autograd node whose table gradient is delivered row-sparse to ``table_holder``
+    (dense table gradients would cost V x D per step)."""
+
+    @staticmethod
+    def forward(ctx, ids, table, anchor, holder):
+        ctx.save_for_backward(ids)
+        ctx.holder = holder
+        ctx.V = table.shape[0]
+        return embedding_bag(ids, table)
+
+    @staticmethod
+    def backward(ctx, grad):
+        (ids,) = ctx.saved_tensors
+        ctx.holder.sparse_grads.append(embedding_bag_backward(ids, grad, ctx.V))
+        return None, None, torch.zeros_like(ctx.holder.anchor), None
+
+
+class SparseEmbedding(torch.nn.Module):
+    """fp32 master table + Adagrad accumulator; bf16 lookups; row-sparse updates."""
+
+    def __init__(self, num_rows: int, dim: int, device=None, init_std: float = 0.01, seed: int = 0):
+        super().__init__()
+        g = torch.Generator().manual_seed(seed)
+        self.table = torch.nn.Parameter((torch.randn(num_rows, dim, generator=g) * init_std).to(device),
+                                        requires_grad=False)
+        self.register_buffer("accum", torch.full((num_rows, dim), 0.1, device=device))
+        # a scalar leaf that makes the lookup part of the autograd graph
+        self.anchor = torch.nn.Parameter(torch.zeros((), device=device))
+        self.sparse_grads: list = []
+
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        return EmbeddingBagFunction.apply(ids, self.table, self.anchor, self)
+
+    def apply_updates(self, lr: float, sync=None):
+        """Applies the step's sparse gradients (optionally synchronised across ranks)."""
+        if not self.sparse_grads:
+            return 0
+        uids = torch.cat([u for u, _ in self.sparse_grads])
+        rows = torch.cat([r for _, r in self.sparse_grads])
+        self.sparse_grads.clear()
+        if sync is not None:
+            uids, rows = sync(uids, rows)
+        # merge duplicate rows (several lookups, several ranks) with the deterministic
+        # segment sum so every replica applies bit-identical updates
+        uids, rows = segment_sum(uids, rows, self.table.shape[0])
+        sparse_adagrad(self.table.data, self.accum, uids.to(torch.int32).contiguous(), rows.contiguous(), lr)
+        return int(uids.numel())
