@@ -61,16 +61,20 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, act=
 
 
 class Linear(torch.nn.Module):
-    """bf16 weights [out, in] + fp32 bias, MFMA GEMM forward/backward on the GPU."""
+    """fp32 master weights [out, in] + fp32 bias; on the GPU the forward casts the weights
+    to bf16 for the MFMA GEMM (the cast's backward returns fp32 gradients), so optimizers
+    update full-precision weights."""
 
-    def __init__(self, in_features: int, out_features: int, act=None, bias: bool = True, dtype=torch.bfloat16,
+    def __init__(self, in_features: int, out_features: int, act=None, bias: bool = True, dtype=torch.float32,
                  device=None):
         super().__init__()
         w = torch.empty(out_features, in_features, dtype=torch.float32)
         torch.nn.init.kaiming_uniform_(w, a=5 ** 0.5)
-        self.weight = torch.nn.Parameter(w.to(dtype).to(device))
+        self.weight = torch.nn.Parameter(w.to(device))
         self.bias = torch.nn.Parameter(torch.zeros(out_features, dtype=torch.float32, device=device)) if bias else None
         self.act = K.act_code(act)
+        self.compute_dtype = dtype
 
     def forward(self, x):
-        return linear(x, self.weight, self.bias, self.act)
+        w = self.weight.to(torch.bfloat16) if x.is_cuda else self.weight
+        return linear(x, w, self.bias, self.act)

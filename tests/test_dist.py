@@ -107,6 +107,27 @@ def _stream(rank, world):
     return sorted(env.from_collection(list(range(40)), parallelism=2).map(lambda v: v * 10).execute_and_collect())
 
 
+def _widedeep(rank, world):
+    from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, WideDeepTrainer, synthetic_click_records
+
+    t = WideDeepTrainer(WideDeepConfig.tiny(), device="cpu", seed=rank)  # different seeds: broadcast fixes
+    t.open()
+    recs = synthetic_click_records(256, t.cfg, seed=100 + rank)  # different data per rank
+    for i in range(4):
+        t.train_step(recs[i * 64:(i + 1) * 64])
+    sd = {k: v.detach().numpy().copy() for k, v in t.model.state_dict().items()}  # plain arrays over the queue
+    t.close()
+    return sd
+
+
+def test_widedeep_dp_replicas_stay_identical():
+    out = _run(_widedeep)
+    a, b = out[0], out[1]
+    assert a.keys() == b.keys()
+    for k in a:
+        assert (a[k] == b[k]).all(), k
+
+
 def test_distributed_stream_partitions_sources():
     out = _run(_stream)
     allv = sorted(out[0] + out[1])
