@@ -46,32 +46,51 @@ __global__ __launch_bounds__(256) void embedding_bag_fwd_kernel(const int* __res
 
 // grad rows: grad_out[(b*F+f), :] (bf16 or fp32, pitch D); perm lists source rows sorted
 // by destination; seg[u]..seg[u+1] is destination u's range in perm.
-template <typename T>
+// One wave per destination row.  The wave's lanes are CW column chunks (8 elements each)
+// x RG = 64 / CW row groups: row group g sums rows s0+g, s0+g+RG, ... (many independent
+// loads in flight for hot ids), then the RG partials are combined by a fixed xor-shuffle
+// tree — the summation order depends only on the segment, so results are bit-identical
+// run to run.  D > 8 * 64 loops over 512-column blocks with RG = 1.
+template <typename T, int CW>
 __global__ __launch_bounds__(256) void segment_sum_rows_kernel(const T* __restrict__ grad, const int* __restrict__ perm,
                                                                const int* __restrict__ seg, float* __restrict__ out,
                                                                int U, int D, int L) {
+  constexpr int RG = 64 / CW;
   const int lane = threadIdx.x & 63;
   const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (u >= U) return;
   const int s0 = seg[u], s1 = seg[u + 1];
-  for (int c = lane * 8; c < D; c += 64 * 8) {
+  const int cl = lane % CW;
+  const int rg = lane / CW;
+  for (int c0 = 0; c0 < D; c0 += CW * 8) {
+    const int c = c0 + cl * 8;
+    const bool cv = c < D;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int i = s0; i < s1; ++i) {
-      const int src = perm[i] / L;  // bag element -> its (b, f) output row
-      if constexpr (sizeof(T) == 2) {
-        const bf16x8 g = *reinterpret_cast<const bf16x8*>(grad + (size_t)src * D + c);
+    if (cv) {
+      for (int i = s0 + rg; i < s1; i += RG) {
+        const int src = perm[i] / L;  // bag element -> its (b, f) output row
+        if constexpr (sizeof(T) == 2) {
+          const bf16x8 g = *reinterpret_cast<const bf16x8*>(grad + (size_t)src * D + c);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += (float)g[e];
-      } else {
-        const f32x4* gp = reinterpret_cast<const f32x4*>(grad + (size_t)src * D + c);
-        const f32x4 a = gp[0], b = gp[1];
-        acc[0] += a[0]; acc[1] += a[1]; acc[2] += a[2]; acc[3] += a[3];
-        acc[4] += b[0]; acc[5] += b[1]; acc[6] += b[2]; acc[7] += b[3];
+          for (int e = 0; e < 8; ++e) acc[e] += (float)g[e];
+        } else {
+          const f32x4* gp = reinterpret_cast<const f32x4*>(grad + (size_t)src * D + c);
+          const f32x4 a = gp[0], b = gp[1];
+          acc[0] += a[0]; acc[1] += a[1]; acc[2] += a[2]; acc[3] += a[3];
+          acc[4] += b[0]; acc[5] += b[1]; acc[6] += b[2]; acc[7] += b[3];
+        }
       }
     }
-    f32x4* dst = reinterpret_cast<f32x4*>(out + (size_t)u * D + c);
-    dst[0] = f32x4{acc[0], acc[1], acc[2], acc[3]};
-    dst[1] = f32x4{acc[4], acc[5], acc[6], acc[7]};
+#pragma unroll
+    for (int off = CW; off < 64; off <<= 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += __shfl_xor(acc[e], off, 64);
+    }
+    if (rg == 0 && cv) {
+      f32x4* dst = reinterpret_cast<f32x4*>(out + (size_t)u * D + c);
+      dst[0] = f32x4{acc[0], acc[1], acc[2], acc[3]};
+      dst[1] = f32x4{acc[4], acc[5], acc[6], acc[7]};
+    }
   }
 }
 
@@ -108,6 +127,21 @@ void embedding_bag_fwd(uintptr_t ids, uintptr_t table, uintptr_t out, int rows, 
   FTM_CHECK_LAUNCH();
 }
 
+template <typename T>
+void launch_segment_sum(const void* grad, const int* P, const int* S, float* O, int U, int D, int L, hipStream_t s) {
+  const T* g = reinterpret_cast<const T*>(grad);
+  const dim3 grid((U + 3) / 4), block(256);
+  switch (D / 8) {  // column chunks per row: pick the widest power of two that divides the work
+    case 1: hipLaunchKernelGGL((segment_sum_rows_kernel<T, 1>), grid, block, 0, s, g, P, S, O, U, D, L); break;
+    case 2: hipLaunchKernelGGL((segment_sum_rows_kernel<T, 2>), grid, block, 0, s, g, P, S, O, U, D, L); break;
+    case 4: hipLaunchKernelGGL((segment_sum_rows_kernel<T, 4>), grid, block, 0, s, g, P, S, O, U, D, L); break;
+    case 8: hipLaunchKernelGGL((segment_sum_rows_kernel<T, 8>), grid, block, 0, s, g, P, S, O, U, D, L); break;
+    case 16: hipLaunchKernelGGL((segment_sum_rows_kernel<T, 16>), grid, block, 0, s, g, P, S, O, U, D, L); break;
+    case 32: hipLaunchKernelGGL((segment_sum_rows_kernel<T, 32>), grid, block, 0, s, g, P, S, O, U, D, L); break;
+    default: hipLaunchKernelGGL((segment_sum_rows_kernel<T, 64>), grid, block, 0, s, g, P, S, O, U, D, L); break;
+  }
+}
+
 void segment_sum_rows(uintptr_t grad, uintptr_t perm, uintptr_t seg, uintptr_t out, int U, int D, int L,
                       int grad_is_fp32, uintptr_t stream) {
   if (D % 8) throw std::invalid_argument("segment_sum_rows: D % 8 != 0");
@@ -117,12 +151,8 @@ void segment_sum_rows(uintptr_t grad, uintptr_t perm, uintptr_t seg, uintptr_t o
   auto P = reinterpret_cast<const int*>(perm);
   auto S = reinterpret_cast<const int*>(seg);
   auto O = reinterpret_cast<float*>(out);
-  if (grad_is_fp32)
-    hipLaunchKernelGGL(segment_sum_rows_kernel<float>, dim3((U + 3) / 4), dim3(256), 0, s,
-                       reinterpret_cast<const float*>(grad), P, S, O, U, D, L);
-  else
-    hipLaunchKernelGGL(segment_sum_rows_kernel<bf16>, dim3((U + 3) / 4), dim3(256), 0, s,
-                       reinterpret_cast<const bf16*>(grad), P, S, O, U, D, L);
+  if (grad_is_fp32) launch_segment_sum<float>(reinterpret_cast<const void*>(grad), P, S, O, U, D, L, s);
+  else launch_segment_sum<bf16>(reinterpret_cast<const void*>(grad), P, S, O, U, D, L, s);
   FTM_CHECK_LAUNCH();
 }
 

@@ -48,8 +48,12 @@ def segment_sum(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L: int = 
         fp32 = g.dtype == torch.float32
         if not fp32 and g.dtype != torch.bfloat16:
             g = g.to(torch.bfloat16)
-        _hip().segment_sum_rows(g.data_ptr(), perm.to(torch.int32).data_ptr(), seg.to(torch.int32).data_ptr(),
-                                out.data_ptr(), U, D, L, int(fp32), _stream())
+        # keep the int32 copies referenced until the launch is enqueued: a temporary freed
+        # back to the caching allocator mid-call would let the next one reuse its block
+        perm32 = perm.to(torch.int32)
+        seg32 = seg.to(torch.int32)
+        _hip().segment_sum_rows(g.data_ptr(), perm32.data_ptr(), seg32.data_ptr(), out.data_ptr(), U, D, L, int(fp32),
+                                _stream())
         return uids.to(torch.int32), out
     src = perm[: int(seg[-1])] // L
     dst = torch.repeat_interleave(torch.arange(U), counts)
