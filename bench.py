@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "records/sec (whole node) + p50 per-record latency, ResNet-50 stream DP=1/8"
 METRIC_BERT = "records/sec (whole node) + p50 per-record latency, BERT-base text-classification stream"
+METRIC_INCEPTION = "records/sec (whole node) + p50 per-record latency, Inception-v3 fp8 image stream"
 
 
 def main():
@@ -42,14 +43,22 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="micro-batch (records per GPU per step)")
-    ap.add_argument("--image-hw", type=int, default=256, help="decoded source image size (resized to 224)")
+    ap.add_argument("--image-hw", type=int, default=None,
+                    help="decoded source image size (resnet50: 256 resized to 224; inception_v3: 299)")
     ap.add_argument("--depth", type=int, default=3, help="pipeline slots")
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
     ap.add_argument("--pool", type=int, default=512, help="distinct synthetic records cycled by the source")
-    ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert", "widedeep"],
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert", "widedeep", "inception_v3"],
                     help="resnet50 = BASELINE headline; bert = BERT-base text-classification stream; "
-                         "widedeep = Wide&Deep online training (DP gradient all-reduce)")
+                         "widedeep = Wide&Deep online training (DP gradient all-reduce); "
+                         "inception_v3 = fp8 Inception-v3 stream with bucketed dynamic batching")
     ap.add_argument("--seq-len", type=int, default=128)
+    ap.add_argument("--precision", default=None, choices=["bf16", "fp8"],
+                    help="compute precision of the compiled CNN plan (inception_v3 default fp8)")
+    ap.add_argument("--buckets", default=None,
+                    help="comma-separated extra batch buckets compiled next to --batch; with --dynamic the "
+                         "per-step batch size varies and each micro-batch runs on the smallest bucket")
+    ap.add_argument("--dynamic", action="store_true", help="variable micro-batch sizes (uniform in [B/4, B])")
     args = ap.parse_args()
 
     import torch
@@ -72,13 +81,37 @@ def main():
 
     if args.model == "widedeep":
         return run_widedeep(args, dev, rank, ws)
-    B, HW = args.batch, args.image_hw
+    B = args.batch
+    HW = args.image_hw or (299 if args.model == "inception_v3" else 256)
+    precision = args.precision or ("fp8" if args.model == "inception_v3" else "bf16")
     t0 = time.perf_counter()
-    if args.model == "resnet50":
+    plans = None
+    if args.model == "inception_v3":
+        from flink_tensorflow_amd.models.zoo.inception_v3 import inception_v3_flops_per_image, inception_v3_graph_def
+
+        graph = Graph.from_graph_def(inception_v3_graph_def(image_hw=(HW, HW), top_k=5, seed=0))
+        sizes = sorted({B} | {int(b) for b in (args.buckets or "").split(",") if b})
+        rng = np.random.default_rng(1234 + rank)
+        pool = rng.integers(0, 256, size=(args.pool, HW, HW, 3), dtype=np.uint8)
+        calib = torch.from_numpy(pool[: min(64, args.pool)])
+        plans = {}
+        for b in sizes:  # one captured plan per batch bucket; fp8 scales calibrated per plan
+            cb = {"images:0": calib[:b] if b <= calib.shape[0] else calib.repeat((b + 63) // 64, 1, 1, 1)[:b]}
+            plans[b] = CompiledFunction(graph, {"images:0": ((b, HW, HW, 3), "UINT8")}, ["top_k:0", "top_k:1"], dev,
+                                        use_graph=not args.no_graph, strict=True, precision=precision,
+                                        calibration=cb if precision == "fp8" else None)
+        plan = plans[B]
+        params = [t for p in plans.values() for t in p.params]
+        feed, rec_shape, rec_dtype = "images:0", (HW, HW, 3), torch.uint8
+        flops_per_record = inception_v3_flops_per_image(299)
+        model_name = "Inception-v3"
+        data = f"synthetic decoded uint8 {HW}x{HW}x3 images, random-init weights, fp8 scales calibrated on them"
+        seq = None
+    elif args.model == "resnet50":
         gd = resnet50_graph_def(image_hw=(HW, HW), top_k=5, seed=0)
         graph = Graph.from_graph_def(gd)
         plan = CompiledFunction(graph, {"images:0": ((B, HW, HW, 3), "UINT8")}, ["top_k:0", "top_k:1"], dev,
-                                use_graph=not args.no_graph, strict=True)
+                                use_graph=not args.no_graph, strict=True, precision=precision)
         params = plan.params
         feed, rec_shape, rec_dtype = "images:0", (HW, HW, 3), torch.uint8
         flops_per_record = resnet50_flops_per_image(224)
@@ -110,19 +143,24 @@ def main():
     compile_s = time.perf_counter() - t0
 
     records = [pool[i] for i in range(args.pool)]
-    runner = PipelinedGpuRunner({B: plan}, feed, lambda p: p.output_tensors(), rec_shape, rec_dtype,
+    runner = PipelinedGpuRunner(plans or {B: plan}, feed, lambda p: p.output_tensors(), rec_shape, rec_dtype,
                                 depth=args.depth, device=dev)
 
     cursor = 0
     lat = []
     n_done = 0
+    n_sub = 0
+    size_rng = np.random.default_rng(99)
 
     def step(collect):
-        nonlocal cursor, n_done
-        batch = [records[(cursor + i) % args.pool] for i in range(B)]
-        cursor += B
+        nonlocal cursor, n_done, n_sub
+        n = int(size_rng.integers(max(1, B // 4), B + 1)) if args.dynamic else B
+        batch = [records[(cursor + i) % args.pool] for i in range(n)]
+        cursor += n
+        if collect:
+            n_sub += n
         now = time.perf_counter()
-        ts = np.full(B, now)
+        ts = np.full(n, now)
         for r in runner.poll() + runner.submit(batch, ts):
             n_done += r.n
             if collect:
@@ -150,12 +188,13 @@ def main():
     p50 = float(np.percentile(lat_all, 50) * 1e3)
     p99 = float(np.percentile(lat_all, 99) * 1e3)
     p50s = comm.all_gather_object(p50)
-    per_gpu = B * args.steps / elapsed
-    total = ws * B * args.steps / elapsed_max
+    n_rec = n_sub if args.dynamic else B * args.steps
+    per_gpu = n_rec / elapsed
+    total = comm.all_reduce_scalar(float(n_rec), "sum", device=dev) / elapsed_max
     flops = flops_per_record * total
     if rank == 0:
         out = {
-            "metric": METRIC if args.model == "resnet50" else METRIC_BERT,
+            "metric": {"resnet50": METRIC, "bert": METRIC_BERT, "inception_v3": METRIC_INCEPTION}[args.model],
             "value": round(total, 1),
             "unit": "records/s",
             "n_gpus": ws,
@@ -165,11 +204,12 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp8 (e4m3 weights+activations, fp32 accumulate)" if precision == "fp8" else "bf16",
             "data": data,
             "config": {"model": model_name, "global_batch": B * ws, "seq_len": seq,
                        "parallelism": f"dp{ws}", "micro_batch_per_gpu": B,
-                       "input_hw": 224 if seq is None else None},
+                       "input_hw": (299 if args.model == "inception_v3" else 224) if seq is None else None,
+                       "batch_buckets": sorted(plans) if plans else [B], "dynamic_batching": args.dynamic},
             "p50_latency_ms": round(float(np.median(p50s)), 3),
             "p99_latency_ms": round(p99, 3),
             "per_gpu_records_per_s": round(per_gpu, 1),

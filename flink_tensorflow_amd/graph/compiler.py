@@ -24,6 +24,14 @@ This is the MI355X replacement of libtensorflow's session executor for the hot p
 5. **capture**: one hipGraph per (signature, batch size).
 
 Activations are bf16 NHWC on device; fetched outputs are cast back to the graph dtype.
+
+``precision="fp8"`` (BASELINE "Inception-v3 fp8 weights"): a bf16 twin of the plan is
+first run on calibration inputs to record every activation's absolute maximum; then each
+Conv2D chain whose channels are multiples of 16 (and has no residual) is lowered onto the
+fp8 MFMA kernel with per-channel e4m3 weights, and its output is stored as e4m3 with a
+static per-tensor scale whenever every consumer reads fp8 (convs, pools, concats,
+global-average-pool).  Concat branches write with the concat buffer's scale; max/avg
+pools requantise on the fly; anything else reads a dequantised bf16 copy.
 """
 from __future__ import annotations
 
@@ -34,6 +42,7 @@ from typing import Any, Callable
 import numpy as np
 import torch
 
+from ..ops import fp8 as F8
 from ..ops import kernels as K
 from ..types.dtypes import DataType
 from ..types.names import TensorName
@@ -64,6 +73,7 @@ class Val:
     alias_of: "Val | None" = None
     last_use: int = -1
     concat_slot: tuple | None = None  # (target Val, channel offset) for concat-by-stride-write
+    qscale: float | None = None  # fp8 e4m3 storage (uint8 buffer) with this per-tensor scale
 
     @property
     def is_const(self):
@@ -90,8 +100,11 @@ class _ConstSession:
 class CompiledFunction:
     def __init__(self, graph: Graph, feeds: dict[str, tuple[tuple, Any]], fetches: list[str], device,
                  variables: dict | None = None, use_graph: bool = True, strict: bool = False,
-                 topk_fetch: bool = True):
+                 topk_fetch: bool = True, precision: str = "bf16", calibration: dict | None = None):
+        if precision not in ("bf16", "fp8"):
+            raise ValueError(f"precision must be bf16 or fp8, not {precision!r}")
         self.graph = graph
+        self.precision = precision
         self.device = torch.device(device)
         if self.device.type != "cuda":
             use_graph = False  # host plans run the fp32 reference ops (used by CPU tests)
@@ -110,7 +123,14 @@ class CompiledFunction:
         self._input_bufs: dict[str, torch.Tensor] = {}
         self._outputs: list = []
         self._graph_obj: torch.cuda.CUDAGraph | None = None
+        self._amax: dict[str, float] = {}
+        self.fp8_layers = 0
         import contextlib
+
+        if precision == "fp8":  # calibrate activation ranges on a bf16 twin of the plan
+            twin = CompiledFunction(graph, feeds, fetches, device, variables, use_graph=False, strict=strict)
+            self._amax = twin.calibrate(calibration)
+            del twin
 
         with torch.cuda.device(self.device) if self.device.type == "cuda" else contextlib.nullcontext():
             self._compile()
@@ -186,6 +206,53 @@ class CompiledFunction:
             tn = TensorName.parse(f)
             if (tn.name, tn.index) not in self.vals:
                 raise CompileError(f"fetch {f} was not produced by the plan")
+
+    # ------------------------------------------------------------------ calibration
+    def synthetic_feeds(self, seed: int = 0) -> dict:
+        g = torch.Generator().manual_seed(seed)
+        out = {}
+        for f in self.feed_names:
+            shape, dt = self.feed_specs[f]
+            dt = DataType.of(dt).torch
+            if dt == torch.uint8:
+                out[f] = torch.randint(0, 256, tuple(shape), generator=g, dtype=torch.uint8)
+            elif dt.is_floating_point:
+                out[f] = torch.randn(tuple(shape), generator=g).to(dt)
+            else:
+                out[f] = torch.randint(0, 100, tuple(shape), generator=g).to(dt)
+        return out
+
+    @torch.no_grad()
+    def calibrate(self, feeds: dict | None = None) -> dict[str, float]:
+        """Runs the plan step by step on ``feeds`` (synthetic when None) and returns the
+        absolute maximum of every computed value, keyed by graph node name."""
+        for k, v in (feeds or self.synthetic_feeds()).items():
+            self.input_buffer(k).copy_(v)
+        by_id: dict[int, float] = {}
+        for s in self.steps:
+            s.fn()
+            for o in s.outputs:
+                t = _view(o)
+                if t.is_floating_point() and t.numel():
+                    by_id[id(_root(o))] = float(t.float().abs().max())
+        for v in self.vals.values():  # concat targets: max over their stride-written children
+            kids = getattr(v, "_concat_children", None)
+            if kids:
+                by_id[id(v)] = max(by_id.get(id(_root(c)), 0.0) for c in kids)
+        return {n: by_id[id(_root(v))] for (n, _), v in self.vals.items() if id(_root(v)) in by_id}
+
+    def _qscale(self, name: str) -> float | None:
+        a = self._amax.get(name)
+        return None if a is None else F8.scale_for(a)
+
+    def _fp8_consumers_ok(self, name: str) -> bool:
+        """True when ``name``'s value may be stored as fp8: not fetched, and every consumer
+        reads fp8 natively."""
+        if any(TensorName.parse(f).name == name for f in self.fetch_names):
+            return False
+        cons = self.cons.get(name, [])
+        return bool(cons) and all(self.graph[c].op in ("Conv2D", "MaxPool", "AvgPool", "ConcatV2", "Mean")
+                                  for c in cons)
 
     # ------------------------------------------------------------------ helpers
     def _in(self, node: Node, i: int) -> Val:
@@ -386,6 +453,9 @@ class CompiledFunction:
             w = w * scale  # fold BN into the output channels
         Ho = (H + pt + pb - ((KH - 1) * dh + 1)) // sh + 1
         Wo = (W + pl + pr - ((KW - 1) * dw + 1)) // sw + 1
+        if self.precision == "fp8" and self._conv_fp8_ok(node, x, Cin, Cout, residual, act):
+            return self._lower_conv_fp8(node, x, w, bias, act, last, absorbed, (KH, KW, Cin, Cout),
+                                        (sh, sw), (pt, pb, pl, pr), (dh, dw), (N, Ho, Wo))
         if self._s2d_ok(x, node, C, sh, sw, dh, dw, pt, pl, H, W):
             # stride-2 RGB stem over the space-to-depth preprocess output (K 392 -> 256)
             w_ohwi, (pt, pb, pl, pr) = K.s2d_stem_weights(w, H, W, (pt, pb, pl, pr))
@@ -423,6 +493,40 @@ class CompiledFunction:
         self.vals[(last.name, 0)] = out
         self._alias_fused_outputs(absorbed, out)
 
+    def _conv_fp8_ok(self, node: Node, x: Val, Cin, Cout, residual, act) -> bool:
+        if residual is not None or act not in (K.ACT_NONE, K.ACT_RELU) or Cin % 16 or Cout % 16 or x.phys_c:
+            return False
+        if x.qscale is not None:
+            return True
+        return x.dtype == torch.bfloat16 and self._qscale(node.inputs[0][0]) is not None
+
+    def _lower_conv_fp8(self, node, x, w, bias, act, last, absorbed, kdims, stride, pads, dil, out_nhw):
+        KH, KW, Cin, Cout = kdims
+        w_ohwi = w.permute(3, 0, 1, 2).contiguous()
+        wq, ws = F8.quantize_weight(w_ohwi)
+        x_scale = x.qscale if x.qscale is not None else self._qscale(node.inputs[0][0])
+        dev = self.device
+        wq_dev = wq.to(dev)
+        ws_dev = ws.to(dev)
+        cs_dev = (ws * x_scale).to(dev, torch.float32).contiguous()
+        b_dev = bias.to(dev, torch.float32).contiguous() if bias is not None else \
+            torch.zeros(Cout, dtype=torch.float32, device=dev)
+        self.params += [wq_dev, cs_dev, b_dev]
+        o_scale = self._qscale(last.name) if self._fp8_consumers_ok(last.name) else None
+        out = self._new((*out_nhw, Cout), torch.uint8 if o_scale is not None else torch.bfloat16)
+        out.qscale = o_scale
+        for a in absorbed:
+            self._fused.add(a.name)
+        self.fp8_layers += 1
+
+        def run(x=x, out=out, wq=wq_dev, ws=ws_dev, cs=cs_dev, b=b_dev, x_scale=x_scale):
+            F8.conv2d_nhwc_fp8(_view(x), x_scale, wq, (KH, KW), ws, b, stride, pads, dil, act,
+                               out_scale=_eff_scale(out), out=_target(out), out_channel_offset=_coff(out), chan_scale=cs)
+
+        self._emit(node.name, "conv_fp8", run, [x], [out])
+        self.vals[(last.name, 0)] = out
+        self._alias_fused_outputs(absorbed, out)
+
     def _s2d_ok(self, x: Val, node: Node, C, sh, sw, dh, dw, pt, pl, H, W) -> bool:
         cfg = getattr(x, "pre_cfg", None)
         if cfg is None or C != 3 or (sh, sw) != (2, 2) or (dh, dw) != (1, 1) or pt % 2 or pl % 2 or H % 2 or W % 2:
@@ -441,6 +545,8 @@ class CompiledFunction:
             self.vals[(a.name, 0)] = out
 
     def _ensure_padded(self, x: Val, cin_pad: int, name: str) -> Val:
+        if x.qscale is not None:
+            x = self._as_bf16(x, name)
         phys = x.phys_c or x.shape[-1]
         if phys == cin_pad and x.dtype == torch.bfloat16:
             return x
@@ -463,15 +569,23 @@ class CompiledFunction:
         wt = b.const.float()
         w_nk = wt if node.attr("transpose_b", False) else wt.t()
         N, Kd = w_nk.shape
-        if Kd % 8 or N % 8:
+        if Kd % 8:
             return self._lower_glue(node)
         last, scale, bias, residual, act, absorbed = self._conv_chain(node)
         if scale is not None:
             w_nk = w_nk * scale[:, None]
+        n_pad = -(-N // 8) * 8  # e.g. 1001 classes: zero rows, output rows strided by n_pad
+        if n_pad != N and residual is not None:
+            return self._lower_glue(node)
+        if n_pad != N:
+            w_nk = torch.nn.functional.pad(w_nk, (0, 0, 0, n_pad - N))
+            bias = torch.nn.functional.pad(bias if bias is not None else torch.zeros(N), (0, n_pad - N))
         w_dev = w_nk.to(self.device, torch.bfloat16).contiguous()
         b_dev = bias.to(self.device, torch.float32).contiguous() if bias is not None else None
         self.params += [w_dev] + ([b_dev] if b_dev is not None else [])
-        out = self._new((a.shape[0], N))
+        out = self._new((a.shape[0], N), phys_c=n_pad if n_pad != N else None)
+        if n_pad != N:
+            out.buf_shape = (a.shape[0], n_pad)
         res_val = self.vals[residual[0].inputs[residual[1]]] if residual is not None else None
         xin = self._as_bf16(a, node.name)
         for n in absorbed:
@@ -488,6 +602,12 @@ class CompiledFunction:
         if v.dtype == torch.bfloat16:
             return v
         y = self._new(v.shape)
+        if v.qscale is not None:
+            def deq(v=v, y=y):
+                F8.dequantize(_view(v), _eff_scale(v), out=y.buf)
+
+            self._emit(name + "/dequant", "dequant", deq, [v], [y])
+            return y
 
         def run(v=v, y=y):
             y.buf.copy_(v.buf)
@@ -567,8 +687,21 @@ class CompiledFunction:
             pt = pb = pl = pr = 0
         Ho = (H + pt + pb - kh) // sh + 1
         Wo = (W + pl + pr - kw) // sw + 1
-        out = self._new((N, Ho, Wo, C))
         mode = "max" if node.op == "MaxPool" else "avg"
+        if x.qscale is not None and C % 16 == 0:
+            # pooled values stay within the input range: keep the input scale, requantise
+            # only when written into a concat buffer of another scale
+            out = self._new((N, Ho, Wo, C), torch.uint8)
+            out.qscale = x.qscale
+
+            def run8(x=x, out=out):
+                F8.pool2d_nhwc_fp8(_view(x), (kh, kw), (sh, sw), (pt, pb, pl, pr), mode,
+                                   rq=x.qscale / _eff_scale(out), out=_target(out), out_channel_offset=_coff(out))
+
+            self._emit(node.name, "pool_fp8", run8, [x], [out])
+            self.vals[(node.name, 0)] = out
+            return
+        out = self._new((N, Ho, Wo, C))
         xin = self._as_bf16(x, node.name)
 
         def run(xin=xin, out=out):
@@ -589,6 +722,13 @@ class CompiledFunction:
         keep = node.attr("keep_dims", False)
         N, H, W, C = x.shape
         out = self._new((N, 1, 1, C) if keep else (N, C))
+        if x.qscale is not None and C % 16 == 0:
+            def run8(x=x, out=out):
+                F8.global_avgpool_fp8(_view(x), _eff_scale(x), out=out.buf.view(N, C))
+
+            self._emit(node.name, "gap_fp8", run8, [x], [out])
+            self.vals[(node.name, 0)] = out
+            return True
         xin = self._as_bf16(x, node.name)
 
         def run(xin=xin, out=out):
@@ -617,7 +757,7 @@ class CompiledFunction:
         idxs = self._new((R, k), torch.int32)
 
         def run(xin=xin, probs=probs, vals=vals, idxs=idxs):
-            K.softmax_topk(xin.buf, k, want_probs=True, vals=vals.buf, idxs=idxs.buf, probs=probs.buf)
+            K.softmax_topk(_view(xin), k, want_probs=True, vals=vals.buf, idxs=idxs.buf, probs=probs.buf)
 
         self._emit(node.name, "softmax_topk", run, [xin], [probs, vals, idxs])
         self.vals[(node.name, 0)] = probs
@@ -648,7 +788,10 @@ class CompiledFunction:
         axis = int(av.const.item()) % len(ins[0].shape)
         shape = list(ins[0].shape)
         shape[axis] = sum(v.shape[axis] for v in ins)
-        out = self._new(tuple(shape), ins[0].dtype)
+        fp8 = all(v.qscale is not None for v in ins) and self._qscale(node.name) is not None
+        out = self._new(tuple(shape), torch.uint8 if fp8 else torch.bfloat16)
+        if fp8:
+            out.qscale = self._qscale(node.name)
         stride_write = (axis == len(shape) - 1 and len(shape) == 4
                         and all(self._concat_writable(v, node.inputs[i][0], node.name) for i, v in enumerate(ins)))
         if stride_write:
@@ -659,6 +802,9 @@ class CompiledFunction:
             self.vals[(node.name, 0)] = out
             out._concat_children = ins
             return
+        if fp8 or any(v.qscale is not None for v in ins):  # mixed scales: concatenate in bf16
+            out = self._new(tuple(shape))
+            ins = [self._as_bf16(v, f"{node.name}/in{i}") for i, v in enumerate(ins)]
 
         def run(ins=ins, out=out, axis=axis):
             torch.cat([v.buf for v in ins], dim=axis, out=out.buf)
@@ -670,16 +816,18 @@ class CompiledFunction:
         # produced by exactly one conv/pool step (which can write at a channel offset),
         # consumed by nothing but this concat, and not fetched
         prods = [s for s in self.steps if any(o is v for o in s.outputs)]
-        if len(prods) != 1 or prods[0].kind not in ("conv", "pool") or v.concat_slot is not None:
+        if len(prods) != 1 or prods[0].kind not in ("conv", "pool", "conv_fp8", "pool_fp8") or v.concat_slot is not None:
             return False
         if v.alias_of is not None or v.phys_c:
             return False
         # every graph node that maps to this value must feed only the concat
         for (n, _), val in self.vals.items():
-            if val is v and any(c != concat_node for c in self.cons.get(n, [])):
+            if val is v and any(c != concat_node and c not in self._fused for c in self.cons.get(n, [])):
                 return False
             if val is v and any(TensorName.parse(f).name == n for f in self.fetch_names):
                 return False
+        if v.qscale is not None:
+            return v.shape[-1] % 16 == 0 and src_node in self.cons
         return v.shape[-1] % 8 == 0 and v.dtype == torch.bfloat16 and src_node in self.cons
 
     def _lower_glue(self, node: Node):
@@ -813,7 +961,9 @@ class CompiledFunction:
         for o in self._outputs:
             if isinstance(o, Val):
                 b = _view(o)
-                if cast_outputs and b.dtype == torch.bfloat16:
+                if o.qscale is not None:
+                    b = F8.from_fp8_bytes(b) * _eff_scale(o)
+                elif cast_outputs and b.dtype == torch.bfloat16:
                     b = b.float()
                 elif copy_outputs:
                     b = b.clone()
@@ -834,7 +984,8 @@ class CompiledFunction:
         for s in self.steps:
             kinds[s.kind] = kinds.get(s.kind, 0) + 1
         return {"steps": len(self.steps), "kinds": kinds, "glue_ops": sorted(set(self.glue_ops)),
-                "hip_graph": self._graph_obj is not None}
+                "hip_graph": self._graph_obj is not None, "precision": self.precision,
+                "fp8_layers": self.fp8_layers}
 
 
 def _root(v: Val) -> Val:
@@ -850,7 +1001,9 @@ def _view(v: Val) -> torch.Tensor:
         return tgt.buf[..., off:off + r.shape[-1]]
     b = r.buf
     if r.phys_c and b.shape[-1] != r.shape[-1] and v is r:
-        return b
+        if tuple(b.shape[:-1]) == tuple(r.shape[:-1]):
+            return b[..., :r.shape[-1]]  # channel-padded buffer: the logical columns
+        return b  # space-to-depth packed stem input
     if v is not r:
         return b.reshape(v.shape)
     return b
@@ -861,6 +1014,14 @@ def _target(v: Val) -> torch.Tensor:
     if r.concat_slot is not None:
         return r.concat_slot[0].buf
     return r.buf
+
+
+def _eff_scale(v: Val) -> float | None:
+    """Storage scale of an fp8 value: a concat branch is stored with its buffer's scale."""
+    r = _root(v)
+    if r.concat_slot is not None and r.concat_slot[0].qscale is not None:
+        return r.concat_slot[0].qscale
+    return r.qscale
 
 
 def _coff(v: Val) -> int:
@@ -875,6 +1036,7 @@ def _host(t):
 
 
 def compile_signature(session, feeds: dict[str, tuple[tuple, Any]], fetches: list[str], use_graph=True,
-                      strict=False) -> CompiledFunction:
+                      strict=False, precision: str = "bf16", calibration: dict | None = None) -> CompiledFunction:
     """Compiles ``session``'s graph for the given feed shapes on the session's GPU."""
-    return CompiledFunction(session.graph, feeds, fetches, session.device, session.variables, use_graph, strict)
+    return CompiledFunction(session.graph, feeds, fetches, session.device, session.variables, use_graph, strict,
+                            precision=precision, calibration=calibration)

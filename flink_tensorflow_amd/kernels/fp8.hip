@@ -1,6 +1,563 @@
-// OCP FP8 (e4m3fn) kernels: placeholder TU, filled in with the fp8 implicit GEMM.
+// OCP FP8 (e4m3fn) inference path for CDNA4 (BASELINE config "Inception-v3 fp8 weights").
+//
+// Quantisation scheme (static, calibrated by the graph compiler):
+//   weights      per-output-channel scale  w = wq * sw[c]            (wq e4m3, |wq| <= 448)
+//   activations  per-tensor scale          x = xq * sx               (one scale per buffer;
+//                the branches of a concat share the concat buffer's scale)
+//   conv/GEMM    acc = sum_k wq * xq (fp32, v_mfma_scale_f32_16x16x128_f8f6f4, unit E8M0
+//                block scales), then y = act(acc * (sw[c] * sx) + bias[c]) and either
+//                yq = sat(y / sy) written as fp8 (the next layer's input) or bf16.
+//
+// The implicit GEMM follows the bf16 kernel (igemm_bf16.hip) with the K stage widened to
+// 128 one-byte elements: an LDS row is still 128 B = 8 chunks of 16 B with the
+// chunk ^ (row & 7) swizzle, and one 16x16x128 MFMA per fragment pair consumes a whole
+// stage (2x the K per instruction of bf16 at the same LDS traffic per byte).  The A
+// (weights) and B (pixels) fragments are read with the SAME (lane group, byte) -> k
+// assignment, so the product is independent of the instruction's internal K order.
+// A layer whose producer writes bf16 (the stem) is quantised on load (IN_BF16).
+//
+// Also here: quantise / dequantise, max/avg pooling on fp8 with requantisation (pool
+// branches write straight into concat buffers of another scale), and global average
+// pooling fp8 -> bf16 (classifier input).
 #include <pybind11/pybind11.h>
+
+#include <stdexcept>
+#include <string>
 
 #include "common.h"
 
-void register_fp8(pybind11::module_& m) {}
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+namespace {
+
+constexpr int BK = 128;  // K (bytes) per stage
+constexpr int NT = 256;
+constexpr float FP8_MAX = 448.f;
+constexpr int E8M0_ONE = 127;  // unit block scale
+
+FTM_DEVICE float sat(float v) { return fminf(fmaxf(v, -FP8_MAX), FP8_MAX); }
+
+// 4 floats -> 4 e4m3 bytes (RNE, saturated first: the converter does not clamp)
+FTM_DEVICE uint32_t pack4(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(a), sat(b), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(c), sat(d), w, true);
+  return (uint32_t)w;
+}
+
+FTM_DEVICE void unpack4(uint32_t w, float* o) {
+  o[0] = __builtin_amdgcn_cvt_f32_fp8((int)w, 0);
+  o[1] = __builtin_amdgcn_cvt_f32_fp8((int)w, 1);
+  o[2] = __builtin_amdgcn_cvt_f32_fp8((int)w, 2);
+  o[3] = __builtin_amdgcn_cvt_f32_fp8((int)w, 3);
+}
+
+// 16 bf16 (two 16-B vectors) * q -> 16 fp8 (one 16-B vector)
+FTM_DEVICE u32x4 quant16(u32x4 lo, u32x4 hi, float q) {
+  bf16x8 a = __builtin_bit_cast(bf16x8, lo), b = __builtin_bit_cast(bf16x8, hi);
+  u32x4 r;
+  r[0] = pack4((float)a[0] * q, (float)a[1] * q, (float)a[2] * q, (float)a[3] * q);
+  r[1] = pack4((float)a[4] * q, (float)a[5] * q, (float)a[6] * q, (float)a[7] * q);
+  r[2] = pack4((float)b[0] * q, (float)b[1] * q, (float)b[2] * q, (float)b[3] * q);
+  r[3] = pack4((float)b[4] * q, (float)b[5] * q, (float)b[6] * q, (float)b[7] * q);
+  return r;
+}
+
+struct Fp8Params {
+  const uint8_t* x;    // fp8 activations (bf16 when IN_BF16)
+  const uint8_t* w;    // fp8 weights [Cout][K]
+  const float* scale;  // per output channel: sw[c] * sx
+  const float* bias;   // per output channel (zeros when absent)
+  uint8_t* y;          // fp8 or bf16 output (OUT_FP8)
+  float in_q;          // IN_BF16: 1 / sx
+  float out_q;         // OUT_FP8: 1 / sy
+  int N, H, W, Cin, Ho, Wo, Cout, KH, KW, sh, sw, ph, pw, dh, dw;
+  int M, K;
+  int ldx;          // GEMM mode: row stride of X in elements
+  int ldy, y_coff;  // output pixel stride / channel offset (elements)
+  int tiles_m, tiles_n;
+};
+
+FTM_DEVICE int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 4); }
+
+template <int BM, int BN, bool CONV, bool IN_BF16, bool OUT_FP8, int ACT>
+__global__ __launch_bounds__(NT, 2) void igemm_fp8_kernel(Fp8Params p) {
+  constexpr int WAVES_N = BN / 64;
+  constexpr int WAVES_M = 4 / WAVES_N;
+  constexpr int TM = BM / WAVES_M;
+  constexpr int J = TM / 16;
+  constexpr int XR = BM / 32;
+  constexpr int WR = BN / 32;
+  constexpr int OB = OUT_FP8 ? 1 : 2;            // output bytes per element
+  constexpr int OLD = BN * OB + 16;              // epilogue LDS row pitch (bytes)
+  constexpr int STAGE_BYTES = (BM + BN) * BK;
+  constexpr int EPI_BYTES = BM * OLD;
+  constexpr int LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
+  uint8_t* Xs = smem;
+  uint8_t* Ws = smem + BM * BK;
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int tm = tile / p.tiles_n;
+  const int tn = tile % p.tiles_n;
+  const int m0 = tm * BM;
+  const int n0 = tn * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wp = wave % WAVES_M;
+  const int wc = wave / WAVES_M;
+
+  const int kc = tid & 7;   // 16-byte k chunk staged by this thread
+  const int r0 = tid >> 3;  // rows r0 + 32 i
+
+  int xbase[XR], hb[XR], wb[XR];
+  bool mvalid[XR];
+#pragma unroll
+  for (int i = 0; i < XR; ++i) {
+    int m = m0 + r0 + 32 * i;
+    mvalid[i] = m < p.M;
+    int mm = mvalid[i] ? m : 0;
+    if constexpr (CONV) {
+      int wo = mm % p.Wo;
+      int t = mm / p.Wo;
+      int ho = t % p.Ho;
+      int n = t / p.Ho;
+      xbase[i] = n * p.H * p.W * p.Cin;
+      hb[i] = ho * p.sh - p.ph;
+      wb[i] = wo * p.sw - p.pw;
+    } else {
+      xbase[i] = mm * p.ldx;
+      hb[i] = 0;
+      wb[i] = 0;
+    }
+  }
+  const uint8_t* wrow[WR];
+  bool nvalid[WR];
+#pragma unroll
+  for (int i = 0; i < WR; ++i) {
+    int co = n0 + r0 + 32 * i;
+    nvalid[i] = co < p.Cout;
+    wrow[i] = p.w + (size_t)(nvalid[i] ? co : 0) * p.K;
+  }
+
+  constexpr int XV = IN_BF16 ? 2 : 1;  // 16-B global loads per staged chunk
+  u32x4 xr[XR][XV], wr[WR];
+  const u32x4 zero4 = {0u, 0u, 0u, 0u};
+
+  auto load_tile = [&](int k0) {
+    const int k = k0 + kc * 16;
+    const bool kvalid = k < p.K;
+    size_t off[XR];
+    bool ok[XR];
+    if constexpr (CONV) {
+      int kidx = k / p.Cin;
+      int ci = k - kidx * p.Cin;
+      int kh = kidx / p.KW;
+      int kw = kidx - kh * p.KW;
+#pragma unroll
+      for (int i = 0; i < XR; ++i) {
+        int hi = hb[i] + kh * p.dh;
+        int wi = wb[i] + kw * p.dw;
+        ok[i] = kvalid && mvalid[i] && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
+        off[i] = (size_t)xbase[i] + ((size_t)hi * p.W + wi) * p.Cin + ci;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < XR; ++i) {
+        ok[i] = kvalid && mvalid[i];
+        off[i] = (size_t)xbase[i] + k;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      if constexpr (IN_BF16) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16*>(p.x) + off[i]);
+        xr[i][0] = ok[i] ? src[0] : zero4;
+        xr[i][1] = ok[i] ? src[1] : zero4;
+      } else {
+        xr[i][0] = ok[i] ? *reinterpret_cast<const u32x4*>(p.x + off[i]) : zero4;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < WR; ++i) {
+      bool okw = kvalid && nvalid[i];
+      wr[i] = okw ? *reinterpret_cast<const u32x4*>(wrow[i] + k) : zero4;
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      u32x4 v;
+      if constexpr (IN_BF16) v = quant16(xr[i][0], xr[i][1], p.in_q);
+      else v = xr[i][0];
+      *reinterpret_cast<u32x4*>(Xs + swz(r0 + 32 * i, kc)) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < WR; ++i) *reinterpret_cast<u32x4*>(Ws + swz(r0 + 32 * i, kc)) = wr[i];
+  };
+
+  f32x4 acc[4][J];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BK - 1) / BK;
+  load_tile(0);
+  store_tile();
+  __syncthreads();
+
+  const int frow = lane & 15;
+  const int c0 = 2 * (lane >> 4);  // this lane group's two 16-B chunks of the 128-deep stage
+
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) load_tile((kt + 1) * BK);
+    i32x8 a[4], b[J];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wc * 64 + i * 16 + frow;
+      u32x4 lo = *reinterpret_cast<const u32x4*>(Ws + swz(row, c0));
+      u32x4 hi = *reinterpret_cast<const u32x4*>(Ws + swz(row, c0 + 1));
+      a[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int row = wp * TM + j * 16 + frow;
+      u32x4 lo = *reinterpret_cast<const u32x4*>(Xs + swz(row, c0));
+      u32x4 hi = *reinterpret_cast<const u32x4*>(Xs + swz(row, c0 + 1));
+      b[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < J; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, E8M0_ONE, 0,
+                                                                     E8M0_ONE);
+    if (kt + 1 < nk) {
+      __syncthreads();  // single LDS stage: everyone is done reading it
+      store_tile();
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue phase 1: dequant + bias + act (+ requant) -> LDS tile [BM][OLD bytes]
+  uint8_t* Os = smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int cl = wc * 64 + i * 16 + (lane >> 4) * 4;
+    f32x4 sv = {0.f, 0.f, 0.f, 0.f}, bv = {0.f, 0.f, 0.f, 0.f};
+    if (n0 + cl < p.Cout) {
+      sv = *reinterpret_cast<const f32x4*>(p.scale + n0 + cl);
+      bv = *reinterpret_cast<const f32x4*>(p.bias + n0 + cl);
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int pl = wp * TM + j * 16 + (lane & 15);
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act<ACT>(acc[i][j][r] * sv[r] + bv[r]);
+      if constexpr (OUT_FP8) {
+        *reinterpret_cast<uint32_t*>(Os + pl * OLD + cl) =
+            pack4(v[0] * p.out_q, v[1] * p.out_q, v[2] * p.out_q, v[3] * p.out_q);
+      } else {
+        bf16x4 o;
+        o[0] = f2bf(v[0]); o[1] = f2bf(v[1]); o[2] = f2bf(v[2]); o[3] = f2bf(v[3]);
+        *reinterpret_cast<bf16x4*>(Os + pl * OLD + cl * 2) = o;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue phase 2: coalesced 16-B row segments
+  constexpr int EPC = 16 / OB;   // elements per 16-B chunk
+  constexpr int CPR = BN / EPC;  // chunks per tile row
+#pragma unroll
+  for (int q = tid; q < BM * CPR; q += NT) {
+    const int pl = q / CPR;
+    const int cc = q % CPR;
+    const int m = m0 + pl;
+    const int c = n0 + cc * EPC;
+    if (m >= p.M || c >= p.Cout) continue;
+    u32x4 v = *reinterpret_cast<const u32x4*>(Os + pl * OLD + cc * 16);
+    *reinterpret_cast<u32x4*>(p.y + ((size_t)m * p.ldy + p.y_coff + c) * OB) = v;
+  }
+}
+
+template <int BM, int BN, bool CONV, bool IN_BF16, bool OUT_FP8>
+void launch_cfg(const Fp8Params& p0, int act, hipStream_t s) {
+  Fp8Params p = p0;
+  p.tiles_m = (p.M + BM - 1) / BM;
+  p.tiles_n = (p.Cout + BN - 1) / BN;
+  dim3 grid(p.tiles_m * p.tiles_n), block(NT);
+  switch (act) {
+    case ACT_NONE: hipLaunchKernelGGL((igemm_fp8_kernel<BM, BN, CONV, IN_BF16, OUT_FP8, ACT_NONE>), grid, block, 0, s, p); break;
+    case ACT_RELU: hipLaunchKernelGGL((igemm_fp8_kernel<BM, BN, CONV, IN_BF16, OUT_FP8, ACT_RELU>), grid, block, 0, s, p); break;
+    default: throw std::invalid_argument("fp8 igemm: activation must be none/relu");
+  }
+}
+
+// Tile configurations: 0 = 128x128, 1 = 256x64 (Cout <= 64), 2 = 128x64.
+constexpr int NCFG = 3;
+
+template <bool CONV, bool IN_BF16, bool OUT_FP8>
+void launch_tile(const Fp8Params& p, int act, int cfg, hipStream_t s) {
+  if (cfg < 0) cfg = p.Cout <= 64 ? (IN_BF16 ? 2 : 1) : 0;  // 256x64 + bf16 staging spills
+  switch (cfg) {
+    case 0: launch_cfg<128, 128, CONV, IN_BF16, OUT_FP8>(p, act, s); break;
+    case 1: launch_cfg<256, 64, CONV, IN_BF16, OUT_FP8>(p, act, s); break;
+    case 2: launch_cfg<128, 64, CONV, IN_BF16, OUT_FP8>(p, act, s); break;
+    default: throw std::invalid_argument("unknown fp8 igemm config " + std::to_string(cfg));
+  }
+}
+
+template <bool CONV>
+void launch_io(const Fp8Params& p, bool in_bf16, bool out_fp8, int act, int cfg, hipStream_t s) {
+  if (in_bf16) {
+    if (out_fp8) launch_tile<CONV, true, true>(p, act, cfg, s);
+    else launch_tile<CONV, true, false>(p, act, cfg, s);
+  } else {
+    if (out_fp8) launch_tile<CONV, false, true>(p, act, cfg, s);
+    else launch_tile<CONV, false, false>(p, act, cfg, s);
+  }
+  FTM_CHECK_LAUNCH();
+}
+
+void check_align(uintptr_t ptr, int bytes, const char* what) {
+  if (ptr % bytes) throw std::invalid_argument(std::string(what) + " is not " + std::to_string(bytes) + "-byte aligned");
+}
+
+// ---------------------------------------------------------------- elementwise / pooling
+__global__ __launch_bounds__(256) void quantize_kernel(const bf16* __restrict__ x, uint8_t* __restrict__ y, long n16,
+                                                       float q) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n16; i += (long)gridDim.x * blockDim.x) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(x + i * 16);
+    reinterpret_cast<u32x4*>(y)[i] = quant16(src[0], src[1], q);
+  }
+}
+
+__global__ __launch_bounds__(256) void dequantize_kernel(const uint8_t* __restrict__ x, bf16* __restrict__ y, long n16,
+                                                         float s) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n16; i += (long)gridDim.x * blockDim.x) {
+    u32x4 v = reinterpret_cast<const u32x4*>(x)[i];
+    bf16x8 o0, o1;
+    float f[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      unpack4(v[w], f);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (w < 2) o0[w * 4 + e] = f2bf(f[e] * s);
+        else o1[(w - 2) * 4 + e] = f2bf(f[e] * s);
+      }
+    }
+    reinterpret_cast<bf16x8*>(y + i * 16)[0] = o0;
+    reinterpret_cast<bf16x8*>(y + i * 16)[1] = o1;
+  }
+}
+
+// NHWC fp8 pooling, 16 channels per thread; avg divides by the in-bounds count (TF SAME).
+// Output value = pooled input * rq (rq = sx / sy requantises into the destination buffer).
+template <bool MAX>
+__global__ __launch_bounds__(256) void pool_fp8_kernel(const uint8_t* __restrict__ x, uint8_t* __restrict__ y, int N,
+                                                       int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh,
+                                                       int sw, int ph, int pw, int ldy, int y_coff, float rq) {
+  const int cchunks = C / 16;
+  const long total = (long)N * Ho * Wo * cchunks;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int cc = idx % cchunks;
+    long t = idx / cchunks;
+    const int ox = t % Wo;
+    t /= Wo;
+    const int oy = t % Ho;
+    const int n = t / Ho;
+    float acc[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = MAX ? -INFINITY : 0.f;
+    int cnt = 0;
+    const int iy0 = oy * sh - ph, ix0 = ox * sw - pw;
+    for (int dy = 0; dy < kh; ++dy) {
+      const int iy = iy0 + dy;
+      if ((unsigned)iy >= (unsigned)H) continue;
+      for (int dx = 0; dx < kw; ++dx) {
+        const int ix = ix0 + dx;
+        if ((unsigned)ix >= (unsigned)W) continue;
+        u32x4 v = *reinterpret_cast<const u32x4*>(x + (((size_t)n * H + iy) * W + ix) * C + cc * 16);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          float f[4];
+          unpack4(v[w], f);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[w * 4 + e] = MAX ? fmaxf(acc[w * 4 + e], f[e]) : acc[w * 4 + e] + f[e];
+        }
+        ++cnt;
+      }
+    }
+    const float sc = MAX ? rq : rq / (float)max(cnt, 1);
+    u32x4 o;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) o[w] = pack4(acc[w * 4] * sc, acc[w * 4 + 1] * sc, acc[w * 4 + 2] * sc, acc[w * 4 + 3] * sc);
+    *reinterpret_cast<u32x4*>(y + (((size_t)n * Ho + oy) * Wo + ox) * ldy + y_coff + cc * 16) = o;
+  }
+}
+
+// [N, HW, C] fp8 -> [N, C] bf16 mean * s.  One block per image, 16 channels per thread.
+__global__ __launch_bounds__(256) void gap_fp8_kernel(const uint8_t* __restrict__ x, bf16* __restrict__ y, int HW, int C,
+                                                      float s) {
+  const int n = blockIdx.x;
+  const float inv = s / (float)HW;
+  for (int cc = threadIdx.x; cc < C / 16; cc += blockDim.x) {
+    float acc[16] = {};
+    const uint8_t* p = x + (size_t)n * HW * C + cc * 16;
+    for (int i = 0; i < HW; ++i) {
+      u32x4 v = *reinterpret_cast<const u32x4*>(p + (size_t)i * C);
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        float f[4];
+        unpack4(v[w], f);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[w * 4 + e] += f[e];
+      }
+    }
+    bf16x8 o0, o1;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o0[e] = f2bf(acc[e] * inv);
+      o1[e] = f2bf(acc[8 + e] * inv);
+    }
+    bf16x8* dst = reinterpret_cast<bf16x8*>(y + (size_t)n * C + cc * 16);
+    dst[0] = o0;
+    dst[1] = o1;
+  }
+}
+
+int grid_for(long work, int block) {
+  long g = (work + block - 1) / block;
+  return (int)(g < 1 ? 1 : (g > 65536 ? 65536 : g));
+}
+
+}  // namespace
+
+// Conv2D NHWC on fp8 (see header).  x: fp8 [N,H,W,Cin] (bf16 when in_bf16), w: fp8
+// [Cout, KH*KW*Cin], scale/bias fp32 [Cout]; out_fp8 selects fp8 (out_q = 1/sy) or bf16.
+void conv2d_nhwc_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t y, int N, int H, int W,
+                     int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw, int Ho, int Wo,
+                     int ldy, int y_coff, int in_bf16, float in_q, int out_fp8, float out_q, int act, uintptr_t stream,
+                     int cfg) {
+  const int ealign = out_fp8 ? 16 : 8;
+  if (Cin % 16) throw std::invalid_argument("conv2d_nhwc_fp8: Cin must be a multiple of 16");
+  if (Cout % ealign || ldy % ealign || y_coff % ealign)
+    throw std::invalid_argument("conv2d_nhwc_fp8: Cout/ldy/y_coff not a multiple of the 16-byte output chunk");
+  if (Cout % 4) throw std::invalid_argument("conv2d_nhwc_fp8: Cout % 4 != 0");
+  if (N <= 0 || Ho <= 0 || Wo <= 0 || Cout <= 0) throw std::invalid_argument("conv2d_nhwc_fp8: empty problem");
+  if ((long)N * H * W * Cin >= (1L << 31) || (long)N * Ho * Wo >= (1L << 31))
+    throw std::invalid_argument("conv2d_nhwc_fp8: tensor too large for 32-bit indexing");
+  if (!scale || !bias) throw std::invalid_argument("conv2d_nhwc_fp8: scale and bias pointers are required");
+  check_align(x, 16, "x");
+  check_align(w, 16, "w");
+  check_align(y, 16, "y");
+  check_align(scale, 16, "scale");
+  check_align(bias, 16, "bias");
+  Fp8Params p{};
+  p.x = reinterpret_cast<const uint8_t*>(x);
+  p.w = reinterpret_cast<const uint8_t*>(w);
+  p.scale = reinterpret_cast<const float*>(scale);
+  p.bias = reinterpret_cast<const float*>(bias);
+  p.y = reinterpret_cast<uint8_t*>(y);
+  p.in_q = in_q;
+  p.out_q = out_q;
+  p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout;
+  p.KH = KH; p.KW = KW; p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
+  p.M = N * Ho * Wo;
+  p.K = KH * KW * Cin;
+  p.ldx = Cin;
+  p.ldy = ldy; p.y_coff = y_coff;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const bool pointwise = KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
+  if (pointwise) launch_io<false>(p, in_bf16, out_fp8, act, cfg, s);
+  else launch_io<true>(p, in_bf16, out_fp8, act, cfg, s);
+}
+
+// Y[M, N] = act(Xq[M, K] . Wq[N, K]^T * scale + bias)
+void gemm_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t y, int M, int N, int K, int ldx,
+              int ldy, int in_bf16, float in_q, int out_fp8, float out_q, int act, uintptr_t stream, int cfg) {
+  const int ealign = out_fp8 ? 16 : 8;
+  if (K % 16 || ldx % 16) throw std::invalid_argument("gemm_fp8: K and ldx must be multiples of 16");
+  if (N % ealign || ldy % ealign) throw std::invalid_argument("gemm_fp8: N/ldy not a multiple of the output chunk");
+  if (M <= 0 || N <= 0) throw std::invalid_argument("gemm_fp8: empty problem");
+  if (!scale || !bias) throw std::invalid_argument("gemm_fp8: scale and bias pointers are required");
+  check_align(x, 16, "x");
+  check_align(w, 16, "w");
+  check_align(y, 16, "y");
+  check_align(scale, 16, "scale");
+  check_align(bias, 16, "bias");
+  Fp8Params p{};
+  p.x = reinterpret_cast<const uint8_t*>(x);
+  p.w = reinterpret_cast<const uint8_t*>(w);
+  p.scale = reinterpret_cast<const float*>(scale);
+  p.bias = reinterpret_cast<const float*>(bias);
+  p.y = reinterpret_cast<uint8_t*>(y);
+  p.in_q = in_q;
+  p.out_q = out_q;
+  p.M = M; p.Cout = N; p.K = K; p.ldx = ldx; p.ldy = ldy; p.y_coff = 0;
+  launch_io<false>(p, in_bf16, out_fp8, act, cfg, reinterpret_cast<hipStream_t>(stream));
+}
+
+void quantize_bf16_fp8(uintptr_t x, uintptr_t y, long n, float q, uintptr_t stream) {
+  if (n % 16) throw std::invalid_argument("quantize_bf16_fp8: n % 16 != 0");
+  check_align(x, 16, "x");
+  check_align(y, 16, "y");
+  if (n == 0) return;
+  hipLaunchKernelGGL(quantize_kernel, dim3(grid_for(n / 16, 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const bf16*>(x), reinterpret_cast<uint8_t*>(y), n / 16, q);
+  FTM_CHECK_LAUNCH();
+}
+
+void dequantize_fp8_bf16(uintptr_t x, uintptr_t y, long n, float s, uintptr_t stream) {
+  if (n % 16) throw std::invalid_argument("dequantize_fp8_bf16: n % 16 != 0");
+  check_align(x, 16, "x");
+  check_align(y, 16, "y");
+  if (n == 0) return;
+  hipLaunchKernelGGL(dequantize_kernel, dim3(grid_for(n / 16, 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const uint8_t*>(x),
+                     reinterpret_cast<bf16*>(y), n / 16, s);
+  FTM_CHECK_LAUNCH();
+}
+
+void pool2d_nhwc_fp8(uintptr_t x, uintptr_t y, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh,
+                     int sw, int ph, int pw, int ldy, int y_coff, int is_max, float rq, uintptr_t stream) {
+  if (C % 16 || ldy % 16 || y_coff % 16) throw std::invalid_argument("pool2d_nhwc_fp8: C/ldy/y_coff % 16 != 0");
+  check_align(x, 16, "x");
+  check_align(y, 16, "y");
+  const long work = (long)N * Ho * Wo * (C / 16);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (is_max)
+    hipLaunchKernelGGL(pool_fp8_kernel<true>, dim3(grid_for(work, 256)), dim3(256), 0, s,
+                       reinterpret_cast<const uint8_t*>(x), reinterpret_cast<uint8_t*>(y), N, H, W, C, Ho, Wo, kh, kw,
+                       sh, sw, ph, pw, ldy, y_coff, rq);
+  else
+    hipLaunchKernelGGL(pool_fp8_kernel<false>, dim3(grid_for(work, 256)), dim3(256), 0, s,
+                       reinterpret_cast<const uint8_t*>(x), reinterpret_cast<uint8_t*>(y), N, H, W, C, Ho, Wo, kh, kw,
+                       sh, sw, ph, pw, ldy, y_coff, rq);
+  FTM_CHECK_LAUNCH();
+}
+
+void global_avgpool_fp8(uintptr_t x, uintptr_t y, int N, int HW, int C, float s, uintptr_t stream) {
+  if (C % 16) throw std::invalid_argument("global_avgpool_fp8: C % 16 != 0");
+  check_align(x, 16, "x");
+  check_align(y, 16, "y");
+  hipLaunchKernelGGL(gap_fp8_kernel, dim3(N), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const uint8_t*>(x), reinterpret_cast<bf16*>(y), HW, C, s);
+  FTM_CHECK_LAUNCH();
+}
+
+void register_fp8(pybind11::module_& m) {
+  m.def("conv2d_nhwc_fp8", &conv2d_nhwc_fp8);
+  m.def("gemm_fp8", &gemm_fp8);
+  m.def("quantize_bf16_fp8", &quantize_bf16_fp8);
+  m.def("dequantize_fp8_bf16", &dequantize_fp8_bf16);
+  m.def("pool2d_nhwc_fp8", &pool2d_nhwc_fp8);
+  m.def("global_avgpool_fp8", &global_avgpool_fp8);
+  m.attr("fp8_igemm_num_configs") = NCFG;
+}

@@ -1,0 +1,163 @@
+"""FP8 (OCP e4m3fn) path: quantisation, fp8 MFMA conv/GEMM/pool kernels against fp32
+references with the same quantisation points, and the Inception-v3 fp8 compiled plan
+(calibrated scales, concat-by-stride-write in fp8) against the bf16 plan."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from flink_tensorflow_amd.graph.compiler import CompiledFunction
+from flink_tensorflow_amd.graph.graph import Graph
+from flink_tensorflow_amd.graph.session import Session
+from flink_tensorflow_amd.models.zoo.inception_v3 import inception_v3_graph_def
+from flink_tensorflow_amd.ops import fp8 as Q
+
+
+def test_quantize_roundtrip_and_saturation():
+    x = torch.tensor([0.0, 0.1, 1.0, 447.0, 1e4, -1e4, -3.3])
+    b = Q.to_fp8_bytes(x)
+    y = Q.from_fp8_bytes(b)
+    assert y[4] == 448 and y[5] == -448  # saturating, never NaN
+    assert (y[:4] - x[:4]).abs().max() <= 0.0625 * x[:4].abs().max()
+    w = torch.randn(16, 3, 3, 32)
+    wq, ws = Q.quantize_weight(w)
+    assert wq.dtype == torch.uint8 and wq.shape == (16, 288) and ws.shape == (16,)
+    back = Q.from_fp8_bytes(wq) * ws[:, None]
+    assert ((back - w.reshape(16, -1)).abs() / w.reshape(16, -1).abs().amax(1, keepdim=True)).max() < 0.07
+
+
+def test_conv_fp8_host_reference_tracks_fp32():
+    torch.manual_seed(0)
+    x = torch.randn(2, 9, 9, 32).relu()
+    w = torch.randn(48, 3, 3, 32) * 0.1
+    b = torch.randn(48) * 0.1
+    sx = Q.scale_for(x.abs().max())
+    wq, ws = Q.quantize_weight(w)
+    y = Q.conv2d_nhwc_fp8(Q.quantize(x, sx), sx, wq, (3, 3), ws, b, (2, 2), (1, 1, 1, 1), act="relu")
+    ref = F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), b, 2, 1).relu().permute(0, 2, 3, 1)
+    assert (y - ref).abs().max() < 0.08 * ref.abs().max()
+
+
+def _inception_plans(device, hw=75, batch=2, **kw):
+    g = Graph.from_graph_def(inception_v3_graph_def(image_hw=(hw, hw), out_hw=(hw, hw)))
+    feeds = {"images:0": ((batch, hw, hw, 3), "UINT8")}
+    fetch = ["logits:0", "top_k:1"]
+    p16 = CompiledFunction(g, feeds, fetch, device, strict=True, **kw)
+    p8 = CompiledFunction(g, feeds, fetch, device, strict=True, precision="fp8", **kw)
+    return g, p16, p8
+
+
+def test_inception_v3_fp8_plan_host():
+    g, p16, p8 = _inception_plans("cpu")
+    s8 = p8.summary()
+    assert s8["glue_ops"] == [] and s8["fp8_layers"] == 93
+    assert "concat" not in s8["kinds"] and "dequant" not in s8["kinds"]  # stride-written fp8 concats
+    img = torch.randint(0, 256, (2, 75, 75, 3), dtype=torch.uint8)
+    l16, _ = p16({"images:0": img})
+    l8, _ = p8({"images:0": img})
+    assert F.cosine_similarity(l16.flatten(), l8.flatten(), dim=0) > 0.99
+    # the bf16 plan itself matches the op-by-op interpreter
+    ref = Session(g).run(["logits:0"], {"images:0": img})[0]
+    assert F.cosine_similarity(l16.flatten(), ref.flatten().float(), dim=0) > 0.999
+
+
+# ------------------------------------------------------------------------------ GPU
+DEV = torch.device("cuda", 0)
+
+
+def _conv_case(cin, cout, k, stride, pads, in_bf16, out_fp8, cfg, offset=0, extra=0, N=2, H=11, W=13):
+    torch.manual_seed(cin + cout + k + cfg)
+    kh, kw = (k, k) if isinstance(k, int) else k
+    x = torch.randn(N, H, W, cin).relu()
+    w = torch.randn(cout, kh, kw, cin) / (kh * kw * cin) ** 0.5
+    b = torch.randn(cout) * 0.1
+    sx = Q.scale_for(x.abs().max())
+    wq, ws = Q.quantize_weight(w)
+    xin = x.to(torch.bfloat16) if in_bf16 else Q.quantize(x, sx)
+    if in_bf16:  # the host reference quantises the same bf16 values
+        x_host = xin.float()
+    else:
+        x_host = xin
+    so = 0.02 if out_fp8 else None
+    ref = Q.conv2d_nhwc_fp8(x_host, sx, wq, (kh, kw), ws, b, (stride, stride), pads, act="relu", out_scale=so)
+    Ho, Wo = ref.shape[1:3]
+    odt = torch.uint8 if out_fp8 else torch.bfloat16
+    out = torch.zeros((N, Ho, Wo, cout + extra), dtype=odt, device=DEV)
+    got = Q.conv2d_nhwc_fp8(xin.to(DEV), sx, wq.to(DEV), (kh, kw), ws.to(DEV), b.to(DEV), (stride, stride), pads,
+                            act="relu", out_scale=so, out=out, out_channel_offset=offset, cfg=cfg)
+    torch.cuda.synchronize()
+    g = got[..., offset:offset + cout].cpu()
+    if out_fp8:
+        gd, rd = Q.from_fp8_bytes(g.contiguous()) * so, Q.from_fp8_bytes(ref) * so
+        # accumulation order may flip a rounding tie: allow one e4m3 step (2^-3 relative)
+        assert ((gd - rd).abs() <= 0.13 * rd.abs() + 1e-3).all()
+        assert (gd == rd).float().mean() > 0.97
+        if extra:
+            assert (got[..., :offset] == 0).all() and (got[..., offset + cout:] == 0).all()
+    else:
+        torch.testing.assert_close(g.float(), ref.float(), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+def test_conv_fp8_configs_gpu(cfg):
+    _conv_case(32, 64, 3, 1, (1, 1, 1, 1), False, True, cfg)
+    _conv_case(64, 192, 3, 2, (0, 0, 0, 0), False, False, cfg)
+    _conv_case(48, 96, (1, 7), 1, (0, 0, 3, 3), False, True, cfg, offset=32, extra=64)
+
+
+@pytest.mark.gpu
+def test_conv_fp8_pointwise_and_bf16_input_gpu():
+    _conv_case(160, 128, 1, 1, (0, 0, 0, 0), False, True, -1, N=3, H=17, W=17)
+    _conv_case(32, 32, 3, 1, (0, 0, 0, 0), True, True, -1)  # stem output (bf16) quantised on load
+    _conv_case(32, 80, 3, 2, (0, 1, 0, 1), True, False, -1)
+
+
+@pytest.mark.gpu
+def test_gemm_fp8_gpu():
+    torch.manual_seed(1)
+    x = torch.randn(300, 256)
+    w = torch.randn(96, 256) / 16
+    sx = Q.scale_for(x.abs().max())
+    wq, ws = Q.quantize_weight(w)
+    ref = Q.gemm_fp8(Q.quantize(x, sx), sx, wq, ws, act=None)
+    got = Q.gemm_fp8(Q.quantize(x, sx).to(DEV), sx, wq.to(DEV), ws.to(DEV), act=None)
+    torch.testing.assert_close(got.float().cpu(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+def test_quantize_dequantize_bitexact_gpu():
+    x = (torch.randn(4096) * 30).to(torch.bfloat16)
+    ref = Q.quantize(x.float(), 0.5)
+    got = Q.quantize(x.to(DEV), 0.5).cpu()
+    assert torch.equal(got, ref)
+    back = Q.dequantize(got.to(DEV), 0.5).cpu()
+    assert torch.equal(back, (Q.from_fp8_bytes(ref) * 0.5).to(torch.bfloat16))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["max", "avg"])
+def test_pool_fp8_gpu(mode):
+    torch.manual_seed(2)
+    x = Q.quantize(torch.randn(2, 9, 9, 48).relu(), 0.01)
+    for ks, st, pad in (((3, 3), (1, 1), (1, 1, 1, 1)), ((3, 3), (2, 2), (0, 0, 0, 0))):
+        ref = Q.pool2d_nhwc_fp8(x, ks, st, pad, mode, rq=0.7)
+        got = Q.pool2d_nhwc_fp8(x.to(DEV), ks, st, pad, mode, rq=0.7).cpu()
+        gd, rd = Q.from_fp8_bytes(got), Q.from_fp8_bytes(ref)
+        assert ((gd - rd).abs() <= 0.13 * rd.abs() + 1e-6).all(), mode
+    ref = Q.global_avgpool_fp8(x, 0.01)
+    got = Q.global_avgpool_fp8(x.to(DEV), 0.01).float().cpu()
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_inception_v3_fp8_plan_gpu():
+    g = Graph.from_graph_def(inception_v3_graph_def(image_hw=(75, 75), out_hw=(75, 75)))
+    feeds = {"images:0": ((4, 75, 75, 3), "UINT8")}
+    img = torch.randint(0, 256, (4, 75, 75, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(5))
+    calib = {"images:0": img}
+    host = CompiledFunction(g, feeds, ["logits:0"], "cpu", strict=True, precision="fp8", calibration=calib)
+    dev = CompiledFunction(g, feeds, ["logits:0"], DEV, strict=True, precision="fp8", calibration=calib)
+    assert dev.summary()["hip_graph"] and dev.summary()["fp8_layers"] == 93
+    lh = host({"images:0": img})[0]
+    ld = dev({"images:0": img.to(DEV)})[0].cpu()
+    assert F.cosine_similarity(lh.flatten(), ld.flatten(), dim=0) > 0.99
