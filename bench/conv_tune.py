@@ -49,7 +49,7 @@ def main():
         y = torch.empty(B, Ho, Wo, Cout, device=dev, dtype=torch.bfloat16)
         flops = 2.0 * B * Ho * Wo * Cout * k * k * Cin
         nbytes = x.numel() * 2 + y.numel() * 2 * (2 if res else 1) + w.numel() * 2
-        cfgs = list(range(ncfg)) + [-1]
+        cfgs = list(range(ncfg)) + list(K.V2_CONFIGS) + [-1]
         times = {c: [] for c in cfgs}
         for c in cfgs:  # warmup
             K.conv2d_nhwc(x, w, b, r, (s, s), pad, (1, 1), "relu", out=y, cfg=c)
@@ -64,7 +64,7 @@ def main():
                 e1.synchronize()
                 times[c].append(e0.elapsed_time(e1) / 10 * 1e3)
         med = {c: sorted(v)[len(v) // 2] for c, v in times.items()}
-        best = min(range(ncfg), key=lambda c: med[c])
+        best = min([c for c in cfgs if c >= 0], key=lambda c: med[c])
         row = {"layer": name, "us": {str(c): round(med[c], 1) for c in cfgs}, "best": best,
                "auto_us": round(med[-1], 1), "best_us": round(med[best], 1),
                "best_tflops": round(flops / med[best] / 1e6, 1), "best_gbps": round(nbytes / med[best] / 1e3, 1)}

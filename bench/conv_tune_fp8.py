@@ -1,0 +1,75 @@
+"""Times the fp8 conv tile configurations (register-staged 0/1/2, pipelined LDS-DMA 16/17)
+on the Inception-v3 layer shapes at B=256 (random e4m3 data, interleaved rounds)."""
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, __file__.rsplit("/bench/", 1)[0])
+from flink_tensorflow_amd.ops import fp8 as Q  # noqa: E402
+from flink_tensorflow_amd.ops import kernels as K  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+# (name, H, W, Cin, Cout, (kh, kw), stride, pad(t,b,l,r))
+LAYERS = [
+    ("2b_3x3", 147, 147, 32, 64, (3, 3), 1, (1, 1, 1, 1)),
+    ("3b_1x1", 73, 73, 64, 80, (1, 1), 1, (0, 0, 0, 0)),
+    ("4a_3x3", 73, 73, 80, 192, (3, 3), 1, (0, 0, 0, 0)),
+    ("5b_1x1", 35, 35, 192, 64, (1, 1), 1, (0, 0, 0, 0)),
+    ("5b_5x5", 35, 35, 48, 64, (5, 5), 1, (2, 2, 2, 2)),
+    ("5b_3x3a", 35, 35, 64, 96, (3, 3), 1, (1, 1, 1, 1)),
+    ("5b_3x3b", 35, 35, 96, 96, (3, 3), 1, (1, 1, 1, 1)),
+    ("6a_3x3s2", 35, 35, 288, 384, (3, 3), 2, (0, 0, 0, 0)),
+    ("6b_1x1", 17, 17, 768, 192, (1, 1), 1, (0, 0, 0, 0)),
+    ("6c_1x7", 17, 17, 160, 160, (1, 7), 1, (0, 0, 3, 3)),
+    ("6c_7x1", 17, 17, 160, 192, (7, 1), 1, (3, 3, 0, 0)),
+    ("7b_1x1", 8, 8, 1280, 448, (1, 1), 1, (0, 0, 0, 0)),
+    ("7b_3x3", 8, 8, 448, 384, (3, 3), 1, (1, 1, 1, 1)),
+    ("7b_1x3", 8, 8, 384, 384, (1, 3), 1, (0, 0, 1, 1)),
+]
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    out = []
+    for name, H, W, Cin, Cout, (kh, kw), s, pad in LAYERS:
+        x = torch.randint(0, 126, (B, H, W, Cin), dtype=torch.uint8, device=dev)  # positive e4m3 codes
+        wq = torch.randint(0, 126, (Cout, kh * kw * Cin), dtype=torch.uint8, device=dev)
+        ws = torch.full((Cout,), 1e-3, device=dev)
+        b = torch.zeros(Cout, device=dev)
+        cs = ws * 0.01
+        Ho, Wo = K.conv_out_hw(H, W, kh, kw, s, s, pad[0], pad[2], 1, 1, pad[1], pad[3])
+        y = torch.empty(B, Ho, Wo, Cout, device=dev, dtype=torch.uint8)
+        flops = 2.0 * B * Ho * Wo * Cout * kh * kw * Cin
+        cfgs = [0, 1, 2, 16, 17, -1]
+        times = {c: [] for c in cfgs}
+
+        def run(c):
+            Q.conv2d_nhwc_fp8(x, 0.01, wq, (kh, kw), ws, b, (s, s), pad, act="relu", out_scale=0.05, out=y, cfg=c,
+                              chan_scale=cs)
+
+        for c in cfgs:
+            run(c)
+        torch.cuda.synchronize()
+        for _ in range(5):
+            for c in cfgs:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(10):
+                    run(c)
+                e1.record()
+                e1.synchronize()
+                times[c].append(e0.elapsed_time(e1) / 10 * 1e3)
+        med = {c: sorted(v)[len(v) // 2] for c, v in times.items()}
+        best = min([c for c in cfgs if c >= 0], key=lambda c: med[c])
+        row = {"layer": name, "us": {str(c): round(med[c], 1) for c in cfgs}, "best": best,
+               "auto_us": round(med[-1], 1), "best_us": round(med[best], 1),
+               "best_tflops": round(flops / med[best] / 1e6, 1)}
+        out.append(row)
+        print(json.dumps(row), flush=True)
+    print(json.dumps({"sum_auto_us": round(sum(r["auto_us"] for r in out), 1),
+                      "sum_best_us": round(sum(r["best_us"] for r in out), 1)}))
+
+
+if __name__ == "__main__":
+    main()

@@ -477,6 +477,11 @@ class CompiledFunction:
         b_dev = bias.to(self.device, torch.float32).contiguous() if bias is not None else None
         self.params += [w_dev] + ([b_dev] if b_dev is not None else [])
         out = self._new((N, Ho, Wo, Cout))
+        if (self.precision == "fp8" and residual is None and act in (K.ACT_NONE, K.ACT_RELU) and Cout % 16 == 0
+                and self._fp8_consumers_ok(last.name) and self._qscale(last.name) is not None):
+            # bf16 layer (e.g. the RGB stem) feeding fp8 consumers: emit e4m3 directly
+            out = self._new((N, Ho, Wo, Cout), torch.uint8)
+            out.qscale = self._qscale(last.name)
         res_val = None
         if residual is not None:
             rn, ri = residual
@@ -484,14 +489,39 @@ class CompiledFunction:
         xin = x if xin_shape_override is not None else self._ensure_padded(x, cin_pad, node.name)
         for a in absorbed:
             self._fused.add(a.name)
+        KHe, KWe = w_ohwi.shape[1], w_ohwi.shape[2]
+        if self._use_dconv(cin_pad, KHe, KWe, (sh, sw), (dh, dw), 2, residual, act):
+            bn = 64 if Cout >= 64 else 32
+            w_arr = K.dconv_bf16_weight_bytes(w_ohwi, bn).to(self.device)
+            if b_dev is None:
+                b_dev = torch.zeros(Cout, dtype=torch.float32, device=self.device)
+            self.params += [w_arr, b_dev]
+
+            def run_d(xin=xin, out=out, w_arr=w_arr, b_dev=b_dev, bn=bn):
+                K.conv2d_direct(xin.buf, w_arr, (KHe, KWe), Cout, b_dev, (sh, sw), (pt, pb, pl, pr), act,
+                                out=_target(out), out_channel_offset=_coff(out), bn=bn,
+                                out_scale=_eff_scale(out) if out.qscale is not None else None)
+
+            self._emit(node.name, "conv", run_d, [xin], [out])
+            self.vals[(last.name, 0)] = out
+            self._alias_fused_outputs(absorbed, out)
+            return
 
         def run(xin=xin, out=out, res_val=res_val, w_dev=w_dev, b_dev=b_dev):
             K.conv2d_nhwc(xin.buf, w_dev, b_dev, res_val.buf if res_val is not None else None, (sh, sw),
-                          (pt, pb, pl, pr), (dh, dw), act, out=_target(out), out_channel_offset=_coff(out))
+                          (pt, pb, pl, pr), (dh, dw), act, out=_target(out), out_channel_offset=_coff(out),
+                          out_scale=_eff_scale(out) if out.qscale is not None else None)
 
         self._emit(node.name, "conv", run, [xin] + ([res_val] if res_val else []), [out])
         self.vals[(last.name, 0)] = out
         self._alias_fused_outputs(absorbed, out)
+
+    def _use_dconv(self, cin_phys, KH, KW, stride, dil, es, residual, act) -> bool:
+        """Direct LDS conv for narrow layers (input row <= 32 B: RGB stems, Inception's
+        32-channel fp8 layers); measured faster there by bench/dconv_tune.py, slower for
+        wider inputs, which stay on the implicit GEMM."""
+        return (self.device.type == "cuda" and residual is None and act in (K.ACT_NONE, K.ACT_RELU)
+                and cin_phys * es <= 32 and K.dconv_eligible(cin_phys, KH, KW, stride, dil, es))
 
     def _conv_fp8_ok(self, node: Node, x: Val, Cin, Cout, residual, act) -> bool:
         if residual is not None or act not in (K.ACT_NONE, K.ACT_RELU) or Cin % 16 or Cout % 16 or x.phys_c:
@@ -518,6 +548,19 @@ class CompiledFunction:
         for a in absorbed:
             self._fused.add(a.name)
         self.fp8_layers += 1
+        if x.qscale is not None and self._use_dconv(Cin, KH, KW, stride, dil, 1, None, act):
+            bn = 64 if Cout >= 64 else 32
+            w_arr = K.dconv_weights(wq, Cout, 1, bn).to(dev)
+            self.params.append(w_arr)
+
+            def run_d(x=x, out=out, w_arr=w_arr, cs=cs_dev, b=b_dev, bn=bn):
+                K.conv2d_direct(_view(x), w_arr, (KH, KW), Cout, b, stride, pads, act, out=_target(out),
+                                out_channel_offset=_coff(out), bn=bn, chan_scale=cs, out_scale=_eff_scale(out))
+
+            self._emit(node.name, "conv_fp8", run_d, [x], [out])
+            self.vals[(last.name, 0)] = out
+            self._alias_fused_outputs(absorbed, out)
+            return
 
         def run(x=x, out=out, wq=wq_dev, ws=ws_dev, cs=cs_dev, b=b_dev, x_scale=x_scale):
             F8.conv2d_nhwc_fp8(_view(x), x_scale, wq, (KH, KW), ws, b, stride, pads, dil, act,

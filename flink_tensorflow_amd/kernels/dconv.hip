@@ -1,0 +1,295 @@
+// Direct convolution for narrow layers (few input channels x taps): the whole reduction
+// of one output tile runs out of LDS.
+//
+// The implicit-GEMM kernels re-read every input pixel once per filter tap (KH*KW x im2col
+// traffic).  For layers whose weights and input halo fit on chip at once — the RGB stems
+// (3 -> 32/64 channels), Inception's 147x147 / 73x73 / 35x35 3x3 layers (32..128 fp8 input
+// channels) — that re-read traffic, not the MFMAs, bounds the layer.  Here one workgroup
+//   1. DMAs its input patch ((TH-1)*S + KH) x ((TW-1)*S + KW) pixels x Cin (zero page for
+//      padding) and the filter bank [BN][KH*KW*Cin (+pad)] into LDS (global_load_lds),
+//   2. runs the K loop from LDS: an MFMA K-step covers 4 lane groups x KL bytes (KL = 16 B
+//      bf16 / 32 B fp8); each lane group's KL-byte K segment lies inside ONE filter tap
+//      (Cin*ES is a multiple of KL), so its B fragment is the tap-shifted patch row —
+//      im2col happens in the LDS address, never in memory traffic,
+//   3. stages the [256 px][BN] result through LDS and stores 16-B row segments (bf16 or
+//      e4m3 with the successor's scale), channel-offset capable (concat slices).
+// Output tile: 16 x 16 pixels of one image (wave w owns tile rows 4w..4w+3 = 4 fragments),
+// BN = 32 or 64 channels.  Weights are pre-arranged by the host: row pitch WP bytes =
+// round_up(KH*KW*Cin*ES, 4*KL) + 16 (the +16 keeps the 16 rows of a fragment read on
+// different banks).
+#include <pybind11/pybind11.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+namespace {
+
+__device__ __attribute__((aligned(16))) uint32_t g_zero16[4];
+
+constexpr int TH = 16, TW = 16, NT = 256;
+
+struct DconvParams {
+  const uint8_t* x;    // [N, H, W, Cin] (bf16 or e4m3)
+  const uint8_t* w;    // [Cout_pad][WP] bytes, K order (kh, kw, ci)
+  const float* scale;  // fp8: per-channel sw[c]*sx (nullptr for bf16)
+  const float* bias;
+  uint8_t* y;
+  float out_q;
+  int N, H, W, Cin, Ho, Wo, Cout, KH, KW, S, ph, pw;
+  int RB;      // patch row bytes = Cin * ES
+  int WP;      // weight row pitch (bytes)
+  int ksteps;  // MFMA K-steps = (WP - 16) / (4 * KL)
+  int PH, PW;  // patch rows / cols
+  int ldy, y_coff;
+  int tiles_h, tiles_w, tiles_n;
+};
+
+FTM_DEVICE void glds16(const void* src, uint8_t* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+FTM_DEVICE uint32_t pack4_fp8(float a, float b, float c, float d) {
+  const float M = 448.f;
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(a, -M), M), fminf(fmaxf(b, -M), M), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(c, -M), M), fminf(fmaxf(d, -M), M), w, true);
+  return (uint32_t)w;
+}
+
+template <int ES, int BN, int ACT, bool OUT_FP8>
+__global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int KL = ES == 2 ? 16 : 32;  // K bytes per lane per MFMA
+  constexpr int I = BN / 16;             // channel fragments
+  constexpr int J = 4;                   // pixel fragments (tile rows) per wave
+  constexpr int OB = OUT_FP8 ? 1 : 2;
+  constexpr int OLD = BN * OB + 16;
+
+  // block -> (image, tile row, tile col, channel tile); channel tiles of one spatial tile
+  // are adjacent so they share the patch through L2
+  int b = blockIdx.x;
+  const int tn = b % p.tiles_n; b /= p.tiles_n;
+  const int tw = b % p.tiles_w; b /= p.tiles_w;
+  const int th = b % p.tiles_h;
+  const int n = b / p.tiles_h;
+  const int oy0 = th * TH, ox0 = tw * TW, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int patch_bytes = p.PH * p.PW * p.RB;
+  uint8_t* Ps = smem;                                     // patch [PH*PW][RB]
+  uint8_t* Wsm = smem + ((patch_bytes + 1023) & ~1023);   // weights [BN][WP]
+
+  // ---- 1. DMA the patch and the filter bank (lane-linear 16-B chunks)
+  {
+    const int cpr = p.RB >> 4;  // 16-B chunks per patch row
+    const int nchunks = p.PH * p.PW * cpr;
+    const int iy0 = oy0 * p.S - p.ph, ix0 = ox0 * p.S - p.pw;
+    const uint8_t* xb = p.x + (size_t)n * p.H * p.W * p.RB;
+    for (int q0 = wave * 64; q0 < nchunks; q0 += NT) {
+      const int q = q0 + lane;
+      const int r = q / cpr, c = q - r * cpr;
+      const int py = r / p.PW, px = r - py * p.PW;
+      const int iy = iy0 + py, ix = ix0 + px;
+      const bool ok = q < nchunks && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+      const void* src = ok ? (const void*)(xb + ((size_t)iy * p.W + ix) * p.RB + c * 16) : (const void*)g_zero16;
+      glds16(src, Ps + q0 * 16);  // a short last wave-instruction writes past nchunks: slack is reserved
+    }
+    const int wchunks = BN * (p.WP >> 4);
+    const uint8_t* wb = p.w + (size_t)n0 * p.WP;
+    for (int q0 = wave * 64; q0 < wchunks; q0 += NT) {
+      const int q = q0 + lane;
+      const void* src = q < wchunks ? (const void*)(wb + (size_t)q * 16) : (const void*)g_zero16;
+      glds16(src, Wsm + q0 * 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- 2. K loop out of LDS
+  const int frow = lane & 15, fq = lane >> 4;
+  f32x4 acc[I][J];
+#pragma unroll
+  for (int i = 0; i < I; ++i)
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ntaps = p.KH * p.KW;
+  // patch row of fragment j's pixel for this lane at tap offset 0
+  int prow0[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) prow0[j] = ((wave * J + j) * p.S) * p.PW + frow * p.S;
+
+  for (int s = 0; s < p.ksteps; ++s) {
+    const int kb = s * 4 * KL + fq * KL;  // this lane group's K byte offset
+    int tap = kb / p.RB;
+    const int cb = kb - tap * p.RB;
+    if (tap >= ntaps) tap = 0;  // K padding: zero weights, any finite patch data
+    const int dy = tap / p.KW, dx = tap - dy * p.KW;
+    const int toff = dy * p.PW + dx;
+    if constexpr (ES == 2) {
+      bf16x8 a[I], bb[J];
+#pragma unroll
+      for (int i = 0; i < I; ++i) a[i] = *reinterpret_cast<const bf16x8*>(Wsm + (i * 16 + frow) * p.WP + kb);
+#pragma unroll
+      for (int j = 0; j < J; ++j) bb[j] = *reinterpret_cast<const bf16x8*>(Ps + (prow0[j] + toff) * p.RB + cb);
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
+    } else {
+      i32x8 a[I], bb[J];
+#pragma unroll
+      for (int i = 0; i < I; ++i) {
+        const uint8_t* src = Wsm + (i * 16 + frow) * p.WP + kb;
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(src), hi = *reinterpret_cast<const u32x4*>(src + 16);
+        a[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const uint8_t* src = Ps + (prow0[j] + toff) * p.RB + cb;
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(src), hi = *reinterpret_cast<const u32x4*>(src + 16);
+        bb[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], bb[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+    }
+  }
+  __syncthreads();  // everyone done with the patch: reuse LDS for the output tile
+
+  // ---- 3. epilogue: [dequant] + bias + act -> LDS [256 px][BN] -> 16-B row segments
+  uint8_t* Os = smem;
+#pragma unroll
+  for (int i = 0; i < I; ++i) {
+    const int cl = i * 16 + fq * 4;
+    f32x4 sv = {1.f, 1.f, 1.f, 1.f}, bv = {0.f, 0.f, 0.f, 0.f};
+    if (n0 + cl < p.Cout) {
+      if constexpr (ES == 1) sv = *reinterpret_cast<const f32x4*>(p.scale + n0 + cl);
+      bv = *reinterpret_cast<const f32x4*>(p.bias + n0 + cl);
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int pl = (wave * J + j) * TW + frow;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act<ACT>(acc[i][j][r] * sv[r] + bv[r]);
+      if constexpr (OUT_FP8) {
+        *reinterpret_cast<uint32_t*>(Os + pl * OLD + cl) =
+            pack4_fp8(v[0] * p.out_q, v[1] * p.out_q, v[2] * p.out_q, v[3] * p.out_q);
+      } else {
+        bf16x4 o;
+        o[0] = f2bf(v[0]); o[1] = f2bf(v[1]); o[2] = f2bf(v[2]); o[3] = f2bf(v[3]);
+        *reinterpret_cast<bf16x4*>(Os + pl * OLD + cl * 2) = o;
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int EPO = 16 / OB;
+  constexpr int CPR = BN / EPO;
+  for (int q = tid; q < TH * TW * CPR; q += NT) {
+    const int pl = q / CPR, cc = q % CPR;
+    const int oy = oy0 + pl / TW, ox = ox0 + pl % TW;
+    const int c = n0 + cc * EPO;
+    if (oy >= p.Ho || ox >= p.Wo || c >= p.Cout) continue;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(Os + pl * OLD + cc * 16);
+    const size_t m = ((size_t)n * p.Ho + oy) * p.Wo + ox;
+    *reinterpret_cast<u32x4*>(p.y + (m * p.ldy + p.y_coff + c) * OB) = v;
+  }
+}
+
+template <int ES, int BN, bool OUT_FP8>
+void launch_act(const DconvParams& p, int act, size_t lds, hipStream_t s) {
+  dim3 grid(p.N * p.tiles_h * p.tiles_w * p.tiles_n), block(NT);
+  switch (act) {
+    case ACT_NONE:
+      hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_NONE, OUT_FP8>), grid, block, lds, s, p);
+      break;
+    case ACT_RELU:
+      hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_RELU, OUT_FP8>), grid, block, lds, s, p);
+      break;
+    default: throw std::invalid_argument("dconv: activation must be none/relu");
+  }
+}
+
+template <int ES, int BN, bool OUT_FP8>
+void set_lds_limit() {
+  static bool done = false;
+  if (done) return;
+  for (auto f : {(const void*)dconv_kernel<ES, BN, ACT_NONE, OUT_FP8>, (const void*)dconv_kernel<ES, BN, ACT_RELU, OUT_FP8>})
+    hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  done = true;
+}
+
+}  // namespace
+
+int dconv_lds_bytes(int es, int bn, int KH, int KW, int S, int Cin, int wp) {
+  const int PH = (TH - 1) * S + KH, PW = (TW - 1) * S + KW;
+  const int patch = PH * PW * Cin * es;
+  const int ob = 2;  // bound by the bf16 output tile
+  int need = ((patch + 1023) & ~1023) + bn * wp + 1024;  // + slack for a short last DMA
+  const int epi = TH * TW * (bn * ob + 16);
+  return need > epi ? need : epi;
+}
+
+// x: NHWC (bf16 es=2 / e4m3 es=1); w: host-arranged [Cout_pad][wp] bytes.
+void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t y, int es, int N, int H, int W,
+           int Cin, int Cout, int KH, int KW, int S, int ph, int pw, int Ho, int Wo, int wp, int ldy, int y_coff,
+           int out_fp8, float out_q, int act, int bn, uintptr_t stream) {
+  const int KL = es == 2 ? 16 : 32;
+  if (es != 1 && es != 2) throw std::invalid_argument("dconv: es must be 1 or 2");
+  if ((Cin * es) % KL) throw std::invalid_argument("dconv: Cin*es must be a multiple of " + std::to_string(KL));
+  if (bn != 32 && bn != 64) throw std::invalid_argument("dconv: bn must be 32 or 64");
+  const int kb = KH * KW * Cin * es;
+  const int kpad = (kb + 4 * KL - 1) / (4 * KL) * (4 * KL);
+  if (wp != kpad + 16) throw std::invalid_argument("dconv: weight pitch must be round_up(K bytes, 4*KL) + 16");
+  const int oe = out_fp8 ? 16 : 8;
+  if (Cout % oe || ldy % oe || y_coff % oe) throw std::invalid_argument("dconv: Cout/ldy/y_coff alignment");
+  if (S != 1 && S != 2) throw std::invalid_argument("dconv: stride must be 1 or 2");
+  if (!bias || (es == 1 && !scale)) throw std::invalid_argument("dconv: bias (and fp8 scale) required");
+  if (x % 16 || w % 16 || y % 16 || bias % 16 || (scale && scale % 16)) throw std::invalid_argument("dconv: alignment");
+  const int lds = dconv_lds_bytes(es, bn, KH, KW, S, Cin, wp);
+  if (lds > 160 * 1024) throw std::invalid_argument("dconv: tile does not fit LDS (" + std::to_string(lds) + " B)");
+  DconvParams p{};
+  p.x = reinterpret_cast<const uint8_t*>(x);
+  p.w = reinterpret_cast<const uint8_t*>(w);
+  p.scale = reinterpret_cast<const float*>(scale);
+  p.bias = reinterpret_cast<const float*>(bias);
+  p.y = reinterpret_cast<uint8_t*>(y);
+  p.out_q = out_q;
+  p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = KH; p.KW = KW; p.S = S;
+  p.ph = ph; p.pw = pw;
+  p.RB = Cin * es;
+  p.WP = wp;
+  p.ksteps = kpad / (4 * KL);
+  p.PH = (TH - 1) * S + KH;
+  p.PW = (TW - 1) * S + KW;
+  p.ldy = ldy; p.y_coff = y_coff;
+  p.tiles_h = (Ho + TH - 1) / TH;
+  p.tiles_w = (Wo + TW - 1) / TW;
+  p.tiles_n = (Cout + bn - 1) / bn;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+#define FTM_DCONV(ES_, BN_, OF_)            \
+  do {                                      \
+    set_lds_limit<ES_, BN_, OF_>();         \
+    launch_act<ES_, BN_, OF_>(p, act, lds, s); \
+  } while (0)
+  if (es == 2) {
+    if (bn == 32) { if (out_fp8) FTM_DCONV(2, 32, true); else FTM_DCONV(2, 32, false); }
+    else { if (out_fp8) FTM_DCONV(2, 64, true); else FTM_DCONV(2, 64, false); }
+  } else {
+    if (bn == 32) { if (out_fp8) FTM_DCONV(1, 32, true); else FTM_DCONV(1, 32, false); }
+    else { if (out_fp8) FTM_DCONV(1, 64, true); else FTM_DCONV(1, 64, false); }
+  }
+#undef FTM_DCONV
+  FTM_CHECK_LAUNCH();
+}
+
+void register_dconv(pybind11::module_& m) {
+  m.def("dconv", &dconv);
+  m.def("dconv_lds_bytes", &dconv_lds_bytes);
+}

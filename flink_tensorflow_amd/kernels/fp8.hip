@@ -303,7 +303,14 @@ constexpr int NCFG = 3;
 
 template <bool CONV, bool IN_BF16, bool OUT_FP8>
 void launch_tile(const Fp8Params& p, int act, int cfg, hipStream_t s) {
-  if (cfg < 0) cfg = p.Cout <= 64 ? (IN_BF16 ? 2 : 1) : 0;  // 256x64 + bf16 staging spills
+  if (cfg < 0) {
+    // measured on the Inception-v3 layer set (bench/conv_tune_fp8.py): narrow layers with a
+    // short K take 256x64; otherwise the channel tile that pads Cout least (64 on ties
+    // loses to 128's higher intensity); 256x64 with bf16 staging spills
+    const int pad64 = (p.Cout + 63) / 64 * 64, pad128 = (p.Cout + 127) / 128 * 128;
+    if (p.Cout <= 64) cfg = (p.K <= 512 && !IN_BF16) ? 1 : 2;
+    else cfg = pad64 < pad128 ? 2 : 0;
+  }
   switch (cfg) {
     case 0: launch_cfg<128, 128, CONV, IN_BF16, OUT_FP8>(p, act, s); break;
     case 1: launch_cfg<256, 64, CONV, IN_BF16, OUT_FP8>(p, act, s); break;

@@ -10,6 +10,8 @@ void register_transformer(pybind11::module_& m);
 void register_embedding(pybind11::module_& m);
 void register_fp8(pybind11::module_& m);
 void register_attention(pybind11::module_& m);
+void register_igemm_v2(pybind11::module_& m);
+void register_dconv(pybind11::module_& m);
 
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "flink_tensorflow_amd CDNA4 (gfx950) kernels";
@@ -20,4 +22,6 @@ PYBIND11_MODULE(_hip, m) {
   register_embedding(m);
   register_fp8(m);
   register_attention(m);
+  register_igemm_v2(m);
+  register_dconv(m);
 }

@@ -31,8 +31,10 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
     def __init__(self, graph_source: Callable[[], GraphDef] | str, image_hw: tuple[int, int],
                  buckets: Sequence[int] = (64, 256), top_k: int = 5, labels: Sequence[str] | None = None,
                  feed: str = "images:0", fetches: Sequence[str] = ("top_k:0", "top_k:1"), depth: int = 3,
-                 device=None, use_graph: bool = True):
+                 device=None, use_graph: bool = True, precision: str = "bf16", calibration_images=None):
         super().__init__(device)
+        self.precision = precision
+        self.calibration_images = calibration_images  # uint8 [n, H, W, 3] for fp8 scales (synthetic if None)
         self.graph_source = graph_source
         self.image_hw = tuple(image_hw)
         self.buckets = tuple(sorted(buckets))
@@ -60,10 +62,18 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
 
             H, W = self.image_hw
             self._plans = {b: CompiledFunction(self._graph, {self.feed: ((b, H, W, 3), "UINT8")}, self.fetches, dev,
-                                               use_graph=self.use_graph, strict=True)
+                                               use_graph=self.use_graph, strict=True, precision=self.precision,
+                                               calibration=self._calibration(b))
                            for b in self.buckets}
             self._runner = PipelinedGpuRunner(self._plans, self.feed, lambda p: p.output_tensors(), (H, W, 3),
                                               torch.uint8, depth=self.depth, device=dev)
+
+    def _calibration(self, b: int):
+        if self.precision != "fp8" or self.calibration_images is None:
+            return None
+        imgs = torch.as_tensor(np.asarray(self.calibration_images, dtype=np.uint8))
+        reps = -(-b // imgs.shape[0])
+        return {self.feed: imgs.repeat(reps, 1, 1, 1)[:b]}
 
     def close(self) -> None:
         if self._runner is not None:
@@ -147,3 +157,19 @@ class ResNet50Model(ImageClassifierModel):
         from .resnet import resnet50_graph_def
 
         return resnet50_graph_def(image_hw=self.image_hw, top_k=self.top_k, seed=self.seed, depth=self.depth_layers)
+
+
+class InceptionV3Model(ImageClassifierModel):
+    """Inception-v3 (random-init frozen graph) compiled for fp8 by default — BASELINE config
+    5: e4m3 weights and activations on the CDNA4 fp8 MFMA, bucketed dynamic batching per
+    operator (each micro-batch runs on the smallest captured bucket that holds it)."""
+
+    def __init__(self, image_hw=(299, 299), buckets=(32, 64, 128, 256), top_k=5, seed: int = 0, device=None,
+                 precision: str = "fp8", **kw):
+        self.seed = seed
+        super().__init__(self._make_graph, image_hw, buckets, top_k, device=device, precision=precision, **kw)
+
+    def _make_graph(self) -> GraphDef:
+        from .inception_v3 import inception_v3_graph_def
+
+        return inception_v3_graph_def(image_hw=self.image_hw, top_k=self.top_k, seed=self.seed)

@@ -81,6 +81,9 @@ def _zeros_bias(n: int, device) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------------------ conv
+# tile configs >= 16 select the pipelined 256-pixel LDS-DMA kernel (igemm_v2.hip) with
+# 128 or 64 output channels per tile; 0..4 are the register-staged igemm_bf16 tiles
+V2_CONFIGS = {16: 128, 17: 64}
 def conv_out_hw(H, W, KH, KW, sh, sw, ph, pw, dh=1, dw=1, ph_hi=None, pw_hi=None):
     ph_hi = ph if ph_hi is None else ph_hi
     pw_hi = pw if pw_hi is None else pw_hi
@@ -91,11 +94,14 @@ def conv_out_hw(H, W, KH, KW, sh, sw, ph, pw, dh=1, dw=1, ph_hi=None, pw_hi=None
 
 def conv2d_nhwc(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor | None = None,
                 residual: torch.Tensor | None = None, stride=(1, 1), pad=(0, 0, 0, 0), dilation=(1, 1),
-                act=None, out: torch.Tensor | None = None, out_channel_offset: int = 0, cfg: int = -1) -> torch.Tensor:
+                act=None, out: torch.Tensor | None = None, out_channel_offset: int = 0, cfg: int = -1,
+                out_scale: float | None = None) -> torch.Tensor:
     """NHWC conv, weights [Cout, KH, KW, Cin]; ``pad = (top, bottom, left, right)``.
 
     Fused epilogue ``act(conv + bias + residual)``.  With ``out`` given, the result is
     written at channel offset ``out_channel_offset`` of ``out`` (concat-by-stride-write).
+    ``out_scale`` stores the result as OCP e4m3 bytes (``y / out_scale``, uint8) — the bf16
+    stem of an fp8 network hands its successor fp8 directly (pipelined kernel only).
     """
     a = act_code(act)
     N, H, W, Cin = x.shape
@@ -106,8 +112,14 @@ def conv2d_nhwc(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor | None
     pt, pb, pl, pr = pad
     dh, dw = dilation
     Ho, Wo = conv_out_hw(H, W, KH, KW, sh, sw, pt, pl, dh, dw, pb, pr)
+    if out_scale is not None:
+        if residual is not None:
+            raise ValueError("conv2d_nhwc: fp8 output does not take a residual")
+        if cfg not in V2_CONFIGS:
+            cfg = 17 if Cout <= 64 else 16
     if out is None:
-        out = torch.empty((N, Ho, Wo, Cout), dtype=x.dtype if x.is_cuda else torch.float32, device=x.device)
+        odt = torch.uint8 if out_scale is not None else (x.dtype if x.is_cuda else torch.float32)
+        out = torch.empty((N, Ho, Wo, Cout), dtype=odt, device=x.device)
         out_channel_offset = 0
     if out.shape[:3] != (N, Ho, Wo) or out_channel_offset + Cout > out.shape[3]:
         raise ValueError(f"conv2d_nhwc: out {tuple(out.shape)} cannot hold [{N},{Ho},{Wo},{Cout}] at "
@@ -115,8 +127,9 @@ def conv2d_nhwc(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor | None
     if residual is not None and tuple(residual.shape) != (N, Ho, Wo, Cout):
         raise ValueError(f"conv2d_nhwc: residual {tuple(residual.shape)} != {(N, Ho, Wo, Cout)}")
     if x.is_cuda:
-        for t, n in ((x, "x"), (w_ohwi, "w"), (out, "out")):
+        for t, n in ((x, "x"), (w_ohwi, "w")):
             _check(t, n, device=x.device)
+        _check(out, "out", torch.uint8 if out_scale is not None else torch.bfloat16, x.device)
         if residual is not None:
             _check(residual, "residual", device=x.device)
         if bias is not None:
@@ -126,6 +139,12 @@ def conv2d_nhwc(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor | None
         else:
             bias = _zeros_bias(Cout, x.device)
         # bottom/right padding is implied by the kernel's bounds check (Ho/Wo carry it)
+        if cfg in V2_CONFIGS:  # pipelined LDS-DMA kernel (igemm_v2.hip)
+            _hip().igemm_v2(x.data_ptr(), w_ohwi.data_ptr(), 0, bias.data_ptr(), _ptr(residual), out.data_ptr(), 2,
+                            N, H, W, Cin, Cout, KH, KW, sh, sw, pt, pl, dh, dw, Ho, Wo, out.shape[3], out_channel_offset,
+                            Cout if residual is None else residual.shape[3], int(out_scale is not None),
+                            1.0 / out_scale if out_scale is not None else 1.0, a, V2_CONFIGS[cfg], _stream())
+            return out
         _hip().conv2d_nhwc_bf16(x.data_ptr(), w_ohwi.data_ptr(), bias.data_ptr(), _ptr(residual), out.data_ptr(),
                                 N, H, W, Cin, Cout, KH, KW, sh, sw, pt, pl, dh, dw, Ho, Wo, out.shape[3],
                                 out_channel_offset, Cout if residual is None else residual.shape[3], a, _stream(), cfg)
@@ -140,6 +159,11 @@ def conv2d_nhwc(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor | None
     if residual is not None:
         y = y + residual.float()
     y = _apply_act_ref(y, a)
+    if out_scale is not None:
+        from .fp8 import to_fp8_bytes
+
+        out[..., out_channel_offset:out_channel_offset + Cout] = to_fp8_bytes(y / out_scale)
+        return out
     out[..., out_channel_offset:out_channel_offset + Cout] = y.to(out.dtype)
     return out
 
@@ -402,4 +426,67 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, residual
     if sum_out is not None:
         sum_out.copy_(s.to(sum_out.dtype))
     out.copy_(F.layer_norm(s, (D,), gamma.float(), beta.float(), eps).to(out.dtype))
+    return out
+
+
+# ------------------------------------------------------------------------------ direct conv
+def dconv_eligible(Cin: int, KH: int, KW: int, stride, dilation, es: int, bn: int = 64) -> bool:
+    """Narrow-layer direct conv (kernels/dconv.hip): stride 1/2, no dilation, Cin*es a
+    multiple of the MFMA lane segment, weights + input patch within LDS."""
+    sh, sw = stride
+    if sh != sw or sh not in (1, 2) or tuple(dilation) != (1, 1) or KH * KW == 1:
+        return False
+    kl = 16 if es == 2 else 32
+    if (Cin * es) % kl:
+        return False
+    kb = KH * KW * Cin * es
+    wp = -(-kb // (4 * kl)) * (4 * kl) + 16
+    ph, pw = 15 * sh + KH, 15 * sw + KW
+    lds = ((ph * pw * Cin * es + 1023) & ~1023) + bn * wp + 1024
+    return lds <= 96 * 1024  # leave room for >= 1 more resident workgroup
+
+
+def dconv_weights(w_ohwi_bytes: torch.Tensor, Cout: int, es: int, bn: int) -> torch.Tensor:
+    """[Cout, KH*KW*Cin*es] weight bytes → [round_up(Cout, bn), wp] with the kernel's pitch."""
+    kl = 16 if es == 2 else 32
+    kb = w_ohwi_bytes.shape[1]
+    wp = -(-kb // (4 * kl)) * (4 * kl) + 16
+    cpad = -(-Cout // bn) * bn
+    out = torch.zeros((cpad, wp), dtype=torch.uint8, device=w_ohwi_bytes.device)
+    out[:Cout, :kb] = w_ohwi_bytes
+    return out
+
+
+def dconv_bf16_weight_bytes(w_ohwi: torch.Tensor, bn: int) -> torch.Tensor:
+    Cout = w_ohwi.shape[0]
+    wb = w_ohwi.to(torch.bfloat16).contiguous().reshape(Cout, -1).view(torch.uint8)
+    return dconv_weights(wb, Cout, 2, bn)
+
+
+def conv2d_direct(x: torch.Tensor, w_arr: torch.Tensor, kshape, Cout: int, bias: torch.Tensor, stride=(1, 1),
+                  pad=(0, 0, 0, 0), act=None, out: torch.Tensor | None = None, out_channel_offset: int = 0,
+                  bn: int = 64, chan_scale: torch.Tensor | None = None, out_scale: float | None = None) -> torch.Tensor:
+    """Direct conv on device: ``x`` NHWC bf16 (``chan_scale`` None) or e4m3 bytes (uint8, with
+    the per-channel dequant scale ``chan_scale``); ``w_arr`` from :func:`dconv_weights`;
+    ``out_scale`` → e4m3 output.  Device-only (the host paths use the reference convs)."""
+    N, H, W, Cin = x.shape
+    KH, KW = kshape
+    s = stride[0]
+    pt, pb, pl, pr = pad
+    Ho, Wo = conv_out_hw(H, W, KH, KW, s, s, pt, pl, 1, 1, pb, pr)
+    es = 2 if x.dtype == torch.bfloat16 else 1
+    out_fp8 = out_scale is not None
+    if out is None:
+        out = torch.empty((N, Ho, Wo, Cout), dtype=torch.uint8 if out_fp8 else torch.bfloat16, device=x.device)
+        out_channel_offset = 0
+    if out.shape[:3] != (N, Ho, Wo) or out_channel_offset + Cout > out.shape[3]:
+        raise ValueError(f"conv2d_direct: out {tuple(out.shape)} cannot hold [{N},{Ho},{Wo},{Cout}]")
+    if es == 1 and chan_scale is None:
+        raise ValueError("conv2d_direct: fp8 input needs chan_scale")
+    _check(x, "x", x.dtype, x.device)
+    _check(w_arr, "w", torch.uint8, x.device)
+    _check(bias, "bias", torch.float32, x.device)
+    _hip().dconv(x.data_ptr(), w_arr.data_ptr(), _ptr(chan_scale), bias.data_ptr(), out.data_ptr(), es, N, H, W, Cin,
+                 Cout, KH, KW, s, pt, pl, Ho, Wo, w_arr.shape[1], out.shape[3], out_channel_offset, int(out_fp8),
+                 1.0 / out_scale if out_fp8 else 1.0, act_code(act), bn, _stream())
     return out

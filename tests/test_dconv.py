@@ -1,0 +1,85 @@
+"""Direct (LDS-resident) convolution kernel for narrow layers vs the fp32 references:
+bf16 and fp8 inputs, stride 1/2, asymmetric padding, bf16/e4m3 outputs, concat slices."""
+import pytest
+import torch
+
+from flink_tensorflow_amd.ops import fp8 as Q
+from flink_tensorflow_amd.ops import kernels as K
+
+DEV = torch.device("cuda", 0)
+
+
+def test_dconv_eligibility_host():
+    assert K.dconv_eligible(8, 3, 3, (2, 2), (1, 1), 2)
+    assert K.dconv_eligible(32, 3, 3, (1, 1), (1, 1), 1)
+    assert not K.dconv_eligible(48, 5, 5, (1, 1), (1, 1), 1)  # 48 B is not a 32-B lane segment multiple
+    assert not K.dconv_eligible(64, 1, 1, (1, 1), (1, 1), 2)  # pointwise stays on the GEMM path
+    w = torch.randn(40, 3, 3, 8)
+    arr = K.dconv_bf16_weight_bytes(w, 32)
+    assert arr.shape == (64, 9 * 8 * 2 + (64 - 144 % 64) % 64 + 16)
+
+
+BF16_CASES = [  # N, H, W, Cin, Cout, (kh, kw), stride, pad, bn, out_fp8
+    (2, 31, 31, 8, 32, (3, 3), 2, (0, 0, 0, 0), 32, False),
+    (2, 31, 31, 8, 32, (3, 3), 2, (0, 0, 0, 0), 32, True),
+    (2, 28, 28, 16, 64, (4, 4), 1, (1, 2, 1, 2), 64, False),
+    (2, 19, 21, 64, 64, (3, 3), 1, (1, 1, 1, 1), 32, False),
+    (1, 9, 40, 32, 48, (1, 7), 1, (0, 0, 3, 3), 64, False),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", BF16_CASES)
+def test_dconv_bf16_gpu(case):
+    N, H, W, Cin, Cout, (kh, kw), s, pad, bn, out_fp8 = case
+    torch.manual_seed(hash(case) % 1000)
+    x = torch.randn(N, H, W, Cin).to(torch.bfloat16)
+    w = (torch.randn(Cout, kh, kw, Cin) / (kh * kw * Cin) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout) * 0.1
+    so = 0.01 if out_fp8 else None
+    ref = K.conv2d_nhwc(x, w, b, None, (s, s), pad, (1, 1), "relu", out_scale=so)
+    arr = K.dconv_bf16_weight_bytes(w.float(), bn).to(DEV)
+    got = K.conv2d_direct(x.to(DEV), arr, (kh, kw), Cout, b.to(DEV), (s, s), pad, "relu", bn=bn, out_scale=so).cpu()
+    if out_fp8:
+        gd, rd = Q.from_fp8_bytes(got), Q.from_fp8_bytes(ref)
+        assert ((gd - rd).abs() <= 0.13 * rd.abs() + 1e-3).all()
+    else:
+        torch.testing.assert_close(got.float(), ref.float(), rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+
+
+FP8_CASES = [  # N, H, W, Cin, Cout, k, stride, pad, bn, offset, extra
+    (2, 23, 23, 32, 32, 3, 1, (0, 0, 0, 0), 32, 0, 0),
+    (2, 20, 17, 32, 64, 3, 1, (1, 1, 1, 1), 64, 0, 0),
+    (2, 35, 35, 64, 96, 3, 1, (1, 1, 1, 1), 32, 32, 64),
+    (2, 35, 35, 96, 96, 3, 1, (1, 1, 1, 1), 64, 0, 0),
+    (2, 17, 17, 128, 128, (1, 7), 1, (0, 0, 3, 3), 64, 0, 0),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", FP8_CASES)
+def test_dconv_fp8_gpu(case):
+    N, H, W, Cin, Cout, k, s, pad, bn, off, extra = case
+    kh, kw = (k, k) if isinstance(k, int) else k
+    torch.manual_seed(Cin * 7 + Cout + kh)
+    x = torch.randn(N, H, W, Cin).relu()
+    sx = Q.scale_for(x.max())
+    xq = Q.quantize(x, sx)
+    wq, ws = Q.quantize_weight(torch.randn(Cout, kh, kw, Cin) / (kh * kw * Cin) ** 0.5)
+    b = torch.randn(Cout) * 0.1
+    so = 0.02
+    ref = Q.conv2d_nhwc_fp8(xq, sx, wq, (kh, kw), ws, b, (s, s), pad, act="relu", out_scale=so)
+    Ho, Wo = ref.shape[1:3]
+    out = torch.zeros((N, Ho, Wo, Cout + extra), dtype=torch.uint8, device=DEV)
+    arr = K.dconv_weights(wq, Cout, 1, bn).to(DEV)
+    K.conv2d_direct(xq.to(DEV), arr, (kh, kw), Cout, b.to(DEV), (s, s), pad, "relu", out=out, out_channel_offset=off,
+                    bn=bn, chan_scale=(ws * sx).to(DEV), out_scale=so)
+    got = out[..., off:off + Cout].cpu()
+    gd, rd = Q.from_fp8_bytes(got.contiguous()), Q.from_fp8_bytes(ref)
+    # raw e4m3 units: one step (2^-3 relative) of slack for accumulation-order rounding flips;
+    # near zero the subnormal step is 2^-9, so allow a few of those absolutely
+    bad = (gd - rd).abs() > 0.13 * rd.abs() + 0.02
+    assert not bad.any(), (gd[bad][:8], rd[bad][:8])
+    assert (gd == rd).float().mean() > 0.97
+    if extra:
+        assert (out[..., :off] == 0).all() and (out[..., off + Cout:] == 0).all()

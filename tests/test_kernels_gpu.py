@@ -34,9 +34,13 @@ CONV_CASES = [
 ]
 
 
+@pytest.mark.parametrize("cfg", [-1, 16, 17])
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv2d_nhwc(case):
+def test_conv2d_nhwc(case, cfg):
+    """cfg -1: auto register-staged tiles; 16/17: pipelined LDS-DMA kernel (igemm_v2)."""
     N, H, W, Cin, Cout, k, s, pad, act, has_res, has_b = case
+    if cfg >= 16 and act not in ("relu", "none"):
+        pytest.skip("igemm_v2 epilogue: none/relu")
     kh, kw = (k, k) if k != 7 or Cin == 8 else (1, 7)
     if case[5] == 1 and case[6] == 7:  # the 1x7 Inception-style case
         kh, kw, s = 1, 7, 1
@@ -49,7 +53,7 @@ def test_conv2d_nhwc(case):
     r = torch.randn(N, Ho, Wo, Cout, generator=g).to(torch.bfloat16) if has_res else None
     ref = K.conv2d_nhwc(x, w, b, r, (s, s), pad, (1, 1), act)
     got = K.conv2d_nhwc(x.to(DEV), w.to(DEV), b.to(DEV) if b is not None else None,
-                        r.to(DEV) if r is not None else None, (s, s), pad, (1, 1), act)
+                        r.to(DEV) if r is not None else None, (s, s), pad, (1, 1), act, cfg=cfg)
     torch.cuda.synchronize()
     assert got.shape == ref.shape
     _close(got, ref)
@@ -60,17 +64,19 @@ def test_conv_identity_asymmetric():
     N, H, W, C = 1, 4, 4, 64
     x = torch.arange(N * H * W * C, dtype=torch.float32).reshape(N, H, W, C).remainder(7).to(torch.bfloat16)
     w = torch.eye(C).reshape(C, 1, 1, C).to(torch.bfloat16)
-    got = K.conv2d_nhwc(x.to(DEV), w.to(DEV))
-    assert torch.equal(got.cpu(), x)
+    for cfg in (-1, 16, 17):
+        got = K.conv2d_nhwc(x.to(DEV), w.to(DEV), cfg=cfg)
+        assert torch.equal(got.cpu(), x), cfg
 
 
-def test_conv_concat_slice_write():
+@pytest.mark.parametrize("cfg", [-1, 16])
+def test_conv_concat_slice_write(cfg):
     x = torch.randn(2, 8, 8, 64).to(torch.bfloat16).to(DEV)
     w1 = torch.randn(32, 1, 1, 64).to(torch.bfloat16).to(DEV)
     w2 = torch.randn(64, 1, 1, 64).to(torch.bfloat16).to(DEV)
     out = torch.zeros(2, 8, 8, 96, dtype=torch.bfloat16, device=DEV)
-    K.conv2d_nhwc(x, w1, out=out, out_channel_offset=0)
-    K.conv2d_nhwc(x, w2, out=out, out_channel_offset=32)
+    K.conv2d_nhwc(x, w1, out=out, out_channel_offset=0, cfg=cfg)
+    K.conv2d_nhwc(x, w2, out=out, out_channel_offset=32, cfg=cfg)
     ref = torch.cat([K.conv2d_nhwc(x, w1), K.conv2d_nhwc(x, w2)], -1)
     assert torch.equal(out, ref)
 
