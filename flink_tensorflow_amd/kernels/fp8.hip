@@ -364,48 +364,81 @@ __global__ __launch_bounds__(256) void dequantize_kernel(const uint8_t* __restri
   }
 }
 
-// NHWC fp8 pooling, 16 channels per thread; avg divides by the in-bounds count (TF SAME).
-// Output value = pooled input * rq (rq = sx / sy requantises into the destination buffer).
-template <bool MAX>
+// NHWC fp8 pooling, 16 channels x PX adjacent output pixels per thread: the PX outputs
+// share the (PX-1)*sw + kw input columns of each window row, and 2 e4m3 values decode per
+// instruction (v_cvt_pk_f32_fp8) into packed-f32 sums (v_pk_add_f32).  Avg divides by
+// the in-bounds count (TF SAME).  Output = pooled * rq (rq = sx / sy requantises into the
+// destination buffer, e.g. a concat of another scale).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+FTM_DEVICE void decode16(u32x4 v, f32x2* d) {
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    d[2 * w] = __builtin_amdgcn_cvt_pk_f32_fp8((int)v[w], false);
+    d[2 * w + 1] = __builtin_amdgcn_cvt_pk_f32_fp8((int)v[w], true);
+  }
+}
+
+template <bool MAX, int PX>
 __global__ __launch_bounds__(256) void pool_fp8_kernel(const uint8_t* __restrict__ x, uint8_t* __restrict__ y, int N,
                                                        int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh,
                                                        int sw, int ph, int pw, int ldy, int y_coff, float rq) {
   const int cchunks = C / 16;
-  const long total = (long)N * Ho * Wo * cchunks;
+  const int wgroups = (Wo + PX - 1) / PX;
+  const long total = (long)N * Ho * wgroups * cchunks;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
     const int cc = idx % cchunks;
     long t = idx / cchunks;
-    const int ox = t % Wo;
-    t /= Wo;
+    const int oxg = t % wgroups;
+    t /= wgroups;
     const int oy = t % Ho;
     const int n = t / Ho;
-    float acc[16];
+    const int ox0 = oxg * PX;
+    f32x2 acc[PX][8];
+    int cnt_w[PX];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = MAX ? -INFINITY : 0.f;
-    int cnt = 0;
-    const int iy0 = oy * sh - ph, ix0 = ox * sw - pw;
+    for (int p = 0; p < PX; ++p) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[p][e] = MAX ? f32x2{-INFINITY, -INFINITY} : f32x2{0.f, 0.f};
+      const int lo = max((ox0 + p) * sw - pw, 0), hi = min((ox0 + p) * sw - pw + kw, W);
+      cnt_w[p] = max(hi - lo, 0);
+    }
+    int cnt_h = 0;
+    const int iy0 = oy * sh - ph, ixs = ox0 * sw - pw;
+    const int ncols = (PX - 1) * sw + kw;
     for (int dy = 0; dy < kh; ++dy) {
       const int iy = iy0 + dy;
       if ((unsigned)iy >= (unsigned)H) continue;
-      for (int dx = 0; dx < kw; ++dx) {
-        const int ix = ix0 + dx;
+      ++cnt_h;
+      const uint8_t* row = x + ((size_t)n * H + iy) * W * C + cc * 16;
+      for (int c = 0; c < ncols; ++c) {
+        const int ix = ixs + c;
         if ((unsigned)ix >= (unsigned)W) continue;
-        u32x4 v = *reinterpret_cast<const u32x4*>(x + (((size_t)n * H + iy) * W + ix) * C + cc * 16);
+        f32x2 d[8];
+        decode16(*reinterpret_cast<const u32x4*>(row + (size_t)ix * C), d);
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          float f[4];
-          unpack4(v[w], f);
+        for (int p = 0; p < PX; ++p) {
+          const int rel = c - p * sw;  // column inside output p's window?
+          if (rel < 0 || rel >= kw) continue;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[w * 4 + e] = MAX ? fmaxf(acc[w * 4 + e], f[e]) : acc[w * 4 + e] + f[e];
+          for (int e = 0; e < 8; ++e) {
+            if constexpr (MAX) acc[p][e] = f32x2{fmaxf(acc[p][e][0], d[e][0]), fmaxf(acc[p][e][1], d[e][1])};
+            else acc[p][e] += d[e];
+          }
         }
-        ++cnt;
       }
     }
-    const float sc = MAX ? rq : rq / (float)max(cnt, 1);
-    u32x4 o;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) o[w] = pack4(acc[w * 4] * sc, acc[w * 4 + 1] * sc, acc[w * 4 + 2] * sc, acc[w * 4 + 3] * sc);
-    *reinterpret_cast<u32x4*>(y + (((size_t)n * Ho + oy) * Wo + ox) * ldy + y_coff + cc * 16) = o;
+    for (int p = 0; p < PX; ++p) {
+      const int ox = ox0 + p;
+      if (ox >= Wo) break;
+      const float sc = MAX ? rq : rq / (float)max(cnt_h * cnt_w[p], 1);
+      u32x4 o;
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        o[w] = pack4(acc[p][2 * w][0] * sc, acc[p][2 * w][1] * sc, acc[p][2 * w + 1][0] * sc, acc[p][2 * w + 1][1] * sc);
+      *reinterpret_cast<u32x4*>(y + (((size_t)n * Ho + oy) * Wo + ox) * ldy + y_coff + cc * 16) = o;
+    }
   }
 }
 
@@ -537,16 +570,27 @@ void pool2d_nhwc_fp8(uintptr_t x, uintptr_t y, int N, int H, int W, int C, int H
   if (C % 16 || ldy % 16 || y_coff % 16) throw std::invalid_argument("pool2d_nhwc_fp8: C/ldy/y_coff % 16 != 0");
   check_align(x, 16, "x");
   check_align(y, 16, "y");
-  const long work = (long)N * Ho * Wo * (C / 16);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (is_max)
-    hipLaunchKernelGGL(pool_fp8_kernel<true>, dim3(grid_for(work, 256)), dim3(256), 0, s,
-                       reinterpret_cast<const uint8_t*>(x), reinterpret_cast<uint8_t*>(y), N, H, W, C, Ho, Wo, kh, kw,
-                       sh, sw, ph, pw, ldy, y_coff, rq);
-  else
-    hipLaunchKernelGGL(pool_fp8_kernel<false>, dim3(grid_for(work, 256)), dim3(256), 0, s,
-                       reinterpret_cast<const uint8_t*>(x), reinterpret_cast<uint8_t*>(y), N, H, W, C, Ho, Wo, kh, kw,
-                       sh, sw, ph, pw, ldy, y_coff, rq);
+  auto X = reinterpret_cast<const uint8_t*>(x);
+  auto Y = reinterpret_cast<uint8_t*>(y);
+  // stride-1 windows: 2 outputs per thread share window columns; strided: 1
+  if (sw == 1) {
+    const long work = (long)N * Ho * ((Wo + 1) / 2) * (C / 16);
+    if (is_max)
+      hipLaunchKernelGGL((pool_fp8_kernel<true, 2>), dim3(grid_for(work, 256)), dim3(256), 0, s, X, Y, N, H, W, C, Ho,
+                         Wo, kh, kw, sh, sw, ph, pw, ldy, y_coff, rq);
+    else
+      hipLaunchKernelGGL((pool_fp8_kernel<false, 2>), dim3(grid_for(work, 256)), dim3(256), 0, s, X, Y, N, H, W, C, Ho,
+                         Wo, kh, kw, sh, sw, ph, pw, ldy, y_coff, rq);
+  } else {
+    const long work = (long)N * Ho * Wo * (C / 16);
+    if (is_max)
+      hipLaunchKernelGGL((pool_fp8_kernel<true, 1>), dim3(grid_for(work, 256)), dim3(256), 0, s, X, Y, N, H, W, C, Ho,
+                         Wo, kh, kw, sh, sw, ph, pw, ldy, y_coff, rq);
+    else
+      hipLaunchKernelGGL((pool_fp8_kernel<false, 1>), dim3(grid_for(work, 256)), dim3(256), 0, s, X, Y, N, H, W, C, Ho,
+                         Wo, kh, kw, sh, sw, ph, pw, ldy, y_coff, rq);
+  }
   FTM_CHECK_LAUNCH();
 }
 
