@@ -85,6 +85,31 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
     return lib
 
 
+SANITIZERS = {
+    "asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
+    "tsan": ["-fsanitize=thread", "-fno-omit-frame-pointer"],
+}
+
+
+def build_native_sanitized(kind: str, out_dir: str | os.PathLike) -> Path:
+    """Host runtime built with a sanitizer (``asan`` = AddressSanitizer + UBSan, ``tsan`` =
+    ThreadSanitizer) into ``out_dir`` — never over the production library.  Load it in a
+    child process with the matching runtime preloaded (``LD_PRELOAD``) and
+    ``FTM_NATIVE_LIB`` pointing at it (``tests/test_sanitizers.py``)."""
+    srcs = sorted(CSRC.glob("*.cpp"))
+    flags = ["-O1", "-g", "-std=c++17", "-shared", "-fPIC", "-msse4.2", "-pthread", *SANITIZERS[kind]]
+    out = Path(out_dir) / f"_native{EXT_SUFFIX}"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    _run([os.environ.get("CXX", "g++"), *flags, *_pybind_includes(), *map(str, srcs), "-o", str(out)])
+    return out
+
+
+def sanitizer_runtime(kind: str) -> str:
+    lib = {"asan": "libasan.so", "tsan": "libtsan.so"}[kind]
+    cxx = os.environ.get("CXX", "g++")
+    return subprocess.run([cxx, f"-print-file-name={lib}"], stdout=subprocess.PIPE, text=True).stdout.strip()
+
+
 def hip_flags() -> list[str]:
     return [
         f"--offload-arch={HIP_ARCH}",

@@ -10,6 +10,7 @@ Policy (see README "native code"):
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 import threading
 
@@ -27,6 +28,12 @@ def native(required: bool = True):
     with _lock:
         if _native_mod is None:
             try:
+                override = os.environ.get("FTM_NATIVE_LIB")  # e.g. a sanitizer build
+                if override:
+                    spec = importlib.util.spec_from_file_location("flink_tensorflow_amd._native", override)
+                    _native_mod = importlib.util.module_from_spec(spec)
+                    spec.loader.exec_module(_native_mod)
+                    return _native_mod
                 if os.environ.get("FTM_NO_AUTOBUILD") != "1":
                     _build.build_native()
                 _native_mod = importlib.import_module("flink_tensorflow_amd._native")

@@ -25,6 +25,8 @@ from typing import Any, Callable, Sequence
 import numpy as np
 import torch
 
+from ..utils.tracing import trace_range
+
 from .. import _ext
 
 
@@ -103,20 +105,24 @@ class PipelinedGpuRunner:
         if slot.busy:
             finished.append(self._harvest(slot))
         # host gather into the pinned slot (zero padding rows only when needed)
-        self._native.gather_into(slot.pinned_in.data_ptr(), slot.pinned_in.numel() * slot.pinned_in.element_size(),
-                                 list(payloads), self.record_bytes, self.gather_threads)
-        if n < b:
-            slot.pinned_in[n:].zero_()
+        with trace_range(f"gather[{n}/{b}]"):
+            self._native.gather_into(slot.pinned_in.data_ptr(),
+                                     slot.pinned_in.numel() * slot.pinned_in.element_size(), list(payloads),
+                                     self.record_bytes, self.gather_threads)
+            if n < b:
+                slot.pinned_in[n:].zero_()
         plan = self.plans[b]
-        with torch.cuda.stream(self.copy_stream):
+        with trace_range("h2d"), torch.cuda.stream(self.copy_stream):
             slot.dev_in.copy_(slot.pinned_in, non_blocking=True)
             slot.h2d.record(self.copy_stream)
         with torch.cuda.stream(self.compute_stream):
             self.compute_stream.wait_event(slot.h2d)
-            plan.input_buffer(self.feed).copy_(slot.dev_in, non_blocking=True)
-            plan.replay()
-            for dst, src in zip(slot.pinned_out, self.fetch_bufs(plan)):
-                dst.copy_(src, non_blocking=True)
+            with trace_range(f"forward[{b}]"):
+                plan.input_buffer(self.feed).copy_(slot.dev_in, non_blocking=True)
+                plan.replay()
+            with trace_range("d2h"):
+                for dst, src in zip(slot.pinned_out, self.fetch_bufs(plan)):
+                    dst.copy_(src, non_blocking=True)
             slot.done.record(self.compute_stream)
         slot.busy = True
         slot.n = n

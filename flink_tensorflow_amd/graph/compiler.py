@@ -47,6 +47,7 @@ from ..ops import kernels as K
 from ..types.dtypes import DataType
 from ..types.names import TensorName
 from ..types.tensor import StringTensor
+from ..utils import tracing
 from . import ops_core  # noqa: F401
 from .graph import Graph, Node
 from .op_registry import OpContext, lookup
@@ -125,6 +126,10 @@ class CompiledFunction:
         self._graph_obj: torch.cuda.CUDAGraph | None = None
         self._amax: dict[str, float] = {}
         self.fp8_layers = 0
+        self._debug_sync = tracing.debug_sync()
+        self._poison_after: dict[int, list] = {}
+        if self._debug_sync or tracing.debug_poison():
+            use_graph = False  # debug modes act between launches: run the plan eagerly
         import contextlib
 
         if precision == "fp8":  # calibrate activation ranges on a bf16 twin of the plan
@@ -939,6 +944,7 @@ class CompiledFunction:
                         and not any(v is self.vals.get((TensorName.parse(f).name, TensorName.parse(f).index))
                                     for f in self.feed_names):
                     self._free(v.buf)
+                    self._poison_after.setdefault(i, []).append(v.buf)
         for v in self.vals.values():
             if v.alias_of is not None:
                 r = _root(v)
@@ -967,8 +973,54 @@ class CompiledFunction:
 
     # ================================================================== execution
     def _run_steps(self):
-        for s in self.steps:
+        if not (self._debug_sync or self._poison_after and tracing.debug_poison()):
+            for s in self.steps:
+                s.fn()
+            return
+        poison = tracing.debug_poison()
+        for i, s in enumerate(self.steps):
             s.fn()
+            if self._debug_sync and self.device.type == "cuda":
+                try:
+                    torch.cuda.synchronize(self.device)
+                except RuntimeError as e:
+                    raise RuntimeError(f"step {i} ({s.kind} {s.name}) failed: {e}") from e
+            if poison:
+                for b in self._poison_after.get(i, ()):
+                    b.view(-1).view(torch.uint8).fill_(0xFF)  # NaN in bf16/fp32, 0xFF in e4m3 = NaN
+
+    def profile(self, feeds: dict | None = None):
+        """One eager run with a HIP event pair around every launch: a ``RunMetadata``
+        whose ``NodeExecStats`` carry the per-step device time (``timeline_label`` = kind)
+        — the compiled counterpart of ``Session.run(run_metadata=True)``."""
+        from ..proto.messages import DeviceStepStats, NodeExecStats, RunMetadata, StepStats
+
+        for k, v in (feeds or {}).items():
+            self.input_buffer(k).copy_(v)
+        stats = []
+        if self.device.type == "cuda":
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in self.steps]
+            for s, (e0, e1) in zip(self.steps, evs):
+                e0.record()
+                s.fn()
+                e1.record()
+            torch.cuda.synchronize(self.device)
+            times = [e0.elapsed_time(e1) * 1e3 for e0, e1 in evs]
+        else:
+            import time
+
+            times = []
+            for s in self.steps:
+                t0 = time.perf_counter()
+                s.fn()
+                times.append((time.perf_counter() - t0) * 1e6)
+        t = 0
+        for s, us in zip(self.steps, times):
+            stats.append(NodeExecStats(node_name=s.name, all_start_micros=int(t), op_end_rel_micros=int(us),
+                                       all_end_rel_micros=int(us), timeline_label=s.kind))
+            t += us
+        return RunMetadata(step_stats=StepStats(dev_stats=[DeviceStepStats(device=str(self.device),
+                                                                           node_stats=stats)]))
 
     def _capture(self):
         s = torch.cuda.Stream(self.device)

@@ -46,6 +46,13 @@ def init_distributed(backend: str | None = None, timeout_s: int = 600) -> bool:
     return True
 
 
+def destroy() -> None:
+    """Tears down the process group (RCCL communicator abort + free on the GPU path), so
+    a restarted worker group can rendezvous afresh."""
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def is_dist() -> bool:
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 

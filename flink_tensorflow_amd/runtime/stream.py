@@ -34,6 +34,14 @@ class ExecutionConfig:
         if t not in self.registered_types:
             self.registered_types.append(t)
 
+    @property
+    def engine(self):
+        """The job's :class:`~flink_tensorflow_amd.config.EngineConfig` (defaults if none)."""
+        from ..config import EngineConfig
+
+        e = self.global_job_parameters.get("engine")
+        return e if e is not None else EngineConfig()
+
 
 def register_types(config: ExecutionConfig) -> None:
     """``RegistrationUtils.registerTypes`` (``LIB/util/RegistrationUtils.java:18-86``):

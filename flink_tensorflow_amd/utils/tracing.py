@@ -1,0 +1,60 @@
+"""Tracing hooks.
+
+* ``trace_range(name)`` — a roctx range (``torch.cuda.nvtx`` is roctx on ROCm) around a
+  pipeline stage (gather, H2D, plan replay, D2H, operator batches), so
+  ``rocprofv3 --kernel-trace --marker-trace`` shows stages next to the kernels.  Enabled
+  by ``FTM_TRACE=1``; otherwise a no-op context manager with no per-call cost beyond a
+  flag check.
+* ``debug_sync()`` / ``debug_poison()`` — the ordering-assertion and use-after-release
+  debug modes of the compiled plans (``FTM_DEBUG_SYNC=1``: run eagerly and synchronize +
+  check the HIP error state after every launch, naming the failing step;
+  ``FTM_DEBUG_POISON=1``: fill every plan buffer with NaN bytes right after its last
+  reader, so a liveness-planning bug reads poison instead of stale-but-plausible data).
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+
+_TRACE = os.environ.get("FTM_TRACE") == "1"
+
+
+def tracing_enabled() -> bool:
+    return _TRACE
+
+
+def set_tracing(on: bool) -> None:
+    global _TRACE
+    _TRACE = bool(on)
+
+
+@contextlib.contextmanager
+def _range(name: str):
+    import torch
+
+    torch.cuda.nvtx.range_push(name)
+    try:
+        yield
+    finally:
+        torch.cuda.nvtx.range_pop()
+
+
+def trace_range(name: str):
+    if not _TRACE:
+        return contextlib.nullcontext()
+    try:
+        import torch
+
+        if not torch.cuda.is_available():
+            return contextlib.nullcontext()
+    except Exception:  # noqa: BLE001
+        return contextlib.nullcontext()
+    return _range(name)
+
+
+def debug_sync() -> bool:
+    return os.environ.get("FTM_DEBUG_SYNC") == "1"
+
+
+def debug_poison() -> bool:
+    return os.environ.get("FTM_DEBUG_POISON") == "1"

@@ -67,3 +67,30 @@ def test_s2d_stem_equivalence():
     got = K.conv2d_nhwc(b, w2, pad=pads)
     assert pads == (1, 2, 1, 2)
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-2)
+
+
+def test_plan_profile_and_debug_modes(monkeypatch):
+    """Compiled-plan RunMetadata (one NodeExecStats per launch) and the eager debug modes:
+    FTM_DEBUG_SYNC checks after each launch, FTM_DEBUG_POISON fills dead buffers with NaN
+    bytes — results must be unchanged when the liveness plan is right."""
+    import torch
+
+    from flink_tensorflow_amd.graph.compiler import CompiledFunction
+    from flink_tensorflow_amd.graph.graph import Graph
+    from flink_tensorflow_amd.models.zoo.resnet import resnet50_graph_def
+
+    g = Graph.from_graph_def(resnet50_graph_def(image_hw=(32, 32), out_hw=(32, 32), depth=26))
+    feeds = {"images:0": ((2, 32, 32, 3), "UINT8")}
+    img = torch.randint(0, 256, (2, 32, 32, 3), dtype=torch.uint8)
+    base = CompiledFunction(g, feeds, ["logits:0"], "cpu", strict=True)
+    ref = base({"images:0": img})[0]
+    md = base.profile({"images:0": img})
+    stats = md.step_stats.dev_stats[0].node_stats
+    assert len(stats) == len(base.steps) and {s.timeline_label for s in stats} >= {"conv", "preprocess"}
+    monkeypatch.setenv("FTM_DEBUG_POISON", "1")
+    monkeypatch.setenv("FTM_DEBUG_SYNC", "1")
+    dbg = CompiledFunction(g, feeds, ["logits:0"], "cpu", strict=True)
+    assert dbg._poison_after  # some buffers die mid-plan
+    out = dbg({"images:0": img})[0]
+    assert torch.isfinite(out).all()
+    torch.testing.assert_close(out, ref)

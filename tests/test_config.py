@@ -1,0 +1,48 @@
+"""EngineConfig: defaults → YAML → FT_* env → CLI precedence, validation, and delivery to
+operators (``open(parameters)`` / ``get_runtime_context().config.engine``)."""
+import pytest
+
+from flink_tensorflow_amd.config import EngineConfig
+from flink_tensorflow_amd.runtime import StreamExecutionEnvironment
+from flink_tensorflow_amd.runtime.functions import RichMapFunction
+
+
+def test_precedence(tmp_path):
+    y = tmp_path / "eng.yaml"
+    y.write_text("parallelism: 2\nmax_batch: 64\nprecision: fp8\nbatch_buckets: [32, 128]\ncustom_knob: 7\n")
+    env = {"FT_MAX_BATCH": "128", "FT_USE_HIP_GRAPH": "false", "FT_CONFIG": str(y)}
+    cfg = EngineConfig.load(["--max-delay-ms", "2.5", "--parallelism", "4"], environ=env)
+    assert cfg.parallelism == 4            # CLI beats YAML
+    assert cfg.max_batch == 128            # env beats YAML
+    assert cfg.precision == "fp8"          # YAML beats default
+    assert cfg.batch_buckets == (32, 128)
+    assert cfg.use_hip_graph is False and cfg.max_delay_ms == 2.5
+    assert cfg.extra["custom_knob"] == 7
+    assert cfg.to_dict()["batch_buckets"] == [32, 128]
+
+
+def test_validation():
+    with pytest.raises(ValueError):
+        EngineConfig().update({"precision": "fp4"})
+    with pytest.raises(ValueError):
+        EngineConfig().update({"parallelism": 0})
+    assert EngineConfig().arena_bytes() == int(288 * 1024 ** 3 * 0.9)
+
+
+class _Probe(RichMapFunction):
+    def open(self, parameters):
+        # Flink-style: open() receives the job configuration; the runtime context has it too
+        assert self.get_runtime_context().config.engine is parameters.engine
+        self.batch = parameters.engine.max_batch
+
+    def map(self, v):
+        return (v, self.batch)
+
+
+def test_operators_see_engine_config(tmp_path):
+    cfg = EngineConfig(parallelism=2, max_batch=17, checkpoint_interval_s=0.05,
+                       checkpoint_dir=str(tmp_path / "chk"), restart_attempts=2)
+    env = cfg.apply(StreamExecutionEnvironment.get_execution_environment())
+    assert env.parallelism == 2 and env.restart_strategy.attempts == 2 and env.checkpoint_interval == 0.05
+    out = env.from_collection(list(range(10))).map(_Probe()).execute_and_collect()
+    assert sorted(out) == [(i, 17) for i in range(10)]

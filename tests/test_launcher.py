@@ -1,0 +1,62 @@
+"""Supervised launcher: a crashed rank and a hung rank are detected, the
+whole group is restarted, and the job resumes from its checkpoint on the next attempt
+(gloo, world size 2, CPU)."""
+import json
+import os
+
+import pytest
+import torch
+
+from flink_tensorflow_amd.parallel.launcher import WorkerFailure, launch
+
+
+def _train(rank, world, attempt, ckpt_dir, fault):
+    """10 'steps' of an all-reduced counter with a checkpoint after every step; the fault
+    fires once, on attempt 0 at step 4 on rank 1."""
+    import torch.distributed as dist
+
+    from flink_tensorflow_amd.parallel.launcher import heartbeat
+
+    path = os.path.join(ckpt_dir, f"rank{rank}.json")
+    step, total = 0, 0.0
+    if os.path.exists(path):
+        with open(path) as f:
+            st = json.load(f)
+        step, total = st["step"], st["total"]
+    resumed_from = step
+    while step < 10:
+        if attempt == 0 and rank == 1 and step == 4:
+            if fault == "crash":
+                os._exit(3)
+            if fault == "hang":
+                import time
+
+                time.sleep(600)
+        t = torch.tensor([float(rank + 1)])
+        dist.all_reduce(t)
+        total += float(t)
+        step += 1
+        with open(path, "w") as f:
+            json.dump({"step": step, "total": total}, f)
+        heartbeat(f"step {step}")
+    return {"total": total, "resumed_from": resumed_from}
+
+
+@pytest.mark.parametrize("fault", ["crash", "hang"])
+def test_restart_after_failure(tmp_path, fault):
+    rep = launch(_train, 2, args=(str(tmp_path), fault), backend="gloo", max_restarts=1, heartbeat_timeout=5.0,
+                 timeout=120)
+    assert rep.attempts == 2 and len(rep.failures) == 1
+    assert ("exited with code 3" in rep.failures[0]) if fault == "crash" else ("missed heartbeats" in rep.failures[0])
+    for r in rep.results:
+        assert r["total"] == 30.0  # 10 steps x (1 + 2), nothing lost or double counted
+        assert r["resumed_from"] >= 4
+
+
+def test_gives_up_after_max_restarts(tmp_path):
+    with pytest.raises(WorkerFailure):
+        launch(_boom, 2, backend="gloo", max_restarts=1, timeout=60)
+
+
+def _boom(rank, world, attempt):
+    raise RuntimeError("boom")
