@@ -88,6 +88,7 @@ class Step:
     fn: Callable[[], None]
     inputs: list = field(default_factory=list)
     outputs: list = field(default_factory=list)
+    meta: dict = field(default_factory=dict)
 
 
 class _ConstSession:
@@ -348,8 +349,8 @@ class CompiledFunction:
     def _new(self, shape, dtype=torch.bfloat16, phys_c=None) -> Val:
         return Val(tuple(int(s) for s in shape), dtype, phys_c=phys_c)
 
-    def _emit(self, name, kind, fn, inputs, outputs):
-        self.steps.append(Step(name, kind, fn, list(inputs), list(outputs)))
+    def _emit(self, name, kind, fn, inputs, outputs, meta=None):
+        self.steps.append(Step(name, kind, fn, list(inputs), list(outputs), dict(meta or {})))
 
     # ------------------------------------------------------------------ lowering
     def _lower(self, node: Node):
@@ -512,14 +513,67 @@ class CompiledFunction:
             self._alias_fused_outputs(absorbed, out)
             return
 
+        pointwise = (KHe, KWe, sh, sw, pt, pb, pl, pr, dh, dw) == (1, 1, 1, 1, 0, 0, 0, 0, 1, 1)
+        if res_val is not None and pointwise and xin_shape_override is None and out.qscale is None \
+                and self._fuse_shortcut(node, xin, out, w_ohwi, bias, res_val, residual[0], act, absorbed, last):
+            return
+
         def run(xin=xin, out=out, res_val=res_val, w_dev=w_dev, b_dev=b_dev):
             K.conv2d_nhwc(xin.buf, w_dev, b_dev, res_val.buf if res_val is not None else None, (sh, sw),
                           (pt, pb, pl, pr), (dh, dw), act, out=_target(out), out_channel_offset=_coff(out),
                           out_scale=_eff_scale(out) if out.qscale is not None else None)
 
-        self._emit(node.name, "conv", run, [xin] + ([res_val] if res_val else []), [out])
+        shortcut_ok = (KHe == KWe == 1 and sh == sw and (pt, pb, pl, pr) == (0, 0, 0, 0) and (dh, dw) == (1, 1)
+                       and res_val is None and act == K.ACT_NONE and out.qscale is None
+                       and xin_shape_override is None and (xin.phys_c or Cin) == Cin)
+        meta = {"shortcut": dict(x=xin, w=w_ohwi, bias=bias, stride=sh, params=[w_dev, b_dev])} if shortcut_ok else None
+        self._emit(node.name, "conv", run, [xin] + ([res_val] if res_val else []), [out], meta)
         self.vals[(last.name, 0)] = out
         self._alias_fused_outputs(absorbed, out)
+
+    def _fuse_shortcut(self, node, xin, out, w_ohwi, bias, res_val, add_node, act, absorbed, last) -> bool:
+        """Pointwise conv whose residual is a 1x1 (strided) projection conv used by nothing
+        else: drop the projection's launch and run both as one K loop
+        (``conv1x1_dual``) — the projection output never round-trips through HBM."""
+        prod = [st for st in self.steps if any(o is res_val for o in st.outputs)]
+        if len(prod) != 1 or "shortcut" not in prod[0].meta or res_val.concat_slot is not None:
+            return False
+        for (n, _), v in self.vals.items():  # the projection feeds only this Add
+            if v is res_val:
+                if any(TensorName.parse(f).name == n for f in self.fetch_names):
+                    return False
+                if any(c != add_node.name and c not in self._fused for c in self.cons.get(n, [])):
+                    return False
+        sc = prod[0].meta["shortcut"]
+        x2 = sc["x"]
+        s2 = sc["stride"]
+        N, Ho, Wo, _ = out.shape
+        if x2.shape[0] != N or (Ho - 1) * s2 >= x2.shape[1] or (Wo - 1) * s2 >= x2.shape[2]:
+            return False
+        Cout, K1 = w_ohwi.shape[0], w_ohwi.shape[3]
+        C2 = sc["w"].shape[3]
+        if K1 % 8 or C2 % 8:
+            return False
+        self.steps.remove(prod[0])
+        for t in sc["params"]:
+            if t is not None:
+                self.params = [q for q in self.params if q is not t]
+        w_cat = torch.cat([w_ohwi.reshape(Cout, K1), sc["w"].reshape(Cout, C2)], 1)
+        b = (bias if bias is not None else torch.zeros(Cout)) + (sc["bias"] if sc["bias"] is not None else 0)
+        w_dev = w_cat.to(self.device, torch.bfloat16).contiguous()
+        b_dev = b.to(self.device, torch.float32).contiguous()
+        self.params += [w_dev, b_dev]
+        for a in absorbed:
+            self._fused.add(a.name)
+
+        def run(xin=xin, x2=x2, out=out, w_dev=w_dev, b_dev=b_dev):
+            K.conv1x1_dual(xin.buf, x2.buf, w_dev, b_dev, s2, act, out=_target(out), out_channel_offset=_coff(out))
+
+        self._emit(node.name, "conv", run, [xin, x2], [out])
+        self.vals[(last.name, 0)] = out
+        self._alias_fused_outputs(absorbed, out)
+        self.fused_shortcuts = getattr(self, "fused_shortcuts", 0) + 1
+        return True
 
     def _use_dconv(self, cin_phys, KH, KW, stride, dil, es, residual, act) -> bool:
         """Direct LDS conv for narrow layers (input row <= 32 B: RGB stems, Inception's
@@ -1080,7 +1134,7 @@ class CompiledFunction:
             kinds[s.kind] = kinds.get(s.kind, 0) + 1
         return {"steps": len(self.steps), "kinds": kinds, "glue_ops": sorted(set(self.glue_ops)),
                 "hip_graph": self._graph_obj is not None, "precision": self.precision,
-                "fp8_layers": self.fp8_layers}
+                "fp8_layers": self.fp8_layers, "fused_shortcuts": getattr(self, "fused_shortcuts", 0)}
 
 
 def _root(v: Val) -> Val:

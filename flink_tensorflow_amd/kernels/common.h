@@ -26,11 +26,13 @@ FTM_DEVICE float apply_act(float x) {
   if constexpr (ACT == ACT_RELU) return x > 0.f ? x : 0.f;
   else if constexpr (ACT == ACT_RELU6) return fminf(fmaxf(x, 0.f), 6.f);
   else if constexpr (ACT == ACT_GELU_TANH) {
+    // 0.5 x (1 + tanh(u)) == x * sigmoid(2u): one v_exp_f32 + one v_rcp_f32 instead of a
+    // libm tanhf (the FFN1 epilogue runs it on every one of B*S*3072 outputs)
     const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-    float u = k0 * (x + k1 * x * x * x);
-    return 0.5f * x * (1.f + tanhf(u));
-  } else if constexpr (ACT == ACT_SIGMOID) return 1.f / (1.f + __expf(-x));
-  else if constexpr (ACT == ACT_TANH) return tanhf(x);
+    const float u2 = 2.f * k0 * (x + k1 * x * x * x);
+    return __fdividef(x, 1.f + __expf(-u2));
+  } else if constexpr (ACT == ACT_SIGMOID) return __fdividef(1.f, 1.f + __expf(-x));
+  else if constexpr (ACT == ACT_TANH) return 2.f * __fdividef(1.f, 1.f + __expf(-2.f * x)) - 1.f;
   else return x;
 }
 

@@ -46,11 +46,16 @@ struct IgemmParams {
   int ldy, y_coff;  // output pixel stride (elements) and channel offset
   int ldr;          // residual pixel stride
   int tiles_m, tiles_n;
+  // DUAL (pointwise GEMM + fused strided 1x1 shortcut): K = K1 + C2; k >= K1 reads the
+  // second source x2 [N, H2, W2, C2] at pixel (n, ho*s2, wo*s2) of output pixel (n, ho, wo)
+  const bf16* x2;
+  int K1, C2, H2, W2, s2;
 };
 
 FTM_DEVICE int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
 
-template <int BM, int BN, int STAGES, bool CONV, int ACT, bool HAS_BIAS, bool HAS_RES>
+template <int BM, int BN, int STAGES, bool CONV, int ACT, bool HAS_BIAS, bool HAS_RES, bool DUAL = false,
+          bool RES_PF = false>
 __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
   constexpr int WAVES_N = BN / 64;
   constexpr int WAVES_M = 4 / WAVES_N;
@@ -84,12 +89,20 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
   const int r0 = tid >> 3;
 
   int xbase[XR], hb[XR], wb[XR];
+  int x2base[DUAL ? XR : 1];
   bool mvalid[XR];
 #pragma unroll
   for (int i = 0; i < XR; ++i) {
     int m = m0 + r0 + 32 * i;
     mvalid[i] = m < p.M;
     int mm = mvalid[i] ? m : 0;
+    if constexpr (DUAL) {
+      const int wo = mm % p.Wo;
+      const int t = mm / p.Wo;
+      const int ho = t % p.Ho;
+      const int n = t / p.Ho;
+      x2base[i] = ((n * p.H2 + ho * p.s2) * p.W2 + wo * p.s2) * p.C2;
+    }
     if constexpr (CONV) {
       int wo = mm % p.Wo;
       int t = mm / p.Wo;
@@ -131,6 +144,14 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
         bool ok = kvalid && mvalid[i] && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
         xr[i] = ok ? *reinterpret_cast<const u32x4*>(p.x + xbase[i] + ((size_t)hi * p.W + wi) * p.Cin + ci) : zero4;
       }
+    } else if constexpr (DUAL) {
+      const bool second = k >= p.K1;  // chunk-uniform: K1 % 8 == 0
+#pragma unroll
+      for (int i = 0; i < XR; ++i) {
+        bool ok = kvalid && mvalid[i];
+        const bf16* src = second ? p.x2 + (size_t)x2base[i] + (k - p.K1) : p.x + (size_t)xbase[i] + k;
+        xr[i] = ok ? *reinterpret_cast<const u32x4*>(src) : zero4;
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < XR; ++i) {
@@ -158,6 +179,25 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // RES_PF: the residual tile is prefetched into registers before the K loop — for the
+  // short-K 1x1 expansion convs (K <= 128) the residual read is otherwise a second exposed
+  // HBM round trip after the MFMAs; for long K the extra 32 VGPRs cost more occupancy
+  // than they hide (bench/conv_tune.py)
+  constexpr int CPR_R = BN / 8;
+  constexpr int RIT = RES_PF ? (BM * CPR_R + NT - 1) / NT : 1;
+  bf16x8 rres[RIT];
+  if constexpr (RES_PF) {
+#pragma unroll
+    for (int it = 0; it < RIT; ++it) {
+      const int q = tid + it * NT;
+      const int m = m0 + q / CPR_R;
+      const int c = n0 + (q % CPR_R) * 8;
+      rres[it] = (q < BM * CPR_R && m < p.M && c < p.Cout)
+                     ? *reinterpret_cast<const bf16x8*>(p.res + (size_t)m * p.ldr + c)
+                     : bf16x8{};
+    }
+  }
 
   const int nk = (p.K + BK - 1) / BK;
   load_tile(0);
@@ -223,15 +263,17 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
   // ---- epilogue phase 2: coalesced 16-B row segments (+ residual, activation)
   constexpr int CPR = BN / 8;  // 16-B chunks per tile row
 #pragma unroll
-  for (int q = tid; q < BM * CPR; q += NT) {
+  for (int it = 0; it < (BM * CPR + NT - 1) / NT; ++it) {
+    const int q = tid + it * NT;
     const int pl = q / CPR;
     const int cc = q % CPR;
     const int m = m0 + pl;
     const int c = n0 + cc * 8;
-    if (m >= p.M || c >= p.Cout) continue;
+    if (q >= BM * CPR || m >= p.M || c >= p.Cout) continue;
     bf16x8 v = *reinterpret_cast<const bf16x8*>(Os + pl * OLD + cc * 8);
     if constexpr (HAS_RES) {
-      bf16x8 r = *reinterpret_cast<const bf16x8*>(p.res + (size_t)m * p.ldr + c);
+      const bf16x8 r = RES_PF ? rres[RES_PF ? it : 0]
+                              : *reinterpret_cast<const bf16x8*>(p.res + (size_t)m * p.ldr + c);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = f2bf(apply_act<ACT>((float)v[e] + (float)r[e]));
     }
@@ -246,8 +288,20 @@ void launch_act(const IgemmParams& p0, hipStream_t s) {
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (p.Cout + BN - 1) / BN;
   dim3 grid(p.tiles_m * p.tiles_n), block(NT);
-  if (p.res) hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, STAGES, CONV, ACT, true, true>), grid, block, 0, s, p);
+  if (p.res && p.K <= 128)
+    hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, STAGES, CONV, ACT, true, true, false, true>), grid, block, 0, s, p);
+  else if (p.res)
+    hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, STAGES, CONV, ACT, true, true>), grid, block, 0, s, p);
   else hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, STAGES, CONV, ACT, true, false>), grid, block, 0, s, p);
+}
+
+template <int BM, int BN, int STAGES, int ACT>
+void launch_dual(const IgemmParams& p0, hipStream_t s) {
+  IgemmParams p = p0;
+  p.tiles_m = (p.M + BM - 1) / BM;
+  p.tiles_n = (p.Cout + BN - 1) / BN;
+  dim3 grid(p.tiles_m * p.tiles_n), block(NT);
+  hipLaunchKernelGGL((igemm_bf16_kernel<BM, BN, STAGES, false, ACT, true, false, true>), grid, block, 0, s, p);
 }
 
 // Tile configurations: 0 = 128x128 double-buffered, 1 = 256x64 double-buffered,
@@ -368,7 +422,57 @@ void gemm_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_
   launch<false>(p, act, cfg, s);
 }
 
+// y = act(x[M, K1] . W[:, :K1]^T + x2_strided[M, C2] . W[:, K1:]^T + bias): a pointwise
+// conv with its 1x1 (optionally strided) projection shortcut fused into the same K loop,
+// so the shortcut's output never round-trips through HBM (ResNet bottleneck unit 1).
+void conv1x1_dual_bf16(uintptr_t x, uintptr_t x2, uintptr_t w, uintptr_t bias, uintptr_t y, int N, int Ho, int Wo,
+                       int K1, int C2, int H2, int W2, int s2, int Cout, int ldy, int y_coff, int act,
+                       uintptr_t stream, int cfg) {
+  if (K1 % 8 || C2 % 8 || Cout % 8 || ldy % 8 || y_coff % 8)
+    throw std::invalid_argument("conv1x1_dual_bf16: channel counts must be multiples of 8");
+  if ((Ho - 1) * s2 >= H2 || (Wo - 1) * s2 >= W2) throw std::invalid_argument("conv1x1_dual_bf16: shortcut geometry");
+  if ((long)N * H2 * W2 * C2 >= (1L << 31) || (long)N * Ho * Wo * K1 >= (1L << 31))
+    throw std::invalid_argument("conv1x1_dual_bf16: tensor too large for 32-bit indexing");
+  require_bias(reinterpret_cast<const float*>(bias));
+  check_align(x, 16, "x");
+  check_align(x2, 16, "x2");
+  check_align(w, 16, "w");
+  check_align(y, 16, "y");
+  check_align(bias, 16, "bias");
+  IgemmParams p{};
+  p.x = reinterpret_cast<const bf16*>(x);
+  p.x2 = reinterpret_cast<const bf16*>(x2);
+  p.w = reinterpret_cast<const bf16*>(w);
+  p.bias = reinterpret_cast<const float*>(bias);
+  p.y = reinterpret_cast<bf16*>(y);
+  p.N = N; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout;
+  p.M = N * Ho * Wo;
+  p.K1 = K1; p.C2 = C2; p.H2 = H2; p.W2 = W2; p.s2 = s2;
+  p.K = K1 + C2;
+  p.ldx = K1;
+  p.ldy = ldy; p.y_coff = y_coff;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (cfg < 0) cfg = Cout <= 64 ? 3 : 2;
+  if (act != ACT_RELU && act != ACT_NONE) throw std::invalid_argument("conv1x1_dual_bf16: act must be none/relu");
+#define FTM_DUAL(BM_, BN_, ST_)                                                    \
+  do {                                                                             \
+    if (act == ACT_RELU) launch_dual<BM_, BN_, ST_, ACT_RELU>(p, s);               \
+    else launch_dual<BM_, BN_, ST_, ACT_NONE>(p, s);                               \
+  } while (0)
+  switch (cfg) {
+    case 0: FTM_DUAL(128, 128, 2); break;
+    case 1: FTM_DUAL(256, 64, 2); break;
+    case 2: FTM_DUAL(128, 128, 1); break;
+    case 3: FTM_DUAL(256, 64, 1); break;
+    case 4: FTM_DUAL(64, 128, 2); break;
+    default: throw std::invalid_argument("conv1x1_dual_bf16: unknown config");
+  }
+#undef FTM_DUAL
+  FTM_CHECK_LAUNCH();
+}
+
 void register_igemm(pybind11::module_& m) {
+  m.def("conv1x1_dual_bf16", &conv1x1_dual_bf16);
   m.def("conv2d_nhwc_bf16", &conv2d_nhwc_bf16);
   m.def("gemm_bf16", &gemm_bf16);
   m.attr("igemm_num_configs") = NCFG;

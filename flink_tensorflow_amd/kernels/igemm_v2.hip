@@ -330,7 +330,13 @@ void launch_act(const V2Params& p, int act, hipStream_t s) {
   switch (act) {
     case ACT_NONE: launch_res<ES, BN, CONV, OUT_FP8, ACT_NONE>(p, s); break;
     case ACT_RELU: launch_res<ES, BN, CONV, OUT_FP8, ACT_RELU>(p, s); break;
-    default: throw std::invalid_argument("igemm_v2: activation must be none/relu");
+    case ACT_GELU_TANH:
+      if constexpr (!CONV && ES == 2 && !OUT_FP8) {  // transformer FFN GEMMs
+        launch_res<ES, BN, CONV, OUT_FP8, ACT_GELU_TANH>(p, s);
+        break;
+      }
+      [[fallthrough]];
+    default: throw std::invalid_argument("igemm_v2: activation must be none/relu (gelu: bf16 GEMM only)");
   }
 }
 

@@ -194,6 +194,10 @@ def gemm(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = None, 
             bias = _zeros_bias(N, x.device)
         if residual is not None:
             _check(residual, "residual", device=x.device)
+        if cfg in V2_CONFIGS:  # pipelined LDS-DMA kernel, GEMM mode (1x1 "conv" over M rows)
+            _hip().igemm_v2(x2.data_ptr(), w_nk.data_ptr(), 0, bias.data_ptr(), _ptr(residual), out2.data_ptr(), 2, 1,
+                            M, 1, K, N, 1, 1, 1, 1, 0, 0, 1, 1, M, 1, N, 0, N, 0, 1.0, a, V2_CONFIGS[cfg], _stream())
+            return out
         _hip().gemm_bf16(x2.data_ptr(), w_nk.data_ptr(), bias.data_ptr(), _ptr(residual), out2.data_ptr(), M, N, K, K,
                          N, N, a, _stream(), cfg)
         return out
@@ -489,4 +493,32 @@ def conv2d_direct(x: torch.Tensor, w_arr: torch.Tensor, kshape, Cout: int, bias:
     _hip().dconv(x.data_ptr(), w_arr.data_ptr(), _ptr(chan_scale), bias.data_ptr(), out.data_ptr(), es, N, H, W, Cin,
                  Cout, KH, KW, s, pt, pl, Ho, Wo, w_arr.shape[1], out.shape[3], out_channel_offset, int(out_fp8),
                  1.0 / out_scale if out_fp8 else 1.0, act_code(act), bn, _stream())
+    return out
+
+
+# ------------------------------------------------------------------------------ fused shortcut
+def conv1x1_dual(x: torch.Tensor, x2: torch.Tensor, w_cat: torch.Tensor, bias: torch.Tensor, stride2: int = 1,
+                 act=None, out: torch.Tensor | None = None, out_channel_offset: int = 0, cfg: int = -1) -> torch.Tensor:
+    """``act(conv1x1(x, W[:, :K1]) + conv1x1_stride(x2, W[:, K1:]) + bias)`` in ONE K loop —
+    a bottleneck's expansion conv with its projection shortcut fused (the shortcut output
+    never touches HBM).  ``x`` [N,Ho,Wo,K1], ``x2`` [N,H2,W2,C2], ``w_cat`` [Cout, K1+C2]."""
+    N, Ho, Wo, K1 = x.shape
+    _, H2, W2, C2 = x2.shape
+    Cout = w_cat.shape[0]
+    if w_cat.shape[1] != K1 + C2:
+        raise ValueError(f"conv1x1_dual: weights K {w_cat.shape[1]} != {K1} + {C2}")
+    if out is None:
+        out = torch.empty((N, Ho, Wo, Cout), dtype=x.dtype if x.is_cuda else torch.float32, device=x.device)
+        out_channel_offset = 0
+    a = act_code(act)
+    if x.is_cuda:
+        for t, n in ((x, "x"), (x2, "x2"), (w_cat, "w"), (out, "out")):
+            _check(t, n, device=x.device)
+        _check(bias, "bias", torch.float32, x.device)
+        _hip().conv1x1_dual_bf16(x.data_ptr(), x2.data_ptr(), w_cat.data_ptr(), bias.data_ptr(), out.data_ptr(), N, Ho,
+                                 Wo, K1, C2, H2, W2, stride2, Cout, out.shape[3], out_channel_offset, a, _stream(), cfg)
+        return out
+    xs = x2[:, ::stride2, ::stride2, :][:, :Ho, :Wo, :]
+    y = x.float() @ w_cat[:, :K1].float().t() + xs.float() @ w_cat[:, K1:].float().t() + bias.float()
+    out[..., out_channel_offset:out_channel_offset + Cout] = _apply_act_ref(y, a).to(out.dtype)
     return out

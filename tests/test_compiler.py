@@ -18,7 +18,9 @@ def _check_plan(graph, device, imgs):
     plan = CompiledFunction(graph, {"images:0": (tuple(imgs.shape), "UINT8")}, ["logits:0", "top_k:1"], device,
                             strict=True)
     s = plan.summary()
-    assert s["glue_ops"] == [] and s["kinds"]["conv"] == 29 and s["kinds"]["preprocess"] == 1
+    # 29 convs, the 4 projection shortcuts fused into their unit's expansion conv
+    assert s["glue_ops"] == [] and s["kinds"]["conv"] == 25 and s["fused_shortcuts"] == 4
+    assert s["kinds"]["preprocess"] == 1
     logits, idx = plan({"images:0": imgs.to(device)})
     err = (logits.cpu() - ref[0]).abs().max().item() / ref[0].abs().max().item()
     assert err < 0.05, err

@@ -166,3 +166,21 @@ def test_preprocess_s2d():
     ref = K.preprocess_images(img, (224, 224), s2d=True)
     got = K.preprocess_images(img.to(DEV), (224, 224), s2d=True)
     _close(got, ref, rtol=1e-2, atol_scale=1e-2)
+
+
+@pytest.mark.parametrize("stride2,cfg", [(1, -1), (2, -1), (2, 0), (1, 3)])
+def test_conv1x1_dual(stride2, cfg):
+    """Expansion conv + fused (strided) projection shortcut vs the two-conv reference."""
+    g = torch.Generator().manual_seed(11 + stride2)
+    N, Ho, Wo, K1, C2, Cout = 2, 14, 14, 64, 96, 256
+    x = torch.randn(N, Ho, Wo, K1, generator=g).to(torch.bfloat16)
+    x2 = torch.randn(N, Ho * stride2, Wo * stride2, C2, generator=g).to(torch.bfloat16)
+    w = (torch.randn(Cout, K1 + C2, generator=g) / 12).to(torch.bfloat16)
+    b = torch.randn(Cout, generator=g)
+    ref = K.conv1x1_dual(x, x2, w, b, stride2, "relu")
+    two = K.conv2d_nhwc(x, w[:, :K1].reshape(Cout, 1, 1, K1), b,
+                        K.conv2d_nhwc(x2, w[:, K1:].reshape(Cout, 1, 1, C2), None, None, (stride2, stride2)),
+                        act="relu")
+    torch.testing.assert_close(ref, two, rtol=1e-2, atol=1e-2)
+    got = K.conv1x1_dual(x.to(DEV), x2.to(DEV), w.to(DEV), b.to(DEV), stride2, "relu", cfg=cfg)
+    _close(got, ref)
