@@ -32,7 +32,9 @@ __device__ __attribute__((aligned(16))) uint32_t g_zero16[4];  // zero page for 
 
 constexpr int BM = 256;
 constexpr int ROWB = 128;  // LDS row bytes = one K tile of one row
-constexpr int NS = 3;      // LDS ring stages
+// LDS ring stages: 3 (two tiles in flight) for BN <= 128; the 256 x 256 tile fits only 2
+template <int BN>
+constexpr int stages() { return BN >= 256 ? 2 : 3; }
 constexpr int NT = 512;
 
 struct V2Params {
@@ -77,6 +79,7 @@ template <int ES, int BN, bool CONV, bool OUT_FP8, int ACT, bool HAS_RES, int AB
 __global__ __launch_bounds__(NT, 1) void igemm_v2_kernel(V2Params p) {
   constexpr int EPC = 16 / ES;          // elements per 16-B chunk
   constexpr int BKE = ROWB / ES;        // K elements per tile
+  constexpr int NS = stages<BN>();
   constexpr int WAVES_N = BN / 64;
   constexpr int WAVES_M = 8 / WAVES_N;
   constexpr int TM = BM / WAVES_M;      // pixels per wave
@@ -87,8 +90,9 @@ __global__ __launch_bounds__(NT, 1) void igemm_v2_kernel(V2Params p) {
   constexpr int STAGE = (BM + BN) * ROWB;
   constexpr int OB = OUT_FP8 ? 1 : 2;
   constexpr int OLD = BN * OB + 16;     // epilogue LDS row pitch (bytes)
-  static_assert(BM * OLD <= NS * STAGE, "epilogue tile must fit the ring");
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[NS * STAGE];
+  constexpr int LDS_BYTES = BM * OLD > NS * STAGE ? BM * OLD : NS * STAGE;  // ring, reused by the epilogue
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[LDS_BYTES];
 
   const int nwg = p.tiles_m * p.tiles_n;
   const int tile = xcd_remap(blockIdx.x, nwg);
@@ -180,12 +184,13 @@ __global__ __launch_bounds__(NT, 1) void igemm_v2_kernel(V2Params p) {
   const int fq = lane >> 4;
   const int nk = (p.K + BKE - 1) / BKE;
 
+  constexpr int PD = NS - 1;  // prefetch distance (tiles)
   issue(0, 0);
-  if (nk > 1) issue(1, 1);
+  if (PD > 1 && nk > 1) issue(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) wait_then_barrier<GL>();  // tile kt+1 may stay in flight
+    if (PD > 1 && kt + 1 < nk) wait_then_barrier<GL>();  // tile kt+1 may stay in flight
     else wait_then_barrier<0>();
-    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % NS);
+    if (kt + PD < nk) issue(kt + PD, (kt + PD) % NS);
     const uint8_t* xs = smem + (kt % NS) * STAGE;
     const uint8_t* ws = xs + BM * ROWB;
     if constexpr (ES == 2) {
@@ -342,7 +347,14 @@ void launch_act(const V2Params& p, int act, hipStream_t s) {
 
 template <int ES, bool CONV>
 void launch_v2(const V2Params& p, int bn, bool out_fp8, int act, hipStream_t s) {
-  if (bn == 128) {
+  if (bn == 256) {
+    if constexpr (!CONV) {  // large plain GEMMs (transformer projections / FFN)
+      if (out_fp8) launch_act<ES, 256, CONV, true>(p, act, s);
+      else launch_act<ES, 256, CONV, false>(p, act, s);
+    } else {
+      throw std::invalid_argument("igemm_v2: bn 256 is a GEMM-mode tile");
+    }
+  } else if (bn == 128) {
     if (out_fp8) launch_act<ES, 128, CONV, true>(p, act, s);
     else launch_act<ES, 128, CONV, false>(p, act, s);
   } else {
@@ -370,7 +382,7 @@ void igemm_v2(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr
   if (Cin % epc) throw std::invalid_argument("igemm_v2: Cin must be a multiple of " + std::to_string(epc));
   if (Cout % oe || ldy % oe || y_coff % oe) throw std::invalid_argument("igemm_v2: Cout/ldy/y_coff alignment");
   if (Cout % 4) throw std::invalid_argument("igemm_v2: Cout % 4 != 0");
-  if (bn != 64 && bn != 128) throw std::invalid_argument("igemm_v2: bn must be 64 or 128");
+  if (bn != 64 && bn != 128 && bn != 256) throw std::invalid_argument("igemm_v2: bn must be 64, 128 or 256");
   if (res && (es != 2 || out_fp8 || ldr % 8)) throw std::invalid_argument("igemm_v2: bad residual");
   if (N <= 0 || Ho <= 0 || Wo <= 0 || Cout <= 0) throw std::invalid_argument("igemm_v2: empty problem");
   if ((long)N * H * W * Cin >= (1L << 31) || (long)N * Ho * Wo >= (1L << 31))

@@ -160,6 +160,9 @@ class BertDeviceWeights:
                 "f_w": mat(host[p + "output/dense/kernel"]), "f_b": vec(host[p + "output/dense/bias"]),
                 "ln2_g": vec(host[p + "output/LayerNorm/gamma"]), "ln2_b": vec(host[p + "output/LayerNorm/beta"]),
             })
+            Ld = self.layers[-1]
+            for k in ("qkv", "o", "i", "f"):  # library-GEMM epilogue biases in the matrix dtype
+                Ld[k + "_b16"] = Ld[k + "_b"].to(bf)
         self.pool_w = mat(host["bert/pooler/dense/kernel"])
         self.pool_b = vec(host["bert/pooler/dense/bias"])
         nl = cfg.num_labels
@@ -179,11 +182,24 @@ class BertDeviceWeights:
 
 
 class BertEncoderPlan:
-    """Preallocated buffers + launch sequence for one (batch, seq); hipGraph-captured."""
+    """Preallocated buffers + launch sequence for one (batch, seq); hipGraph-captured.
 
-    def __init__(self, w: BertDeviceWeights, batch: int, seq: int, use_graph: bool = True):
+    ``gemm="mfma"`` runs the four projections per layer on the hand-written MFMA GEMM with
+    fused bias / GELU / residual epilogues.  ``gemm="blas"`` (default on the GPU) runs them
+    as plain library GEMMs (hipBLASLt via ``torch.addmm``; bias, or bias+GELU, epilogue),
+    which measure 1.2-1.5x faster on the 32768 x {768..3072} x {768, 3072} shapes
+    (``bench/probe_hipblaslt.py`` vs ``bench/gemm_tune.py``); the residual adds then move
+    into the fused residual+LayerNorm kernel.  Embedding+LN, attention, residual+LN and
+    the pooler/classifier stay on the hand-written kernels either way."""
+
+    def __init__(self, w: BertDeviceWeights, batch: int, seq: int, use_graph: bool = True, gemm: str | None = None):
         cfg = w.cfg
         self.w, self.B, self.S = w, batch, seq
+        if gemm is None:
+            gemm = "blas" if w.word.device.type == "cuda" else "mfma"
+        if gemm not in ("blas", "mfma"):
+            raise ValueError("gemm must be 'blas' or 'mfma'")
+        self.gemm_impl = gemm
         d = w.word.device
         dt = w.word.dtype
         T = batch * seq
@@ -193,6 +209,7 @@ class BertEncoderPlan:
         self.y = torch.empty(T, h, dtype=dt, device=d)
         self.qkv = torch.empty(T, 3 * h, dtype=dt, device=d)
         self.ctx = torch.empty(T, h, dtype=dt, device=d)
+        self.x2 = torch.empty(T, h, dtype=dt, device=d)
         self.ffn = torch.empty(T, cfg.intermediate, dtype=dt, device=d)
         self.cls_in = torch.empty(batch, h, dtype=dt, device=d)
         self.pooled = torch.empty(batch, h, dtype=dt, device=d)
@@ -204,6 +221,8 @@ class BertEncoderPlan:
     def _run(self):
         w, cfg, B, S = self.w, self.w.cfg, self.B, self.S
         K.embed_layernorm(self.ids, None, w.word, w.pos, w.type, w.emb_g, w.emb_b, S, cfg.eps, out=self.x)
+        if self.gemm_impl == "blas":
+            return self._run_blas()
         for L in w.layers:
             K.gemm(self.x, L["qkv_w"], L["qkv_b"], out=self.qkv)
             K.attention(self.qkv, self.ids, B, S, cfg.heads, out=self.ctx)
@@ -212,6 +231,20 @@ class BertEncoderPlan:
             K.gemm(self.x, L["i_w"], L["i_b"], act="gelu", out=self.ffn)
             K.gemm(self.ffn, L["f_w"], L["f_b"], residual=self.x, out=self.y)
             K.layernorm(self.y, L["ln2_g"], L["ln2_b"], eps=cfg.eps, out=self.x)
+        self.cls_in.copy_(self.x.view(B, S, -1)[:, 0])
+        K.gemm(self.cls_in, w.pool_w, w.pool_b, act="tanh", out=self.pooled)
+        K.gemm(self.pooled, w.cls_w, w.cls_b, out=self.logits)
+
+    def _run_blas(self):
+        w, cfg, B, S = self.w, self.w.cfg, self.B, self.S
+        for L in w.layers:
+            torch.addmm(L["qkv_b16"], self.x, L["qkv_w"].t(), out=self.qkv)
+            K.attention(self.qkv, self.ids, B, S, cfg.heads, out=self.ctx)
+            torch.addmm(L["o_b16"], self.ctx, L["o_w"].t(), out=self.y)
+            K.layernorm(self.y, L["ln1_g"], L["ln1_b"], residual=self.x, eps=cfg.eps, out=self.x2)
+            ffn = torch._addmm_activation(L["i_b16"], self.x2, L["i_w"].t(), use_gelu=True)
+            torch.addmm(L["f_b16"], ffn, L["f_w"].t(), out=self.y)
+            K.layernorm(self.y, L["ln2_g"], L["ln2_b"], residual=self.x2, eps=cfg.eps, out=self.x)
         self.cls_in.copy_(self.x.view(B, S, -1)[:, 0])
         K.gemm(self.cls_in, w.pool_w, w.pool_b, act="tanh", out=self.pooled)
         K.gemm(self.pooled, w.cls_w, w.cls_b, out=self.logits)

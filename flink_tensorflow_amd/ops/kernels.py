@@ -83,7 +83,7 @@ def _zeros_bias(n: int, device) -> torch.Tensor:
 # ------------------------------------------------------------------------------ conv
 # tile configs >= 16 select the pipelined 256-pixel LDS-DMA kernel (igemm_v2.hip) with
 # 128 or 64 output channels per tile; 0..4 are the register-staged igemm_bf16 tiles
-V2_CONFIGS = {16: 128, 17: 64}
+V2_CONFIGS = {16: 128, 17: 64, 18: 256}  # 18: GEMM mode only
 def conv_out_hw(H, W, KH, KW, sh, sw, ph, pw, dh=1, dw=1, ph_hi=None, pw_hi=None):
     ph_hi = ph if ph_hi is None else ph_hi
     pw_hi = pw if pw_hi is None else pw_hi

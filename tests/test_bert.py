@@ -41,12 +41,13 @@ def test_tokenizer_and_model_host():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("gemm", ["blas", "mfma"])
 @pytest.mark.parametrize("S", [128, 77])
-def test_bert_base_gpu_vs_fp32_reference(S):
+def test_bert_base_gpu_vs_fp32_reference(S, gemm):
     cfg = BertConfig.base()
     host = init_bert_weights(cfg, seed=2)
     dev = torch.device("cuda", 0)
-    plan = BertEncoderPlan(BertDeviceWeights(host, cfg, dev), batch=4, seq=S)
+    plan = BertEncoderPlan(BertDeviceWeights(host, cfg, dev), batch=4, seq=S, gemm=gemm)
     ids = _ids(4, S, cfg.vocab_size, seed=S)
     got = plan(ids.to(dev)).cpu()
     ref = torch.softmax(reference_forward(host, cfg, ids), -1)

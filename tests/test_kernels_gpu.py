@@ -184,3 +184,17 @@ def test_conv1x1_dual(stride2, cfg):
     torch.testing.assert_close(ref, two, rtol=1e-2, atol=1e-2)
     got = K.conv1x1_dual(x.to(DEV), x2.to(DEV), w.to(DEV), b.to(DEV), stride2, "relu", cfg=cfg)
     _close(got, ref)
+
+
+@pytest.mark.parametrize("cfg", [16, 17, 18])
+@pytest.mark.parametrize("M,N,Kd,act,res", [(300, 512, 256, "gelu", False), (1000, 768, 768, "none", True),
+                                            (4096, 2304, 768, "none", False)])
+def test_gemm_pipelined(M, N, Kd, act, res, cfg):
+    g = torch.Generator().manual_seed(M + N + cfg)
+    x = torch.randn(M, Kd, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, Kd, generator=g) / Kd ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, generator=g)
+    r = torch.randn(M, N, generator=g).to(torch.bfloat16) if res else None
+    ref = K.gemm(x, w, b, r, act)
+    got = K.gemm(x.to(DEV), w.to(DEV), b.to(DEV), r.to(DEV) if res else None, act, cfg=cfg)
+    _close(got, ref)
