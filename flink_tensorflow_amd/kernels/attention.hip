@@ -6,11 +6,14 @@
 // (id == pad_id -> masked), output ctx [T, H*D] bf16 — exactly the layout the output
 // projection GEMM consumes, so no transposes exist anywhere in the layer.
 //
-// One workgroup = one (batch, head, 64-query block); 4 waves x 16 query rows.  Per 64-key
-// block: K is staged row-major (d-contiguous, chunk-swizzled) and V transposed ([d][key])
-// in LDS; S = Q K^T and O += P V run on v_mfma_f32_16x16x32_bf16 (D = 64: 2 k-steps for
-// QK^T, 2 for PV); P goes through a per-wave LDS tile to become an A operand.  Softmax
-// statistics are per-row, reduced across the 16-lane column groups with __shfl_xor.
+// One workgroup = one (batch, head, QB-query block); QB/16 waves x 16 query rows (QB = 128
+// for BERT's S <= 128, so K/V of a head are staged once).  Per 64-key block: K is staged
+// row-major with a chunk XOR swizzle (conflict-free b128 fragment reads), V row-major
+// (coalesced 16-B writes) and consumed transposed by ds_read_b64_tr_b16 (the hardware
+// transpose read, guide T10) as the PV B operand.  S = Q K^T and O += P V run on
+// v_mfma_f32_16x16x32_bf16; P goes through a per-wave LDS tile to become an A operand;
+// softmax statistics are per row, reduced across the 16-lane column groups with
+// __shfl_xor; the normalised O tile is staged through LDS and stored as whole 128-B rows.
 #include <pybind11/pybind11.h>
 
 #include <stdexcept>
@@ -19,18 +22,29 @@
 
 namespace {
 
-constexpr int D = 64;     // head dim
-constexpr int QB = 64;    // queries per workgroup
-constexpr int KB = 64;    // keys per block
+constexpr int D = 64;      // head dim
+constexpr int KB = 64;     // keys per block
+constexpr int VP = D + 8;  // V row pitch (elements): tr-read rows land on distinct banks
+constexpr int PP = KB + 8;
+
+typedef short v4s __attribute__((ext_vector_type(4)));
 
 FTM_DEVICE int kswz(int row, int chunk) { return row * D + ((chunk ^ (row & 7)) << 3); }
 
-__global__ __launch_bounds__(256) void attention_fwd_kernel(const bf16* __restrict__ qkv, const int* __restrict__ ids,
-                                                            bf16* __restrict__ out, int B, int S, int H, int pad_id,
-                                                            float scale_log2e) {
-  __shared__ __attribute__((aligned(16))) bf16 Ks[KB * D];       // [key][d] swizzled
-  __shared__ __attribute__((aligned(16))) bf16 Vt[D * (KB + 8)];  // [d][key] (+pad)
-  __shared__ __attribute__((aligned(16))) bf16 Ps[4][16 * (KB + 8)];
+// 4 consecutive keys x 1 d column per lane (a 16-lane group reads 4 keys x 16 d columns)
+FTM_DEVICE v4s tr_read(const bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)p);
+}
+
+template <int QB>
+__global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __restrict__ qkv, const int* __restrict__ ids,
+                                                               bf16* __restrict__ out, int B, int S, int H, int pad_id,
+                                                               float scale_log2e) {
+  constexpr int NW = QB / 16;  // waves
+  constexpr int NTH = NW * 64;
+  __shared__ __attribute__((aligned(16))) bf16 Ks[KB * D];   // [key][d] swizzled
+  __shared__ __attribute__((aligned(16))) bf16 Vs[KB * VP];  // [key][d] (+pad)
+  __shared__ __attribute__((aligned(16))) bf16 Ps[NW][16 * PP];
   __shared__ float kmask[KB];
 
   const int qblocks = (S + QB - 1) / QB;
@@ -61,26 +75,28 @@ __global__ __launch_bounds__(256) void attention_fwd_kernel(const bf16* __restri
     mrow[r] = -INFINITY;
     lrow[r] = 0.f;
   }
+  // this lane's supplier address inside a 4-key x 16-d transposed-read block
+  const int trq = (lane & 15) >> 2, trp = lane & 3;
 
   const int nkb = (S + KB - 1) / KB;
   for (int kb = 0; kb < nkb; ++kb) {
-    // ---- stage K (row-major, swizzled) and V (transposed) for keys kb*64 .. +63
+    // ---- stage K (row-major, swizzled) and V (row-major) for keys kb*64 .. +63
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int q = tid + it * 256;        // 512 chunks of 8 elements
-      const int key = q >> 3, ch = q & 7;
-      const int kg = kb * KB + key;
-      u32x4 kv = {0u, 0u, 0u, 0u}, vv = {0u, 0u, 0u, 0u};
-      if (kg < S) {
-        const bf16* row = qkv + (tok0 + kg) * ld + h * D + ch * 8;
-        kv = *reinterpret_cast<const u32x4*>(row + H * D);
-        vv = *reinterpret_cast<const u32x4*>(row + 2 * H * D);
+    for (int it = 0; it < (KB * 8 + NTH - 1) / NTH; ++it) {
+      const int q = tid + it * NTH;  // 512 chunks of 8 elements
+      if (q < KB * 8) {
+        const int key = q >> 3, ch = q & 7;
+        const int kg = kb * KB + key;
+        u32x4 kv = {0u, 0u, 0u, 0u}, vv = {0u, 0u, 0u, 0u};
+        if (kg < S) {
+          const bf16* row = qkv + (tok0 + kg) * ld + h * D + ch * 8;
+          kv = *reinterpret_cast<const u32x4*>(row + H * D);
+          vv = *reinterpret_cast<const u32x4*>(row + 2 * H * D);
+        }
+        *reinterpret_cast<u32x4*>(Ks + kswz(key, ch)) = kv;
+        *reinterpret_cast<u32x4*>(Vs + key * VP + ch * 8) = vv;
       }
-      *reinterpret_cast<u32x4*>(Ks + kswz(key, ch)) = kv;
-      const bf16x8 v8 = *reinterpret_cast<const bf16x8*>(&vv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) Vt[(ch * 8 + e) * (KB + 8) + key] = v8[e];
     }
     if (tid < KB) {
       const int kg = kb * KB + tid;
@@ -140,31 +156,45 @@ __global__ __launch_bounds__(256) void attention_fwd_kernel(const bf16* __restri
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) ps[((lane >> 4) * 4 + r) * (KB + 8) + n * 16 + (lane & 15)] = f2bf(s[n][r]);
+      for (int r = 0; r < 4; ++r) ps[((lane >> 4) * 4 + r) * PP + n * 16 + (lane & 15)] = f2bf(s[n][r]);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P writes landed
     __builtin_amdgcn_wave_barrier();
-    // ---- O += P V  (A = P[q][key], B = V[key][d] read from Vt[d][key])
+    // ---- O += P V  (A = P[q][key]; B[key][d] by transposed reads of row-major V)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 pa = *reinterpret_cast<const bf16x8*>(ps + (lane & 15) * (KB + 8) + ks * 32 + (lane >> 4) * 8);
+      const bf16x8 pa = *reinterpret_cast<const bf16x8*>(ps + (lane & 15) * PP + ks * 32 + (lane >> 4) * 8);
+      const int key0 = ks * 32 + (lane >> 4) * 8;  // this lane group's 8 keys
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
-        const bf16x8 vb =
-            *reinterpret_cast<const bf16x8*>(Vt + (n * 16 + (lane & 15)) * (KB + 8) + ks * 32 + (lane >> 4) * 8);
+        const bf16* src = Vs + (key0 + trq) * VP + n * 16 + trp * 4;
+        const v4s lo = tr_read(src), hi = tr_read(src + 4 * VP);
+        // whole-vector reinterpretation (element-wise short->bf16 inserts miscompile here)
+        const bf16x8 vb = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[n], 0, 0, 0);
       }
     }
   }
 
-  // ---- normalise and store: o[n][r] = O[q = (lane>>4)*4 + r][d = n*16 + (lane&15)]
+  // ---- normalise, stage the wave's [16 q][64 d] tile in its P slot, store 128-B rows
+  bf16* os = Ps[wave];
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int q = qb * QB + wave * 16 + (lane >> 4) * 4 + r;
-    if (q >= S) continue;
     const float inv = lrow[r] > 0.f ? 1.f / lrow[r] : 0.f;
-    bf16* dst = out + (tok0 + q) * (H * D) + h * D;
 #pragma unroll
-    for (int n = 0; n < 4; ++n) dst[n * 16 + (lane & 15)] = f2bf(o[n][r] * inv);
+    for (int n = 0; n < 4; ++n) os[((lane >> 4) * 4 + r) * PP + n * 16 + (lane & 15)] = f2bf(o[n][r] * inv);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int c = lane + it * 64;  // 16 rows x 8 chunks
+    const int r = c >> 3, ch = c & 7;
+    const int q = qb * QB + wave * 16 + r;
+    if (q < S)
+      *reinterpret_cast<u32x4*>(out + (tok0 + q) * (H * D) + h * D + ch * 8) =
+          *reinterpret_cast<const u32x4*>(os + r * PP + ch * 8);
   }
 }
 
@@ -229,11 +259,20 @@ void attention_fwd_bf16(uintptr_t qkv, uintptr_t ids, uintptr_t out, int B, int 
   if (Dh != D) throw std::invalid_argument("attention_fwd: head dim must be 64");
   if (B <= 0 || S <= 0 || H <= 0) throw std::invalid_argument("attention_fwd: empty problem");
   if (qkv % 16 || out % 16) throw std::invalid_argument("attention_fwd: pointers must be 16-byte aligned");
-  const int qblocks = (S + QB - 1) / QB;
   const float kLog2e = 1.4426950408889634f;
-  hipLaunchKernelGGL(attention_fwd_kernel, dim3(B * H * qblocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     reinterpret_cast<const bf16*>(qkv), reinterpret_cast<const int*>(ids), reinterpret_cast<bf16*>(out),
-                     B, S, H, pad_id, scale * kLog2e);
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  auto Q = reinterpret_cast<const bf16*>(qkv);
+  auto I = reinterpret_cast<const int*>(ids);
+  auto O = reinterpret_cast<bf16*>(out);
+  if (S > 64) {  // 128-query blocks: K/V of a head staged once for S <= 128
+    const int qblocks = (S + 127) / 128;
+    hipLaunchKernelGGL(attention_fwd_kernel<128>, dim3(B * H * qblocks), dim3(512), 0, st, Q, I, O, B, S, H, pad_id,
+                       scale * kLog2e);
+  } else {
+    const int qblocks = (S + 63) / 64;
+    hipLaunchKernelGGL(attention_fwd_kernel<64>, dim3(B * H * qblocks), dim3(256), 0, st, Q, I, O, B, S, H, pad_id,
+                       scale * kLog2e);
+  }
   FTM_CHECK_LAUNCH();
 }
 
@@ -256,7 +295,27 @@ void embed_ln_bf16(uintptr_t ids, uintptr_t tt, uintptr_t word, uintptr_t pos, u
   FTM_CHECK_LAUNCH();
 }
 
+// Diagnostic: LDS[r][c] = r * 256 + c (16-bit, 16 rows x 64 cols); every lane issues one
+// transposed read at (row = 4*(lane>>4) + ((lane&15)>>2), col = 4*(lane&3) + 16*blk);
+// out[lane][0..3] = the 4 returned elements.
+__global__ void probe_tr_kernel(short* out, int blk) {
+  __shared__ __attribute__((aligned(16))) short t[16 * 64];
+  for (int i = threadIdx.x; i < 16 * 64; i += 64) t[i] = (short)((i / 64) * 256 + (i % 64));
+  __syncthreads();
+  const int lane = threadIdx.x;
+  const int row = 4 * (lane >> 4) + ((lane & 15) >> 2), col = 4 * (lane & 3) + 16 * blk;
+  v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(t + row * 64 + col));
+  for (int e = 0; e < 4; ++e) out[lane * 4 + e] = v[e];
+}
+
+void probe_tr_read(uintptr_t out, int blk, uintptr_t stream) {
+  hipLaunchKernelGGL(probe_tr_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<short*>(out), blk);
+  FTM_CHECK_LAUNCH();
+}
+
 void register_attention(pybind11::module_& m) {
+  m.def("probe_tr_read", &probe_tr_read);
   m.def("attention_fwd_bf16", &attention_fwd_bf16);
   m.def("embed_ln_bf16", &embed_ln_bf16);
 }

@@ -373,8 +373,10 @@ class BertClassifierModel(RichModel, BatchedGpuModel):
         return [self._res(b) for b in self._runner.drain()] if self._runner is not None else []
 
 
-def reference_forward(host: dict[str, torch.Tensor], cfg: BertConfig, ids: torch.Tensor) -> torch.Tensor:
-    """Plain PyTorch fp32 BERT (numerics oracle): ids [B, S] → logits [B, num_labels]."""
+def reference_forward(host: dict[str, torch.Tensor], cfg: BertConfig, ids: torch.Tensor,
+                      return_hidden: bool = False):
+    """Plain PyTorch fp32 BERT (numerics oracle): ids [B, S] → logits [B, num_labels]
+    (and the final hidden states [B, S, hidden] with ``return_hidden``)."""
     import torch.nn.functional as F
 
     B, S = ids.shape
@@ -402,4 +404,5 @@ def reference_forward(host: dict[str, torch.Tensor], cfg: BertConfig, ids: torch
         x = F.layer_norm(lin(f, "output/dense") + x, (h,), host[p + "output/LayerNorm/gamma"],
                          host[p + "output/LayerNorm/beta"], cfg.eps)
     pooled = torch.tanh(x[:, 0] @ host["bert/pooler/dense/kernel"] + host["bert/pooler/dense/bias"])
-    return pooled @ host["output_weights"].t() + host["output_bias"]
+    logits = pooled @ host["output_weights"].t() + host["output_bias"]
+    return (logits, x) if return_hidden else logits
