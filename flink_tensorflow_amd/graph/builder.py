@@ -122,6 +122,10 @@ class GraphBuilder:
         return self.op("FusedBatchNormV3", [x, scale, offset, mean, var], name=name, epsilon=float(epsilon),
                        is_training=False, data_format=b"NHWC")
 
+    def lrn(self, x, depth_radius=5, bias=1.0, alpha=1.0, beta=0.5, name=None) -> str:
+        return self.op("LRN", [x], name=name, depth_radius=int(depth_radius), bias=float(bias), alpha=float(alpha),
+                       beta=float(beta))
+
     def max_pool(self, x, ksize, strides, padding="VALID", name=None) -> str:
         return self.op("MaxPool", [x], name=name, ksize=[1, ksize[0], ksize[1], 1],
                        strides=[1, strides[0], strides[1], 1], padding=padding.encode(), data_format=b"NHWC")

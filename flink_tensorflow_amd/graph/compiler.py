@@ -56,6 +56,8 @@ from .ops_nn import same_pads
 LOG = logging.getLogger("flink_tensorflow_amd.compiler")
 
 _ACTS = {"Relu": K.ACT_RELU, "Relu6": K.ACT_RELU6, "Sigmoid": K.ACT_SIGMOID, "Tanh": K.ACT_TANH}
+_BINARY = {"Add": "add", "AddV2": "add", "Sub": "sub", "Mul": "mul", "RealDiv": "div", "Div": "div",
+           "Maximum": "max", "Minimum": "min"}
 
 
 class CompileError(RuntimeError):
@@ -379,7 +381,95 @@ class CompiledFunction:
             return self._lower_concat(node)
         if op == "NoOp":
             return
+        if op == "LRN" and self._lower_lrn(node):
+            return
+        if op in _BINARY and self._lower_binary(node):
+            return
+        if op in _ACTS and self._lower_unary_act(node):
+            return
+        if op == "Cast" and self._lower_float_cast(node):
+            return
         return self._lower_glue(node)
+
+    # ---- standalone elementwise / LRN (ops no producer epilogue absorbed)
+    def _ew_ok(self, v: Val) -> bool:
+        # bf16 activations, fp8 activations (dequantised first) or fed fp32 tensors (cast first)
+        return v is not None and not v.is_const and v.dtype in (torch.bfloat16, torch.uint8, torch.float32) and \
+            (v.qscale is not None or v.dtype != torch.uint8) and not v.phys_c and int(np.prod(v.shape)) % 8 == 0
+
+    def _lower_binary(self, node: Node) -> bool:
+        a, b = self._get(node.inputs[0]), self._get(node.inputs[1])
+        op = _BINARY[node.op]
+        if a is not None and a.is_const and b is not None and not b.is_const:
+            a, b = b, a
+            op = {"sub": "rsub", "div": "rdiv"}.get(op, op)
+        if not self._ew_ok(a) or b is None:
+            return False
+        if b.is_const:
+            c = b.const.float().reshape(-1) if isinstance(b.const, torch.Tensor) else None
+            if c is None:
+                return False
+            if c.numel() == 1:
+                operand, kind = float(c.item()), "scalar"
+            elif c.numel() == a.shape[-1] and c.numel() % 8 == 0 and len(b.const.shape) == 1:
+                operand, kind = c.to(self.device).contiguous(), "vector"
+                self.params.append(operand)
+            else:
+                return False
+        else:
+            if not self._ew_ok(b) or tuple(b.shape) != tuple(a.shape):
+                return False
+            operand, kind = None, "tensor"
+        xa = self._as_bf16(a, node.name + "/a")
+        xb = self._as_bf16(b, node.name + "/b") if kind == "tensor" else None
+        out = self._new(a.shape)
+
+        def run(xa=xa, xb=xb, out=out, operand=operand):
+            K.binary(_view(xa), _view(xb) if xb is not None else operand, op, out=out.buf)
+
+        self._emit(node.name, "elementwise", run, [xa] + ([xb] if xb is not None else []), [out])
+        self.vals[(node.name, 0)] = out
+        return True
+
+    def _lower_unary_act(self, node: Node) -> bool:
+        x = self._get(node.inputs[0])
+        if not self._ew_ok(x):
+            return False
+        xa = self._as_bf16(x, node.name)
+        out = self._new(x.shape)
+        act = _ACTS[node.op]
+
+        def run(xa=xa, out=out):
+            K.binary(_view(xa), 0.0, "add", act=act, out=out.buf)
+
+        self._emit(node.name, "elementwise", run, [xa], [out])
+        self.vals[(node.name, 0)] = out
+        return True
+
+    def _lower_float_cast(self, node: Node) -> bool:
+        x = self._get(node.inputs[0])
+        dst = node.attr("DstT")
+        if x is None or x.is_const or x.dtype != torch.bfloat16 or DataType.of(dst).torch not in (
+                torch.float32, torch.bfloat16, torch.float16):
+            return False
+        self.vals[(node.name, 0)] = x  # device activations are bf16 either way
+        return True
+
+    def _lower_lrn(self, node: Node) -> bool:
+        x = self._get(node.inputs[0])
+        if not self._ew_ok(x) or len(x.shape) != 4 or x.shape[-1] % 8 or node.attr("depth_radius", 5) > 8:
+            return False
+        xa = self._as_bf16(x, node.name)
+        out = self._new(x.shape)
+        r, bias = int(node.attr("depth_radius", 5)), float(node.attr("bias", 1.0))
+        alpha, beta = float(node.attr("alpha", 1.0)), float(node.attr("beta", 0.5))
+
+        def run(xa=xa, out=out):
+            K.lrn(_view(xa), r, bias, alpha, beta, out=out.buf)
+
+        self._emit(node.name, "lrn", run, [xa], [out])
+        self.vals[(node.name, 0)] = out
+        return True
 
     # ---- conv chain
     def _conv_chain(self, start: Node):

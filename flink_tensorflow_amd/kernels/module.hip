@@ -12,6 +12,7 @@ void register_fp8(pybind11::module_& m);
 void register_attention(pybind11::module_& m);
 void register_igemm_v2(pybind11::module_& m);
 void register_dconv(pybind11::module_& m);
+void register_elementwise(pybind11::module_& m);
 
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "flink_tensorflow_amd CDNA4 (gfx950) kernels";
@@ -24,4 +25,5 @@ PYBIND11_MODULE(_hip, m) {
   register_attention(m);
   register_igemm_v2(m);
   register_dconv(m);
+  register_elementwise(m);
 }

@@ -88,8 +88,10 @@ def googlenet_like_graph_def(num_classes: int = 1008, seed: int = 0, width: floa
     x = b.placeholder("input", "FLOAT", [None, 224, 224, 3])
     x = conv(x, 3, c(64), 7, 2, "conv2d0")
     x = b.max_pool(x, (3, 3), (2, 2), "SAME", name="maxpool0")
+    x = b.lrn(x, 5, 1.0, 1e-4, 0.75, name="localresponsenorm0")  # as in inception5h
     x = conv(x, c(64), c(64), 1, 1, "conv2d1")
     x = conv(x, c(64), c(192), 3, 1, "conv2d2")
+    x = b.lrn(x, 5, 1.0, 1e-4, 0.75, name="localresponsenorm1")
     x = b.max_pool(x, (3, 3), (2, 2), "SAME", name="maxpool1")
     cin = c(192)
     for i, (o1, r3, o3, r5, o5, pp) in enumerate([(64, 96, 128, 16, 32, 32), (128, 128, 192, 32, 96, 64)]):

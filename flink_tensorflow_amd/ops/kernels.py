@@ -522,3 +522,58 @@ def conv1x1_dual(x: torch.Tensor, x2: torch.Tensor, w_cat: torch.Tensor, bias: t
     y = x.float() @ w_cat[:, :K1].float().t() + xs.float() @ w_cat[:, K1:].float().t() + bias.float()
     out[..., out_channel_offset:out_channel_offset + Cout] = _apply_act_ref(y, a).to(out.dtype)
     return out
+
+
+# ------------------------------------------------------------------------------ elementwise
+BIN_OPS = {"add": 0, "sub": 1, "mul": 2, "div": 3, "max": 4, "min": 5, "rsub": 6, "rdiv": 7}
+_BIN_REF = {0: lambda a, b: a + b, 1: lambda a, b: a - b, 2: lambda a, b: a * b, 3: lambda a, b: a / b,
+            4: torch.maximum, 5: torch.minimum, 6: lambda a, b: b - a, 7: lambda a, b: b / a}
+
+
+def binary(a: torch.Tensor, b, op: str, act=None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``act(a OP b)`` with ``b`` a Python scalar, a fp32 vector over the last dim of ``a``,
+    or a tensor of ``a``'s shape (the standalone elementwise kernel)."""
+    code = BIN_OPS[op]
+    a_act = act_code(act)
+    if out is None:
+        out = torch.empty(a.shape, dtype=a.dtype if a.is_cuda else torch.float32, device=a.device)
+    if a.is_cuda:
+        _check(a, "a", device=a.device)
+        _check(out, "out", device=a.device)
+        if isinstance(b, (int, float)):
+            _hip().binary_bf16(code, a.data_ptr(), 0, out.data_ptr(), a.numel(), 0, 0, float(b), a_act, _stream())
+        elif b.dim() == 1 and b.numel() == a.shape[-1]:
+            _check(b, "b", torch.float32, a.device)
+            _hip().binary_bf16(code, a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), 1, b.numel(), 0.0, a_act,
+                               _stream())
+        else:
+            if tuple(b.shape) != tuple(a.shape):
+                raise ValueError(f"binary: cannot broadcast {tuple(b.shape)} to {tuple(a.shape)}")
+            _check(b, "b", device=a.device)
+            _hip().binary_bf16(code, a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), 2, 0, 0.0, a_act, _stream())
+        return out
+    bb = b if isinstance(b, (int, float)) else b.float()
+    out.copy_(_apply_act_ref(_BIN_REF[code](a.float(), bb if not isinstance(bb, (int, float)) else torch.tensor(bb)),
+                             a_act).to(out.dtype))
+    return out
+
+
+def lrn(x: torch.Tensor, depth_radius: int = 5, bias: float = 1.0, alpha: float = 1.0, beta: float = 0.5,
+        out: torch.Tensor | None = None) -> torch.Tensor:
+    """TF ``LRN`` on NHWC (normalisation across channels)."""
+    if out is None:
+        out = torch.empty(x.shape, dtype=x.dtype if x.is_cuda else torch.float32, device=x.device)
+    C = x.shape[-1]
+    if x.is_cuda:
+        _check(x, "x", device=x.device)
+        _check(out, "out", device=x.device)
+        _hip().lrn_bf16(x.data_ptr(), out.data_ptr(), x.numel() // C, C, int(depth_radius), float(bias), float(alpha),
+                        float(beta), _stream())
+        return out
+    sq = x.float() ** 2
+    acc = torch.zeros_like(sq)
+    for d in range(-depth_radius, depth_radius + 1):
+        lo, hi = max(0, -d), min(C, C - d)
+        acc[..., lo:hi] += sq[..., lo + d:hi + d]
+    out.copy_((x.float() / (bias + alpha * acc) ** beta).to(out.dtype))
+    return out

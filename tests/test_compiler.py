@@ -96,3 +96,49 @@ def test_plan_profile_and_debug_modes(monkeypatch):
     out = dbg({"images:0": img})[0]
     assert torch.isfinite(out).all()
     torch.testing.assert_close(out, ref)
+
+
+def _elementwise_graph():
+    import numpy as np
+
+    from flink_tensorflow_amd.graph.builder import GraphBuilder
+    from flink_tensorflow_amd.graph.graph import Graph
+
+    gb = GraphBuilder()
+    x = gb.placeholder("x", "FLOAT", [2, 4, 4, 16])
+    y = gb.mul(x, gb.constant("two", np.float32(2.0)), name="scale")
+    y = gb.add(y, gb.constant("bias", np.linspace(-1, 1, 16).astype(np.float32)), name="shift")
+    y = gb.relu(y, name="act")
+    y = gb.lrn(y, 2, 1.0, 0.5, 0.75, name="lrn")
+    y = gb.sub(y, x, name="diff")
+    y = gb.op("Maximum", [y, gb.constant("floor", np.float32(-0.25))], name="clip")
+    y = gb.div(gb.constant("one", np.float32(1.0)), gb.add(gb.op("Abs", [y], name="abs"),
+                                                            gb.constant("eps", np.float32(1.0))), name="out")
+    return Graph.from_graph_def(gb.build_graph_def())
+
+
+def _check_elementwise(device):
+    import torch
+
+    from flink_tensorflow_amd.graph.compiler import CompiledFunction
+    from flink_tensorflow_amd.graph.session import Session
+
+    g = _elementwise_graph()
+    x = torch.randn(2, 4, 4, 16)
+    ref = Session(g).run(["clip:0"], {"x:0": x})[0]
+    plan = CompiledFunction(g, {"x:0": ((2, 4, 4, 16), "FLOAT")}, ["clip:0"], device, strict=True)
+    kinds = plan.summary()["kinds"]
+    assert kinds.get("elementwise") == 5 and kinds.get("lrn") == 1, kinds
+    got = plan({"x:0": x.to(device)})[0].cpu()
+    torch.testing.assert_close(got, ref.float(), rtol=2e-2, atol=3e-2)
+
+
+def test_standalone_elementwise_and_lrn_host():
+    _check_elementwise("cpu")
+
+
+@pytest.mark.gpu
+def test_standalone_elementwise_and_lrn_gpu():
+    import torch
+
+    _check_elementwise(torch.device("cuda", 0))

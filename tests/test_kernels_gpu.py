@@ -198,3 +198,23 @@ def test_gemm_pipelined(M, N, Kd, act, res, cfg):
     ref = K.gemm(x, w, b, r, act)
     got = K.gemm(x.to(DEV), w.to(DEV), b.to(DEV), r.to(DEV) if res else None, act, cfg=cfg)
     _close(got, ref)
+
+
+@pytest.mark.parametrize("op", ["add", "sub", "mul", "div", "max", "rsub"])
+def test_binary_elementwise(op):
+    g = torch.Generator().manual_seed(3)
+    a = torch.randn(3, 5, 64, generator=g).to(torch.bfloat16)
+    b_full = (torch.rand(3, 5, 64, generator=g) + 0.5).to(torch.bfloat16)
+    b_vec = torch.rand(64, generator=g) + 0.5
+    for b in (b_full, b_vec, 1.5):
+        ref = K.binary(a, b, op, act="relu")
+        got = K.binary(a.to(DEV), b.to(DEV) if torch.is_tensor(b) else b, op, act="relu")
+        _close(got, ref)
+
+
+def test_lrn_kernel():
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 7, 7, 96, generator=g).to(torch.bfloat16)
+    ref = K.lrn(x, 5, 1.0, 1e-2, 0.75)
+    got = K.lrn(x.to(DEV), 5, 1.0, 1e-2, 0.75)
+    _close(got, ref)
