@@ -250,6 +250,9 @@ def run_widedeep(args, dev, rank, ws):
         batch = tuple(t.to(dev, non_blocking=True) for t in host[i % nb])
         return tr.train_step(batch=batch)
 
+    if ws == 1 and not args.no_graph:  # whole train step as one hipGraph (sync-free sparse path)
+        tr.capture(tuple(t.to(dev) for t in host[0]))
+
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
@@ -274,7 +277,8 @@ def run_widedeep(args, dev, rank, ws):
             "data": "synthetic Criteo-shaped click records (13 dense, 26 categorical), random init",
             "config": {"model": "Wide&Deep (26x100k x32 embeddings, MLP 1024-512-256)", "global_batch": B * ws,
                        "seq_len": None, "parallelism": f"dp{ws}", "micro_batch_per_gpu": B},
-            "final_loss": round(float(loss), 4), "setup_s": round(compile_s, 2)}), flush=True)
+            "final_loss": round(float(loss), 4), "setup_s": round(compile_s, 2),
+            "hip_graph": tr._graph is not None}), flush=True)
     tr.close()
 
 

@@ -94,13 +94,32 @@ __global__ __launch_bounds__(256) void segment_sum_rows_kernel(const T* __restri
   }
 }
 
+// Segment boundaries of a sorted key array, static shapes: for every i that starts a run
+// (i == 0 or sorted[i] != sorted[i-1]) with run index s = seg_id[i]:  seg[s] = i and
+// uids[s] = key (or -1 for the invalid bucket key == num_rows).  Each run is written by
+// exactly one thread: deterministic, no atomics, no host round trip.
+__global__ __launch_bounds__(256) void segment_starts_kernel(const long long* __restrict__ sorted,
+                                                             const int* __restrict__ seg_id, int* __restrict__ seg,
+                                                             int* __restrict__ uids, int n, long long num_rows) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long long k = sorted[i];
+  if (i == 0 || sorted[i - 1] != k) {
+    const int sidx = seg_id[i];
+    seg[sidx] = i;
+    uids[sidx] = k >= num_rows ? -1 : (int)k;
+  }
+}
+
 __global__ __launch_bounds__(256) void sparse_adagrad_kernel(float* __restrict__ table, float* __restrict__ accum,
                                                              const int* __restrict__ uids, const float* __restrict__ g,
-                                                             int U, int D, float lr, float eps) {
+                                                             int U, int D, int V, float lr, float eps) {
   const int lane = threadIdx.x & 63;
   const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (u >= U) return;
-  const size_t row = (size_t)uids[u] * D;
+  const int id = uids[u];
+  if (id < 0 || id >= V) return;  // padding of the static-shape sparse pipeline
+  const size_t row = (size_t)id * D;
   for (int c = lane * 4; c < D; c += 64 * 4) {
     f32x4 gv = *reinterpret_cast<const f32x4*>(g + (size_t)u * D + c);
     f32x4 av = *reinterpret_cast<f32x4*>(accum + row + c);
@@ -156,18 +175,28 @@ void segment_sum_rows(uintptr_t grad, uintptr_t perm, uintptr_t seg, uintptr_t o
   FTM_CHECK_LAUNCH();
 }
 
-void sparse_adagrad(uintptr_t table, uintptr_t accum, uintptr_t uids, uintptr_t g, int U, int D, float lr, float eps,
-                    uintptr_t stream) {
+void sparse_adagrad(uintptr_t table, uintptr_t accum, uintptr_t uids, uintptr_t g, int U, int D, int V, float lr,
+                    float eps, uintptr_t stream) {
   if (D % 4) throw std::invalid_argument("sparse_adagrad: D % 4 != 0");
   if (table % 16 || accum % 16 || g % 16) throw std::invalid_argument("sparse_adagrad: 16-byte alignment required");
   if (U <= 0) return;
   hipLaunchKernelGGL(sparse_adagrad_kernel, dim3((U + 3) / 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      reinterpret_cast<float*>(table), reinterpret_cast<float*>(accum), reinterpret_cast<const int*>(uids),
-                     reinterpret_cast<const float*>(g), U, D, lr, eps);
+                     reinterpret_cast<const float*>(g), U, D, V, lr, eps);
+  FTM_CHECK_LAUNCH();
+}
+
+void segment_starts(uintptr_t sorted, uintptr_t seg_id, uintptr_t seg, uintptr_t uids, int n, long long num_rows,
+                    uintptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(segment_starts_kernel, dim3((n + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const long long*>(sorted), reinterpret_cast<const int*>(seg_id),
+                     reinterpret_cast<int*>(seg), reinterpret_cast<int*>(uids), n, num_rows);
   FTM_CHECK_LAUNCH();
 }
 
 void register_embedding(pybind11::module_& m) {
+  m.def("segment_starts", &segment_starts);
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
   m.def("segment_sum_rows", &segment_sum_rows);
   m.def("sparse_adagrad", &sparse_adagrad);

@@ -98,37 +98,33 @@ class WideDeep(torch.nn.Module):
 
 
 def _sparse_sync(uids: torch.Tensor, rows: torch.Tensor):
-    """All-gather row-sparse gradients (variable length: pad to the max count)."""
+    """All-gather row-sparse gradients.  The static-shape sparse pipeline pads every rank's
+    (uids, rows) to the same length (one slot per looked-up id, uid -1 = empty), so the
+    exchange is two fixed-size all-gathers with no size round trip or host sync."""
     if not comm.is_dist():
         return uids, rows
     import torch.distributed as dist
 
-    n = torch.tensor([uids.numel()], device=uids.device, dtype=torch.int64)
-    ns = [torch.zeros_like(n) for _ in range(dist.get_world_size())]
-    dist.all_gather(ns, n)
-    mx = int(max(x.item() for x in ns))
-    pu = torch.full((mx,), -1, dtype=torch.int32, device=uids.device)
-    pu[: uids.numel()] = uids
-    pr = torch.zeros((mx, rows.shape[1]), dtype=rows.dtype, device=rows.device)
-    pr[: rows.shape[0]] = rows
-    gu = [torch.empty_like(pu) for _ in ns]
-    gr = [torch.empty_like(pr) for _ in ns]
-    dist.all_gather(gu, pu)
-    dist.all_gather(gr, pr)
-    return torch.cat(gu), torch.cat(gr)  # -1 ids are dropped by the merge
+    ws = dist.get_world_size()
+    gu = torch.empty((ws * uids.numel(),), dtype=uids.dtype, device=uids.device)
+    gr = torch.empty((ws * rows.shape[0], rows.shape[1]), dtype=rows.dtype, device=rows.device)
+    dist.all_gather_into_tensor(gu, uids.contiguous())
+    dist.all_gather_into_tensor(gr, rows.contiguous())
+    return gu, gr  # -1 ids are dropped by the merge
 
 
 class WideDeepTrainer(RichModel, CheckpointedModel):
     """Online trainer: ``train_step(records)`` on micro-batches of
     ``(label, dense[13], cats[26], cross[C])`` records; ``predict(records)``."""
 
-    _TRANSIENT = ("_model", "_opt", "_bucketer")
+    _TRANSIENT = ("_model", "_opt", "_bucketer", "_graph", "_static", "_static_loss")
 
     def __init__(self, cfg: WideDeepConfig | None = None, device=None, seed: int = 0):
         self.cfg = cfg or WideDeepConfig()
         self.device = device
         self.seed = seed
         self._model = self._opt = self._bucketer = None
+        self._graph = self._static = self._static_loss = None
         self.steps = 0
 
     def open(self):
@@ -136,13 +132,16 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         self._model = WideDeep(self.cfg, dev, self.seed)
         if comm.is_dist():  # identical initial replicas: rank 0's weights to everyone
             comm.broadcast_tensors([p.data for p in self._model.parameters()] + list(self._model.buffers()), 0)
-        self._opt = torch.optim.Adam(self._model.dense_parameters(), lr=self.cfg.lr_dense)
+        fused = dev.type == "cuda"  # one multi-tensor Adam launch instead of one per parameter tensor
+        self._opt = torch.optim.Adam(self._model.dense_parameters(), lr=self.cfg.lr_dense, fused=fused,
+                                     capturable=fused)
         self._bucketer = comm.GradBucketer(self._model.dense_parameters())
 
     def close(self):
         if self._bucketer is not None:
             self._bucketer.remove()
         self._model = self._opt = self._bucketer = None
+        self._graph = self._static = self._static_loss = None
 
     @property
     def is_open(self):
@@ -164,8 +163,39 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
                 cross.to(d, non_blocking=nb))
 
     def train_step(self, records=None, batch=None) -> float:
+        batch = batch if batch is not None else self.collate(records)
+        if self._graph is not None and all(a.shape == b.shape for a, b in zip(batch, self._static)):
+            for dst, src in zip(self._static, batch):  # new micro-batch into the captured inputs
+                dst.copy_(src, non_blocking=True)
+            self._graph.replay()
+            self.steps += 1
+            return self._static_loss
+        return self._step(batch)
+
+    def capture(self, batch) -> None:
+        """Captures one whole training step (forward, backward, fused Adam, sparse Adagrad
+        row updates) as a hipGraph for micro-batches shaped like ``batch``; later
+        ``train_step`` calls with that shape replay it (one launch instead of ~190).  The
+        sparse pipeline is static-shape and sync-free, which is what makes this possible.
+        Single-process only (the data-parallel path keeps its collectives outside graphs)."""
+        if comm.is_dist():
+            return
+        dev = self._model.device
+        self._static = tuple(t.to(dev).clone() for t in batch)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm-up (real steps): allocator pools, optimizer state
+                self._step(self._static)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._static_loss = self._step(self._static)
+        self._graph = g
+
+    def _step(self, batch):
         m = self._model
-        labels, dense, cats, cross = batch if batch is not None else self.collate(records)
+        labels, dense, cats, cross = batch
         logits = m(dense, cats, cross)
         loss = F.binary_cross_entropy_with_logits(logits, labels)
         self._opt.zero_grad(set_to_none=True)

@@ -28,10 +28,52 @@ def embedding_bag(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | No
     return out
 
 
-def segment_sum(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L: int = 1):
-    """Deterministic sum of ``rows[i // L]`` grouped by ``keys[i]`` (keys outside
-    ``[0, num_rows)`` dropped).  Returns ``(unique keys int32 [U], sums fp32 [U, D])``."""
+def _segment_sum_static(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L: int):
+    """Sync-free, static-shape segment sum on the GPU: outputs are sized by the number of
+    keys n (an upper bound of the unique count); unused slots carry uid -1 and zero rows.
+    No ``.item()`` / ``unique`` host round trip, so a training step stays asynchronous
+    (and capturable)."""
+    n = keys.numel()
     D = rows.shape[1]
+    dev = keys.device
+    flat = keys.reshape(-1).long()
+    key = torch.where((flat >= 0) & (flat < num_rows), flat, torch.full_like(flat, num_rows))
+    sorted_k, perm = torch.sort(key, stable=True)
+    first = torch.ones(n, dtype=torch.bool, device=dev)
+    if n > 1:
+        first[1:] = sorted_k[1:] != sorted_k[:-1]
+    seg_id = torch.cumsum(first.to(torch.int32), 0, dtype=torch.int32) - 1
+    uids = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    seg = torch.full((n + 1,), n, dtype=torch.int32, device=dev)
+    _hip().segment_starts(sorted_k.data_ptr(), seg_id.data_ptr(), seg.data_ptr(), uids.data_ptr(), n, num_rows,
+                          _stream())
+    out = torch.empty((n, D), dtype=torch.float32, device=rows.device)
+    g = rows.contiguous()
+    fp32 = g.dtype == torch.float32
+    if not fp32 and g.dtype != torch.bfloat16:
+        g = g.to(torch.bfloat16)
+    perm32 = perm.to(torch.int32)
+    _hip().segment_sum_rows(g.data_ptr(), perm32.data_ptr(), seg.data_ptr(), out.data_ptr(), n, D, L, int(fp32),
+                            _stream())
+    return uids, out
+
+
+def segment_sum(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L: int = 1, static: bool = False):
+    """Deterministic sum of ``rows[i // L]`` grouped by ``keys[i]`` (keys outside
+    ``[0, num_rows)`` dropped).  Returns ``(unique keys int32 [U], sums fp32 [U, D])``;
+    with ``static=True`` the outputs have one slot per key (padding uid -1, zero rows) and
+    the GPU path never synchronises with the host."""
+    D = rows.shape[1]
+    if static:
+        if keys.is_cuda and keys.numel():
+            return _segment_sum_static(keys, rows, num_rows, L)
+        u, r = segment_sum(keys, rows, num_rows, L)
+        n = keys.numel()
+        up = torch.full((n,), -1, dtype=torch.int32, device=keys.device)
+        rp = torch.zeros((n, D), dtype=torch.float32, device=rows.device)
+        up[: u.numel()] = u
+        rp[: r.shape[0]] = r
+        return up, rp
     flat = keys.reshape(-1).long()
     valid = (flat >= 0) & (flat < num_rows)
     key = torch.where(valid, flat, torch.full_like(flat, num_rows))
@@ -62,9 +104,9 @@ def segment_sum(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L: int = 
     return uids.to(torch.int32), out
 
 
-def embedding_bag_backward(ids: torch.Tensor, grad_out: torch.Tensor, num_rows: int):
+def embedding_bag_backward(ids: torch.Tensor, grad_out: torch.Tensor, num_rows: int, static: bool = False):
     """Row-sparse gradient of ``embedding_bag``: returns ``(uids int32 [U], rows fp32 [U, D])``."""
-    return segment_sum(ids, grad_out, num_rows, ids.shape[1])
+    return segment_sum(ids, grad_out, num_rows, ids.shape[1], static=static)
 
 
 def sparse_adagrad(table: torch.Tensor, accum: torch.Tensor, uids: torch.Tensor, grads: torch.Tensor, lr: float,
@@ -75,9 +117,11 @@ def sparse_adagrad(table: torch.Tensor, accum: torch.Tensor, uids: torch.Tensor,
         _check(accum, "accum", torch.float32, table.device)
         _check(grads, "grads", torch.float32, table.device)
         _check(uids, "uids", torch.int32, table.device)
-        _hip().sparse_adagrad(table.data_ptr(), accum.data_ptr(), uids.data_ptr(), grads.data_ptr(), U, D, float(lr),
-                              float(eps), _stream())
+        _hip().sparse_adagrad(table.data_ptr(), accum.data_ptr(), uids.data_ptr(), grads.data_ptr(), U, D,
+                              table.shape[0], float(lr), float(eps), _stream())
         return
+    keep = (uids >= 0) & (uids < table.shape[0])  # static-shape padding slots
+    uids, grads = uids[keep], grads[keep]
     idx = uids.long()
     a = accum[idx] + grads * grads
     accum[idx] = a
@@ -98,7 +142,7 @@ class EmbeddingBagFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad):
         (ids,) = ctx.saved_tensors
-        ctx.holder.sparse_grads.append(embedding_bag_backward(ids, grad, ctx.V))
+        ctx.holder.sparse_grads.append(embedding_bag_backward(ids, grad, ctx.V, static=True))
         return None, None, torch.zeros_like(ctx.holder.anchor), None
 
 
@@ -122,13 +166,16 @@ class SparseEmbedding(torch.nn.Module):
         """Applies the step's sparse gradients (optionally synchronised across ranks)."""
         if not self.sparse_grads:
             return 0
+        several = len(self.sparse_grads) > 1
         uids = torch.cat([u for u, _ in self.sparse_grads])
         rows = torch.cat([r for _, r in self.sparse_grads])
         self.sparse_grads.clear()
         if sync is not None:
             uids, rows = sync(uids, rows)
         # merge duplicate rows (several lookups, several ranks) with the deterministic
-        # segment sum so every replica applies bit-identical updates
-        uids, rows = segment_sum(uids, rows, self.table.shape[0])
+        # segment sum so every replica applies bit-identical updates (one lookup on one
+        # rank is already unique); static shapes keep the step free of host syncs
+        if several or sync is not None:
+            uids, rows = segment_sum(uids, rows, self.table.shape[0], static=True)
         sparse_adagrad(self.table.data, self.accum, uids.to(torch.int32).contiguous(), rows.contiguous(), lr)
         return int(uids.numel())
