@@ -76,7 +76,7 @@ def main():
             print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={ws}; using WORLD_SIZE", file=sys.stderr)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", comm.local_device(local))
     torch.cuda.set_device(dev)
 
     if args.model == "widedeep":

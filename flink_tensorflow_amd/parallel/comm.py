@@ -29,19 +29,27 @@ def world() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
+def local_device(local_rank: int) -> int:
+    """GPU index of a local rank (wraps when ranks outnumber visible GPUs — rehearsal only)."""
+    n = torch.cuda.device_count()
+    return local_rank % n if n else 0
+
+
 def init_distributed(backend: str | None = None, timeout_s: int = 600) -> bool:
     """Initialises the default process group when launched with WORLD_SIZE > 1."""
     rank, ws, local = world()
     if ws <= 1 or dist.is_initialized():
         return dist.is_initialized()
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # FTM_DIST_BACKEND=gloo rehearses the multi-rank flow with several ranks sharing
+        # one GPU (RCCL needs one GPU per rank)
+        backend = os.environ.get("FTM_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
     kw = {}
     if backend == "nccl":
-        torch.cuda.set_device(local)
-        kw["device_id"] = torch.device("cuda", local)
+        torch.cuda.set_device(local_device(local))
+        kw["device_id"] = torch.device("cuda", local_device(local))
     dist.init_process_group(backend, rank=rank, world_size=ws, timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return True
 
