@@ -23,9 +23,9 @@
 namespace {
 
 constexpr int D = 64;      // head dim
-constexpr int KB = 64;     // keys per block
 constexpr int VP = D + 8;  // V row pitch (elements): tr-read rows land on distinct banks
-constexpr int PP = KB + 8;
+constexpr int OP = D + 8;   // output staging row pitch
+constexpr int QP = 16 + 4;  // P^T row pitch: [key][16 q] tiles, 40-B rows (tr-read friendly)
 
 typedef short v4s __attribute__((ext_vector_type(4)));
 
@@ -36,15 +36,18 @@ FTM_DEVICE v4s tr_read(const bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)p);
 }
 
-template <int QB>
+// QB queries x KB keys per step (KB = 128 covers BERT's S <= 128 in ONE staging round:
+// no second K/V round trip and no online-softmax rescale)
+template <int QB, int KB>
 __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __restrict__ qkv, const int* __restrict__ ids,
                                                                bf16* __restrict__ out, int B, int S, int H, int pad_id,
                                                                float scale_log2e) {
   constexpr int NW = QB / 16;  // waves
   constexpr int NTH = NW * 64;
+  constexpr int NF = KB / 16;  // key fragments of S per wave
   __shared__ __attribute__((aligned(16))) bf16 Ks[KB * D];   // [key][d] swizzled
   __shared__ __attribute__((aligned(16))) bf16 Vs[KB * VP];  // [key][d] (+pad)
-  __shared__ __attribute__((aligned(16))) bf16 Ps[NW][16 * PP];
+  __shared__ __attribute__((aligned(16))) bf16 Ps[NW][KB * QP];  // per-wave P^T, reused for O staging
   __shared__ float kmask[KB];
 
   const int qblocks = (S + QB - 1) / QB;
@@ -104,10 +107,10 @@ __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __res
     }
     __syncthreads();
 
-    // ---- S = Q K^T  (16 q x 64 keys per wave: 4 fragments)
-    f32x4 s[4];
+    // ---- S = Q K^T  (16 q x KB keys per wave: NF fragments)
+    f32x4 s[NF];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
+    for (int n = 0; n < NF; ++n) {
       s[n] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -121,7 +124,7 @@ __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __res
     for (int r = 0; r < 4; ++r) {
       float mx = -INFINITY;
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
+      for (int n = 0; n < NF; ++n) {
         s[n][r] = s[n][r] * scale_log2e + kmask[n * 16 + (lane & 15)];
         mx = fmaxf(mx, s[n][r]);
       }
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __res
       alpha[r] = exp2f(mrow[r] - mref);
       float sum = 0.f;
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
+      for (int n = 0; n < NF; ++n) {
         const float pv = exp2f(s[n][r] - mref);
         s[n][r] = pv;
         sum += pv;
@@ -151,19 +154,25 @@ __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __res
     for (int n = 0; n < 4; ++n)
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[n][r] *= alpha[r];
-    // ---- P -> per-wave LDS tile [16 q][64 keys] (bf16)
+    // ---- P^T -> per-wave LDS tile [64 keys][16 q]: a lane's 4 rows r are 4 consecutive q
+    // of one key, i.e. one 8-byte store per fragment (instead of 4 scalar 2-byte stores)
     bf16* ps = Ps[wave];
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ps[((lane >> 4) * 4 + r) * PP + n * 16 + (lane & 15)] = f2bf(s[n][r]);
+    for (int n = 0; n < NF; ++n) {
+      bf16x4 pk;
+      pk[0] = f2bf(s[n][0]); pk[1] = f2bf(s[n][1]); pk[2] = f2bf(s[n][2]); pk[3] = f2bf(s[n][3]);
+      *reinterpret_cast<bf16x4*>(ps + (n * 16 + (lane & 15)) * QP + (lane >> 4) * 4) = pk;
+    }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P writes landed
     __builtin_amdgcn_wave_barrier();
     // ---- O += P V  (A = P[q][key]; B[key][d] by transposed reads of row-major V)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 pa = *reinterpret_cast<const bf16x8*>(ps + (lane & 15) * PP + ks * 32 + (lane >> 4) * 8);
+    for (int ks = 0; ks < KB / 32; ++ks) {
       const int key0 = ks * 32 + (lane >> 4) * 8;  // this lane group's 8 keys
+      // A = P[q][keys]: transposed reads of P^T (lane i <- q = i, 4 keys per read)
+      const bf16* psrc = ps + (key0 + trq) * QP + trp * 4;
+      const v4s plo = tr_read(psrc), phi = tr_read(psrc + 4 * QP);
+      const bf16x8 pa = __builtin_bit_cast(bf16x8, __builtin_shufflevector(plo, phi, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
         const bf16* src = Vs + (key0 + trq) * VP + n * 16 + trp * 4;
@@ -183,7 +192,7 @@ __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __res
   for (int r = 0; r < 4; ++r) {
     const float inv = lrow[r] > 0.f ? 1.f / lrow[r] : 0.f;
 #pragma unroll
-    for (int n = 0; n < 4; ++n) os[((lane >> 4) * 4 + r) * PP + n * 16 + (lane & 15)] = f2bf(o[n][r] * inv);
+    for (int n = 0; n < 4; ++n) os[((lane >> 4) * 4 + r) * OP + n * 16 + (lane & 15)] = f2bf(o[n][r] * inv);
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
@@ -194,7 +203,7 @@ __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __res
     const int q = qb * QB + wave * 16 + r;
     if (q < S)
       *reinterpret_cast<u32x4*>(out + (tok0 + q) * (H * D) + h * D + ch * 8) =
-          *reinterpret_cast<const u32x4*>(os + r * PP + ch * 8);
+          *reinterpret_cast<const u32x4*>(os + r * OP + ch * 8);
   }
 }
 
@@ -266,12 +275,12 @@ void attention_fwd_bf16(uintptr_t qkv, uintptr_t ids, uintptr_t out, int B, int 
   auto O = reinterpret_cast<bf16*>(out);
   if (S > 64) {  // 128-query blocks: K/V of a head staged once for S <= 128
     const int qblocks = (S + 127) / 128;
-    hipLaunchKernelGGL(attention_fwd_kernel<128>, dim3(B * H * qblocks), dim3(512), 0, st, Q, I, O, B, S, H, pad_id,
-                       scale * kLog2e);
+    hipLaunchKernelGGL((attention_fwd_kernel<128, 128>), dim3(B * H * qblocks), dim3(512), 0, st, Q, I, O, B, S, H,
+                       pad_id, scale * kLog2e);
   } else {
     const int qblocks = (S + 63) / 64;
-    hipLaunchKernelGGL(attention_fwd_kernel<64>, dim3(B * H * qblocks), dim3(256), 0, st, Q, I, O, B, S, H, pad_id,
-                       scale * kLog2e);
+    hipLaunchKernelGGL((attention_fwd_kernel<64, 64>), dim3(B * H * qblocks), dim3(256), 0, st, Q, I, O, B, S, H,
+                       pad_id, scale * kLog2e);
   }
   FTM_CHECK_LAUNCH();
 }
