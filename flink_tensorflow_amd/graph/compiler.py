@@ -592,13 +592,26 @@ class CompiledFunction:
             if b_dev is None:
                 b_dev = torch.zeros(Cout, dtype=torch.float32, device=self.device)
             self.params += [w_arr, b_dev]
+            pool = self._fusable_maxpool(last, act, out)
+            if pool is not None:
+                # ReLU stem + 3x3/s2 max pool in one kernel: the full-resolution stem
+                # output never reaches HBM
+                pnode, mpad, (Hp, Wp) = pool
+                out = self._new((N, Hp, Wp, Cout))
+                self._fused.add(pnode.name)
+            else:
+                mpad = None
 
-            def run_d(xin=xin, out=out, w_arr=w_arr, b_dev=b_dev, bn=bn):
+            def run_d(xin=xin, out=out, w_arr=w_arr, b_dev=b_dev, bn=bn, mpad=mpad):
                 K.conv2d_direct(xin.buf, w_arr, (KHe, KWe), Cout, b_dev, (sh, sw), (pt, pb, pl, pr), act,
                                 out=_target(out), out_channel_offset=_coff(out), bn=bn,
-                                out_scale=_eff_scale(out) if out.qscale is not None else None)
+                                out_scale=_eff_scale(out) if out.qscale is not None else None, maxpool_pad=mpad)
 
             self._emit(node.name, "conv", run_d, [xin], [out])
+            if pool is not None:
+                self.vals[(pool[0].name, 0)] = out
+                self.fused_pools = getattr(self, "fused_pools", 0) + 1
+                return
             self.vals[(last.name, 0)] = out
             self._alias_fused_outputs(absorbed, out)
             return
@@ -664,6 +677,31 @@ class CompiledFunction:
         self._alias_fused_outputs(absorbed, out)
         self.fused_shortcuts = getattr(self, "fused_shortcuts", 0) + 1
         return True
+
+    def _fusable_maxpool(self, last: Node, act, out: Val):
+        """The single consumer of a ReLU conv chain when it is a 3x3 / stride-2 NHWC
+        MaxPool whose padding is at most one row/column per side (ResNet's pool1):
+        ``(pool node, (top, bottom, left, right), (Hp, Wp))`` or None."""
+        if act != K.ACT_RELU or out.qscale is not None or out.dtype != torch.bfloat16:
+            return None
+        if any(TensorName.parse(f).name == last.name for f in self.fetch_names):
+            return None
+        cons = [c for c in self.cons.get(last.name, []) if c not in self._fused]
+        if len(cons) != 1 or self.graph[cons[0]].op != "MaxPool":
+            return None
+        pn = self.graph[cons[0]]
+        if pn.attr("data_format", "NHWC") != "NHWC" or list(pn.attr("ksize")) != [1, 3, 3, 1] \
+                or list(pn.attr("strides")) != [1, 2, 2, 1]:
+            return None
+        _, Ho, Wo, _ = out.shape
+        if pn.attr("padding", "VALID") == "SAME":
+            pt, pb = same_pads(Ho, 3, 2)
+            pl, pr = same_pads(Wo, 3, 2)
+        else:
+            pt = pb = pl = pr = 0
+        if max(pt, pb, pl, pr) > 1:
+            return None
+        return pn, (pt, pb, pl, pr), ((Ho + pt + pb - 3) // 2 + 1, (Wo + pl + pr - 3) // 2 + 1)
 
     def _use_dconv(self, cin_phys, KH, KW, stride, dil, es, residual, act) -> bool:
         """Direct LDS conv for narrow layers (input row <= 32 B: RGB stems, Inception's
@@ -1224,7 +1262,8 @@ class CompiledFunction:
             kinds[s.kind] = kinds.get(s.kind, 0) + 1
         return {"steps": len(self.steps), "kinds": kinds, "glue_ops": sorted(set(self.glue_ops)),
                 "hip_graph": self._graph_obj is not None, "precision": self.precision,
-                "fp8_layers": self.fp8_layers, "fused_shortcuts": getattr(self, "fused_shortcuts", 0)}
+                "fp8_layers": self.fp8_layers, "fused_shortcuts": getattr(self, "fused_shortcuts", 0),
+                "fused_pools": getattr(self, "fused_pools", 0)}
 
 
 def _root(v: Val) -> Val:

@@ -46,6 +46,11 @@ struct DconvParams {
   int PH, PW;  // patch rows / cols
   int ldy, y_coff;
   int tiles_h, tiles_w, tiles_n;
+  // POOL: fused 3x3 / stride-2 max pool of the (ReLU) conv output.  A workgroup owns a
+  // 7 x 8 pooled tile, i.e. a 15 x 17 conv tile (255 of the 256 fragment pixels, rows
+  // 14t - ppt.., cols 16t - ppl..); out-of-range conv positions enter the max as 0
+  // (exact after a ReLU).
+  int Hp, Wp, ppt, ppl;
 };
 
 FTM_DEVICE void glds16(const void* src, uint8_t* lds) {
@@ -60,7 +65,7 @@ FTM_DEVICE uint32_t pack4_fp8(float a, float b, float c, float d) {
   return (uint32_t)w;
 }
 
-template <int ES, int BN, int ACT, bool OUT_FP8>
+template <int ES, int BN, int ACT, bool OUT_FP8, bool POOL = false>
 __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int KL = ES == 2 ? 16 : 32;  // K bytes per lane per MFMA
@@ -76,7 +81,8 @@ __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
   const int tw = b % p.tiles_w; b /= p.tiles_w;
   const int th = b % p.tiles_h;
   const int n = b / p.tiles_h;
-  const int oy0 = th * TH, ox0 = tw * TW, n0 = tn * BN;
+  constexpr int TPW = POOL ? 17 : TW;  // conv tile width (pixel p of the tile = row p / TPW, col p % TPW)
+  const int oy0 = POOL ? th * 14 - p.ppt : th * TH, ox0 = POOL ? tw * 16 - p.ppl : tw * TW, n0 = tn * BN;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int patch_bytes = p.PH * p.PW * p.RB;
@@ -120,7 +126,10 @@ __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
   // patch row of fragment j's pixel for this lane at tap offset 0
   int prow0[J];
 #pragma unroll
-  for (int j = 0; j < J; ++j) prow0[j] = ((wave * J + j) * p.S) * p.PW + frow * p.S;
+  for (int j = 0; j < J; ++j) {
+    const int pix = (wave * J + j) * 16 + frow, r = pix / TPW, c = pix - r * TPW;
+    prow0[j] = (r * p.S) * p.PW + c * p.S;
+  }
 
   for (int s = 0; s < p.ksteps; ++s) {
     const int kb = s * 4 * KL + fq * KL;  // this lane group's K byte offset
@@ -178,6 +187,10 @@ __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = apply_act<ACT>(acc[i][j][r] * sv[r] + bv[r]);
+      if constexpr (POOL) {  // conv positions outside the image must not win the max
+        const int oy = oy0 + pl / TPW, ox = ox0 + pl % TPW;
+        if ((unsigned)oy >= (unsigned)p.Ho || (unsigned)ox >= (unsigned)p.Wo) v[0] = v[1] = v[2] = v[3] = 0.f;
+      }
       if constexpr (OUT_FP8) {
         *reinterpret_cast<uint32_t*>(Os + pl * OLD + cl) =
             pack4_fp8(v[0] * p.out_q, v[1] * p.out_q, v[2] * p.out_q, v[3] * p.out_q);
@@ -191,6 +204,28 @@ __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
   __syncthreads();
   constexpr int EPO = 16 / OB;
   constexpr int CPR = BN / EPO;
+  if constexpr (POOL) {
+    static_assert(!OUT_FP8, "pooled epilogue is bf16");
+    for (int q = tid; q < 56 * CPR; q += NT) {
+      const int pp = q / CPR, cc = q % CPR;
+      const int pyl = pp >> 3, pxl = pp & 7;
+      const int py = (oy0 + p.ppt) / 2 + pyl, px = (ox0 + p.ppl) / 2 + pxl;
+      const int c = n0 + cc * EPO;
+      if (py >= p.Hp || px >= p.Wp || c >= p.Cout) continue;
+      bf16x8 m = *reinterpret_cast<const bf16x8*>(Os + ((2 * pyl) * TPW + 2 * pxl) * OLD + cc * 16);
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(Os + ((2 * pyl + dy) * TPW + 2 * pxl + dx) * OLD + cc * 16);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) m[e] = (float)v[e] > (float)m[e] ? v[e] : m[e];
+        }
+      const size_t mo = ((size_t)n * p.Hp + py) * p.Wp + px;
+      *reinterpret_cast<bf16x8*>(p.y + (mo * p.ldy + p.y_coff + c) * 2) = m;
+    }
+    return;
+  }
   for (int q = tid; q < TH * TW * CPR; q += NT) {
     const int pl = q / CPR, cc = q % CPR;
     const int oy = oy0 + pl / TW, ox = ox0 + pl % TW;
@@ -205,6 +240,21 @@ __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
 template <int ES, int BN, bool OUT_FP8>
 void launch_act(const DconvParams& p, int act, size_t lds, hipStream_t s) {
   dim3 grid(p.N * p.tiles_h * p.tiles_w * p.tiles_n), block(NT);
+  if constexpr (ES == 2 && !OUT_FP8) {
+    if (p.Hp > 0) {  // fused max pool (ReLU stems)
+      if (act != ACT_RELU) throw std::invalid_argument("dconv: fused pool needs a ReLU conv");
+      static bool done = false;
+      if (!done) {
+        hipFuncSetAttribute((const void*)dconv_kernel<ES, BN, ACT_RELU, false, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        done = true;
+      }
+      hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_RELU, false, true>), grid, block, lds, s, p);
+      return;
+    }
+  } else {
+    if (p.Hp > 0) throw std::invalid_argument("dconv: fused pool is bf16-only");
+  }
   switch (act) {
     case ACT_NONE:
       hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_NONE, OUT_FP8>), grid, block, lds, s, p);
@@ -227,8 +277,8 @@ void set_lds_limit() {
 
 }  // namespace
 
-int dconv_lds_bytes(int es, int bn, int KH, int KW, int S, int Cin, int wp) {
-  const int PH = (TH - 1) * S + KH, PW = (TW - 1) * S + KW;
+int lds_bytes(int es, int bn, int KH, int KW, int S, int Cin, int wp, bool pool) {
+  const int PH = (TH - 1) * S + KH, PW = (pool ? TW : TW - 1) * S + KW;
   const int patch = PH * PW * Cin * es;
   const int ob = 2;  // bound by the bf16 output tile
   int need = ((patch + 1023) & ~1023) + bn * wp + 1024;  // + slack for a short last DMA
@@ -236,10 +286,14 @@ int dconv_lds_bytes(int es, int bn, int KH, int KW, int S, int Cin, int wp) {
   return need > epi ? need : epi;
 }
 
+int dconv_lds_bytes(int es, int bn, int KH, int KW, int S, int Cin, int wp) {
+  return lds_bytes(es, bn, KH, KW, S, Cin, wp, false);
+}
+
 // x: NHWC (bf16 es=2 / e4m3 es=1); w: host-arranged [Cout_pad][wp] bytes.
 void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t y, int es, int N, int H, int W,
            int Cin, int Cout, int KH, int KW, int S, int ph, int pw, int Ho, int Wo, int wp, int ldy, int y_coff,
-           int out_fp8, float out_q, int act, int bn, uintptr_t stream) {
+           int out_fp8, float out_q, int act, int bn, uintptr_t stream, int Hp, int Wp, int ppt, int ppl) {
   const int KL = es == 2 ? 16 : 32;
   if (es != 1 && es != 2) throw std::invalid_argument("dconv: es must be 1 or 2");
   if ((Cin * es) % KL) throw std::invalid_argument("dconv: Cin*es must be a multiple of " + std::to_string(KL));
@@ -252,7 +306,7 @@ void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t 
   if (S != 1 && S != 2) throw std::invalid_argument("dconv: stride must be 1 or 2");
   if (!bias || (es == 1 && !scale)) throw std::invalid_argument("dconv: bias (and fp8 scale) required");
   if (x % 16 || w % 16 || y % 16 || bias % 16 || (scale && scale % 16)) throw std::invalid_argument("dconv: alignment");
-  const int lds = dconv_lds_bytes(es, bn, KH, KW, S, Cin, wp);
+  const int lds = lds_bytes(es, bn, KH, KW, S, Cin, wp, Hp > 0);
   if (lds > 160 * 1024) throw std::invalid_argument("dconv: tile does not fit LDS (" + std::to_string(lds) + " B)");
   DconvParams p{};
   p.x = reinterpret_cast<const uint8_t*>(x);
@@ -267,10 +321,19 @@ void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t 
   p.WP = wp;
   p.ksteps = kpad / (4 * KL);
   p.PH = (TH - 1) * S + KH;
-  p.PW = (TW - 1) * S + KW;
+  p.PW = (Hp > 0 ? TW : TW - 1) * S + KW;  // pooled tiles are 17 conv columns wide
   p.ldy = ldy; p.y_coff = y_coff;
-  p.tiles_h = (Ho + TH - 1) / TH;
-  p.tiles_w = (Wo + TW - 1) / TW;
+  p.Hp = Hp; p.Wp = Wp; p.ppt = ppt; p.ppl = ppl;
+  if (Hp > 0) {  // pooled tiles of 7 x 8 (15 x 17 conv pixels)
+    if (ppt < 0 || ppt > 1 || ppl < 0 || ppl > 1) throw std::invalid_argument("dconv: pool padding must be 0/1");
+    if ((Hp - 1) * 2 + 3 > Ho + ppt + 1 || (Wp - 1) * 2 + 3 > Wo + ppl + 1)
+      throw std::invalid_argument("dconv: pooled shape inconsistent with conv output");
+    p.tiles_h = (Hp + 6) / 7;
+    p.tiles_w = (Wp + 7) / 8;
+  } else {
+    p.tiles_h = (Ho + TH - 1) / TH;
+    p.tiles_w = (Wo + TW - 1) / TW;
+  }
   p.tiles_n = (Cout + bn - 1) / bn;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 #define FTM_DCONV(ES_, BN_, OF_)            \

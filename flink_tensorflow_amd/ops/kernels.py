@@ -469,10 +469,13 @@ def dconv_bf16_weight_bytes(w_ohwi: torch.Tensor, bn: int) -> torch.Tensor:
 
 def conv2d_direct(x: torch.Tensor, w_arr: torch.Tensor, kshape, Cout: int, bias: torch.Tensor, stride=(1, 1),
                   pad=(0, 0, 0, 0), act=None, out: torch.Tensor | None = None, out_channel_offset: int = 0,
-                  bn: int = 64, chan_scale: torch.Tensor | None = None, out_scale: float | None = None) -> torch.Tensor:
+                  bn: int = 64, chan_scale: torch.Tensor | None = None, out_scale: float | None = None,
+                  maxpool_pad: tuple | None = None) -> torch.Tensor:
     """Direct conv on device: ``x`` NHWC bf16 (``chan_scale`` None) or e4m3 bytes (uint8, with
     the per-channel dequant scale ``chan_scale``); ``w_arr`` from :func:`dconv_weights`;
-    ``out_scale`` → e4m3 output.  Device-only (the host paths use the reference convs)."""
+    ``out_scale`` → e4m3 output.  ``maxpool_pad = (top, bottom, left, right)`` fuses a 3x3 /
+    stride-2 max pool of the ReLU output (ResNet stem → pool1).  Device-only (the host
+    paths use the reference convs)."""
     N, H, W, Cin = x.shape
     KH, KW = kshape
     s = stride[0]
@@ -480,11 +483,17 @@ def conv2d_direct(x: torch.Tensor, w_arr: torch.Tensor, kshape, Cout: int, bias:
     Ho, Wo = conv_out_hw(H, W, KH, KW, s, s, pt, pl, 1, 1, pb, pr)
     es = 2 if x.dtype == torch.bfloat16 else 1
     out_fp8 = out_scale is not None
+    Hp = Wp = ppt = ppl = 0
+    oh, ow = Ho, Wo
+    if maxpool_pad is not None:
+        ppt, ppb, ppl, ppr = maxpool_pad
+        Hp, Wp = (Ho + ppt + ppb - 3) // 2 + 1, (Wo + ppl + ppr - 3) // 2 + 1
+        oh, ow = Hp, Wp
     if out is None:
-        out = torch.empty((N, Ho, Wo, Cout), dtype=torch.uint8 if out_fp8 else torch.bfloat16, device=x.device)
+        out = torch.empty((N, oh, ow, Cout), dtype=torch.uint8 if out_fp8 else torch.bfloat16, device=x.device)
         out_channel_offset = 0
-    if out.shape[:3] != (N, Ho, Wo) or out_channel_offset + Cout > out.shape[3]:
-        raise ValueError(f"conv2d_direct: out {tuple(out.shape)} cannot hold [{N},{Ho},{Wo},{Cout}]")
+    if out.shape[:3] != (N, oh, ow) or out_channel_offset + Cout > out.shape[3]:
+        raise ValueError(f"conv2d_direct: out {tuple(out.shape)} cannot hold [{N},{oh},{ow},{Cout}]")
     if es == 1 and chan_scale is None:
         raise ValueError("conv2d_direct: fp8 input needs chan_scale")
     _check(x, "x", x.dtype, x.device)
@@ -492,7 +501,7 @@ def conv2d_direct(x: torch.Tensor, w_arr: torch.Tensor, kshape, Cout: int, bias:
     _check(bias, "bias", torch.float32, x.device)
     _hip().dconv(x.data_ptr(), w_arr.data_ptr(), _ptr(chan_scale), bias.data_ptr(), out.data_ptr(), es, N, H, W, Cin,
                  Cout, KH, KW, s, pt, pl, Ho, Wo, w_arr.shape[1], out.shape[3], out_channel_offset, int(out_fp8),
-                 1.0 / out_scale if out_fp8 else 1.0, act_code(act), bn, _stream())
+                 1.0 / out_scale if out_fp8 else 1.0, act_code(act), bn, _stream(), Hp, Wp, ppt, ppl)
     return out
 
 

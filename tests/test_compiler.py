@@ -21,6 +21,8 @@ def _check_plan(graph, device, imgs):
     # 29 convs, the 4 projection shortcuts fused into their unit's expansion conv
     assert s["glue_ops"] == [] and s["kinds"]["conv"] == 25 and s["fused_shortcuts"] == 4
     assert s["kinds"]["preprocess"] == 1
+    # on the GPU the stem runs on the direct conv with pool1 fused into its epilogue
+    assert s["fused_pools"] == (1 if torch.device(device).type == "cuda" else 0)
     logits, idx = plan({"images:0": imgs.to(device)})
     err = (logits.cpu() - ref[0]).abs().max().item() / ref[0].abs().max().item()
     assert err < 0.05, err

@@ -83,3 +83,36 @@ def test_dconv_fp8_gpu(case):
     assert (gd == rd).float().mean() > 0.97
     if extra:
         assert (out[..., :off] == 0).all() and (out[..., off + Cout:] == 0).all()
+
+
+POOL_CASES = [  # N, H, W, Cin, Cout, (kh, kw), stride, pad, pool padding (TF "SAME"/"VALID"), bn
+    (2, 56, 56, 16, 64, (4, 4), 1, (2, 1, 2, 1), "SAME", 64),  # ResNet s2d stem at 1/2 scale
+    (1, 45, 39, 8, 32, (3, 3), 1, (1, 1, 1, 1), "SAME", 32),  # odd sizes: pads 1/1
+    (2, 33, 30, 16, 64, (3, 3), 1, (1, 1, 1, 1), "VALID", 64),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", POOL_CASES)
+def test_dconv_maxpool_gpu(case):
+    """Stem conv + ReLU + fused 3x3/s2 max pool == conv then pool (the same bf16 values
+    are compared inside the max, so the results are exact up to conv rounding)."""
+    N, H, W, Cin, Cout, (kh, kw), s, pad, ppad, bn = case
+    torch.manual_seed(H * W + Cin)
+    x = torch.randn(N, H, W, Cin).to(torch.bfloat16)
+    w = (torch.randn(Cout, kh, kw, Cin) / (kh * kw * Cin) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout) * 0.1
+    conv = K.conv2d_nhwc(x, w, b, None, (s, s), pad, (1, 1), "relu")
+    Ho, Wo = conv.shape[1:3]
+    if ppad == "SAME":
+        ph = max((-(-Ho // 2) - 1) * 2 + 3 - Ho, 0)
+        pw = max((-(-Wo // 2) - 1) * 2 + 3 - Wo, 0)
+        mp = (ph // 2, ph - ph // 2, pw // 2, pw - pw // 2)
+    else:
+        mp = (0, 0, 0, 0)
+    ref = K.pool2d_nhwc(conv, (3, 3), (2, 2), mp, "max")
+    arr = K.dconv_bf16_weight_bytes(w.float(), bn).to(DEV)
+    got = K.conv2d_direct(x.to(DEV), arr, (kh, kw), Cout, b.to(DEV), (s, s), pad, "relu", bn=bn,
+                          maxpool_pad=mp).cpu()
+    assert got.shape == ref.shape
+    torch.testing.assert_close(got.float(), ref.float(), rtol=2e-2, atol=2e-2 * ref.abs().max().item())
