@@ -11,6 +11,7 @@
 //                                   10,000-byte cap and with a working inverse)
 //   * CRC32C + LevelDB-table build/parse for TensorBundle V2 checkpoints
 //                                  (SaveV2/RestoreV2 driven by LIB/io/Saver.scala:55-89)
+//   * tensor-arena offset planning / allocation (arena.cpp)
 //   * multithreaded gather of record payloads into one pinned staging slot
 //                                  (the micro-batch assembler; no reference analogue:
 //                                   the reference runs batch 1)
@@ -20,6 +21,8 @@
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+
+#include "native.h"
 
 #include <algorithm>
 #include <atomic>
@@ -36,8 +39,6 @@
 #if defined(__SSE4_2__)
 #include <nmmintrin.h>
 #endif
-
-namespace py = pybind11;
 
 namespace {
 
@@ -863,6 +864,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("sstable_parse", &sstable_parse, py::arg("data"), py::arg("verify") = true);
   m.def("gather_into", &gather_into, py::arg("dst"), py::arg("dst_bytes"), py::arg("srcs"), py::arg("stride"),
         py::arg("nthreads") = 8);
+  register_arena(m);
   m.attr("has_sse42") =
 #if defined(__SSE4_2__)
       true;

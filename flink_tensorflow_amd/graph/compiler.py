@@ -20,7 +20,9 @@ This is the MI355X replacement of libtensorflow's session executor for the hot p
    * ``ConcatV2`` on channels → producers write straight into channel slices of one
      buffer (no copy) when every producer is a kernel that supports it;
    * everything else runs as captured PyTorch glue ops (logged; ``strict=True`` rejects).
-4. **memory planning**: liveness-based reuse of exact-size HBM buffers;
+4. **memory planning**: every intermediate gets an offset in one activation slab from the
+   native liveness planner (``csrc/arena.cpp``); with a subtask ``DeviceArena`` the slab is
+   shared by all of the subtask's bucket plans and identical weights are stored once;
 5. **capture**: one hipGraph per (signature, batch size).
 
 Activations are bf16 NHWC on device; fetched outputs are cast back to the graph dtype.
@@ -104,10 +106,13 @@ class _ConstSession:
 class CompiledFunction:
     def __init__(self, graph: Graph, feeds: dict[str, tuple[tuple, Any]], fetches: list[str], device,
                  variables: dict | None = None, use_graph: bool = True, strict: bool = False,
-                 topk_fetch: bool = True, precision: str = "bf16", calibration: dict | None = None):
+                 topk_fetch: bool = True, precision: str = "bf16", calibration: dict | None = None,
+                 arena=None):
         if precision not in ("bf16", "fp8"):
             raise ValueError(f"precision must be bf16 or fp8, not {precision!r}")
         self.graph = graph
+        self.arena = arena  # subtask DeviceArena (shared slab + interned weights) or None
+        self.activation_bytes = 0
         self.precision = precision
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -121,7 +126,6 @@ class CompiledFunction:
         self.params: list[torch.Tensor] = []  # device weights/biases baked into the plan
         self.glue_ops: list[str] = []
         self.vals: dict[tuple[str, int], Val] = {}
-        self._pool: dict[int, list[torch.Tensor]] = {}
         self._fused: set[str] = set()
         self._const_sess = _ConstSession(self.variables)
         self._input_bufs: dict[str, torch.Tensor] = {}
@@ -569,8 +573,8 @@ class CompiledFunction:
             w_ohwi = w.permute(3, 0, 1, 2).contiguous()
             if cin_pad != Cin:
                 w_ohwi = torch.nn.functional.pad(w_ohwi, (0, cin_pad - Cin))
-        w_dev = w_ohwi.to(self.device, torch.bfloat16).contiguous()
-        b_dev = bias.to(self.device, torch.float32).contiguous() if bias is not None else None
+        w_dev = self._dev(w_ohwi, torch.bfloat16)
+        b_dev = self._dev(bias, torch.float32) if bias is not None else None
         self.params += [w_dev] + ([b_dev] if b_dev is not None else [])
         out = self._new((N, Ho, Wo, Cout))
         if (self.precision == "fp8" and residual is None and act in (K.ACT_NONE, K.ACT_RELU) and Cout % 16 == 0
@@ -588,7 +592,7 @@ class CompiledFunction:
         KHe, KWe = w_ohwi.shape[1], w_ohwi.shape[2]
         if self._use_dconv(cin_pad, KHe, KWe, (sh, sw), (dh, dw), 2, residual, act):
             bn = 64 if Cout >= 64 else 32
-            w_arr = K.dconv_bf16_weight_bytes(w_ohwi, bn).to(self.device)
+            w_arr = self._dev(K.dconv_bf16_weight_bytes(w_ohwi, bn))
             if b_dev is None:
                 b_dev = torch.zeros(Cout, dtype=torch.float32, device=self.device)
             self.params += [w_arr, b_dev]
@@ -663,8 +667,8 @@ class CompiledFunction:
                 self.params = [q for q in self.params if q is not t]
         w_cat = torch.cat([w_ohwi.reshape(Cout, K1), sc["w"].reshape(Cout, C2)], 1)
         b = (bias if bias is not None else torch.zeros(Cout)) + (sc["bias"] if sc["bias"] is not None else 0)
-        w_dev = w_cat.to(self.device, torch.bfloat16).contiguous()
-        b_dev = b.to(self.device, torch.float32).contiguous()
+        w_dev = self._dev(w_cat, torch.bfloat16)
+        b_dev = self._dev(b, torch.float32)
         self.params += [w_dev, b_dev]
         for a in absorbed:
             self._fused.add(a.name)
@@ -723,10 +727,10 @@ class CompiledFunction:
         wq, ws = F8.quantize_weight(w_ohwi)
         x_scale = x.qscale if x.qscale is not None else self._qscale(node.inputs[0][0])
         dev = self.device
-        wq_dev = wq.to(dev)
-        ws_dev = ws.to(dev)
-        cs_dev = (ws * x_scale).to(dev, torch.float32).contiguous()
-        b_dev = bias.to(dev, torch.float32).contiguous() if bias is not None else \
+        wq_dev = self._dev(wq)
+        ws_dev = self._dev(ws)
+        cs_dev = self._dev(ws * x_scale, torch.float32)
+        b_dev = self._dev(bias, torch.float32) if bias is not None else \
             torch.zeros(Cout, dtype=torch.float32, device=dev)
         self.params += [wq_dev, cs_dev, b_dev]
         o_scale = self._qscale(last.name) if self._fp8_consumers_ok(last.name) else None
@@ -737,7 +741,7 @@ class CompiledFunction:
         self.fp8_layers += 1
         if x.qscale is not None and self._use_dconv(Cin, KH, KW, stride, dil, 1, None, act):
             bn = 64 if Cout >= 64 else 32
-            w_arr = K.dconv_weights(wq, Cout, 1, bn).to(dev)
+            w_arr = self._dev(K.dconv_weights(wq, Cout, 1, bn))
             self.params.append(w_arr)
 
             def run_d(x=x, out=out, w_arr=w_arr, cs=cs_dev, b=b_dev, bn=bn):
@@ -810,8 +814,8 @@ class CompiledFunction:
         if n_pad != N:
             w_nk = torch.nn.functional.pad(w_nk, (0, 0, 0, n_pad - N))
             bias = torch.nn.functional.pad(bias if bias is not None else torch.zeros(N), (0, n_pad - N))
-        w_dev = w_nk.to(self.device, torch.bfloat16).contiguous()
-        b_dev = bias.to(self.device, torch.float32).contiguous() if bias is not None else None
+        w_dev = self._dev(w_nk, torch.bfloat16)
+        b_dev = self._dev(bias, torch.float32) if bias is not None else None
         self.params += [w_dev] + ([b_dev] if b_dev is not None else [])
         out = self._new((a.shape[0], N), phys_c=n_pad if n_pad != N else None)
         if n_pad != N:
@@ -1097,36 +1101,52 @@ class CompiledFunction:
 
     # ================================================================== memory
     def _plan_memory_and_bind(self):
-        # feeds get dedicated input buffers
+        """Feeds and fetched values get persistent buffers (arena blocks); every other
+        produced value lives at a planned offset of one activation slab — lifetimes
+        [producing step, last reading step] never overlap in memory (native liveness
+        planner, ``batching/arena.py``).  With a subtask arena the slab is shared by all
+        of the subtask's plans (they replay serially on one stream)."""
+        from ..batching.arena import plan_offsets
+
         for f in self.feed_names:
             tn = TensorName.parse(f)
             v = self.vals[(tn.name, tn.index)]
-            v.buf = torch.empty(v.shape, dtype=v.dtype, device=self.device)
+            v.buf = self._persistent(v.shape, v.dtype)
             self._input_bufs[f] = v.buf
         fetch_vals = [self.vals[(TensorName.parse(f).name, TensorName.parse(f).index)] for f in self.fetch_names]
         for i, s in enumerate(self.steps):
             for v in s.inputs:
                 _root(v).last_use = max(_root(v).last_use, i)
         keep = {id(_root(v)) for v in fetch_vals}
+        owners: dict[int, Val] = {}   # buffer-owning values in order of first production
+        born: dict[int, int] = {}
         for i, s in enumerate(self.steps):
             for o in s.outputs:
                 r = _root(o)
-                if r.buf is None:
-                    tgt = r.concat_slot[0] if r.concat_slot else None
-                    if tgt is not None:
-                        if tgt.buf is None:
-                            tgt.buf = self._alloc(tgt.shape, tgt.dtype, keep_forever=id(tgt) in keep)
-                            tgt.last_use = max(tgt.last_use, max((c.last_use for c in getattr(tgt, "_concat_children", [])), default=-1))
-                        continue
-                    shape = getattr(r, "buf_shape", None) or (*r.shape[:-1], r.phys_c) if r.phys_c else r.shape
-                    r.buf = self._alloc(tuple(shape), r.dtype, keep_forever=id(r) in keep)
-            # release buffers whose last use is this step
-            for v in {id(_root(x)): _root(x) for x in s.inputs}.values():
-                if v.last_use == i and id(v) not in keep and v.buf is not None and not v.is_const \
-                        and not any(v is self.vals.get((TensorName.parse(f).name, TensorName.parse(f).index))
-                                    for f in self.feed_names):
-                    self._free(v.buf)
-                    self._poison_after.setdefault(i, []).append(v.buf)
+                if r.buf is not None:
+                    continue
+                tgt = r.concat_slot[0] if r.concat_slot else r  # branches write into their concat
+                if tgt.buf is None and id(tgt) not in owners:
+                    owners[id(tgt)] = tgt
+                    born[id(tgt)] = i
+        for t in owners.values():
+            t.last_use = max([t.last_use] + [c.last_use for c in getattr(t, "_concat_children", [])])
+        transient = []
+        for k, t in owners.items():
+            if k in keep:
+                t.buf = self._persistent(_buf_shape(t), t.dtype)
+            else:
+                transient.append(t)
+        sizes = [_nbytes(_buf_shape(t), t.dtype) for t in transient]
+        first = [born[id(t)] for t in transient]
+        last = [max(born[id(t)], t.last_use) for t in transient]
+        offs, total = plan_offsets(sizes, first, last)
+        self.activation_bytes = total
+        slab = self.arena.shared_slab(total) if self.arena is not None else \
+            torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
+        for t, off, nb, lu in zip(transient, offs, sizes, last):
+            t.buf = slab[off:off + nb].view(t.dtype).view(tuple(_buf_shape(t)))
+            self._poison_after.setdefault(lu, []).append(t.buf)
         for v in self.vals.values():
             if v.alias_of is not None:
                 r = _root(v)
@@ -1139,19 +1159,19 @@ class CompiledFunction:
             else:
                 self._outputs.append(fv)
 
-    def _alloc(self, shape, dtype, keep_forever=False):
-        nbytes = int(np.prod(shape)) * torch.empty((), dtype=dtype).element_size()
-        lst = self._pool.get(nbytes)
-        if lst and not keep_forever:
-            raw = lst.pop()
-        else:
-            raw = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
-        return raw[:nbytes].view(dtype).view(shape)
+    def _persistent(self, shape, dtype) -> torch.Tensor:
+        """A buffer outside the shared slab (plan inputs, fetched outputs)."""
+        if self.arena is not None:
+            return self.arena.alloc(tuple(shape), dtype)
+        return torch.empty(tuple(shape), dtype=dtype, device=self.device)
 
-    def _free(self, buf: torch.Tensor):
-        raw = buf.view(-1).view(torch.uint8) if buf.numel() else None
-        if raw is not None:
-            self._pool.setdefault(raw.numel(), []).append(raw)
+    def _dev(self, t: torch.Tensor, dtype=None) -> torch.Tensor:
+        """A baked-in weight on the device; identical weights of a subtask's bucket plans
+        are stored once in its arena."""
+        t = t.to(dtype) if dtype is not None else t
+        if self.arena is not None:
+            return self.arena.intern(t.contiguous())
+        return t.to(self.device).contiguous()
 
     # ================================================================== execution
     def _run_steps(self):
@@ -1263,7 +1283,19 @@ class CompiledFunction:
         return {"steps": len(self.steps), "kinds": kinds, "glue_ops": sorted(set(self.glue_ops)),
                 "hip_graph": self._graph_obj is not None, "precision": self.precision,
                 "fp8_layers": self.fp8_layers, "fused_shortcuts": getattr(self, "fused_shortcuts", 0),
-                "fused_pools": getattr(self, "fused_pools", 0)}
+                "fused_pools": getattr(self, "fused_pools", 0), "activation_bytes": self.activation_bytes,
+                "param_bytes": self.param_bytes()}
+
+
+def _buf_shape(r: Val) -> tuple:
+    """Physical buffer shape of a value (channel-padded / space-to-depth stem inputs)."""
+    if r.phys_c:
+        return tuple(getattr(r, "buf_shape", None) or (*r.shape[:-1], r.phys_c))
+    return tuple(r.shape)
+
+
+def _nbytes(shape, dtype) -> int:
+    return int(np.prod(shape, dtype=np.int64)) * torch.empty((), dtype=dtype).element_size()
 
 
 def _root(v: Val) -> Val:

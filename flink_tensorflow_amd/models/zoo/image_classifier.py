@@ -26,7 +26,7 @@ from ..core import DefaultGraphLoader, GenericModel, GraphDefGraphLoader, GraphL
 
 
 class ImageClassifierModel(GenericModel, BatchedGpuModel):
-    _TRANSIENT = ("_graph", "_session", "_plans", "_runner")
+    _TRANSIENT = ("_graph", "_session", "_plans", "_runner", "_arena")
 
     def __init__(self, graph_source: Callable[[], GraphDef] | str, image_hw: tuple[int, int],
                  buckets: Sequence[int] = (64, 256), top_k: int = 5, labels: Sequence[str] | None = None,
@@ -46,6 +46,7 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
         self.use_graph = use_graph
         self._plans: dict | None = None
         self._runner = None
+        self._arena = None
 
     @property
     def graph_loader(self) -> GraphLoader:
@@ -60,11 +61,17 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
         if dev.type == "cuda":
             from ...batching.engine import PipelinedGpuRunner
 
+            from ...batching.arena import DeviceArena
+            from ...config import EngineConfig
+
             H, W = self.image_hw
+            # one arena per subtask: the bucket plans share its activation slab (largest
+            # compiled first) and its interned weights
+            self._arena = DeviceArena(dev, EngineConfig().arena_bytes(dev), name=type(self).__name__)
             self._plans = {b: CompiledFunction(self._graph, {self.feed: ((b, H, W, 3), "UINT8")}, self.fetches, dev,
                                                use_graph=self.use_graph, strict=True, precision=self.precision,
-                                               calibration=self._calibration(b))
-                           for b in self.buckets}
+                                               calibration=self._calibration(b), arena=self._arena)
+                           for b in sorted(self.buckets, reverse=True)}
             self._runner = PipelinedGpuRunner(self._plans, self.feed, lambda p: p.output_tensors(), (H, W, 3),
                                               torch.uint8, depth=self.depth, device=dev)
 
@@ -80,6 +87,7 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
             self._runner.drain()
         self._runner = None
         self._plans = None
+        self._arena = None
         super().close()
 
     def label_of(self, i: int) -> str:

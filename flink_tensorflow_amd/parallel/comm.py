@@ -91,7 +91,11 @@ def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0) -> int:
     if not is_dist():
         return 0
     by_dtype: dict = {}
-    for t in tensors:
+    seen = set()
+    for t in tensors:  # plans of one arena share interned weights: send each storage once
+        if t.data_ptr() in seen and t.numel():
+            continue
+        seen.add(t.data_ptr())
         by_dtype.setdefault((t.dtype, t.device), []).append(t)
     total = 0
     for (dt, dev), ts in sorted(by_dtype.items(), key=lambda kv: str(kv[0])):

@@ -224,14 +224,19 @@ class _Task:
         self.thread.start()
 
     def _guarded(self):
+        done = False
         try:
             self.run()
+            done = True
         except JobCancelled:
             pass
         except BaseException as e:  # noqa: BLE001
             self.job.fail(self, e, traceback.format_exc())
         finally:
-            if self.job.coordinator is not None:
+            # only a task that ran to its end stops being expected by checkpoints: a failed
+            # or cancelled task must not let an in-flight checkpoint complete without its
+            # state (the restart would restore the sources' offsets but lose this task's)
+            if done and self.job.coordinator is not None:
                 self.job.coordinator.task_finished((self.uid, self.subtask))
 
     def run(self):
@@ -429,6 +434,8 @@ class LocalExecutor:
             if self.error is None:
                 self.error = (task, exc, tb)
         LOG.error("task %s[%d] failed: %s", task.node.name, task.subtask, exc)
+        if self.coordinator is not None:
+            self.coordinator.abort_pending()  # no checkpoint of a failed attempt may complete
         self.cancel.set()
         for s in self.sources:
             try:

@@ -1,0 +1,99 @@
+"""Tensor arena: native liveness offset planner, first-fit allocator, and compiled plans
+sharing one subtask arena (activation slab + interned weights)."""
+import pytest
+import torch
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from flink_tensorflow_amd import _ext
+from flink_tensorflow_amd.batching.arena import ArenaExhausted, DeviceArena, plan_offsets
+from flink_tensorflow_amd.graph.compiler import CompiledFunction
+from flink_tensorflow_amd.graph.graph import Graph
+from flink_tensorflow_amd.models.zoo.resnet import resnet50_graph_def
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.tuples(st.integers(0, 5000), st.integers(0, 30), st.integers(0, 10)), min_size=1, max_size=40))
+def test_plan_offsets_never_overlaps_live_buffers(bufs):
+    sizes = [b[0] for b in bufs]
+    first = [b[1] for b in bufs]
+    last = [b[1] + b[2] for b in bufs]
+    offs, total = plan_offsets(sizes, first, last, 64)
+    ext = [(o, o + max(-(-max(s, 1) // 64) * 64, 64)) for o, s in zip(offs, sizes)]
+    for i in range(len(bufs)):
+        assert offs[i] % 64 == 0 and ext[i][1] <= total
+        for j in range(i):
+            if last[i] < first[j] or last[j] < first[i]:
+                continue  # never alive together
+            assert ext[i][1] <= ext[j][0] or ext[j][1] <= ext[i][0], (i, j)
+    # never worse than giving every buffer its own region
+    assert total <= sum(e - s for s, e in ext)
+
+
+def test_plan_offsets_reuses_dead_memory():
+    # a chain: each buffer is read only by the next step -> two regions suffice
+    n = 10
+    offs, total = plan_offsets([1 << 20] * n, list(range(n)), [i + 1 for i in range(n)], 256)
+    assert total == 2 << 20 and len(set(offs)) == 2
+
+
+def test_offset_allocator_coalesces():
+    a = _ext.native().OffsetAllocator(1 << 12, 256)
+    blocks = [a.alloc(256) for _ in range(16)]
+    assert blocks == [i * 256 for i in range(16)] and a.alloc(1) == -1
+    for b in blocks[4:12]:
+        a.free(b)
+    assert a.largest_free == 8 * 256 and a.num_free_blocks == 1
+    assert a.alloc(8 * 256) == 4 * 256
+    with pytest.raises(ValueError):
+        a.free(123)
+    assert a.peak == 1 << 12
+
+
+@pytest.fixture(scope="module")
+def small_graph():
+    return Graph.from_graph_def(resnet50_graph_def(depth=26, image_hw=(48, 48), num_classes=32))
+
+
+def test_bucket_plans_share_one_arena(small_graph):
+    arena = DeviceArena("cpu", budget_bytes=1 << 30)
+    feeds = lambda b: {"images:0": ((b, 48, 48, 3), "UINT8")}  # noqa: E731
+    p4 = CompiledFunction(small_graph, feeds(4), ["logits:0"], "cpu", strict=True, arena=arena)
+    p2 = CompiledFunction(small_graph, feeds(2), ["logits:0"], "cpu", strict=True, arena=arena)
+    st_ = arena.stats()
+    # the smaller bucket reuses the bigger bucket's slab and its weights
+    assert st_["slab_bytes"] == p4.activation_bytes >= p2.activation_bytes and st_["retired_slab_bytes"] == 0
+    assert st_["interned_hits"] >= len(p2.params) - 2
+    assert {t.data_ptr() for t in p2.params} <= {t.data_ptr() for t in p4.params}
+    imgs = torch.randint(0, 256, (4, 48, 48, 3), dtype=torch.uint8)
+    ref4 = CompiledFunction(small_graph, feeds(4), ["logits:0"], "cpu", strict=True)({"images:0": imgs})[0]
+    ref2 = CompiledFunction(small_graph, feeds(2), ["logits:0"], "cpu", strict=True)({"images:0": imgs[:2]})[0]
+    # interleaved replays on the shared slab give the private plans' results
+    for _ in range(2):
+        torch.testing.assert_close(p2({"images:0": imgs[:2]})[0], ref2)
+        torch.testing.assert_close(p4({"images:0": imgs})[0], ref4)
+    # the planned slab is far smaller than one buffer per produced value
+    produced = sum(o.buf.numel() * o.buf.element_size() for s in p4.steps for o in s.outputs if o.buf is not None)
+    assert p4.activation_bytes < 0.5 * produced
+
+
+def test_arena_budget_is_enforced(small_graph):
+    arena = DeviceArena("cpu", budget_bytes=1 << 20, chunk_bytes=1 << 16)
+    with pytest.raises(ArenaExhausted):
+        CompiledFunction(small_graph, {"images:0": ((8, 48, 48, 3), "UINT8")}, ["logits:0"], "cpu", arena=arena)
+
+
+@pytest.mark.gpu
+def test_arena_plans_gpu(small_graph):
+    dev = torch.device("cuda", 0)
+    arena = DeviceArena(dev, budget_bytes=8 << 30)
+    feeds = lambda b: {"images:0": ((b, 48, 48, 3), "UINT8")}  # noqa: E731
+    p4 = CompiledFunction(small_graph, feeds(4), ["logits:0"], dev, strict=True, arena=arena)
+    p2 = CompiledFunction(small_graph, feeds(2), ["logits:0"], dev, strict=True, arena=arena)
+    assert p4.summary()["hip_graph"] and arena.stats()["interned_hits"] > 0
+    imgs = torch.randint(0, 256, (4, 48, 48, 3), dtype=torch.uint8)
+    ref4 = CompiledFunction(small_graph, feeds(4), ["logits:0"], dev, strict=True)({"images:0": imgs.to(dev)})[0]
+    ref2 = CompiledFunction(small_graph, feeds(2), ["logits:0"], dev, strict=True)({"images:0": imgs[:2].to(dev)})[0]
+    for _ in range(2):
+        torch.testing.assert_close(p2({"images:0": imgs[:2].to(dev)})[0], ref2)
+        torch.testing.assert_close(p4({"images:0": imgs.to(dev)})[0], ref4)

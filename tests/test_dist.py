@@ -24,7 +24,9 @@ def _worker(rank, world, port, fn, q):
         from flink_tensorflow_amd.parallel import comm
 
         comm.init_distributed(backend="gloo")
-        q.put((rank, fn(rank, world)))
+        # tensors cross the queue as numpy: torch's fd-sharing pickler needs the child alive
+        # until the parent unpickles, which races with the child's exit
+        q.put((rank, _to_numpy(fn(rank, world))))
         import torch.distributed as dist
 
         dist.destroy_process_group()
@@ -32,6 +34,16 @@ def _worker(rank, world, port, fn, q):
         import traceback
 
         q.put((rank, f"ERROR {e}\n{traceback.format_exc()}"))
+
+
+def _to_numpy(v):
+    if isinstance(v, torch.Tensor):
+        return v.numpy()
+    if isinstance(v, (list, tuple)):
+        return type(v)(_to_numpy(x) for x in v)
+    if isinstance(v, dict):
+        return {k: _to_numpy(x) for k, x in v.items()}
+    return v
 
 
 def _run(fn, world=2):
@@ -83,6 +95,7 @@ def test_grad_bucketer_averages():
     g0, nb, total = out[0]
     g1, _, _ = out[1]
     assert nb > 1 and total == 3.0
+    g0, g1 = [torch.from_numpy(a) for a in g0], [torch.from_numpy(b) for b in g1]
     for a, b in zip(g0, g1):
         torch.testing.assert_close(a, b)
     # compare with the single-process average of both ranks' gradients
