@@ -76,7 +76,7 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
         return lib
     cxx = os.environ.get("CXX", "g++")
     tmp = lib.with_name(lib.name + ".tmp")
-    cmd = [cxx, *flags, *extra, *_pybind_includes(), *map(str, srcs), "-o", str(tmp)]
+    cmd = [cxx, *flags, *extra, *_pybind_includes(), *map(str, srcs), "-lrt", "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     _run(cmd)
@@ -100,7 +100,7 @@ def build_native_sanitized(kind: str, out_dir: str | os.PathLike) -> Path:
     flags = ["-O1", "-g", "-std=c++17", "-shared", "-fPIC", "-msse4.2", "-pthread", *SANITIZERS[kind]]
     out = Path(out_dir) / f"_native{EXT_SUFFIX}"
     out.parent.mkdir(parents=True, exist_ok=True)
-    _run([os.environ.get("CXX", "g++"), *flags, *_pybind_includes(), *map(str, srcs), "-o", str(out)])
+    _run([os.environ.get("CXX", "g++"), *flags, *_pybind_includes(), *map(str, srcs), "-lrt", "-o", str(out)])
     return out
 
 

@@ -12,6 +12,7 @@
 //   * CRC32C + LevelDB-table build/parse for TensorBundle V2 checkpoints
 //                                  (SaveV2/RestoreV2 driven by LIB/io/Saver.scala:55-89)
 //   * tensor-arena offset planning / allocation (arena.cpp)
+//   * SPSC shared-memory record rings to worker-process subtasks (shm_ring.cpp)
 //   * multithreaded gather of record payloads into one pinned staging slot
 //                                  (the micro-batch assembler; no reference analogue:
 //                                   the reference runs batch 1)
@@ -865,6 +866,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("gather_into", &gather_into, py::arg("dst"), py::arg("dst_bytes"), py::arg("srcs"), py::arg("stride"),
         py::arg("nthreads") = 8);
   register_arena(m);
+  register_shm_ring(m);
   m.attr("has_sse42") =
 #if defined(__SSE4_2__)
       true;

@@ -7,4 +7,5 @@
 
 namespace py = pybind11;
 
-void register_arena(py::module_& m);  // arena.cpp: plan_offsets, OffsetAllocator
+void register_arena(py::module_& m);     // arena.cpp: plan_offsets, OffsetAllocator
+void register_shm_ring(py::module_& m);  // shm_ring.cpp: ShmRing (SPSC shared-memory channel)

@@ -280,7 +280,12 @@ class _OpTask(_Task):
         super().__init__(job, node, subtask, writer, restore)
         self.gate = gate
         self.channel_input = dict(channels)  # channel id -> input index
-        self.op = self.node.make_operator()
+        if getattr(self.node, "remote", False):
+            from .remote import RemoteOperatorProxy
+
+            self.op = RemoteOperatorProxy(self.node, subtask, job)  # subtask runs in a worker process
+        else:
+            self.op = self.node.make_operator()
 
     def run(self):
         op = self.op

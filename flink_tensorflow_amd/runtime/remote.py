@@ -1,0 +1,380 @@
+"""Operator subtasks in worker processes, connected by native shared-memory rings.
+
+``DataStream.run_in_processes()`` moves every subtask of an operator into its own worker
+process (``spawn``; one per GPU for model operators — ``cuda:(subtask % #GPUs)``), the
+MI355X-native replacement for the TaskManager slots the reference's Flink job deploys its
+subtasks to (SURVEY §2.12 "one subtask per GPU", §2.13 data exchange; the reference ships
+records through ``TensorValue.write/read`` over Netty, ``LIB/types/TensorValue.java:150-187``).
+
+Per remote subtask the coordinator keeps its usual task thread (input gates, barrier
+alignment, watermarks) and forwards elements through a SPSC ring in ``/dev/shm``
+(``csrc/shm_ring.cpp``) to the worker, which runs the unchanged operator (user function,
+keyed state, timers, micro-batching, the GPU plan).  The worker's emissions come back on a
+second ring and are re-emitted by a drainer thread in order, so a checkpoint barrier is
+forwarded downstream only after every record the worker emitted before its snapshot.
+
+Messages (cloudpickle, fragmented when larger than half a ring):
+
+=====================  ==============================================================
+coordinator → worker   ``init`` (operator factory, context, restore state), ``recs``
+                       [(value, ts, input)], ``wm`` ts, ``snap`` (id, dir), ``notify``
+                       id, ``end``, ``close``
+worker → coordinator   ``out`` [elements], ``side`` [(tag, value)], ``state`` (id, state),
+                       ``ended``, ``closed`` (metrics), ``error`` (message, traceback)
+=====================  ==============================================================
+"""
+from __future__ import annotations
+
+import os
+import queue
+import threading
+import time
+import traceback
+import uuid
+
+import cloudpickle
+
+from .. import _ext
+from .operators import Output, Record, Watermark
+
+_RING_BYTES = 64 << 20
+_BATCH = 64
+_IDLE_S = 0.02
+
+
+class RemoteTaskError(RuntimeError):
+    pass
+
+
+class ShmChannel:
+    """One direction of a worker link: pickled messages over a ``ShmRing``."""
+
+    def __init__(self, name: str, create: bool, capacity: int = _RING_BYTES):
+        self.ring = _ext.native().ShmRing(name, capacity if create else 0, create)
+        self.name = name
+        self.owner = create
+
+    def send(self, msg, timeout_s: float = -1.0, alive=None):
+        data = cloudpickle.dumps(msg, protocol=5)
+        step = self.ring.max_message - 1
+        parts = [data[i:i + step] for i in range(0, len(data), step)] or [b""]
+        for i, p in enumerate(parts):
+            flag = b"\x01" if i + 1 < len(parts) else b"\x00"
+            while not self.ring.push(flag + p, 0.5 if timeout_s < 0 else timeout_s):
+                if alive is not None and not alive():
+                    raise RemoteTaskError(f"peer of {self.name} died")
+                if timeout_s >= 0:
+                    raise TimeoutError(f"{self.name}: ring full")
+
+    def recv(self, timeout_s: float):
+        """A message, or None on timeout (or when the producer closed the ring)."""
+        chunks = []
+        while True:
+            m = self.ring.pop(timeout_s if not chunks else 30.0)
+            if m is None:
+                if chunks:
+                    raise RemoteTaskError(f"{self.name}: truncated message")
+                return None
+            chunks.append(m[1:])
+            if m[:1] == b"\x00":
+                return cloudpickle.loads(b"".join(chunks))
+
+    def close(self):
+        self.ring.close_producer()
+
+    def unlink(self):
+        if self.owner:
+            _ext.native().ShmRing.unlink(self.name)
+            self.owner = False
+
+
+# ------------------------------------------------------------------ worker side
+def _worker_main(in_name: str, out_name: str):
+    inp = ShmChannel(in_name, create=False)
+    out = ShmChannel(out_name, create=False)
+    op = None
+    pending: list = []
+
+    def flush():
+        if pending:
+            out.send(("out", list(pending)))
+            pending.clear()
+
+    def emit(elem):
+        pending.append(elem)
+        if len(pending) >= _BATCH or not isinstance(elem, Record):
+            flush()
+
+    parent = os.getppid()
+    try:
+        out.send(("attached",))  # the coordinator may now unlink the segment names
+        while True:
+            msg = inp.recv(1.0)
+            if msg is not None:
+                break
+            if os.getppid() != parent:
+                return  # coordinator gone
+        kind, factory, spec, restore, restore_dir = msg
+        assert kind == "init", kind
+        from .functions import RuntimeContext
+        from ..utils.metrics import MetricGroup
+
+        device = None
+        if spec["gpu"]:
+            import torch
+
+            if torch.cuda.is_available():
+                device = torch.device("cuda", spec["subtask"] % torch.cuda.device_count())
+                torch.cuda.set_device(device)
+        metrics = MetricGroup(f"{spec['name']}[{spec['subtask']}]")
+        ctx = RuntimeContext(spec["name"], spec["subtask"], spec["parallelism"], device, spec["attempt"], metrics,
+                             spec["config"], None)
+        ctx.global_index, ctx.global_parallelism = spec["global_index"], spec["global_parallelism"]
+        ctx.worker_pid = os.getpid()
+        op = cloudpickle.loads(factory)()
+        op.setup(ctx, Output(emit, lambda tag, v: (flush(), out.send(("side", [(tag, v)])))))
+        op.initialize(restore, restore_dir)
+        op.open()
+        while True:
+            msg = inp.recv(_IDLE_S)
+            if msg is None:
+                if os.getppid() != parent:
+                    break  # orphaned: the coordinator died
+                op.on_idle(time.time())
+                flush()
+                continue
+            kind = msg[0]
+            if kind == "recs":
+                for value, ts, idx in msg[1]:
+                    op.process(Record(value, ts), idx)
+                    metrics.inc("records_in")
+            elif kind == "wm":
+                op.process_watermark(Watermark(msg[1]))
+            elif kind == "snap":
+                op.prepare_snapshot()
+                state = op.snapshot_state(msg[1], msg[2])
+                flush()
+                out.send(("state", msg[1], state))
+                continue
+            elif kind == "notify":
+                op.notify_checkpoint_complete(msg[1])
+            elif kind == "end":
+                op.end_input()
+                flush()
+                out.send(("ended",))
+                continue
+            elif kind == "close":
+                op.close()
+                op = None
+                flush()
+                out.send(("closed", metrics.snapshot()))
+                break
+            op.on_idle(time.time())
+            flush()
+    except BaseException as e:  # noqa: BLE001
+        try:
+            pending.clear()
+            out.send(("error", f"{type(e).__name__}: {e}", traceback.format_exc()), timeout_s=5.0)
+        except Exception:  # noqa: BLE001
+            pass
+    finally:
+        if op is not None:
+            try:
+                op.close()
+            except Exception:  # noqa: BLE001
+                pass
+        out.close()
+
+
+# ------------------------------------------------------------------ coordinator side
+class RemoteOperatorProxy:
+    """Stands in for the operator inside the coordinator's task loop."""
+
+    chainable = False
+
+    def __init__(self, node, subtask: int, job, ring_bytes: int = _RING_BYTES):
+        self.node = node
+        self.subtask = subtask
+        self.job = job
+        self.num_inputs = 1
+        self.ring_bytes = ring_bytes
+        self.to_worker = self.from_worker = None  # created when the subtask starts
+        self.proc = None
+        self.out: Output | None = None
+        self.ctx = None
+        self._buf: list = []
+        self._replies: queue.Queue = queue.Queue()
+        self._send_lock = threading.Lock()
+        self._error: tuple | None = None
+        self._drainer: threading.Thread | None = None
+        self.worker_metrics: dict | None = None
+
+    # ---- lifecycle (called by the task thread)
+    def setup(self, ctx, out: Output):
+        self.ctx = ctx
+        self.out = out
+
+    def initialize(self, snapshot, checkpoint_dir):
+        try:
+            self._start(snapshot, checkpoint_dir)
+        except BaseException:
+            self._shutdown()
+            raise
+
+    def _start(self, snapshot, checkpoint_dir):
+        import multiprocessing as mp
+
+        tag = f"/ftm-{os.getpid()}-{uuid.uuid4().hex[:10]}"
+        self.to_worker = ShmChannel(tag + "-in", True, self.ring_bytes)
+        self.from_worker = ShmChannel(tag + "-out", True, self.ring_bytes)
+        self.proc = mp.get_context("spawn").Process(target=_worker_main, name=f"ftm-{self.node.name}-{self.subtask}",
+                                                    args=(self.to_worker.name, self.from_worker.name), daemon=True)
+        self.proc.start()
+        self._drainer = threading.Thread(target=self._drain, name=f"drain-{self.node.name}-{self.subtask}",
+                                         daemon=True)
+        self._drainer.start()
+        self._wait("attached", 120.0)
+        self.to_worker.unlink()  # both ends are mapped: the names can go (no /dev/shm leak on a crash)
+        self.from_worker.unlink()
+        spec = {"name": self.node.name, "subtask": self.subtask, "parallelism": self.node.parallelism,
+                "gpu": bool(self.node.uses_gpu), "attempt": self.job.attempt, "config": self.job.config,
+                "global_index": self.ctx.global_index, "global_parallelism": self.ctx.global_parallelism}
+        self._send(("init", cloudpickle.dumps(self.node.factory), spec, snapshot, checkpoint_dir))
+
+    def open(self):
+        pass
+
+    def close(self):
+        graceful = False
+        try:
+            if self._alive() and self._error is None and not self.job.cancel.is_set():
+                self._flush()
+                self._send(("close",))
+                self._wait("closed", 60.0)
+                graceful = True
+        finally:
+            self._shutdown(graceful)
+
+    def _shutdown(self, graceful: bool = False):
+        if self.proc is not None:
+            if not graceful and self.proc.is_alive():
+                self.proc.terminate()  # failed / cancelled attempt: its state is discarded anyway
+            self.proc.join(timeout=10)
+            if self.proc.is_alive():
+                self.proc.kill()
+                self.proc.join(timeout=5)
+        if self.from_worker is not None:
+            self.from_worker.close()  # wakes the drainer if it is still waiting
+        if self._drainer is not None:
+            self._drainer.join(timeout=5)
+        for ch in (self.to_worker, self.from_worker):
+            if ch is not None:
+                ch.unlink()
+
+    # ---- data path
+    def process(self, rec: Record, input_index: int = 0):
+        self._buf.append((rec.value, rec.ts, input_index))
+        if len(self._buf) >= _BATCH:
+            self._flush()
+
+    def process_watermark(self, wm: Watermark, input_index: int = 0):
+        self._flush()
+        self._send(("wm", wm.ts))
+
+    def on_idle(self, now: float):
+        self._flush()
+        self._check()
+
+    def next_deadline(self):
+        return None  # the worker runs its own timers between messages
+
+    def end_input(self):
+        self._flush()
+        self._send(("end",))
+        self._wait("ended", None)
+
+    # ---- checkpoints
+    def prepare_snapshot(self):
+        self._flush()
+
+    def snapshot_state(self, checkpoint_id: int, checkpoint_dir):
+        self._send(("snap", checkpoint_id, checkpoint_dir))
+        return self._wait("state", None)[2]
+
+    def notify_checkpoint_complete(self, checkpoint_id: int):
+        self._send(("notify", checkpoint_id))
+
+    # ---- plumbing
+    def _alive(self) -> bool:
+        return self.proc is not None and self.proc.is_alive()
+
+    def _send(self, msg):
+        self._check()
+        with self._send_lock:  # task thread + checkpoint-complete notifications: one producer at a time
+            self.to_worker.send(msg, alive=self._alive)
+
+    def _flush(self):
+        if self._buf:
+            batch, self._buf = self._buf, []
+            self._send(("recs", batch))
+
+    def _check(self):
+        if self._error is not None:
+            raise RemoteTaskError(f"{self.node.name}[{self.subtask}] worker failed: {self._error[0]}\n{self._error[1]}")
+
+    def _wait(self, kind: str, timeout_s):
+        t_end = None if timeout_s is None else time.time() + timeout_s
+        while True:
+            self._check()
+            try:
+                msg = self._replies.get(timeout=0.1)
+            except queue.Empty:
+                if t_end is not None and time.time() > t_end:
+                    raise TimeoutError(f"{self.node.name}[{self.subtask}]: no {kind!r} from the worker") from None
+                if self.job.cancel.is_set():
+                    from .executor import JobCancelled
+
+                    raise JobCancelled() from None
+                continue
+            if msg[0] != kind:
+                raise RemoteTaskError(f"{self.node.name}[{self.subtask}]: expected {kind!r}, got {msg[0]!r}")
+            return msg
+
+    def _drain(self):
+        """Re-emits the worker's output in order; hands control replies to the task."""
+        while True:
+            try:
+                msg = self.from_worker.recv(0.2)
+            except Exception as e:  # noqa: BLE001
+                self._error = (f"{type(e).__name__}: {e}", traceback.format_exc())
+                return
+            if msg is None:
+                if self.from_worker.ring.closed and self.from_worker.ring.used == 0:
+                    if self._error is None and self.worker_metrics is None:
+                        self._error = ("worker exited without closing", "")
+                    return
+                if self.proc is not None and not self.proc.is_alive() and self.from_worker.ring.used == 0:
+                    if self.worker_metrics is None and self._error is None:
+                        self._error = (f"worker process died (exit code {self.proc.exitcode})", "")
+                    return
+                continue
+            kind = msg[0]
+            try:
+                if kind == "out":
+                    for elem in msg[1]:
+                        self.out._emit(elem)
+                elif kind == "side":
+                    for tag, v in msg[1]:
+                        self.out.emit_side(tag, v)
+                elif kind == "error":
+                    self._error = (msg[1], msg[2])
+                    return
+                else:
+                    if kind == "closed":
+                        self.worker_metrics = msg[1]
+                    self._replies.put(msg)
+                    if kind == "closed":
+                        return
+            except Exception as e:  # noqa: BLE001 - e.g. a cancelled downstream
+                self._error = (f"{type(e).__name__}: {e}", traceback.format_exc())
+                return

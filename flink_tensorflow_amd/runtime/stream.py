@@ -172,6 +172,14 @@ class DataStream:
         self.node.parallelism = int(p)
         return self
 
+    def run_in_processes(self, enable: bool = True) -> "DataStream":
+        """Runs each subtask of this operator in its own worker process (one per GPU for
+        model operators), fed through shared-memory rings (``runtime/remote.py``)."""
+        if self.node.is_source:
+            raise ValueError("sources run in the coordinator process")
+        self.node.remote = bool(enable)
+        return self
+
     def name(self, n: str) -> "DataStream":
         self.node.name = n
         return self

@@ -1,0 +1,119 @@
+"""Worker-process subtasks over native shared-memory rings: ring protocol across
+processes, remote operators with keyed state, checkpoints/restarts and error propagation,
+and (GPU) a micro-batched ResNet operator whose subtasks are worker processes."""
+import multiprocessing as mp
+import os
+
+import pytest
+
+from flink_tensorflow_amd import _ext
+from flink_tensorflow_amd.runtime import (JobExecutionException, ListStateDescriptor, ProcessFunction,
+                                          RestartStrategy, StreamExecutionEnvironment, ValueStateDescriptor)
+from flink_tensorflow_amd.runtime.remote import ShmChannel
+from flink_tensorflow_amd.utils.fault import FailAfter
+
+
+def _echo_worker(a, b):
+    inp, out = ShmChannel(a, False), ShmChannel(b, False)
+    while True:
+        m = inp.recv(10.0)
+        if m is None or m == "stop":
+            break
+        out.send(m)
+    out.close()
+
+
+def test_shm_channel_across_processes():
+    tag = f"/ftm-t-{os.getpid()}"
+    a, b = ShmChannel(tag + "a", True, 1 << 16), ShmChannel(tag + "b", True, 1 << 16)
+    p = mp.get_context("spawn").Process(target=_echo_worker, args=(a.name, b.name))
+    p.start()
+    try:
+        msgs = [("small", i) for i in range(500)] + [bytes(100_000), list(range(50_000))]  # > ring: fragmented
+        for m in msgs:
+            a.send(m)
+            assert b.recv(10.0) == m
+        a.send("stop")
+        assert b.recv(10.0) is None  # producer closed its ring
+    finally:
+        p.join(10)
+        a.unlink()
+        b.unlink()
+    with pytest.raises(RuntimeError):
+        _ext.native().ShmRing(tag + "a", 0, False)  # unlinked
+
+
+def test_remote_map_runs_in_worker_processes():
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    out = env.from_collection(list(range(300))).rebalance() \
+        .map(lambda v: (os.getpid(), v * 2)).run_in_processes().execute_and_collect()
+    pids = {p for p, _ in out}
+    assert sorted(v for _, v in out) == [2 * i for i in range(300)]
+    assert len(pids) == 2 and os.getpid() not in pids
+
+
+class _RunningSum(ProcessFunction):
+    def open(self, config=None):
+        self.total = self.get_runtime_context().get_state(ValueStateDescriptor("total", 0))
+
+    def process_element(self, value, ctx, out):
+        self.total.update(self.total.value() + value)
+        out.collect((ctx.get_current_key(), self.total.value()))
+
+
+def test_remote_keyed_state_survives_failure_and_restart(tmp_path):
+    """A worker-process keyed operator snapshots through the ring; after an injected
+    failure the restarted workers resume from the checkpoint consistently."""
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    env.enable_checkpointing(0.05, str(tmp_path / "chk"))
+    env.set_restart_strategy(RestartStrategy.fixed_delay(2, 0.0))
+    from flink_tensorflow_amd.runtime.sources import CollectionSource
+
+    src = env.add_source(CollectionSource(list(range(1, 301)), delay_s=0.002), "numbers")
+    res_sink = src.map(FailAfter(100, attempts=(0,))).key_by(lambda v: v % 3).process(_RunningSum()) \
+        .run_in_processes().collect_into()
+    res = env.execute("remote-recover")
+    assert res.attempts == 1 and len(res.checkpoints) >= 1
+    final = {}
+    for k, t in res_sink.results():
+        final[k] = max(final.get(k, 0), t)
+    assert final == {k: sum(v for v in range(1, 301) if v % 3 == k) for k in range(3)}
+
+
+def _boom(v):
+    if v == 7:
+        raise ValueError("bad record 7")
+    return v
+
+
+def test_remote_error_propagates():
+    env = StreamExecutionEnvironment.get_execution_environment()
+    env.from_collection(list(range(20))).map(_boom).run_in_processes().collect_into()
+    with pytest.raises(JobExecutionException, match="bad record 7"):
+        env.execute("remote-boom")
+
+
+@pytest.mark.gpu
+def test_remote_batched_resnet_gpu():
+    """Two ResNet subtasks as worker processes sharing the box's GPU (one per GPU on a
+    node), each with its own arena, pinned ring and captured plans."""
+    import numpy as np
+
+    from flink_tensorflow_amd.models.zoo.image_classifier import ResNet50Model
+
+    rng = np.random.default_rng(0)
+    imgs = [rng.integers(0, 256, (64, 64, 3), dtype=np.uint8) for _ in range(40)]
+    model = ResNet50Model(image_hw=(64, 64), buckets=(8, 16), top_k=3, depth_layers=26)
+
+    def run(remote):
+        env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+        s = env.from_collection(list(enumerate(imgs))).rebalance() \
+            .map_with_model_batched(model, None, max_batch=16, max_delay_ms=5, emit_batches=False)
+        if remote:
+            s = s.run_in_processes()
+        return s.execute_and_collect()
+
+    local, remote = run(False), run(True)
+    assert len(remote) == len(local) == 40
+    top1 = lambda res: sorted(r[0][1] for r in res)  # noqa: E731
+    assert top1(remote) == top1(local)
