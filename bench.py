@@ -59,6 +59,7 @@ def main():
                     help="comma-separated extra batch buckets compiled next to --batch; with --dynamic the "
                          "per-step batch size varies and each micro-batch runs on the smallest bucket")
     ap.add_argument("--dynamic", action="store_true", help="variable micro-batch sizes (uniform in [B/4, B])")
+    ap.add_argument("--no-pack", action="store_true", help="bert: run padded batches (no token packing)")
     args = ap.parse_args()
 
     import torch
@@ -125,22 +126,28 @@ def main():
         seq = None
     else:
         from flink_tensorflow_amd.models.zoo.bert import (BertConfig, BertDeviceWeights, BertEncoderPlan,
-                                                          init_bert_weights)
+                                                          PackedBertEncoder, init_bert_weights)
 
         cfg = BertConfig.base()
         seq = args.seq_len
         w = BertDeviceWeights(init_bert_weights(cfg, seed=rank), cfg, dev)  # rank-local init, then broadcast
-        plan = BertEncoderPlan(w, B, seq, use_graph=not args.no_graph)
+        if args.no_pack:
+            plan = BertEncoderPlan(w, B, seq, use_graph=not args.no_graph)
+        else:  # padding-free: each micro-batch runs on the token capacity of its real tokens
+            plan = PackedBertEncoder(w, B, seq, use_graph=not args.no_graph)
         params = w.tensors()
         feed, rec_shape, rec_dtype = "ids", (seq,), torch.int32
-        flops_per_record = plan.flops() / B
         rng = np.random.default_rng(1234 + rank)
         pool = rng.integers(1000, cfg.vocab_size, size=(args.pool, seq), dtype=np.int32)
         lens = rng.integers(seq // 2, seq + 1, size=args.pool)
         for i, n in enumerate(lens):
             pool[i, n:] = 0
         pool[:, 0] = 101
-        model_name, data = "BERT-base (seq classification)", f"synthetic token ids, seq {seq}, random-init weights"
+        # useful work: the real tokens of the records (padding rows are not counted as FLOPs)
+        flops_per_record = plan.flops(lens) / len(lens)
+        model_name = "BERT-base (seq classification)"
+        data = (f"synthetic token ids, seq {seq} (real lengths U[{seq // 2},{seq}]), random-init weights, "
+                + ("padded execution" if args.no_pack else "padding-free (packed) execution"))
     # rank 0's weights to all ranks over RCCL (one flattened buffer per dtype); in place,
     # so the captured hipGraph stays valid
     nbytes = comm.broadcast_tensors(params, src=0)

@@ -62,7 +62,9 @@ class PipelinedGpuRunner:
 
     ``plans``: ``{bucket_size: plan}`` where ``plan.input_buffer(feed)`` is the static
     device input and ``plan.replay()`` launches the captured graph; ``fetch_bufs(plan)``
-    returns the device output tensors to bring back (small: top-k values/indices).
+    returns the device output tensors to bring back (small: top-k values/indices).  A plan
+    with ``select(host_batch, n)`` chooses the concrete plan per batch from the staged
+    host records (before the H2D copy).
     """
 
     def __init__(self, plans: dict[int, Any], feed: str, fetch_bufs: Callable[[Any], Sequence[torch.Tensor]],
@@ -112,6 +114,9 @@ class PipelinedGpuRunner:
             if n < b:
                 slot.pinned_in[n:].zero_()
         plan = self.plans[b]
+        select = getattr(plan, "select", None)
+        if select is not None:  # e.g. the padding-free BERT encoder: pick a token-capacity plan
+            plan = select(slot.pinned_in, n)
         with trace_range("h2d"), torch.cuda.stream(self.copy_stream):
             slot.dev_in.copy_(slot.pinned_in, non_blocking=True)
             slot.h2d.record(self.copy_stream)

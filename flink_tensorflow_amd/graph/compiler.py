@@ -1233,7 +1233,7 @@ class CompiledFunction:
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with tracing.graph_capture(g):
             self._run_steps()
         self._graph_obj = g
 

@@ -1,5 +1,6 @@
 // Fused multi-head attention forward (flash-style, online softmax) for the BERT path,
-// plus the fused token-embedding + LayerNorm kernel.
+// plus the fused token-embedding + LayerNorm kernel and the token-packing kernel of the
+// padding-free encoder (attention then runs per packed sequence via cu_seqlens).
 //
 // attention:  qkv [T = B*S, 3*H*D] bf16 straight from the fused QKV projection GEMM
 // (Q | K | V column blocks, head h at columns h*D), key-padding mask from the token ids
@@ -40,8 +41,8 @@ FTM_DEVICE v4s tr_read(const bf16* p) {
 // no second K/V round trip and no online-softmax rescale)
 template <int QB, int KB>
 __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __restrict__ qkv, const int* __restrict__ ids,
-                                                               bf16* __restrict__ out, int B, int S, int H, int pad_id,
-                                                               float scale_log2e) {
+                                                               const int* __restrict__ cu, bf16* __restrict__ out, int B,
+                                                               int S, int H, int pad_id, float scale_log2e) {
   constexpr int NW = QB / 16;  // waves
   constexpr int NTH = NW * 64;
   constexpr int NF = KB / 16;  // key fragments of S per wave
@@ -56,14 +57,18 @@ __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __res
   const int b = bh / H, h = bh % H;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ld = 3 * H * D;
-  const size_t tok0 = (size_t)b * S;
+  // padded batch: sequence b is rows [b*S, b*S + S), padding keys masked by id; packed
+  // (cu != null): sequence b is rows [cu[b], cu[b+1]) of the token-packed batch, no padding
+  const size_t tok0 = cu ? (size_t)cu[b] : (size_t)b * S;
+  const int Sb = cu ? cu[b + 1] - cu[b] : S;
+  if (qb * QB >= Sb) return;  // block-uniform: this query block lies past the sequence
 
   // Q fragments for this wave's 16 rows (A operand: row = lane&15, k = 8*(lane>>4) + j)
   const int qrow = qb * QB + wave * 16 + (lane & 15);
   bf16x8 qa[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
-    if (qrow < S)
+    if (qrow < Sb)
       qa[ks] = *reinterpret_cast<const bf16x8*>(qkv + (tok0 + qrow) * ld + h * D + ks * 32 + (lane >> 4) * 8);
     else
       qa[ks] = bf16x8{};
@@ -81,7 +86,7 @@ __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __res
   // this lane's supplier address inside a 4-key x 16-d transposed-read block
   const int trq = (lane & 15) >> 2, trp = lane & 3;
 
-  const int nkb = (S + KB - 1) / KB;
+  const int nkb = (Sb + KB - 1) / KB;
   for (int kb = 0; kb < nkb; ++kb) {
     // ---- stage K (row-major, swizzled) and V (row-major) for keys kb*64 .. +63
     __syncthreads();
@@ -92,7 +97,7 @@ __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __res
         const int key = q >> 3, ch = q & 7;
         const int kg = kb * KB + key;
         u32x4 kv = {0u, 0u, 0u, 0u}, vv = {0u, 0u, 0u, 0u};
-        if (kg < S) {
+        if (kg < Sb) {
           const bf16* row = qkv + (tok0 + kg) * ld + h * D + ch * 8;
           kv = *reinterpret_cast<const u32x4*>(row + H * D);
           vv = *reinterpret_cast<const u32x4*>(row + 2 * H * D);
@@ -103,7 +108,7 @@ __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __res
     }
     if (tid < KB) {
       const int kg = kb * KB + tid;
-      kmask[tid] = (kg < S && ids[tok0 + kg] != pad_id) ? 0.f : -INFINITY;
+      kmask[tid] = (kg < Sb && (cu || ids[tok0 + kg] != pad_id)) ? 0.f : -INFINITY;
     }
     __syncthreads();
 
@@ -201,7 +206,7 @@ __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __res
     const int c = lane + it * 64;  // 16 rows x 8 chunks
     const int r = c >> 3, ch = c & 7;
     const int q = qb * QB + wave * 16 + r;
-    if (q < S)
+    if (q < Sb)
       *reinterpret_cast<u32x4*>(out + (tok0 + q) * (H * D) + h * D + ch * 8) =
           *reinterpret_cast<const u32x4*>(os + r * OP + ch * 8);
   }
@@ -210,6 +215,7 @@ __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __res
 // x[t] = LN(word[ids[t]] + pos[t % S] + type[tt[t]]) * gamma + beta   (D % 8 == 0, D <= 1024)
 template <int MAXV>
 __global__ __launch_bounds__(256) void embed_ln_kernel(const int* __restrict__ ids, const int* __restrict__ tt,
+                                                       const int* __restrict__ pos_ids,
                                                        const bf16* __restrict__ word, const bf16* __restrict__ pos,
                                                        const bf16* __restrict__ type, const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, bf16* __restrict__ y, int T,
@@ -221,7 +227,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int* __restrict__ i
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
   const int ty = tt ? tt[t] : 0;
   const bf16* wp = word + (size_t)id * D;
-  const bf16* pp = pos + (size_t)(t % S) * D;
+  const bf16* pp = pos + (size_t)(pos_ids ? pos_ids[t] : t % S) * D;
   const bf16* tp = type + (size_t)ty * D;
   float v[MAXV][8];
   float s = 0.f;
@@ -261,10 +267,72 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int* __restrict__ i
   }
 }
 
+// Token packing for padding-free encoders: the non-pad tokens of ids[B, S] (row order)
+// -> packed[0, T_eff) with their in-row positions, cu[B + 1] row offsets and cls[B] (row
+// starts, where each row's first token lands); rows [T_eff, T_cap) are zero-filled.  One
+// 1024-thread workgroup (B <= 1024): per-row counts by wave ballots, an LDS scan, then a
+// ballot-ranked scatter.  Writes past T_cap are dropped (the host sizes T_cap >= T_eff).
+__global__ __launch_bounds__(1024) void pack_tokens_kernel(const int* __restrict__ ids, int B, int S, int pad_id,
+                                                           int T_cap, int* __restrict__ packed,
+                                                           int* __restrict__ pos, int* __restrict__ cu,
+                                                           int* __restrict__ cls) {
+  __shared__ int lens[1024];
+  __shared__ int starts[1025];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (int r = wave; r < B; r += 16) {
+    int n = 0;
+    for (int c = 0; c < S; c += 64) {
+      const bool ok = c + lane < S && ids[(size_t)r * S + c + lane] != pad_id;
+      n += __popcll(__ballot(ok));
+    }
+    if (lane == 0) lens[r] = n;
+  }
+  __syncthreads();
+  if (tid == 0) {  // B <= 1024 row counts: a serial scan is ~1 us, below the launch cost
+    int acc = 0;
+    for (int r = 0; r < B; ++r) {
+      starts[r] = acc;
+      acc += lens[r];
+    }
+    starts[B] = acc;
+  }
+  __syncthreads();
+  for (int r = tid; r <= B; r += 1024) cu[r] = starts[r];
+  for (int r = tid; r < B; r += 1024) cls[r] = starts[r] < T_cap ? starts[r] : T_cap - 1;
+  for (int r = wave; r < B; r += 16) {
+    int dst = starts[r];
+    for (int c = 0; c < S; c += 64) {
+      const int tok = c + lane < S ? ids[(size_t)r * S + c + lane] : pad_id;
+      const bool ok = c + lane < S && tok != pad_id;
+      const unsigned long long m = __ballot(ok);
+      const int d = dst + __popcll(m & below);
+      if (ok && d < T_cap) {
+        packed[d] = tok;
+        pos[d] = c + lane;
+      }
+      dst += __popcll(m);
+    }
+  }
+  for (int t = starts[B] + tid; t < T_cap; t += 1024) {
+    packed[t] = pad_id;
+    pos[t] = 0;
+  }
+}
+
 }  // namespace
 
-void attention_fwd_bf16(uintptr_t qkv, uintptr_t ids, uintptr_t out, int B, int S, int H, int Dh, int pad_id,
-                        float scale, uintptr_t stream) {
+void pack_tokens(uintptr_t ids, int B, int S, int pad_id, int T_cap, uintptr_t packed, uintptr_t pos, uintptr_t cu,
+                 uintptr_t cls, uintptr_t stream) {
+  if (B <= 0 || B > 1024 || S <= 0 || T_cap <= 0) throw std::invalid_argument("pack_tokens: need 0 < B <= 1024");
+  hipLaunchKernelGGL(pack_tokens_kernel, dim3(1), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const int*>(ids), B, S, pad_id, T_cap, reinterpret_cast<int*>(packed),
+                     reinterpret_cast<int*>(pos), reinterpret_cast<int*>(cu), reinterpret_cast<int*>(cls));
+  FTM_CHECK_LAUNCH();
+}
+
+void attention_fwd_bf16(uintptr_t qkv, uintptr_t ids, uintptr_t cu_seqlens, uintptr_t out, int B, int S, int H,
+                        int Dh, int pad_id, float scale, uintptr_t stream) {
   if (Dh != D) throw std::invalid_argument("attention_fwd: head dim must be 64");
   if (B <= 0 || S <= 0 || H <= 0) throw std::invalid_argument("attention_fwd: empty problem");
   if (qkv % 16 || out % 16) throw std::invalid_argument("attention_fwd: pointers must be 16-byte aligned");
@@ -272,35 +340,39 @@ void attention_fwd_bf16(uintptr_t qkv, uintptr_t ids, uintptr_t out, int B, int 
   auto st = reinterpret_cast<hipStream_t>(stream);
   auto Q = reinterpret_cast<const bf16*>(qkv);
   auto I = reinterpret_cast<const int*>(ids);
+  auto CU = reinterpret_cast<const int*>(cu_seqlens);
+  if (!I && !CU) throw std::invalid_argument("attention_fwd: need token ids (padded) or cu_seqlens (packed)");
   auto O = reinterpret_cast<bf16*>(out);
   if (S > 64) {  // 128-query blocks: K/V of a head staged once for S <= 128
     const int qblocks = (S + 127) / 128;
-    hipLaunchKernelGGL((attention_fwd_kernel<128, 128>), dim3(B * H * qblocks), dim3(512), 0, st, Q, I, O, B, S, H,
-                       pad_id, scale * kLog2e);
+    hipLaunchKernelGGL((attention_fwd_kernel<128, 128>), dim3(B * H * qblocks), dim3(512), 0, st, Q, I, CU, O, B, S,
+                       H, pad_id, scale * kLog2e);
   } else {
     const int qblocks = (S + 63) / 64;
-    hipLaunchKernelGGL((attention_fwd_kernel<64, 64>), dim3(B * H * qblocks), dim3(256), 0, st, Q, I, O, B, S, H,
+    hipLaunchKernelGGL((attention_fwd_kernel<64, 64>), dim3(B * H * qblocks), dim3(256), 0, st, Q, I, CU, O, B, S, H,
                        pad_id, scale * kLog2e);
   }
   FTM_CHECK_LAUNCH();
 }
 
-void embed_ln_bf16(uintptr_t ids, uintptr_t tt, uintptr_t word, uintptr_t pos, uintptr_t type, uintptr_t gamma,
-                   uintptr_t beta, uintptr_t y, int T, int S, int D, int vocab, float eps, uintptr_t stream) {
+void embed_ln_bf16(uintptr_t ids, uintptr_t tt, uintptr_t pos_ids, uintptr_t word, uintptr_t pos, uintptr_t type,
+                   uintptr_t gamma, uintptr_t beta, uintptr_t y, int T, int S, int D, int vocab, float eps,
+                   uintptr_t stream) {
   if (D % 8 || D > 2048) throw std::invalid_argument("embed_ln: D must be a multiple of 8 and <= 2048");
   dim3 grid((T + 3) / 4), block(256);
   auto s = reinterpret_cast<hipStream_t>(stream);
   auto I = reinterpret_cast<const int*>(ids);
   auto TT = reinterpret_cast<const int*>(tt);
+  auto PI = reinterpret_cast<const int*>(pos_ids);
   auto Wd = reinterpret_cast<const bf16*>(word);
   auto P = reinterpret_cast<const bf16*>(pos);
   auto Ty = reinterpret_cast<const bf16*>(type);
   auto G = reinterpret_cast<const float*>(gamma);
   auto Bt = reinterpret_cast<const float*>(beta);
   auto Y = reinterpret_cast<bf16*>(y);
-  if (D <= 512) hipLaunchKernelGGL(embed_ln_kernel<1>, grid, block, 0, s, I, TT, Wd, P, Ty, G, Bt, Y, T, S, D, vocab, eps);
-  else if (D <= 1024) hipLaunchKernelGGL(embed_ln_kernel<2>, grid, block, 0, s, I, TT, Wd, P, Ty, G, Bt, Y, T, S, D, vocab, eps);
-  else hipLaunchKernelGGL(embed_ln_kernel<4>, grid, block, 0, s, I, TT, Wd, P, Ty, G, Bt, Y, T, S, D, vocab, eps);
+  if (D <= 512) hipLaunchKernelGGL(embed_ln_kernel<1>, grid, block, 0, s, I, TT, PI, Wd, P, Ty, G, Bt, Y, T, S, D, vocab, eps);
+  else if (D <= 1024) hipLaunchKernelGGL(embed_ln_kernel<2>, grid, block, 0, s, I, TT, PI, Wd, P, Ty, G, Bt, Y, T, S, D, vocab, eps);
+  else hipLaunchKernelGGL(embed_ln_kernel<4>, grid, block, 0, s, I, TT, PI, Wd, P, Ty, G, Bt, Y, T, S, D, vocab, eps);
   FTM_CHECK_LAUNCH();
 }
 
@@ -327,4 +399,5 @@ void register_attention(pybind11::module_& m) {
   m.def("probe_tr_read", &probe_tr_read);
   m.def("attention_fwd_bf16", &attention_fwd_bf16);
   m.def("embed_ln_bf16", &embed_ln_bf16);
+  m.def("pack_tokens", &pack_tokens);
 }

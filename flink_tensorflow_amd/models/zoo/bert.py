@@ -27,6 +27,7 @@ import torch
 
 from ...ops import kernels as K
 from ...runtime.model_functions import BatchedGpuModel
+from ...utils.tracing import graph_capture
 from ..core import RichModel, default_device
 
 
@@ -181,6 +182,57 @@ class BertDeviceWeights:
         return out
 
 
+_GEMM_TABLE: bool | None = None
+
+
+def load_gemm_table() -> bool:
+    """Pre-tuned library GEMM solutions for the BERT projection shapes at every token
+    capacity (``bench/tune_bert_gemms.py``; only the picks that beat the hipBLASLt default
+    in a timed comparison are kept, ``profiles/r01_bert_pack/tunableop_compare.jsonl``).
+    Installed as a PyTorch TunableOp lookup table with tuning OFF, so no tuning ever runs
+    inside a stream job; shapes not in the table use the library default.
+    ``FTM_GEMM_TABLE=0`` disables it."""
+    global _GEMM_TABLE
+    if _GEMM_TABLE is not None:
+        return _GEMM_TABLE
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "data", "tunableop_gfx950.csv")
+    _GEMM_TABLE = False
+    if os.environ.get("FTM_GEMM_TABLE", "1") != "0" and os.path.exists(path) and torch.cuda.is_available():
+        tun = torch.cuda.tunable
+        tun.enable(True)
+        tun.tuning_enable(False)
+        _GEMM_TABLE = bool(tun.read_file(os.path.normpath(path)))
+        if not _GEMM_TABLE:  # validators differ (other ROCm / hipBLASLt build): library defaults
+            tun.enable(False)
+    return _GEMM_TABLE
+
+
+class BertBuffers:
+    """Activation buffers of one (batch, seq) encoder, sized for ``tokens`` rows; the
+    token-capacity plans of a packed encoder share one set (they replay serially)."""
+
+    def __init__(self, cfg: "BertConfig", batch: int, seq: int, tokens: int, device, dtype):
+        d, h = device, cfg.hidden
+        self.ids = torch.zeros(batch * seq, dtype=torch.int32, device=d)   # padded [B, S] input
+        self.pids = torch.zeros(tokens, dtype=torch.int32, device=d)       # packed token ids
+        self.ppos = torch.zeros(tokens, dtype=torch.int32, device=d)       # their in-row positions
+        self.cu = torch.zeros(batch + 1, dtype=torch.int32, device=d)      # sequence row offsets
+        self.cls = torch.zeros(batch, dtype=torch.int32, device=d)         # first-token rows
+        self.x = torch.empty(tokens, h, dtype=dtype, device=d)
+        self.y = torch.empty(tokens, h, dtype=dtype, device=d)
+        self.qkv = torch.empty(tokens, 3 * h, dtype=dtype, device=d)
+        self.ctx = torch.zeros(tokens, h, dtype=dtype, device=d)  # rows past the packed tokens stay finite
+        self.x2 = torch.empty(tokens, h, dtype=dtype, device=d)
+        self.ffn = torch.empty(tokens, cfg.intermediate, dtype=dtype, device=d)
+        self.cls_in = torch.empty(batch, h, dtype=dtype, device=d)
+        self.pooled = torch.empty(batch, h, dtype=dtype, device=d)
+        # one hipGraph memory pool for every plan on these buffers (graph temporaries such as
+        # the GELU projection output are reused across capacities instead of duplicated)
+        self.pool = torch.cuda.graph_pool_handle() if torch.device(d).type == "cuda" else None
+
+
 class BertEncoderPlan:
     """Preallocated buffers + launch sequence for one (batch, seq); hipGraph-captured.
 
@@ -190,9 +242,16 @@ class BertEncoderPlan:
     which measure 1.2-1.5x faster on the 32768 x {768..3072} x {768, 3072} shapes
     (``bench/probe_hipblaslt.py`` vs ``bench/gemm_tune.py``); the residual adds then move
     into the fused residual+LayerNorm kernel.  Embedding+LN, attention, residual+LN and
-    the pooler/classifier stay on the hand-written kernels either way."""
+    the pooler/classifier stay on the hand-written kernels either way.
 
-    def __init__(self, w: BertDeviceWeights, batch: int, seq: int, use_graph: bool = True, gemm: str | None = None):
+    ``tokens=T`` makes the plan padding-free: a packing kernel compacts the batch's
+    non-pad tokens into T rows (positions and per-sequence offsets on the device), every
+    projection / LayerNorm runs on those T rows, attention runs per packed sequence
+    (``cu_seqlens``) and the pooler gathers each sequence's first row — the classifier
+    output is that of the padded plan, for the tokens that exist."""
+
+    def __init__(self, w: BertDeviceWeights, batch: int, seq: int, use_graph: bool = True, gemm: str | None = None,
+                 tokens: int | None = None, shared: BertBuffers | None = None):
         cfg = w.cfg
         self.w, self.B, self.S = w, batch, seq
         if gemm is None:
@@ -200,54 +259,81 @@ class BertEncoderPlan:
         if gemm not in ("blas", "mfma"):
             raise ValueError("gemm must be 'blas' or 'mfma'")
         self.gemm_impl = gemm
+        if gemm == "blas" and w.word.device.type == "cuda":
+            load_gemm_table()
+        self.packed = tokens is not None
+        T = tokens if self.packed else batch * seq
+        self.T = T
         d = w.word.device
         dt = w.word.dtype
-        T = batch * seq
-        h = cfg.hidden
-        self.ids = torch.zeros(T, dtype=torch.int32, device=d)
-        self.x = torch.empty(T, h, dtype=dt, device=d)
-        self.y = torch.empty(T, h, dtype=dt, device=d)
-        self.qkv = torch.empty(T, 3 * h, dtype=dt, device=d)
-        self.ctx = torch.empty(T, h, dtype=dt, device=d)
-        self.x2 = torch.empty(T, h, dtype=dt, device=d)
-        self.ffn = torch.empty(T, cfg.intermediate, dtype=dt, device=d)
-        self.cls_in = torch.empty(batch, h, dtype=dt, device=d)
-        self.pooled = torch.empty(batch, h, dtype=dt, device=d)
-        self.logits = torch.empty(batch, w.cls_w.shape[0], dtype=dt, device=d)
+        b = shared if shared is not None else BertBuffers(cfg, batch, seq, T, d, dt)
+        if b.x.shape[0] < T:
+            raise ValueError(f"shared buffers hold {b.x.shape[0]} rows, plan needs {T}")
+        self.bufs = b
+        self.ids = b.ids
+        self.pids, self.ppos, self.cu, self.cls_idx = b.pids[:T], b.ppos[:T], b.cu, b.cls
+        self.x, self.y, self.qkv, self.ctx, self.x2, self.ffn = (t[:T] for t in (b.x, b.y, b.qkv, b.ctx, b.x2, b.ffn))
+        self.cls_in, self.pooled = b.cls_in, b.pooled
+        if not hasattr(b, "logits"):
+            b.logits = torch.empty(batch, w.cls_w.shape[0], dtype=dt, device=d)
+        self.logits = b.logits
         self.graph = None
         if use_graph and d.type == "cuda":
             self._capture()
 
+    def _embed(self):
+        w, cfg = self.w, self.w.cfg
+        if self.packed:
+            K.pack_tokens(self.ids.view(self.B, self.S), HashingTokenizer.PAD, self.T, self.pids, self.ppos, self.cu,
+                          self.cls_idx)
+            K.embed_layernorm(self.pids, None, w.word, w.pos, w.type, w.emb_g, w.emb_b, self.S, cfg.eps, out=self.x,
+                              pos_ids=self.ppos)
+        else:
+            K.embed_layernorm(self.ids, None, w.word, w.pos, w.type, w.emb_g, w.emb_b, self.S, cfg.eps, out=self.x)
+
+    def _attention(self):
+        cfg = self.w.cfg
+        if self.packed:
+            K.attention(self.qkv, None, self.B, self.S, cfg.heads, out=self.ctx, cu_seqlens=self.cu)
+        else:
+            K.attention(self.qkv, self.ids, self.B, self.S, cfg.heads, out=self.ctx)
+
+    def _pool(self):
+        w, B, S = self.w, self.B, self.S
+        if self.packed:
+            torch.index_select(self.x, 0, self.cls_idx, out=self.cls_in)
+        else:
+            self.cls_in.copy_(self.x.view(B, S, -1)[:, 0])
+        K.gemm(self.cls_in, w.pool_w, w.pool_b, act="tanh", out=self.pooled)
+        K.gemm(self.pooled, w.cls_w, w.cls_b, out=self.logits)
+
     def _run(self):
-        w, cfg, B, S = self.w, self.w.cfg, self.B, self.S
-        K.embed_layernorm(self.ids, None, w.word, w.pos, w.type, w.emb_g, w.emb_b, S, cfg.eps, out=self.x)
+        w = self.w
+        self._embed()
         if self.gemm_impl == "blas":
             return self._run_blas()
+        cfg = w.cfg
         for L in w.layers:
             K.gemm(self.x, L["qkv_w"], L["qkv_b"], out=self.qkv)
-            K.attention(self.qkv, self.ids, B, S, cfg.heads, out=self.ctx)
+            self._attention()
             K.gemm(self.ctx, L["o_w"], L["o_b"], residual=self.x, out=self.y)
             K.layernorm(self.y, L["ln1_g"], L["ln1_b"], eps=cfg.eps, out=self.x)
             K.gemm(self.x, L["i_w"], L["i_b"], act="gelu", out=self.ffn)
             K.gemm(self.ffn, L["f_w"], L["f_b"], residual=self.x, out=self.y)
             K.layernorm(self.y, L["ln2_g"], L["ln2_b"], eps=cfg.eps, out=self.x)
-        self.cls_in.copy_(self.x.view(B, S, -1)[:, 0])
-        K.gemm(self.cls_in, w.pool_w, w.pool_b, act="tanh", out=self.pooled)
-        K.gemm(self.pooled, w.cls_w, w.cls_b, out=self.logits)
+        self._pool()
 
     def _run_blas(self):
-        w, cfg, B, S = self.w, self.w.cfg, self.B, self.S
+        w, cfg = self.w, self.w.cfg
         for L in w.layers:
             torch.addmm(L["qkv_b16"], self.x, L["qkv_w"].t(), out=self.qkv)
-            K.attention(self.qkv, self.ids, B, S, cfg.heads, out=self.ctx)
+            self._attention()
             torch.addmm(L["o_b16"], self.ctx, L["o_w"].t(), out=self.y)
             K.layernorm(self.y, L["ln1_g"], L["ln1_b"], residual=self.x, eps=cfg.eps, out=self.x2)
             ffn = torch._addmm_activation(L["i_b16"], self.x2, L["i_w"].t(), use_gelu=True)
             torch.addmm(L["f_b16"], ffn, L["f_w"].t(), out=self.y)
             K.layernorm(self.y, L["ln2_g"], L["ln2_b"], residual=self.x2, eps=cfg.eps, out=self.x)
-        self.cls_in.copy_(self.x.view(B, S, -1)[:, 0])
-        K.gemm(self.cls_in, w.pool_w, w.pool_b, act="tanh", out=self.pooled)
-        K.gemm(self.pooled, w.cls_w, w.cls_b, out=self.logits)
+        self._pool()
 
     def _capture(self):
         s = torch.cuda.Stream(self.ids.device)
@@ -258,7 +344,7 @@ class BertEncoderPlan:
         torch.cuda.current_stream(self.ids.device).wait_stream(s)
         torch.cuda.synchronize(self.ids.device)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with graph_capture(g, pool=self.bufs.pool):
             self._run()
         self.graph = g
 
@@ -280,11 +366,67 @@ class BertEncoderPlan:
         self.replay()
         return torch.softmax(self.logits[:, : self.w.cfg.num_labels].float(), -1)
 
-    def flops(self) -> float:
-        cfg, T = self.w.cfg, self.B * self.S
+    def flops(self, lengths=None) -> float:
+        """Encoder FLOPs of one replay; with ``lengths`` (per-sequence real tokens) the
+        useful FLOPs of a padding-free batch."""
+        cfg = self.w.cfg
         h, i = cfg.hidden, cfg.intermediate
-        per_layer = 2 * T * (3 * h * h + h * h + 2 * h * i) + 4 * self.B * cfg.heads * self.S * self.S * (h // cfg.heads)
+        lens = np.full(self.B, self.S) if lengths is None else np.asarray(lengths)
+        T = float(lens.sum())
+        per_layer = 2 * T * (3 * h * h + h * h + 2 * h * i) + 4 * cfg.heads * float((lens ** 2).sum()) * (h // cfg.heads)
         return cfg.layers * per_layer
+
+
+class PackedBertEncoder:
+    """Padding-free encoder for a (batch, seq) micro-batch: one captured plan per token
+    capacity (multiples of ``granule`` up to batch*seq), all on one shared buffer set.
+    ``select(host_ids, n)`` picks the smallest capacity holding the batch's real tokens —
+    counted on the host from the pinned staging slot, so no device sync is needed; the
+    device-side packing kernel then compacts the same tokens.  Implements the plan
+    protocol of ``PipelinedGpuRunner`` (``input_buffer`` / ``replay`` / ``output_tensors``)."""
+
+    def __init__(self, w: BertDeviceWeights, batch: int, seq: int, use_graph: bool = True, gemm: str | None = None,
+                 granule: int = 2048):
+        self.w, self.B, self.S = w, batch, seq
+        full = batch * seq
+        granule = max(16, min(granule, full))
+        caps = sorted({min(full, g) for g in range(granule, full + granule, granule)})
+        self.bufs = BertBuffers(w.cfg, batch, seq, full, w.word.device, w.word.dtype)
+        self.plans = {c: BertEncoderPlan(w, batch, seq, use_graph, gemm, tokens=c, shared=self.bufs) for c in caps}
+        self.caps = caps
+        self.current = self.plans[caps[-1]]
+        self.ids = self.bufs.ids
+        self.graph = self.current.graph
+
+    def capacity_for(self, n_tokens: int) -> int:
+        for c in self.caps:
+            if c >= n_tokens:
+                return c
+        raise ValueError(f"{n_tokens} tokens exceed batch*seq = {self.caps[-1]}")
+
+    def select(self, host_ids, n: int | None = None) -> BertEncoderPlan:
+        a = host_ids.numpy() if isinstance(host_ids, torch.Tensor) else np.asarray(host_ids)
+        self.current = self.plans[self.capacity_for(int(np.count_nonzero(a != HashingTokenizer.PAD)))]
+        return self.current
+
+    # plan protocol
+    def input_buffer(self, feed: str) -> torch.Tensor:
+        return self.ids.view(self.B, self.S)
+
+    def replay(self):
+        self.current.replay()
+
+    def output_tensors(self):
+        return self.current.output_tensors()
+
+    def __call__(self, ids: torch.Tensor) -> torch.Tensor:
+        self.select(ids.cpu())
+        self.ids.view(self.B, self.S).copy_(ids)
+        self.current.replay()
+        return torch.softmax(self.current.logits[:, : self.w.cfg.num_labels].float(), -1)
+
+    def flops(self, lengths=None) -> float:
+        return self.current.flops(lengths)
 
 
 class BertClassifierModel(RichModel, BatchedGpuModel):
@@ -309,7 +451,8 @@ class BertClassifierModel(RichModel, BatchedGpuModel):
         dev = torch.device(self.device) if self.device is not None else default_device()
         host = load_tf_checkpoint(self.checkpoint, self.cfg) if self.checkpoint else init_bert_weights(self.cfg, self.seed)
         self._w = BertDeviceWeights(host, self.cfg, dev)
-        self._plans = {b: BertEncoderPlan(self._w, b, self.seq_len, self.use_graph) for b in self.buckets}
+        # padding-free encoders: each micro-batch runs on the token capacity of its real tokens
+        self._plans = {b: PackedBertEncoder(self._w, b, self.seq_len, self.use_graph) for b in self.buckets}
         if dev.type == "cuda":
             from ...batching.engine import PipelinedGpuRunner
 

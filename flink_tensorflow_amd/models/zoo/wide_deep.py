@@ -30,6 +30,7 @@ import torch.nn.functional as F
 
 from ...io import bundle
 from ...ops.autograd import Linear
+from ...utils.tracing import graph_capture
 from ...ops.embedding import SparseEmbedding
 from ...parallel import comm
 from ...runtime.model_functions import CheckpointedModel, model_state_dir
@@ -189,7 +190,7 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
                 self._step(self._static)
         torch.cuda.current_stream(dev).wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with graph_capture(g):
             self._static_loss = self._step(self._static)
         self._graph = g
 

@@ -350,27 +350,45 @@ def softmax_topk(logits: torch.Tensor, k: int, want_probs: bool = False, vals=No
 
 
 # ------------------------------------------------------------------------------ attention
-def attention(qkv: torch.Tensor, ids: torch.Tensor, batch: int, seq: int, heads: int, pad_id: int = 0,
-              scale: float | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+def attention(qkv: torch.Tensor, ids: torch.Tensor | None, batch: int, seq: int, heads: int, pad_id: int = 0,
+              scale: float | None = None, out: torch.Tensor | None = None,
+              cu_seqlens: torch.Tensor | None = None) -> torch.Tensor:
     """Multi-head self-attention over the fused QKV projection output.
 
-    ``qkv`` [B*S, 3*H*64] bf16 (Q|K|V blocks, head h at h*64), ``ids`` [B*S] int32 token
-    ids (keys whose id == ``pad_id`` are masked).  Returns ctx [B*S, H*64]."""
-    T = batch * seq
+    Padded batch: ``qkv`` [B*S, 3*H*64] bf16 (Q|K|V blocks, head h at h*64), ``ids`` [B*S]
+    int32 token ids (keys whose id == ``pad_id`` are masked).  Packed batch
+    (``cu_seqlens`` [B+1] int32 given, ``seq`` = the longest sequence): sequence b is rows
+    ``cu[b]:cu[b+1]`` of ``qkv``, no padding; rows past ``cu[B]`` are left untouched.
+    Returns ctx [rows, H*64]."""
+    T = qkv.shape[0] if cu_seqlens is not None else batch * seq
     Dh = qkv.shape[1] // (3 * heads)
     if qkv.shape != (T, 3 * heads * Dh):
         raise ValueError(f"attention: qkv shape {tuple(qkv.shape)} != {(T, 3 * heads * Dh)}")
-    if ids.numel() != T:
+    if cu_seqlens is None and (ids is None or ids.numel() != T):
         raise ValueError("attention: ids must have B*S entries")
+    if cu_seqlens is not None and cu_seqlens.numel() != batch + 1:
+        raise ValueError("attention: cu_seqlens must have B+1 entries")
     scale = (1.0 / Dh ** 0.5) if scale is None else scale
     if out is None:
         out = torch.empty((T, heads * Dh), dtype=qkv.dtype, device=qkv.device)
     if qkv.is_cuda:
         _check(qkv, "qkv", device=qkv.device)
         _check(out, "out", device=qkv.device)
-        _check(ids, "ids", torch.int32, qkv.device)
-        _hip().attention_fwd_bf16(qkv.data_ptr(), ids.data_ptr(), out.data_ptr(), batch, seq, heads, Dh, pad_id,
-                                  float(scale), _stream())
+        if cu_seqlens is not None:
+            _check(cu_seqlens, "cu_seqlens", torch.int32, qkv.device)
+        else:
+            _check(ids, "ids", torch.int32, qkv.device)
+        _hip().attention_fwd_bf16(qkv.data_ptr(), _ptr(ids) if cu_seqlens is None else 0, _ptr(cu_seqlens),
+                                  out.data_ptr(), batch, seq, heads, Dh, pad_id, float(scale), _stream())
+        return out
+    if cu_seqlens is not None:
+        cu = cu_seqlens.tolist()
+        for b in range(batch):
+            a, e = cu[b], cu[b + 1]
+            if e > a:
+                q, k, v = qkv[a:e].float().reshape(e - a, 3, heads, Dh).permute(1, 2, 0, 3)
+                p = torch.softmax((q @ k.transpose(-1, -2)) * scale, -1)
+                out[a:e] = (p @ v).permute(1, 0, 2).reshape(e - a, heads * Dh).to(out.dtype)
         return out
     q, k, v = qkv.float().reshape(batch, seq, 3, heads, Dh).permute(2, 0, 3, 1, 4)
     s = (q @ k.transpose(-1, -2)) * scale
@@ -382,10 +400,40 @@ def attention(qkv: torch.Tensor, ids: torch.Tensor, batch: int, seq: int, heads:
     return out
 
 
+def pack_tokens(ids: torch.Tensor, pad_id: int, t_cap: int, packed: torch.Tensor, pos: torch.Tensor,
+                cu: torch.Tensor, cls: torch.Tensor) -> int | None:
+    """Padding-free packing of ``ids`` [B, S]: the non-pad tokens in row order into
+    ``packed[:T_eff]`` (their in-row positions into ``pos``), row offsets ``cu`` [B+1] and
+    the first-token row of each sequence ``cls`` [B]; ``packed[T_eff:t_cap]`` = pad.
+    Device path: one kernel, no host sync (returns None); host path returns T_eff."""
+    B, S = ids.shape
+    if ids.is_cuda:
+        for t, n in ((ids, "ids"), (packed, "packed"), (pos, "pos"), (cu, "cu"), (cls, "cls")):
+            _check(t, n, torch.int32, ids.device)
+        _hip().pack_tokens(ids.data_ptr(), B, S, pad_id, t_cap, packed.data_ptr(), pos.data_ptr(), cu.data_ptr(),
+                           cls.data_ptr(), _stream())
+        return None
+    keep = ids != pad_id
+    lens = keep.sum(1)
+    offs = torch.zeros(B + 1, dtype=torch.int64)
+    offs[1:] = torch.cumsum(lens, 0)
+    n = int(offs[-1])
+    if n > t_cap:
+        raise ValueError(f"pack_tokens: {n} tokens exceed the capacity {t_cap}")
+    packed.zero_().add_(pad_id)
+    pos.zero_()
+    packed[:n] = ids[keep]
+    pos[:n] = torch.arange(S, dtype=torch.int32).expand(B, S)[keep]
+    cu.copy_(offs.to(torch.int32))
+    cls.copy_(offs[:-1].clamp(max=t_cap - 1).to(torch.int32))
+    return n
+
+
 def embed_layernorm(ids: torch.Tensor, type_ids: torch.Tensor | None, word: torch.Tensor, pos: torch.Tensor,
                     type_emb: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, seq: int, eps: float = 1e-12,
-                    out: torch.Tensor | None = None) -> torch.Tensor:
-    """``LN(word[ids] + pos[t % S] + type[type_ids])`` → [T, D] bf16 (one fused pass)."""
+                    out: torch.Tensor | None = None, pos_ids: torch.Tensor | None = None) -> torch.Tensor:
+    """``LN(word[ids] + pos[p] + type[type_ids])`` → [T, D] bf16 (one fused pass), with the
+    position ``p = t % seq`` (padded batch) or ``pos_ids[t]`` (packed batch)."""
     T = ids.numel()
     V, D = word.shape
     if out is None:
@@ -396,13 +444,17 @@ def embed_layernorm(ids: torch.Tensor, type_ids: torch.Tensor | None, word: torc
             _check(t, n, device=ids.device)
         if type_ids is not None:
             _check(type_ids, "type_ids", torch.int32, ids.device)
+        if pos_ids is not None:
+            _check(pos_ids, "pos_ids", torch.int32, ids.device)
         if pos.shape[0] < seq:
             raise ValueError("embed_layernorm: position table shorter than the sequence")
-        _hip().embed_ln_bf16(ids.data_ptr(), _ptr(type_ids), word.data_ptr(), pos.data_ptr(), type_emb.data_ptr(),
-                             gamma.data_ptr(), beta.data_ptr(), out.data_ptr(), T, seq, D, V, float(eps), _stream())
+        _hip().embed_ln_bf16(ids.data_ptr(), _ptr(type_ids), _ptr(pos_ids), word.data_ptr(), pos.data_ptr(),
+                             type_emb.data_ptr(), gamma.data_ptr(), beta.data_ptr(), out.data_ptr(), T, seq, D, V,
+                             float(eps), _stream())
         return out
     idx = ids.long().clamp(0, V - 1)
-    x = word.float()[idx] + pos.float()[torch.arange(T) % seq]
+    p = pos_ids.long() if pos_ids is not None else torch.arange(T) % seq
+    x = word.float()[idx] + pos.float()[p]
     x = x + type_emb.float()[type_ids.long() if type_ids is not None else torch.zeros(T, dtype=torch.long)]
     out.copy_(F.layer_norm(x, (D,), gamma.float(), beta.float(), eps).to(out.dtype))
     return out

@@ -29,6 +29,15 @@ def world() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
+def gpu_count() -> int:
+    """Visible GPUs.  ``torch.cuda.device_count()`` may answer 0 from its non-initialising
+    probe on a box where the HIP runtime does see the card; ask the runtime then."""
+    n = torch.cuda.device_count()
+    if n == 0 and torch.cuda.is_available():
+        n = torch._C._cuda_getDeviceCount()
+    return n
+
+
 def local_device(local_rank: int) -> int:
     """GPU index of a local rank (wraps when ranks outnumber visible GPUs — rehearsal only)."""
     n = torch.cuda.device_count()

@@ -406,7 +406,9 @@ class LocalExecutor:
 
         if not node.uses_gpu or not torch.cuda.is_available():
             return None
-        n = torch.cuda.device_count()
+        from ..parallel.comm import gpu_count
+
+        n = max(1, gpu_count())
         if self.world_size > 1:
             import os
 

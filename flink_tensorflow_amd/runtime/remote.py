@@ -124,7 +124,9 @@ def _worker_main(in_name: str, out_name: str):
             import torch
 
             if torch.cuda.is_available():
-                device = torch.device("cuda", spec["subtask"] % torch.cuda.device_count())
+                from ..parallel.comm import gpu_count
+
+                device = torch.device("cuda", spec["subtask"] % max(1, gpu_count()))
                 torch.cuda.set_device(device)
         metrics = MetricGroup(f"{spec['name']}[{spec['subtask']}]")
         ctx = RuntimeContext(spec["name"], spec["subtask"], spec["parallelism"], device, spec["attempt"], metrics,

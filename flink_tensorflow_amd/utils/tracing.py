@@ -58,3 +58,31 @@ def debug_sync() -> bool:
 
 def debug_poison() -> bool:
     return os.environ.get("FTM_DEBUG_POISON") == "1"
+
+
+# ------------------------------------------------------------------ hipGraph capture
+_CAPTURE_LOCK = None
+
+
+def graph_capture(graph, stream=None, pool=None):
+    """``torch.cuda.graph`` (hipGraph stream capture) safe next to other operator threads
+    of the same process: captures are serialised, and ``thread_local`` error mode keeps a
+    sibling subtask's allocations / launches on its own stream from invalidating (or being
+    rejected by) this capture.  ``pool`` shares one private memory pool between graphs that
+    never replay concurrently (e.g. the token-capacity plans of one encoder)."""
+    import contextlib
+    import threading
+
+    import torch
+
+    global _CAPTURE_LOCK
+    if _CAPTURE_LOCK is None:
+        _CAPTURE_LOCK = threading.RLock()
+
+    @contextlib.contextmanager
+    def _cm():
+        with _CAPTURE_LOCK:
+            with torch.cuda.graph(graph, pool=pool, stream=stream, capture_error_mode="thread_local"):
+                yield
+
+    return _cm()

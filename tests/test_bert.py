@@ -86,3 +86,87 @@ def test_embed_ln_kernel():
     ref = K.embed_layernorm(ids, None, word, pos, typ, gm, bt, S)
     got = K.embed_layernorm(ids.cuda(), None, word.cuda(), pos.cuda(), typ.cuda(), gm.cuda(), bt.cuda(), S)
     torch.testing.assert_close(got.float().cpu(), ref.float(), rtol=2e-2, atol=5e-2)
+
+
+def test_pack_tokens_host():
+    from flink_tensorflow_amd.ops import kernels as K
+
+    ids = _ids(5, 24, 2000, seed=3).reshape(5, 24)
+    T = int((ids != 0).sum())
+    packed, pos = torch.empty(T + 7, dtype=torch.int32), torch.empty(T + 7, dtype=torch.int32)
+    cu, cls = torch.empty(6, dtype=torch.int32), torch.empty(5, dtype=torch.int32)
+    assert K.pack_tokens(ids, 0, T + 7, packed, pos, cu, cls) == T
+    for b in range(5):
+        n = int((ids[b] != 0).sum())
+        assert cu[b + 1] - cu[b] == n and cls[b] == cu[b]
+        assert torch.equal(packed[cu[b]:cu[b + 1]], ids[b, :n]) and torch.equal(pos[cu[b]:cu[b + 1]], torch.arange(n, dtype=torch.int32))
+    assert (packed[T:] == 0).all()
+
+
+def test_packed_encoder_host_matches_padded():
+    """Padding-free execution changes nothing for the real tokens: same class
+    probabilities as the padded plan and as the fp32 reference."""
+    from flink_tensorflow_amd.models.zoo.bert import PackedBertEncoder
+
+    cfg = BertConfig.tiny(vocab_size=2000)
+    host = init_bert_weights(cfg, seed=4)
+    w = BertDeviceWeights(host, cfg, "cpu")
+    ids = _ids(6, 32, cfg.vocab_size, seed=5)
+    packed = PackedBertEncoder(w, 6, 32, granule=16)
+    got = packed(ids)
+    assert packed.current.T == packed.capacity_for(int((ids != 0).sum())) < 6 * 32
+    ref = torch.softmax(reference_forward(host, cfg, ids), -1)
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(got, BertEncoderPlan(w, 6, 32)(ids), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_packed_encoder_gpu_matches_padded():
+    from flink_tensorflow_amd.models.zoo.bert import PackedBertEncoder
+
+    cfg = BertConfig.base()
+    host = init_bert_weights(cfg, seed=6)
+    dev = torch.device("cuda", 0)
+    w = BertDeviceWeights(host, cfg, dev)
+    B, S = 16, 128
+    ids = _ids(B, S, cfg.vocab_size, seed=7)
+    padded = BertEncoderPlan(w, B, S)
+    packed = PackedBertEncoder(w, B, S, granule=256)
+    p_pad = padded(ids.to(dev)).cpu()
+    p_pack = packed(ids.to(dev)).cpu()
+    n = int((ids != 0).sum())
+    assert packed.current.T == packed.capacity_for(n) < B * S and packed.current.graph is not None
+    torch.testing.assert_close(p_pack, p_pad, rtol=0, atol=2e-2)
+    # final hidden state of every real token: packed rows vs the padded rows
+    hp = padded.x.view(B, S, -1).float().cpu()
+    hk = packed.current.x.float().cpu()
+    cu = packed.current.cu.cpu().tolist()
+    for b in range(B):
+        m = cu[b + 1] - cu[b]
+        cos = torch.nn.functional.cosine_similarity(hk[cu[b]:cu[b + 1]], hp[b, :m], dim=-1)
+        assert cos.min() > 0.99, (b, cos.min())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [128, 77])
+def test_packed_attention_and_pack_kernel_gpu(S):
+    from flink_tensorflow_amd.ops import kernels as K
+
+    B, H = 5, 12
+    ids = _ids(B, S, 30000, seed=S).reshape(B, S)
+    T = int((ids != 0).sum())
+    cap = T + 100
+    outs = [torch.empty(cap, dtype=torch.int32) for _ in range(2)] + [torch.empty(B + 1, dtype=torch.int32),
+                                                                      torch.empty(B, dtype=torch.int32)]
+    K.pack_tokens(ids, 0, cap, *outs)
+    douts = [torch.full_like(t, -7).cuda() for t in outs]
+    K.pack_tokens(ids.cuda(), 0, cap, *douts)
+    torch.cuda.synchronize()
+    for a, b in zip(outs, douts):
+        assert torch.equal(a, b.cpu())
+    g = torch.Generator().manual_seed(1)
+    qkv = torch.randn(cap, 3 * H * 64, generator=g).to(torch.bfloat16)
+    ref = K.attention(qkv, None, B, S, H, out=torch.zeros(cap, H * 64, dtype=torch.bfloat16), cu_seqlens=outs[2])
+    got = K.attention(qkv.cuda(), None, B, S, H, out=torch.zeros(cap, H * 64, dtype=torch.bfloat16, device="cuda"),
+                      cu_seqlens=douts[2])
+    torch.testing.assert_close(got.float().cpu(), ref.float(), rtol=2e-2, atol=2e-2)

@@ -107,7 +107,7 @@ def test_remote_batched_resnet_gpu():
 
     def run(remote):
         env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
-        s = env.from_collection(list(enumerate(imgs))).rebalance() \
+        s = env.from_collection(imgs).rebalance() \
             .map_with_model_batched(model, None, max_batch=16, max_delay_ms=5, emit_batches=False)
         if remote:
             s = s.run_in_processes()
@@ -115,5 +115,5 @@ def test_remote_batched_resnet_gpu():
 
     local, remote = run(False), run(True)
     assert len(remote) == len(local) == 40
-    top1 = lambda res: sorted(r[0][1] for r in res)  # noqa: E731
+    top1 = lambda res: sorted(r[0][1] for r in res)  # noqa: E731 - each result: top-k (prob, label)
     assert top1(remote) == top1(local)

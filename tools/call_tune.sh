@@ -1,5 +1,4 @@
 source tools/gpu_steps.sh
-step build 400 python -c "import __graft_entry__ as g; g.build()"
-step pytest_gpu 600 python -m pytest tests -q -m gpu -x
-step tune 600 python bench/conv_tune.py 256
-step bench 400 python bench.py --steps 20 --warmup 5
+step pytest_remote 300 python -u -m pytest tests/test_remote.py -x -v -m gpu --timeout 200 --timeout-method thread
+step tune_bert 600 python -u bench/tune_bert_gemms.py --out gpurun_out/tunableop_gfx950.csv
+step tune_cmp 300 python -u bench/tune_bert_gemms.py --out gpurun_out/tunableop_gfx950.csv --compare
