@@ -435,8 +435,13 @@ class BertClassifierModel(RichModel, BatchedGpuModel):
     _TRANSIENT = ("_w", "_plans", "_runner")
 
     def __init__(self, cfg: BertConfig | None = None, seq_len: int = 128, buckets=(64, 256), seed: int = 0,
-                 device=None, checkpoint: str | None = None, depth: int = 3, use_graph: bool = True):
+                 device=None, checkpoint: str | None = None, depth: int = 3, use_graph: bool = True,
+                 distributed_weights: bool = False):
         self.cfg = cfg or BertConfig.base()
+        # DP over ranks (one process per GPU): rank 0's weights are broadcast to every rank
+        # at open (one flattened RCCL broadcast per dtype over xGMI) instead of each rank
+        # reading the checkpoint (SURVEY §2.13 model distribution)
+        self.distributed_weights = distributed_weights
         self.seq_len = seq_len
         self.buckets = tuple(sorted(buckets))
         self.seed = seed
@@ -451,6 +456,10 @@ class BertClassifierModel(RichModel, BatchedGpuModel):
         dev = torch.device(self.device) if self.device is not None else default_device()
         host = load_tf_checkpoint(self.checkpoint, self.cfg) if self.checkpoint else init_bert_weights(self.cfg, self.seed)
         self._w = BertDeviceWeights(host, self.cfg, dev)
+        if self.distributed_weights:
+            from ...parallel import comm
+
+            comm.broadcast_tensors(self._w.tensors(), src=0)  # before capture: plans read these in place
         # padding-free encoders: each micro-batch runs on the token capacity of its real tokens
         self._plans = {b: PackedBertEncoder(self._w, b, self.seq_len, self.use_graph) for b in self.buckets}
         if dev.type == "cuda":

@@ -31,8 +31,10 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
     def __init__(self, graph_source: Callable[[], GraphDef] | str, image_hw: tuple[int, int],
                  buckets: Sequence[int] = (64, 256), top_k: int = 5, labels: Sequence[str] | None = None,
                  feed: str = "images:0", fetches: Sequence[str] = ("top_k:0", "top_k:1"), depth: int = 3,
-                 device=None, use_graph: bool = True, precision: str = "bf16", calibration_images=None):
+                 device=None, use_graph: bool = True, precision: str = "bf16", calibration_images=None,
+                 distributed_weights: bool = False):
         super().__init__(device)
+        self.distributed_weights = distributed_weights  # DP: broadcast rank 0's compiled weights at open
         self.precision = precision
         self.calibration_images = calibration_images  # uint8 [n, H, W, 3] for fp8 scales (synthetic if None)
         self.graph_source = graph_source
@@ -72,6 +74,11 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
                                                use_graph=self.use_graph, strict=True, precision=self.precision,
                                                calibration=self._calibration(b), arena=self._arena)
                            for b in sorted(self.buckets, reverse=True)}
+            if self.distributed_weights:
+                from ...parallel import comm
+
+                # in place, so the captured hipGraphs keep reading the same buffers
+                comm.broadcast_tensors([t for p in self._plans.values() for t in p.params], src=0)
             self._runner = PipelinedGpuRunner(self._plans, self.feed, lambda p: p.output_tensors(), (H, W, 3),
                                               torch.uint8, depth=self.depth, device=dev)
 

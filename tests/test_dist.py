@@ -146,3 +146,24 @@ def test_distributed_stream_partitions_sources():
     allv = sorted(out[0] + out[1])
     assert allv == [v * 10 for v in range(40)]
     assert set(out[0]).isdisjoint(out[1])
+
+
+def _bert_weights(rank, world):
+    import numpy as np
+
+    from flink_tensorflow_amd.models.zoo.bert import BertClassifierModel, BertConfig
+
+    m = BertClassifierModel(BertConfig.tiny(), seq_len=16, buckets=(4,), seed=rank, device="cpu",
+                            distributed_weights=True)
+    m.open()
+    p = m.predict(["streaming inference", "on every rank", "same weights"])
+    m.close()
+    return np.asarray(p)
+
+
+def test_model_weights_broadcast_at_open():
+    """Ranks initialise different weights (seed = rank); with distributed_weights every rank
+    serves rank 0's model after open."""
+    out = _run(_bert_weights)
+    assert out[0].shape == (3, 2)
+    assert (out[0] == out[1]).all()
