@@ -20,16 +20,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from flink_tensorflow_amd.models.zoo.image_classifier import ResNet50Model  # noqa: E402
 from flink_tensorflow_amd.runtime import StreamExecutionEnvironment  # noqa: E402
-from flink_tensorflow_amd.runtime.functions import SinkFunction  # noqa: E402
+from flink_tensorflow_amd.runtime.sources import ThroughputSink  # noqa: E402
 
 
-class CountSink(SinkFunction):
-    def __init__(self):
-        super().__init__()
-        self.n = 0
-
-    def invoke(self, value):
-        self.n += 1
 
 
 def main():
@@ -50,12 +43,14 @@ def main():
     env = StreamExecutionEnvironment.get_execution_environment()
     model = ResNet50Model(image_hw=(a.hw, a.hw), buckets=(a.batch,), depth_layers=a.depth_layers)
     env.generate(images).map_with_model_batched(model, None, max_batch=a.batch, max_delay_ms=a.delay_ms,
-                                                name="resnet50").add_sink(CountSink())
+                                                name="resnet50").add_sink(sink := ThroughputSink())
     t0 = time.time()
     res = env.execute("resnet50-stream")
     el = time.time() - t0
     m = [v for k, v in res.metrics.items() if k.startswith("resnet50")][0]
+    steady = sink.rate(0.2)  # steady state: skip the first fifth (compile, capture, pipeline fill)
     print(json.dumps({"records": a.records, "seconds": round(el, 3), "records_per_s": round(a.records / el, 1),
+                      "steady_records_per_s": round(steady, 1) if steady else None,
                       "latency_s": m["histograms"].get("latency_s"), "batch": m["histograms"].get("batch_size")}))
 
 

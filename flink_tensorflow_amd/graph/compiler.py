@@ -825,6 +825,22 @@ class CompiledFunction:
         for n in absorbed:
             self._fused.add(n.name)
 
+        M = a.shape[0]
+        tiles = -(-M // 128) * -(-n_pad // 128)
+        if self.device.type == "cuda" and tiles < 64 and act == K.ACT_NONE and res_val is None:
+            # classifier heads (M = batch, e.g. 256 x 2048 -> 1000): 16 output tiles cannot
+            # fill 256 CUs; the library GEMM's split-K kernels do (measured 39 -> ~6 us)
+            b16 = self._dev(bias if bias is not None else torch.zeros(n_pad), torch.bfloat16)
+            self.params.append(b16)
+
+            def run_lib(xin=xin, out=out, w_dev=w_dev, b16=b16):
+                torch.addmm(b16, xin.buf, w_dev.t(), out=out.buf)
+
+            self._emit(node.name, "gemm_lib", run_lib, [xin], [out])
+            self.vals[(last.name, 0)] = out
+            self._alias_fused_outputs(absorbed, out)
+            return
+
         def run(xin=xin, out=out, res_val=res_val, w_dev=w_dev, b_dev=b_dev):
             K.gemm(xin.buf, w_dev, b_dev, res_val.buf if res_val is not None else None, act, out=out.buf)
 

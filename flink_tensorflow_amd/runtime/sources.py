@@ -242,3 +242,35 @@ class MemorySink(SinkFunction):
 
 class CollectSink(MemorySink):
     """A MemorySink whose results are returned by ``DataStream.execute_and_collect``."""
+
+
+class ThroughputSink(SinkFunction):
+    """Counts records and timestamps every ``every``-th one (process-wide registry keyed
+    like ``MemorySink``): ``rate(skip_fraction)`` is the steady-state records/s after the
+    warm-up part of the stream (compile, capture, pipeline fill)."""
+
+    STAMPS: dict[int, list] = defaultdict(list)
+    _LOCK = threading.Lock()
+    _NEXT = [0]
+
+    def __init__(self, every: int = 256):
+        super().__init__()
+        with ThroughputSink._LOCK:
+            self.key = ThroughputSink._NEXT[0]
+            ThroughputSink._NEXT[0] += 1
+        self.every = every
+        self._n = 0
+
+    def invoke(self, value):
+        self._n += 1
+        if self._n % self.every == 0:
+            with ThroughputSink._LOCK:
+                ThroughputSink.STAMPS[self.key].append((self._n, time.perf_counter()))
+
+    def rate(self, skip_fraction: float = 0.2) -> float | None:
+        with ThroughputSink._LOCK:
+            ts = sorted(ThroughputSink.STAMPS[self.key], key=lambda x: x[1])
+        k = int(len(ts) * skip_fraction)
+        if len(ts) < k + 2:
+            return None
+        return (ts[-1][0] - ts[k][0]) / (ts[-1][1] - ts[k][1])
