@@ -548,8 +548,21 @@ class LocalExecutor:
             if storage is not None and storage.latest() is not None:
                 restore_states = storage.load(storage.latest())
                 self.restore_dir = storage.chk_dir(storage.latest())
-        metrics = {f"{t.node.name}[{t.subtask}]": t.metrics.snapshot() for t in self.tasks}
+        metrics = {f"{t.node.name}[{t.subtask}]": _task_metrics(t) for t in self.tasks}
         return JobExecutionResult(self.job_name, time.time() - t0, self.attempt, completed, metrics)
+
+
+def _task_metrics(task) -> dict:
+    """The task's metrics; a worker-process subtask adds what its operator recorded in the
+    worker (latency / batch-size histograms, operator counters)."""
+    snap = task.metrics.snapshot()
+    w = getattr(getattr(task, "op", None), "worker_metrics", None)
+    if w:
+        for section in ("histograms", "gauges", "rates"):
+            snap.setdefault(section, {}).update(w.get(section, {}))
+        for k, v in w.get("counters", {}).items():
+            snap.setdefault("counters", {}).setdefault(k, v)
+    return snap
 
 
 def clone_function(fn):

@@ -94,10 +94,14 @@ def _worker_main(in_name: str, out_name: str):
     out = ShmChannel(out_name, create=False)
     op = None
     pending: list = []
+    parent = os.getppid()
+
+    def parent_alive() -> bool:
+        return os.getppid() == parent
 
     def flush():
         if pending:
-            out.send(("out", list(pending)))
+            out.send(("out", list(pending)), alive=parent_alive)  # a full ring never outlives the coordinator
             pending.clear()
 
     def emit(elem):
@@ -105,14 +109,13 @@ def _worker_main(in_name: str, out_name: str):
         if len(pending) >= _BATCH or not isinstance(elem, Record):
             flush()
 
-    parent = os.getppid()
     try:
         out.send(("attached",))  # the coordinator may now unlink the segment names
         while True:
             msg = inp.recv(1.0)
             if msg is not None:
                 break
-            if os.getppid() != parent:
+            if not parent_alive():
                 return  # coordinator gone
         kind, factory, spec, restore, restore_dir = msg
         assert kind == "init", kind
@@ -134,13 +137,13 @@ def _worker_main(in_name: str, out_name: str):
         ctx.global_index, ctx.global_parallelism = spec["global_index"], spec["global_parallelism"]
         ctx.worker_pid = os.getpid()
         op = cloudpickle.loads(factory)()
-        op.setup(ctx, Output(emit, lambda tag, v: (flush(), out.send(("side", [(tag, v)])))))
+        op.setup(ctx, Output(emit, lambda tag, v: (flush(), out.send(("side", [(tag, v)]), alive=parent_alive))))
         op.initialize(restore, restore_dir)
         op.open()
         while True:
             msg = inp.recv(_IDLE_S)
             if msg is None:
-                if os.getppid() != parent:
+                if not parent_alive():
                     break  # orphaned: the coordinator died
                 op.on_idle(time.time())
                 flush()
@@ -156,20 +159,20 @@ def _worker_main(in_name: str, out_name: str):
                 op.prepare_snapshot()
                 state = op.snapshot_state(msg[1], msg[2])
                 flush()
-                out.send(("state", msg[1], state))
+                out.send(("state", msg[1], state), alive=parent_alive)
                 continue
             elif kind == "notify":
                 op.notify_checkpoint_complete(msg[1])
             elif kind == "end":
                 op.end_input()
                 flush()
-                out.send(("ended",))
+                out.send(("ended",), alive=parent_alive)
                 continue
             elif kind == "close":
                 op.close()
                 op = None
                 flush()
-                out.send(("closed", metrics.snapshot()))
+                out.send(("closed", metrics.snapshot()), alive=parent_alive)
                 break
             op.on_idle(time.time())
             flush()

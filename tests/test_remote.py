@@ -52,6 +52,18 @@ def test_remote_map_runs_in_worker_processes():
     assert len(pids) == 2 and os.getpid() not in pids
 
 
+def test_remote_batched_operator_metrics():
+    """A micro-batching operator in a worker: its batch-size histogram (recorded in the
+    worker) reaches the job result."""
+    env = StreamExecutionEnvironment.get_execution_environment()
+    res_sink = env.from_collection(list(range(100))).map_with_model_batched(
+        object(), lambda m, vals: [v + 1 for v in vals], max_batch=16, max_delay_ms=2).run_in_processes().collect_into()
+    res = env.execute("remote-batched")
+    assert sorted(res_sink.results()) == list(range(1, 101))
+    m = [v for k, v in res.metrics.items() if k.startswith("batched-model")][0]
+    assert m["histograms"]["batch_size"]["max"] == 16
+
+
 class _RunningSum(ProcessFunction):
     def open(self, config=None):
         self.total = self.get_runtime_context().get_state(ValueStateDescriptor("total", 0))
