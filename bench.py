@@ -79,6 +79,7 @@ def main():
         raise SystemExit("bench.py needs a GPU")
     dev = torch.device("cuda", comm.local_device(local))
     torch.cuda.set_device(dev)
+    numa = comm.bind_to_gpu_numa(dev) if ws > 1 else None  # DP ranks stage records on their GPU's socket
 
     if args.model == "widedeep":
         return run_widedeep(args, dev, rank, ws)
@@ -229,6 +230,7 @@ def main():
             "weights_broadcast_bytes": nbytes,
             "plan": plan.summary() if hasattr(plan, "summary") else {"hip_graph": plan.graph is not None},
             "arena": arena.stats(),
+            "numa_binding_rank0": numa,
         }
         print(json.dumps(out), flush=True)
     if comm.is_dist():

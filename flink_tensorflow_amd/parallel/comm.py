@@ -44,6 +44,44 @@ def local_device(local_rank: int) -> int:
     return local_rank % n if n else 0
 
 
+def _cpulist(text: str) -> set[int]:
+    out = set()
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            out.update(range(int(a), int(b or a) + 1))
+    return out
+
+
+def bind_to_gpu_numa(device) -> dict | None:
+    """Pins this rank's CPU threads to the NUMA node of its GPU (best effort).
+
+    Every DP rank stages ~10 GB/s of decoded records through pinned host memory on an
+    8-GPU node; threads started after this call (the C++ gather pool) inherit the mask and
+    first-touch their staging memory on the GPU's socket instead of across the
+    inter-socket link.  Returns ``{"numa_node", "cpus"}`` or None when nothing was changed
+    (no NUMA info, or the allowed CPUs are all on another node)."""
+    import os
+
+    try:
+        p = torch.cuda.get_device_properties(device)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            node = int(f.read())
+        if node < 0:
+            return None
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            cpus = _cpulist(f.read())
+        allowed = os.sched_getaffinity(0)
+        mine = cpus & allowed
+        if not mine or mine == allowed:
+            return None
+        os.sched_setaffinity(0, mine)
+        return {"numa_node": node, "cpus": len(mine)}
+    except (OSError, ValueError, AttributeError, RuntimeError):
+        return None
+
+
 def init_distributed(backend: str | None = None, timeout_s: int = 600) -> bool:
     """Initialises the default process group when launched with WORLD_SIZE > 1."""
     rank, ws, local = world()

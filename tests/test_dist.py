@@ -167,3 +167,21 @@ def test_model_weights_broadcast_at_open():
     out = _run(_bert_weights)
     assert out[0].shape == (3, 2)
     assert (out[0] == out[1]).all()
+
+
+@pytest.mark.gpu
+def test_numa_binding_gpu():
+    """Best-effort NUMA pinning of a DP rank: either nothing to do, or a non-empty subset
+    of the CPUs this process may use; the mask is restored afterwards."""
+    from flink_tensorflow_amd.parallel import comm
+
+    before = os.sched_getaffinity(0)
+    try:
+        r = comm.bind_to_gpu_numa(torch.device("cuda", 0))
+        after = os.sched_getaffinity(0)
+        if r is None:
+            assert after == before
+        else:
+            assert after and after <= before and r["cpus"] == len(after)
+    finally:
+        os.sched_setaffinity(0, before)
