@@ -38,6 +38,7 @@ pools requantise on the fly; anything else reads a dequantised bf16 copy.
 from __future__ import annotations
 
 import logging
+import os
 from dataclasses import dataclass, field
 from typing import Any, Callable
 
@@ -616,6 +617,22 @@ class CompiledFunction:
                 self.vals[(pool[0].name, 0)] = out
                 self.fused_pools = getattr(self, "fused_pools", 0) + 1
                 return
+            self.vals[(last.name, 0)] = out
+            self._alias_fused_outputs(absorbed, out)
+            return
+
+        if (res_val is None and out.qscale is None and xin_shape_override is None and (xin.phys_c or Cin) == Cin
+                and os.environ.get("FTM_CONV3X3C64", "1") != "0"
+                and K.conv3x3_c64_eligible(tuple(xin.shape), tuple(w_ohwi.shape), (sh, sw), (pt, pb, pl, pr), (dh, dw),
+                                           None, act)):
+            # 64-channel 3x3 (ResNet stage 1): persistent kernel, filter bank resident in LDS
+            bz = b_dev if b_dev is not None else self._dev(torch.zeros(Cout), torch.float32)
+
+            def run_c(xin=xin, out=out, w_dev=w_dev, bz=bz):
+                K.conv3x3_c64(xin.buf, w_dev, bz, act, out=_target(out), out_channel_offset=_coff(out))
+
+            self._emit(node.name, "conv", run_c, [xin], [out], {"impl": "conv3x3c64"})
+            self.conv3x3c64 = getattr(self, "conv3x3c64", 0) + 1
             self.vals[(last.name, 0)] = out
             self._alias_fused_outputs(absorbed, out)
             return
@@ -1299,7 +1316,8 @@ class CompiledFunction:
         return {"steps": len(self.steps), "kinds": kinds, "glue_ops": sorted(set(self.glue_ops)),
                 "hip_graph": self._graph_obj is not None, "precision": self.precision,
                 "fp8_layers": self.fp8_layers, "fused_shortcuts": getattr(self, "fused_shortcuts", 0),
-                "fused_pools": getattr(self, "fused_pools", 0), "activation_bytes": self.activation_bytes,
+                "fused_pools": getattr(self, "fused_pools", 0), "conv3x3c64": getattr(self, "conv3x3c64", 0),
+                "activation_bytes": self.activation_bytes,
                 "param_bytes": self.param_bytes()}
 
 

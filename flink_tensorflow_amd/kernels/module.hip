@@ -13,6 +13,7 @@ void register_attention(pybind11::module_& m);
 void register_igemm_v2(pybind11::module_& m);
 void register_dconv(pybind11::module_& m);
 void register_elementwise(pybind11::module_& m);
+void register_conv3x3c64(pybind11::module_& m);
 
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "flink_tensorflow_amd CDNA4 (gfx950) kernels";
@@ -26,4 +27,5 @@ PYBIND11_MODULE(_hip, m) {
   register_igemm_v2(m);
   register_dconv(m);
   register_elementwise(m);
+  register_conv3x3c64(m);
 }

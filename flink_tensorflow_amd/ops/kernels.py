@@ -168,6 +168,47 @@ def conv2d_nhwc(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor | None
     return out
 
 
+def conv3x3_c64_eligible(x_shape, w_shape, stride, pad, dilation, residual, act) -> bool:
+    """The persistent LDS-resident-weights kernel (kernels/conv3x3c64.hip): 3x3, stride 1,
+    SAME padding, 64 -> 64 channels, no residual, bias (+ReLU) epilogue, H >= 8, W >= 32."""
+    N, H, W, Cin = x_shape
+    Cout, KH, KW, _ = w_shape
+    return (Cin == 64 and Cout == 64 and (KH, KW) == (3, 3) and tuple(stride) == (1, 1) and tuple(pad) == (1, 1, 1, 1)
+            and tuple(dilation) == (1, 1) and residual is None and act_code(act) in (ACT_NONE, ACT_RELU)
+            and H >= 8 and W >= 32)
+
+
+_NUM_CU: dict = {}
+
+
+def conv3x3_c64(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor, act=None, out: torch.Tensor | None = None,
+                out_channel_offset: int = 0) -> torch.Tensor:
+    """3x3 / s1 / SAME conv, 64 -> 64 channels, ``act(conv + bias)``; GPU: persistent
+    kernel with the filter bank resident in LDS; host: the fp32 reference conv."""
+    N, H, W, _ = x.shape
+    a = act_code(act)
+    if out is None:
+        out = torch.empty((N, H, W, 64), dtype=x.dtype if x.is_cuda else torch.float32, device=x.device)
+        out_channel_offset = 0
+    if not conv3x3_c64_eligible(tuple(x.shape), tuple(w_ohwi.shape), (1, 1), (1, 1, 1, 1), (1, 1), None, a):
+        raise ValueError(f"conv3x3_c64: unsupported shapes x {tuple(x.shape)} w {tuple(w_ohwi.shape)}")
+    if out.shape[:3] != (N, H, W) or out_channel_offset + 64 > out.shape[3]:
+        raise ValueError("conv3x3_c64: output buffer does not fit")
+    if x.is_cuda:
+        _check(x, "x", device=x.device)
+        _check(w_ohwi, "w", device=x.device)
+        _check(out, "out", device=x.device)
+        _check(bias, "bias", torch.float32, x.device)
+        dev = x.device.index if x.device.index is not None else torch.cuda.current_device()
+        if dev not in _NUM_CU:
+            _NUM_CU[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+        _hip().conv3x3c64_bf16(x.data_ptr(), w_ohwi.data_ptr(), bias.data_ptr(), out.data_ptr(), N, H, W, out.shape[3],
+                               out_channel_offset, a, _NUM_CU[dev], _stream())
+        return out
+    return conv2d_nhwc(x, w_ohwi, bias, None, (1, 1), (1, 1, 1, 1), (1, 1), a, out=out,
+                       out_channel_offset=out_channel_offset)
+
+
 def gemm(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = None, residual: torch.Tensor | None = None,
          act=None, out: torch.Tensor | None = None, cfg: int = -1) -> torch.Tensor:
     """``act(x[M,K] @ w[N,K]^T + bias + residual)``; leading dims of x are flattened."""

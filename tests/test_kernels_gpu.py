@@ -218,3 +218,25 @@ def test_lrn_kernel():
     ref = K.lrn(x, 5, 1.0, 1e-2, 0.75)
     got = K.lrn(x.to(DEV), 5, 1.0, 1e-2, 0.75)
     _close(got, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 56, 56), (3, 20, 40), (1, 8, 32), (2, 13, 37)])
+@pytest.mark.parametrize("act", [None, "relu"])
+def test_conv3x3_c64_kernel(shape, act):
+    """Persistent LDS-resident-weights 3x3 conv vs the fp32 reference (edge tiles overlap
+    when H % 8 or W % 32 != 0; output written into a wider buffer at a channel offset)."""
+    from flink_tensorflow_amd.ops import kernels as K
+
+    N, H, W = shape
+    g = torch.Generator().manual_seed(H * W)
+    x = torch.randn(N, H, W, 64, generator=g).to(torch.bfloat16)
+    w = (torch.randn(64, 3, 3, 64, generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(64, generator=g)
+    ref = K.conv2d_nhwc(x.float(), w.float(), b, None, (1, 1), (1, 1, 1, 1), (1, 1), act)
+    out = torch.full((N, H, W, 96), 7.0, dtype=torch.bfloat16, device="cuda")
+    K.conv3x3_c64(x.cuda(), w.cuda(), b.cuda(), act, out=out, out_channel_offset=16)
+    torch.cuda.synchronize()
+    got = out[..., 16:80].float().cpu()
+    torch.testing.assert_close(got, ref, rtol=2e-2, atol=3e-2)
+    assert (out[..., :16] == 7).all() and (out[..., 80:] == 7).all()
