@@ -60,6 +60,9 @@ def main():
                          "per-step batch size varies and each micro-batch runs on the smallest bucket")
     ap.add_argument("--dynamic", action="store_true", help="variable micro-batch sizes (uniform in [B/4, B])")
     ap.add_argument("--no-pack", action="store_true", help="bert: run padded batches (no token packing)")
+    ap.add_argument("--lanes", type=int, default=None,
+                    help="compute lanes: independent plan instances on their own HIP streams, batches round-robin "
+                         "(default: 3 for bert, 2 otherwise; measured in profiles/r01_lanes)")
     args = ap.parse_args()
 
     import torch
@@ -87,11 +90,12 @@ def main():
     HW = args.image_hw or (299 if args.model == "inception_v3" else 256)
     precision = args.precision or ("fp8" if args.model == "inception_v3" else "bf16")
     t0 = time.perf_counter()
-    plans = None
     from flink_tensorflow_amd.batching.arena import DeviceArena
     from flink_tensorflow_amd.config import EngineConfig
 
-    arena = DeviceArena(dev, EngineConfig().arena_bytes(dev), name=f"rank{rank}")  # this subtask's HBM share
+    lanes = args.lanes or (3 if args.model == "bert" else 2)
+    budget = EngineConfig().arena_bytes(dev) // lanes  # this subtask's HBM share, split over its lanes
+    lane_plans, params = [], []
     if args.model == "inception_v3":
         from flink_tensorflow_amd.models.zoo.inception_v3 import inception_v3_flops_per_image, inception_v3_graph_def
 
@@ -100,14 +104,16 @@ def main():
         rng = np.random.default_rng(1234 + rank)
         pool = rng.integers(0, 256, size=(args.pool, HW, HW, 3), dtype=np.uint8)
         calib = torch.from_numpy(pool[: min(64, args.pool)])
-        plans = {}
-        for b in sorted(sizes, reverse=True):  # one captured plan per bucket, largest first: one shared slab
-            cb = {"images:0": calib[:b] if b <= calib.shape[0] else calib.repeat((b + 63) // 64, 1, 1, 1)[:b]}
-            plans[b] = CompiledFunction(graph, {"images:0": ((b, HW, HW, 3), "UINT8")}, ["top_k:0", "top_k:1"], dev,
-                                        use_graph=not args.no_graph, strict=True, precision=precision,
-                                        calibration=cb if precision == "fp8" else None, arena=arena)
-        plan = plans[B]
-        params = list({t.data_ptr(): t for p in plans.values() for t in p.params}.values())  # interned: once
+        for lane in range(lanes):
+            arena = DeviceArena(dev, budget, name=f"rank{rank}/lane{lane}")
+            plans = {}
+            for b in sorted(sizes, reverse=True):  # one captured plan per bucket, largest first: one shared slab
+                cb = {"images:0": calib[:b] if b <= calib.shape[0] else calib.repeat((b + 63) // 64, 1, 1, 1)[:b]}
+                plans[b] = CompiledFunction(graph, {"images:0": ((b, HW, HW, 3), "UINT8")}, ["top_k:0", "top_k:1"],
+                                            dev, use_graph=not args.no_graph, strict=True, precision=precision,
+                                            calibration=cb if precision == "fp8" else None, arena=arena)
+            lane_plans.append(plans)
+            params += [t for p in plans.values() for t in p.params]
         feed, rec_shape, rec_dtype = "images:0", (HW, HW, 3), torch.uint8
         flops_per_record = inception_v3_flops_per_image(299)
         model_name = "Inception-v3"
@@ -116,9 +122,12 @@ def main():
     elif args.model == "resnet50":
         gd = resnet50_graph_def(image_hw=(HW, HW), top_k=5, seed=0)
         graph = Graph.from_graph_def(gd)
-        plan = CompiledFunction(graph, {"images:0": ((B, HW, HW, 3), "UINT8")}, ["top_k:0", "top_k:1"], dev,
-                                use_graph=not args.no_graph, strict=True, precision=precision, arena=arena)
-        params = plan.params
+        for lane in range(lanes):
+            arena = DeviceArena(dev, budget, name=f"rank{rank}/lane{lane}")
+            p = CompiledFunction(graph, {"images:0": ((B, HW, HW, 3), "UINT8")}, ["top_k:0", "top_k:1"], dev,
+                                 use_graph=not args.no_graph, strict=True, precision=precision, arena=arena)
+            lane_plans.append({B: p})
+            params += p.params
         feed, rec_shape, rec_dtype = "images:0", (HW, HW, 3), torch.uint8
         flops_per_record = resnet50_flops_per_image(224)
         rng = np.random.default_rng(1234 + rank)
@@ -132,10 +141,12 @@ def main():
         cfg = BertConfig.base()
         seq = args.seq_len
         w = BertDeviceWeights(init_bert_weights(cfg, seed=rank), cfg, dev)  # rank-local init, then broadcast
-        if args.no_pack:
-            plan = BertEncoderPlan(w, B, seq, use_graph=not args.no_graph)
-        else:  # padding-free: each micro-batch runs on the token capacity of its real tokens
-            plan = PackedBertEncoder(w, B, seq, use_graph=not args.no_graph)
+        for lane in range(lanes):  # lanes share the weights, each has its own activation buffers
+            if args.no_pack:
+                p = BertEncoderPlan(w, B, seq, use_graph=not args.no_graph)
+            else:  # padding-free: each micro-batch runs on the token capacity of its real tokens
+                p = PackedBertEncoder(w, B, seq, use_graph=not args.no_graph)
+            lane_plans.append({B: p})
         params = w.tensors()
         feed, rec_shape, rec_dtype = "ids", (seq,), torch.int32
         rng = np.random.default_rng(1234 + rank)
@@ -145,17 +156,19 @@ def main():
             pool[i, n:] = 0
         pool[:, 0] = 101
         # useful work: the real tokens of the records (padding rows are not counted as FLOPs)
-        flops_per_record = plan.flops(lens) / len(lens)
+        flops_per_record = lane_plans[0][B].flops(lens) / len(lens)
         model_name = "BERT-base (seq classification)"
         data = (f"synthetic token ids, seq {seq} (real lengths U[{seq // 2},{seq}]), random-init weights, "
                 + ("padded execution" if args.no_pack else "padding-free (packed) execution"))
+    plan = lane_plans[0][B]
+    params = list({t.data_ptr(): t for t in params}.values())  # interned / shared: each storage once
     # rank 0's weights to all ranks over RCCL (one flattened buffer per dtype); in place,
-    # so the captured hipGraph stays valid
+    # so the captured hipGraphs stay valid
     nbytes = comm.broadcast_tensors(params, src=0)
     compile_s = time.perf_counter() - t0
 
     records = [pool[i] for i in range(args.pool)]
-    runner = PipelinedGpuRunner(plans or {B: plan}, feed, lambda p: p.output_tensors(), rec_shape, rec_dtype,
+    runner = PipelinedGpuRunner(lane_plans, feed, lambda p: p.output_tensors(), rec_shape, rec_dtype,
                                 depth=args.depth, device=dev)
 
     cursor = 0
@@ -221,7 +234,8 @@ def main():
             "config": {"model": model_name, "global_batch": B * ws, "seq_len": seq,
                        "parallelism": f"dp{ws}", "micro_batch_per_gpu": B,
                        "input_hw": (299 if args.model == "inception_v3" else 224) if seq is None else None,
-                       "batch_buckets": sorted(plans) if plans else [B], "dynamic_batching": args.dynamic},
+                       "batch_buckets": sorted(lane_plans[0]), "dynamic_batching": args.dynamic,
+                       "compute_lanes": lanes},
             "p50_latency_ms": round(float(np.median(p50s)), 3),
             "p99_latency_ms": round(p99, 3),
             "per_gpu_records_per_s": round(per_gpu, 1),
@@ -229,7 +243,7 @@ def main():
             "compile_s": round(compile_s, 2),
             "weights_broadcast_bytes": nbytes,
             "plan": plan.summary() if hasattr(plan, "summary") else {"hip_graph": plan.graph is not None},
-            "arena": arena.stats(),
+            "arena": arena.stats() if args.model != "bert" else None,
             "numa_binding_rank0": numa,
         }
         print(json.dumps(out), flush=True)

@@ -25,7 +25,7 @@ from typing import Any, Callable, Sequence
 import numpy as np
 import torch
 
-from ..utils.tracing import trace_range
+from ..utils.tracing import capture_lock, trace_range
 
 from .. import _ext
 
@@ -65,12 +65,22 @@ class PipelinedGpuRunner:
     returns the device output tensors to bring back (small: top-k values/indices).  A plan
     with ``select(host_batch, n)`` chooses the concrete plan per batch from the staged
     host records (before the H2D copy).
+
+    ``plans`` may also be a list of such dicts — one per **compute lane**: independent plan
+    instances (own buffers) replayed on their own HIP streams, batches assigned round-robin,
+    so consecutive micro-batches overlap on the GPU (the tail of one graph's kernels fills
+    with the next graph's instead of idling CUs).  Results are always returned in
+    submission order.
     """
 
-    def __init__(self, plans: dict[int, Any], feed: str, fetch_bufs: Callable[[Any], Sequence[torch.Tensor]],
+    def __init__(self, plans, feed: str, fetch_bufs: Callable[[Any], Sequence[torch.Tensor]],
                  record_shape, record_dtype=torch.uint8, depth: int = 3, device=None, gather_threads: int = 8):
-        self.plans = dict(sorted(plans.items()))
+        lanes = plans if isinstance(plans, (list, tuple)) else [plans]
+        self.lanes = [dict(sorted(p.items())) for p in lanes]
+        self.plans = self.lanes[0]
         self.buckets = list(self.plans)
+        if any(list(p) != self.buckets for p in self.lanes):
+            raise ValueError("every compute lane needs the same batch buckets")
         self.feed = feed
         self.fetch_bufs = fetch_bufs
         self.device = torch.device(device or "cuda")
@@ -78,15 +88,18 @@ class PipelinedGpuRunner:
         self.record_dtype = record_dtype
         self.record_bytes = int(np.prod(record_shape)) * torch.empty((), dtype=record_dtype).element_size()
         self.copy_stream = torch.cuda.Stream(self.device)
-        self.compute_stream = torch.cuda.Stream(self.device)
+        self.compute_streams = [torch.cuda.Stream(self.device) for _ in self.lanes]
+        self.compute_stream = self.compute_streams[0]
         self.gather_threads = gather_threads
         self._native = _ext.native()
+        depth = max(depth, len(self.lanes) + 2)  # every lane busy + one batch being staged
         self.slots: dict[int, list[_Slot]] = {}
         for b, plan in self.plans.items():
             outs = [(tuple(t.shape), t.dtype) for t in fetch_bufs(plan)]
             self.slots[b] = [_Slot(b, self.record_shape, record_dtype, outs, self.device) for _ in range(depth)]
         self._next = {b: 0 for b in self.buckets}
-        self._inflight: list[_Slot] = []
+        self._lane = 0
+        self._inflight: list[_Slot] = []  # submission order
 
     def bucket_for(self, n: int) -> int:
         i = bisect.bisect_left(self.buckets, n)
@@ -103,9 +116,7 @@ class PipelinedGpuRunner:
         slots = self.slots[b]
         slot = slots[self._next[b]]
         self._next[b] = (self._next[b] + 1) % len(slots)
-        finished = []
-        if slot.busy:
-            finished.append(self._harvest(slot))
+        finished = self._harvest_through(slot) if slot.busy else []
         # host gather into the pinned slot (zero padding rows only when needed)
         with trace_range(f"gather[{n}/{b}]"):
             self._native.gather_into(slot.pinned_in.data_ptr(),
@@ -113,22 +124,25 @@ class PipelinedGpuRunner:
                                      self.record_bytes, self.gather_threads)
             if n < b:
                 slot.pinned_in[n:].zero_()
-        plan = self.plans[b]
+        lane = self._lane
+        self._lane = (self._lane + 1) % len(self.lanes)
+        plan = self.lanes[lane][b]
         select = getattr(plan, "select", None)
         if select is not None:  # e.g. the padding-free BERT encoder: pick a token-capacity plan
             plan = select(slot.pinned_in, n)
+        stream = self.compute_streams[lane]
         with trace_range("h2d"), torch.cuda.stream(self.copy_stream):
             slot.dev_in.copy_(slot.pinned_in, non_blocking=True)
             slot.h2d.record(self.copy_stream)
-        with torch.cuda.stream(self.compute_stream):
-            self.compute_stream.wait_event(slot.h2d)
-            with trace_range(f"forward[{b}]"):
+        with torch.cuda.stream(stream):
+            stream.wait_event(slot.h2d)
+            with trace_range(f"forward[{b}]@lane{lane}"):
                 plan.input_buffer(self.feed).copy_(slot.dev_in, non_blocking=True)
                 plan.replay()
             with trace_range("d2h"):
                 for dst, src in zip(slot.pinned_out, self.fetch_bufs(plan)):
                     dst.copy_(src, non_blocking=True)
-            slot.done.record(self.compute_stream)
+            slot.done.record(stream)
         slot.busy = True
         slot.n = n
         slot.ts = ingest_ts
@@ -137,24 +151,45 @@ class PipelinedGpuRunner:
         return finished
 
     def _harvest(self, slot: _Slot) -> BatchResult:
-        slot.done.synchronize()
+        # event waits / queries are rejected while a sibling subtask thread captures a
+        # hipGraph (its plans compile while this one already streams): query under the
+        # capture lock, never block while holding it
+        while True:
+            with capture_lock():
+                if slot.done.query():
+                    break
+            time.sleep(5e-5)
         slot.busy = False
         self._inflight.remove(slot)
         return BatchResult([t.clone() for t in slot.pinned_out], slot.n, slot.ts, time.perf_counter(),
                            slot.tags or [])
 
-    def poll(self) -> list[BatchResult]:
-        """Harvests completed batches without blocking."""
+    def _harvest_through(self, slot: _Slot) -> list[BatchResult]:
+        """Harvests every in-flight batch up to and including ``slot`` (order preserved)."""
         out = []
-        for s in list(self._inflight):
-            if s.done.query():
-                out.append(self._harvest(s))
+        while self._inflight:
+            head = self._inflight[0]
+            out.append(self._harvest(head))
+            if head is slot:
+                break
+        return out
+
+    def poll(self) -> list[BatchResult]:
+        """Harvests completed batches without blocking, oldest first, stopping at the
+        first one still running."""
+        out = []
+        while self._inflight:
+            with capture_lock():
+                ready = self._inflight[0].done.query()
+            if not ready:
+                break
+            out.append(self._harvest(self._inflight[0]))
         return out
 
     def drain(self) -> list[BatchResult]:
         out = []
-        for s in list(self._inflight):
-            out.append(self._harvest(s))
+        while self._inflight:
+            out.append(self._harvest(self._inflight[0]))
         return out
 
 

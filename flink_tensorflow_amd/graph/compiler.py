@@ -1258,17 +1258,18 @@ class CompiledFunction:
                                                                            node_stats=stats)]))
 
     def _capture(self):
-        s = torch.cuda.Stream(self.device)
-        s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
-            for _ in range(2):
+        with tracing.capture_lock():  # warm-up + device sync + capture: no sibling capture in between
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    self._run_steps()
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with tracing.graph_capture(g):
                 self._run_steps()
-        torch.cuda.current_stream(self.device).wait_stream(s)
-        torch.cuda.synchronize(self.device)
-        g = torch.cuda.CUDAGraph()
-        with tracing.graph_capture(g):
-            self._run_steps()
-        self._graph_obj = g
+            self._graph_obj = g
 
     def input_buffer(self, feed: str) -> torch.Tensor:
         return self._input_bufs[str(TensorName.parse(feed))]

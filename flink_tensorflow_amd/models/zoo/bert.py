@@ -27,7 +27,7 @@ import torch
 
 from ...ops import kernels as K
 from ...runtime.model_functions import BatchedGpuModel
-from ...utils.tracing import graph_capture
+from ...utils.tracing import capture_lock, graph_capture
 from ..core import RichModel, default_device
 
 
@@ -336,17 +336,18 @@ class BertEncoderPlan:
         self._pool()
 
     def _capture(self):
-        s = torch.cuda.Stream(self.ids.device)
-        s.wait_stream(torch.cuda.current_stream(self.ids.device))
-        with torch.cuda.stream(s):
-            for _ in range(2):
+        with capture_lock():  # warm-up + device sync + capture: no sibling capture in between
+            s = torch.cuda.Stream(self.ids.device)
+            s.wait_stream(torch.cuda.current_stream(self.ids.device))
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    self._run()
+            torch.cuda.current_stream(self.ids.device).wait_stream(s)
+            torch.cuda.synchronize(self.ids.device)
+            g = torch.cuda.CUDAGraph()
+            with graph_capture(g, pool=self.bufs.pool):
                 self._run()
-        torch.cuda.current_stream(self.ids.device).wait_stream(s)
-        torch.cuda.synchronize(self.ids.device)
-        g = torch.cuda.CUDAGraph()
-        with graph_capture(g, pool=self.bufs.pool):
-            self._run()
-        self.graph = g
+            self.graph = g
 
     # plan protocol used by PipelinedGpuRunner
     def input_buffer(self, feed: str) -> torch.Tensor:
@@ -436,8 +437,9 @@ class BertClassifierModel(RichModel, BatchedGpuModel):
 
     def __init__(self, cfg: BertConfig | None = None, seq_len: int = 128, buckets=(64, 256), seed: int = 0,
                  device=None, checkpoint: str | None = None, depth: int = 3, use_graph: bool = True,
-                 distributed_weights: bool = False):
+                 distributed_weights: bool = False, lanes: int = 3):
         self.cfg = cfg or BertConfig.base()
+        self.lanes = max(1, int(lanes))  # concurrent encoder instances on their own HIP streams
         # DP over ranks (one process per GPU): rank 0's weights are broadcast to every rank
         # at open (one flattened RCCL broadcast per dtype over xGMI) instead of each rank
         # reading the checkpoint (SURVEY §2.13 model distribution)
@@ -461,11 +463,13 @@ class BertClassifierModel(RichModel, BatchedGpuModel):
 
             comm.broadcast_tensors(self._w.tensors(), src=0)  # before capture: plans read these in place
         # padding-free encoders: each micro-batch runs on the token capacity of its real tokens
-        self._plans = {b: PackedBertEncoder(self._w, b, self.seq_len, self.use_graph) for b in self.buckets}
+        lanes = [{b: PackedBertEncoder(self._w, b, self.seq_len, self.use_graph) for b in self.buckets}
+                 for _ in range(self.lanes if dev.type == "cuda" else 1)]
+        self._plans = lanes[0]
         if dev.type == "cuda":
             from ...batching.engine import PipelinedGpuRunner
 
-            self._runner = PipelinedGpuRunner(self._plans, "ids", lambda p: p.output_tensors(), (self.seq_len,),
+            self._runner = PipelinedGpuRunner(lanes, "ids", lambda p: p.output_tensors(), (self.seq_len,),
                                               torch.int32, depth=self.depth, device=dev)
 
     def close(self):

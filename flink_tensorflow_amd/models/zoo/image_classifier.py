@@ -32,8 +32,9 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
                  buckets: Sequence[int] = (64, 256), top_k: int = 5, labels: Sequence[str] | None = None,
                  feed: str = "images:0", fetches: Sequence[str] = ("top_k:0", "top_k:1"), depth: int = 3,
                  device=None, use_graph: bool = True, precision: str = "bf16", calibration_images=None,
-                 distributed_weights: bool = False):
+                 distributed_weights: bool = False, lanes: int = 2):
         super().__init__(device)
+        self.lanes = max(1, int(lanes))  # concurrent plan instances on their own HIP streams
         self.distributed_weights = distributed_weights  # DP: broadcast rank 0's compiled weights at open
         self.precision = precision
         self.calibration_images = calibration_images  # uint8 [n, H, W, 3] for fp8 scales (synthetic if None)
@@ -61,25 +62,26 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
         super().open()
         dev = self._session.device
         if dev.type == "cuda":
-            from ...batching.engine import PipelinedGpuRunner
-
             from ...batching.arena import DeviceArena
+            from ...batching.engine import PipelinedGpuRunner
             from ...config import EngineConfig
 
             H, W = self.image_hw
-            # one arena per subtask: the bucket plans share its activation slab (largest
-            # compiled first) and its interned weights
-            self._arena = DeviceArena(dev, EngineConfig().arena_bytes(dev), name=type(self).__name__)
-            self._plans = {b: CompiledFunction(self._graph, {self.feed: ((b, H, W, 3), "UINT8")}, self.fetches, dev,
-                                               use_graph=self.use_graph, strict=True, precision=self.precision,
-                                               calibration=self._calibration(b), arena=self._arena)
-                           for b in sorted(self.buckets, reverse=True)}
+            # per compute lane one arena: its bucket plans share that arena's activation slab
+            # (largest compiled first) and interned weights; lanes replay concurrently
+            budget = EngineConfig().arena_bytes(dev) // self.lanes
+            self._arena = [DeviceArena(dev, budget, name=f"{type(self).__name__}/lane{i}") for i in range(self.lanes)]
+            lanes = [{b: CompiledFunction(self._graph, {self.feed: ((b, H, W, 3), "UINT8")}, self.fetches, dev,
+                                          use_graph=self.use_graph, strict=True, precision=self.precision,
+                                          calibration=self._calibration(b), arena=arena)
+                      for b in sorted(self.buckets, reverse=True)} for arena in self._arena]
+            self._plans = lanes[0]
             if self.distributed_weights:
                 from ...parallel import comm
 
                 # in place, so the captured hipGraphs keep reading the same buffers
-                comm.broadcast_tensors([t for p in self._plans.values() for t in p.params], src=0)
-            self._runner = PipelinedGpuRunner(self._plans, self.feed, lambda p: p.output_tensors(), (H, W, 3),
+                comm.broadcast_tensors([t for ln in lanes for p in ln.values() for t in p.params], src=0)
+            self._runner = PipelinedGpuRunner(lanes, self.feed, lambda p: p.output_tensors(), (H, W, 3),
                                               torch.uint8, depth=self.depth, device=dev)
 
     def _calibration(self, b: int):

@@ -30,7 +30,7 @@ import torch.nn.functional as F
 
 from ...io import bundle
 from ...ops.autograd import Linear
-from ...utils.tracing import graph_capture
+from ...utils.tracing import capture_lock, graph_capture
 from ...ops.embedding import SparseEmbedding
 from ...parallel import comm
 from ...runtime.model_functions import CheckpointedModel, model_state_dir
@@ -183,16 +183,17 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
             return
         dev = self._model.device
         self._static = tuple(t.to(dev).clone() for t in batch)
-        s = torch.cuda.Stream(dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s):
-            for _ in range(2):  # warm-up (real steps): allocator pools, optimizer state
-                self._step(self._static)
-        torch.cuda.current_stream(dev).wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with graph_capture(g):
-            self._static_loss = self._step(self._static)
-        self._graph = g
+        with capture_lock():
+            s = torch.cuda.Stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                for _ in range(2):  # warm-up (real steps): allocator pools, optimizer state
+                    self._step(self._static)
+            torch.cuda.current_stream(dev).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with graph_capture(g):
+                self._static_loss = self._step(self._static)
+            self._graph = g
 
     def _step(self, batch):
         m = self._model

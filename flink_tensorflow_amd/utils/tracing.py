@@ -64,6 +64,18 @@ def debug_poison() -> bool:
 _CAPTURE_LOCK = None
 
 
+def capture_lock():
+    """The process-wide capture lock: hold it around a capture's warm-up and device
+    synchronisation too (a device-wide synchronise while another thread captures is
+    rejected by the runtime)."""
+    import threading
+
+    global _CAPTURE_LOCK
+    if _CAPTURE_LOCK is None:
+        _CAPTURE_LOCK = threading.RLock()
+    return _CAPTURE_LOCK
+
+
 def graph_capture(graph, stream=None, pool=None):
     """``torch.cuda.graph`` (hipGraph stream capture) safe next to other operator threads
     of the same process: captures are serialised, and ``thread_local`` error mode keeps a
@@ -75,13 +87,11 @@ def graph_capture(graph, stream=None, pool=None):
 
     import torch
 
-    global _CAPTURE_LOCK
-    if _CAPTURE_LOCK is None:
-        _CAPTURE_LOCK = threading.RLock()
+    lock = capture_lock()
 
     @contextlib.contextmanager
     def _cm():
-        with _CAPTURE_LOCK:
+        with lock:
             with torch.cuda.graph(graph, pool=pool, stream=stream, capture_error_mode="thread_local"):
                 yield
 

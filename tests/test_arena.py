@@ -97,3 +97,36 @@ def test_arena_plans_gpu(small_graph):
     for _ in range(2):
         torch.testing.assert_close(p2({"images:0": imgs[:2].to(dev)})[0], ref2)
         torch.testing.assert_close(p4({"images:0": imgs.to(dev)})[0], ref4)
+
+
+@pytest.mark.gpu
+def test_two_compute_lanes_keep_order_gpu(small_graph):
+    """Two plan instances on two HIP streams (batches round-robin): results come back in
+    submission order and equal the single-lane results."""
+    import numpy as np
+
+    from flink_tensorflow_amd.batching.engine import PipelinedGpuRunner
+
+    dev = torch.device("cuda", 0)
+    feeds = {"images:0": ((4, 48, 48, 3), "UINT8")}
+
+    def lane():
+        return {4: CompiledFunction(small_graph, feeds, ["top_k:0", "top_k:1"], dev, strict=True,
+                                    arena=DeviceArena(dev, 4 << 30))}
+
+    rng = np.random.default_rng(0)
+    batches = [[rng.integers(0, 256, (48, 48, 3), dtype=np.uint8) for _ in range(4)] for _ in range(7)]
+
+    def run(lanes):
+        r = PipelinedGpuRunner(lanes, "images:0", lambda p: p.output_tensors(), (48, 48, 3), depth=3, device=dev)
+        out = []
+        for i, b in enumerate(batches):
+            out += r.submit(b, np.full(4, float(i)), [i] * 4)
+        out += r.drain()
+        return out
+
+    one, two = run(lane()), run([lane(), lane()])
+    assert [r.tags[0] for r in two] == list(range(7))
+    for a, b in zip(one, two):
+        torch.testing.assert_close(a.outputs[0], b.outputs[0])
+        assert torch.equal(a.outputs[1], b.outputs[1])
