@@ -28,6 +28,25 @@ class FailAfter(RichMapFunction):
         return value
 
 
+class KillProcessAfter(FailAfter):
+    """Like ``FailAfter`` but the subtask's PROCESS dies (``os._exit``, no Python unwinding,
+    no goodbye message) — a crashed worker of ``run_in_processes()``: the coordinator must
+    detect the dead process and restart the job from the last completed checkpoint."""
+
+    def __init__(self, n: int, attempts=(0,), subtask: int = 0, exit_code: int = 137):
+        super().__init__(n, attempts, subtask)
+        self.exit_code = exit_code
+
+    def map(self, value):
+        ctx = self.get_runtime_context()
+        self.seen += 1
+        if ctx.attempt in self.attempts and ctx.subtask_index == self.subtask and self.seen == self.n:
+            if getattr(ctx, "worker_pid", None) != os.getpid():
+                raise InjectedFault("KillProcessAfter must run in a worker process (run_in_processes)")
+            os._exit(self.exit_code)
+        return value
+
+
 class FaultInjector:
     """Hook object for ``env.fault_injector`` (armed at each job attempt)."""
 

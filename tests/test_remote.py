@@ -92,6 +92,27 @@ def test_remote_keyed_state_survives_failure_and_restart(tmp_path):
     assert final == {k: sum(v for v in range(1, 301) if v % 3 == k) for k in range(3)}
 
 
+def test_killed_worker_process_restarts_from_checkpoint(tmp_path):
+    """A worker process dies mid-stream (os._exit, no error message): the coordinator
+    notices the dead process, fails the attempt, and the restart resumes every keyed sum
+    consistently from the last completed checkpoint."""
+    from flink_tensorflow_amd.runtime.sources import CollectionSource
+    from flink_tensorflow_amd.utils.fault import KillProcessAfter
+
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    env.enable_checkpointing(0.05, str(tmp_path / "chk"))
+    env.set_restart_strategy(RestartStrategy.fixed_delay(2, 0.0))
+    src = env.add_source(CollectionSource(list(range(1, 301)), delay_s=0.002), "numbers")
+    sink = src.map(KillProcessAfter(80)).run_in_processes().key_by(lambda v: v % 3).process(_RunningSum()) \
+        .collect_into()
+    res = env.execute("worker-crash")
+    assert res.attempts == 1 and len(res.checkpoints) >= 1
+    final = {}
+    for k, t in sink.results():
+        final[k] = max(final.get(k, 0), t)
+    assert final == {k: sum(v for v in range(1, 301) if v % 3 == k) for k in range(3)}
+
+
 def _boom(v):
     if v == 7:
         raise ValueError("bad record 7")
