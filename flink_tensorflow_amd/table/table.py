@@ -365,6 +365,26 @@ class Table:
         f = ModelScalarFunction(model, lambda m, *vals: fn(m, Row.of(self.fields, vals)), name="map_with_model")
         return self.add_columns(f(*[col(c) for c in self.fields]).alias(out_field))
 
+    def map_with_model_batched(self, model, fn, out_field: str = "prediction", max_batch: int = 64,
+                               max_delay_ms: float = 5.0) -> "Table":
+        """Adds ``fn(model, rows) -> [value per row]`` as a column, evaluated on
+        micro-batches of up to ``max_batch`` rows (or whatever arrived within
+        ``max_delay_ms``) by the batched model operator — one GPU launch per batch instead
+        of one per row (e.g. ``fn = lambda m, rows: m.predict([r.text for r in rows])``)."""
+        if self.kind != "append":
+            raise TableError("map_with_model_batched needs an append-only table")
+        out = self.fields + (out_field,)
+
+        def batch(m, rows, fn=fn, out=out):
+            vals = list(fn(m, rows))
+            if len(vals) != len(rows):
+                raise TableError(f"model function returned {len(vals)} values for {len(rows)} rows")
+            return [Row.of(out, tuple(r) + (v,)) for r, v in zip(rows, vals)]
+
+        s = self.stream.map_with_model_batched(model, batch, max_batch=max_batch, max_delay_ms=max_delay_ms,
+                                               name="table-batched-model")
+        return self._derive(s, out, op=f"BatchedModelMap({out_field})")
+
     # ---- conversions
     def to_data_stream(self):
         return self.t_env.to_data_stream(self)

@@ -145,3 +145,19 @@ def test_model_function_in_sql(half_plus_two):
     t = t_env.from_elements([(float(v),) for v in range(2)], ["x"])
     out = t.map_with_model(HalfPlusTwo(half_plus_two), lambda m, row: regress(m, row.x), "y").execute().collect()
     assert sorted(out) == [(0.0, 2.0), (1.0, 2.5)]
+
+
+def test_batched_model_column(half_plus_two):
+    """Micro-batched model inference on a table: one SavedModel call per batch of rows."""
+    env, t_env = _env(1)
+    t = t_env.from_elements([(float(v), f"r{v}") for v in range(40)], ["x", "tag"])
+
+    def regress_batch(model, rows):
+        fn = model.function("regress_x_to_y", RegressionMethod())
+        ys = fn.apply([example(("x", feature(r.x))) for r in rows]).reshape(-1).tolist()
+        return ys
+
+    out = t.map_with_model_batched(HalfPlusTwo(half_plus_two), regress_batch, "y", max_batch=16).where(
+        col("y") > 20).execute().collect()
+    assert sorted((r.x, r.y) for r in out) == [(float(v), 0.5 * v + 2) for v in range(37, 40)]
+    assert all(r.tag == f"r{int(r.x)}" for r in out)
