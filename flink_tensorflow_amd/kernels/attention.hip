@@ -320,6 +320,59 @@ __global__ __launch_bounds__(1024) void pack_tokens_kernel(const int* __restrict
   }
 }
 
+// First-token ("CLS") attention of a packed batch: the final encoder layer of a sequence
+// classifier only needs each sequence's first row, so its attention is one query per
+// (sequence, head).  One wave per (b, h): lanes score keys (q . k_j, 64-d dot products from
+// 16-B loads), the softmax is a wave reduction, then lane d accumulates sum_j p_j v_j[d]
+// over coalesced 128-B V rows.  out [B, H*64] bf16.
+__global__ __launch_bounds__(256) void cls_attention_kernel(const bf16* __restrict__ qkv, const int* __restrict__ cu,
+                                                            bf16* __restrict__ out, int B, int H, float scale_log2e) {
+  __shared__ float probs[4][512];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int bh = blockIdx.x * 4 + wave;
+  if (bh >= B * H) return;  // wave-uniform; no block barrier below
+  const int b = bh / H, h = bh % H;
+  const int ld = 3 * H * D;
+  const int t0 = cu[b];
+  const int n = min(cu[b + 1] - t0, 512);
+  const bf16* qrow = qkv + (size_t)t0 * ld + h * D;
+  float q[D];
+#pragma unroll
+  for (int c = 0; c < D / 8; ++c) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + c * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q[c * 8 + e] = (float)v[e];
+  }
+  float mx = -INFINITY;
+  for (int j = lane; j < n; j += 64) {
+    const bf16* krow = qkv + (size_t)(t0 + j) * ld + H * D + h * D;
+    float sdot = 0.f;
+#pragma unroll
+    for (int c = 0; c < D / 8; ++c) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(krow + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sdot += q[c * 8 + e] * (float)v[e];
+    }
+    sdot *= scale_log2e;
+    probs[wave][j] = sdot;
+    mx = fmaxf(mx, sdot);
+  }
+  mx = wave_reduce_max(mx);
+  float sum = 0.f;
+  for (int j = lane; j < n; j += 64) {
+    const float p = exp2f(probs[wave][j] - mx);
+    probs[wave][j] = p;
+    sum += p;
+  }
+  sum = wave_reduce_sum(sum);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's probabilities are in LDS
+  float acc = 0.f;
+  const bf16* vcol = qkv + (size_t)t0 * ld + 2 * H * D + h * D + lane;
+  for (int j = 0; j < n; ++j) acc += probs[wave][j] * (float)vcol[(size_t)j * ld];
+  out[(size_t)b * H * D + h * D + lane] = f2bf(n > 0 ? acc / sum : 0.f);
+}
+
 }  // namespace
 
 void pack_tokens(uintptr_t ids, int B, int S, int pad_id, int T_cap, uintptr_t packed, uintptr_t pos, uintptr_t cu,
@@ -395,7 +448,20 @@ void probe_tr_read(uintptr_t out, int blk, uintptr_t stream) {
   FTM_CHECK_LAUNCH();
 }
 
+void cls_attention_bf16(uintptr_t qkv, uintptr_t cu, uintptr_t out, int B, int H, int Dh, float scale,
+                        uintptr_t stream) {
+  if (Dh != D) throw std::invalid_argument("cls_attention: head dim must be 64");
+  if (B <= 0 || H <= 0 || !cu) throw std::invalid_argument("cls_attention: empty problem / no cu_seqlens");
+  if (qkv % 16 || out % 2) throw std::invalid_argument("cls_attention: misaligned pointers");
+  const int waves = B * H;
+  hipLaunchKernelGGL(cls_attention_kernel, dim3((waves + 3) / 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const bf16*>(qkv), reinterpret_cast<const int*>(cu), reinterpret_cast<bf16*>(out),
+                     B, H, scale * 1.4426950408889634f);
+  FTM_CHECK_LAUNCH();
+}
+
 void register_attention(pybind11::module_& m) {
+  m.def("cls_attention_bf16", &cls_attention_bf16);
   m.def("probe_tr_read", &probe_tr_read);
   m.def("attention_fwd_bf16", &attention_fwd_bf16);
   m.def("embed_ln_bf16", &embed_ln_bf16);

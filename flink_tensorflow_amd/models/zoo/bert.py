@@ -228,6 +228,9 @@ class BertBuffers:
         self.ffn = torch.empty(tokens, cfg.intermediate, dtype=dtype, device=d)
         self.cls_in = torch.empty(batch, h, dtype=dtype, device=d)
         self.pooled = torch.empty(batch, h, dtype=dtype, device=d)
+        # final-layer first-token rows (packed classifier: only they feed the pooler)
+        self.c_ctx, self.c_y, self.c_x, self.c_x2 = (torch.empty(batch, h, dtype=dtype, device=d) for _ in range(4))
+        self.c_ffn = torch.empty(batch, cfg.intermediate, dtype=dtype, device=d)
         # one hipGraph memory pool for every plan on these buffers (graph temporaries such as
         # the GELU projection output are reused across capacities instead of duplicated)
         self.pool = torch.cuda.graph_pool_handle() if torch.device(d).type == "cuda" else None
@@ -274,6 +277,7 @@ class BertEncoderPlan:
         self.pids, self.ppos, self.cu, self.cls_idx = b.pids[:T], b.ppos[:T], b.cu, b.cls
         self.x, self.y, self.qkv, self.ctx, self.x2, self.ffn = (t[:T] for t in (b.x, b.y, b.qkv, b.ctx, b.x2, b.ffn))
         self.cls_in, self.pooled = b.cls_in, b.pooled
+        self.c_ctx, self.c_y, self.c_x, self.c_x2, self.c_ffn = b.c_ctx, b.c_y, b.c_x, b.c_x2, b.c_ffn
         if not hasattr(b, "logits"):
             b.logits = torch.empty(batch, w.cls_w.shape[0], dtype=dt, device=d)
         self.logits = b.logits
@@ -313,8 +317,10 @@ class BertEncoderPlan:
         if self.gemm_impl == "blas":
             return self._run_blas()
         cfg = w.cfg
-        for L in w.layers:
+        for li, L in enumerate(w.layers):
             K.gemm(self.x, L["qkv_w"], L["qkv_b"], out=self.qkv)
+            if self.packed and li == len(w.layers) - 1:
+                return self._last_layer_cls(L)
             self._attention()
             K.gemm(self.ctx, L["o_w"], L["o_b"], residual=self.x, out=self.y)
             K.layernorm(self.y, L["ln1_g"], L["ln1_b"], eps=cfg.eps, out=self.x)
@@ -325,8 +331,10 @@ class BertEncoderPlan:
 
     def _run_blas(self):
         w, cfg = self.w, self.w.cfg
-        for L in w.layers:
+        for li, L in enumerate(w.layers):
             torch.addmm(L["qkv_b16"], self.x, L["qkv_w"].t(), out=self.qkv)
+            if self.packed and li == len(w.layers) - 1:
+                return self._last_layer_cls(L)
             self._attention()
             torch.addmm(L["o_b16"], self.ctx, L["o_w"].t(), out=self.y)
             K.layernorm(self.y, L["ln1_g"], L["ln1_b"], residual=self.x, eps=cfg.eps, out=self.x2)
@@ -334,6 +342,28 @@ class BertEncoderPlan:
             torch.addmm(L["f_b16"], ffn, L["f_w"].t(), out=self.y)
             K.layernorm(self.y, L["ln2_g"], L["ln2_b"], residual=self.x2, eps=cfg.eps, out=self.x)
         self._pool()
+
+    def _last_layer_cls(self, L):
+        """Final layer of a packed classifier: only each sequence's first row reaches the
+        pooler, so after the (all-token) QKV projection everything runs on B rows —
+        first-token attention over the sequence's keys, then output projection, residual
+        LayerNorm, FFN and LayerNorm of those rows (the pooler input is unchanged)."""
+        w, cfg = self.w, self.w.cfg
+        K.cls_attention(self.qkv, self.cu, self.B, cfg.heads, out=self.c_ctx)
+        torch.index_select(self.x, 0, self.cls_idx, out=self.c_x)  # the layer input = residual
+        if self.gemm_impl == "blas":
+            torch.addmm(L["o_b16"], self.c_ctx, L["o_w"].t(), out=self.c_y)
+            K.layernorm(self.c_y, L["ln1_g"], L["ln1_b"], residual=self.c_x, eps=cfg.eps, out=self.c_x2)
+            ffn = torch._addmm_activation(L["i_b16"], self.c_x2, L["i_w"].t(), use_gelu=True)
+            torch.addmm(L["f_b16"], ffn, L["f_w"].t(), out=self.c_y)
+        else:
+            K.gemm(self.c_ctx, L["o_w"], L["o_b"], residual=self.c_x, out=self.c_y)
+            K.layernorm(self.c_y, L["ln1_g"], L["ln1_b"], eps=cfg.eps, out=self.c_x2)
+            K.gemm(self.c_x2, L["i_w"], L["i_b"], act="gelu", out=self.c_ffn)
+            K.gemm(self.c_ffn, L["f_w"], L["f_b"], out=self.c_y)
+        K.layernorm(self.c_y, L["ln2_g"], L["ln2_b"], residual=self.c_x2, eps=cfg.eps, out=self.cls_in)
+        K.gemm(self.cls_in, w.pool_w, w.pool_b, act="tanh", out=self.pooled)
+        K.gemm(self.pooled, w.cls_w, w.cls_b, out=self.logits)
 
     def _capture(self):
         with capture_lock():  # warm-up + device sync + capture: no sibling capture in between
@@ -375,7 +405,12 @@ class BertEncoderPlan:
         lens = np.full(self.B, self.S) if lengths is None else np.asarray(lengths)
         T = float(lens.sum())
         per_layer = 2 * T * (3 * h * h + h * h + 2 * h * i) + 4 * cfg.heads * float((lens ** 2).sum()) * (h // cfg.heads)
-        return cfg.layers * per_layer
+        if not self.packed:
+            return cfg.layers * per_layer
+        # packed classifier: the final layer computes QKV for every token but attention,
+        # projection and FFN only for each sequence's first token
+        last = 2 * T * 3 * h * h + 4 * cfg.heads * float(lens.sum()) * (h // cfg.heads) + 2 * len(lens) * (h * h + 2 * h * i)
+        return (cfg.layers - 1) * per_layer + last
 
 
 class PackedBertEncoder:

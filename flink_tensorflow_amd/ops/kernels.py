@@ -441,6 +441,35 @@ def attention(qkv: torch.Tensor, ids: torch.Tensor | None, batch: int, seq: int,
     return out
 
 
+def cls_attention(qkv: torch.Tensor, cu_seqlens: torch.Tensor, batch: int, heads: int, scale: float | None = None,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+    """Attention of each packed sequence's FIRST token only (the classifier's final layer):
+    ``qkv`` [T, 3*H*64] packed rows, ``cu_seqlens`` [B+1] → [B, H*64]."""
+    Dh = qkv.shape[1] // (3 * heads)
+    scale = (1.0 / Dh ** 0.5) if scale is None else scale
+    if out is None:
+        out = torch.empty((batch, heads * Dh), dtype=qkv.dtype, device=qkv.device)
+    if qkv.is_cuda:
+        _check(qkv, "qkv", device=qkv.device)
+        _check(out, "out", device=qkv.device)
+        _check(cu_seqlens, "cu_seqlens", torch.int32, qkv.device)
+        _hip().cls_attention_bf16(qkv.data_ptr(), cu_seqlens.data_ptr(), out.data_ptr(), batch, heads, Dh,
+                                  float(scale), _stream())
+        return out
+    cu = cu_seqlens.tolist()
+    for b in range(batch):
+        a, e = cu[b], cu[b + 1]
+        if e <= a:
+            out[b] = 0
+            continue
+        q = qkv[a, :heads * Dh].float().reshape(heads, 1, Dh)
+        k = qkv[a:e, heads * Dh:2 * heads * Dh].float().reshape(e - a, heads, Dh).transpose(0, 1)
+        v = qkv[a:e, 2 * heads * Dh:].float().reshape(e - a, heads, Dh).transpose(0, 1)
+        p = torch.softmax((q @ k.transpose(-1, -2)) * scale, -1)
+        out[b] = (p @ v).reshape(heads * Dh).to(out.dtype)
+    return out
+
+
 def pack_tokens(ids: torch.Tensor, pad_id: int, t_cap: int, packed: torch.Tensor, pos: torch.Tensor,
                 cu: torch.Tensor, cls: torch.Tensor) -> int | None:
     """Padding-free packing of ``ids`` [B, S]: the non-pad tokens in row order into
