@@ -245,6 +245,7 @@ def main():
             "plan": plan.summary() if hasattr(plan, "summary") else {"hip_graph": plan.graph is not None},
             "arena": arena.stats() if args.model != "bert" else None,
             "numa_binding_rank0": numa,
+            "host_ms_per_batch": {k: round(v * 1e3 / max(1, runner.batches), 3) for k, v in runner.host_s.items()},
         }
         print(json.dumps(out), flush=True)
     if comm.is_dist():

@@ -100,6 +100,10 @@ class PipelinedGpuRunner:
         self._next = {b: 0 for b in self.buckets}
         self._lane = 0
         self._inflight: list[_Slot] = []  # submission order
+        # host seconds per phase (gather / select / launch / wait): where the driving
+        # thread's time goes when the GPU is not saturated
+        self.host_s = {"gather": 0.0, "select": 0.0, "launch": 0.0, "wait": 0.0}
+        self.batches = 0
 
     def bucket_for(self, n: int) -> int:
         i = bisect.bisect_left(self.buckets, n)
@@ -116,7 +120,9 @@ class PipelinedGpuRunner:
         slots = self.slots[b]
         slot = slots[self._next[b]]
         self._next[b] = (self._next[b] + 1) % len(slots)
+        t0 = time.perf_counter()
         finished = self._harvest_through(slot) if slot.busy else []
+        t1 = time.perf_counter()
         # host gather into the pinned slot (zero padding rows only when needed)
         with trace_range(f"gather[{n}/{b}]"):
             self._native.gather_into(slot.pinned_in.data_ptr(),
@@ -124,12 +130,14 @@ class PipelinedGpuRunner:
                                      self.record_bytes, self.gather_threads)
             if n < b:
                 slot.pinned_in[n:].zero_()
+        t2 = time.perf_counter()
         lane = self._lane
         self._lane = (self._lane + 1) % len(self.lanes)
         plan = self.lanes[lane][b]
         select = getattr(plan, "select", None)
         if select is not None:  # e.g. the padding-free BERT encoder: pick a token-capacity plan
             plan = select(slot.pinned_in, n)
+        t3 = time.perf_counter()
         stream = self.compute_streams[lane]
         with trace_range("h2d"), torch.cuda.stream(self.copy_stream):
             slot.dev_in.copy_(slot.pinned_in, non_blocking=True)
@@ -148,6 +156,13 @@ class PipelinedGpuRunner:
         slot.ts = ingest_ts
         slot.tags = tags
         self._inflight.append(slot)
+        t4 = time.perf_counter()
+        hs = self.host_s
+        hs["wait"] += t1 - t0
+        hs["gather"] += t2 - t1
+        hs["select"] += t3 - t2
+        hs["launch"] += t4 - t3
+        self.batches += 1
         return finished
 
     def _harvest(self, slot: _Slot) -> BatchResult:
