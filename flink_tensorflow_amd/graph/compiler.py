@@ -641,6 +641,9 @@ class CompiledFunction:
         if res_val is not None and pointwise and xin_shape_override is None and out.qscale is None \
                 and self._fuse_shortcut(node, xin, out, w_ohwi, bias, res_val, residual[0], act, absorbed, last):
             return
+        if res_val is not None and pointwise and xin_shape_override is None \
+                and self._fuse_block_tail(xin, out, w_ohwi, w_dev, b_dev, res_val, act, absorbed, last, node.name):
+            return
 
         def run(xin=xin, out=out, res_val=res_val, w_dev=w_dev, b_dev=b_dev):
             K.conv2d_nhwc(xin.buf, w_dev, b_dev, res_val.buf if res_val is not None else None, (sh, sw),
@@ -697,6 +700,63 @@ class CompiledFunction:
         self.vals[(last.name, 0)] = out
         self._alias_fused_outputs(absorbed, out)
         self.fused_shortcuts = getattr(self, "fused_shortcuts", 0) + 1
+        return True
+
+    def _fuse_block_tail(self, xin, out, w_ohwi, w_dev, b_dev, res_val, act, absorbed, last, name) -> bool:
+        """ResNet stage-1 block boundary: this 1x1 64 -> 256 expand conv (+ residual, ReLU)
+        and the next block's 1x1 256 -> 64|128 reduce conv (+ ReLU) that reads its output
+        run as one persistent kernel (``bottleneck_tail``): the 256-channel output is still
+        stored (it is the next residual) but the reduce GEMM reads it from LDS instead of
+        HBM."""
+        if os.environ.get("FTM_TAIL_FUSE", "1") == "0" or self.precision == "fp8":
+            return False
+        if act != K.ACT_RELU or out.qscale is not None or tuple(w_ohwi.shape[:3]) != (256, 1, 1) \
+                or w_ohwi.shape[3] != 64 or (xin.phys_c or 64) != 64 or res_val.shape != out.shape \
+                or res_val.qscale is not None or res_val.concat_slot is not None or xin.concat_slot is not None:
+            return False
+        cand = [self.graph[c] for c in self.cons.get(last.name, []) if c not in self._fused]
+
+        def reduce_conv(c):  # 1x1 / s1 256 -> 64|128 reading this output (not the stage's projection)
+            if c.op != "Conv2D" or c.inputs[0] != (last.name, 0) or c.attr("data_format", "NHWC") != "NHWC" \
+                    or list(c.attr("strides")) != [1, 1, 1, 1] \
+                    or list(c.attr("dilations") or [1, 1, 1, 1]) != [1, 1, 1, 1]:
+                return None
+            wv = self._get(c.inputs[1])
+            if wv is None or not wv.is_const:
+                return None
+            w = wv.const.float()  # HWIO
+            return w if tuple(w.shape[:3]) == (1, 1, 256) and w.shape[3] in (64, 128) else None
+
+        cand = [(c, w) for c in cand for w in [reduce_conv(c)] if w is not None]
+        if len(cand) != 1:
+            return False
+        c, w2 = cand[0]
+        last2, scale2, bias2, residual2, act2, absorbed2 = self._conv_chain(c)
+        if residual2 is not None or act2 != K.ACT_RELU:
+            return False
+        cn = w2.shape[3]
+        if scale2 is not None:
+            w2 = w2 * scale2
+        w3_dev = w_dev  # 1x1 OHWI [256, 1, 1, 64] == row-major [256][64]
+        b3_dev = b_dev if b_dev is not None else self._dev(torch.zeros(256), torch.float32)
+        w1_dev = self._dev(w2.reshape(256, cn).t().contiguous(), torch.bfloat16)
+        b1_dev = self._dev(bias2 if bias2 is not None else torch.zeros(cn), torch.float32)
+        self.params += [b3_dev, w1_dev, b1_dev]
+        N, H, W, _ = out.shape
+        out2 = self._new((N, H, W, cn))
+        for a in absorbed + absorbed2:
+            self._fused.add(a.name)
+        self._fused.add(c.name)
+
+        def run(xin=xin, res_val=res_val, out=out, out2=out2):
+            K.bottleneck_tail(xin.buf, res_val.buf, w3_dev, b3_dev, w1_dev, b1_dev, y3=out.buf, y1=out2.buf)
+
+        self._emit(name, "conv", run, [xin, res_val], [out, out2], {"impl": "bottleneck_tail"})
+        self.vals[(last.name, 0)] = out
+        self._alias_fused_outputs(absorbed, out)
+        self.vals[(last2.name, 0)] = out2
+        self._alias_fused_outputs(absorbed2, out2)
+        self.fused_tails = getattr(self, "fused_tails", 0) + 1
         return True
 
     def _fusable_maxpool(self, last: Node, act, out: Val):
@@ -1083,7 +1143,8 @@ class CompiledFunction:
         # produced by exactly one conv/pool step (which can write at a channel offset),
         # consumed by nothing but this concat, and not fetched
         prods = [s for s in self.steps if any(o is v for o in s.outputs)]
-        if len(prods) != 1 or prods[0].kind not in ("conv", "pool", "conv_fp8", "pool_fp8") or v.concat_slot is not None:
+        if len(prods) != 1 or prods[0].kind not in ("conv", "pool", "conv_fp8", "pool_fp8") or v.concat_slot is not None \
+                or len(prods[0].outputs) != 1:
             return False
         if v.alias_of is not None or v.phys_c:
             return False
@@ -1317,6 +1378,7 @@ class CompiledFunction:
         return {"steps": len(self.steps), "kinds": kinds, "glue_ops": sorted(set(self.glue_ops)),
                 "hip_graph": self._graph_obj is not None, "precision": self.precision,
                 "fp8_layers": self.fp8_layers, "fused_shortcuts": getattr(self, "fused_shortcuts", 0),
+                "fused_tails": getattr(self, "fused_tails", 0),
                 "fused_pools": getattr(self, "fused_pools", 0), "conv3x3c64": getattr(self, "conv3x3c64", 0),
                 "activation_bytes": self.activation_bytes,
                 "param_bytes": self.param_bytes()}

@@ -14,6 +14,7 @@ void register_igemm_v2(pybind11::module_& m);
 void register_dconv(pybind11::module_& m);
 void register_elementwise(pybind11::module_& m);
 void register_conv3x3c64(pybind11::module_& m);
+void register_bottleneck(pybind11::module_& m);
 
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "flink_tensorflow_amd CDNA4 (gfx950) kernels";
@@ -28,4 +29,5 @@ PYBIND11_MODULE(_hip, m) {
   register_dconv(m);
   register_elementwise(m);
   register_conv3x3c64(m);
+  register_bottleneck(m);
 }

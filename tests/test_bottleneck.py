@@ -1,0 +1,62 @@
+"""Fused ResNet stage-1 block boundary (``ops.kernels.bottleneck_tail``): the host
+reference, and the compiler's fusion of a 1x1 expand conv with the next block's 1x1
+reduce conv (two boundaries in ResNet-50: inside stage 1 and stage 1 -> stage 2)."""
+import os
+
+import pytest
+import torch
+
+from flink_tensorflow_amd.graph.compiler import CompiledFunction
+from flink_tensorflow_amd.graph.graph import Graph
+from flink_tensorflow_amd.models.zoo.resnet import resnet50_graph_def
+from flink_tensorflow_amd.ops import kernels as K
+
+
+def test_host_reference_matches_two_convs():
+    g = torch.Generator().manual_seed(0)
+    x2, res = torch.randn(2, 5, 7, 64, generator=g), torch.randn(2, 5, 7, 256, generator=g)
+    w3, w1 = torch.randn(256, 64, generator=g), torch.randn(128, 256, generator=g)
+    b3, b1 = torch.randn(256, generator=g), torch.randn(128, generator=g)
+    y3, y1 = K.bottleneck_tail(x2, res, w3, b3, w1, b1)
+    e3 = K.conv2d_nhwc(x2, w3.reshape(256, 1, 1, 64), b3, res, act="relu")
+    e1 = K.conv2d_nhwc(e3, w1.reshape(128, 1, 1, 256), b1, act="relu")
+    torch.testing.assert_close(y3, e3)
+    torch.testing.assert_close(y1, e1, rtol=1e-4, atol=1e-3)
+    with pytest.raises(ValueError):
+        K.bottleneck_tail(x2, res, w3, b3, w1[:96], b1[:96])
+
+
+def _compile(g, dev, fuse):
+    old = os.environ.get("FTM_TAIL_FUSE")
+    os.environ["FTM_TAIL_FUSE"] = "1" if fuse else "0"
+    try:
+        return CompiledFunction(g, {"images:0": ((2, 64, 64, 3), "UINT8")}, ["logits:0"], dev, strict=True)
+    finally:
+        if old is None:
+            os.environ.pop("FTM_TAIL_FUSE")
+        else:
+            os.environ["FTM_TAIL_FUSE"] = old
+
+
+@pytest.fixture(scope="module")
+def r50():
+    return Graph.from_graph_def(resnet50_graph_def(depth=50, image_hw=(64, 64), num_classes=16))
+
+
+def _check(r50, dev):
+    fused, plain = _compile(r50, dev, True), _compile(r50, dev, False)
+    assert fused.summary()["fused_tails"] == 2 and plain.summary()["fused_tails"] == 0
+    assert len(fused.steps) == len(plain.steps) - 2
+    imgs = torch.randint(0, 256, (2, 64, 64, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(1))
+    a = fused({"images:0": imgs.to(dev)})[0].float().cpu()
+    b = plain({"images:0": imgs.to(dev)})[0].float().cpu()
+    torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2 * b.abs().max().item())
+
+
+def test_compiled_resnet50_fuses_block_boundaries_cpu(r50):
+    _check(r50, torch.device("cpu"))
+
+
+@pytest.mark.gpu
+def test_compiled_resnet50_fuses_block_boundaries_gpu(r50):
+    _check(r50, torch.device("cuda", 0))

@@ -240,3 +240,24 @@ def test_conv3x3_c64_kernel(shape, act):
     got = out[..., 16:80].float().cpu()
     torch.testing.assert_close(got, ref, rtol=2e-2, atol=3e-2)
     assert (out[..., :16] == 7).all() and (out[..., 80:] == 7).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cn", [64, 128])
+@pytest.mark.parametrize("M", [2 * 56 * 56, 1000 + 37, 50])
+def test_bottleneck_tail_kernel(cn, M):
+    """Fused 1x1 expand (+residual, ReLU) -> 1x1 reduce (+ReLU) vs the two fp32 reference
+    convs; M not a multiple of the pixel tile exercises the tail tile, M < tile a single
+    partial tile."""
+    g = torch.Generator().manual_seed(M + cn)
+    x2 = torch.randn(M, 64, generator=g).to(torch.bfloat16)
+    res = torch.randn(M, 256, generator=g).to(torch.bfloat16)
+    w3 = (torch.randn(256, 64, generator=g) * 0.1).to(torch.bfloat16)
+    w1 = (torch.randn(cn, 256, generator=g) * 0.05).to(torch.bfloat16)
+    b3, b1 = torch.randn(256, generator=g), torch.randn(cn, generator=g)
+    y3_ref = torch.relu(x2.float() @ w3.float().t() + b3 + res.float())
+    y1_ref = torch.relu(y3_ref.to(torch.bfloat16).float() @ w1.float().t() + b1)
+    y3, y1 = K.bottleneck_tail(x2.to(DEV), res.to(DEV), w3.to(DEV), b3.to(DEV), w1.to(DEV), b1.to(DEV))
+    torch.cuda.synchronize()
+    _close(y3, y3_ref)
+    _close(y1, y1_ref)
