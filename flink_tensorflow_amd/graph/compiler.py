@@ -638,6 +638,28 @@ class CompiledFunction:
             return
 
         pointwise = (KHe, KWe, sh, sw, pt, pb, pl, pr, dh, dw) == (1, 1, 1, 1, 0, 0, 0, 0, 1, 1)
+        if (self.device.type == "cuda" and pointwise and res_val is None and act in (K.ACT_NONE, K.ACT_RELU)
+                and out.qscale is None and xin_shape_override is None and (xin.phys_c or Cin) == Cin
+                and Cin >= 1024 and os.environ.get("FTM_CONV_LIB", "1") != "0"):
+            # deep-K 1x1 reduce convs (ResNet stages 3/4: K = 1024 / 2048): a plain GEMM with
+            # a bias+ReLU epilogue, where the library kernel measured 1.5x the implicit GEMM
+            # (bench/probe_lib_convs.py, profiles/r01_lib)
+            b16 = self._dev(bias if bias is not None else torch.zeros(Cout), torch.bfloat16)
+            w_kn = w_dev.reshape(Cout, Cin).t()
+            self.params.append(b16)
+            relu = act == K.ACT_RELU
+
+            def run_lib(xin=xin, out=out, w_kn=w_kn, b16=b16, relu=relu):
+                x2, y2 = xin.buf.view(-1, Cin), out.buf.view(-1, Cout)
+                if relu:
+                    torch._addmm_activation(b16, x2, w_kn, out=y2)
+                else:
+                    torch.addmm(b16, x2, w_kn, out=y2)
+
+            self._emit(node.name, "gemm_lib", run_lib, [xin], [out])
+            self.vals[(last.name, 0)] = out
+            self._alias_fused_outputs(absorbed, out)
+            return
         if res_val is not None and pointwise and xin_shape_override is None and out.qscale is None \
                 and self._fuse_shortcut(node, xin, out, w_ohwi, bias, res_val, residual[0], act, absorbed, last):
             return

@@ -1,6 +1,7 @@
 """Fused ResNet stage-1 block boundary (``ops.kernels.bottleneck_tail``): the host
 reference, and the compiler's fusion of a 1x1 expand conv with the next block's 1x1
-reduce conv (two boundaries in ResNet-50: inside stage 1 and stage 1 -> stage 2)."""
+reduce conv (two boundaries in ResNet-50: inside stage 1 and stage 1 -> stage 2), and
+the library-GEMM lowering of the deep-K 1x1 convs (GPU)."""
 import os
 
 import pytest
@@ -26,16 +27,18 @@ def test_host_reference_matches_two_convs():
         K.bottleneck_tail(x2, res, w3, b3, w1[:96], b1[:96])
 
 
-def _compile(g, dev, fuse):
-    old = os.environ.get("FTM_TAIL_FUSE")
-    os.environ["FTM_TAIL_FUSE"] = "1" if fuse else "0"
+def _compile(g, dev, fuse, lib="1"):
+    env = {"FTM_TAIL_FUSE": "1" if fuse else "0", "FTM_CONV_LIB": lib}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         return CompiledFunction(g, {"images:0": ((2, 64, 64, 3), "UINT8")}, ["logits:0"], dev, strict=True)
     finally:
-        if old is None:
-            os.environ.pop("FTM_TAIL_FUSE")
-        else:
-            os.environ["FTM_TAIL_FUSE"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
 
 
 @pytest.fixture(scope="module")
@@ -44,9 +47,12 @@ def r50():
 
 
 def _check(r50, dev):
-    fused, plain = _compile(r50, dev, True), _compile(r50, dev, False)
+    fused, plain = _compile(r50, dev, True), _compile(r50, dev, False, lib="0")
     assert fused.summary()["fused_tails"] == 2 and plain.summary()["fused_tails"] == 0
     assert len(fused.steps) == len(plain.steps) - 2
+    # deep-K 1x1 reduce convs (stages 3/4) go to the library GEMM on the GPU only
+    n_lib = fused.summary()["kinds"].get("gemm_lib", 0) - plain.summary()["kinds"].get("gemm_lib", 0)
+    assert n_lib == (8 if dev.type == "cuda" else 0)
     imgs = torch.randint(0, 256, (2, 64, 64, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(1))
     a = fused({"images:0": imgs.to(dev)})[0].float().cpu()
     b = plain({"images:0": imgs.to(dev)})[0].float().cpu()
