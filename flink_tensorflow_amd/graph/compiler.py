@@ -561,9 +561,9 @@ class CompiledFunction:
             # stride-2 RGB stem over the space-to-depth preprocess output (K 392 -> 256)
             w_ohwi, (pt, pb, pl, pr) = K.s2d_stem_weights(w, H, W, (pt, pb, pl, pr))
             x.pre_cfg["s2d"] = True
-            x.buf_shape = (N, H // 2, W // 2, 16)
+            x.buf_shape = (N, (H + 1) // 2, (W + 1) // 2, 16)
             x.phys_c = 16
-            xin_shape_override = (N, H // 2, W // 2, 16)
+            xin_shape_override = x.buf_shape
             KH, KW = w_ohwi.shape[1], w_ohwi.shape[2]
             sh = sw = 1
             cin_pad = 16
@@ -862,7 +862,7 @@ class CompiledFunction:
 
     def _s2d_ok(self, x: Val, node: Node, C, sh, sw, dh, dw, pt, pl, H, W) -> bool:
         cfg = getattr(x, "pre_cfg", None)
-        if cfg is None or C != 3 or (sh, sw) != (2, 2) or (dh, dw) != (1, 1) or pt % 2 or pl % 2 or H % 2 or W % 2:
+        if cfg is None or C != 3 or (sh, sw) != (2, 2) or (dh, dw) != (1, 1) or pt % 2 or pl % 2:
             return False
         chain = x.pre_chain
         users = set()

@@ -47,12 +47,14 @@ FTM_DEVICE void resize_pixel(const uint8_t* img, const PreParams& q, int oy, int
 }
 
 // Layout 0: [B, Ho, Wo, 8] (RGB + 5 zero channels).
-// Layout 1 (space-to-depth 2x2, for the stride-2 stem conv): [B, Ho/2, Wo/2, 16] with
-// channel (dy*2+dx)*3 + c = pixel (2*oy2+dy, 2*ox2+dx) channel c, channels 12..15 zero.
+// Layout 1 (space-to-depth 2x2, for the stride-2 stem conv): [B, ceil(Ho/2), ceil(Wo/2), 16]
+// with channel (dy*2+dx)*3 + c = pixel (2*oy2+dy, 2*ox2+dx) channel c, channels 12..15 zero;
+// an odd size's last row / column block holds zeros for the pixels past the image (the
+// stem weights of those taps are zero, e.g. Inception's 3x3 / s2 VALID stem on 299 x 299).
 template <int S2D>
 __global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restrict__ src, bf16* __restrict__ dst,
                                                          int B, PreParams q) {
-  const int Wo = S2D ? q.Wo / 2 : q.Wo, Ho = S2D ? q.Ho / 2 : q.Ho;
+  const int Wo = S2D ? (q.Wo + 1) / 2 : q.Wo, Ho = S2D ? (q.Ho + 1) / 2 : q.Ho;
   const int total = B * Ho * Wo;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
     const int ox = idx % Wo;
@@ -65,7 +67,11 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restri
       bf16x8 o0, o1;
       float pix[4][3];
 #pragma unroll
-      for (int d = 0; d < 4; ++d) resize_pixel(img, q, 2 * oy + (d >> 1), 2 * ox + (d & 1), pix[d]);
+      for (int d = 0; d < 4; ++d) {
+        const int py = 2 * oy + (d >> 1), px = 2 * ox + (d & 1);
+        if (py < q.Ho && px < q.Wo) resize_pixel(img, q, py, px, pix[d]);
+        else pix[d][0] = pix[d][1] = pix[d][2] = 0.f;
+      }
       o0[0] = f2bf(pix[0][0]); o0[1] = f2bf(pix[0][1]); o0[2] = f2bf(pix[0][2]);
       o0[3] = f2bf(pix[1][0]); o0[4] = f2bf(pix[1][1]); o0[5] = f2bf(pix[1][2]);
       o0[6] = f2bf(pix[2][0]); o0[7] = f2bf(pix[2][1]);
@@ -237,7 +243,6 @@ void preprocess_u8_to_bf16(uintptr_t src, uintptr_t dst, int B, int Hi, int Wi, 
   if (B <= 0 || Hi <= 0 || Wi <= 0 || Ho <= 0 || Wo <= 0) throw std::invalid_argument("preprocess: bad shape");
   if (src_stride < Hi * Wi * 3) throw std::invalid_argument("preprocess: src_stride smaller than one image");
   if (dst % 16) throw std::invalid_argument("preprocess: dst not 16-byte aligned");
-  if (s2d && (Ho % 2 || Wo % 2)) throw std::invalid_argument("preprocess: space-to-depth needs even output size");
   PreParams q;
   q.Hi = Hi; q.Wi = Wi; q.Ho = Ho; q.Wo = Wo;
   q.sy = (align_corners && Ho > 1) ? (float)(Hi - 1) / (Ho - 1) : (float)Hi / Ho;
@@ -246,7 +251,7 @@ void preprocess_u8_to_bf16(uintptr_t src, uintptr_t dst, int B, int Hi, int Wi, 
   q.m[0] = m0; q.m[1] = m1; q.m[2] = m2;
   q.s[0] = s0; q.s[1] = s1; q.s[2] = s2;
   q.src_stride = src_stride;
-  long work = s2d ? (long)B * (Ho / 2) * (Wo / 2) : (long)B * Ho * Wo;
+  long work = s2d ? (long)B * ((Ho + 1) / 2) * ((Wo + 1) / 2) : (long)B * Ho * Wo;
   auto s = reinterpret_cast<hipStream_t>(stream);
   auto S = reinterpret_cast<const uint8_t*>(src);
   auto D = reinterpret_cast<bf16*>(dst);

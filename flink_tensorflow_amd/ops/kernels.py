@@ -300,14 +300,13 @@ def preprocess_images(images_u8: torch.Tensor, out_hw=(224, 224), mean=(117.0, 1
     """uint8 [B,H,W,3] → resize (TF ResizeBilinear) → (v-mean)/std → bf16.
 
     Layout ``[B,Ho,Wo,8]`` (channels 3..7 zero), or with ``s2d`` the 2x2 space-to-depth
-    layout ``[B,Ho/2,Wo/2,16]`` consumed by the stride-2 stem conv (``s2d_stem_weights``)."""
+    layout ``[B,ceil(Ho/2),ceil(Wo/2),16]`` consumed by the stride-2 stem conv
+    (``s2d_stem_weights``); an odd size zero-fills the pixels past the image."""
     if images_u8.dtype != torch.uint8 or images_u8.dim() != 4 or images_u8.shape[3] != 3:
         raise ValueError("preprocess_images expects uint8 [B,H,W,3]")
     B, Hi, Wi, _ = images_u8.shape
     Ho, Wo = out_hw
-    oshape = (B, Ho // 2, Wo // 2, 16) if s2d else (B, Ho, Wo, 8)
-    if s2d and (Ho % 2 or Wo % 2):
-        raise ValueError("space-to-depth preprocess needs an even output size")
+    oshape = (B, (Ho + 1) // 2, (Wo + 1) // 2, 16) if s2d else (B, Ho, Wo, 8)
     if out is None:
         out = torch.empty(oshape, dtype=torch.bfloat16 if images_u8.is_cuda else torch.float32,
                           device=images_u8.device)
@@ -327,7 +326,9 @@ def preprocess_images(images_u8: torch.Tensor, out_hw=(224, 224), mean=(117.0, 1
     y = (y - torch.tensor(mean)) / torch.tensor(std)
     out.zero_()
     if s2d:
-        blk = y.reshape(B, Ho // 2, 2, Wo // 2, 2, 3).permute(0, 1, 3, 2, 4, 5).reshape(B, Ho // 2, Wo // 2, 12)
+        Hb, Wb = (Ho + 1) // 2, (Wo + 1) // 2
+        y = F.pad(y, (0, 0, 0, 2 * Wb - Wo, 0, 2 * Hb - Ho))
+        blk = y.reshape(B, Hb, 2, Wb, 2, 3).permute(0, 1, 3, 2, 4, 5).reshape(B, Hb, Wb, 12)
         out[..., :12] = blk.to(out.dtype)
     else:
         out[..., :3] = y.to(out.dtype)
@@ -343,8 +344,8 @@ def s2d_stem_weights(w_hwio: torch.Tensor, H: int, W: int, pads):
     """
     KH, KW, C, Cout = w_hwio.shape
     pt, pb, pl, pr = pads
-    if C != 3 or pt % 2 or pl % 2 or H % 2 or W % 2:
-        raise ValueError("s2d stem needs RGB input, even top/left padding and even H/W")
+    if C != 3 or pt % 2 or pl % 2:
+        raise ValueError("s2d stem needs RGB input and even top/left padding")
     KBH, KBW = (KH + 1) // 2, (KW + 1) // 2
     w2 = torch.zeros(Cout, KBH, KBW, 16, dtype=torch.float32)
     wf = w_hwio.float()
@@ -354,7 +355,7 @@ def s2d_stem_weights(w_hwio: torch.Tensor, H: int, W: int, pads):
             w2[:, kh // 2, kw // 2, ch:ch + 3] = wf[kh, kw].t()
     Ho = (H + pt + pb - KH) // 2 + 1
     Wo = (W + pl + pr - KW) // 2 + 1
-    Hb, Wb = H // 2, W // 2
+    Hb, Wb = (H + 1) // 2, (W + 1) // 2  # an odd size's last block is zero-filled past the image
     pt_b, pl_b = pt // 2, pl // 2
     pb_b = Ho - 1 + KBH - Hb - pt_b
     pr_b = Wo - 1 + KBW - Wb - pl_b

@@ -75,6 +75,17 @@ def test_s2d_stem_equivalence():
     got = K.conv2d_nhwc(b, w2, pad=pads)
     assert pads == (1, 2, 1, 2)
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-2)
+    # odd size (Inception's 3x3 / s2 VALID stem on 299 x 299): the last block row / column
+    # is zero-filled past the image and meets only zero weights
+    w3 = torch.randn(3, 3, 3, 32)
+    a = K.preprocess_images(img, (75, 75))
+    ref = conv2d_tf(a[..., :3].float(), w3, (2, 2), "VALID")
+    w2, pads = K.s2d_stem_weights(w3, 75, 75, (0, 0, 0, 0))
+    b = K.preprocess_images(img, (75, 75), s2d=True)
+    assert b.shape == (2, 38, 38, 16) and (b[:, -1, :, 6:12] == 0).all() and (b[:, :, -1, 3:6] == 0).all()
+    got = K.conv2d_nhwc(b, w2, pad=pads)
+    assert pads == (0, 0, 0, 0) and got.shape == ref.shape == (2, 37, 37, 32)
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-2)
 
 
 def test_plan_profile_and_debug_modes(monkeypatch):

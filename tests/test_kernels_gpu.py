@@ -161,10 +161,11 @@ def test_linear_autograd():
     _close(bs[1].grad, bs[0].grad)
 
 
-def test_preprocess_s2d():
+@pytest.mark.parametrize("hw", [224, 299, 100])
+def test_preprocess_s2d(hw):
     img = torch.randint(0, 256, (3, 256, 256, 3), dtype=torch.uint8)
-    ref = K.preprocess_images(img, (224, 224), s2d=True)
-    got = K.preprocess_images(img.to(DEV), (224, 224), s2d=True)
+    ref = K.preprocess_images(img, (hw, hw), s2d=True)
+    got = K.preprocess_images(img.to(DEV), (hw, hw), s2d=True)
     _close(got, ref, rtol=1e-2, atol_scale=1e-2)
 
 
