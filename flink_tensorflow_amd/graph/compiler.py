@@ -664,7 +664,8 @@ class CompiledFunction:
                 and self._fuse_shortcut(node, xin, out, w_ohwi, bias, res_val, residual[0], act, absorbed, last):
             return
         if res_val is not None and pointwise and xin_shape_override is None \
-                and self._fuse_block_tail(xin, out, w_ohwi, w_dev, b_dev, res_val, act, absorbed, last, node.name):
+                and self._fuse_block_tail(xin, out, w_ohwi.reshape(w_ohwi.shape[0], -1), w_dev, b_dev, res_val, None, act,
+                                      absorbed, last, node.name):
             return
 
         def run(xin=xin, out=out, res_val=res_val, w_dev=w_dev, b_dev=b_dev):
@@ -714,6 +715,9 @@ class CompiledFunction:
         self.params += [w_dev, b_dev]
         for a in absorbed:
             self._fused.add(a.name)
+        if s2 == 1 and self._fuse_block_tail(xin, out, w_cat, w_dev, b_dev, None, x2, act, absorbed, last, node.name):
+            self.fused_shortcuts = getattr(self, "fused_shortcuts", 0) + 1
+            return True
 
         def run(xin=xin, x2=x2, out=out, w_dev=w_dev, b_dev=b_dev):
             K.conv1x1_dual(xin.buf, x2.buf, w_dev, b_dev, s2, act, out=_target(out), out_channel_offset=_coff(out))
@@ -724,17 +728,27 @@ class CompiledFunction:
         self.fused_shortcuts = getattr(self, "fused_shortcuts", 0) + 1
         return True
 
-    def _fuse_block_tail(self, xin, out, w_ohwi, w_dev, b_dev, res_val, act, absorbed, last, name) -> bool:
+    def _fuse_block_tail(self, xin, out, w3, w_dev, b_dev, res_val, xs_val, act, absorbed, last, name) -> bool:
         """ResNet stage-1 block boundary: this 1x1 64 -> 256 expand conv (+ residual, ReLU)
         and the next block's 1x1 256 -> 64|128 reduce conv (+ ReLU) that reads its output
         run as one persistent kernel (``bottleneck_tail``): the 256-channel output is still
         stored (it is the next residual) but the reduce GEMM reads it from LDS instead of
-        HBM."""
+        HBM.  ``w3`` is the host [256, K] expand weight; with ``xs_val`` (a stage's first
+        block) K = 64 + 64 covers the stride-1 projection shortcut of ``xs_val`` too."""
         if os.environ.get("FTM_TAIL_FUSE", "1") == "0" or self.precision == "fp8":
             return False
-        if act != K.ACT_RELU or out.qscale is not None or tuple(w_ohwi.shape[:3]) != (256, 1, 1) \
-                or w_ohwi.shape[3] != 64 or (xin.phys_c or 64) != 64 or res_val.shape != out.shape \
-                or res_val.qscale is not None or res_val.concat_slot is not None or xin.concat_slot is not None:
+
+        def plain(v):
+            return v.shape[-1] == 64 and (v.phys_c or 64) == 64 and v.concat_slot is None and v.qscale is None \
+                and v.dtype == torch.bfloat16 and tuple(v.shape[:-1]) == tuple(out.shape[:-1])
+
+        if act != K.ACT_RELU or out.qscale is not None or tuple(w3.shape) != (256, 64 if xs_val is None else 128) \
+                or not plain(xin):
+            return False
+        if res_val is not None and (res_val.shape != out.shape or res_val.qscale is not None
+                                    or res_val.concat_slot is not None):
+            return False
+        if xs_val is not None and not plain(xs_val):
             return False
         cand = [self.graph[c] for c in self.cons.get(last.name, []) if c not in self._fused]
 
@@ -750,7 +764,7 @@ class CompiledFunction:
             return w if tuple(w.shape[:3]) == (1, 1, 256) and w.shape[3] in (64, 128) else None
 
         cand = [(c, w) for c in cand for w in [reduce_conv(c)] if w is not None]
-        if len(cand) != 1:
+        if len(cand) != 1 or (xs_val is not None and cand[0][1].shape[3] != 64):
             return False
         c, w2 = cand[0]
         last2, scale2, bias2, residual2, act2, absorbed2 = self._conv_chain(c)
@@ -759,7 +773,7 @@ class CompiledFunction:
         cn = w2.shape[3]
         if scale2 is not None:
             w2 = w2 * scale2
-        w3_dev = w_dev  # 1x1 OHWI [256, 1, 1, 64] == row-major [256][64]
+        w3_dev = w_dev  # row-major [256][K] (1x1 OHWI [256, 1, 1, 64], or the dual [W3 | Wsc])
         b3_dev = b_dev if b_dev is not None else self._dev(torch.zeros(256), torch.float32)
         w1_dev = self._dev(w2.reshape(256, cn).t().contiguous(), torch.bfloat16)
         b1_dev = self._dev(bias2 if bias2 is not None else torch.zeros(cn), torch.float32)
@@ -770,10 +784,13 @@ class CompiledFunction:
             self._fused.add(a.name)
         self._fused.add(c.name)
 
-        def run(xin=xin, res_val=res_val, out=out, out2=out2):
-            K.bottleneck_tail(xin.buf, res_val.buf, w3_dev, b3_dev, w1_dev, b1_dev, y3=out.buf, y1=out2.buf)
+        second = res_val if xs_val is None else xs_val
 
-        self._emit(name, "conv", run, [xin, res_val], [out, out2], {"impl": "bottleneck_tail"})
+        def run(xin=xin, second=second, out=out, out2=out2, dual=xs_val is not None):
+            K.bottleneck_tail(xin.buf, None if dual else second.buf, w3_dev, b3_dev, w1_dev, b1_dev, y3=out.buf,
+                              y1=out2.buf, xs=second.buf if dual else None)
+
+        self._emit(name, "conv", run, [xin, second], [out, out2], {"impl": "bottleneck_tail"})
         self.vals[(last.name, 0)] = out
         self._alias_fused_outputs(absorbed, out)
         self.vals[(last2.name, 0)] = out2

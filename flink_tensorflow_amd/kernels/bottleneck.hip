@@ -4,7 +4,9 @@
 //   y1  = relu(y3 . W1^T + b1)            1x1 reduce 256 -> CN              (block k + 1)
 //
 // CN = 64 inside stage 1, CN = 128 where stage 1 hands over to stage 2 (ResNet v1.5 keeps
-// stage 2's first 1x1 at stride 1).  Unfused, the 256-channel y3 (411 MB at micro-batch
+// stage 2's first 1x1 at stride 1).  The first block's expand conv, whose shortcut is a
+// stride-1 projection of the block input, runs as the dual variant: K = 64 + 64 over
+// [x2 | x] (the projection never reaches HBM) and no residual read.  Unfused, the 256-channel y3 (411 MB at micro-batch
 // 256 x 56 x 56) is written by one kernel and read back whole by the next; here each tile
 // of y3 is produced into LDS, stored once (it is still the next block's residual) and
 // consumed from LDS by the reduce GEMM.  Persistent: one workgroup per CU keeps BOTH
@@ -29,7 +31,7 @@
 
 namespace {
 
-constexpr int CM = 64;    // x2 channels
+constexpr int CX = 64;    // channels of each GEMM-1 source (x2, and the shortcut input xs)
 constexpr int CO = 256;   // y3 channels
 constexpr int NT = 512;   // threads (8 waves)
 
@@ -42,12 +44,16 @@ FTM_DEVICE int swz(int row, int c) {
 }
 
 // TP pixels per tile, CN channels of the reduce output y1 (64 within stage 1, 128 for the
-// stage-2 entry block)
-template <int TP, int CN>
-__global__ __launch_bounds__(NT, 1) void bottleneck_tail_kernel(const bf16* __restrict__ x2, const bf16* __restrict__ res,
+// stage-2 entry block).  DUAL: stage 1's first block, whose shortcut is a stride-1 1x1
+// projection of the block input xs instead of an identity residual — GEMM 1 runs over
+// K = 64 + 64 ([x2 | xs] . [W3 | Wsc]^T, bias summed) and there is no residual read.
+template <int TP, int CN, bool DUAL>
+__global__ __launch_bounds__(NT, 1) void bottleneck_tail_kernel(const bf16* __restrict__ x2, const bf16* __restrict__ xs,
+                                                                const bf16* __restrict__ res,
                                                                 const bf16* __restrict__ w3, const float* __restrict__ b3,
                                                                 const bf16* __restrict__ w1, const float* __restrict__ b1,
                                                                 bf16* __restrict__ y3, bf16* __restrict__ y1, int M) {
+  constexpr int CM = DUAL ? 2 * CX : CX;  // GEMM-1 depth
   constexpr int W3_BYTES = CO * CM * 2;
   constexpr int W1_BYTES = CN * CO * 2;
   constexpr int X_BYTES = TP * (CN > CM ? CN : CM) * 2;  // x2 tile, then the y1 staging tile
@@ -66,8 +72,9 @@ __global__ __launch_bounds__(NT, 1) void bottleneck_tail_kernel(const bf16* __re
   const int ntiles = (M + TP - 1) / TP;
   if ((int)blockIdx.x >= ntiles) return;  // block-uniform, before any barrier
 
-  // ---- resident weights: w3 [256][64], w1 [CN][256] (1x1 OHWI = row-major [co][ci])
-  for (int q = tid; q < CO * CM / 8; q += NT) W3s[swz<8>(q >> 3, q & 7)] = reinterpret_cast<const u32x4*>(w3)[q];
+  // ---- resident weights: w3 [256][CM], w1 [CN][256] (1x1 OHWI = row-major [co][ci])
+  constexpr int XC = CM / 8;  // 16-B chunks per X / W3 row
+  for (int q = tid; q < CO * CM / 8; q += NT) W3s[swz<XC>(q / XC, q % XC)] = reinterpret_cast<const u32x4*>(w3)[q];
   for (int q = tid; q < CN * CO / 8; q += NT) W1s[swz<32>(q >> 5, q & 31)] = reinterpret_cast<const u32x4*>(w1)[q];
 
   constexpr int XIT = XCH / NT;
@@ -76,15 +83,16 @@ __global__ __launch_bounds__(NT, 1) void bottleneck_tail_kernel(const bf16* __re
 #pragma unroll
     for (int it = 0; it < XIT; ++it) {
       const int q = tid + it * NT;
-      const int px = t * TP + (q >> 3);
-      xr[it] = px < M ? reinterpret_cast<const u32x4*>(x2 + (size_t)px * CM)[q & 7] : u32x4{0u, 0u, 0u, 0u};
+      const int px = t * TP + q / XC, c = q % XC;
+      const bf16* srcp = (!DUAL || c < 8) ? x2 : xs;
+      xr[it] = px < M ? reinterpret_cast<const u32x4*>(srcp + (size_t)px * CX)[c & 7] : u32x4{0u, 0u, 0u, 0u};
     }
   };
   auto store_x = [&]() {
 #pragma unroll
     for (int it = 0; it < XIT; ++it) {
       const int q = tid + it * NT;
-      Xs[swz<8>(q >> 3, q & 7)] = xr[it];
+      Xs[swz<XC>(q / XC, q % XC)] = xr[it];
     }
   };
 
@@ -105,10 +113,10 @@ __global__ __launch_bounds__(NT, 1) void bottleneck_tail_kernel(const bf16* __re
       const int c = ks * 4 + kg;
       bf16x8 a[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = __builtin_bit_cast(bf16x8, W3s[swz<8>(wave * 32 + i * 16 + prow, c)]);
+      for (int i = 0; i < 2; ++i) a[i] = __builtin_bit_cast(bf16x8, W3s[swz<XC>(wave * 32 + i * 16 + prow, c)]);
 #pragma unroll
       for (int j = 0; j < PF; ++j) {
-        const bf16x8 b = __builtin_bit_cast(bf16x8, Xs[swz<8>(j * 16 + prow, c)]);
+        const bf16x8 b = __builtin_bit_cast(bf16x8, Xs[swz<XC>(j * 16 + prow, c)]);
 #pragma unroll
         for (int i = 0; i < 2; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][j], 0, 0, 0);
       }
@@ -137,7 +145,8 @@ __global__ __launch_bounds__(NT, 1) void bottleneck_tail_kernel(const bf16* __re
       for (int it = 0; it < YIT; ++it) {  // all residual loads in flight first
         const int q = tid + it * NT;
         const int px = p0 + (q >> 5);
-        rv[it] = px < M ? reinterpret_cast<const u32x4*>(res + (size_t)px * CO)[q & 31] : u32x4{0u, 0u, 0u, 0u};
+        rv[it] = (!DUAL && px < M) ? reinterpret_cast<const u32x4*>(res + (size_t)px * CO)[q & 31]
+                                   : u32x4{0u, 0u, 0u, 0u};
       }
 #pragma unroll
       for (int it = 0; it < YIT; ++it) {
@@ -197,36 +206,45 @@ __global__ __launch_bounds__(NT, 1) void bottleneck_tail_kernel(const bf16* __re
   }
 }
 
-template <int TP, int CN>
-void launch_tail(const bf16* x2, const bf16* res, const bf16* w3, const float* b3, const bf16* w1, const float* b1,
-                 bf16* y3, bf16* y1, int M, int num_cu, hipStream_t stream) {
+template <int TP, int CN, bool DUAL>
+void launch_tail(const bf16* x2, const bf16* xs, const bf16* res, const bf16* w3, const float* b3, const bf16* w1,
+                 const float* b1, bf16* y3, bf16* y1, int M, int num_cu, hipStream_t stream) {
+  constexpr int CM = DUAL ? 2 * CX : CX;
   const int tiles = (M + TP - 1) / TP;
   const int grid = tiles < num_cu ? tiles : num_cu;
   const size_t lds = CO * CM * 2 + CN * CO * 2 + TP * (CN > CM ? CN : CM) * 2 + TP * CO * 2;
-  hipFuncSetAttribute((const void*)bottleneck_tail_kernel<TP, CN>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL((bottleneck_tail_kernel<TP, CN>), dim3(grid), dim3(NT), lds, stream, x2, res, w3, b3, w1, b1, y3,
-                     y1, M);
+  static_assert(CO * CM * 2 + CN * CO * 2 + TP * (CN > CM ? CN : CM) * 2 + TP * CO * 2 <= 160 * 1024, "LDS");
+  hipFuncSetAttribute((const void*)bottleneck_tail_kernel<TP, CN, DUAL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      lds);
+  hipLaunchKernelGGL((bottleneck_tail_kernel<TP, CN, DUAL>), dim3(grid), dim3(NT), lds, stream, x2, xs, res, w3, b3, w1,
+                     b1, y3, y1, M);
 }
 
 }  // namespace
 
-// x2 [M, 64], res [M, 256], w3 [256, 64], b3 [256], w1 [cn, 256], b1 [cn] -> y3 [M, 256],
-// y1 [M, cn] (all bf16 rows contiguous; biases fp32); cn = 64 or 128.
-void bottleneck_tail_bf16(uintptr_t x2, uintptr_t res, uintptr_t w3, uintptr_t b3, uintptr_t w1, uintptr_t b1,
-                          uintptr_t y3, uintptr_t y1, int M, int cn, int num_cu, uintptr_t stream) {
+// x2 [M, 64], res [M, 256] (or, dual: xs [M, 64] and no residual), w3 [256, 64] (dual:
+// [256, 128] = [W3 | Wsc]), b3 [256], w1 [cn, 256], b1 [cn] -> y3 [M, 256], y1 [M, cn]
+// (all bf16 rows contiguous; biases fp32); cn = 64 or 128 (128: identity residual only).
+void bottleneck_tail_bf16(uintptr_t x2, uintptr_t xs, uintptr_t res, uintptr_t w3, uintptr_t b3, uintptr_t w1,
+                          uintptr_t b1, uintptr_t y3, uintptr_t y1, int M, int cn, int num_cu, uintptr_t stream) {
   if (M <= 0) throw std::invalid_argument("bottleneck_tail: empty problem");
   if ((long)M * CO >= (1L << 31)) throw std::invalid_argument("bottleneck_tail: tensor too large for 32-bit indexing");
-  for (uintptr_t p : {x2, res, w3, w1, y3, y1, b3, b1})
+  const bool dual = xs != 0;
+  if (dual == (res != 0)) throw std::invalid_argument("bottleneck_tail: pass exactly one of xs (dual) and res");
+  for (uintptr_t p : {x2, dual ? xs : res, w3, w1, y3, y1, b3, b1})
     if (!p || p % 16) throw std::invalid_argument("bottleneck_tail: null or non-16-byte-aligned pointer");
   auto s = reinterpret_cast<hipStream_t>(stream);
   auto bp = [](uintptr_t p) { return reinterpret_cast<bf16*>(p); };
   auto fp = [](uintptr_t p) { return reinterpret_cast<const float*>(p); };
-  if (cn == 64)
-    launch_tail<128, 64>(bp(x2), bp(res), bp(w3), fp(b3), bp(w1), fp(b1), bp(y3), bp(y1), M, num_cu, s);
-  else if (cn == 128)
-    launch_tail<64, 128>(bp(x2), bp(res), bp(w3), fp(b3), bp(w1), fp(b1), bp(y3), bp(y1), M, num_cu, s);
+  if (dual && cn == 64)
+    launch_tail<64, 64, true>(bp(x2), bp(xs), nullptr, bp(w3), fp(b3), bp(w1), fp(b1), bp(y3), bp(y1), M, num_cu, s);
+  else if (!dual && cn == 64)
+    launch_tail<128, 64, false>(bp(x2), nullptr, bp(res), bp(w3), fp(b3), bp(w1), fp(b1), bp(y3), bp(y1), M, num_cu, s);
+  else if (!dual && cn == 128)
+    launch_tail<64, 128, false>(bp(x2), nullptr, bp(res), bp(w3), fp(b3), bp(w1), fp(b1), bp(y3), bp(y1), M, num_cu, s);
   else
-    throw std::invalid_argument("bottleneck_tail: reduce width must be 64 or 128, got " + std::to_string(cn));
+    throw std::invalid_argument("bottleneck_tail: unsupported variant (dual " + std::to_string(dual) + ", cn " +
+                                std::to_string(cn) + ")");
   FTM_CHECK_LAUNCH();
 }
 

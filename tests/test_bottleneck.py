@@ -1,6 +1,7 @@
 """Fused ResNet stage-1 block boundary (``ops.kernels.bottleneck_tail``): the host
 reference, and the compiler's fusion of a 1x1 expand conv with the next block's 1x1
-reduce conv (two boundaries in ResNet-50: inside stage 1 and stage 1 -> stage 2), and
+reduce conv (three boundaries in ResNet-50: the two inside stage 1 — the first one with the
+projection shortcut folded in — and stage 1 -> stage 2), and
 the library-GEMM lowering of the deep-K 1x1 convs (GPU)."""
 import os
 
@@ -25,6 +26,14 @@ def test_host_reference_matches_two_convs():
     torch.testing.assert_close(y1, e1, rtol=1e-4, atol=1e-3)
     with pytest.raises(ValueError):
         K.bottleneck_tail(x2, res, w3, b3, w1[:96], b1[:96])
+    # dual form: expand + stride-1 projection shortcut over [x2 | xs], no residual
+    xs, wsc = torch.randn(2, 5, 7, 64, generator=g), torch.randn(256, 64, generator=g)
+    w1 = w1[:64]
+    y3, y1 = K.bottleneck_tail(x2, None, torch.cat([w3, wsc], 1), b3, w1, b1[:64], xs=xs)
+    e3 = torch.relu(K.conv2d_nhwc(x2, w3.reshape(256, 1, 1, 64), b3) + K.conv2d_nhwc(xs, wsc.reshape(256, 1, 1, 64)))
+    e1 = K.conv2d_nhwc(e3, w1.reshape(64, 1, 1, 256), b1[:64], act="relu")
+    torch.testing.assert_close(y3, e3, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(y1, e1, rtol=1e-4, atol=1e-3)
 
 
 def _compile(g, dev, fuse, lib="1"):
@@ -48,8 +57,10 @@ def r50():
 
 def _check(r50, dev):
     fused, plain = _compile(r50, dev, True), _compile(r50, dev, False, lib="0")
-    assert fused.summary()["fused_tails"] == 2 and plain.summary()["fused_tails"] == 0
-    assert len(fused.steps) == len(plain.steps) - 2
+    # stage 1: block 1 (dual: projection shortcut) -> 2 -> 3 -> stage 2 block 1
+    assert fused.summary()["fused_tails"] == 3 and plain.summary()["fused_tails"] == 0
+    assert fused.summary()["fused_shortcuts"] == plain.summary()["fused_shortcuts"] == 4
+    assert len(fused.steps) == len(plain.steps) - 3
     # deep-K 1x1 reduce convs (stages 3/4) go to the library GEMM on the GPU only
     n_lib = fused.summary()["kinds"].get("gemm_lib", 0) - plain.summary()["kinds"].get("gemm_lib", 0)
     assert n_lib == (8 if dev.type == "cuda" else 0)

@@ -262,3 +262,22 @@ def test_bottleneck_tail_kernel(cn, M):
     torch.cuda.synchronize()
     _close(y3, y3_ref)
     _close(y1, y1_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [2 * 56 * 56, 1000 + 37])
+def test_bottleneck_tail_dual_kernel(M):
+    """Dual form: [x2 | xs] . [W3 | Wsc]^T (expand + stride-1 projection shortcut) -> relu
+    -> 1x1 reduce, vs the fp32 reference."""
+    g = torch.Generator().manual_seed(M)
+    x2 = torch.randn(M, 64, generator=g).to(torch.bfloat16)
+    xs = torch.randn(M, 64, generator=g).to(torch.bfloat16)
+    w3 = (torch.randn(256, 128, generator=g) * 0.1).to(torch.bfloat16)
+    w1 = (torch.randn(64, 256, generator=g) * 0.05).to(torch.bfloat16)
+    b3, b1 = torch.randn(256, generator=g), torch.randn(64, generator=g)
+    y3_ref = torch.relu(torch.cat([x2, xs], 1).float() @ w3.float().t() + b3)
+    y1_ref = torch.relu(y3_ref.to(torch.bfloat16).float() @ w1.float().t() + b1)
+    y3, y1 = K.bottleneck_tail(x2.to(DEV), None, w3.to(DEV), b3.to(DEV), w1.to(DEV), b1.to(DEV), xs=xs.to(DEV))
+    torch.cuda.synchronize()
+    _close(y3, y3_ref)
+    _close(y1, y1_ref)
