@@ -729,21 +729,29 @@ class CompiledFunction:
         return True
 
     def _fuse_block_tail(self, xin, out, w3, w_dev, b_dev, res_val, xs_val, act, absorbed, last, name) -> bool:
-        """ResNet stage-1 block boundary: this 1x1 64 -> 256 expand conv (+ residual, ReLU)
-        and the next block's 1x1 256 -> 64|128 reduce conv (+ ReLU) that reads its output
-        run as one persistent kernel (``bottleneck_tail``): the 256-channel output is still
-        stored (it is the next residual) but the reduce GEMM reads it from LDS instead of
-        HBM.  ``w3`` is the host [256, K] expand weight; with ``xs_val`` (a stage's first
-        block) K = 64 + 64 covers the stride-1 projection shortcut of ``xs_val`` too."""
+        """ResNet bottleneck block boundary: this 1x1 CX -> 4 CX expand conv (+ residual,
+        ReLU) and the next block's 1x1 reduce conv (+ ReLU) that reads its output run as one
+        persistent kernel (``bottleneck_tail``): the wide output is still stored (it is the
+        next residual) but the reduce GEMM reads it from LDS instead of HBM.  Stage 1
+        (CX = 64, reduce to 64 or 128) and stage 2 (CX = 128, reduce to 128).  ``w3`` is the
+        host [4 CX, K] expand weight; with ``xs_val`` (stage 1's first block) K = 64 + 64
+        covers the stride-1 projection shortcut of ``xs_val`` too."""
         if os.environ.get("FTM_TAIL_FUSE", "1") == "0" or self.precision == "fp8":
             return False
+        cx = xin.shape[-1]
+        co = 4 * cx
+        # stage 2 (weights streamed through LDS) measured no faster than the two convs it
+        # replaces (profiles/r01_tail): opt-in only
+        wide = os.environ.get("FTM_TAIL_WIDE", "0") == "1"
+        widths = {64: (64, 128), 128: (128,) if wide else ()}.get(cx, ()) if xs_val is None \
+            else ((64,) if cx == 64 else ())
 
         def plain(v):
-            return v.shape[-1] == 64 and (v.phys_c or 64) == 64 and v.concat_slot is None and v.qscale is None \
+            return v.shape[-1] == cx and (v.phys_c or cx) == cx and v.concat_slot is None and v.qscale is None \
                 and v.dtype == torch.bfloat16 and tuple(v.shape[:-1]) == tuple(out.shape[:-1])
 
-        if act != K.ACT_RELU or out.qscale is not None or tuple(w3.shape) != (256, 64 if xs_val is None else 128) \
-                or not plain(xin):
+        if not widths or act != K.ACT_RELU or out.qscale is not None \
+                or tuple(w3.shape) != (co, cx if xs_val is None else 2 * cx) or not plain(xin):
             return False
         if res_val is not None and (res_val.shape != out.shape or res_val.qscale is not None
                                     or res_val.concat_slot is not None):
@@ -752,7 +760,7 @@ class CompiledFunction:
             return False
         cand = [self.graph[c] for c in self.cons.get(last.name, []) if c not in self._fused]
 
-        def reduce_conv(c):  # 1x1 / s1 256 -> 64|128 reading this output (not the stage's projection)
+        def reduce_conv(c):  # 1x1 / s1 reduce conv reading this output (not the stage's projection)
             if c.op != "Conv2D" or c.inputs[0] != (last.name, 0) or c.attr("data_format", "NHWC") != "NHWC" \
                     or list(c.attr("strides")) != [1, 1, 1, 1] \
                     or list(c.attr("dilations") or [1, 1, 1, 1]) != [1, 1, 1, 1]:
@@ -761,10 +769,10 @@ class CompiledFunction:
             if wv is None or not wv.is_const:
                 return None
             w = wv.const.float()  # HWIO
-            return w if tuple(w.shape[:3]) == (1, 1, 256) and w.shape[3] in (64, 128) else None
+            return w if tuple(w.shape[:3]) == (1, 1, co) and w.shape[3] in widths else None
 
         cand = [(c, w) for c in cand for w in [reduce_conv(c)] if w is not None]
-        if len(cand) != 1 or (xs_val is not None and cand[0][1].shape[3] != 64):
+        if len(cand) != 1:
             return False
         c, w2 = cand[0]
         last2, scale2, bias2, residual2, act2, absorbed2 = self._conv_chain(c)
@@ -773,9 +781,9 @@ class CompiledFunction:
         cn = w2.shape[3]
         if scale2 is not None:
             w2 = w2 * scale2
-        w3_dev = w_dev  # row-major [256][K] (1x1 OHWI [256, 1, 1, 64], or the dual [W3 | Wsc])
-        b3_dev = b_dev if b_dev is not None else self._dev(torch.zeros(256), torch.float32)
-        w1_dev = self._dev(w2.reshape(256, cn).t().contiguous(), torch.bfloat16)
+        w3_dev = w_dev  # row-major [4 CX][K] (1x1 OHWI [4 CX, 1, 1, CX], or the dual [W3 | Wsc])
+        b3_dev = b_dev if b_dev is not None else self._dev(torch.zeros(co), torch.float32)
+        w1_dev = self._dev(w2.reshape(co, cn).t().contiguous(), torch.bfloat16)
         b1_dev = self._dev(bias2 if bias2 is not None else torch.zeros(cn), torch.float32)
         self.params += [b3_dev, w1_dev, b1_dev]
         N, H, W, _ = out.shape

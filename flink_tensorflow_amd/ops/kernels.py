@@ -212,35 +212,38 @@ def conv3x3_c64(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor, act=N
 def bottleneck_tail(x2: torch.Tensor, res: torch.Tensor | None, w3: torch.Tensor, b3: torch.Tensor, w1: torch.Tensor,
                     b1: torch.Tensor, y3: torch.Tensor | None = None, y1: torch.Tensor | None = None,
                     xs: torch.Tensor | None = None):
-    """Fused ResNet stage-1 block boundary (kernels/bottleneck.hip):
-    ``y3 = relu(x2 @ w3^T + b3 + res)`` (1x1 64 -> 256 with residual) and
-    ``y1 = relu(y3 @ w1^T + b1)`` (the next block's 1x1 256 -> CN, CN = 64 or 128);
-    returns ``(y3, y1)``.  ``x2 [..., 64]``, ``res [..., 256]``, ``w3 [256, 64]``, ``w1 [CN, 256]``
-    (1x1 OHWI squeezed), fp32 biases.  Dual form (a stage's first block, projection shortcut):
-    ``xs [..., 64]`` instead of ``res`` and ``w3 [256, 128]`` = [expand | projection] —
-    ``y3 = relu([x2 | xs] @ w3^T + b3)`` (CN = 64).  GPU: one persistent kernel, y3 reused
-    from LDS; host: the fp32 reference with y3 rounded to the output dtype before the second
-    GEMM."""
+    """Fused ResNet bottleneck block boundary (kernels/bottleneck.hip):
+    ``y3 = relu(x2 @ w3^T + b3 + res)`` (1x1 expand CX -> 4 CX with residual) and
+    ``y1 = relu(y3 @ w1^T + b1)`` (the next block's 1x1 reduce 4 CX -> CN); returns
+    ``(y3, y1)``.  Variants: CX = 64 (stage 1) with CN = 64 or 128; CX = 128 (stage 2) with
+    CN = 128 (weights streamed through LDS).  Dual form (stage 1's first block, stride-1
+    projection shortcut): ``xs [..., 64]`` instead of ``res`` and ``w3 [256, 128]`` =
+    [expand | projection] — ``y3 = relu([x2 | xs] @ w3^T + b3)`` (CN = 64).  Weights are 1x1
+    OHWI squeezed ([out, in]), biases fp32.  GPU: one persistent kernel, y3 reused from LDS;
+    host: the fp32 reference with y3 rounded to the output dtype before the second GEMM."""
     lead = x2.shape[:-1]
     dual = xs is not None
+    cx = x2.shape[-1]
+    co = 4 * cx
+    cn = w1.shape[0]
     if (res is None) != dual:
         raise ValueError("bottleneck_tail: pass exactly one of res and xs")
-    k3 = 128 if dual else 64
-    if x2.shape[-1] != 64 or (dual and tuple(xs.shape) != (*lead, 64)) or (not dual and tuple(res.shape) != (*lead, 256)):
-        raise ValueError(f"bottleneck_tail: x2 {tuple(x2.shape)} must be [..., 64] with res [..., 256] or xs [..., 64]")
-    cn = w1.shape[0]
-    if w3.numel() != 256 * k3 or w3.shape[0] != 256 or cn not in (64, 128) or w1.numel() != cn * 256 \
-            or (dual and cn != 64):
-        raise ValueError(f"bottleneck_tail: weights must be [256, {k3}] and [64|128, 256] (dual: 64), got "
-                         f"{tuple(w3.shape)} {tuple(w1.shape)}")
-    if b3.numel() != 256 or b1.numel() != cn:
+    if (cx, dual, cn) not in ((64, True, 64), (64, False, 64), (64, False, 128), (128, False, 128)):
+        raise ValueError(f"bottleneck_tail: unsupported variant x2 [..., {cx}], dual {dual}, reduce width {cn}")
+    k3 = 2 * cx if dual else cx
+    if (dual and tuple(xs.shape) != (*lead, cx)) or (not dual and tuple(res.shape) != (*lead, co)):
+        raise ValueError(f"bottleneck_tail: the second input must be [..., {cx if dual else co}]")
+    if tuple(w3.reshape(w3.shape[0], -1).shape) != (co, k3) or tuple(w1.reshape(cn, -1).shape) != (cn, co):
+        raise ValueError(f"bottleneck_tail: weights must be [{co}, {k3}] and [{cn}, {co}], got {tuple(w3.shape)} "
+                         f"{tuple(w1.shape)}")
+    if b3.numel() != co or b1.numel() != cn:
         raise ValueError("bottleneck_tail: bias sizes must match the output channels")
     odt = x2.dtype if x2.is_cuda else torch.float32
-    y3 = torch.empty((*lead, 256), dtype=odt, device=x2.device) if y3 is None else y3
+    y3 = torch.empty((*lead, co), dtype=odt, device=x2.device) if y3 is None else y3
     y1 = torch.empty((*lead, cn), dtype=odt, device=x2.device) if y1 is None else y1
-    if tuple(y3.shape) != (*lead, 256) or tuple(y1.shape) != (*lead, cn):
+    if tuple(y3.shape) != (*lead, co) or tuple(y1.shape) != (*lead, cn):
         raise ValueError("bottleneck_tail: output buffers do not fit")
-    M = x2.numel() // 64
+    M = x2.numel() // cx
     second = xs if dual else res
     if x2.is_cuda:
         for t, n in ((x2, "x2"), (second, "xs" if dual else "res"), (w3, "w3"), (w1, "w1"), (y3, "y3"), (y1, "y1")):
@@ -250,15 +253,21 @@ def bottleneck_tail(x2: torch.Tensor, res: torch.Tensor | None, w3: torch.Tensor
         dev = x2.device.index if x2.device.index is not None else torch.cuda.current_device()
         if dev not in _NUM_CU:
             _NUM_CU[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
-        _hip().bottleneck_tail_bf16(x2.data_ptr(), _ptr(xs), _ptr(res), w3.data_ptr(), b3.data_ptr(), w1.data_ptr(),
-                                    b1.data_ptr(), y3.data_ptr(), y1.data_ptr(), M, cn, _NUM_CU[dev], _stream())
+        if cx == 128:
+            _hip().bottleneck_tail_wide_bf16(x2.data_ptr(), res.data_ptr(), w3.data_ptr(), b3.data_ptr(),
+                                             w1.data_ptr(), b1.data_ptr(), y3.data_ptr(), y1.data_ptr(), M,
+                                             _NUM_CU[dev], _stream())
+        else:
+            _hip().bottleneck_tail_bf16(x2.data_ptr(), _ptr(xs), _ptr(res), w3.data_ptr(), b3.data_ptr(),
+                                        w1.data_ptr(), b1.data_ptr(), y3.data_ptr(), y1.data_ptr(), M, cn,
+                                        _NUM_CU[dev], _stream())
         return y3, y1
-    xin = torch.cat([x2.reshape(M, 64), xs.reshape(M, 64)], 1) if dual else x2.reshape(M, 64)
-    a = xin.float() @ w3.reshape(256, k3).float().t() + b3.float()
+    xin = torch.cat([x2.reshape(M, cx), xs.reshape(M, cx)], 1) if dual else x2.reshape(M, cx)
+    a = xin.float() @ w3.reshape(co, k3).float().t() + b3.float()
     a = a.to(odt).float()  # the kernel rounds acc + bias first
-    a = torch.relu(a if dual else a + res.reshape(M, 256).float())
+    a = torch.relu(a if dual else a + res.reshape(M, co).float())
     y3.copy_(a.reshape(y3.shape).to(y3.dtype))
-    b = torch.relu(y3.reshape(M, 256).float() @ w1.reshape(cn, 256).float().t() + b1.float())
+    b = torch.relu(y3.reshape(M, co).float() @ w1.reshape(cn, co).float().t() + b1.float())
     y1.copy_(b.reshape(y1.shape).to(y1.dtype))
     return y3, y1
 

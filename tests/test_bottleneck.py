@@ -1,7 +1,7 @@
 """Fused ResNet stage-1 block boundary (``ops.kernels.bottleneck_tail``): the host
 reference, and the compiler's fusion of a 1x1 expand conv with the next block's 1x1
-reduce conv (three boundaries in ResNet-50: the two inside stage 1 — the first one with the
-projection shortcut folded in — and stage 1 -> stage 2), and
+reduce conv (five boundaries in ResNet-50: the two inside stage 1 — the first one with the
+projection shortcut folded in —, stage 1 -> stage 2, and, opt-in, two inside stage 2), and
 the library-GEMM lowering of the deep-K 1x1 convs (GPU)."""
 import os
 
@@ -34,10 +34,21 @@ def test_host_reference_matches_two_convs():
     e1 = K.conv2d_nhwc(e3, w1.reshape(64, 1, 1, 256), b1[:64], act="relu")
     torch.testing.assert_close(y3, e3, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(y1, e1, rtol=1e-4, atol=1e-3)
+    # stage-2 form: 128 -> 512 (+ residual) -> 128
+    x2, res = torch.randn(3, 4, 128, generator=g), torch.randn(3, 4, 512, generator=g)
+    w3, w1 = torch.randn(512, 128, generator=g), torch.randn(128, 512, generator=g)
+    b3, b1 = torch.randn(512, generator=g), torch.randn(128, generator=g)
+    y3, y1 = K.bottleneck_tail(x2, res, w3, b3, w1, b1)
+    e3 = K.conv2d_nhwc(x2[None], w3.reshape(512, 1, 1, 128), b3, res[None], act="relu")[0]
+    e1 = K.conv2d_nhwc(e3[None], w1.reshape(128, 1, 1, 512), b1, act="relu")[0]
+    torch.testing.assert_close(y3, e3, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(y1, e1, rtol=1e-4, atol=1e-3)
+    with pytest.raises(ValueError):
+        K.bottleneck_tail(x2, res, w3, b3, w1[:64], b1[:64])  # stage 2 reduces to 128 only
 
 
-def _compile(g, dev, fuse, lib="1"):
-    env = {"FTM_TAIL_FUSE": "1" if fuse else "0", "FTM_CONV_LIB": lib}
+def _compile(g, dev, fuse, lib="1", wide="0"):
+    env = {"FTM_TAIL_FUSE": "1" if fuse else "0", "FTM_CONV_LIB": lib, "FTM_TAIL_WIDE": wide}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -55,12 +66,14 @@ def r50():
     return Graph.from_graph_def(resnet50_graph_def(depth=50, image_hw=(64, 64), num_classes=16))
 
 
-def _check(r50, dev):
-    fused, plain = _compile(r50, dev, True), _compile(r50, dev, False, lib="0")
-    # stage 1: block 1 (dual: projection shortcut) -> 2 -> 3 -> stage 2 block 1
-    assert fused.summary()["fused_tails"] == 3 and plain.summary()["fused_tails"] == 0
+def _check(r50, dev, wide="0"):
+    fused, plain = _compile(r50, dev, True, wide=wide), _compile(r50, dev, False, lib="0")
+    # stage 1: block 1 (dual: projection shortcut) -> 2 -> 3 -> stage 2 block 1; opt-in
+    # (FTM_TAIL_WIDE=1), stage 2: block 2 -> 3 -> 4 (weights streamed through LDS)
+    n = 5 if wide == "1" else 3
+    assert fused.summary()["fused_tails"] == n and plain.summary()["fused_tails"] == 0
     assert fused.summary()["fused_shortcuts"] == plain.summary()["fused_shortcuts"] == 4
-    assert len(fused.steps) == len(plain.steps) - 3
+    assert len(fused.steps) == len(plain.steps) - n
     # deep-K 1x1 reduce convs (stages 3/4) go to the library GEMM on the GPU only
     n_lib = fused.summary()["kinds"].get("gemm_lib", 0) - plain.summary()["kinds"].get("gemm_lib", 0)
     assert n_lib == (8 if dev.type == "cuda" else 0)
@@ -70,10 +83,12 @@ def _check(r50, dev):
     torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2 * b.abs().max().item())
 
 
-def test_compiled_resnet50_fuses_block_boundaries_cpu(r50):
-    _check(r50, torch.device("cpu"))
+@pytest.mark.parametrize("wide", ["0", "1"])
+def test_compiled_resnet50_fuses_block_boundaries_cpu(r50, wide):
+    _check(r50, torch.device("cpu"), wide)
 
 
 @pytest.mark.gpu
-def test_compiled_resnet50_fuses_block_boundaries_gpu(r50):
-    _check(r50, torch.device("cuda", 0))
+@pytest.mark.parametrize("wide", ["0", "1"])
+def test_compiled_resnet50_fuses_block_boundaries_gpu(r50, wide):
+    _check(r50, torch.device("cuda", 0), wide)
