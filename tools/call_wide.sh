@@ -1,6 +1,4 @@
+# Wide register-staged igemm tiles (cfg 5-8): numerics, then the ResNet layer sweep
 source tools/gpu_steps.sh
-step pytest_wide 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_bottleneck.py tests/test_compiler.py -x -v -m gpu -k "bottleneck or plan" --timeout 200 --timeout-method thread
-step bench_rn 300 python bench.py --steps 30 --warmup 5
-step bench_rn2 300 python bench.py --steps 30 --warmup 5
-cd /tmp && export TMPDIR=/tmp
-step rocprof_rn 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_rn_wide" -o run -- python "$REPO/bench.py" --steps 5 --warmup 2 --lanes 1
+step pytest_conv 300 python -u -m pytest tests/test_kernels_gpu.py -x -q -m gpu -k "conv2d_nhwc or identity" --timeout 120 --timeout-method thread
+step conv_tune 400 python bench/conv_tune.py 256
