@@ -51,7 +51,16 @@ struct DconvParams {
   // 14t - ppt.., cols 16t - ppl..); out-of-range conv positions enter the max as 0
   // (exact after a ReLU).
   int Hp, Wp, ppt, ppl;
+  // byte offset into the patch of each (K-step, lane group) relative to the lane's pixel:
+  // (dy * PW + dx) * RB + channel byte of the K segment's tap; host-built so the K loop has
+  // no integer divisions (two runtime divides per step used to cost more than its MFMAs)
+  int koff[4 * 64];
 };
+
+FTM_DEVICE int koff_of(const DconvParams& p, int s, int fq) {
+  const int k0 = p.koff[s * 4], k1 = p.koff[s * 4 + 1], k2 = p.koff[s * 4 + 2], k3 = p.koff[s * 4 + 3];
+  return fq == 0 ? k0 : fq == 1 ? k1 : fq == 2 ? k2 : k3;
+}
 
 FTM_DEVICE void glds16(const void* src, uint8_t* lds) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -63,6 +72,22 @@ FTM_DEVICE uint32_t pack4_fp8(float a, float b, float c, float d) {
   int w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(a, -M), M), fminf(fmaxf(b, -M), M), 0, false);
   w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(c, -M), M), fminf(fmaxf(d, -M), M), w, true);
   return (uint32_t)w;
+}
+
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+// 3x3 max over bf16 rows of the LDS output tile.  The pooled convs are ReLU convs, so every
+// value is +0 or positive (out-of-image positions enter as +0) and the bf16 bit patterns
+// order like the values: the max is an unsigned 16-bit max, 4 v_pk_max_u16 per 8 channels
+// (a float compare per element made this epilogue, not the MFMAs, bound the stem).
+FTM_DEVICE u16x8 pool3x3_max(const uint8_t* base, int row_bytes, int px_bytes) {
+  u16x8 m = *reinterpret_cast<const u16x8*>(base);
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx)
+      if (dy | dx) m = __builtin_elementwise_max(m, *reinterpret_cast<const u16x8*>(base + dy * row_bytes + dx * px_bytes));
+  return m;
 }
 
 template <int ES, int BN, int ACT, bool OUT_FP8, bool POOL = false>
@@ -122,7 +147,6 @@ __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
   for (int i = 0; i < I; ++i)
 #pragma unroll
     for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int ntaps = p.KH * p.KW;
   // patch row of fragment j's pixel for this lane at tap offset 0
   int prow0[J];
 #pragma unroll
@@ -133,17 +157,13 @@ __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
 
   for (int s = 0; s < p.ksteps; ++s) {
     const int kb = s * 4 * KL + fq * KL;  // this lane group's K byte offset
-    int tap = kb / p.RB;
-    const int cb = kb - tap * p.RB;
-    if (tap >= ntaps) tap = 0;  // K padding: zero weights, any finite patch data
-    const int dy = tap / p.KW, dx = tap - dy * p.KW;
-    const int toff = dy * p.PW + dx;
+    const int bo = koff_of(p, s, fq);
     if constexpr (ES == 2) {
       bf16x8 a[I], bb[J];
 #pragma unroll
       for (int i = 0; i < I; ++i) a[i] = *reinterpret_cast<const bf16x8*>(Wsm + (i * 16 + frow) * p.WP + kb);
 #pragma unroll
-      for (int j = 0; j < J; ++j) bb[j] = *reinterpret_cast<const bf16x8*>(Ps + (prow0[j] + toff) * p.RB + cb);
+      for (int j = 0; j < J; ++j) bb[j] = *reinterpret_cast<const bf16x8*>(Ps + prow0[j] * p.RB + bo);
 #pragma unroll
       for (int i = 0; i < I; ++i)
 #pragma unroll
@@ -158,7 +178,7 @@ __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
       }
 #pragma unroll
       for (int j = 0; j < J; ++j) {
-        const uint8_t* src = Ps + (prow0[j] + toff) * p.RB + cb;
+        const uint8_t* src = Ps + prow0[j] * p.RB + bo;
         const u32x4 lo = *reinterpret_cast<const u32x4*>(src), hi = *reinterpret_cast<const u32x4*>(src + 16);
         bb[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
       }
@@ -212,17 +232,9 @@ __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
       const int py = (oy0 + p.ppt) / 2 + pyl, px = (ox0 + p.ppl) / 2 + pxl;
       const int c = n0 + cc * EPO;
       if (py >= p.Hp || px >= p.Wp || c >= p.Cout) continue;
-      bf16x8 m = *reinterpret_cast<const bf16x8*>(Os + ((2 * pyl) * TPW + 2 * pxl) * OLD + cc * 16);
-#pragma unroll
-      for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx) {
-          const bf16x8 v = *reinterpret_cast<const bf16x8*>(Os + ((2 * pyl + dy) * TPW + 2 * pxl + dx) * OLD + cc * 16);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) m[e] = (float)v[e] > (float)m[e] ? v[e] : m[e];
-        }
+      const u16x8 m = pool3x3_max(Os + ((2 * pyl) * TPW + 2 * pxl) * OLD + cc * 16, TPW * OLD, OLD);
       const size_t mo = ((size_t)n * p.Hp + py) * p.Wp + px;
-      *reinterpret_cast<bf16x8*>(p.y + (mo * p.ldy + p.y_coff + c) * 2) = m;
+      *reinterpret_cast<u16x8*>(p.y + (mo * p.ldy + p.y_coff + c) * 2) = m;
     }
     return;
   }
@@ -320,10 +332,20 @@ void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t 
   p.RB = Cin * es;
   p.WP = wp;
   p.ksteps = kpad / (4 * KL);
+  if (p.ksteps > 64) throw std::invalid_argument("dconv: more than 64 K-steps");
   p.PH = (TH - 1) * S + KH;
   p.PW = (Hp > 0 ? TW : TW - 1) * S + KW;  // pooled tiles are 17 conv columns wide
   p.ldy = ldy; p.y_coff = y_coff;
   p.Hp = Hp; p.Wp = Wp; p.ppt = ppt; p.ppl = ppl;
+  for (int st = 0; st < p.ksteps; ++st)
+    for (int fq = 0; fq < 4; ++fq) {
+      const int kb = st * 4 * KL + fq * KL;
+      int tap = kb / p.RB;
+      const int cb = kb - tap * p.RB;
+      if (tap >= KH * KW) tap = 0;  // K padding: zero weights, any finite patch data
+      const int dy = tap / KW, dx = tap - dy * KW;
+      p.koff[st * 4 + fq] = (dy * p.PW + dx) * p.RB + cb;
+    }
   if (Hp > 0) {  // pooled tiles of 7 x 8 (15 x 17 conv pixels)
     if (ppt < 0 || ppt > 1 || ppl < 0 || ppl > 1) throw std::invalid_argument("dconv: pool padding must be 0/1");
     if ((Hp - 1) * 2 + 3 > Ho + ppt + 1 || (Wp - 1) * 2 + 3 > Wo + ppl + 1)

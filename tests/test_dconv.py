@@ -89,6 +89,8 @@ POOL_CASES = [  # N, H, W, Cin, Cout, (kh, kw), stride, pad, pool padding (TF "S
     (2, 56, 56, 16, 64, (4, 4), 1, (2, 1, 2, 1), "SAME", 64),  # ResNet s2d stem at 1/2 scale
     (1, 45, 39, 8, 32, (3, 3), 1, (1, 1, 1, 1), "SAME", 32),  # odd sizes: pads 1/1
     (2, 33, 30, 16, 64, (3, 3), 1, (1, 1, 1, 1), "VALID", 64),
+    (1, 30, 40, 16, 64, (4, 4), 1, (2, 1, 2, 1), "SAME", 64),  # partial last tile row and column
+    (12, 112, 112, 16, 64, (4, 4), 1, (2, 1, 2, 1), "SAME", 64),  # the 224x224 ResNet s2d stem
 ]
 
 
