@@ -46,6 +46,7 @@ struct IgemmParams {
   int ldy, y_coff;  // output pixel stride (elements) and channel offset
   int ldr;          // residual pixel stride
   int tiles_m, tiles_n;
+  int kq, kr;  // CONV: divmod(BK, Cin), the (tap, channel) advance of one K tile
   // DUAL (pointwise GEMM + fused strided 1x1 shortcut): K = K1 + C2; k >= K1 reads the
   // second source x2 [N, H2, W2, C2] at pixel (n, ho*s2, wo*s2) of output pixel (n, ho, wo)
   const bf16* x2;
@@ -88,7 +89,12 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
   const int kc = tid & 7;
   const int r0 = tid >> 3;
 
-  int xbase[XR], hb[XR], wb[XR];
+  // CONV: per staged row the byte offset of its receptive field's (tap 0) corner pixel and a
+  // bitmask of the filter taps that land inside the image (padding taps and rows past M read
+  // through the buffer descriptor's range check as zeros).  The K loop then needs no
+  // divides and no bounds compares: it walks (tap, channel) incrementally.
+  int xbase[XR];
+  uint64_t tmask[CONV ? XR : 1];
   int x2base[DUAL ? XR : 1];
   bool mvalid[XR];
 #pragma unroll
@@ -104,46 +110,73 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
       x2base[i] = ((n * p.H2 + ho * p.s2) * p.W2 + wo * p.s2) * p.C2;
     }
     if constexpr (CONV) {
-      int wo = mm % p.Wo;
-      int t = mm / p.Wo;
-      int ho = t % p.Ho;
-      int n = t / p.Ho;
-      xbase[i] = n * p.H * p.W * p.Cin;
-      hb[i] = ho * p.sh - p.ph;
-      wb[i] = wo * p.sw - p.pw;
+      const int wo = mm % p.Wo;
+      const int t = mm / p.Wo;
+      const int ho = t % p.Ho;
+      const int n = t / p.Ho;
+      const int hb = ho * p.sh - p.ph, wb = wo * p.sw - p.pw;
+      xbase[i] = (((n * p.H + hb) * p.W + wb) * p.Cin) * 2;  // bytes; only used for in-image taps
+      uint64_t cols = 0, tm = 0;  // in-image filter columns, then rows x columns
+      for (int kw = 0; kw < p.KW; ++kw)
+        if ((unsigned)(wb + kw * p.dw) < (unsigned)p.W) cols |= 1ull << kw;
+      if (mvalid[i])
+        for (int kh = 0; kh < p.KH; ++kh)
+          if ((unsigned)(hb + kh * p.dh) < (unsigned)p.H) tm |= cols << (kh * p.KW);
+      tmask[i] = tm;
     } else {
       xbase[i] = mm * p.ldx;
-      hb[i] = 0;
-      wb[i] = 0;
     }
   }
-  const bf16* wrow[WR];
-  bool nvalid[WR];
+  // weight rows: CONV reads them through a buffer descriptor (rows past Cout and the K tail
+  // read as zeros, no branches); the GEMM modes keep plain predicated loads
+  int wrow[WR];  // byte offset of this thread's weight row (0x7fffffff: past Cout)
 #pragma unroll
   for (int i = 0; i < WR; ++i) {
-    int co = n0 + r0 + 32 * i;
-    nvalid[i] = co < p.Cout;
-    wrow[i] = p.w + (size_t)(nvalid[i] ? co : 0) * p.K;
+    const int co = n0 + r0 + 32 * i;
+    wrow[i] = co < p.Cout ? co * p.K * 2 : 0x7fffffff;
   }
+  const __amdgpu_buffer_rsrc_t wrsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p.w), 0, CONV ? p.Cout * p.K * 2 : 0, 0x00020000);
 
   u32x4 xr[XR], wr[WR];
   const u32x4 zero4 = {0u, 0u, 0u, 0u};
+
+  // CONV K walk: this thread's 8-channel chunk sits at channel ci of filter tap `tap`
+  // (= kh * KW + kw); tapoff = the tap's byte offset relative to the corner pixel.  One
+  // K tile advances (tap, ci) by (kq, kr) = divmod(BK, Cin) (host-computed): no divides.
+  const int cin2 = p.Cin * 2;
+  int tap = 0, ci = 0, kh = 0, kw = 0, tapoff = 0;
+  if constexpr (CONV) {
+    tap = kc * 8 / p.Cin;
+    ci = kc * 8 - tap * p.Cin;
+    kh = tap / p.KW;
+    kw = tap - kh * p.KW;
+    tapoff = (kh * p.dh * p.W + kw * p.dw) * cin2;
+  }
+  auto advance_k = [&]() {
+    ci += p.kr;
+    tap += p.kq;
+    kw += p.kq;
+    if (ci >= p.Cin) { ci -= p.Cin; ++tap; ++kw; }
+    while (kw >= p.KW) { kw -= p.KW; ++kh; }
+    tapoff = (kh * p.dh * p.W + kw * p.dw) * cin2;
+  };
+  const __amdgpu_buffer_rsrc_t xrsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p.x), 0, CONV ? p.N * p.H * p.W * cin2 : 0, 0x00020000);
+  const int ntaps = p.KH * p.KW;
 
   auto load_tile = [&](int k0) {
     const int k = k0 + kc * 8;
     const bool kvalid = k < p.K;
     if constexpr (CONV) {
-      int kidx = k / p.Cin;
-      int ci = k - kidx * p.Cin;
-      int kh = kidx / p.KW;
-      int kw = kidx - kh * p.KW;
+      const bool tvalid = tap < ntaps;
+      const int koff = tapoff + ci * 2;
 #pragma unroll
       for (int i = 0; i < XR; ++i) {
-        int hi = hb[i] + kh * p.dh;
-        int wi = wb[i] + kw * p.dw;
-        bool ok = kvalid && mvalid[i] && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
-        xr[i] = ok ? *reinterpret_cast<const u32x4*>(p.x + xbase[i] + ((size_t)hi * p.W + wi) * p.Cin + ci) : zero4;
+        const bool ok = tvalid && ((tmask[i] >> tap) & 1);
+        xr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc, ok ? xbase[i] + koff : 0x7fffffff, 0, 0));
       }
+      advance_k();
     } else if constexpr (DUAL) {
       const bool second = k >= p.K1;  // chunk-uniform: K1 % 8 == 0
 #pragma unroll
@@ -161,8 +194,11 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
     }
 #pragma unroll
     for (int i = 0; i < WR; ++i) {
-      bool ok = kvalid && nvalid[i];
-      wr[i] = ok ? *reinterpret_cast<const u32x4*>(wrow[i] + k) : zero4;
+      const bool ok = kvalid && wrow[i] != 0x7fffffff;
+      if constexpr (CONV)
+        wr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, ok ? wrow[i] + k * 2 : 0x7fffffff, 0, 0));
+      else
+        wr[i] = ok ? *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint8_t*>(p.w) + wrow[i] + k * 2) : zero4;
     }
   };
   auto store_tile = [&](int buf) {
@@ -372,8 +408,9 @@ void conv2d_nhwc_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, u
   if (Cout % 8 || ldy % 8 || y_coff % 8) throw std::invalid_argument("conv2d_nhwc_bf16: Cout/ldy/y_coff % 8 != 0");
   if (res && ldr % 8) throw std::invalid_argument("conv2d_nhwc_bf16: residual stride % 8 != 0");
   if (N <= 0 || Ho <= 0 || Wo <= 0 || Cout <= 0) throw std::invalid_argument("conv2d_nhwc_bf16: empty problem");
-  if ((long)N * H * W * Cin >= (1L << 31) || (long)N * Ho * Wo >= (1L << 31))
-    throw std::invalid_argument("conv2d_nhwc_bf16: tensor too large for 32-bit indexing");
+  if ((long)N * H * W * Cin * 2 >= (1L << 31) || (long)N * Ho * Wo >= (1L << 31))
+    throw std::invalid_argument("conv2d_nhwc_bf16: tensor too large for 32-bit (byte) indexing");
+  if (KH * KW > 64) throw std::invalid_argument("conv2d_nhwc_bf16: more than 64 filter taps");
   check_align(x, 16, "x");
   check_align(w, 16, "w");
   check_align(y, 16, "y");
@@ -391,6 +428,8 @@ void conv2d_nhwc_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, u
   p.K = KH * KW * Cin;
   p.ldx = Cin;
   p.ldy = ldy; p.y_coff = y_coff; p.ldr = ldr;
+  p.kq = BK / Cin;
+  p.kr = BK % Cin;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   require_bias(p.bias);
   const bool pointwise = KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
