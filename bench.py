@@ -72,6 +72,7 @@ def main():
     from flink_tensorflow_amd.graph.graph import Graph
     from flink_tensorflow_amd.models.zoo.resnet import resnet50_flops_per_image, resnet50_graph_def
     from flink_tensorflow_amd.parallel import comm
+    from flink_tensorflow_amd.utils.metrics import MetricGroup
 
     comm.init_distributed()
     rank, ws, local = comm.world()
@@ -210,9 +211,10 @@ def main():
     elapsed_max = comm.all_reduce_scalar(elapsed, "max", device=dev)
 
     lat_all = np.concatenate(lat) if lat else np.zeros(1)
-    p50 = float(np.percentile(lat_all, 50) * 1e3)
-    p99 = float(np.percentile(lat_all, 99) * 1e3)
-    p50s = comm.all_gather_object(p50)
+    # node-level percentiles: per-rank latency histograms merged bucket-wise (one all-reduce)
+    mg = MetricGroup("bench")
+    mg.histogram("latency_s").update_many(lat_all)
+    node_lat = comm.allgather_metrics(mg)["histograms"]["latency_s"]
     n_rec = n_sub if args.dynamic else B * args.steps
     per_gpu = n_rec / elapsed
     total = comm.all_reduce_scalar(float(n_rec), "sum", device=dev) / elapsed_max
@@ -236,8 +238,8 @@ def main():
                        "input_hw": (299 if args.model == "inception_v3" else 224) if seq is None else None,
                        "batch_buckets": sorted(lane_plans[0]), "dynamic_batching": args.dynamic,
                        "compute_lanes": lanes},
-            "p50_latency_ms": round(float(np.median(p50s)), 3),
-            "p99_latency_ms": round(p99, 3),
+            "p50_latency_ms": round(node_lat["p50"] * 1e3, 3),
+            "p99_latency_ms": round(node_lat["p99"] * 1e3, 3),
             "per_gpu_records_per_s": round(per_gpu, 1),
             "model_tflops_per_s": round(flops / 1e12, 1),
             "compile_s": round(compile_s, 2),

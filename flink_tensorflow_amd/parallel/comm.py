@@ -19,6 +19,7 @@ import datetime
 import os
 from typing import Iterable, Sequence
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -245,3 +246,36 @@ class GradBucketer:
         for h in self._hooks:
             h.remove()
         self._hooks.clear()
+
+
+def allgather_metrics(group) -> dict:
+    """Whole-job metrics (SURVEY §2.13 ``allgather_metrics``): counters are summed and every
+    latency histogram is merged bucket-wise across ranks, so p50/p99 are node-level
+    percentiles.  Two collectives: the (small) name sets, then ONE int64 all-reduce holding
+    all counters and all bucket vectors.  ``group`` is a ``utils.metrics.MetricGroup``.
+    """
+    from ..utils.metrics import BucketHistogram, histogram_buckets
+    cnames = sorted(group.counters)
+    hnames = sorted(group.histograms)
+    if is_dist():
+        names = all_gather_object((cnames, hnames))
+        cnames = sorted({n for c, _ in names for n in c})
+        hnames = sorted({n for _, h in names for n in h})
+    vec = np.zeros(len(cnames) + len(hnames) * BucketHistogram.N, np.int64)
+    for i, n in enumerate(cnames):
+        vec[i] = group.counters.get(n, 0)
+    for j, n in enumerate(hnames):
+        if n in group.histograms:
+            o = len(cnames) + j * BucketHistogram.N
+            vec[o:o + BucketHistogram.N] = histogram_buckets(group.histograms[n]).counts
+    if is_dist():
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+        t = torch.from_numpy(vec).to(dev)
+        dist.all_reduce(t)
+        vec = t.cpu().numpy()
+    out = {"world_size": dist.get_world_size() if is_dist() else 1,
+           "counters": {n: int(vec[i]) for i, n in enumerate(cnames)}, "histograms": {}}
+    for j, n in enumerate(hnames):
+        o = len(cnames) + j * BucketHistogram.N
+        out["histograms"][n] = BucketHistogram(vec[o:o + BucketHistogram.N]).snapshot()
+    return out

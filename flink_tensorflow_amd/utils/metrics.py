@@ -86,3 +86,61 @@ class MetricGroup:
 
     def to_json(self) -> str:
         return json.dumps({"name": self.name, **self.snapshot()})
+
+
+class BucketHistogram:
+    """Log-spaced fixed buckets (0.5 % relative width, 1e-7 .. 1e4): mergeable by summing counts.
+
+    Percentiles of a merged ``BucketHistogram`` are whole-job percentiles (not a median of
+    per-rank percentiles): ``parallel.comm.allgather_metrics`` sums the count vectors of all
+    ranks with one all-reduce of a fixed-size int64 tensor.
+    """
+    LO = 1e-7
+    GROWTH = 1.005
+    N = int(np.ceil(np.log(1e4 / 1e-7) / np.log(1.005))) + 1
+
+    def __init__(self, counts=None):
+        self.counts = np.zeros(self.N, np.int64) if counts is None else np.asarray(counts, np.int64).copy()
+
+    @classmethod
+    def index(cls, vs) -> np.ndarray:
+        v = np.maximum(np.asarray(vs, np.float64).reshape(-1), cls.LO)
+        return np.minimum((np.log(v / cls.LO) / np.log(cls.GROWTH)).astype(np.int64), cls.N - 1)
+
+    def update_many(self, vs):
+        np.add.at(self.counts, self.index(vs), 1)
+
+    def merge(self, other: "BucketHistogram") -> "BucketHistogram":
+        self.counts += other.counts
+        return self
+
+    @property
+    def count(self) -> int:
+        return int(self.counts.sum())
+
+    def percentile(self, q: float) -> float:
+        n = self.count
+        if n == 0:
+            return float("nan")
+        rank = min(n - 1, max(0, int(np.ceil(q / 100.0 * n)) - 1))
+        i = int(np.searchsorted(np.cumsum(self.counts), rank + 1))
+        return float(self.LO * self.GROWTH ** (i + 0.5))     # bucket's geometric midpoint
+
+    def snapshot(self) -> dict:
+        if self.count == 0:
+            return {"count": 0}
+        return {"count": self.count, "p50": self.percentile(50), "p95": self.percentile(95),
+                "p99": self.percentile(99), "max": self.percentile(100)}
+
+
+def histogram_buckets(h: Histogram) -> BucketHistogram:
+    """Bins a raw-sample ``Histogram`` (decimated samples are re-weighted to ``h.count``)."""
+    with h._lock:
+        v = np.asarray(h._v, np.float64)
+        count = h.count
+    b = BucketHistogram()
+    if len(v):
+        b.update_many(v)
+        if count != len(v):          # decimated: scale counts back to the true total
+            b.counts = np.round(b.counts * (count / len(v))).astype(np.int64)
+    return b

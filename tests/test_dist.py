@@ -185,3 +185,50 @@ def test_numa_binding_gpu():
             assert after and after <= before and r["cpus"] == len(after)
     finally:
         os.sched_setaffinity(0, before)
+
+
+def _metrics(rank, world):
+    import numpy as np
+
+    from flink_tensorflow_amd.parallel import comm
+    from flink_tensorflow_amd.utils.metrics import MetricGroup
+
+    g = MetricGroup("op")
+    g.inc("records_in", 100 * (rank + 1))
+    # rank 0: 1..100 ms, rank 1: 101..300 ms -> node-level p50 is ~150 ms, not median(p50s)
+    lo, hi = (1, 100) if rank == 0 else (101, 300)
+    g.histogram("latency_s").update_many(np.arange(lo, hi + 1) * 1e-3)
+    if rank == 1:
+        g.histogram("only_rank1").update_many([0.5])
+    return comm.allgather_metrics(g)
+
+
+def test_allgather_metrics_merges_histograms_across_ranks():
+    out = _run(_metrics)
+    m = out[0]
+    assert m == out[1]
+    assert m["world_size"] == 2 and m["counters"]["records_in"] == 300
+    h = m["histograms"]["latency_s"]
+    assert h["count"] == 300
+    assert abs(h["p50"] - 0.150) / 0.150 < 0.01          # true node-level median of 1..300 ms
+    assert abs(h["p99"] - 0.297) / 0.297 < 0.01
+    assert m["histograms"]["only_rank1"]["count"] == 1
+
+
+def test_bucket_histogram_percentiles_match_numpy():
+    import numpy as np
+
+    from flink_tensorflow_amd.utils.metrics import BucketHistogram, Histogram, histogram_buckets
+
+    rng = np.random.default_rng(0)
+    v = rng.lognormal(-5, 1, 20000)
+    b = BucketHistogram()
+    b.update_many(v)
+    for q in (50, 90, 99):
+        ref = np.percentile(v, q)
+        assert abs(b.percentile(q) - ref) / ref < 0.01
+    h = Histogram(cap=1000)
+    h.update_many(v)                                     # decimated to <= cap samples
+    hb = histogram_buckets(h)
+    assert hb.count == pytest.approx(20000, rel=0.01)
+    assert abs(hb.percentile(50) - np.percentile(v, 50)) / np.percentile(v, 50) < 0.05
