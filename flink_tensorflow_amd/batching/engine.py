@@ -7,7 +7,8 @@ image.  Here records are staged into GPU micro-batches
 
     host:  gather B record payloads → pinned slot (C++ multithreaded memcpy, GIL released)
     copy stream:    pinned slot ──hipMemcpyAsync──▶ HBM staging slot      (event h2d[s])
-    compute stream: wait h2d[s] → D2D into the plan's input → hipGraph replay
+    compute stream: wait h2d[s] → preprocess kernel on the staging slot (or D2D into the
+                    plan's input) → hipGraph replay
                     → outputs ──hipMemcpyAsync──▶ pinned result slot       (event done[s])
     host:  (later) wait done[s] → emit results, per-record latency
 
@@ -145,8 +146,12 @@ class PipelinedGpuRunner:
         with torch.cuda.stream(stream):
             stream.wait_event(slot.h2d)
             with trace_range(f"forward[{b}]@lane{lane}"):
-                plan.input_buffer(self.feed).copy_(slot.dev_in, non_blocking=True)
-                plan.replay()
+                replay_from = getattr(plan, "replay_from", None)
+                if replay_from is not None:  # head kernel reads the staging slot: no D2D copy
+                    replay_from(self.feed, slot.dev_in)
+                else:
+                    plan.input_buffer(self.feed).copy_(slot.dev_in, non_blocking=True)
+                    plan.replay()
             with trace_range("d2h"):
                 for dst, src in zip(slot.pinned_out, self.fetch_bufs(plan)):
                     dst.copy_(src, non_blocking=True)

@@ -159,3 +159,26 @@ def test_standalone_elementwise_and_lrn_gpu():
     import torch
 
     _check_elementwise(torch.device("cuda", 0))
+
+
+@pytest.mark.gpu
+def test_replay_from_staging_buffer_gpu(small_resnet):
+    """``replay_from`` runs the preprocess head on the caller's buffer and replays the tail
+    graph: same outputs as copy-into-input + full replay, and the input buffer is untouched."""
+    dev = torch.device("cuda", 0)
+    imgs = torch.randint(0, 256, (3, 72, 72, 3), dtype=torch.uint8, device=dev)
+    other = torch.randint(0, 256, (3, 72, 72, 3), dtype=torch.uint8, device=dev)
+    plan = CompiledFunction(small_resnet, {"images:0": ((3, 72, 72, 3), "UINT8")}, ["logits:0"], dev, strict=True)
+    assert plan._head is not None and plan._graph_tail is not None
+    ref = plan({"images:0": imgs})[0].clone()
+    plan.input_buffer("images:0").copy_(other)
+    plan.replay_from("images:0", imgs)
+    got = plan.output_tensors()[0].float().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref.float())
+    assert torch.equal(plan.input_buffer("images:0"), other)
+    # a non-contiguous source falls back to copy + full replay
+    nc = imgs.permute(0, 2, 1, 3).contiguous().permute(0, 2, 1, 3)
+    plan.replay_from("images:0", nc)
+    torch.cuda.synchronize()
+    assert torch.equal(plan.output_tensors()[0].float(), ref.float())
