@@ -645,23 +645,20 @@ class CompiledFunction:
         pointwise = (KHe, KWe, sh, sw, pt, pb, pl, pr, dh, dw) == (1, 1, 1, 1, 0, 0, 0, 0, 1, 1)
         if (self.device.type == "cuda" and pointwise and res_val is None and act in (K.ACT_NONE, K.ACT_RELU)
                 and out.qscale is None and xin_shape_override is None and (xin.phys_c or Cin) == Cin
-                and Cin >= 1024 and os.environ.get("FTM_CONV_LIB", "1") != "0"):
-            # deep-K 1x1 reduce convs (ResNet stages 3/4: K = 1024 / 2048): a plain GEMM with
-            # a bias+ReLU epilogue, where the library kernel measured 1.5x the implicit GEMM
-            # (bench/probe_lib_convs.py, profiles/r01_lib)
-            b16 = self._dev(bias if bias is not None else torch.zeros(Cout), torch.bfloat16)
-            w_kn = w_dev.reshape(Cout, Cin).t()
-            self.params.append(b16)
-            relu = act == K.ACT_RELU
+                and Cin >= 1024 and Cin % 64 == 0 and Cout % 8 == 0 and _coff(out) % 8 == 0):
+            # deep-K 1x1 reduce convs (ResNet stages 3/4: K = 1024 / 2048) are plain GEMMs over
+            # the pixel matrix: the ping-pong 256x256 MFMA kernel (kernels/gemm_pp.hip)
+            w_nk = w_dev.reshape(Cout, Cin)
+            bz = b_dev if b_dev is not None else self._dev(torch.zeros(Cout), torch.float32)
+            M = int(np.prod(xin.shape[:-1]))
+            splits = K.gemm_pp_splits(M, Cout, Cin)
+            ws = torch.empty(splits * M * Cout, dtype=torch.float32, device=self.device) if splits > 1 else None
 
-            def run_lib(xin=xin, out=out, w_kn=w_kn, b16=b16, relu=relu):
-                x2, y2 = xin.buf.view(-1, Cin), out.buf.view(-1, Cout)
-                if relu:
-                    torch._addmm_activation(b16, x2, w_kn, out=y2)
-                else:
-                    torch.addmm(b16, x2, w_kn, out=y2)
+            def run_pp(xin=xin, out=out, w_nk=w_nk, bz=bz, act=act, splits=splits, ws=ws):
+                K.gemm_pp(xin.buf.view(-1, Cin), w_nk, bz, None, act, out=_target(out), out_col=_coff(out),
+                          splits=splits, ws=ws)
 
-            self._emit(node.name, "gemm_lib", run_lib, [xin], [out])
+            self._emit(node.name, "gemm", run_pp, [xin], [out], {"impl": "gemm_pp"})
             self.vals[(last.name, 0)] = out
             self._alias_fused_outputs(absorbed, out)
             return
@@ -955,17 +952,18 @@ class CompiledFunction:
             self._fused.add(n.name)
 
         M = a.shape[0]
-        tiles = -(-M // 128) * -(-n_pad // 128)
-        if self.device.type == "cuda" and tiles < 64 and act == K.ACT_NONE and res_val is None:
-            # classifier heads (M = batch, e.g. 256 x 2048 -> 1000): 16 output tiles cannot
-            # fill 256 CUs; the library GEMM's split-K kernels do (measured 39 -> ~6 us)
-            b16 = self._dev(bias if bias is not None else torch.zeros(n_pad), torch.bfloat16)
-            self.params.append(b16)
+        if self.device.type == "cuda" and Kd % 64 == 0:
+            # ping-pong MFMA GEMM; small-M heads (e.g. the 256 x 2048 -> 1000 classifier)
+            # run split-K through this step's own fp32 workspace
+            splits = K.gemm_pp_splits(M, n_pad, Kd)
+            ws = torch.empty(splits * M * n_pad, dtype=torch.float32, device=self.device) if splits > 1 else None
 
-            def run_lib(xin=xin, out=out, w_dev=w_dev, b16=b16):
-                torch.addmm(b16, xin.buf, w_dev.t(), out=out.buf)
+            def run_pp(xin=xin, out=out, res_val=res_val, w_dev=w_dev, b_dev=b_dev, splits=splits, ws=ws):
+                K.gemm_pp(xin.buf, w_dev, b_dev, res_val.buf if res_val is not None else None, act, out=out.buf,
+                          splits=splits, ws=ws)
 
-            self._emit(node.name, "gemm_lib", run_lib, [xin], [out])
+            self._emit(node.name, "gemm", run_pp, [xin] + ([res_val] if res_val else []), [out],
+                       {"impl": "gemm_pp", "splits": splits})
             self.vals[(last.name, 0)] = out
             self._alias_fused_outputs(absorbed, out)
             return
@@ -1403,7 +1401,14 @@ class CompiledFunction:
         feeds = [k for k, b in self._input_bufs.items() if b.data_ptr() == x.buf.data_ptr()]
         if len(feeds) != 1:
             return None
-        if any(i is x for t in self.steps[1:] for i in t.inputs) or any(o is x for o in self._outputs):
+        # compare alias roots (a Reshape of the feed is an alias Val sharing its buffer) and
+        # buffer addresses: any other reader of the raw feed needs the input_buffer copy
+        rx, ptr = _root(x), x.buf.data_ptr()
+
+        def reads_feed(v):
+            return v is not None and (_root(v) is rx or (v.buf is not None and v.buf.data_ptr() == ptr))
+
+        if any(reads_feed(i) for t in self.steps[1:] for i in t.inputs) or any(reads_feed(o) for o in self._outputs):
             return None
         return feeds[0], st
 

@@ -161,9 +161,6 @@ class BertDeviceWeights:
                 "f_w": mat(host[p + "output/dense/kernel"]), "f_b": vec(host[p + "output/dense/bias"]),
                 "ln2_g": vec(host[p + "output/LayerNorm/gamma"]), "ln2_b": vec(host[p + "output/LayerNorm/beta"]),
             })
-            Ld = self.layers[-1]
-            for k in ("qkv", "o", "i", "f"):  # library-GEMM epilogue biases in the matrix dtype
-                Ld[k + "_b16"] = Ld[k + "_b"].to(bf)
         self.pool_w = mat(host["bert/pooler/dense/kernel"])
         self.pool_b = vec(host["bert/pooler/dense/bias"])
         nl = cfg.num_labels
@@ -180,33 +177,6 @@ class BertDeviceWeights:
         for L in self.layers:
             out += list(L.values())
         return out
-
-
-_GEMM_TABLE: bool | None = None
-
-
-def load_gemm_table() -> bool:
-    """Pre-tuned library GEMM solutions for the BERT projection shapes at every token
-    capacity (``bench/tune_bert_gemms.py``; only the picks that beat the hipBLASLt default
-    in a timed comparison are kept, ``profiles/r01_bert_pack/tunableop_compare.jsonl``).
-    Installed as a PyTorch TunableOp lookup table with tuning OFF, so no tuning ever runs
-    inside a stream job; shapes not in the table use the library default.
-    ``FTM_GEMM_TABLE=0`` disables it."""
-    global _GEMM_TABLE
-    if _GEMM_TABLE is not None:
-        return _GEMM_TABLE
-    import os
-
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "data", "tunableop_gfx950.csv")
-    _GEMM_TABLE = False
-    if os.environ.get("FTM_GEMM_TABLE", "1") != "0" and os.path.exists(path) and torch.cuda.is_available():
-        tun = torch.cuda.tunable
-        tun.enable(True)
-        tun.tuning_enable(False)
-        _GEMM_TABLE = bool(tun.read_file(os.path.normpath(path)))
-        if not _GEMM_TABLE:  # validators differ (other ROCm / hipBLASLt build): library defaults
-            tun.enable(False)
-    return _GEMM_TABLE
 
 
 class BertBuffers:
@@ -231,6 +201,11 @@ class BertBuffers:
         # final-layer first-token rows (packed classifier: only they feed the pooler)
         self.c_ctx, self.c_y, self.c_x, self.c_x2 = (torch.empty(batch, h, dtype=dtype, device=d) for _ in range(4))
         self.c_ffn = torch.empty(batch, cfg.intermediate, dtype=dtype, device=d)
+        # split-K workspace of the final-layer first-token GEMMs (B rows); owned per buffer
+        # set because the plans of different compute lanes replay concurrently
+        shapes = [(h, h), (cfg.intermediate, h), (h, cfg.intermediate)]
+        need = max(K.gemm_pp_splits(batch, n, k) * batch * n for n, k in shapes)
+        self.ws = torch.empty(need, dtype=torch.float32, device=d)
         # one hipGraph memory pool for every plan on these buffers (graph temporaries such as
         # the GELU projection output are reused across capacities instead of duplicated)
         self.pool = torch.cuda.graph_pool_handle() if torch.device(d).type == "cuda" else None
@@ -239,13 +214,11 @@ class BertBuffers:
 class BertEncoderPlan:
     """Preallocated buffers + launch sequence for one (batch, seq); hipGraph-captured.
 
-    ``gemm="mfma"`` runs the four projections per layer on the hand-written MFMA GEMM with
-    fused bias / GELU / residual epilogues.  ``gemm="blas"`` (default on the GPU) runs them
-    as plain library GEMMs (hipBLASLt via ``torch.addmm``; bias, or bias+GELU, epilogue),
-    which measure 1.2-1.5x faster on the 32768 x {768..3072} x {768, 3072} shapes
-    (``bench/probe_hipblaslt.py`` vs ``bench/gemm_tune.py``); the residual adds then move
-    into the fused residual+LayerNorm kernel.  Embedding+LN, attention, residual+LN and
-    the pooler/classifier stay on the hand-written kernels either way.
+    Every projection runs on the hand-written ping-pong MFMA GEMM (``kernels/gemm_pp.hip``,
+    256x256 tiles, LDS-DMA pipeline) with the bias (+GELU) fused in its epilogue; the
+    residual adds are fused into the residual+LayerNorm kernel.  The final-layer
+    first-token GEMMs (B rows) run split-K.  Embedding+LN, attention, residual+LN and the
+    pooler/classifier are hand-written kernels too — no library GEMM on the path.
 
     ``tokens=T`` makes the plan padding-free: a packing kernel compacts the batch's
     non-pad tokens into T rows (positions and per-sequence offsets on the device), every
@@ -257,13 +230,9 @@ class BertEncoderPlan:
                  tokens: int | None = None, shared: BertBuffers | None = None):
         cfg = w.cfg
         self.w, self.B, self.S = w, batch, seq
-        if gemm is None:
-            gemm = "blas" if w.word.device.type == "cuda" else "mfma"
-        if gemm not in ("blas", "mfma"):
-            raise ValueError("gemm must be 'blas' or 'mfma'")
-        self.gemm_impl = gemm
-        if gemm == "blas" and w.word.device.type == "cuda":
-            load_gemm_table()
+        if gemm not in (None, "mfma"):
+            raise ValueError("gemm must be 'mfma' (the hand-written MFMA GEMM)")
+        self.gemm_impl = "mfma"
         self.packed = tokens is not None
         T = tokens if self.packed else batch * seq
         self.T = T
@@ -314,32 +283,16 @@ class BertEncoderPlan:
     def _run(self):
         w = self.w
         self._embed()
-        if self.gemm_impl == "blas":
-            return self._run_blas()
         cfg = w.cfg
         for li, L in enumerate(w.layers):
-            K.gemm(self.x, L["qkv_w"], L["qkv_b"], out=self.qkv)
+            K.gemm_pp(self.x, L["qkv_w"], L["qkv_b"], out=self.qkv)
             if self.packed and li == len(w.layers) - 1:
                 return self._last_layer_cls(L)
             self._attention()
-            K.gemm(self.ctx, L["o_w"], L["o_b"], residual=self.x, out=self.y)
-            K.layernorm(self.y, L["ln1_g"], L["ln1_b"], eps=cfg.eps, out=self.x)
-            K.gemm(self.x, L["i_w"], L["i_b"], act="gelu", out=self.ffn)
-            K.gemm(self.ffn, L["f_w"], L["f_b"], residual=self.x, out=self.y)
-            K.layernorm(self.y, L["ln2_g"], L["ln2_b"], eps=cfg.eps, out=self.x)
-        self._pool()
-
-    def _run_blas(self):
-        w, cfg = self.w, self.w.cfg
-        for li, L in enumerate(w.layers):
-            torch.addmm(L["qkv_b16"], self.x, L["qkv_w"].t(), out=self.qkv)
-            if self.packed and li == len(w.layers) - 1:
-                return self._last_layer_cls(L)
-            self._attention()
-            torch.addmm(L["o_b16"], self.ctx, L["o_w"].t(), out=self.y)
+            K.gemm_pp(self.ctx, L["o_w"], L["o_b"], out=self.y)
             K.layernorm(self.y, L["ln1_g"], L["ln1_b"], residual=self.x, eps=cfg.eps, out=self.x2)
-            ffn = torch._addmm_activation(L["i_b16"], self.x2, L["i_w"].t(), use_gelu=True)
-            torch.addmm(L["f_b16"], ffn, L["f_w"].t(), out=self.y)
+            K.gemm_pp(self.x2, L["i_w"], L["i_b"], act="gelu", out=self.ffn)
+            K.gemm_pp(self.ffn, L["f_w"], L["f_b"], out=self.y)
             K.layernorm(self.y, L["ln2_g"], L["ln2_b"], residual=self.x2, eps=cfg.eps, out=self.x)
         self._pool()
 
@@ -347,20 +300,16 @@ class BertEncoderPlan:
         """Final layer of a packed classifier: only each sequence's first row reaches the
         pooler, so after the (all-token) QKV projection everything runs on B rows —
         first-token attention over the sequence's keys, then output projection, residual
-        LayerNorm, FFN and LayerNorm of those rows (the pooler input is unchanged)."""
+        LayerNorm, FFN and LayerNorm of those rows (the pooler input is unchanged).  The
+        B-row GEMMs run split-K through this buffer set's own workspace."""
         w, cfg = self.w, self.w.cfg
+        ws = self.bufs.ws
         K.cls_attention(self.qkv, self.cu, self.B, cfg.heads, out=self.c_ctx)
         torch.index_select(self.x, 0, self.cls_idx, out=self.c_x)  # the layer input = residual
-        if self.gemm_impl == "blas":
-            torch.addmm(L["o_b16"], self.c_ctx, L["o_w"].t(), out=self.c_y)
-            K.layernorm(self.c_y, L["ln1_g"], L["ln1_b"], residual=self.c_x, eps=cfg.eps, out=self.c_x2)
-            ffn = torch._addmm_activation(L["i_b16"], self.c_x2, L["i_w"].t(), use_gelu=True)
-            torch.addmm(L["f_b16"], ffn, L["f_w"].t(), out=self.c_y)
-        else:
-            K.gemm(self.c_ctx, L["o_w"], L["o_b"], residual=self.c_x, out=self.c_y)
-            K.layernorm(self.c_y, L["ln1_g"], L["ln1_b"], eps=cfg.eps, out=self.c_x2)
-            K.gemm(self.c_x2, L["i_w"], L["i_b"], act="gelu", out=self.c_ffn)
-            K.gemm(self.c_ffn, L["f_w"], L["f_b"], out=self.c_y)
+        K.gemm_pp(self.c_ctx, L["o_w"], L["o_b"], out=self.c_y, ws=ws)
+        K.layernorm(self.c_y, L["ln1_g"], L["ln1_b"], residual=self.c_x, eps=cfg.eps, out=self.c_x2)
+        K.gemm_pp(self.c_x2, L["i_w"], L["i_b"], act="gelu", out=self.c_ffn, ws=ws)
+        K.gemm_pp(self.c_ffn, L["f_w"], L["f_b"], out=self.c_y, ws=ws)
         K.layernorm(self.c_y, L["ln2_g"], L["ln2_b"], residual=self.c_x2, eps=cfg.eps, out=self.cls_in)
         K.gemm(self.cls_in, w.pool_w, w.pool_b, act="tanh", out=self.pooled)
         K.gemm(self.pooled, w.cls_w, w.cls_b, out=self.logits)

@@ -314,6 +314,83 @@ def gemm(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = None, 
     return out
 
 
+# ------------------------------------------------------------------------------ gemm_pp
+_PP_KTILE_US = 1.5    # one 256x256x64 K step of one workgroup (measured: 1.39 PF at 8192^3)
+_PP_SPLIT_BW = 5.0e6  # bytes per microsecond of the fp32 partial round trip (write + read)
+
+
+def gemm_pp_splits(M: int, N: int, K: int, num_cu: int = 256) -> int:
+    """Split-K factor for ``gemm_pp`` from a small cost model: waves of 256x256 tiles times
+    K steps, plus the fp32 partial slices written and re-read by the reduction and one
+    extra launch.  Splits only when that wins by >10 % (small-M heads, few-tile shapes)."""
+    tiles = -(-M // 256) * -(-N // 256)
+    nk = K // 64
+    best_s, best_t = 1, -(-tiles // num_cu) * nk * _PP_KTILE_US
+    for s in range(2, min(16, nk) + 1):
+        per = -(-nk // s)
+        se = -(-nk // per)
+        t = -(-tiles * se // num_cu) * per * _PP_KTILE_US + 2.0 * se * M * N * 4 / _PP_SPLIT_BW + 2.0
+        if t < 0.9 * best_t:
+            best_s, best_t = se, t
+    return best_s
+
+
+def gemm_pp(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = None,
+            residual: torch.Tensor | None = None, act=None, out: torch.Tensor | None = None,
+            splits: int | None = None, out_col: int = 0, ws: torch.Tensor | None = None) -> torch.Tensor:
+    """``act(x[M,K] @ w[N,K]^T + bias (+ residual))`` on the ping-pong 256x256 MFMA kernel
+    (``kernels/gemm_pp.hip``).  ``out`` may be wider than N (``out_col`` = first column:
+    concat-by-stride-write).  ``splits`` > 1 runs split-K (None: cost model) through the
+    fp32 workspace ``ws`` (>= splits*M*N floats); without one a temporary is allocated per
+    call — stream-ordered, and inside hipGraph capture it comes from the graph's pool."""
+    a = act_code(act)
+    lead = x.shape[:-1]
+    K = x.shape[-1]
+    N, K2 = w_nk.shape
+    if K != K2:
+        raise ValueError(f"gemm_pp: K mismatch {K} vs {K2}")
+    x2 = x.reshape(-1, K)
+    M = x2.shape[0]
+    if out is None:
+        out = torch.empty((*lead, N), dtype=x.dtype if x.is_cuda else torch.float32, device=x.device)
+    ldy = out.shape[-1]
+    out2 = out.reshape(-1, ldy)
+    if out2.shape[0] != M or out_col + N > ldy:
+        raise ValueError("gemm_pp: output shape mismatch")
+    if residual is not None and residual.numel() != M * N:
+        raise ValueError("gemm_pp: residual shape mismatch")
+    if x.is_cuda:
+        if K % 64 or N % 8 or ldy % 8 or out_col % 8:
+            raise ValueError("gemm_pp: needs K % 64 == 0 and N, ldy, out_col % 8 == 0")
+        _check(x2, "x", device=x.device)
+        _check(w_nk, "w", device=x.device)
+        _check(out2, "out", device=x.device)
+        if bias is not None:
+            _check(bias, "bias", torch.float32, x.device)
+        if residual is not None:
+            _check(residual, "residual", device=x.device)
+        if splits is None:
+            splits = gemm_pp_splits(M, N, K)
+        splits = _hip().gemm_pp_splits(K, splits)
+        if splits > 1:
+            if ws is None:
+                ws = torch.empty(splits * M * N, dtype=torch.float32, device=x.device)
+            elif ws.dtype != torch.float32 or ws.device != x.device or ws.numel() < splits * M * N:
+                raise ValueError(f"gemm_pp: workspace needs {splits * M * N} fp32 elements on {x.device}")
+        else:
+            ws = None
+        _hip().gemm_pp(x2.data_ptr(), w_nk.data_ptr(), _ptr(bias), _ptr(residual), out2.data_ptr(), M, N, K, K, K,
+                       ldy, out_col, N, a, splits, _ptr(ws), _stream())
+        return out
+    y = x2.float() @ w_nk.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    if residual is not None:
+        y = y + residual.reshape(M, N).float()
+    out2[:, out_col:out_col + N] = _apply_act_ref(y, a).to(out.dtype)
+    return out
+
+
 # ------------------------------------------------------------------------------ preprocess
 def preprocess_images(images_u8: torch.Tensor, out_hw=(224, 224), mean=(117.0, 117.0, 117.0),
                       std=(1.0, 1.0, 1.0), align_corners=False, half_pixel_centers=False,

@@ -306,6 +306,11 @@ class _OpTask(_Task):
             while True:
                 if cancel.is_set():
                     raise JobCancelled()
+                if not replay and finished >= channels:
+                    # checked at the top of every iteration: the last EndOfInput may have
+                    # completed an alignment whose blocked records were replayed since
+                    op.end_input()
+                    break
                 if replay:
                     ch, elem = replay.popleft()
                 else:
@@ -317,7 +322,9 @@ class _OpTask(_Task):
                         self.writer.flush()
                         op.on_idle(time.time())
                         continue
-                if aligning is not None and ch in arrived and not isinstance(elem, EndOfInput):
+                if aligning is not None and ch in arrived:
+                    # a channel past its barrier is blocked until the alignment completes,
+                    # its EndOfInput included (so it is processed after its records)
                     blocked_buf[ch].append((ch, elem))
                     continue
                 if isinstance(elem, RecordBuffer):
@@ -356,9 +363,6 @@ class _OpTask(_Task):
                             replay.extend(blocked_buf[c])
                             blocked_buf[c].clear()
                         arrived = set()
-                    if finished >= channels and not replay:
-                        op.end_input()
-                        break
                 op.on_idle(time.time())
         finally:
             op.close()
