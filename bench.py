@@ -250,10 +250,7 @@ def main():
             "host_ms_per_batch": {k: round(v * 1e3 / max(1, runner.batches), 3) for k, v in runner.host_s.items()},
         }
         print(json.dumps(out), flush=True)
-    if comm.is_dist():
-        import torch.distributed as dist
-
-        dist.destroy_process_group()
+    comm.destroy()
 
 
 def run_widedeep(args, dev, rank, ws):

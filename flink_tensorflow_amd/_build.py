@@ -1,11 +1,14 @@
-"""In-tree build of the two native extensions.
+"""In-tree build of the three native extensions.
 
 * ``_native``  — host C++ runtime (csrc/*.cpp): wire codecs, protobuf scanning, Example
   parsing, STRING tensors, CRC32C/SSTable bundle I/O, staging gather.  Built with g++.
 * ``_hip``     — CDNA4 (gfx950) HIP kernels (kernels/*.hip) + their pybind11 launchers.
   Built with ``hipcc --offload-arch=gfx950``; cross-compiles without a GPU.
+* ``_rccl``    — direct RCCL C-API binding (csrc_rccl/rccl.cpp): communicator init from a
+  ncclUniqueId, broadcast / all-reduce / all-gather / reduce-scatter on HIP streams.
+  Host-only code built with hipcc, linked against ``librccl.so.1``.
 
-Both land next to this file (``setup.py build_ext --inplace`` semantics) so that the
+All land next to this file (``setup.py build_ext --inplace`` semantics) so that the
 ``.so`` travels with a repo snapshot to the GPU box.  A content hash of the sources and
 flags is stored beside each library; a rebuild happens only when it changes.
 """
@@ -21,6 +24,7 @@ from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
+CSRC_RCCL = PKG / "csrc_rccl"
 KERNELS = PKG / "kernels"
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 HIP_ARCH = os.environ.get("FTM_HIP_ARCH", "gfx950")
@@ -154,9 +158,34 @@ def build_hip(force: bool = False, verbose: bool = False, jobs: int | None = Non
     return lib
 
 
+def rccl_lib_path() -> Path:
+    return PKG / f"_rccl{EXT_SUFFIX}"
+
+
+def build_rccl(force: bool = False, verbose: bool = False) -> Path:
+    srcs = sorted(CSRC_RCCL.glob("*.cpp"))
+    flags = ["-O2", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-D__HIP_PLATFORM_AMD__",
+             f"-I{ROCM}/include", f"-L{ROCM}/lib", "-lrccl", "-lamdhip64"]
+    lib = rccl_lib_path()
+    dig = _digest(srcs, flags)
+    if not force and _up_to_date(lib, dig):
+        return lib
+    hipcc = os.environ.get("HIPCC", f"{ROCM}/bin/hipcc")
+    tmp = lib.with_name(lib.name + ".tmp")
+    # -x c++ : host-only translation unit (no device code, no offload bundle)
+    cmd = [hipcc, "-x", "c++", *_pybind_includes(), *map(str, srcs), *flags, "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    _run(cmd)
+    os.replace(tmp, lib)
+    _stamp(lib, dig)
+    return lib
+
+
 def build_all(force: bool = False, verbose: bool = False) -> None:
     build_native(force=force, verbose=verbose)
     build_hip(force=force, verbose=verbose)
+    build_rccl(force=force, verbose=verbose)
 
 
 if __name__ == "__main__":
@@ -165,9 +194,11 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
-    ap.add_argument("what", nargs="?", default="all", choices=["all", "native", "hip"])
+    ap.add_argument("what", nargs="?", default="all", choices=["all", "native", "hip", "rccl"])
     a = ap.parse_args()
     if a.what in ("all", "native"):
         print(build_native(a.force, a.verbose))
     if a.what in ("all", "hip"):
         print(build_hip(a.force, a.verbose))
+    if a.what in ("all", "rccl"):
+        print(build_rccl(a.force, a.verbose))

@@ -69,6 +69,29 @@ def hip(required: bool = True):
     return _hip_mod
 
 
+_rccl_mod = None
+
+
+def rccl():
+    """Returns the `_rccl` RCCL binding (never a fallback: collectives have no other
+    product path).  Imports torch first so the binding resolves ``librccl.so.1`` to the
+    RCCL torch already mapped (one RCCL instance per process)."""
+    global _rccl_mod
+    if _rccl_mod is not None:
+        return _rccl_mod
+    with _lock:
+        if _rccl_mod is None:
+            import torch  # noqa: F401
+
+            if os.environ.get("FTM_AUTOBUILD_HIP") == "1":
+                _build.build_rccl()
+            if not _build.rccl_lib_path().exists():
+                raise ImportError(f"RCCL binding {_build.rccl_lib_path()} is missing: run "
+                                  "`python -m flink_tensorflow_amd._build rccl` (or __graft_entry__.build())")
+            _rccl_mod = importlib.import_module("flink_tensorflow_amd._rccl")
+    return _rccl_mod
+
+
 def hip_available() -> bool:
     """True when a GPU is visible AND the kernel library imports."""
     import torch

@@ -7,6 +7,9 @@ Layout for a checkpoint ``prefix``::
     prefix.data-00000-of-0000N      concatenated little-endian tensor payloads
 
 STRING tensors are stored TF-style: ``varint64 len[i]… | u32 masked_crc(lengths) | bytes…``.
+Their entry checksum is NOT a CRC of that raw payload: like TF's ``WriteStringTensor`` it
+covers each length as a fixed-width little-endian integer (u32, or u64 above 4 GiB), then
+the 4 stored length-checksum bytes, then the string bytes (``_string_crc``).
 The table build/parse and CRC32C run in C++ (``_native.sstable_*``, SSE4.2 ``crc32``).
 The reference reaches this format only through the graph's saver subgraph
 (``LIB/io/Saver.scala:55-89``); we implement it natively so both the
@@ -45,15 +48,33 @@ def index_filename(prefix: str) -> str:
     return f"{prefix}.index"
 
 
-def _tensor_bytes(t) -> bytes:
+def _fixed_lengths(lens) -> bytes:
+    return b"".join(struct.pack("<I", n) if n <= 0xFFFFFFFF else struct.pack("<Q", n) for n in lens)
+
+
+def _string_crc(lens, cks: bytes, elems) -> int:
+    """Unmasked entry CRC of a STRING tensor: fixed-width lengths, the stored length
+    checksum, then every element's bytes."""
+    nat = _ext.native()
+    crc = nat.crc32c(_fixed_lengths(lens))
+    crc = nat.crc32c(cks, crc)
+    for e in elems:
+        crc = nat.crc32c(e, crc)
+    return crc
+
+
+def _tensor_bytes(t) -> tuple[bytes, int]:
+    """(payload, masked entry crc32c)."""
+    nat = _ext.native()
     if isinstance(t, StringTensor):
-        elems = list(t.array.reshape(-1))
-        lens = b"".join(encode_varint(len(e)) for e in elems)
-        nat = _ext.native()
-        cks = struct.pack("<I", _mask(nat.crc32c(lens)))
-        return lens + cks + b"".join(elems)
+        elems = [bytes(e) for e in t.array.reshape(-1)]
+        lens = [len(e) for e in elems]
+        cks = struct.pack("<I", _mask(nat.crc32c(_fixed_lengths(lens))))
+        payload = b"".join(encode_varint(n) for n in lens) + cks + b"".join(elems)
+        return payload, _mask(_string_crc(lens, cks, elems))
     t = t.detach().to("cpu").contiguous()
-    return t.reshape(-1).view(torch.uint8).numpy().tobytes() if t.numel() else b""
+    payload = t.reshape(-1).view(torch.uint8).numpy().tobytes() if t.numel() else b""
+    return payload, _mask(nat.crc32c(payload))
 
 
 class BundleWriter:
@@ -74,11 +95,9 @@ class BundleWriter:
     def add(self, name: str, tensor) -> None:
         if name in self.entries:
             raise ValueError(f"duplicate tensor {name!r} in bundle")
-        payload = _tensor_bytes(tensor)
-        nat = _ext.native()
+        payload, crc = _tensor_bytes(tensor)
         e = BundleEntryProto(dtype=int(dtype_of(tensor)), shape=TensorShapeProto.of(tensor.shape),
-                             shard_id=self.shard_id, offset=self._off, size=len(payload),
-                             crc32c=_mask(nat.crc32c(payload)))
+                             shard_id=self.shard_id, offset=self._off, size=len(payload), crc32c=crc)
         self._f.write(payload)
         self._off += len(payload)
         self.entries[name] = e
@@ -158,8 +177,6 @@ class BundleReader:
         payload = f.read(e.size)
         if len(payload) != e.size:
             raise DataLossError(f"truncated data for {name!r}")
-        if self.verify and _mask(_ext.native().crc32c(payload)) != e.crc32c:
-            raise DataLossError(f"checksum mismatch for tensor {name!r} in {self.prefix}")
         dt = DataType(e.dtype)
         shape = tuple(e.shape.as_list() or [])
         if dt == DataType.STRING:
@@ -169,12 +186,20 @@ class BundleReader:
             for _ in range(n):
                 ln, off = decode_varint(payload, off)
                 lens.append(ln)
-            off += 4  # masked crc of the length block
+            cks = payload[off:off + 4]
+            off += 4
             vals = []
             for ln in lens:
                 vals.append(payload[off:off + ln])
                 off += ln
+            if self.verify:
+                if struct.unpack("<I", cks)[0] != _mask(_ext.native().crc32c(_fixed_lengths(lens))):
+                    raise DataLossError(f"length checksum mismatch for string tensor {name!r} in {self.prefix}")
+                if _mask(_string_crc(lens, cks, vals)) != e.crc32c:
+                    raise DataLossError(f"checksum mismatch for tensor {name!r} in {self.prefix}")
             return StringTensor(vals, shape)
+        if self.verify and _mask(_ext.native().crc32c(payload)) != e.crc32c:
+            raise DataLossError(f"checksum mismatch for tensor {name!r} in {self.prefix}")
         t = torch.from_numpy(np.frombuffer(payload, dtype=np.uint8).copy()).view(dt.torch).reshape(shape)
         return t.to(device) if device is not None else t
 

@@ -65,6 +65,20 @@ class RichModel(Model):
         self.close()
 
 
+class CheckpointedModel(abc.ABC):
+    """Model state that participates in checkpoints (repartitionable operator state) —
+    ``LIB/streaming/models/CheckpointedModel.scala:24-46``.  ``ctx`` is the runtime's
+    ``SnapshotContext`` / ``InitializationContext`` (``runtime/functions.py``)."""
+
+    @abc.abstractmethod
+    def snapshot_state(self, ctx) -> None:
+        ...
+
+    @abc.abstractmethod
+    def initialize_state(self, ctx) -> None:
+        ...
+
+
 # ------------------------------------------------------------------ methods
 class GraphMethod(abc.ABC):
     """Typed method: ``name`` + ``inputs(x) -> {signature key: tensor}`` +

@@ -9,7 +9,13 @@
   dirs to a local temp dir (deleted at exit), imports the graph, restores variables from
   the TensorBundle V2 checkpoint through the SaverDef restore op, resolves assets and runs
   the ``main_op``/``legacy_init_op``.
-* ``TensorFlowModel`` — ``LIB/models/savedmodel/TensorFlowModel.scala:12-61``.
+* ``TensorFlowModel`` — ``LIB/models/savedmodel/TensorFlowModel.scala:12-61``.  It is a
+  ``CheckpointedModel`` (``LIB/streaming/models/CheckpointedModel.scala:24-46``, wired as
+  SURVEY §3.5 / F9 designs it): on a checkpoint barrier the session's variables are
+  written D2H as a TensorBundle V2 (the ``Saver`` format, ``LIB/io/Saver.scala:55-89``)
+  under ``chk-N/models/savedmodel-<subtask>/``; on restore they are read back into the
+  session, so variables a streaming job mutates (e.g. ``Assign`` driven by a co-process
+  update stream) survive a restart.
 """
 from __future__ import annotations
 
@@ -24,7 +30,9 @@ from ..graph.session import Session
 from ..proto.messages import AssetFileDef, MetaGraphDef, SavedModel, SignatureDef
 from ..types.tensor import StringTensor
 from ..utils import fs
-from .core import ModelFunction, RichModel, default_device
+from .core import CheckpointedModel, ModelFunction, RichModel, default_device
+
+STATE_NAME = "savedmodel"  # checkpoint sub-directory of TensorFlowModel variables
 
 
 class SignatureConstants:
@@ -142,7 +150,7 @@ class DefaultSavedModelLoader(SavedModelLoader):
         return load_bundle(local, self.tags, device=device)
 
 
-class TensorFlowModel(RichModel):
+class TensorFlowModel(RichModel, CheckpointedModel):
     """A SavedModel-backed model.  Subclasses define ``loader``."""
 
     _TRANSIENT = ("_bundle",)
@@ -150,6 +158,7 @@ class TensorFlowModel(RichModel):
     def __init__(self, device=None):
         self.device = device
         self._bundle: SavedModelBundle | None = None
+        self._pending_restore: str | None = None
 
     @property
     @abc.abstractmethod
@@ -168,6 +177,9 @@ class TensorFlowModel(RichModel):
             raise RuntimeError("model already open")  # checkState(bundle == null)
         dev = self.device if self.device is not None else default_device()
         self._bundle = self.loader.load(device=dev)
+        if self._pending_restore is not None:  # initialize_state ran before open()
+            prefix, self._pending_restore = self._pending_restore, None
+            self.restore_variables(prefix)
 
     def close(self) -> None:
         if self._bundle is not None:
@@ -196,6 +208,35 @@ class TensorFlowModel(RichModel):
     @staticmethod
     def load(path: str, *tags: str) -> DefaultSavedModelLoader:
         return DefaultSavedModelLoader(path, tags or (TAG_SERVE,))
+
+    # ---- CheckpointedModel: session variables <-> bundle V2 in the checkpoint
+    def save_variables(self, prefix: str) -> str:
+        from ..io.saver import VariableSaver
+
+        return VariableSaver().save(self.session(), prefix)
+
+    def restore_variables(self, prefix: str) -> None:
+        from ..io.saver import VariableSaver
+
+        VariableSaver().restore(self.session(), prefix)
+
+    def snapshot_state(self, ctx) -> None:
+        from ..runtime.model_functions import model_state_dir
+
+        d = model_state_dir(ctx, STATE_NAME)
+        if d is not None and self.is_open and self.session().variables:
+            self.save_variables(os.path.join(d, "variables"))
+
+    def initialize_state(self, ctx) -> None:
+        if not ctx.is_restored() or ctx.checkpoint_dir is None:
+            return
+        prefix = os.path.join(ctx.checkpoint_dir, "models", f"{STATE_NAME}-{ctx.subtask_index}", "variables")
+        if not os.path.exists(prefix + ".index"):
+            return
+        if self.is_open:
+            self.restore_variables(prefix)
+        else:
+            self._pending_restore = prefix
 
 
 class SavedModel_(TensorFlowModel):

@@ -104,13 +104,13 @@ def _sparse_sync(uids: torch.Tensor, rows: torch.Tensor):
     exchange is two fixed-size all-gathers with no size round trip or host sync."""
     if not comm.is_dist():
         return uids, rows
-    import torch.distributed as dist
-
-    ws = dist.get_world_size()
+    c = comm.get()
+    ws = c.size
     gu = torch.empty((ws * uids.numel(),), dtype=uids.dtype, device=uids.device)
     gr = torch.empty((ws * rows.shape[0], rows.shape[1]), dtype=rows.dtype, device=rows.device)
-    dist.all_gather_into_tensor(gu, uids.contiguous())
-    dist.all_gather_into_tensor(gr, rows.contiguous())
+    with c.group():  # both gathers in one RCCL launch
+        c.all_gather(gu, uids.contiguous())
+        c.all_gather(gr, rows.contiguous())
     return gu, gr  # -1 ids are dropped by the merge
 
 

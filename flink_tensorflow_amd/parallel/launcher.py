@@ -2,8 +2,9 @@
 (SURVEY §5.3).
 
 The reference delegates failure handling to Flink's restart strategies.  Here the driver
-process spawns one worker per rank, each joining the collective group (``nccl`` = RCCL on
-a GPU node, ``gloo`` on the host), and supervises them:
+process spawns one worker per rank, each creating the job's RCCL communicator on its GPU
+(``comm.init_distributed``; CPU tests inject the loopback ``parallel.fake`` communicator),
+and supervises them:
 
 * **exit detection** — a worker that dies (HIP error → non-zero exit, abort, kill) fails
   the attempt;
@@ -12,7 +13,8 @@ a GPU node, ``gloo`` on the host), and supervises them:
   kernel never returns to Python, so progress beats are the signal);
 * **restart** — the whole group is torn down (the surviving ranks are killed by PID: a
   collective communicator cannot lose a member) and relaunched with ``attempt + 1`` on a
-  fresh rendezvous port, up to ``max_restarts`` times.  The worker function receives the
+  fresh rendezvous port, up to ``max_restarts`` times; a worker that fails aborts its RCCL
+communicator (no waiting on dead peers).  The worker function receives the
   attempt number and resumes from its latest checkpoint (e.g. a streaming job with
   ``restore_from_latest``); the communicator is re-created by the new processes.
 
@@ -51,23 +53,24 @@ def heartbeat(note: str = "") -> None:
             pass
 
 
-def _worker(rank: int, world: int, port: int, attempt: int, backend: str, fn, args, q, env):
+def _worker(rank: int, world: int, port: int, attempt: int, communicator, fn, args, q, env):
     global _BEAT_Q, _RANK
     _BEAT_Q, _RANK = q, rank
     os.environ.update(env)
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), FTM_ATTEMPT=str(attempt))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    try:
-        from . import comm
+    from . import comm
 
-        comm.init_distributed(backend=backend)
+    try:
+        comm.init_distributed(communicator=communicator)
         heartbeat("init")
         res = fn(rank, world, attempt, *args)
         q.put(("done", rank, time.time(), res))
         comm.destroy()
     except BaseException as e:  # noqa: BLE001
         q.put(("error", rank, time.time(), f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
+        comm.destroy(abort=True)
         raise SystemExit(1)
 
 
@@ -82,16 +85,17 @@ class LaunchReport:
     failures: list = field(default_factory=list)
 
 
-def launch(fn: Callable[..., Any], nprocs: int, args: tuple = (), backend: str = "gloo", max_restarts: int = 0,
-           heartbeat_timeout: float | None = None, timeout: float | None = None, env: dict | None = None,
-           restart_delay_s: float = 0.0) -> LaunchReport:
-    """Runs ``fn(rank, world, attempt, *args)`` in ``nprocs`` supervised processes."""
+def launch(fn: Callable[..., Any], nprocs: int, args: tuple = (), communicator: type | None = None,
+           max_restarts: int = 0, heartbeat_timeout: float | None = None, timeout: float | None = None,
+           env: dict | None = None, restart_delay_s: float = 0.0) -> LaunchReport:
+    """Runs ``fn(rank, world, attempt, *args)`` in ``nprocs`` supervised processes.
+    ``communicator`` (a picklable ``comm.Communicator`` class) replaces RCCL — tests only."""
     ctx = mp.get_context("spawn")
     failures = []
     for attempt in range(max_restarts + 1):
         q = ctx.Queue()
         port = _free_port()
-        procs = [ctx.Process(target=_worker, args=(r, nprocs, port, attempt, backend, fn, args, q, env or {}),
+        procs = [ctx.Process(target=_worker, args=(r, nprocs, port, attempt, communicator, fn, args, q, env or {}),
                              daemon=False) for r in range(nprocs)]
         for p in procs:
             p.start()
@@ -110,9 +114,23 @@ def launch(fn: Callable[..., Any], nprocs: int, args: tuple = (), backend: str =
             except queue.Empty:
                 pass
             now = time.time()
-            for r, p in enumerate(procs):
-                if r not in results and p.exitcode is not None and p.exitcode != 0:
-                    reason = reason or f"rank {r} exited with code {p.exitcode}"
+            exited = [r for r, p in enumerate(procs) if r not in results and p.exitcode is not None]
+            if exited and reason is None:
+                # a rank may have posted 'done' just before exiting: drain once more, then any
+                # exited rank without a result failed — whatever its exit code (sys.exit(0)
+                # inside fn, os._exit) — or the attempt would wait forever
+                try:
+                    while True:
+                        kind, rank, ts, payload = q.get(timeout=0.05)
+                        if kind == "done":
+                            results[rank] = payload
+                        elif kind == "error":
+                            reason = f"rank {rank} raised: {payload}"
+                except queue.Empty:
+                    pass
+                for r in exited:
+                    if r not in results:
+                        reason = reason or f"rank {r} exited with code {procs[r].exitcode} without a result"
             if heartbeat_timeout is not None:
                 stale = [r for r in range(nprocs) if r not in results and now - last[r] > heartbeat_timeout]
                 if stale:

@@ -104,9 +104,14 @@ class CheckpointCoordinator:
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
         self.completed_ids: list[int] = []
+        # state at end-of-input of tasks that finished (sources: their final offsets): part of
+        # every later checkpoint, so a restore does not replay a finished source's records
+        # into operators whose state already contains them
+        self.final_states: dict[tuple[str, int], dict] = {}
 
     def start(self, expected_tasks: set[tuple[str, int]]):
         self.expected = set(expected_tasks)
+        self.final_states = {}
         self._thread = threading.Thread(target=self._loop, name="checkpoint-coordinator", daemon=True)
         self._thread.start()
 
@@ -137,9 +142,11 @@ class CheckpointCoordinator:
             p[task] = state
             self._maybe_complete(cid)
 
-    def task_finished(self, task: tuple[str, int]):
+    def task_finished(self, task: tuple[str, int], final_state: dict | None = None):
         with self.lock:
             self.expected.discard(task)
+            if final_state is not None:
+                self.final_states[task] = final_state
             for cid in list(self.pending):
                 self._maybe_complete(cid)
 
@@ -148,6 +155,7 @@ class CheckpointCoordinator:
         if self.expected and not self.expected.issubset(p.keys()):
             return
         del self.pending[cid]
+        p = {**{t: st for t, st in self.final_states.items() if t not in p}, **p}
         self.storage.write(cid, p, {"tasks": sorted(f"{u}/{s}" for u, s in p)})
         self.completed_ids.append(cid)
         self.executor.notify_complete(cid)

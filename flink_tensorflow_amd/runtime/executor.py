@@ -237,7 +237,7 @@ class _Task:
             # or cancelled task must not let an in-flight checkpoint complete without its
             # state (the restart would restore the sources' offsets but lose this task's)
             if done and self.job.coordinator is not None:
-                self.job.coordinator.task_finished((self.uid, self.subtask))
+                self.job.coordinator.task_finished((self.uid, self.subtask), getattr(self, "final_state", None))
 
     def run(self):
         raise NotImplementedError
@@ -269,6 +269,8 @@ class _SourceTask(_Task):
             fn.run(sctx)
             with sctx.checkpoint_lock:
                 self.check_trigger()
+                # end-of-input offsets: later checkpoints restore this source as exhausted
+                self.final_state = self.op.snapshot_state(-1, None)
         finally:
             self.op.close()
         self.writer.emit(Watermark(float("inf")))

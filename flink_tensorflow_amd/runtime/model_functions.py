@@ -6,8 +6,10 @@
   throws ``MatchError``, B6).
 * ``CheckpointedModel`` — ``LIB/streaming/models/CheckpointedModel.scala:24-46``;
   ``CheckpointedModelAwareFunction`` connects it to the checkpoint barriers with a
-  **no-op default** for stateless models (B6).  ``TensorFlowModel`` variables and the
-  online-training models implement it (variables written as TensorBundle V2).
+  **no-op default** for stateless models (B6).  ``TensorFlowModel``
+  (``models/savedmodel.py``: session variables) and the online-training
+  ``WideDeepTrainer`` (``models/zoo/wide_deep.py``: weights + optimizer state) implement
+  it; both write TensorBundle V2 under ``chk-N/models/``.
 * ``Model{Map,FlatMap,Process,CoProcess,Window,AllWindow}Function`` —
   ``Abstract*Function`` of ``LIB/common/functions`` and ``LIB/streaming/functions``.
 * ``BatchedModelOperator`` — the micro-batching operator behind
@@ -22,21 +24,11 @@ import time
 
 import numpy as np
 
-from ..models.core import RichModel
+from ..models.core import CheckpointedModel, RichModel  # noqa: F401  (re-exported)
 from . import functions as F
 from .operators import Collector, Operator, Record
 
 
-class CheckpointedModel(abc.ABC):
-    """Model state that participates in checkpoints (repartitionable operator state)."""
-
-    @abc.abstractmethod
-    def snapshot_state(self, ctx: F.SnapshotContext) -> None:
-        ...
-
-    @abc.abstractmethod
-    def initialize_state(self, ctx: F.InitializationContext) -> None:
-        ...
 
 
 def open_model(model, device=None):

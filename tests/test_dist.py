@@ -1,4 +1,5 @@
-"""Collective layer on CPU processes (gloo, world_size 2): weight broadcast, bucketed
+"""Collective layer on CPU processes (loopback fake communicator, world_size 2 — no RCCL,
+no gloo): weight broadcast, bucketed
 overlapped gradient all-reduce, metric reduction, and a distributed stream whose sources
 are partitioned by rank (the one-process-per-GPU DP layout, rehearsed on the host)."""
 import os
@@ -7,6 +8,7 @@ import socket
 import pytest
 import torch
 import torch.multiprocessing as mp
+from _helpers import torchrun_smoke as _torchrun
 
 
 def _free_port():
@@ -22,14 +24,13 @@ def _worker(rank, world, port, fn, q):
                       MASTER_PORT=str(port))
     try:
         from flink_tensorflow_amd.parallel import comm
+        from flink_tensorflow_amd.parallel.fake import FakeCommunicator
 
-        comm.init_distributed(backend="gloo")
+        comm.init_distributed(communicator=FakeCommunicator)
         # tensors cross the queue as numpy: torch's fd-sharing pickler needs the child alive
         # until the parent unpickles, which races with the child's exit
         q.put((rank, _to_numpy(fn(rank, world))))
-        import torch.distributed as dist
-
-        dist.destroy_process_group()
+        comm.destroy()
     except Exception as e:  # noqa: BLE001
         import traceback
 
@@ -232,3 +233,12 @@ def test_bucket_histogram_percentiles_match_numpy():
     hb = histogram_buckets(h)
     assert hb.count == pytest.approx(20000, rel=0.01)
     assert abs(hb.percentile(50) - np.percentile(v, 50)) / np.percentile(v, 50) < 0.05
+
+
+def test_torchrun_agent_store_rendezvous():
+    """bench.py's launch path: ``torch.distributed.run`` workers find the job's store (the
+    agent's, on MASTER_PORT) and exchange through the communicator."""
+    out = _torchrun(2, "--fake")
+    assert [o["rank"] for o in out] == [0, 1]
+    for o in out:
+        assert o["bcast"] == [1.0] * 4 and o["sum"] == [3.0] * 3 and o["objs"] == [0, 1]

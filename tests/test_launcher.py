@@ -1,20 +1,20 @@
 """Supervised launcher: a crashed rank and a hung rank are detected, the
 whole group is restarted, and the job resumes from its checkpoint on the next attempt
-(gloo, world size 2, CPU)."""
+(loopback fake communicator, world size 2, CPU)."""
 import json
 import os
 
 import pytest
 import torch
 
+from flink_tensorflow_amd.parallel.fake import FakeCommunicator
 from flink_tensorflow_amd.parallel.launcher import WorkerFailure, launch
 
 
 def _train(rank, world, attempt, ckpt_dir, fault):
     """10 'steps' of an all-reduced counter with a checkpoint after every step; the fault
     fires once, on attempt 0 at step 4 on rank 1."""
-    import torch.distributed as dist
-
+    from flink_tensorflow_amd.parallel import comm
     from flink_tensorflow_amd.parallel.launcher import heartbeat
 
     path = os.path.join(ckpt_dir, f"rank{rank}.json")
@@ -33,7 +33,7 @@ def _train(rank, world, attempt, ckpt_dir, fault):
 
                 time.sleep(600)
         t = torch.tensor([float(rank + 1)])
-        dist.all_reduce(t)
+        comm.get().all_reduce(t)
         total += float(t)
         step += 1
         with open(path, "w") as f:
@@ -44,7 +44,7 @@ def _train(rank, world, attempt, ckpt_dir, fault):
 
 @pytest.mark.parametrize("fault", ["crash", "hang"])
 def test_restart_after_failure(tmp_path, fault):
-    rep = launch(_train, 2, args=(str(tmp_path), fault), backend="gloo", max_restarts=1, heartbeat_timeout=5.0,
+    rep = launch(_train, 2, args=(str(tmp_path), fault), communicator=FakeCommunicator, max_restarts=1, heartbeat_timeout=5.0,
                  timeout=120)
     assert rep.attempts == 2 and len(rep.failures) == 1
     assert ("exited with code 3" in rep.failures[0]) if fault == "crash" else ("missed heartbeats" in rep.failures[0])
@@ -55,8 +55,19 @@ def test_restart_after_failure(tmp_path, fault):
 
 def test_gives_up_after_max_restarts(tmp_path):
     with pytest.raises(WorkerFailure):
-        launch(_boom, 2, backend="gloo", max_restarts=1, timeout=60)
+        launch(_boom, 2, communicator=FakeCommunicator, max_restarts=1, timeout=60)
 
 
 def _boom(rank, world, attempt):
     raise RuntimeError("boom")
+
+
+def _silent_exit(rank, world, attempt):
+    if rank == 1:
+        os._exit(0)  # exits "successfully" without posting a result
+    return rank
+
+
+def test_clean_exit_without_result_is_a_failure():
+    with pytest.raises(WorkerFailure, match="without a result"):
+        launch(_silent_exit, 2, communicator=FakeCommunicator, max_restarts=0, timeout=60)

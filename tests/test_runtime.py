@@ -237,3 +237,45 @@ def test_batched_model_operator(half_plus_two):
     assert len(out) == 100 and sorted(set(out)) == [2.0, 2.5, 3.0, 3.5]
     hist = [m for k, m in res.metrics.items() if k.startswith("batched-model")][0]["histograms"]["batch_size"]
     assert hist["max"] == 16
+
+
+class _OnlineA(ModelCoProcessFunction):
+    """Data stream: y = a*x + b through the regress signature.  Update stream: assigns a
+    new value to the SavedModel variable ``a`` with the graph's own ``a/Assign`` op."""
+
+    def process_element1(self, x, ctx, out):
+        y = self.model.regress_x_to_y([example(("x", feature(float(x))))]).item()
+        out.collect((x, y))
+
+    def process_element2(self, a, ctx, out):
+        self.model.session().run(targets=["a/Assign"], feed_dict={"a/initial_value:0": torch.tensor(a)})
+
+
+class _UncheckpointedHalfPlusTwo(HalfPlusTwo):
+    def snapshot_state(self, ctx):  # control: variables are NOT part of the checkpoint
+        pass
+
+
+@pytest.mark.parametrize("checkpointed", [True, False])
+def test_savedmodel_variables_survive_worker_kill(half_plus_two, tmp_path, checkpointed):
+    """TensorFlowModel is a CheckpointedModel (``CheckpointedModel.scala:24-46``):
+    an update stream assigns ``a = 3`` once; a worker process is killed mid-stream; after the
+    restart (the update record is not replayed — its source offset was checkpointed) the
+    late records are still computed with the restored ``a``.  The control run, whose model
+    does not snapshot its variables, falls back to the SavedModel's ``a = 0.5``."""
+    from flink_tensorflow_amd.runtime.sources import CollectionSource
+    from flink_tensorflow_amd.utils.fault import KillProcessAfter
+
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(1)
+    env.enable_checkpointing(0.05, str(tmp_path / "chk"))
+    env.set_restart_strategy(RestartStrategy.fixed_delay(2, 0.0))
+    data = env.add_source(CollectionSource(list(range(1, 201)), delay_s=0.004), "xs")
+    updates = env.add_source(CollectionSource([3.0]), "updates")
+    m = (HalfPlusTwo if checkpointed else _UncheckpointedHalfPlusTwo)(half_plus_two)
+    sink = data.map(KillProcessAfter(120)).run_in_processes().connect(updates).process(_OnlineA(m)).collect_into()
+    res = env.execute("online-a")
+    assert res.attempts == 1 and len(res.checkpoints) >= 1
+    late = {x: y for x, y in sink.results() if x >= 150}   # only computed after the restart
+    assert sorted(late) == list(range(150, 201))
+    a = 3.0 if checkpointed else 0.5
+    assert all(y == pytest.approx(a * x + 2.0) for x, y in late.items()), sorted(late.items())[:3]

@@ -64,6 +64,41 @@ def test_bundle_detects_corruption(tmp_path):
         bundle.BundleReader(p)
 
 
+def _py_crc32c(data: bytes, crc: int = 0) -> int:
+    """Bitwise CRC-32C (Castagnoli), independent of the native SSE4.2 implementation."""
+    crc ^= 0xFFFFFFFF
+    for b in data:
+        crc ^= b
+        for _ in range(8):
+            crc = (crc >> 1) ^ (0x82F63B78 if crc & 1 else 0)
+    return crc ^ 0xFFFFFFFF
+
+
+def _py_mask(crc: int) -> int:
+    return (((crc >> 15) | (crc << 17)) + 0xA282EAD8) & 0xFFFFFFFF
+
+
+def test_string_tensor_entry_crc_follows_tf_layout(tmp_path):
+    """Hand-built fixture of TF's ``WriteStringTensor`` layout: the entry CRC covers u32
+    lengths + the stored (masked) length checksum + bytes, not the varint payload."""
+    import struct
+
+    from flink_tensorflow_amd.types import StringTensor
+
+    elems = [b"hello", b"", b"x" * 200]
+    fixed = b"".join(struct.pack("<I", len(e)) for e in elems)
+    cks = struct.pack("<I", _py_mask(_py_crc32c(fixed)))
+    varints = bytes([5, 0]) + bytes([200 & 0x7F | 0x80, 200 >> 7])
+    want_payload = varints + cks + b"".join(elems)
+    want_crc = _py_mask(_py_crc32c(b"".join(elems), _py_crc32c(cks, _py_crc32c(fixed))))
+    p = str(tmp_path / "s")
+    bundle.save_tensors(p, {"s": StringTensor(elems, (3,))})
+    assert open(p + ".data-00000-of-00001", "rb").read() == want_payload
+    r = bundle.BundleReader(p)
+    assert r.entries["s"].crc32c == want_crc
+    assert r.read("s").tolist() == elems
+
+
 class HalfPlusTwo(TensorFlowModel):
     """``TST/.../ml/HalfPlusTwo.scala:14-28``."""
 
