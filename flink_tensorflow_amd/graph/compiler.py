@@ -1383,8 +1383,10 @@ class CompiledFunction:
             self._graph_obj = g
             self._head = self._head_feed_step()
             if self._head is not None:
+                # the two graphs of a plan never replay concurrently (one lane = one stream):
+                # the tail graph shares the full graph's private memory pool
                 gt = torch.cuda.CUDAGraph()
-                with tracing.graph_capture(gt):
+                with tracing.graph_capture(gt, pool=g.pool()):
                     for st in self.steps[1:]:
                         st.fn()
                 self._graph_tail = gt

@@ -38,6 +38,9 @@ class VarRef:
         if (cur is not None and isinstance(cur, torch.Tensor) and isinstance(value, torch.Tensor)
                 and cur.shape == value.shape and cur.dtype == value.dtype and cur.device == value.device):
             cur.copy_(value)  # in-place: keeps buffers captured by compiled plans valid
+            touch = getattr(self.session.variables, "touch", None)
+            if touch is not None:
+                touch()
             return cur
         v = value.clone() if isinstance(value, torch.Tensor) else value
         self.session.variables[self.name] = v

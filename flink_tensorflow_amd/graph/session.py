@@ -43,11 +43,26 @@ class Run:
         self.metadata = metadata
 
 
+class VariableStore(dict):
+    """A session's variables; ``version`` increases on every write, so compiled plans
+    (which fold variables into their weights) know when they went stale."""
+
+    version = 0
+
+    def __setitem__(self, k, v):
+        super().__setitem__(k, v)
+        self.version += 1
+
+    def touch(self) -> None:
+        """Records an in-place write (``copy_`` into an existing variable buffer)."""
+        self.version += 1
+
+
 class Session:
     def __init__(self, graph: Graph, device: str | torch.device | None = None):
         self.graph = graph
         self.device = torch.device(device) if device is not None else torch.device("cpu")
-        self.variables: dict[str, Any] = {}
+        self.variables: VariableStore = VariableStore()
         self._const_cache: dict = {}
         self._plans: dict = {}
         self._lock = threading.RLock()

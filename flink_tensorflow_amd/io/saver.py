@@ -64,5 +64,7 @@ class VariableSaver(Saver):
                 cur = session.variables.get(k)
                 if cur is not None and hasattr(cur, "copy_") and tuple(cur.shape) == tuple(val.shape):
                     cur.copy_(val)
+                    if hasattr(session.variables, "touch"):
+                        session.variables.touch()
                 else:
                     session.variables[k] = val

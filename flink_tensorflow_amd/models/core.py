@@ -10,6 +10,17 @@
   method) into a callable.  Calling it returns a context manager over the outputs
   (``with model.fn(x) as y:``), the equivalent of the reference's lazy
   ``ManagedResource``; ``fn.apply(x)`` returns outputs directly.
+
+  On a GPU session the signature is **compiled** (``graph/compiler.py``: MFMA conv/GEMM
+  kernels, fused epilogues, hipGraph) once per feed-shape bucket and replayed: feeds are
+  staged through pinned host buffers and copied H2D asynchronously into the plan's input
+  buffers.  The leading (batch) dimension is padded up to the next of ``batch_buckets``
+  (default 1, 2, 4, … 256), so a stream of varying micro-batch sizes reuses a handful of
+  captured plans; outputs are sliced back.  Plans fold the session's variables into their
+  weights and are recompiled when a variable is written (``VariableStore.version``).
+  Signatures the compiler cannot take (STRING feeds such as serialized ``tf.Example``s,
+  ops without a lowering and without a glue fallback) run on the op-by-op interpreter;
+  ops lowered as PyTorch glue are logged and listed in ``plan_summary()["glue_ops"]``.
 * ``GraphLoader`` / ``DefaultGraphLoader`` / ``GraphDefGraphLoader`` — ``LIB/graphs/*``.
 * ``GenericModel`` — ``LIB/models/generic/GenericModel.scala:12-44``.
 """
@@ -113,11 +124,20 @@ class _Outputs(contextlib.AbstractContextManager):
         self.closed = True
 
 
+DEFAULT_BATCH_BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256)
+
+
 class ModelFunction:
-    """``ModelFunction(session, signature_def, method)`` → callable."""
+    """``ModelFunction(session, signature_def, method)`` → callable.
+
+    ``compile``: None = compile on GPU sessions, interpret on CPU; True/False force it.
+    ``batch_buckets``: leading-dimension buckets of compiled plans (None: exact shapes).
+    ``precision``: compiled-plan precision (``bf16`` or ``fp8``)."""
 
     def __init__(self, session_provider: Callable[[], Session] | Session, signature_def: SignatureDef,
-                 method: GraphMethod, check_method_name: bool = True):
+                 method: GraphMethod, check_method_name: bool = True, compile: bool | None = None,
+                 batch_buckets: tuple[int, ...] | None = DEFAULT_BATCH_BUCKETS, precision: str = "bf16",
+                 strict: bool = False):
         if check_method_name and method.name and signature_def.method_name != method.name:
             raise ValueError(f"signature method name {signature_def.method_name!r} does not match "
                              f"method {method.name!r}")
@@ -126,24 +146,116 @@ class ModelFunction:
         self.method = method
         self._fetch_keys = sorted(signature_def.outputs)
         self._fetch_names = [str(TensorName.parse(signature_def.outputs[k].name)) for k in self._fetch_keys]
+        self.compile = compile
+        self.batch_buckets = tuple(sorted(batch_buckets)) if batch_buckets else None
+        self.precision = precision
+        self.strict = strict
+        self._plans: dict = {}          # feed-spec key -> (CompiledFunction, variables version, staging)
+        self._interpret_reason: str | None = None
+        self.last_plan = None
 
     @property
     def session(self) -> Session:
         s = self._session
         return s() if callable(s) and not isinstance(s, Session) else s
 
-    def feeds(self, value) -> dict[str, Any]:
+    def feeds(self, value, device=None) -> dict[str, Any]:
         sess = self.session
         mapped = self.method.inputs(value)
         feeds = {}
         for key, info in self.signature_def.inputs.items():
             if key not in mapped:
                 raise ValueError(f"missing input {key!r} for signature (expected {sorted(self.signature_def.inputs)})")
-            feeds[str(TensorName.parse(info.name))] = to_graph_tensor(mapped[key], device=sess.device)
+            feeds[str(TensorName.parse(info.name))] = to_graph_tensor(
+                mapped[key], device=sess.device if device is None else device)
         return feeds
 
+    # ---------------------------------------------------------------- compiled path
+    def _use_compiled(self, sess) -> bool:
+        if self._interpret_reason is not None:
+            return False
+        return self.compile if self.compile is not None else sess.device.type == "cuda"
+
+    def _bucket(self, feeds: dict) -> int | None:
+        if not self.batch_buckets:
+            return None
+        lead = {int(v.shape[0]) for v in feeds.values() if isinstance(v, torch.Tensor) and v.dim() > 0}
+        if len(lead) != 1 or any(not isinstance(v, torch.Tensor) or v.dim() == 0 for v in feeds.values()):
+            return None
+        n = lead.pop()
+        return next((b for b in self.batch_buckets if b >= n), None)
+
+    def _plan_for(self, sess, feeds: dict, bucket: int | None):
+        from ..graph.compiler import compile_signature
+        from ..types.dtypes import DataType
+
+        specs = {k: ((bucket, *v.shape[1:]) if bucket else tuple(v.shape), DataType.from_torch(v.dtype))
+                 for k, v in feeds.items()}
+        key = tuple(sorted((k, sh, int(dt)) for k, (sh, dt) in specs.items()))
+        version = getattr(sess.variables, "version", 0)
+        hit = self._plans.get(key)
+        if hit is not None and hit[1] == version:
+            return hit
+        plan = compile_signature(sess, specs, self._fetch_names, strict=self.strict, precision=self.precision)
+        if plan.glue_ops:
+            LOG.info("signature %s: ops run as PyTorch glue in the compiled plan: %s",
+                     self.signature_def.method_name, sorted(set(plan.glue_ops)))
+        pinned = sess.device.type == "cuda"
+        staging = {k: torch.empty(sh, dtype=feeds[k].dtype, pin_memory=pinned).zero_() for k, (sh, _) in specs.items()}
+        entry = (plan, version, staging)
+        self._plans[key] = entry
+        return entry
+
+    def _run_compiled(self, sess, value):
+        from ..graph.compiler import CompileError
+
+        feeds = self.feeds(value, device=torch.device("cpu"))
+        if any(not isinstance(v, torch.Tensor) for v in feeds.values()):
+            self._interpret_reason = "non-tensor (STRING) feeds"
+            LOG.info("signature %s runs on the interpreter: %s", self.signature_def.method_name,
+                     self._interpret_reason)
+            return None
+        bucket = self._bucket(feeds)
+        try:
+            plan, _, staging = self._plan_for(sess, feeds, bucket)
+        except (CompileError, NotImplementedError, KeyError, TypeError, ValueError) as e:
+            self._interpret_reason = f"{type(e).__name__}: {e}"
+            LOG.warning("signature %s cannot be compiled, using the interpreter: %s",
+                        self.signature_def.method_name, self._interpret_reason)
+            return None
+        n = None
+        for k, v in feeds.items():
+            st = staging[k]
+            if bucket:
+                n = int(v.shape[0])
+                st[:n].copy_(v)
+            else:
+                st.copy_(v)
+            plan.input_buffer(k).copy_(st, non_blocking=True)
+        outs = plan(None)
+        if bucket:
+            outs = [o[:n] if isinstance(o, torch.Tensor) and o.dim() > 0 and o.shape[0] == bucket else o for o in outs]
+        self.last_plan = plan
+        return outs
+
+    def plan_summary(self) -> dict | None:
+        """Summary of the most recently replayed compiled plan (None: interpreter)."""
+        return self.last_plan.summary() if self.last_plan is not None else None
+
+    @property
+    def compiled_plans(self) -> int:
+        return len(self._plans)
+
+    # ---------------------------------------------------------------- call
     def run(self, value, run_metadata: bool = False):
         sess = self.session
+        if self._use_compiled(sess):
+            outs = self._run_compiled(sess, value)
+            if outs is not None:
+                out = self.method.outputs(dict(zip(self._fetch_keys, outs)))
+                if run_metadata:
+                    return out, self.last_plan.profile()
+                return out
         res = sess.run(self._fetch_names, self.feeds(value), run_metadata=run_metadata)
         outs = res.outputs if run_metadata else res
         out = self.method.outputs(dict(zip(self._fetch_keys, outs)))

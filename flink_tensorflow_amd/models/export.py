@@ -14,6 +14,7 @@ import shutil
 from typing import Mapping
 
 import numpy as np
+import torch
 
 from ..graph.builder import GraphBuilder
 from ..io import bundle
@@ -92,3 +93,32 @@ def export_saved_model(export_dir: str, builder: GraphBuilder, variables: Mappin
             with open(os.path.join(export_dir, "assets", k), "wb") as f:
                 f.write(v)
     return export_dir
+
+
+def graph_def_to_saved_model(export_dir: str, graph_def, signatures: Mapping[str, SignatureDef],
+                             tags=("serve",), min_elems: int = 2, overwrite: bool = True) -> str:
+    """Exports a frozen GraphDef as a TF 1.x SavedModel whose weights are **variables**:
+    every floating-point ``Const`` with at least ``min_elems`` elements becomes a
+    ``VariableV2`` of the same name (consumers keep reading ``name:0``), initialised by a
+    ``name/Assign`` from ``name/initial_value`` and restored from ``variables/`` by the
+    saver subgraph — the layout TF's ``freeze_graph`` undoes."""
+    from ..graph.tensor_proto import tensor_from_proto
+
+    b = GraphBuilder()
+    variables: dict[str, object] = {}
+    for nd in graph_def.node:
+        if nd.op == "Const":
+            t = tensor_from_proto(nd.attr["value"].tensor)
+            if isinstance(t, torch.Tensor) and t.is_floating_point() and t.numel() >= min_elems:
+                variables[nd.name] = t.numpy()
+                continue
+        b.nodes.append(nd)
+        b._names.add(nd.name)
+    for name, val in variables.items():
+        init = b.constant(f"{name}/initial_value", val)
+        v = b.op("VariableV2", name=name, dtype=DataType.from_torch(torch.as_tensor(val).dtype),
+                 shape=TensorShapeProto.of(val.shape), container=b"", shared_name=b"")
+        assert v == f"{name}:0", v
+        asg = b.op("Assign", [f"{name}:0", init], name=f"{name}/Assign", validate_shape=True, use_locking=True)
+        b.variables[name] = asg.split(":")[0]
+    return export_saved_model(export_dir, b, variables, signatures, tags=tags, overwrite=overwrite)

@@ -153,7 +153,7 @@ class DefaultSavedModelLoader(SavedModelLoader):
 class TensorFlowModel(RichModel, CheckpointedModel):
     """A SavedModel-backed model.  Subclasses define ``loader``."""
 
-    _TRANSIENT = ("_bundle",)
+    _TRANSIENT = ("_bundle", "_functions")
 
     def __init__(self, device=None):
         self.device = device
@@ -185,6 +185,7 @@ class TensorFlowModel(RichModel, CheckpointedModel):
         if self._bundle is not None:
             self._bundle.close()
         self._bundle = None
+        self.__dict__.pop("_functions", None)
 
     @property
     def is_open(self) -> bool:
@@ -199,11 +200,23 @@ class TensorFlowModel(RichModel, CheckpointedModel):
     def session(self) -> Session:
         return self.bundle.session
 
-    def function(self, signature: str, method) -> ModelFunction:
-        sd = self.signature_def(signature)
-        if sd is None:
-            raise KeyError(f"no signature {signature!r}; available: {sorted(self.metagraph.signature_def)}")
-        return ModelFunction(self.session, sd, method)
+    def function(self, signature: str, method, **options) -> ModelFunction:
+        """The ``ModelFunction`` of ``signature`` (cached per signature / method type /
+        options, so its compiled plans live as long as the open model).  ``options`` go to
+        ``ModelFunction`` (``compile``, ``batch_buckets``, ``precision``, ``strict``)."""
+        key = (signature, type(method), tuple(sorted(options.items())))
+        fns = self.__dict__.get("_functions")
+        if fns is None:  # first use, or a descriptor unpickled in a subtask (transient field)
+            fns = self.__dict__["_functions"] = {}
+        fn = fns.get(key)
+        if fn is None:
+            sd = self.signature_def(signature)
+            if sd is None:
+                raise KeyError(f"no signature {signature!r}; available: {sorted(self.metagraph.signature_def)}")
+            fn = ModelFunction(self.session, sd, method, **options)
+            fns[key] = fn
+        fn.method = method
+        return fn
 
     @staticmethod
     def load(path: str, *tags: str) -> DefaultSavedModelLoader:

@@ -94,3 +94,21 @@ def resnet50_graph_def(num_classes: int = 1000, seed: int = 0, image_hw: tuple[i
 def resnet50_flops_per_image(hw=224) -> float:
     """Forward FLOPs (2·MAC) of ResNet-50 v1.5 at hw×hw (≈8.2 GFLOP at 224)."""
     return 4.09e9 * 2 * (hw / 224) ** 2
+
+
+def export_resnet50_saved_model(export_dir: str, image_hw: tuple[int, int] | None = None, seed: int = 0,
+                                top_k: int = 5, depth: int = 50, num_classes: int = 1000) -> str:
+    """ResNet-50 v1.5 (random init) as a real TF 1.x SavedModel: weights are variables in
+    ``variables/`` and the ``serving_default`` predict signature maps ``images`` (uint8
+    NHWC) to ``probabilities`` / ``scores`` / ``classes`` (top-k)."""
+    from ...proto.messages import SignatureDef
+    from ..export import graph_def_to_saved_model, tensor_info
+
+    gd = resnet50_graph_def(num_classes=num_classes, seed=seed, image_hw=image_hw, top_k=top_k, depth=depth)
+    hw = list(image_hw) if image_hw else [-1, -1]
+    sig = SignatureDef(inputs={"images": tensor_info("images:0", "UINT8", [-1, *hw, 3])},
+                       outputs={"probabilities": tensor_info("probs:0", "FLOAT", [-1, num_classes]),
+                                "scores": tensor_info("top_k:0", "FLOAT", [-1, top_k]),
+                                "classes": tensor_info("top_k:1", "INT32", [-1, top_k])},
+                       method_name="tensorflow/serving/predict")
+    return graph_def_to_saved_model(export_dir, gd, {"serving_default": sig})
