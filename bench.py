@@ -59,6 +59,12 @@ def main():
                     help="comma-separated extra batch buckets compiled next to --batch; with --dynamic the "
                          "per-step batch size varies and each micro-batch runs on the smallest bucket")
     ap.add_argument("--dynamic", action="store_true", help="variable micro-batch sizes (uniform in [B/4, B])")
+    ap.add_argument("--offered-rate", type=float, default=None,
+                    help="open-loop latency mode: records ARRIVE at this rate (records/s per GPU, Poisson); "
+                         "each is stamped at its arrival, micro-batches form in a MicroBatcher (--batch, "
+                         "--max-delay-ms) and p50/p99 are arrival -> result on host.  Runs --steps x --batch "
+                         "arrivals after --warmup x --batch warm-up arrivals")
+    ap.add_argument("--max-delay-ms", type=float, default=2.0, help="MicroBatcher deadline (offered-rate mode)")
     ap.add_argument("--no-pack", action="store_true", help="bert: run padded batches (no token packing)")
     ap.add_argument("--lanes", type=int, default=None,
                     help="compute lanes: independent plan instances on their own HIP streams, batches round-robin "
@@ -123,12 +129,16 @@ def main():
     elif args.model == "resnet50":
         gd = resnet50_graph_def(image_hw=(HW, HW), top_k=5, seed=0)
         graph = Graph.from_graph_def(gd)
+        sizes = sorted({B} | {int(b) for b in (args.buckets or "").split(",") if b})
         for lane in range(lanes):
             arena = DeviceArena(dev, budget, name=f"rank{rank}/lane{lane}")
-            p = CompiledFunction(graph, {"images:0": ((B, HW, HW, 3), "UINT8")}, ["top_k:0", "top_k:1"], dev,
-                                 use_graph=not args.no_graph, strict=True, precision=precision, arena=arena)
-            lane_plans.append({B: p})
-            params += p.params
+            plans = {}
+            for b in sorted(sizes, reverse=True):  # largest first: every bucket plan shares one slab
+                plans[b] = CompiledFunction(graph, {"images:0": ((b, HW, HW, 3), "UINT8")}, ["top_k:0", "top_k:1"],
+                                            dev, use_graph=not args.no_graph, strict=True, precision=precision,
+                                            arena=arena)
+            lane_plans.append(plans)
+            params += [t for p in plans.values() for t in p.params]
         feed, rec_shape, rec_dtype = "images:0", (HW, HW, 3), torch.uint8
         flops_per_record = resnet50_flops_per_image(224)
         rng = np.random.default_rng(1234 + rank)
@@ -172,6 +182,10 @@ def main():
     runner = PipelinedGpuRunner(lane_plans, feed, lambda p: p.output_tensors(), rec_shape, rec_dtype,
                                 depth=args.depth, device=dev)
 
+    if args.offered_rate:
+        return run_offered(args, runner, records, B, rank, ws, dev, comm, MetricGroup, model_name, data, lanes,
+                           sorted(lane_plans[0]))
+
     cursor = 0
     lat = []
     n_done = 0
@@ -185,6 +199,9 @@ def main():
         cursor += n
         if collect:
             n_sub += n
+        # closed loop: a record "arrives" when the source hands it over, i.e. right here,
+        # before staging (the open-loop --offered-rate mode measures arrival -> result
+        # under a rate-limited source, including batch-formation wait)
         now = time.perf_counter()
         ts = np.full(n, now)
         for r in runner.poll() + runner.submit(batch, ts):
@@ -250,6 +267,74 @@ def main():
             "host_ms_per_batch": {k: round(v * 1e3 / max(1, runner.batches), 3) for k, v in runner.host_s.items()},
         }
         print(json.dumps(out), flush=True)
+    comm.destroy()
+
+
+def run_offered(args, runner, records, B, rank, ws, dev, comm, MetricGroup, model_name, data, lanes, buckets):
+    """Open-loop latency: Poisson arrivals at --offered-rate records/s per GPU.  Each record
+    is stamped when it arrives (not when its batch is formed); a MicroBatcher forms
+    micro-batches of up to --batch records or whatever arrived within --max-delay-ms; a
+    batch of n runs on the smallest compiled bucket >= n.  Latency = arrival -> top-k on
+    the host.  Reports achieved records/s and node-level p50/p99 (merged histograms)."""
+    import torch
+
+    from flink_tensorflow_amd.batching.engine import MicroBatcher
+
+    rate = float(args.offered_rate)
+    n_warm, n_meas = args.warmup * B, args.steps * B
+    gaps = np.random.default_rng(7 + rank).exponential(1.0 / rate, n_warm + n_meas)
+    batcher = MicroBatcher(B, args.max_delay_ms)
+    lat, sizes = [], []
+
+    def consume(done, measure_from):
+        for r in done:
+            keep = r.ingest_ts >= measure_from
+            lat.append(r.latencies[: r.n][keep[: r.n]])
+
+    def drive(n, measure_from):
+        arrivals = time.perf_counter() + np.cumsum(gaps[:n])  # schedule relative to now
+        i = 0
+        while i < n or len(batcher):
+            now = time.perf_counter()
+            while i < n and arrivals[i] <= now:  # everything that has arrived by now
+                b = batcher.add(records[i % len(records)], arrivals[i])  # stamped at ARRIVAL
+                i += 1
+                if b is not None:
+                    sizes.append(len(b[0]))
+                    consume(runner.submit(*b), measure_from)
+            if batcher.due(now) or (i >= n and len(batcher)):
+                b = batcher.flush()
+                sizes.append(len(b[0]))
+                consume(runner.submit(*b), measure_from)
+            consume(runner.poll(), measure_from)
+            if i < n and len(batcher) == 0:
+                time.sleep(max(0.0, min(arrivals[i] - time.perf_counter(), 2e-4)))
+        consume(runner.drain(), measure_from)
+
+    drive(n_warm, float("inf"))
+    lat.clear()
+    sizes.clear()
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    t0 = time.perf_counter()
+    drive(n_meas, t0)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    comm.barrier()
+    elapsed_max = comm.all_reduce_scalar(elapsed, "max", device=dev)
+    mg = MetricGroup("bench")
+    mg.histogram("latency_s").update_many(np.concatenate(lat) if lat else np.zeros(1))
+    node_lat = comm.allgather_metrics(mg)["histograms"]["latency_s"]
+    total = comm.all_reduce_scalar(float(n_meas), "sum", device=dev) / elapsed_max
+    if rank == 0:
+        print(json.dumps({
+            "metric": f"p50/p99 arrival->result latency at an offered load, {model_name} stream",
+            "value": round(node_lat["p50"] * 1e3, 3), "unit": "ms (p50)", "higher_is_better": False,
+            "n_gpus": ws, "offered_records_per_s": round(rate * ws, 1), "achieved_records_per_s": round(total, 1),
+            "p50_latency_ms": round(node_lat["p50"] * 1e3, 3), "p99_latency_ms": round(node_lat["p99"] * 1e3, 3),
+            "max_batch": B, "max_delay_ms": args.max_delay_ms, "batch_buckets": buckets, "compute_lanes": lanes,
+            "mean_batch": round(float(np.mean(sizes)), 1) if sizes else None, "batches": len(sizes),
+            "records": n_meas, "dtype": "bf16", "data": data + "; Poisson arrivals"}), flush=True)
     comm.destroy()
 
 

@@ -64,6 +64,47 @@ _BINARY = {"Add": "add", "AddV2": "add", "Sub": "sub", "Mul": "mul", "RealDiv": 
            "Maximum": "max", "Minimum": "min"}
 
 
+_CONV_TUNE: dict = {}  # layer signature -> ("pp", tile, splits) | ("incumbent", None, None)
+
+
+def _time_concurrent(f1, f2, dev, reps: int = 5) -> float:
+    """µs per pair of launches issued on two streams that run concurrently."""
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    cur = torch.cuda.current_stream(dev)
+    for s, f in ((s1, f1), (s2, f2)):
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            f()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(cur)
+    for s in (s1, s2):
+        s.wait_stream(cur)
+    for _ in range(reps):
+        with torch.cuda.stream(s1):
+            f1()
+        with torch.cuda.stream(s2):
+            f2()
+    cur.wait_stream(s1)
+    cur.wait_stream(s2)
+    e1.record(cur)
+    torch.cuda.synchronize(dev)
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
+def _time_launch(fn, dev, reps: int = 5) -> float:
+    """Median-free quick timing of a launch sequence (µs per call) on the current stream."""
+    fn()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
 class CompileError(RuntimeError):
     pass
 
@@ -675,6 +716,16 @@ class CompiledFunction:
                           (pt, pb, pl, pr), (dh, dw), act, out=_target(out), out_channel_offset=_coff(out),
                           out_scale=_eff_scale(out) if out.qscale is not None else None)
 
+        if out.qscale is None and xin_shape_override is None and (xin.phys_c or Cin) == Cin:
+            pp = self._conv_pp_choice(node.name, [(tuple(xin.shape), (KHe, KWe), (sh, sw), (pt, pl), (dh, dw))],
+                                      Cout, out, res_val, act, w_dev, b_dev,
+                                      lambda xs, o, r: K.conv2d_nhwc(xs[0], w_dev, b_dev, r, (sh, sw),
+                                                                     (pt, pb, pl, pr), (dh, dw), act, out=o))
+            if pp is not None:
+                def run(xin=xin, out=out, res_val=res_val, pp=pp, w2=w_dev.reshape(Cout, -1), b_dev=b_dev):  # noqa: F811
+                    pp([xin.buf], w2, b_dev, res_val.buf if res_val is not None else None, act, out=_target(out),
+                       out_channel_offset=_coff(out))
+
         shortcut_ok = (KHe == KWe == 1 and sh == sw and (pt, pb, pl, pr) == (0, 0, 0, 0) and (dh, dw) == (1, 1)
                        and res_val is None and act == K.ACT_NONE and out.qscale is None
                        and xin_shape_override is None and (xin.phys_c or Cin) == Cin)
@@ -723,6 +774,15 @@ class CompiledFunction:
 
         def run(xin=xin, x2=x2, out=out, w_dev=w_dev, b_dev=b_dev):
             K.conv1x1_dual(xin.buf, x2.buf, w_dev, b_dev, s2, act, out=_target(out), out_channel_offset=_coff(out))
+
+        if (xin.phys_c or K1) == K1 and (x2.phys_c or C2) == C2:
+            pp = self._conv_pp_choice(node.name, [(tuple(xin.shape), (1, 1), (1, 1), (0, 0), (1, 1)),
+                                                  (tuple(x2.shape), (1, 1), (s2, s2), (0, 0), (1, 1))],
+                                      Cout, out, None, act, w_dev, b_dev,
+                                      lambda xs, o, r: K.conv1x1_dual(xs[0], xs[1], w_dev, b_dev, s2, act, out=o))
+            if pp is not None:
+                def run(xin=xin, x2=x2, out=out, pp=pp, w_dev=w_dev, b_dev=b_dev):  # noqa: F811
+                    pp([xin.buf, x2.buf], w_dev, b_dev, None, act, out=_target(out), out_channel_offset=_coff(out))
 
         self._emit(node.name, "conv", run, [xin, x2], [out])
         self.vals[(last.name, 0)] = out
@@ -807,6 +867,65 @@ class CompiledFunction:
         self._alias_fused_outputs(absorbed2, out2)
         self.fused_tails = getattr(self, "fused_tails", 0) + 1
         return True
+
+    def _conv_pp_choice(self, name, srcs, Cout, out: Val, res_val, act, w_dev, b_dev, incumbent):
+        """A ``ConvPP`` launch for this convolution when the ping-pong implicit GEMM
+        (kernels/conv_pp.hip) beats the incumbent kernel on this exact layer, else None.
+
+        The choice is measured, not guessed: both candidates (and both conv_pp tile shapes)
+        run a few times on scratch tensors of the layer's shapes on this device, and the
+        result is cached per layer signature for the process (every bucket plan and lane of
+        a model reuses it).  Default off (``FTM_CONV_IMPL=incumbent``): with two compute
+        lanes the probe-selected layers measured ~1 % slower end to end
+        (profiles/r02_conv_pp); ``FTM_CONV_IMPL=auto`` enables the probe, ``=pp`` forces
+        conv_pp wherever eligible."""
+        force = os.environ.get("FTM_CONV_IMPL", "incumbent")
+        if self.device.type != "cuda" or force == "incumbent" or self.precision == "fp8":
+            return None
+        if any(s[0][3] % 64 for s in srcs) or Cout % 8 or _coff(out) % 8 or out.dtype != torch.bfloat16:
+            return None
+        if res_val is not None and (res_val.concat_slot is not None or res_val.qscale is not None
+                                    or tuple(res_val.shape) != tuple(out.shape) or res_val.alias_of is not None):
+            return None
+        N, OH, OW, _ = out.shape
+        key = (tuple(srcs), Cout, (OH, OW), res_val is not None, int(K.act_code(act)), out.shape[-1] != Cout)
+        hit = _CONV_TUNE.get(key)
+        if hit is None:
+            hit = self._tune_conv(srcs, Cout, (OH, OW), res_val is not None, act, w_dev, b_dev, incumbent, force)
+            _CONV_TUNE[key] = hit
+            LOG.info("conv %s %s -> %s", name, key[:3], hit)
+        if hit[0] == "incumbent":
+            return None
+        self.conv_pp_layers = getattr(self, "conv_pp_layers", 0) + 1
+        return K.ConvPP(srcs, Cout, (OH, OW), self.device, tile=hit[1], splits=hit[2])
+
+    def _tune_conv(self, srcs, Cout, ohw, with_res, act, w_dev, b_dev, incumbent, force):
+        dev = self.device
+        g = torch.Generator(device=dev).manual_seed(0)
+        xs = [torch.randn(s[0], device=dev, generator=g).to(torch.bfloat16) for s in srcs]
+        N = srcs[0][0][0]
+        o = torch.empty((N, *ohw, Cout), dtype=torch.bfloat16, device=dev)
+        r = torch.randn((N, *ohw, Cout), device=dev, generator=g).to(torch.bfloat16) if with_res else None
+        o2 = torch.empty_like(o)
+        w2 = w_dev.reshape(Cout, -1)
+        cands = {}
+        for tile in (0, 1):
+            cp = K.ConvPP(srcs, Cout, ohw, dev, tile=tile)
+            cp2 = K.ConvPP(srcs, Cout, ohw, dev, tile=tile)  # own split-K workspace
+            cands[("pp", tile, cp.splits)] = (lambda cp=cp: cp(xs, w2, b_dev, r, act, out=o),
+                                             lambda cp2=cp2: cp2(xs, w2, b_dev, r, act, out=o2))
+        if force != "pp":
+            cands[("incumbent", None, None)] = (lambda: incumbent(xs, o, r), lambda: incumbent(xs, o2, r))
+        # timed as TWO concurrent instances on two streams: plans run in compute lanes, and a
+        # kernel that monopolises the CUs (one 160 KiB-LDS workgroup per CU) can win alone
+        # and lose next to the sibling lane's kernels (measured: profiles/r02_conv_pp)
+        best, best_t = None, float("inf")
+        for k, (f1, f2) in cands.items():
+            t = _time_concurrent(f1, f2, dev)
+            if t < best_t:
+                best, best_t = k, t
+        del xs, o, o2, r
+        return best
 
     def _fusable_maxpool(self, last: Node, act, out: Val):
         """The single consumer of a ReLU conv chain when it is a 3x3 / stride-2 NHWC
@@ -1479,6 +1598,7 @@ class CompiledFunction:
                 "fp8_layers": self.fp8_layers, "fused_shortcuts": getattr(self, "fused_shortcuts", 0),
                 "fused_tails": getattr(self, "fused_tails", 0),
                 "fused_pools": getattr(self, "fused_pools", 0), "conv3x3c64": getattr(self, "conv3x3c64", 0),
+                "conv_pp": getattr(self, "conv_pp_layers", 0),
                 "activation_bytes": self.activation_bytes,
                 "param_bytes": self.param_bytes()}
 

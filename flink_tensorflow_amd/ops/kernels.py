@@ -391,6 +391,124 @@ def gemm_pp(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = Non
     return out
 
 
+def conv_pp_ktab(srcs) -> torch.Tensor:
+    """Host-built K-tile table of ``conv_pp``: for every 64-wide K tile (source, kh, kw,
+    channel chunk order) the byte delta of its input rows relative to the receptive-field
+    origin, and ``src << 20 | kh*dh << 10 | kw*dw``.  ``srcs``: (H, W, C, KH, KW, dh, dw)."""
+    rows = []
+    for si, (H, W, C, KH, KW, dh, dw) in enumerate(srcs):
+        for kh in range(KH):
+            for kw in range(KW):
+                for cc in range(C // 64):
+                    rows.append((((kh * dh * W + kw * dw) * C + cc * 64) * 2, (si << 20) | (kh * dh << 10) | (kw * dw)))
+    return torch.tensor(rows, dtype=torch.int32)
+
+
+def conv_pp_tile(Cout: int) -> int:
+    """0 = 256x256 tiles, 1 = 512x128 tiles (channel counts that would waste half of a
+    256-wide tile)."""
+    return 1 if Cout <= 128 or (Cout % 256 and Cout % 128 == 0) else 0
+
+
+def conv_pp_splits(M: int, N: int, K: int, tile: int, num_cu: int = 256) -> int:
+    """Split-K factor for ``conv_pp`` (same cost model as ``gemm_pp_splits``)."""
+    bm, bn = (512, 128) if tile == 1 else (256, 256)
+    tiles = -(-M // bm) * -(-N // bn)
+    nk = K // 64
+    best_s, best_t = 1, -(-tiles // num_cu) * nk * _PP_KTILE_US
+    for s in range(2, min(16, nk) + 1):
+        per = -(-nk // s)
+        se = -(-nk // per)
+        t = -(-tiles * se // num_cu) * per * _PP_KTILE_US + 2.0 * se * M * N * 4 / _PP_SPLIT_BW + 2.0
+        if t < 0.9 * best_t:
+            best_s, best_t = se, t
+    return best_s
+
+
+class ConvPP:
+    """A planned ``conv_pp`` launch (kernels/conv_pp.hip): implicit-GEMM NHWC convolution
+    of one or two sources into one accumulator on the ping-pong MFMA pipeline.
+
+    ``srcs``: [(x_shape NHWC, (KH, KW), (sh, sw), (pt, pl), (dh, dw))]; the weight is the
+    concatenation of the sources' OHWI filters, [Cout, sum KH*KW*C] bf16.  The K-tile
+    table and the split-K workspace are built once (device tensors kept on the object)."""
+
+    def __init__(self, srcs, Cout: int, out_hw, device, tile: int | None = None, splits: int | None = None):
+        self.srcs = [(tuple(xs), tuple(k), tuple(st), tuple(pd), tuple(dl)) for xs, k, st, pd, dl in srcs]
+        self.N = self.srcs[0][0][0]
+        self.OH, self.OW = out_hw
+        self.Cout = Cout
+        self.K = sum(k[0] * k[1] * xs[3] for xs, k, _, _, _ in self.srcs)
+        for xs, _, _, _, _ in self.srcs:
+            if xs[3] % 64 or xs[0] != self.N:
+                raise ValueError("conv_pp: channels must be multiples of 64 and batches equal")
+        if Cout % 8:
+            raise ValueError("conv_pp: Cout % 8")
+        self.M = self.N * self.OH * self.OW
+        self.tile = conv_pp_tile(Cout) if tile is None else tile
+        self.splits = conv_pp_splits(self.M, Cout, self.K, self.tile) if splits is None else splits
+        self.ktab = conv_pp_ktab([(xs[1], xs[2], xs[3], k[0], k[1], dl[0], dl[1])
+                                  for xs, k, _, _, dl in self.srcs]).to(device)
+        self.ws = (torch.empty(self.splits * self.M * Cout, dtype=torch.float32, device=device)
+                   if self.splits > 1 else None)
+
+    def __call__(self, xs, w, bias=None, residual=None, act=None, out=None, out_channel_offset: int = 0):
+        if len(xs) != len(self.srcs):
+            raise ValueError("conv_pp: source count")
+        for x, (shape, *_r) in zip(xs, self.srcs):
+            if tuple(x.shape) != shape:
+                raise ValueError(f"conv_pp: input shape {tuple(x.shape)} != planned {shape}")
+        if out is None:
+            out = torch.empty((self.N, self.OH, self.OW, self.Cout), dtype=torch.bfloat16, device=xs[0].device)
+        ldy = out.shape[-1]
+        if tuple(out.shape[:3]) != (self.N, self.OH, self.OW) or out_channel_offset + self.Cout > ldy:
+            raise ValueError("conv_pp: output shape mismatch")
+        if tuple(w.shape) != (self.Cout, self.K):
+            raise ValueError(f"conv_pp: weight {tuple(w.shape)} != ({self.Cout}, {self.K})")
+        if not xs[0].is_cuda:
+            return self._reference(xs, w, bias, residual, act, out, out_channel_offset)
+        for i, x in enumerate(xs):
+            _check(x, f"x{i}", device=out.device)
+        _check(w, "w", device=out.device)
+        _check(out, "out", device=out.device)
+        if bias is not None:
+            _check(bias, "bias", torch.float32, out.device)
+        if residual is not None:
+            _check(residual, "residual", device=out.device)
+            if residual.numel() != self.M * self.Cout:
+                raise ValueError("conv_pp: residual shape")
+        srcs = [(x.data_ptr(), self.N, sh[1], sh[2], sh[3], k[0], k[1], st[0], st[1], pd[0], pd[1], dl[0], dl[1])
+                for x, (sh, k, st, pd, dl) in zip(xs, self.srcs)]
+        _hip().conv_pp(srcs, self.ktab.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(),
+                       self.N, self.OH, self.OW, self.Cout, ldy, out_channel_offset, self.Cout, act_code(act),
+                       self.tile, self.splits, _ptr(self.ws), _stream())
+        return out
+
+    def _reference(self, xs, w, bias, residual, act, out, coff):
+        """fp32 host reference (CPU tests): the sum of the sources' convolutions."""
+        import torch.nn.functional as F
+
+        y = 0
+        k0 = 0
+        for x, (sh, (KH, KW), (s_h, s_w), (pt, pl), (dh, dw)) in zip(xs, self.srcs):
+            C = sh[3]
+            wk = w[:, k0:k0 + KH * KW * C].float().reshape(self.Cout, KH, KW, C).permute(0, 3, 1, 2)
+            k0 += KH * KW * C
+            xi = x.float().permute(0, 3, 1, 2)
+            ph_hi = max(0, (self.OH - 1) * s_h + (KH - 1) * dh + 1 - sh[1] - pt)
+            pw_hi = max(0, (self.OW - 1) * s_w + (KW - 1) * dw + 1 - sh[2] - pl)
+            xi = F.pad(xi, (pl, pw_hi, pt, ph_hi))
+            yi = F.conv2d(xi, wk, stride=(s_h, s_w), dilation=(dh, dw))[:, :, :self.OH, :self.OW]
+            y = y + yi
+        y = y.permute(0, 2, 3, 1)
+        if bias is not None:
+            y = y + bias.float()
+        if residual is not None:
+            y = y + residual.reshape(y.shape).float()
+        out[..., coff:coff + self.Cout] = _apply_act_ref(y, act_code(act)).to(out.dtype)
+        return out
+
+
 # ------------------------------------------------------------------------------ preprocess
 def preprocess_images(images_u8: torch.Tensor, out_hw=(224, 224), mean=(117.0, 117.0, 117.0),
                       std=(1.0, 1.0, 1.0), align_corners=False, half_pixel_centers=False,
