@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--delay-ms", type=float, default=5.0)
     ap.add_argument("--hw", type=int, default=256)
     ap.add_argument("--depth-layers", type=int, default=50)
+    ap.add_argument("--processes", action="store_true",
+                    help="run the model operator in a worker process (records cross through the tensor slab)")
     a = ap.parse_args()
     pool = np.random.default_rng(0).integers(0, 256, (256, a.hw, a.hw, 3), dtype=np.uint8)
 
@@ -42,14 +44,17 @@ def main():
 
     env = StreamExecutionEnvironment.get_execution_environment()
     model = ResNet50Model(image_hw=(a.hw, a.hw), buckets=(a.batch,), depth_layers=a.depth_layers)
-    env.generate(images).map_with_model_batched(model, None, max_batch=a.batch, max_delay_ms=a.delay_ms,
-                                                name="resnet50").add_sink(sink := ThroughputSink())
+    op = env.generate(images).map_with_model_batched(model, None, max_batch=a.batch, max_delay_ms=a.delay_ms,
+                                                     name="resnet50")
+    if a.processes:
+        op = op.run_in_processes()
+    op.add_sink(sink := ThroughputSink())
     t0 = time.time()
     res = env.execute("resnet50-stream")
     el = time.time() - t0
     m = [v for k, v in res.metrics.items() if k.startswith("resnet50")][0]
     steady = sink.rate(0.2)  # steady state: skip the first fifth (compile, capture, pipeline fill)
-    print(json.dumps({"records": a.records, "seconds": round(el, 3), "records_per_s": round(a.records / el, 1),
+    print(json.dumps({"records": a.records, "worker_process": a.processes, "seconds": round(el, 3), "records_per_s": round(a.records / el, 1),
                       "steady_records_per_s": round(steady, 1) if steady else None,
                       "latency_s": m["histograms"].get("latency_s"), "batch": m["histograms"].get("batch_size")}))
 

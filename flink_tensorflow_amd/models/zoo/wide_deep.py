@@ -178,9 +178,10 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         row updates) as a hipGraph for micro-batches shaped like ``batch``; later
         ``train_step`` calls with that shape replay it (one launch instead of ~190).  The
         sparse pipeline is static-shape and sync-free, which is what makes this possible.
-        Single-process only (the data-parallel path keeps its collectives outside graphs)."""
-        if comm.is_dist():
-            return
+        Under data parallelism the RCCL collectives are captured too: the bucketed dense
+        all-reduce forks onto the communicator's stream and joins back through events, and
+        the row-sparse all-gathers run on the capturing stream, so one replay is one whole
+        DP step."""
         dev = self._model.device
         self._static = tuple(t.to(dev).clone() for t in batch)
         with capture_lock():
@@ -239,6 +240,70 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
             sd = {k[len("model/"):]: r.read(k) for k in r.keys() if k.startswith("model/")}
         self._model.load_state_dict({k: v.to(self._model.device) for k, v in sd.items()})
         self.steps = ctx.operator_state.blobs.get("widedeep_steps", 0)
+
+
+def click_record_layout(cfg: WideDeepConfig, n_cross: int = 8) -> np.dtype:
+    """Fixed-size binary row of one labelled click record (little-endian):
+    ``label f32 | dense f32[num_dense] | cats i32[num_fields] | cross i32[n_cross]`` —
+    the TensorValue-style wire row a Criteo stream carries (192 B for the default
+    config), so a micro-batch is staged by one native gather of rows into pinned memory
+    and split into tensors on the device (no per-record Python work)."""
+    return np.dtype([("label", "<f4"), ("dense", "<f4", (cfg.num_dense,)), ("cats", "<i4", (cfg.num_fields,)),
+                     ("cross", "<i4", (n_cross,))])
+
+
+def pack_click_records(records, cfg: WideDeepConfig, n_cross: int = 8) -> np.ndarray:
+    """``(label, dense, cats, cross)`` tuples -> uint8 rows ``[n, row_bytes]``."""
+    lay = click_record_layout(cfg, n_cross)
+    arr = np.zeros(len(records), lay)
+    for i, (lab, dense, cats, cross) in enumerate(records):
+        arr[i] = (lab, dense, cats, cross)
+    return arr.view(np.uint8).reshape(len(records), lay.itemsize)
+
+
+class PackedBatchStager:
+    """Micro-batch staging of packed click rows: native multithreaded gather into a pinned
+    slot, async H2D on the current stream, and device-side views split into (labels,
+    dense, cats, cross).  ``depth`` slots rotate; a slot is reused only after the H2D
+    that read it completed (event), so the host can stage batch i+1 while batch i trains."""
+
+    def __init__(self, cfg: WideDeepConfig, batch: int, device, n_cross: int = 8, depth: int = 2):
+        from ... import _ext
+
+        self.lay = click_record_layout(cfg, n_cross)
+        self.row = self.lay.itemsize
+        self.batch = batch
+        self.cfg, self.n_cross = cfg, n_cross
+        self.device = torch.device(device)
+        self._native = _ext.native()
+        pin = self.device.type == "cuda"
+        self.pinned = [torch.empty((batch, self.row), dtype=torch.uint8, pin_memory=pin) for _ in range(depth)]
+        self.dev = [torch.empty((batch, self.row), dtype=torch.uint8, device=self.device) for _ in range(depth)]
+        self.ev = [torch.cuda.Event() if pin else None for _ in range(depth)]
+        self._i = 0
+
+    def stage(self, rows) -> tuple:
+        """``rows``: buffer-protocol rows of ``row`` bytes (exactly ``batch`` of them)."""
+        if len(rows) != self.batch:
+            raise ValueError(f"expected {self.batch} rows, got {len(rows)}")
+        i = self._i
+        self._i = (i + 1) % len(self.pinned)
+        if self.ev[i] is not None:
+            self.ev[i].synchronize()  # the previous H2D out of this pinned slot is done
+        pin, dev = self.pinned[i], self.dev[i]
+        self._native.gather_into(pin.data_ptr(), pin.numel(), list(rows), self.row, 8)
+        dev.copy_(pin, non_blocking=True)
+        if self.ev[i] is not None:
+            self.ev[i].record()
+        c = self.cfg
+        o_d = 4
+        o_c = o_d + 4 * c.num_dense
+        o_x = o_c + 4 * c.num_fields
+        labels = dev[:, 0:4].contiguous().view(torch.float32).reshape(-1)
+        dense = dev[:, o_d:o_c].contiguous().view(torch.float32)
+        cats = dev[:, o_c:o_x].contiguous().view(torch.int32)
+        cross = dev[:, o_x:o_x + 4 * self.n_cross].contiguous().view(torch.int32)
+        return labels, dense, cats, cross
 
 
 def synthetic_click_records(n: int, cfg: WideDeepConfig, seed: int = 0, n_cross: int = 8):

@@ -13,6 +13,14 @@ keyed state, timers, micro-batching, the GPU plan).  The worker's emissions come
 second ring and are re-emitted by a drainer thread in order, so a checkpoint barrier is
 forwarded downstream only after every record the worker emitted before its snapshot.
 
+Record payloads do not ride in the pickles: every ndarray / CPU tensor / ``TensorValue``
+of at least ``_SLAB_MIN`` bytes is written ONCE into the edge's shared-memory tensor slab
+(``TensorSlab``, a ring the coordinator allocates from) and only a descriptor (offset,
+shape, dtype) crosses the ring; the worker hands the operator a zero-copy view of the slab
+(e.g. the batched model operator gathers it straight into its pinned staging slot) and
+returns the space when the view is garbage collected.  Small values, object payloads and a
+full slab fall back to the pickle.
+
 Messages (cloudpickle, fragmented when larger than half a ring):
 
 =====================  ==============================================================
@@ -32,14 +40,180 @@ import time
 import traceback
 import uuid
 
+import collections
+import weakref
+
 import cloudpickle
+import numpy as np
 
 from .. import _ext
 from .operators import Output, Record, Watermark
 
 _RING_BYTES = 64 << 20
+_SLAB_BYTES = int(os.environ.get("FTM_SLAB_BYTES", str(1 << 30)))  # per coordinator -> worker edge
+_SLAB_MIN = 4096       # payloads below this ride in the pickle
+_SLAB_ALIGN = 128
 _BATCH = 64
 _IDLE_S = 0.02
+
+
+class _SlabRef:
+    """Descriptor of a record payload in the tensor slab (what crosses the ring)."""
+
+    __slots__ = ("start", "pos", "end", "shape", "dtype", "kind", "tv_dtype")
+
+    def __init__(self, start, pos, end, shape, dtype, kind, tv_dtype=None):
+        self.start, self.pos, self.end = start, pos, end
+        self.shape, self.dtype, self.kind, self.tv_dtype = shape, dtype, kind, tv_dtype
+
+    def __reduce__(self):
+        return (_SlabRef, (self.start, self.pos, self.end, self.shape, self.dtype, self.kind, self.tv_dtype))
+
+
+class TensorSlab:
+    """Shared-memory ring of record payloads for one coordinator -> worker edge.
+
+    The coordinator allocates monotonically (``head``; an allocation never straddles the
+    end of the ring — the rest of the ring is skipped and released with it) and copies each
+    payload in once; the worker maps the same segment, hands out zero-copy numpy views and
+    publishes, in the 8-byte header, the position up to which every view has been dropped
+    (releases are applied in allocation order).  A full slab makes the coordinator wait
+    briefly, then fall back to pickling (a window operator may legitimately hold many
+    records)."""
+
+    HDR = 64
+
+    def __init__(self, name: str, create: bool, capacity: int = _SLAB_BYTES):
+        import mmap
+
+        self.path = "/dev/shm/" + name.lstrip("/")
+        fd = os.open(self.path, (os.O_RDWR | os.O_CREAT | os.O_EXCL) if create else os.O_RDWR, 0o600)
+        try:
+            if create:
+                os.ftruncate(fd, capacity + self.HDR)
+            size = os.fstat(fd).st_size
+            self._mm = mmap.mmap(fd, size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        finally:
+            os.close(fd)
+        self.name = name
+        self.cap = size - self.HDR
+        self.mem = np.frombuffer(self._mm, np.uint8)
+        self.hdr = np.frombuffer(self._mm, np.int64, 1, 0)
+        self.owner = create
+        self._native = _ext.native()
+        self._base = self.mem.ctypes.data
+        if create:
+            self.hdr[0] = 0
+        self.head = 0
+        self.records = self.bytes = 0
+        # worker side
+        self._lock = threading.Lock()
+        self._pending: collections.deque = collections.deque()
+        self._dropped: set = set()
+
+    # ---- coordinator
+    def put(self, arr: np.ndarray, wait_s: float = 0.05):
+        """Copies ``arr`` (contiguous) in; returns (start, pos, end) or None (no room)."""
+        n = arr.nbytes
+        if n > self.cap // 4:
+            return None
+        off = self.head % self.cap
+        start = self.head
+        pos = self.head + (self.cap - off if off + n > self.cap else 0)
+        end = pos + -(-n // _SLAB_ALIGN) * _SLAB_ALIGN
+        t_end = None
+        while end - int(self.hdr[0]) > self.cap:
+            if t_end is None:
+                t_end = time.time() + wait_s
+            elif time.time() > t_end:
+                return None
+            time.sleep(1e-4)
+        o = self.HDR + pos % self.cap
+        # one native memcpy with the GIL released (several edges copy concurrently)
+        self._native.gather_into(self._base + o, n, [arr], n, 1)
+        self.head = end
+        self.records += 1
+        self.bytes += n
+        return start, pos, end
+
+    # ---- worker
+    def view(self, ref: _SlabRef):
+        o = self.HDR + ref.pos % self.cap
+        n = int(np.prod(ref.shape, dtype=np.int64)) * np.dtype(ref.dtype).itemsize
+        arr = self.mem[o:o + n].view(ref.dtype).reshape(ref.shape)
+        with self._lock:
+            self._pending.append((ref.start, ref.end))
+        weakref.finalize(arr, self._drop, ref.start)
+        return arr
+
+    def _drop(self, start):
+        with self._lock:
+            self._dropped.add(start)
+            rel = None
+            while self._pending and self._pending[0][0] in self._dropped:
+                s0, e0 = self._pending.popleft()
+                self._dropped.discard(s0)
+                rel = e0
+            if rel is not None:
+                self.hdr[0] = rel
+
+    def close(self):
+        """Drops this process's mapping handle (views still alive keep the pages mapped
+        until they are collected)."""
+        self.mem = self.hdr = None
+        self._mm = None
+
+    def unlink(self):
+        if self.owner:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+            self.owner = False
+
+
+def _to_slab(value, slab: TensorSlab):
+    """``value`` with a large contiguous payload moved into the slab (else unchanged)."""
+    import torch
+
+    from ..types.tensor_value import TensorValue
+
+    kind, arr, tvd = None, None, None
+    if isinstance(value, np.ndarray) and value.dtype != object:
+        kind, arr = "np", value
+    elif isinstance(value, torch.Tensor) and value.device.type == "cpu" and value.dtype != torch.bfloat16:
+        kind, arr = "torch", value.detach().numpy()
+    elif isinstance(value, TensorValue):
+        p = value._payload
+        if isinstance(p, np.ndarray):
+            arr = p
+        elif isinstance(p, (bytes, bytearray, memoryview)):
+            arr = np.frombuffer(p, np.uint8)
+        if arr is not None:
+            kind, tvd = "tv", (int(value.dtype), value.shape())
+    if arr is None or arr.nbytes < _SLAB_MIN:
+        return value
+    arr = np.ascontiguousarray(arr)
+    got = slab.put(arr)
+    if got is None:
+        return value
+    return _SlabRef(*got, arr.shape, arr.dtype.str, kind, tvd)
+
+
+def _from_slab(value, slab: TensorSlab):
+    if not isinstance(value, _SlabRef):
+        return value
+    arr = slab.view(value)
+    if value.kind == "torch":
+        import torch
+
+        return torch.from_numpy(arr)
+    if value.kind == "tv":
+        from ..types.tensor_value import TensorValue
+
+        dt, shape = value.tv_dtype
+        return TensorValue(dt, shape, arr)
+    return arr
 
 
 class RemoteTaskError(RuntimeError):
@@ -89,9 +263,10 @@ class ShmChannel:
 
 
 # ------------------------------------------------------------------ worker side
-def _worker_main(in_name: str, out_name: str):
+def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
     inp = ShmChannel(in_name, create=False)
     out = ShmChannel(out_name, create=False)
+    slab = TensorSlab(slab_name, create=False) if slab_name else None
     op = None
     pending: list = []
     parent = os.getppid()
@@ -151,7 +326,7 @@ def _worker_main(in_name: str, out_name: str):
             kind = msg[0]
             if kind == "recs":
                 for value, ts, idx in msg[1]:
-                    op.process(Record(value, ts), idx)
+                    op.process(Record(_from_slab(value, slab) if slab is not None else value, ts), idx)
                     metrics.inc("records_in")
             elif kind == "wm":
                 op.process_watermark(Watermark(msg[1]))
@@ -204,6 +379,7 @@ class RemoteOperatorProxy:
         self.num_inputs = 1
         self.ring_bytes = ring_bytes
         self.to_worker = self.from_worker = None  # created when the subtask starts
+        self.slab: TensorSlab | None = None
         self.proc = None
         self.out: Output | None = None
         self.ctx = None
@@ -232,8 +408,10 @@ class RemoteOperatorProxy:
         tag = f"/ftm-{os.getpid()}-{uuid.uuid4().hex[:10]}"
         self.to_worker = ShmChannel(tag + "-in", True, self.ring_bytes)
         self.from_worker = ShmChannel(tag + "-out", True, self.ring_bytes)
+        self.slab = TensorSlab(tag + "-slab", True) if _SLAB_BYTES > 0 else None
         self.proc = mp.get_context("spawn").Process(target=_worker_main, name=f"ftm-{self.node.name}-{self.subtask}",
-                                                    args=(self.to_worker.name, self.from_worker.name), daemon=True)
+                                                    args=(self.to_worker.name, self.from_worker.name,
+                                                          self.slab.name if self.slab else None), daemon=True)
         self.proc.start()
         self._drainer = threading.Thread(target=self._drain, name=f"drain-{self.node.name}-{self.subtask}",
                                          daemon=True)
@@ -241,6 +419,8 @@ class RemoteOperatorProxy:
         self._wait("attached", 120.0)
         self.to_worker.unlink()  # both ends are mapped: the names can go (no /dev/shm leak on a crash)
         self.from_worker.unlink()
+        if self.slab is not None:
+            self.slab.unlink()
         spec = {"name": self.node.name, "subtask": self.subtask, "parallelism": self.node.parallelism,
                 "gpu": bool(self.node.uses_gpu), "attempt": self.job.attempt, "config": self.job.config,
                 "global_index": self.ctx.global_index, "global_parallelism": self.ctx.global_parallelism}
@@ -275,10 +455,15 @@ class RemoteOperatorProxy:
         for ch in (self.to_worker, self.from_worker):
             if ch is not None:
                 ch.unlink()
+        if self.slab is not None:
+            self.slab.unlink()
+            self.slab.close()
+            self.slab = None
 
     # ---- data path
     def process(self, rec: Record, input_index: int = 0):
-        self._buf.append((rec.value, rec.ts, input_index))
+        v = rec.value if self.slab is None else _to_slab(rec.value, self.slab)
+        self._buf.append((v, rec.ts, input_index))
         if len(self._buf) >= _BATCH:
             self._flush()
 
