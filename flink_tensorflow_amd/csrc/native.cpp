@@ -799,6 +799,44 @@ std::vector<std::pair<py::bytes, py::bytes>> sstable_parse(const py::buffer& buf
 }
 
 // ----------------------------------------------------------------------------------
+// Copy of many payloads to per-payload offsets of one destination region (the
+// worker-process tensor slab: a micro-batch of records of any sizes in one call).
+// ----------------------------------------------------------------------------------
+void scatter_into(uintptr_t dst, size_t dst_bytes, const std::vector<size_t>& offs, const py::list& srcs,
+                  int nthreads) {
+  if (offs.size() != srcs.size()) throw std::runtime_error("scatter_into: offsets / sources length mismatch");
+  std::vector<std::pair<const uint8_t*, size_t>> v;
+  std::vector<py::buffer_info> keep;
+  keep.reserve(srcs.size());
+  size_t total = 0;
+  for (size_t i = 0; i < offs.size(); ++i) {
+    keep.emplace_back(srcs[i].cast<py::buffer>().request());
+    auto& bi = keep.back();
+    size_t nb = size_t(bi.size * bi.itemsize);
+    if (offs[i] + nb > dst_bytes) throw std::runtime_error("scatter_into: payload beyond the destination");
+    v.emplace_back(static_cast<const uint8_t*>(bi.ptr), nb);
+    total += nb;
+  }
+  uint8_t* d = reinterpret_cast<uint8_t*>(dst);
+  py::gil_scoped_release nogil;
+  auto work = [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) std::memcpy(d + offs[i], v[i].first, v[i].second);
+  };
+  int nt = std::max(1, std::min<int>(nthreads, int(v.size())));
+  if (nt == 1 || total < (1u << 20)) {
+    work(0, v.size());
+    return;
+  }
+  std::vector<std::thread> th;
+  size_t chunk = (v.size() + nt - 1) / nt;
+  for (int t = 0; t < nt; ++t) {
+    size_t lo = t * chunk, hi = std::min(v.size(), lo + chunk);
+    if (lo < hi) th.emplace_back(work, lo, hi);
+  }
+  for (auto& t : th) t.join();
+}
+
+// ----------------------------------------------------------------------------------
 // Gather-copy of many record payloads into one contiguous destination (a pinned
 // staging slot).  Releases the GIL and fans the copy across threads.
 // ----------------------------------------------------------------------------------
@@ -865,6 +903,8 @@ PYBIND11_MODULE(_native, m) {
   m.def("sstable_parse", &sstable_parse, py::arg("data"), py::arg("verify") = true);
   m.def("gather_into", &gather_into, py::arg("dst"), py::arg("dst_bytes"), py::arg("srcs"), py::arg("stride"),
         py::arg("nthreads") = 8);
+  m.def("scatter_into", &scatter_into, py::arg("dst"), py::arg("dst_bytes"), py::arg("offsets"), py::arg("srcs"),
+        py::arg("nthreads") = 4);
   register_arena(m);
   register_shm_ring(m);
   m.attr("has_sse42") =

@@ -41,6 +41,7 @@ import traceback
 import uuid
 
 import collections
+import sys
 import weakref
 
 import cloudpickle
@@ -105,46 +106,76 @@ class TensorSlab:
         if create:
             self.hdr[0] = 0
         self.head = 0
-        self.records = self.bytes = 0
+        self.records = self.bytes = self.waits = 0
         # worker side
         self._lock = threading.Lock()
         self._pending: collections.deque = collections.deque()
         self._dropped: set = set()
 
     # ---- coordinator
-    def put(self, arr: np.ndarray, wait_s: float = 0.05):
-        """Copies ``arr`` (contiguous) in; returns (start, pos, end) or None (no room)."""
-        n = arr.nbytes
-        if n > self.cap // 4:
+    def reserve(self, nbytes: int, wait_s: float = 0.05):
+        """Reserves ``nbytes`` contiguous bytes: (start, pos) or None (no room in time)."""
+        if nbytes > self.cap // 2:
             return None
         off = self.head % self.cap
         start = self.head
-        pos = self.head + (self.cap - off if off + n > self.cap else 0)
-        end = pos + -(-n // _SLAB_ALIGN) * _SLAB_ALIGN
+        pos = self.head + (self.cap - off if off + nbytes > self.cap else 0)
         t_end = None
-        while end - int(self.hdr[0]) > self.cap:
+        while pos + nbytes - int(self.hdr[0]) > self.cap:
+            self.waits += 1
             if t_end is None:
                 t_end = time.time() + wait_s
             elif time.time() > t_end:
                 return None
             time.sleep(1e-4)
-        o = self.HDR + pos % self.cap
-        # one native memcpy with the GIL released (several edges copy concurrently)
-        self._native.gather_into(self._base + o, n, [arr], n, 1)
-        self.head = end
-        self.records += 1
-        self.bytes += n
-        return start, pos, end
+        return start, pos
+
+    def put_batch(self, batch: list) -> list:
+        """``batch`` of (value, ts, input) with every large payload copied in (ONE native
+        multithreaded scatter for the micro-batch, GIL released) and replaced by its
+        descriptor; values that do not qualify, or a batch that finds no room, stay as
+        they are (pickled)."""
+        picks = []
+        for i, (v, _ts, _ix) in enumerate(batch):
+            a = _payload(v)
+            if a is not None:
+                picks.append((i, a))
+        if not picks:
+            return batch
+        sizes = [-(-a[1].nbytes // _SLAB_ALIGN) * _SLAB_ALIGN for _, a in picks]
+        got = self.reserve(sum(sizes))
+        if got is None:
+            return batch
+        start, pos = got
+        offs, refs, cur = [], [], pos
+        out = list(batch)
+        for (i, (kind, arr, tvd)), sz in zip(picks, sizes):
+            offs.append(self.HDR + cur % self.cap)
+            refs.append(arr)
+            v, ts, ix = batch[i]
+            out[i] = (_SlabRef(start if cur == pos else cur, cur, cur + sz, arr.shape, arr.dtype.str, kind, tvd),
+                      ts, ix)
+            cur += sz
+        self._native.scatter_into(self._base, self.mem.nbytes, offs, refs, 4)
+        self.head = cur
+        self.records += len(picks)
+        self.bytes += sum(a[1].nbytes for _, a in picks)
+        return out
 
     # ---- worker
-    def view(self, ref: _SlabRef):
+    def view(self, ref: _SlabRef, track: bool = True):
         o = self.HDR + ref.pos % self.cap
         n = int(np.prod(ref.shape, dtype=np.int64)) * np.dtype(ref.dtype).itemsize
         arr = self.mem[o:o + n].view(ref.dtype).reshape(ref.shape)
         with self._lock:
             self._pending.append((ref.start, ref.end))
-        weakref.finalize(arr, self._drop, ref.start)
+        if track:
+            self.track(arr, ref.start)
         return arr
+
+    def track(self, arr, start: int) -> None:
+        """Releases the record's space when ``arr`` (and every view of it) is collected."""
+        weakref.finalize(arr, self._drop, start)
 
     def _drop(self, start):
         with self._lock:
@@ -172,17 +203,19 @@ class TensorSlab:
             self.owner = False
 
 
-def _to_slab(value, slab: TensorSlab):
-    """``value`` with a large contiguous payload moved into the slab (else unchanged)."""
+def _payload(value):
+    """(kind, contiguous ndarray, TensorValue meta) of a slab-eligible record, else None."""
     import torch
 
     from ..types.tensor_value import TensorValue
 
     kind, arr, tvd = None, None, None
-    if isinstance(value, np.ndarray) and value.dtype != object:
-        kind, arr = "np", value
-    elif isinstance(value, torch.Tensor) and value.device.type == "cpu" and value.dtype != torch.bfloat16:
-        kind, arr = "torch", value.detach().numpy()
+    if isinstance(value, np.ndarray):
+        if value.dtype != object:
+            kind, arr = "np", value
+    elif isinstance(value, torch.Tensor):
+        if value.device.type == "cpu" and value.dtype != torch.bfloat16:
+            kind, arr = "torch", value.detach().numpy()
     elif isinstance(value, TensorValue):
         p = value._payload
         if isinstance(p, np.ndarray):
@@ -192,12 +225,8 @@ def _to_slab(value, slab: TensorSlab):
         if arr is not None:
             kind, tvd = "tv", (int(value.dtype), value.shape())
     if arr is None or arr.nbytes < _SLAB_MIN:
-        return value
-    arr = np.ascontiguousarray(arr)
-    got = slab.put(arr)
-    if got is None:
-        return value
-    return _SlabRef(*got, arr.shape, arr.dtype.str, kind, tvd)
+        return None
+    return kind, np.ascontiguousarray(arr), tvd
 
 
 def _from_slab(value, slab: TensorSlab):
@@ -326,7 +355,19 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
             kind = msg[0]
             if kind == "recs":
                 for value, ts, idx in msg[1]:
-                    op.process(Record(_from_slab(value, slab) if slab is not None else value, ts), idx)
+                    if slab is not None and isinstance(value, _SlabRef) and value.kind == "np":
+                        # plain ndarray records: if the operator kept no reference once
+                        # process() returns (maps, batch staging copies), release at once;
+                        # otherwise (windows, pending micro-batches) when it is collected
+                        v = slab.view(value, track=False)
+                        op.process(Record(v, ts), idx)
+                        if sys.getrefcount(v) <= 2:
+                            slab._drop(value.start)
+                        else:
+                            slab.track(v, value.start)
+                        del v
+                    else:
+                        op.process(Record(_from_slab(value, slab) if slab is not None else value, ts), idx)
                     metrics.inc("records_in")
             elif kind == "wm":
                 op.process_watermark(Watermark(msg[1]))
@@ -456,14 +497,16 @@ class RemoteOperatorProxy:
             if ch is not None:
                 ch.unlink()
         if self.slab is not None:
+            if os.environ.get("FTM_SLAB_DEBUG"):
+                print(f"[slab] {self.node.name}[{self.subtask}] records={self.slab.records} "
+                      f"bytes={self.slab.bytes} waits={self.slab.waits} head={self.slab.head}", flush=True)
             self.slab.unlink()
             self.slab.close()
             self.slab = None
 
     # ---- data path
     def process(self, rec: Record, input_index: int = 0):
-        v = rec.value if self.slab is None else _to_slab(rec.value, self.slab)
-        self._buf.append((v, rec.ts, input_index))
+        self._buf.append((rec.value, rec.ts, input_index))
         if len(self._buf) >= _BATCH:
             self._flush()
 
@@ -506,6 +549,8 @@ class RemoteOperatorProxy:
     def _flush(self):
         if self._buf:
             batch, self._buf = self._buf, []
+            if self.slab is not None:
+                batch = self.slab.put_batch(batch)
             self._send(("recs", batch))
 
     def _check(self):
