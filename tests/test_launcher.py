@@ -44,7 +44,7 @@ def _train(rank, world, attempt, ckpt_dir, fault):
 
 @pytest.mark.parametrize("fault", ["crash", "hang"])
 def test_restart_after_failure(tmp_path, fault):
-    rep = launch(_train, 2, args=(str(tmp_path), fault), communicator=FakeCommunicator, max_restarts=1, heartbeat_timeout=5.0,
+    rep = launch(_train, 2, args=(str(tmp_path), fault), communicator=FakeCommunicator, max_restarts=1, heartbeat_timeout=15.0,
                  timeout=120)
     assert rep.attempts == 2 and len(rep.failures) == 1
     assert ("exited with code 3" in rep.failures[0]) if fault == "crash" else ("missed heartbeats" in rep.failures[0])
