@@ -14,6 +14,9 @@
   ``*.jpg``/``*.jpeg`` file (``*.crdownload`` excluded; filters merged, B8); JPEG decode
   on the host (Pillow), normalization either on the host through ``ImageNormalization``
   (reference behaviour) or deferred to the fused GPU preprocess kernel.
+* The package type aliases of ``EX/inception/package.scala:7-30`` (``ImageTensor``,
+  ``ImageTensorValue``, ``ImageFile``, ``ImageFileTensor``, ``LabelTensor``): runtime-checked
+  ``TypeTag``s (rank + element type) usable with ``tagged_as``.
 """
 from __future__ import annotations
 
@@ -29,8 +32,26 @@ from ...types.tensor import StringTensor
 from ...types.tensor_value import TensorValue
 from ...utils import fs
 from ..core import GenericModel, GraphDefGraphLoader, GraphLoader, ModelFunction
+from ...types.names import TypedTensor, tagged_as
 from ..signatures import LambdaMethod
 from .image_classifier import ImageClassifierModel
+
+# ---- EX/inception/package.scala:7-30
+ImageTensor = TypedTensor(4, "FLOAT")          # TypedTensor[`4D`, Float]: [N, H, W, 3] normalized
+ImageTensorValue = ImageTensor                 # TensorValue[`4D`, Float] (checked on to_tensor())
+ImageFile = "ImageFile"                        # the ByteString tag of an encoded image file
+ImageFileTensor = TypedTensor(0, "STRING")     # TypedTensor[`0D`, ByteString[ImageFile]]
+LabelTensor = TypedTensor(2, "FLOAT")          # TypedTensor[`2D`, Float]: [N, classes] scores
+
+
+def as_image_tensor(t):
+    """``t.taggedAs[ImageTensor]`` (rank-4 float, checked)."""
+    return tagged_as(t, ImageTensor)
+
+
+def as_label_tensor(t):
+    """``t.taggedAs[LabelTensor]`` (rank-2 float, checked)."""
+    return tagged_as(t, LabelTensor)
 
 IMAGE_H = IMAGE_W = 224
 MEAN = 117.0

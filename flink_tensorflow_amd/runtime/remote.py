@@ -58,17 +58,17 @@ _BATCH = 64
 _IDLE_S = 0.02
 
 
-class _SlabRef:
-    """Descriptor of a record payload in the tensor slab (what crosses the ring)."""
+_SLAB_TAG = "__ftm_slab_ref__"
 
-    __slots__ = ("start", "pos", "end", "shape", "dtype", "kind", "tv_dtype")
 
-    def __init__(self, start, pos, end, shape, dtype, kind, tv_dtype=None):
-        self.start, self.pos, self.end = start, pos, end
-        self.shape, self.dtype, self.kind, self.tv_dtype = shape, dtype, kind, tv_dtype
+def _SlabRef(start, pos, end, shape, dtype, kind, tv_dtype=None):  # noqa: N802
+    """Descriptor of a record payload in the tensor slab (what crosses the ring): a plain
+    tuple, so pickling it stays on the C fast path."""
+    return (_SLAB_TAG, start, pos, end, shape, dtype, kind, tv_dtype)
 
-    def __reduce__(self):
-        return (_SlabRef, (self.start, self.pos, self.end, self.shape, self.dtype, self.kind, self.tv_dtype))
+
+def _is_ref(v) -> bool:
+    return type(v) is tuple and len(v) == 8 and v[0] == _SLAB_TAG
 
 
 class TensorSlab:
@@ -163,14 +163,16 @@ class TensorSlab:
         return out
 
     # ---- worker
-    def view(self, ref: _SlabRef, track: bool = True):
-        o = self.HDR + ref.pos % self.cap
-        n = int(np.prod(ref.shape, dtype=np.int64)) * np.dtype(ref.dtype).itemsize
-        arr = self.mem[o:o + n].view(ref.dtype).reshape(ref.shape)
+    def view(self, ref, track: bool = True):
+        _, start, pos, end, shape, dtype, _kind, _tvd = ref
+        o = self.HDR + pos % self.cap
+        dt = np.dtype(dtype)
+        n = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
+        arr = self.mem[o:o + n].view(dt).reshape(shape)
         with self._lock:
-            self._pending.append((ref.start, ref.end))
+            self._pending.append((start, end))
         if track:
-            self.track(arr, ref.start)
+            self.track(arr, start)
         return arr
 
     def track(self, arr, start: int) -> None:
@@ -203,20 +205,30 @@ class TensorSlab:
             self.owner = False
 
 
+_TYPES: list = []
+
+
 def _payload(value):
     """(kind, contiguous ndarray, TensorValue meta) of a slab-eligible record, else None."""
-    import torch
+    if type(value) is np.ndarray:  # the common case first, no imports / isinstance chain
+        if value.dtype.hasobject or value.nbytes < _SLAB_MIN:
+            return None
+        return "np", (value if value.flags.c_contiguous else np.ascontiguousarray(value)), None
+    if not _TYPES:
+        import torch
 
-    from ..types.tensor_value import TensorValue
+        from ..types.tensor_value import TensorValue
 
+        _TYPES.extend((torch.Tensor, TensorValue, torch.bfloat16))
+    tensor_t, tv_t, bf16 = _TYPES
     kind, arr, tvd = None, None, None
     if isinstance(value, np.ndarray):
-        if value.dtype != object:
+        if not value.dtype.hasobject:
             kind, arr = "np", value
-    elif isinstance(value, torch.Tensor):
-        if value.device.type == "cpu" and value.dtype != torch.bfloat16:
+    elif isinstance(value, tensor_t):
+        if value.device.type == "cpu" and value.dtype != bf16:
             kind, arr = "torch", value.detach().numpy()
-    elif isinstance(value, TensorValue):
+    elif isinstance(value, tv_t):
         p = value._payload
         if isinstance(p, np.ndarray):
             arr = p
@@ -230,17 +242,18 @@ def _payload(value):
 
 
 def _from_slab(value, slab: TensorSlab):
-    if not isinstance(value, _SlabRef):
+    if not _is_ref(value):
         return value
     arr = slab.view(value)
-    if value.kind == "torch":
+    kind = value[6]
+    if kind == "torch":
         import torch
 
         return torch.from_numpy(arr)
-    if value.kind == "tv":
+    if kind == "tv":
         from ..types.tensor_value import TensorValue
 
-        dt, shape = value.tv_dtype
+        dt, shape = value[7]
         return TensorValue(dt, shape, arr)
     return arr
 
@@ -355,16 +368,16 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
             kind = msg[0]
             if kind == "recs":
                 for value, ts, idx in msg[1]:
-                    if slab is not None and isinstance(value, _SlabRef) and value.kind == "np":
+                    if slab is not None and _is_ref(value) and value[6] == "np":
                         # plain ndarray records: if the operator kept no reference once
                         # process() returns (maps, batch staging copies), release at once;
                         # otherwise (windows, pending micro-batches) when it is collected
                         v = slab.view(value, track=False)
                         op.process(Record(v, ts), idx)
                         if sys.getrefcount(v) <= 2:
-                            slab._drop(value.start)
+                            slab._drop(value[1])
                         else:
-                            slab.track(v, value.start)
+                            slab.track(v, value[1])
                         del v
                     else:
                         op.process(Record(_from_slab(value, slab) if slab is not None else value, ts), idx)

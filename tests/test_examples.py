@@ -80,3 +80,19 @@ def test_johnny_cep():
                                               lambda partial, ts: ("AccessDenied", ts)).execute_and_collect()
     assert ("AccessGranted", 4.0) in out
     assert ("AccessDenied", 160.0) in out
+
+
+def test_inception_package_type_aliases():
+    """``EX/inception/package.scala:7-30`` aliases: rank / dtype checked at tagging time."""
+    import torch
+
+    from flink_tensorflow_amd.models.zoo import inception as I
+    from flink_tensorflow_amd.types.tensor import StringTensor
+
+    assert I.as_image_tensor(torch.zeros(2, 224, 224, 3)).shape == (2, 224, 224, 3)
+    assert I.as_label_tensor(torch.zeros(2, 1008)).shape == (2, 1008)
+    I.ImageFileTensor.check(StringTensor([b"\xff\xd8jpeg"], ()))
+    with pytest.raises(TypeError):
+        I.as_image_tensor(torch.zeros(224, 224, 3))
+    with pytest.raises(TypeError):
+        I.as_label_tensor(torch.zeros(2, 1008, dtype=torch.int32))
