@@ -429,6 +429,61 @@ int64_t decode_feature(const FeatureRef& fr, int kind, float* fdst, int64_t* ids
   return count;
 }
 
+// Var-length (sparse) features of N serialized Examples: per spec (key, kind FLOAT/INT64)
+// returns (row_splits int64 [N+1], values [nnz]) — the CSR form ParseExample turns into
+// sparse (indices, values, dense_shape).  Two passes: count, then decode in place.
+py::list parse_examples_varlen(const std::vector<py::bytes>& serialized, const py::list& specs_py) {
+  std::vector<std::pair<std::string, int>> specs;
+  std::unordered_map<std::string, int> want;
+  for (auto h : specs_py) {
+    auto t = h.cast<py::tuple>();
+    int kind = t[1].cast<int>();
+    if (kind == kBytes) throw std::runtime_error("var-length bytes features are parsed in Python");
+    want[t[0].cast<std::string>()] = int(specs.size());
+    specs.emplace_back(t[0].cast<std::string>(), kind);
+  }
+  const size_t N = serialized.size(), S = specs.size();
+  std::vector<std::string_view> views(N);
+  for (size_t i = 0; i < N; ++i) {
+    char* ptr;
+    py::ssize_t len;
+    PYBIND11_BYTES_AS_STRING_AND_SIZE(serialized[i].ptr(), &ptr, &len);
+    views[i] = std::string_view(ptr, size_t(len));
+  }
+  std::vector<std::vector<int64_t>> splits(S, std::vector<int64_t>(N + 1, 0));
+  std::vector<std::vector<FeatureRef>> refs(N, std::vector<FeatureRef>(S));
+  {
+    py::gil_scoped_release nogil;
+    for (size_t i = 0; i < N; ++i) {
+      example_features(reinterpret_cast<const uint8_t*>(views[i].data()), views[i].size(), want, refs[i]);
+      for (size_t s = 0; s < S; ++s) {
+        int64_t c = refs[i][s].p ? decode_feature(refs[i][s], specs[s].second, nullptr, nullptr, 0) : 0;
+        splits[s][i + 1] = splits[s][i] + c;
+      }
+    }
+  }
+  py::list out;
+  for (size_t s = 0; s < S; ++s) {
+    const int64_t nnz = splits[s][N];
+    py::array_t<int64_t> rs{py::ssize_t(N + 1)};
+    std::memcpy(rs.mutable_data(), splits[s].data(), (N + 1) * sizeof(int64_t));
+    if (specs[s].second == kFloat) {
+      py::array_t<float> v{py::ssize_t(nnz)};
+      float* d = v.mutable_data();
+      for (size_t i = 0; i < N; ++i)
+        if (refs[i][s].p) decode_feature(refs[i][s], kFloat, d + splits[s][i], nullptr, splits[s][i + 1] - splits[s][i]);
+      out.append(py::make_tuple(rs, v));
+    } else {
+      py::array_t<int64_t> v{py::ssize_t(nnz)};
+      int64_t* d = v.mutable_data();
+      for (size_t i = 0; i < N; ++i)
+        if (refs[i][s].p) decode_feature(refs[i][s], kInt64, nullptr, d + splits[s][i], splits[s][i + 1] - splits[s][i]);
+      out.append(py::make_tuple(rs, v));
+    }
+  }
+  return out;
+}
+
 py::list parse_examples(const std::vector<py::bytes>& serialized, const py::list& specs_py, int nthreads) {
   std::vector<DenseSpec> specs;
   std::unordered_map<std::string, int> want;
@@ -895,6 +950,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("pb_packed_varints", &pb_packed_varints, py::arg("data"), py::arg("zigzag") = false);
   m.def("pb_encode_varints", &pb_encode_varints);
   m.def("parse_examples", &parse_examples, py::arg("serialized"), py::arg("specs"), py::arg("nthreads") = 8);
+  m.def("parse_examples_varlen", &parse_examples_varlen, py::arg("serialized"), py::arg("specs"));
   m.def("encode_float_examples", &encode_float_examples);
   m.def("string_tensor_pack", &string_tensor_pack);
   m.def("string_tensor_unpack", &string_tensor_unpack);

@@ -17,7 +17,7 @@ import torch
 
 from ..io import bundle
 from ..types.dtypes import DataType
-from ..types.example import BYTES, FLOAT, INT64, parse_example_dense
+from ..types.example import BYTES, FLOAT, INT64, parse_example_dense, parse_example_varlen
 from ..types.tensor import StringTensor
 from .op_registry import register
 
@@ -38,14 +38,28 @@ def _str(t) -> str:
 # ------------------------------------------------------------------ ParseExample
 @register("ParseExample")
 def _parse_example(ctx, node, serialized, names, *rest):
+    """TF ``ParseExample``: outputs ``sparse_indices[Nsparse]``, ``sparse_values[Nsparse]``,
+    ``sparse_shapes[Nsparse]``, then ``dense_values[Ndense]``.  Sparse (``VarLenFeature``)
+    keys come back as (indices [nnz, 2], values [nnz], dense_shape [2] = [N, max len])."""
     ns = node.attr("Nsparse", 0)
     nd = node.attr("Ndense", 0)
-    if ns:
-        raise NotImplementedError("sparse features in ParseExample")
     sparse_keys = rest[:ns]
     dense_keys = rest[ns:ns + nd]
     dense_defaults = rest[ns + nd:]
-    del sparse_keys
+    sparse_out: tuple = ()
+    if ns:
+        stypes = node.attr("sparse_types", []) or []
+        sspecs = []
+        for i in range(ns):
+            dt = stypes[i]
+            kind = FLOAT if dt == DataType.FLOAT else INT64 if dt == DataType.INT64 else BYTES
+            sspecs.append((_strs(sparse_keys[i])[0].decode(), kind, dt))
+        trip = parse_example_varlen(_strs(serialized), [(k, kind) for k, kind, _ in sspecs])
+        idx = tuple(torch.from_numpy(t[0]).to(ctx.device) for t in trip)
+        vals = tuple(StringTensor(v, (len(v),)) if kind == BYTES else torch.from_numpy(v).to(dt.torch).to(ctx.device)
+                     for (_, kind, dt), (_, v, _) in zip(sspecs, trip))
+        shp = tuple(torch.from_numpy(t[2]).to(ctx.device) for t in trip)
+        sparse_out = idx + vals + shp
     tdense = node.attr("Tdense", []) or []
     shapes = node.attr("dense_shapes", []) or []
     specs = []
@@ -63,8 +77,8 @@ def _parse_example(ctx, node, serialized, names, *rest):
         kind = FLOAT if dt == DataType.FLOAT else INT64 if dt == DataType.INT64 else BYTES
         specs.append((key, kind, numel, dflt_v, dt, shp))
     ser = _strs(serialized)
-    arrs = parse_example_dense(ser, [(k, kind, n, d) for k, kind, n, d, _, _ in specs])
-    outs = []
+    arrs = parse_example_dense(ser, [(k, kind, n, d) for k, kind, n, d, _, _ in specs]) if specs else []
+    outs = list(sparse_out)
     for (k, kind, n, d, dt, shp), a in zip(specs, arrs):
         shape = (len(ser), *shp)
         if kind == BYTES:

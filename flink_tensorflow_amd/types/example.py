@@ -91,6 +91,38 @@ def parse_example_dense(serialized: Sequence[bytes], specs: Sequence[tuple[str, 
     return out
 
 
+def parse_example_varlen(serialized: Sequence[bytes], specs: Sequence[tuple[str, int]]):
+    """Var-length (``VarLenFeature`` / sparse) features of N serialized Examples as TF's
+    sparse triples ``(indices int64 [nnz, 2], values [nnz], dense_shape int64 [2])`` per
+    spec ``(key, kind)``; numeric kinds are decoded by the C++ parser, BYTES in Python."""
+    ser = [bytes(s) for s in serialized]
+    n = len(ser)
+    numeric = [(i, (k, kind)) for i, (k, kind) in enumerate(specs) if kind != BYTES]
+    csr: list = [None] * len(specs)
+    if numeric:
+        for (i, _), got in zip(numeric, _ext.native().parse_examples_varlen(ser, [s for _, s in numeric])):
+            csr[i] = got
+    for i, (k, kind) in enumerate(specs):
+        if kind != BYTES:
+            continue
+        vals, splits = [], [0]
+        for s in ser:
+            ex = Example.decode(s)
+            f = ex.features.feature.get(k) if ex.features else None
+            v = list(f.bytes_list.value) if f is not None and f.bytes_list is not None else []
+            vals.extend(v)
+            splits.append(splits[-1] + len(v))
+        csr[i] = (np.asarray(splits, np.int64), np.asarray(vals, dtype=object))
+    out = []
+    for splits, vals in csr:
+        lens = np.diff(splits)
+        rows = np.repeat(np.arange(n, dtype=np.int64), lens)
+        cols = np.arange(len(vals), dtype=np.int64) - np.repeat(splits[:-1], lens)
+        out.append((np.stack([rows, cols], 1) if len(vals) else np.zeros((0, 2), np.int64), vals,
+                    np.asarray([n, int(lens.max()) if n else 0], np.int64)))
+    return out
+
+
 def encode_float_examples(columns: dict[str, np.ndarray]) -> list[bytes]:
     """Serializes N examples with float features in C++ (synthetic load generation)."""
     keys = list(columns)

@@ -153,3 +153,42 @@ def test_parse_example_dense(native):
         parse_example_dense(exs, [("missing", FLOAT, 1, None)])
     enc = encode_float_examples({"x": np.arange(6, dtype=np.float32).reshape(3, 2)})
     assert [Example.decode(e).features.feature["x"].float_list.value for e in enc] == [[0, 1], [2, 3], [4, 5]]
+
+
+def test_parse_example_sparse_and_dense_features():
+    """TF ``ParseExample`` with ``VarLenFeature`` keys (int64 and bytes) next to a dense
+    float key: sparse (indices, values, dense_shape) outputs come first, in TF's order.
+    Expected values are written out by hand from the records below (TF is not importable
+    here; the layout follows the op's documented output order — parity unpinned)."""
+    import numpy as np
+    import torch
+
+    from flink_tensorflow_amd.graph.builder import GraphBuilder
+    from flink_tensorflow_amd.graph.graph import Graph
+    from flink_tensorflow_amd.graph.session import Session
+    from flink_tensorflow_amd.proto.messages import TensorShapeProto
+    from flink_tensorflow_amd.types.dtypes import DataType
+    from flink_tensorflow_amd.types.example import make_example
+    from flink_tensorflow_amd.types.tensor import StringTensor
+
+    b = GraphBuilder()
+    ser = b.placeholder("ser", "STRING", [None])
+    names = b.constant("names", np.asarray([], dtype=object))
+    k_ids = b.constant("k_ids", np.asarray(b"ids", dtype=object))
+    k_tags = b.constant("k_tags", np.asarray(b"tags", dtype=object))
+    k_x = b.constant("k_x", np.asarray(b"x", dtype=object))
+    d_x = b.constant("d_x", np.asarray([-1.0], dtype=np.float32))
+    b.op("ParseExample", [ser, names, k_ids, k_tags, k_x, d_x], name="parse", Nsparse=2, Ndense=1,
+         sparse_types=[DataType.INT64, DataType.STRING], Tdense=[DataType.FLOAT],
+         dense_shapes=[TensorShapeProto.of([1])])
+    g = Graph.from_graph_def(b.build_graph_def())
+    exs = [make_example(ids=[5, 6, 7], tags=[b"a"], x=[1.5]), make_example(tags=[b"b", b"c"]),
+           make_example(ids=[9], x=[2.5])]
+    feed = StringTensor([e.encode() for e in exs], (3,))
+    out = Session(g).run([f"parse:{i}" for i in range(7)], {"ser:0": feed})
+    ids_i, tags_i, ids_v, tags_v, ids_s, tags_s, x = out
+    assert ids_i.tolist() == [[0, 0], [0, 1], [0, 2], [2, 0]] and ids_v.tolist() == [5, 6, 7, 9]
+    assert ids_v.dtype == torch.int64 and ids_s.tolist() == [3, 3]
+    assert tags_i.tolist() == [[0, 0], [1, 0], [1, 1]] and tags_v.tolist() == [b"a", b"b", b"c"]
+    assert tags_s.tolist() == [3, 2]
+    assert x.reshape(-1).tolist() == [1.5, -1.0, 2.5]
