@@ -107,7 +107,8 @@ def main():
         from flink_tensorflow_amd.models.zoo.inception_v3 import inception_v3_flops_per_image, inception_v3_graph_def
 
         graph = Graph.from_graph_def(inception_v3_graph_def(image_hw=(HW, HW), top_k=5, seed=0))
-        sizes = sorted({B} | {int(b) for b in (args.buckets or "").split(",") if b})
+        sizes = sorted({B} | {int(b) for b in (args.buckets or "").split(",") if b}
+                       | (set(range(max(32, B // 4), B, 32)) if args.dynamic and not args.buckets else set()))
         rng = np.random.default_rng(1234 + rank)
         pool = rng.integers(0, 256, size=(args.pool, HW, HW, 3), dtype=np.uint8)
         calib = torch.from_numpy(pool[: min(64, args.pool)])
@@ -129,7 +130,8 @@ def main():
     elif args.model == "resnet50":
         gd = resnet50_graph_def(image_hw=(HW, HW), top_k=5, seed=0)
         graph = Graph.from_graph_def(gd)
-        sizes = sorted({B} | {int(b) for b in (args.buckets or "").split(",") if b})
+        sizes = sorted({B} | {int(b) for b in (args.buckets or "").split(",") if b}
+                       | (set(range(max(32, B // 4), B, 32)) if args.dynamic and not args.buckets else set()))
         for lane in range(lanes):
             arena = DeviceArena(dev, budget, name=f"rank{rank}/lane{lane}")
             plans = {}
