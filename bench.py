@@ -48,10 +48,13 @@ def main():
     ap.add_argument("--depth", type=int, default=3, help="pipeline slots")
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
     ap.add_argument("--pool", type=int, default=512, help="distinct synthetic records cycled by the source")
-    ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert", "widedeep", "inception_v3"],
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert", "bert_graph", "widedeep",
+                                                           "inception_v3"],
                     help="resnet50 = BASELINE headline; bert = BERT-base text-classification stream; "
                          "widedeep = Wide&Deep online training (DP gradient all-reduce); "
-                         "inception_v3 = fp8 Inception-v3 stream with bucketed dynamic batching")
+                         "inception_v3 = fp8 Inception-v3 stream with bucketed dynamic batching; bert_graph = "
+                         "the BERT-base classifier as a TF GraphDef (modeling.py layout) through the graph "
+                         "compiler (padded batches)")
     ap.add_argument("--seq-len", type=int, default=128)
     ap.add_argument("--precision", default=None, choices=["bf16", "fp8"],
                     help="compute precision of the compiled CNN plan (inception_v3 default fp8)")
@@ -147,6 +150,32 @@ def main():
         pool = rng.integers(0, 256, size=(args.pool, HW, HW, 3), dtype=np.uint8)
         model_name, data = "ResNet-50 v1.5", f"synthetic decoded uint8 {HW}x{HW}x3 images, random-init weights"
         seq = None
+    elif args.model == "bert_graph":
+        from flink_tensorflow_amd.models.zoo.bert import BertConfig
+        from flink_tensorflow_amd.models.zoo.bert_graph import bert_graph_def
+
+        cfg = BertConfig.base()
+        seq = args.seq_len
+        gd, _ = bert_graph_def(cfg, seq, seed=rank, mask_from_ids=True)
+        graph = Graph.from_graph_def(gd)
+        for lane in range(lanes):
+            arena = DeviceArena(dev, budget, name=f"rank{rank}/lane{lane}")
+            p = CompiledFunction(graph, {"input_ids:0": ((B, seq), "INT32")}, ["logits:0"], dev,
+                                 use_graph=not args.no_graph, strict=True, arena=arena)
+            lane_plans.append({B: p})
+            params += p.params
+        feed, rec_shape, rec_dtype = "input_ids:0", (seq,), torch.int32
+        rng = np.random.default_rng(1234 + rank)
+        pool = rng.integers(1000, cfg.vocab_size, size=(args.pool, seq), dtype=np.int32)
+        lens = rng.integers(seq // 2, seq + 1, size=args.pool)
+        for i, n in enumerate(lens):
+            pool[i, n:] = 0
+        pool[:, 0] = 101
+        h, it = cfg.hidden, cfg.intermediate
+        flops_per_record = 2.0 * seq * cfg.layers * (4 * h * h + 2 * h * it) + 4.0 * seq * seq * h * cfg.layers
+        model_name = "BERT-base (seq classification), TF GraphDef through the graph compiler"
+        data = (f"synthetic token ids, seq {seq} (real lengths U[{seq // 2},{seq}]), random-init weights, "
+                "padded execution")
     else:
         from flink_tensorflow_amd.models.zoo.bert import (BertConfig, BertDeviceWeights, BertEncoderPlan,
                                                           PackedBertEncoder, init_bert_weights)
@@ -240,7 +269,8 @@ def main():
     flops = flops_per_record * total
     if rank == 0:
         out = {
-            "metric": {"resnet50": METRIC, "bert": METRIC_BERT, "inception_v3": METRIC_INCEPTION}[args.model],
+            "metric": {"resnet50": METRIC, "bert": METRIC_BERT, "bert_graph": METRIC_BERT,
+                       "inception_v3": METRIC_INCEPTION}[args.model],
             "value": round(total, 1),
             "unit": "records/s",
             "n_gpus": ws,
@@ -264,7 +294,7 @@ def main():
             "compile_s": round(compile_s, 2),
             "weights_broadcast_bytes": nbytes,
             "plan": plan.summary() if hasattr(plan, "summary") else {"hip_graph": plan.graph is not None},
-            "arena": arena.stats() if args.model != "bert" else None,
+            "arena": arena.stats() if args.model not in ("bert",) else None,
             "numa_binding_rank0": numa,
             "host_ms_per_batch": {k: round(v * 1e3 / max(1, runner.batches), 3) for k, v in runner.host_s.items()},
         }

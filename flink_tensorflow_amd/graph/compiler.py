@@ -56,6 +56,7 @@ from . import ops_core  # noqa: F401
 from .graph import Graph, Node
 from .op_registry import OpContext, lookup
 from .ops_nn import same_pads
+from .transformer_lowering import TransformerLowering
 
 LOG = logging.getLogger("flink_tensorflow_amd.compiler")
 
@@ -146,7 +147,7 @@ class _ConstSession:
         self._const_cache = {}
 
 
-class CompiledFunction:
+class CompiledFunction(TransformerLowering):
     def __init__(self, graph: Graph, feeds: dict[str, tuple[tuple, Any]], fetches: list[str], device,
                  variables: dict | None = None, use_graph: bool = True, strict: bool = False,
                  topk_fetch: bool = True, precision: str = "bf16", calibration: dict | None = None,
@@ -220,6 +221,8 @@ class CompiledFunction:
         for n in self.order:
             for s, _ in g[n].inputs:
                 self.cons.setdefault(s, []).append(n)
+        self._groups = {}
+        self._prematch_transformer()  # layer_norm / attention / embedding patterns (BERT graphs)
         for f in fed:
             shape, dt = self.feed_specs[str(f)]
             dt = DataType.of(dt).torch
@@ -409,6 +412,9 @@ class CompiledFunction:
     def _lower(self, node: Node):
         if self._fold(node):
             return
+        grp = self._groups.get(node.name)
+        if grp is not None and not grp["done"] and self._lower_group(grp):
+            return
         op = node.op
         if op == "Conv2D":
             return self._lower_conv(node)
@@ -428,6 +434,10 @@ class CompiledFunction:
             return
         if op == "Reshape":
             return self._lower_reshape(node)
+        if op == "StridedSlice" and self._lower_strided_slice(node):
+            return
+        if op in ("Squeeze", "ExpandDims") and self._lower_squeeze_like(node):
+            return
         if op == "ConcatV2":
             return self._lower_concat(node)
         if op == "NoOp":
@@ -1051,6 +1061,12 @@ class CompiledFunction:
         if Kd % 8:
             return self._lower_glue(node)
         last, scale, bias, residual, act, absorbed = self._conv_chain(node)
+        if act == K.ACT_NONE and residual is None:
+            gm = self._match_gelu(last)  # BERT's tanh GELU subgraph -> the GEMM's GELU epilogue
+            if gm is not None:
+                last, extra = gm
+                act = K.ACT_GELU
+                absorbed = absorbed + extra
         if scale is not None:
             w_nk = w_nk * scale[:, None]
         n_pad = -(-N // 8) * 8  # e.g. 1001 classes: zero rows, output rows strided by n_pad
