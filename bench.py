@@ -69,6 +69,10 @@ def main():
                          "arrivals after --warmup x --batch warm-up arrivals")
     ap.add_argument("--max-delay-ms", type=float, default=2.0, help="MicroBatcher deadline (offered-rate mode)")
     ap.add_argument("--no-pack", action="store_true", help="bert: run padded batches (no token packing)")
+    ap.add_argument("--rehearse-fake-comm", action="store_true",
+                    help="REHEARSAL ONLY: several ranks on one GPU exchange through the test loopback "
+                         "communicator (host-staged) instead of RCCL, to exercise the multi-rank control flow "
+                         "of this script where there is one GPU; numbers from such runs are not results")
     ap.add_argument("--lanes", type=int, default=None,
                     help="compute lanes: independent plan instances on their own HIP streams, batches round-robin "
                          "(default: 3 for bert, 2 otherwise; measured in profiles/r01_lanes)")
@@ -83,7 +87,13 @@ def main():
     from flink_tensorflow_amd.parallel import comm
     from flink_tensorflow_amd.utils.metrics import MetricGroup
 
-    comm.init_distributed()
+    if args.rehearse_fake_comm:
+        from flink_tensorflow_amd.parallel.fake import FakeCommunicator
+
+        comm.init_distributed(communicator=FakeCommunicator,
+                              device=f"cuda:{comm.local_device(comm.world()[2])}" if comm.gpu_count() else "cpu")
+    else:
+        comm.init_distributed()
     rank, ws, local = comm.world()
     if ws != args.gpus:
         if rank == 0:
