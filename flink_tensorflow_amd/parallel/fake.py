@@ -25,16 +25,34 @@ class FakeCommunicator(Communicator):
         self._store = store
         self._seq = 0
 
+    _CHUNK = 4 << 20  # the TCP store rejects values above 8 MiB
+
+    def _put(self, key: str, payload: bytes) -> None:
+        n = max(1, -(-len(payload) // self._CHUNK))
+        for i in range(n):
+            self._store.set(f"{key}/{i}", payload[i * self._CHUNK:(i + 1) * self._CHUNK])
+        self._store.set(key, str(n).encode())  # written last: the parts are complete
+
+    def _take(self, key: str) -> bytes:
+        n = int(self._store.get(key))
+        return b"".join(self._store.get(f"{key}/{i}") for i in range(n))
+
+    def _forget(self, key: str) -> None:
+        n = int(self._store.get(key))
+        for i in range(n):
+            self._store.delete_key(f"{key}/{i}")
+        self._store.delete_key(key)
+
     # one round: publish my payload, return everyone's (rank order)
     def _exchange(self, payload: bytes) -> list[bytes]:
         self._seq += 1
         key = f"fake/{self._seq}/"
-        self._store.set(key + str(self.rank), payload)
-        out = [payload if r == self.rank else self._store.get(key + str(r)) for r in range(self.size)]
+        self._put(key + str(self.rank), payload)
+        out = [payload if r == self.rank else self._take(key + str(r)) for r in range(self.size)]
         # the last reader of a round deletes it (bounded store growth over long tests)
         if self._store.add(key + "done", 1) == self.size:
             for r in range(self.size):
-                self._store.delete_key(key + str(r))
+                self._forget(key + str(r))
             self._store.delete_key(key + "done")
         return out
 
