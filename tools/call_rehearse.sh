@@ -4,4 +4,3 @@ TR="python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-ad
 step rehearse_rn 400 $TR --master-port 29541 bench.py --gpus 2 --steps 10 --warmup 3 --rehearse-fake-comm
 step rehearse_wd 400 $TR --master-port 29542 bench.py --gpus 2 --model widedeep --steps 10 --warmup 3 --no-graph --rehearse-fake-comm
 step rehearse_bert 400 $TR --master-port 29543 bench.py --gpus 2 --model bert --steps 10 --warmup 3 --rehearse-fake-comm
-step rccl_ws1_bench 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29544 bench.py --gpus 1 --steps 10 --warmup 3
