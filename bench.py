@@ -411,7 +411,13 @@ def run_widedeep(args, dev, rank, ws):
         return tr.train_step(batch=batch)
 
     if not args.no_graph:  # whole train step as one hipGraph (sync-free sparse path)
-        tr.capture(stager.stage(rows[:B]))
+        try:
+            tr.capture(stager.stage(rows[:B]))
+        except RuntimeError as e:  # e.g. a collective library that cannot be stream-captured
+            print(f"[bench] rank {rank}: whole-step capture failed ({e}); running the step eagerly",
+                  file=sys.stderr)
+            tr._graph = None
+            torch.cuda.synchronize(dev)
 
     for _ in range(args.warmup):
         step()
