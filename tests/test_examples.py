@@ -96,3 +96,34 @@ def test_inception_package_type_aliases():
         I.as_image_tensor(torch.zeros(224, 224, 3))
     with pytest.raises(TypeError):
         I.as_label_tensor(torch.zeros(2, 1008, dtype=torch.int32))
+
+
+def test_bert_stream_over_a_savedmodel(tmp_path):
+    """examples/bert_stream.py: sentences -> tokenizer -> micro-batched BERT SavedModel ->
+    (sentence, label, confidence); every record classified, labels agree with a direct
+    (interpreter) call on the same ids."""
+    import sys
+
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples"))
+    import bert_stream as bs
+
+    from flink_tensorflow_amd.models import PredictMethod, SavedModelModel
+    from flink_tensorflow_amd.models.zoo.bert import BertConfig, HashingTokenizer
+    from flink_tensorflow_amd.models.zoo.bert_graph import export_bert_saved_model
+
+    cfg = BertConfig.tiny()
+    d = export_bert_saved_model(str(tmp_path / "bert"), cfg, 32, seed=1, mask_from_ids=True)
+    env, sink = bs.build_job(d, 40, 8, 32, cfg.vocab_size, delay_ms=1.0)
+    env.execute("bert-stream")
+    out = sorted(sink.results())
+    assert len(out) == 40 and all(0.5 <= c <= 1.0 for _, _, c in out)
+    tok = HashingTokenizer(cfg.vocab_size, 32)
+    m = SavedModelModel(d, device="cpu")
+    m.open()
+    sents = [s for s, _, _ in out]
+    p = m.function("serving_default", PredictMethod(), compile=False).apply(
+        {"input_ids": np.stack([tok(s) for s in sents])})["probabilities"]
+    assert [lab for _, lab, _ in out] == p.argmax(-1).tolist()
+    m.close()
