@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--delay-ms", type=float, default=5.0)
     ap.add_argument("--hw", type=int, default=256)
     ap.add_argument("--depth-layers", type=int, default=50)
+    ap.add_argument("--savedmodel", action="store_true",
+                    help="export ResNet-50 as a TF SavedModel and serve its serving_default signature "
+                         "through SignatureBatchedModel (the path a user's own SavedModel takes)")
     ap.add_argument("--processes", action="store_true",
                     help="run the model operator in a worker process (records cross through the tensor slab)")
     a = ap.parse_args()
@@ -43,7 +46,17 @@ def main():
                 yield pool[i % len(pool)]
 
     env = StreamExecutionEnvironment.get_execution_environment()
-    model = ResNet50Model(image_hw=(a.hw, a.hw), buckets=(a.batch,), depth_layers=a.depth_layers)
+    if a.savedmodel:
+        import tempfile
+
+        from flink_tensorflow_amd.models import SignatureBatchedModel
+        from flink_tensorflow_amd.models.zoo.resnet import export_resnet50_saved_model
+
+        d = export_resnet50_saved_model(os.path.join(tempfile.mkdtemp(), "rn50"), image_hw=(a.hw, a.hw),
+                                        depth=a.depth_layers)
+        model = SignatureBatchedModel(d, buckets=(a.batch,), output_keys=["classes", "scores"])
+    else:
+        model = ResNet50Model(image_hw=(a.hw, a.hw), buckets=(a.batch,), depth_layers=a.depth_layers)
     op = env.generate(images).map_with_model_batched(model, None, max_batch=a.batch, max_delay_ms=a.delay_ms,
                                                      name="resnet50")
     if a.processes:
@@ -54,7 +67,7 @@ def main():
     el = time.time() - t0
     m = [v for k, v in res.metrics.items() if k.startswith("resnet50")][0]
     steady = sink.rate(0.2)  # steady state: skip the first fifth (compile, capture, pipeline fill)
-    print(json.dumps({"records": a.records, "worker_process": a.processes, "seconds": round(el, 3), "records_per_s": round(a.records / el, 1),
+    print(json.dumps({"records": a.records, "savedmodel": a.savedmodel, "worker_process": a.processes, "seconds": round(el, 3), "records_per_s": round(a.records / el, 1),
                       "steady_records_per_s": round(steady, 1) if steady else None,
                       "latency_s": m["histograms"].get("latency_s"), "batch": m["histograms"].get("batch_size")}))
 

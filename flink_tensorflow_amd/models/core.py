@@ -106,6 +106,24 @@ class GraphMethod(abc.ABC):
         ...
 
 
+class BatchedGpuModel(abc.ABC):
+    """Models that run micro-batches asynchronously on the GPU (pinned H2D on a side
+    stream + hipGraph replay).  ``submit`` returns finished batches as
+    ``(results, tags, latencies_s)``; ``drain`` waits for all in-flight batches."""
+
+    @abc.abstractmethod
+    def submit(self, records: list, ingest_ts: np.ndarray, tags: list) -> list:
+        ...
+
+    @abc.abstractmethod
+    def poll(self) -> list:
+        ...
+
+    @abc.abstractmethod
+    def drain(self) -> list:
+        ...
+
+
 class _Outputs(contextlib.AbstractContextManager):
     """Holds a call's outputs; closing releases them (arena slots / HBM references)."""
 

@@ -115,3 +115,13 @@ class FakeCommunicator(Communicator):
 
     def barrier(self):
         self._exchange(b"")
+
+    def destroy(self, abort: bool = False):
+        # rank 0's process usually hosts the store: it must outlive every peer's last store
+        # operation (the final round's deletions), or a peer's request hits a closed socket
+        if abort:
+            return
+        if self.rank != 0:
+            self._store.set(f"fake/closed/{self.rank}", b"1")
+        else:
+            self._store.wait([f"fake/closed/{r}" for r in range(1, self.size)])

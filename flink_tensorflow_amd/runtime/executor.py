@@ -237,7 +237,8 @@ class _Task:
             # or cancelled task must not let an in-flight checkpoint complete without its
             # state (the restart would restore the sources' offsets but lose this task's)
             if done and self.job.coordinator is not None:
-                self.job.coordinator.task_finished((self.uid, self.subtask), getattr(self, "final_state", None))
+                for t in [self] + getattr(self, "chain", []):
+                    self.job.coordinator.task_finished((t.uid, t.subtask), getattr(t, "final_state", None))
 
     def run(self):
         raise NotImplementedError
@@ -277,24 +278,64 @@ class _SourceTask(_Task):
         self.writer.emit(END)
 
 
+class _ChainedTask(_Task):
+    """A subtask chained into its upstream subtask's thread (Flink's operator chaining:
+    forward edge, equal parallelism, single input, single consumer).  It has no thread and
+    no input gate: the chain's head task calls its operator directly, records never cross
+    a queue, and it still has its own metrics, state snapshots and checkpoint acks."""
+
+    def __init__(self, job, node, subtask, restore, op):
+        super().__init__(job, node, subtask, None, restore)
+        self.op = op
+
+    def start(self):
+        pass
+
+
+def _chain_emit(task: _Task):
+    op, inc = task.op, task.metrics.inc
+
+    def emit(elem):
+        if type(elem) is Record:
+            inc("records_in")
+            op.process(elem, 0)
+        elif isinstance(elem, Watermark):
+            op.process_watermark(elem, 0)
+        else:
+            raise TypeError(f"operators emit records and watermarks, not {type(elem).__name__}")
+
+    return emit
+
+
+def _drop_side(tag, value):
+    pass  # no consumer of this side output (as for an unchained operator's writer)
+
+
 class _OpTask(_Task):
-    def __init__(self, job, node, subtask, writer, restore, gate: InputGate, channels: list[int]):
+    def __init__(self, job, node, subtask, writer, restore, gate: InputGate, channels: list[int], op=None,
+                 chain: list[_ChainedTask] | None = None):
         super().__init__(job, node, subtask, writer, restore)
         self.gate = gate
         self.channel_input = dict(channels)  # channel id -> input index
+        self.chain = chain or []
         if getattr(self.node, "remote", False):
             from .remote import RemoteOperatorProxy
 
             self.op = RemoteOperatorProxy(self.node, subtask, job)  # subtask runs in a worker process
         else:
-            self.op = self.node.make_operator()
+            self.op = op if op is not None else self.node.make_operator()
 
     def run(self):
         op = self.op
-        ctx = self.runtime_context()
-        op.setup(ctx, Output(self.writer.emit, self.writer.emit_side))
-        op.initialize(self.restore, self.job.restore_dir)
-        op.open()
+        tasks = [self] + self.chain
+        for i, t in enumerate(tasks):
+            nxt = tasks[i + 1] if i + 1 < len(tasks) else None
+            out = Output(_chain_emit(nxt), _drop_side) if nxt else Output(self.writer.emit, self.writer.emit_side)
+            t.op.setup(t.runtime_context(), out)
+            t.op.initialize(t.restore, self.job.restore_dir)
+        for t in reversed(tasks):  # downstream first: ready before anything is emitted into it
+            t.op.open()
+        ops = [t.op for t in tasks]
         channels = set(self.channel_input)
         finished: set[int] = set()
         wms = {c: float("-inf") for c in channels}
@@ -311,18 +352,21 @@ class _OpTask(_Task):
                 if not replay and finished >= channels:
                     # checked at the top of every iteration: the last EndOfInput may have
                     # completed an alignment whose blocked records were replayed since
-                    op.end_input()
+                    for o in ops:  # in chain order: each flush reaches the next operator
+                        o.end_input()
                     break
                 if replay:
                     ch, elem = replay.popleft()
                 else:
-                    dl = op.next_deadline()
-                    timeout = 0.05 if dl is None else max(0.0, min(0.05, dl - time.time()))
+                    dls = [d for d in (o.next_deadline() for o in ops) if d is not None]
+                    timeout = 0.05 if not dls else max(0.0, min(0.05, min(dls) - time.time()))
                     try:
                         ch, elem = self.gate.q.get(timeout=timeout)
                     except queue.Empty:
                         self.writer.flush()
-                        op.on_idle(time.time())
+                        now = time.time()
+                        for o in ops:
+                            o.on_idle(now)
                         continue
                 if aligning is not None and ch in arrived:
                     # a channel past its barrier is blocked until the alignment completes,
@@ -365,16 +409,22 @@ class _OpTask(_Task):
                             replay.extend(blocked_buf[c])
                             blocked_buf[c].clear()
                         arrived = set()
-                op.on_idle(time.time())
+                now = time.time()
+                for o in ops:
+                    o.on_idle(now)
         finally:
-            op.close()
+            for o in ops:
+                o.close()
         self.writer.emit(Watermark(float("inf")))
         self.writer.emit(END)
 
     def _complete_barrier(self, b: Barrier):
-        self.op.prepare_snapshot()
-        state = self.op.snapshot_state(b.checkpoint_id, self.job.chk_dir(b.checkpoint_id))
-        self.job.ack(b.checkpoint_id, (self.uid, self.subtask), state)
+        # in chain order: an operator's pre-snapshot flush reaches the next one before
+        # that one snapshots, so the chain's state is consistent at the barrier
+        for t in [self] + self.chain:
+            t.op.prepare_snapshot()
+            state = t.op.snapshot_state(b.checkpoint_id, self.job.chk_dir(b.checkpoint_id))
+            self.job.ack(b.checkpoint_id, (t.uid, t.subtask), state)
         self.writer.emit(b)
 
 
@@ -460,15 +510,20 @@ class LocalExecutor:
     def _build(self, restore_states: dict | None):
         nodes = self.env._topo_nodes()
         cap = self.config.channel_capacity
+        ops = {(n.uid, i): n.make_operator() for n in nodes if not n.is_source and not getattr(n, "remote", False)
+               for i in range(n.parallelism)}
+        chained_to = self._chains(nodes, ops)  # downstream uid -> upstream node it runs inside
         gates: dict[tuple[str, int], InputGate] = {}
         chan_of: dict[tuple[str, int], list] = {}
         for n in nodes:
-            if not n.is_source:
+            if not n.is_source and n.uid not in chained_to:
                 for i in range(n.parallelism):
                     gates[(n.uid, i)] = InputGate(cap)
                     chan_of[(n.uid, i)] = []
         out_edges: dict[tuple[str, int], list[_OutEdge]] = {(n.uid, i): [] for n in nodes for i in range(n.parallelism)}
         for n in nodes:
+            if n.uid in chained_to:
+                continue  # fed by direct calls from its upstream operator
             for input_index, (up, part, side_tag) in enumerate(n.inputs):
                 for ui in range(up.parallelism):
                     targets = []
@@ -481,16 +536,59 @@ class LocalExecutor:
                         p = Partitioner("rebalance")
                     out_edges[(up.uid, ui)].append(_OutEdge(p, targets, side_tag))
         self.tasks, self.sources = [], []
+        self.chains = []
+        succ = {up.uid: n for n, up in ((n, chained_to[n.uid]) for n in nodes if n.uid in chained_to)}
         for n in nodes:
+            if n.uid in chained_to:
+                continue  # built with its chain's head
+            members = []
+            m = succ.get(n.uid)
+            while m is not None:
+                members.append(m)
+                m = succ.get(m.uid)
+            if members:
+                self.chains.append([n.name] + [m.name for m in members])
+            tail = members[-1] if members else n
             for i in range(n.parallelism):
-                w = RecordWriter(out_edges[(n.uid, i)], i, self.cancel)
+                w = RecordWriter(out_edges[(tail.uid, i)], i, self.cancel)
                 rs = restore_states.get((n.uid, i)) if restore_states else None
                 if n.is_source:
                     t = _SourceTask(self, n, i, w, rs)
                     self.sources.append(t)
-                else:
-                    t = _OpTask(self, n, i, w, rs, gates[(n.uid, i)], chan_of[(n.uid, i)])
-                self.tasks.append(t)
+                    self.tasks.append(t)
+                    continue
+                chain = [_ChainedTask(self, m, i, restore_states.get((m.uid, i)) if restore_states else None,
+                                      ops[(m.uid, i)]) for m in members]
+                self.tasks.append(_OpTask(self, n, i, w, rs, gates[(n.uid, i)], chan_of[(n.uid, i)],
+                                          ops.get((n.uid, i)), chain))
+                self.tasks.extend(chain)
+
+    def _chains(self, nodes, ops) -> dict:
+        """Operator chaining (Flink's ``StreamingJobGraphGenerator.isChainable``): a node runs
+        inside its upstream's thread when the edge is forward, both have the same
+        parallelism, it has exactly that one input, the upstream has no other consumer, and
+        neither side is a source, a worker-process operator, an operator that cannot chain
+        (two-input) or a node marked ``start_new_chain`` / ``disable_chaining``."""
+        if not getattr(self.env, "chaining", True):
+            return {}
+        consumers: dict[str, int] = {}
+        for n in nodes:
+            for up, _, _ in n.inputs:
+                consumers[up.uid] = consumers.get(up.uid, 0) + 1
+
+        def ok(n):
+            return (not n.is_source and not getattr(n, "remote", False) and getattr(n, "chaining", True)
+                    and ops[(n.uid, 0)].chainable)
+
+        out = {}
+        for n in nodes:
+            if len(n.inputs) != 1 or getattr(n, "chain_head", False):
+                continue
+            up, part, side_tag = n.inputs[0]
+            if (side_tag is None and part.kind == "forward" and up.parallelism == n.parallelism
+                    and consumers.get(up.uid) == 1 and ok(up) and ok(n)):
+                out[n.uid] = up
+        return out
 
     def execute(self) -> JobExecutionResult:
         t0 = time.time()
@@ -527,13 +625,14 @@ class LocalExecutor:
             fl = threading.Thread(target=flusher, name="buffer-flusher", daemon=True)
             fl.start()
             for t in self.tasks:
-                while t.thread.is_alive():
+                while t.thread is not None and t.thread.is_alive():
                     t.thread.join(timeout=0.2)
                     if self.error is not None:
                         break
             if self.error is not None:
                 for t in self.tasks:
-                    t.thread.join(timeout=5)
+                    if t.thread is not None:
+                        t.thread.join(timeout=5)
             stop_flush.set()
             fl.join(timeout=1)
             if self.coordinator is not None:

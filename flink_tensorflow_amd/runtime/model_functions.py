@@ -24,7 +24,7 @@ import time
 
 import numpy as np
 
-from ..models.core import CheckpointedModel, RichModel  # noqa: F401  (re-exported)
+from ..models.core import BatchedGpuModel, CheckpointedModel, RichModel  # noqa: F401  (re-exported)
 from . import functions as F
 from .operators import Collector, Operator, Record
 
@@ -99,24 +99,6 @@ class ModelAllWindowFunction(CheckpointedModelAwareFunction, F.AllWindowFunction
 
 
 # ------------------------------------------------------------------ micro-batching
-class BatchedGpuModel(abc.ABC):
-    """Models that run micro-batches asynchronously on the GPU (pinned H2D on a side
-    stream + hipGraph replay).  ``submit`` returns finished batches as
-    ``(results, tags, latencies_s)``; ``drain`` waits for all in-flight batches."""
-
-    @abc.abstractmethod
-    def submit(self, records: list, ingest_ts: np.ndarray, tags: list) -> list:
-        ...
-
-    @abc.abstractmethod
-    def poll(self) -> list:
-        ...
-
-    @abc.abstractmethod
-    def drain(self) -> list:
-        ...
-
-
 class BatchedModelOperator(Operator):
     def __init__(self, model, batch_fn, max_batch: int, max_delay_ms: float, name: str, emit_batches: bool = False):
         super().__init__(None, name)

@@ -81,6 +81,7 @@ class StreamExecutionEnvironment:
         self.restore_from_latest = False
         self.restart_strategy = RestartStrategy.no_restart()
         self.fault_injector = None
+        self.chaining = True
         from ..parallel.comm import world
 
         self.rank, self.world_size, _ = world()
@@ -98,6 +99,14 @@ class StreamExecutionEnvironment:
 
     def get_parallelism(self) -> int:
         return self.parallelism
+
+    def disable_operator_chaining(self) -> "StreamExecutionEnvironment":
+        """Every operator runs in its own subtask thread (records cross a channel between
+        any two operators); by default forward-connected operators are chained."""
+        self.chaining = False
+        return self
+
+    disableOperatorChaining = disable_operator_chaining
 
     def get_config(self) -> ExecutionConfig:
         return self.config
@@ -179,6 +188,20 @@ class DataStream:
             raise ValueError("sources run in the coordinator process")
         self.node.remote = bool(enable)
         return self
+
+    def start_new_chain(self) -> "DataStream":
+        """This operator starts a new chain: it is not chained into its upstream (its own
+        downstream may still chain into it)."""
+        self.node.chain_head = True
+        return self
+
+    def disable_chaining(self) -> "DataStream":
+        """This operator is chained neither into its upstream nor with its downstream."""
+        self.node.chaining = False
+        return self
+
+    startNewChain = start_new_chain
+    disableChaining = disable_chaining
 
     def name(self, n: str) -> "DataStream":
         self.node.name = n

@@ -115,7 +115,7 @@ def test_bert_stream_over_a_savedmodel(tmp_path):
 
     cfg = BertConfig.tiny()
     d = export_bert_saved_model(str(tmp_path / "bert"), cfg, 32, seed=1, mask_from_ids=True)
-    env, sink = bs.build_job(d, 40, 8, 32, cfg.vocab_size, delay_ms=1.0)
+    env, sink = bs.build_job(d, 40, 8, 32, cfg.vocab_size, delay_ms=1.0, sync=True)
     env.execute("bert-stream")
     out = sorted(sink.results())
     assert len(out) == 40 and all(0.5 <= c <= 1.0 for _, _, c in out)
@@ -126,4 +126,13 @@ def test_bert_stream_over_a_savedmodel(tmp_path):
     p = m.function("serving_default", PredictMethod(), compile=False).apply(
         {"input_ids": np.stack([tok(s) for s in sents])})["probabilities"]
     assert [lab for _, lab, _ in out] == p.argmax(-1).tolist()
+    # default path: SignatureBatchedModel behind the pipelined runner (interpreter on the
+    # host), results (label, confidence) in source order
+    env, sink = bs.build_job(d, 40, 16, 32, cfg.vocab_size, delay_ms=1.0)
+    env.execute("bert-stream-pipelined")
+    got = sink.results()
+    p = m.function("serving_default", PredictMethod(), compile=False).apply(
+        {"input_ids": np.stack([tok(s) for s in bs.sentences(40)])})["probabilities"]
+    assert [lab for lab, _ in got] == p.argmax(-1).tolist()
+    np.testing.assert_allclose([c for _, c in got], p.max(-1).values.numpy(), rtol=1e-5)
     m.close()

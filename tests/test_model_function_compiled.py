@@ -121,3 +121,77 @@ def test_resnet50_savedmodel_compiled_on_gpu(tmp_path):
     torch.testing.assert_close(out2["probabilities"], out["probabilities"][:5])
     assert fn.compiled_plans == 1
     m.close()
+
+
+# ---------------------------------------------------------------- SignatureBatchedModel
+def _submit_all(model, recs, chunk):
+    done = []
+    for s in range(0, len(recs), chunk):
+        part = recs[s:s + chunk]
+        done += model.submit(part, np.zeros(len(part)), list(range(s, s + len(part))))
+    done += model.drain()
+    rows, tags = [], []
+    for r, t, _ in done:
+        rows += r
+        tags += list(t)
+    return rows, tags
+
+
+def test_signature_batched_model_on_the_host(small_resnet):
+    """Any SavedModel signature as a ``BatchedGpuModel``: per-record shape from the
+    signature, results ``{output_key: row}`` in submission order (interpreter on a host)."""
+    from flink_tensorflow_amd.models import SignatureBatchedModel
+
+    m = SignatureBatchedModel(small_resnet, device="cpu", buckets=(4, 8))
+    m.open()
+    assert m._shape == (64, 64, 3) and m._out_keys == ["classes", "probabilities", "scores"]
+    imgs = list(_imgs(11, seed=4))
+    rows, tags = _submit_all(m, imgs, 5)
+    assert tags == list(range(11)) and rows[0]["probabilities"].shape == (10,)
+    ref = SavedModelModel(small_resnet, device="cpu")
+    ref.open()
+    want = ref.function("serving_default", PredictMethod(), compile=False).apply({"images": np.stack(imgs)})
+    np.testing.assert_allclose(np.stack([r["probabilities"] for r in rows]), want["probabilities"].numpy(), rtol=1e-5,
+                               atol=1e-6)
+    ref.close()
+    m.close()
+
+
+def test_signature_batched_model_needs_one_static_input(tmp_path):
+    from flink_tensorflow_amd.models import SignatureBatchedModel
+    from flink_tensorflow_amd.models.zoo.bert import BertConfig
+    from flink_tensorflow_amd.models.zoo.bert_graph import export_bert_saved_model
+
+    d = export_bert_saved_model(str(tmp_path / "bert"), BertConfig.tiny(), 16, seed=0)   # input_ids + input_mask
+    m = SignatureBatchedModel(d, device="cpu")
+    with pytest.raises(ValueError, match="input_key"):
+        m.open()
+
+
+@pytest.mark.gpu
+def test_signature_batched_model_pipelined_on_gpu(small_resnet):
+    """The pipelined path (compiled plan per bucket and lane, pinned H2D, hipGraph) over a
+    user SavedModel agrees with the fp32 interpreter, keeps submission order across lanes
+    and recompiles when a variable is assigned."""
+    from flink_tensorflow_amd.models import SignatureBatchedModel
+
+    m = SignatureBatchedModel(small_resnet, device="cuda:0", buckets=(4, 8), lanes=2)
+    m.open()
+    s = m.plan_summary()
+    assert s["glue_ops"] == [] and s["hip_graph"], s
+    imgs = list(_imgs(29, seed=6))
+    rows, tags = _submit_all(m, imgs, 8)
+    assert tags == list(range(29))
+    ref = SavedModelModel(small_resnet, device="cpu")
+    ref.open()
+    want = ref.function("serving_default", PredictMethod(), compile=False).apply({"images": np.stack(imgs)})
+    got = torch.from_numpy(np.stack([r["probabilities"] for r in rows]))
+    assert (got - want["probabilities"]).abs().max() < 0.05
+    sess = m.session()
+    w = sess.variables["fc/biases"]
+    sess.run(targets=["fc/biases/Assign"], feed_dict={"fc/biases/initial_value:0": w + 5.0 * torch.arange(10.0,
+                                                                                                         device=w.device)})
+    rows, _ = _submit_all(m, imgs[:6], 6)
+    assert [int(r["classes"][0]) for r in rows] == [9] * 6
+    ref.close()
+    m.close()

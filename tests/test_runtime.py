@@ -279,3 +279,58 @@ def test_savedmodel_variables_survive_worker_kill(half_plus_two, tmp_path, check
     assert sorted(late) == list(range(150, 201))
     a = 3.0 if checkpointed else 0.5
     assert all(y == pytest.approx(a * x + 2.0) for x, y in late.items()), sorted(late.items())[:3]
+
+
+# ------------------------------------------------------------------ operator chaining
+def _chain_job(**marks):
+    env = StreamExecutionEnvironment.get_execution_environment()
+    s = env.from_collection(list(range(1000))).map(lambda x: x + 1).name("inc")
+    s = s.filter(lambda x: x % 2 == 0).name("even")
+    if marks.get("new_chain"):
+        s = s.start_new_chain()
+    if marks.get("no_chain"):
+        s = s.disable_chaining()
+    s = s.map(lambda x: x * 10).name("x10")
+    return env, s.collect_into()
+
+
+def test_operator_chaining_forms_chains_and_keeps_per_operator_metrics():
+    """Forward-connected operators with equal parallelism run in one subtask thread (Flink's
+    operator chaining); each keeps its own metrics, and the result is unchanged."""
+    from flink_tensorflow_amd.runtime.executor import LocalExecutor
+
+    env, sink = _chain_job()
+    ex = LocalExecutor(env, "chained")
+    res = ex.execute()
+    assert ex.chains == [["inc", "even", "x10", "collect"]]
+    assert sum(t.thread is not None for t in ex.tasks) == 2   # the source + one chain
+    assert sink.results() == [10 * x for x in range(2, 1001, 2)]
+    assert res.metrics["x10[0]"]["counters"]["records_in"] == 500
+
+
+@pytest.mark.parametrize("mark,chains", [("new_chain", [["even", "x10", "collect"]]),   # "even" starts a chain
+                                         ("no_chain", [["x10", "collect"]]),            # "even" chains with nothing
+                                         ("env_off", [])])
+def test_chaining_controls(mark, chains):
+    from flink_tensorflow_amd.runtime.executor import LocalExecutor
+
+    env, sink = _chain_job(**{mark: True})
+    if mark == "env_off":
+        env.disable_operator_chaining()
+    ex = LocalExecutor(env, mark)
+    ex.execute()
+    assert ex.chains == chains
+    assert sink.results() == [10 * x for x in range(2, 1001, 2)]
+
+
+def test_key_by_and_fan_out_break_chains():
+    from flink_tensorflow_amd.runtime.executor import LocalExecutor
+
+    env = StreamExecutionEnvironment.get_execution_environment()
+    base = env.from_collection(list(range(100))).map(lambda x: x).name("id")
+    a = base.map(lambda x: x + 1).name("a").collect_into()          # fan-out: "id" has two consumers
+    b = base.key_by(lambda x: x % 3).map(lambda x: x).name("k").collect_into()
+    ex = LocalExecutor(env, "fanout")
+    ex.execute()
+    assert ["id", "a"] not in ex.chains and all(c[0] != "id" for c in ex.chains)
+    assert len(a.results()) == 100 and len(b.results()) == 100
