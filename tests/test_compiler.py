@@ -1,4 +1,5 @@
 """Graph compiler: fused plan == interpreter (TF semantics), on host and on the GPU."""
+import numpy as np
 import pytest
 import torch
 
@@ -182,3 +183,22 @@ def test_replay_from_staging_buffer_gpu(small_resnet):
     plan.replay_from("images:0", nc)
     torch.cuda.synchronize()
     assert torch.equal(plan.output_tensors()[0].float(), ref.float())
+
+
+def test_head_bypass_refused_when_the_feed_has_other_readers():
+    """``replay_from`` may skip the input copy only if the preprocess step is the raw feed's
+    sole reader: a fetch of the feed itself, or of a Reshape alias of it, keeps the copy."""
+    from flink_tensorflow_amd.graph.builder import GraphBuilder
+    from flink_tensorflow_amd.models.zoo.resnet import resnet50_graph_def
+
+    spec = {"images:0": ((2, 72, 72, 3), "UINT8")}
+    gd = resnet50_graph_def(depth=26, image_hw=(72, 72), num_classes=8)
+    plan = CompiledFunction(Graph.from_graph_def(gd), spec, ["logits:0"], "cpu", strict=True)
+    assert plan._head_feed_step() is not None                      # sole reader: bypass allowed
+    plan = CompiledFunction(Graph.from_graph_def(gd), spec, ["logits:0", "images:0"], "cpu")
+    assert plan._head_feed_step() is None                          # the feed is fetched
+    b = GraphBuilder()
+    b.op("Reshape", ["images:0", b.constant("flat_shape", np.array([2, -1], np.int32))], name="flat_images")
+    gd.node.extend(b.build_graph_def().node)
+    plan = CompiledFunction(Graph.from_graph_def(gd), spec, ["logits:0", "flat_images:0"], "cpu")
+    assert plan._head_feed_step() is None                          # a Reshape alias is fetched
