@@ -17,6 +17,8 @@ SHAPES = {
     "bert_qkv": (32768, 2304, 768, None, False),
     "bert_o": (32768, 768, 768, None, True),
     "bert_ffn1": (32768, 3072, 768, "gelu", False),
+    "bert_ffn1_plain": (32768, 3072, 768, None, False),
+    "k768_n2304_m49152": (49152, 2304, 768, None, False),
     "bert_ffn2": (32768, 768, 3072, None, True),
     "bert_packed_o": (24576, 768, 768, None, True),
     "sq4096": (4096, 4096, 4096, None, False),
@@ -42,6 +44,7 @@ def main():
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--ours-only", action="store_true", help="skip the library arm (profiling)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     for name in a.shapes.split(","):
@@ -67,6 +70,8 @@ def main():
             if r is not None:
                 y.add_(r)
 
+        if a.ours_only:
+            lib = ours  # noqa: F811
         ours(); lib(); torch.cuda.synchronize()
         t_o, t_l = [], []
         for _ in range(a.rounds):

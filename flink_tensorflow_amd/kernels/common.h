@@ -26,14 +26,20 @@ FTM_DEVICE float apply_act(float x) {
   if constexpr (ACT == ACT_RELU) return x > 0.f ? x : 0.f;
   else if constexpr (ACT == ACT_RELU6) return fminf(fmaxf(x, 0.f), 6.f);
   else if constexpr (ACT == ACT_GELU_TANH) {
-    // 0.5 x (1 + tanh(u)) == x * sigmoid(2u): one v_exp_f32 + one v_rcp_f32 instead of a
-    // libm tanhf (the FFN1 epilogue runs it on every one of B*S*3072 outputs)
-    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-    const float u2 = 2.f * k0 * (x + k1 * x * x * x);
-    return __fdividef(x, 1.f + __expf(-u2));
-  } else if constexpr (ACT == ACT_SIGMOID) return __fdividef(1.f, 1.f + __expf(-x));
-  else if constexpr (ACT == ACT_TANH) return 2.f * __fdividef(1.f, 1.f + __expf(-2.f * x)) - 1.f;
-  else return x;
+    // 0.5 x (1 + tanh(u)) == x / (1 + exp(-2u)), u = k0 (x + k1 x^3): 7 VALU per output —
+    // mul, fma, mul, v_exp_f32 (base 2, log2(e) folded into the constants), add, v_rcp_f32,
+    // mul.  (__fdividef / __expf lower to the IEEE division sequence here: ~20 VALU per
+    // output, which made GELU ~20 % of the FFN1 GEMM.)  Large |u|: exp2 -> inf or 0, so the
+    // result -> 0 or x, no NaN.
+    constexpr float c0 = -2.f * 0.7978845608028654f * 1.4426950408889634f;
+    constexpr float c1 = c0 * 0.044715f;
+    const float t = x * __builtin_fmaf(c1, x * x, c0);
+    return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(t));
+  } else if constexpr (ACT == ACT_SIGMOID) {
+    return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+  } else if constexpr (ACT == ACT_TANH) {
+    return 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.8853900817779268f * x)) - 1.f;
+  } else return x;
 }
 
 // Bijective XCD-aware block remap (guide §5 "XCD swizzle must be bijective", T1):
