@@ -8,7 +8,8 @@
 //                       (guide Appendix B "Scatter / gather / embedding": store-and-sum form)
 //   sparse_adagrad      table[u] -= lr * g / (sqrt(acc[u] += g^2) + eps) on the touched rows
 //
-// D % 8 == 0; one wave per (bag, field) row / destination row, 8 elements per lane.
+// D % 8 == 0 (D/8 a power of two); lane groups of D/8 lanes per row for the small rows of
+// recommender tables, 8 elements per lane.
 #include <pybind11/pybind11.h>
 
 #include <stdexcept>
@@ -17,31 +18,32 @@
 
 namespace {
 
+// One LANE GROUP of G = D/8 lanes per (bag, field) row (G a power of two <= 64; 64/G rows
+// per wave), 8 consecutive elements per lane.  With the Wide&Deep shapes (D = 32 / 8) a
+// whole wave per row left 60 / 63 of its lanes idle.
 __global__ __launch_bounds__(256) void embedding_bag_fwd_kernel(const int* __restrict__ ids,
                                                                 const float* __restrict__ table,
                                                                 bf16* __restrict__ out, int rows, int L, int D,
-                                                                int out_ld, int V) {
-  const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);  // r = b * F + f
+                                                                int gshift, int V) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int r = t >> gshift;  // r = b * F + f
   if (r >= rows) return;
+  const int c = (t & ((1 << gshift) - 1)) * 8;
   const int* idp = ids + (size_t)r * L;
-  for (int c = lane * 8; c < D; c += 64 * 8) {
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int l = 0; l < L; ++l) {
-      const int id = idp[l];
-      if (id < 0 || id >= V) continue;
-      const f32x4* src = reinterpret_cast<const f32x4*>(table + (size_t)id * D + c);
-      const f32x4 a = src[0], b = src[1];
-      acc[0] += a[0]; acc[1] += a[1]; acc[2] += a[2]; acc[3] += a[3];
-      acc[4] += b[0]; acc[5] += b[1]; acc[6] += b[2]; acc[7] += b[3];
-    }
-    bf16x8 o;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e]);
-    // out row b, field f -> column f*D (the F field blocks are contiguous per row)
-    *reinterpret_cast<bf16x8*>(out + (size_t)r * D + c) = o;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int l = 0; l < L; ++l) {
+    const int id = idp[l];
+    if (id < 0 || id >= V) continue;
+    const f32x4* src = reinterpret_cast<const f32x4*>(table + (size_t)id * D + c);
+    const f32x4 a = src[0], b = src[1];
+    acc[0] += a[0]; acc[1] += a[1]; acc[2] += a[2]; acc[3] += a[3];
+    acc[4] += b[0]; acc[5] += b[1]; acc[6] += b[2]; acc[7] += b[3];
   }
-  (void)out_ld;
+  bf16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e]);
+  // out row b, field f -> column f*D (the F field blocks are contiguous per row)
+  *reinterpret_cast<bf16x8*>(out + (size_t)r * D + c) = o;
 }
 
 // grad rows: grad_out[(b*F+f), :] (bf16 or fp32, pitch D); perm lists source rows sorted
@@ -94,16 +96,94 @@ __global__ __launch_bounds__(256) void segment_sum_rows_kernel(const T* __restri
   }
 }
 
+// Lane-group variant: G = D/8 lanes per destination, 64/G destinations per wave.
+// 1. every lane group whose segment is short (<= SHORT rows) sums it serially in perm order
+//    with four interleaved accumulators (i mod 4) combined in a fixed order;
+// 2. the wave then takes its long segments (hot ids: Zipf-distributed categorical data puts
+//    ~1/4 of a field's lookups on one id) one at a time with all 64 lanes, lane = (row group
+//    rg, column chunk), RG = 64/G row groups, fixed xor-tree combine.
+// Each destination's path and summation order depend only on its own segment, so replicas
+// given the same input agree bitwise (no float atomics).
+template <typename T, int G>
+__global__ __launch_bounds__(256) void segment_sum_rows_grp_kernel(const T* __restrict__ grad,
+                                                                   const int* __restrict__ perm,
+                                                                   const int* __restrict__ seg,
+                                                                   float* __restrict__ out, int U, int D, int L) {
+  constexpr int SHORT = 16;
+  constexpr int PER_WAVE = 64 / G;
+  constexpr int RG = 64 / G;
+  const int lane = threadIdx.x & 63;
+  const int u0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * PER_WAVE;
+  if (u0 >= U) return;
+  const int gi = lane / G;
+  const int c = (lane % G) * 8;
+  const int u = u0 + gi;
+  const bool live = u < U;
+  const int s0 = live ? seg[u] : 0, s1 = live ? seg[u + 1] : 0;
+  auto load8 = [&](int i, float* a) {
+    const int src = perm[i] / L;
+    if constexpr (sizeof(T) == 2) {
+      const bf16x8 g = *reinterpret_cast<const bf16x8*>(grad + (size_t)src * D + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += (float)g[e];
+    } else {
+      const f32x4* gp = reinterpret_cast<const f32x4*>(grad + (size_t)src * D + c);
+      const f32x4 x = gp[0], y = gp[1];
+      a[0] += x[0]; a[1] += x[1]; a[2] += x[2]; a[3] += x[3];
+      a[4] += y[0]; a[5] += y[1]; a[6] += y[2]; a[7] += y[3];
+    }
+  };
+  auto store8 = [&](int uu, const float* o) {
+    f32x4* dst = reinterpret_cast<f32x4*>(out + (size_t)uu * D + c);
+    dst[0] = f32x4{o[0], o[1], o[2], o[3]};
+    dst[1] = f32x4{o[4], o[5], o[6], o[7]};
+  };
+  const bool is_long = live && s1 - s0 > SHORT;
+  if (live && !is_long) {
+    float acc[4][8] = {};
+    int i = s0;
+    for (; i + 3 < s1; i += 4) {
+      load8(i, acc[0]);
+      load8(i + 1, acc[1]);
+      load8(i + 2, acc[2]);
+      load8(i + 3, acc[3]);
+    }
+    for (int k = 0; i < s1; ++i, ++k) load8(i, acc[k]);
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (acc[0][e] + acc[1][e]) + (acc[2][e] + acc[3][e]);
+    store8(u, o);
+  }
+  // long segments of this wave, cooperatively (lane group gi of destination u is "long"
+  // -> bit gi*G of the ballot; one destination per iteration, lowest first)
+  unsigned long long longs = __ballot(is_long && (lane % G) == 0);
+  const int rg = lane / G;
+  while (longs) {
+    const int k = __builtin_ctzll(longs) / G;
+    longs &= longs - 1;
+    const int uu = u0 + k;
+    const int a0 = seg[uu], a1 = seg[uu + 1];
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i = a0 + rg; i < a1; i += RG) load8(i, acc);
+#pragma unroll
+    for (int off = G; off < 64; off <<= 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += __shfl_xor(acc[e], off, 64);
+    }
+    if (rg == 0) store8(uu, acc);
+  }
+}
+
 // Segment boundaries of a sorted key array, static shapes: for every i that starts a run
 // (i == 0 or sorted[i] != sorted[i-1]) with run index s = seg_id[i]:  seg[s] = i and
 // uids[s] = key (or -1 for the invalid bucket key == num_rows).  Each run is written by
 // exactly one thread: deterministic, no atomics, no host round trip.
-__global__ __launch_bounds__(256) void segment_starts_kernel(const long long* __restrict__ sorted,
+__global__ __launch_bounds__(256) void segment_starts_kernel(const int* __restrict__ sorted,
                                                              const int* __restrict__ seg_id, int* __restrict__ seg,
-                                                             int* __restrict__ uids, int n, long long num_rows) {
+                                                             int* __restrict__ uids, int n, int num_rows) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const long long k = sorted[i];
+  const int k = sorted[i];
   if (i == 0 || sorted[i - 1] != k) {
     const int sidx = seg_id[i];
     seg[sidx] = i;
@@ -111,38 +191,48 @@ __global__ __launch_bounds__(256) void segment_starts_kernel(const long long* __
   }
 }
 
+// G = D/4 lanes per touched row (a power of two <= 64), 4 elements per lane.
 __global__ __launch_bounds__(256) void sparse_adagrad_kernel(float* __restrict__ table, float* __restrict__ accum,
                                                              const int* __restrict__ uids, const float* __restrict__ g,
-                                                             int U, int D, int V, float lr, float eps) {
-  const int lane = threadIdx.x & 63;
-  const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                             int U, int D, int V, float lr, float eps, int gshift) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int u = t >> gshift;
   if (u >= U) return;
   const int id = uids[u];
   if (id < 0 || id >= V) return;  // padding of the static-shape sparse pipeline
+  const int c = (t & ((1 << gshift) - 1)) * 4;
   const size_t row = (size_t)id * D;
-  for (int c = lane * 4; c < D; c += 64 * 4) {
-    f32x4 gv = *reinterpret_cast<const f32x4*>(g + (size_t)u * D + c);
-    f32x4 av = *reinterpret_cast<f32x4*>(accum + row + c);
-    f32x4 tv = *reinterpret_cast<f32x4*>(table + row + c);
+  f32x4 gv = *reinterpret_cast<const f32x4*>(g + (size_t)u * D + c);
+  f32x4 av = *reinterpret_cast<f32x4*>(accum + row + c);
+  f32x4 tv = *reinterpret_cast<f32x4*>(table + row + c);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      av[e] += gv[e] * gv[e];
-      tv[e] -= lr * gv[e] / (sqrtf(av[e]) + eps);
-    }
-    *reinterpret_cast<f32x4*>(accum + row + c) = av;
-    *reinterpret_cast<f32x4*>(table + row + c) = tv;
+  for (int e = 0; e < 4; ++e) {
+    av[e] += gv[e] * gv[e];
+    tv[e] -= lr * gv[e] / (sqrtf(av[e]) + eps);
   }
+  *reinterpret_cast<f32x4*>(accum + row + c) = av;
+  *reinterpret_cast<f32x4*>(table + row + c) = tv;
 }
 
 }  // namespace
 
+// log2 of a power of two in [1, 64], or -1
+int pow2_shift(int g) {
+  for (int k = 0; k <= 6; ++k)
+    if (g == (1 << k)) return k;
+  return -1;
+}
+
 void embedding_bag_fwd(uintptr_t ids, uintptr_t table, uintptr_t out, int rows, int L, int D, int V, uintptr_t stream) {
   if (D % 8) throw std::invalid_argument("embedding_bag_fwd: D % 8 != 0");
+  const int gs = pow2_shift(D / 8);
+  if (gs < 0) throw std::invalid_argument("embedding_bag_fwd: D / 8 must be a power of two <= 64");
   if (table % 16 || out % 16) throw std::invalid_argument("embedding_bag_fwd: 16-byte alignment required");
   if (rows <= 0) return;
-  hipLaunchKernelGGL(embedding_bag_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     reinterpret_cast<const int*>(ids), reinterpret_cast<const float*>(table),
-                     reinterpret_cast<bf16*>(out), rows, L, D, D, V);
+  const long threads = (long)rows << gs;
+  hipLaunchKernelGGL(embedding_bag_fwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const int*>(ids),
+                     reinterpret_cast<const float*>(table), reinterpret_cast<bf16*>(out), rows, L, D, gs, V);
   FTM_CHECK_LAUNCH();
 }
 
@@ -150,6 +240,17 @@ template <typename T>
 void launch_segment_sum(const void* grad, const int* P, const int* S, float* O, int U, int D, int L, hipStream_t s) {
   const T* g = reinterpret_cast<const T*>(grad);
   const dim3 grid((U + 3) / 4), block(256);
+  if (D / 8 <= 8) {  // small rows: lane groups, 64 / G destinations per wave
+    const int G = D / 8, per_wave = 64 / G;
+    const dim3 ggrid((unsigned)(((U + per_wave - 1) / per_wave + 3) / 4));
+    switch (G) {
+      case 1: hipLaunchKernelGGL((segment_sum_rows_grp_kernel<T, 1>), ggrid, block, 0, s, g, P, S, O, U, D, L); return;
+      case 2: hipLaunchKernelGGL((segment_sum_rows_grp_kernel<T, 2>), ggrid, block, 0, s, g, P, S, O, U, D, L); return;
+      case 4: hipLaunchKernelGGL((segment_sum_rows_grp_kernel<T, 4>), ggrid, block, 0, s, g, P, S, O, U, D, L); return;
+      case 8: hipLaunchKernelGGL((segment_sum_rows_grp_kernel<T, 8>), ggrid, block, 0, s, g, P, S, O, U, D, L); return;
+      default: break;
+    }
+  }
   switch (D / 8) {  // column chunks per row: pick the widest power of two that divides the work
     case 1: hipLaunchKernelGGL((segment_sum_rows_kernel<T, 1>), grid, block, 0, s, g, P, S, O, U, D, L); break;
     case 2: hipLaunchKernelGGL((segment_sum_rows_kernel<T, 2>), grid, block, 0, s, g, P, S, O, U, D, L); break;
@@ -178,20 +279,26 @@ void segment_sum_rows(uintptr_t grad, uintptr_t perm, uintptr_t seg, uintptr_t o
 void sparse_adagrad(uintptr_t table, uintptr_t accum, uintptr_t uids, uintptr_t g, int U, int D, int V, float lr,
                     float eps, uintptr_t stream) {
   if (D % 4) throw std::invalid_argument("sparse_adagrad: D % 4 != 0");
+  const int gs = pow2_shift(D / 4);
+  if (gs < 0) throw std::invalid_argument("sparse_adagrad: D / 4 must be a power of two <= 64");
   if (table % 16 || accum % 16 || g % 16) throw std::invalid_argument("sparse_adagrad: 16-byte alignment required");
   if (U <= 0) return;
-  hipLaunchKernelGGL(sparse_adagrad_kernel, dim3((U + 3) / 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     reinterpret_cast<float*>(table), reinterpret_cast<float*>(accum), reinterpret_cast<const int*>(uids),
-                     reinterpret_cast<const float*>(g), U, D, V, lr, eps);
+  const long threads = (long)U << gs;
+  hipLaunchKernelGGL(sparse_adagrad_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<float*>(table),
+                     reinterpret_cast<float*>(accum), reinterpret_cast<const int*>(uids),
+                     reinterpret_cast<const float*>(g), U, D, V, lr, eps, gs);
   FTM_CHECK_LAUNCH();
 }
 
+// sorted: int32 keys (a 32-bit radix sort is half the passes of a 64-bit one)
 void segment_starts(uintptr_t sorted, uintptr_t seg_id, uintptr_t seg, uintptr_t uids, int n, long long num_rows,
                     uintptr_t stream) {
   if (n <= 0) return;
+  if (num_rows >= (1LL << 31) - 1) throw std::invalid_argument("segment_starts: num_rows must fit int32");
   hipLaunchKernelGGL(segment_starts_kernel, dim3((n + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     reinterpret_cast<const long long*>(sorted), reinterpret_cast<const int*>(seg_id),
-                     reinterpret_cast<int*>(seg), reinterpret_cast<int*>(uids), n, num_rows);
+                     reinterpret_cast<const int*>(sorted), reinterpret_cast<const int*>(seg_id),
+                     reinterpret_cast<int*>(seg), reinterpret_cast<int*>(uids), n, (int)num_rows);
   FTM_CHECK_LAUNCH();
 }
 

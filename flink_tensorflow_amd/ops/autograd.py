@@ -20,9 +20,9 @@ from . import kernels as K
 def _act_grad(y: torch.Tensor, dy: torch.Tensor, act: int) -> torch.Tensor:
     if act == K.ACT_NONE:
         return dy
-    yf = y.float()
     if act == K.ACT_RELU:
-        return (dy.float() * (yf > 0)).to(dy.dtype)
+        return dy * (y > 0)
+    yf = y.float()
     if act == K.ACT_SIGMOID:
         return (dy.float() * yf * (1 - yf)).to(dy.dtype)
     if act == K.ACT_TANH:
@@ -30,34 +30,51 @@ def _act_grad(y: torch.Tensor, dy: torch.Tensor, act: int) -> torch.Tensor:
     raise NotImplementedError(f"backward of activation {act}")
 
 
+def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """``a @ b`` with an fp32 result: bf16 operands accumulate in fp32 and are written as
+    fp32 by the library GEMM itself (no bf16 rounding of the weight gradient, no cast)."""
+    if a.is_cuda and a.dtype != torch.float32:
+        return torch.mm(a, b, out_dtype=torch.float32)
+    return torch.mm(a.float(), b.float())
+
+
 class _Linear(torch.autograd.Function):
+    """Forward on the hand-written MFMA GEMM with the fused bias + activation epilogue.
+    Backward: the activation mask, then two plain GEMMs on the library (dX = dA.W, NN;
+    dW = dA^T.X, TN with an fp32 result for the fp32 master weight — no transposed copies,
+    no cast kernels) and the bias gradient as one fp32 column sum."""
+
     @staticmethod
-    def forward(ctx, x, w, b, act):
-        y = K.gemm(x, w, b, None, act)
+    def forward(ctx, x, w, w_compute, b, act):
+        y = K.gemm(x, w_compute, b, None, act)
         ctx.act = act
-        ctx.save_for_backward(x, w, y)
+        ctx.w_dtype = w.dtype
+        ctx.save_for_backward(x, w_compute, y)
         ctx.has_b = b is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w, y = ctx.saved_tensors
-        da = _act_grad(y, dy.contiguous(), ctx.act)
+        x, wc, y = ctx.saved_tensors
+        da = _act_grad(y, dy, ctx.act)
         lead = x.shape[:-1]
         x2 = x.reshape(-1, x.shape[-1])
-        da2 = da.reshape(-1, da.shape[-1]).contiguous()
+        da2 = da.reshape(-1, da.shape[-1])
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = K.gemm(da2, w.t().contiguous()).reshape(*lead, x.shape[-1])
+            dx = torch.mm(da2.to(wc.dtype), wc).to(x.dtype).reshape(*lead, x.shape[-1])
         if ctx.needs_input_grad[1]:
-            dw = K.gemm(da2.t().contiguous(), x2.t().contiguous())
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            db = da2.float().sum(0)
-        return dx, (dw.to(w.dtype) if dw is not None else None), db, None
+            dw = _mm_f32(da2.t(), x2).to(ctx.w_dtype)
+        if ctx.has_b and ctx.needs_input_grad[3]:
+            db = da2.sum(0, dtype=torch.float32)
+        return dx, dw, None, db, None
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, act=None) -> torch.Tensor:
-    return _Linear.apply(x, w, b, K.act_code(act))
+def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, act=None,
+           w_compute: torch.Tensor | None = None) -> torch.Tensor:
+    """``act(x @ w^T + b)``; ``w_compute``: the operand the GEMMs read (e.g. a bf16 copy of
+    an fp32 master ``w``, which receives the fp32 gradient)."""
+    return _Linear.apply(x, w, w if w_compute is None else w_compute, b, K.act_code(act))
 
 
 class Linear(torch.nn.Module):
@@ -76,5 +93,8 @@ class Linear(torch.nn.Module):
         self.compute_dtype = dtype
 
     def forward(self, x):
-        w = self.weight.to(torch.bfloat16) if x.is_cuda else self.weight
-        return linear(x, w, self.bias, self.act)
+        if not x.is_cuda:
+            return linear(x, self.weight, self.bias, self.act)
+        with torch.no_grad():  # the bf16 operand is a copy, outside autograd: dW lands on the master
+            w16 = self.weight.to(torch.bfloat16)
+        return linear(x, self.weight, self.bias, self.act, w_compute=w16)

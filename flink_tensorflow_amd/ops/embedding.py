@@ -36,8 +36,8 @@ def _segment_sum_static(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L
     n = keys.numel()
     D = rows.shape[1]
     dev = keys.device
-    flat = keys.reshape(-1).long()
-    key = torch.where((flat >= 0) & (flat < num_rows), flat, torch.full_like(flat, num_rows))
+    flat = keys.reshape(-1).to(torch.int32)
+    key = torch.where((flat >= 0) & (flat < num_rows), flat, torch.full_like(flat, num_rows))  # int32 radix sort
     sorted_k, perm = torch.sort(key, stable=True)
     first = torch.ones(n, dtype=torch.bool, device=dev)
     if n > 1:

@@ -159,6 +159,14 @@ def test_linear_autograd():
     _close(outs[1], outs[0])
     _close(xs[1].grad, xs[0].grad)
     _close(bs[1].grad, bs[0].grad)
+    # fp32 master weight + bf16 compute copy (ops.autograd.Linear on the GPU): the fp32
+    # gradient lands on the master straight from the library GEMM
+    wm = w.to(DEV).float().requires_grad_(True)
+    x3 = x.to(DEV).requires_grad_(True)
+    y = linear(x3, wm, bs[1].detach(), "relu", w_compute=wm.detach().to(torch.bfloat16))
+    y.float().sum().backward()
+    assert wm.grad.dtype == torch.float32
+    _close(wm.grad, ws[0].grad)
 
 
 @pytest.mark.parametrize("hw", [224, 299, 100])

@@ -116,3 +116,31 @@ def test_captured_train_step_matches_eager_gpu():
     torch.testing.assert_close(torch.tensor(lb), torch.tensor(la), rtol=1e-4, atol=1e-5)
     for (k, va), vb in zip(a.model.state_dict().items(), b.model.state_dict().values()):
         torch.testing.assert_close(vb, va, rtol=1e-4, atol=1e-5, msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [8, 32, 64, 128])
+def test_embedding_lane_groups_and_hot_ids_gpu(D):
+    """Lane-group kernels (D/8 lanes per row) for every row width, and a hot id (600
+    occurrences) that sends its wave down the whole-wave path: sums == the host reference,
+    bit-identical on repeat."""
+    dev = torch.device("cuda", 0)
+    g0 = torch.Generator().manual_seed(D)
+    table = torch.randn(5000, D, generator=g0)
+    ids = torch.randint(-1, 5000, (3000, 2), generator=g0, dtype=torch.int32)
+    ids[::5, 0] = 7                                          # hot id
+    torch.testing.assert_close(E.embedding_bag(ids.to(dev), table.to(dev)).float().cpu(),
+                               E.embedding_bag(ids, table), rtol=1e-2, atol=1e-2)
+    g = torch.randn(3000, D, generator=g0).to(torch.bfloat16)
+    u_ref, r_ref = E.embedding_bag_backward(ids, g.float(), 5000)
+    u, r = E.embedding_bag_backward(ids.to(dev), g.to(dev), 5000, static=True)
+    n = u_ref.numel()
+    assert torch.equal(u[:n].cpu(), u_ref)
+    torch.testing.assert_close(r[:n].cpu(), r_ref, rtol=1e-4, atol=1e-4)
+    _, r2 = E.embedding_bag_backward(ids.to(dev), g.to(dev), 5000, static=True)
+    assert torch.equal(r2, r)
+    acc_ref, tab_ref = torch.full((5000, D), 0.1), table.clone()
+    E.sparse_adagrad(tab_ref, acc_ref, u_ref, r_ref, 0.05)
+    tab, acc = table.to(dev), torch.full((5000, D), 0.1, device=dev)
+    E.sparse_adagrad(tab, acc, u.contiguous(), r.contiguous(), 0.05)
+    torch.testing.assert_close(tab.cpu(), tab_ref, rtol=1e-5, atol=1e-5)
