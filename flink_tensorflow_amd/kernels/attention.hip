@@ -141,11 +141,11 @@ __global__ __launch_bounds__(QB * 4) void attention_fwd_kernel(const bf16* __res
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float mref = mnew[r] == -INFINITY ? 0.f : mnew[r];
-      alpha[r] = exp2f(mrow[r] - mref);
+      alpha[r] = __builtin_amdgcn_exp2f(mrow[r] - mref);
       float sum = 0.f;
 #pragma unroll
       for (int n = 0; n < NF; ++n) {
-        const float pv = exp2f(s[n][r] - mref);
+        const float pv = __builtin_amdgcn_exp2f(s[n][r] - mref);
         s[n][r] = pv;
         sum += pv;
       }
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(256) void cls_attention_kernel(const bf16* __restri
   mx = wave_reduce_max(mx);
   float sum = 0.f;
   for (int j = lane; j < n; j += 64) {
-    const float p = exp2f(probs[wave][j] - mx);
+    const float p = __builtin_amdgcn_exp2f(probs[wave][j] - mx);
     probs[wave][j] = p;
     sum += p;
   }

@@ -19,7 +19,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 FTM_DEVICE float bf2f(bf16 v) { return (float)v; }
 FTM_DEVICE bf16 f2bf(float v) { return (bf16)v; }  // RNE, v_cvt_pk_bf16_f32 at -O3
 
-enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU_TANH = 2, ACT_SIGMOID = 3, ACT_TANH = 4, ACT_RELU6 = 5 };
+// ACT_DRELU (GEMM epilogues with a residual operand only): y = res > 0 ? acc : 0 — the
+// ReLU backward mask of the layer input, fused into the dX GEMM of a training step.
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU_TANH = 2, ACT_SIGMOID = 3, ACT_TANH = 4, ACT_RELU6 = 5, ACT_DRELU = 6 };
 
 template <int ACT>
 FTM_DEVICE float apply_act(float x) {

@@ -148,7 +148,10 @@ __global__ __launch_bounds__(256) void segment_sum_rows_grp_kernel(const T* __re
       load8(i + 2, acc[2]);
       load8(i + 3, acc[3]);
     }
-    for (int k = 0; i < s1; ++i, ++k) load8(i, acc[k]);
+    const int rem = s1 - i;  // static accumulator indices: no dynamic register indexing
+    if (rem > 0) load8(i, acc[0]);
+    if (rem > 1) load8(i + 1, acc[1]);
+    if (rem > 2) load8(i + 2, acc[2]);
     float o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = (acc[0][e] + acc[1][e]) + (acc[2][e] + acc[3][e]);
@@ -163,14 +166,131 @@ __global__ __launch_bounds__(256) void segment_sum_rows_grp_kernel(const T* __re
     longs &= longs - 1;
     const int uu = u0 + k;
     const int a0 = seg[uu], a1 = seg[uu + 1];
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int i = a0 + rg; i < a1; i += RG) load8(i, acc);
+    // 8 rows in flight per lane (hot segments are latency-bound chains of perm -> row
+    // loads), accumulators combined in a fixed tree
+    float q[8][8] = {};
+    for (int i = a0 + rg; i < a1; i += 8 * RG) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (i + j * RG < a1) load8(i + j * RG, q[j]);
+    }
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      acc[e] = ((q[0][e] + q[1][e]) + (q[2][e] + q[3][e])) + ((q[4][e] + q[5][e]) + (q[6][e] + q[7][e]));
 #pragma unroll
     for (int off = G; off < 64; off <<= 1) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] += __shfl_xor(acc[e], off, 64);
     }
     if (rg == 0) store8(uu, acc);
+  }
+}
+
+// Reduce-by-key over the SORTED rows in fixed slices (static-shape pipeline): hot ids
+// (Zipf-distributed categoricals put thousands of a batch's lookups on one id) no longer
+// serialise on the one wave that owns their destination.
+//  pass 1 (segsum_slices): lane group (G = D/8 lanes) k walks sorted rows [kS, kS + S)
+//    in order, 8 rows in flight; a run wholly inside the slice is written to out[run]; the
+//    part of a run that started before the slice goes to head[k], the part of a run that
+//    continues past it to tail[k];
+//  pass 2 (segsum_fixup): one wave per destination: runs spanning slices k0..k1 sum
+//    tail[k0] + head[k0+1 .. k1] (RG row groups + fixed xor tree); empty (padding)
+//    destinations get zero rows.
+// Every sum has a fixed order: bit-identical across runs and replicas.
+template <typename T, int G>
+__global__ __launch_bounds__(256) void segsum_slices_kernel(const T* __restrict__ grad, const int* __restrict__ perm,
+                                                            const int* __restrict__ seg_id,
+                                                            const int* __restrict__ seg, float* __restrict__ out,
+                                                            float* __restrict__ head, float* __restrict__ tail, int n,
+                                                            int D, int L, int S) {
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  const long k = t / G;
+  const int c = (int)(t % G) * 8;
+  const long i0 = k * S;
+  if (i0 >= n) return;
+  const long i1 = i0 + S < n ? i0 + S : n;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int cur = seg_id[i0];
+  auto flush = [&](int r) {
+    const int rs = seg[r], re = seg[r + 1];
+    float* dst = (rs >= i0 && re <= i1) ? out + (size_t)r * D : (rs < i0 ? head : tail) + (size_t)k * D;
+    reinterpret_cast<f32x4*>(dst + c)[0] = f32x4{acc[0], acc[1], acc[2], acc[3]};
+    reinterpret_cast<f32x4*>(dst + c)[1] = f32x4{acc[4], acc[5], acc[6], acc[7]};
+  };
+  for (long b0 = i0; b0 < i1; b0 += 8) {
+    float row[8][8];
+    int rid[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // 8 independent perm -> row loads in flight
+      const long i = b0 + j;
+      rid[j] = i < i1 ? seg_id[i] : -1;
+      if (i < i1) {
+        const int src = perm[i] / L;
+        if constexpr (sizeof(T) == 2) {
+          const bf16x8 gv = *reinterpret_cast<const bf16x8*>(grad + (size_t)src * D + c);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) row[j][e] = (float)gv[e];
+        } else {
+          const f32x4* gp = reinterpret_cast<const f32x4*>(grad + (size_t)src * D + c);
+          const f32x4 x = gp[0], y = gp[1];
+          row[j][0] = x[0]; row[j][1] = x[1]; row[j][2] = x[2]; row[j][3] = x[3];
+          row[j][4] = y[0]; row[j][5] = y[1]; row[j][6] = y[2]; row[j][7] = y[3];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (rid[j] < 0) break;
+      if (rid[j] != cur) {
+        flush(cur);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+        cur = rid[j];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += row[j][e];
+    }
+  }
+  flush(cur);
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void segsum_fixup_kernel(const int* __restrict__ seg, float* __restrict__ out,
+                                                           const float* __restrict__ head,
+                                                           const float* __restrict__ tail, int U, int D, int S) {
+  constexpr int RG = 64 / G;
+  const int lane = threadIdx.x & 63;
+  const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (u >= U) return;
+  const int rs = seg[u], re = seg[u + 1];
+  const int rg = lane / G;
+  const int c = (lane % G) * 8;
+  if (re <= rs) {  // empty (padding) destination
+    if (rg == 0) {
+      reinterpret_cast<f32x4*>(out + (size_t)u * D + c)[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      reinterpret_cast<f32x4*>(out + (size_t)u * D + c)[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    return;
+  }
+  const int k0 = rs / S, k1 = (re - 1) / S;
+  if (k0 == k1) return;  // written whole by its slice
+  const int cnt = k1 - k0 + 1;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int j = rg; j < cnt; j += RG) {
+    const float* src = (j == 0 ? tail : head) + (size_t)(k0 + j) * D + c;
+    const f32x4 x = reinterpret_cast<const f32x4*>(src)[0], y = reinterpret_cast<const f32x4*>(src)[1];
+    acc[0] += x[0]; acc[1] += x[1]; acc[2] += x[2]; acc[3] += x[3];
+    acc[4] += y[0]; acc[5] += y[1]; acc[6] += y[2]; acc[7] += y[3];
+  }
+#pragma unroll
+  for (int off = G; off < 64; off <<= 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += __shfl_xor(acc[e], off, 64);
+  }
+  if (rg == 0) {
+    reinterpret_cast<f32x4*>(out + (size_t)u * D + c)[0] = f32x4{acc[0], acc[1], acc[2], acc[3]};
+    reinterpret_cast<f32x4*>(out + (size_t)u * D + c)[1] = f32x4{acc[4], acc[5], acc[6], acc[7]};
   }
 }
 
@@ -292,6 +412,49 @@ void sparse_adagrad(uintptr_t table, uintptr_t accum, uintptr_t uids, uintptr_t 
 }
 
 // sorted: int32 keys (a 32-bit radix sort is half the passes of a 64-bit one)
+template <typename T, int G>
+void launch_segsum(const void* grad, const int* P, const int* SID, const int* SEG, float* O, float* ws, int n, int U,
+                   int D, int L, int S, hipStream_t s) {
+  const long slices = (n + S - 1) / S;
+  float* head = ws;
+  float* tail = ws + slices * D;
+  const long threads = slices * G;
+  hipLaunchKernelGGL((segsum_slices_kernel<T, G>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<const T*>(grad), P, SID, SEG, O, head, tail, n, D, L, S);
+  hipLaunchKernelGGL((segsum_fixup_kernel<G>), dim3((unsigned)((U + 3) / 4)), dim3(256), 0, s, SEG, O, head, tail, U,
+                     D, S);
+}
+
+// Static-shape deterministic segment sum of sorted rows: seg_id[i] = destination of sorted
+// position i, seg [U + 1] run starts; ws >= 2 * ceil(n / S) * D floats.
+void segment_sum_sorted(uintptr_t grad, uintptr_t perm, uintptr_t seg_id, uintptr_t seg, uintptr_t out, uintptr_t ws,
+                        int n, int U, int D, int L, int S, int grad_is_fp32, uintptr_t stream) {
+  if (D % 8 || D / 8 > 64 || ((D / 8) & (D / 8 - 1))) throw std::invalid_argument("segment_sum_sorted: D/8 power of 2 <= 64");
+  if (S <= 0 || S % 8) throw std::invalid_argument("segment_sum_sorted: slice length must be a positive multiple of 8");
+  if (grad % 16 || out % 16 || ws % 16) throw std::invalid_argument("segment_sum_sorted: 16-byte alignment required");
+  if (n <= 0 || U <= 0) return;
+  auto s = reinterpret_cast<hipStream_t>(stream);
+  auto P = reinterpret_cast<const int*>(perm);
+  auto SID = reinterpret_cast<const int*>(seg_id);
+  auto SEG = reinterpret_cast<const int*>(seg);
+  auto O = reinterpret_cast<float*>(out);
+  auto W = reinterpret_cast<float*>(ws);
+  const void* g = reinterpret_cast<const void*>(grad);
+#define FTM_SEGSUM(T)                                                                      \
+  switch (D / 8) {                                                                         \
+    case 1: launch_segsum<T, 1>(g, P, SID, SEG, O, W, n, U, D, L, S, s); break;            \
+    case 2: launch_segsum<T, 2>(g, P, SID, SEG, O, W, n, U, D, L, S, s); break;            \
+    case 4: launch_segsum<T, 4>(g, P, SID, SEG, O, W, n, U, D, L, S, s); break;            \
+    case 8: launch_segsum<T, 8>(g, P, SID, SEG, O, W, n, U, D, L, S, s); break;            \
+    case 16: launch_segsum<T, 16>(g, P, SID, SEG, O, W, n, U, D, L, S, s); break;          \
+    case 32: launch_segsum<T, 32>(g, P, SID, SEG, O, W, n, U, D, L, S, s); break;          \
+    default: launch_segsum<T, 64>(g, P, SID, SEG, O, W, n, U, D, L, S, s); break;          \
+  }
+  if (grad_is_fp32) { FTM_SEGSUM(float) } else { FTM_SEGSUM(bf16) }
+#undef FTM_SEGSUM
+  FTM_CHECK_LAUNCH();
+}
+
 void segment_starts(uintptr_t sorted, uintptr_t seg_id, uintptr_t seg, uintptr_t uids, int n, long long num_rows,
                     uintptr_t stream) {
   if (n <= 0) return;
@@ -306,5 +469,6 @@ void register_embedding(pybind11::module_& m) {
   m.def("segment_starts", &segment_starts);
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
   m.def("segment_sum_rows", &segment_sum_rows);
+  m.def("segment_sum_sorted", &segment_sum_sorted);
   m.def("sparse_adagrad", &sparse_adagrad);
 }

@@ -295,7 +295,10 @@ __device__ __forceinline__ void pp_tile(const PPParams& p, uint8_t* smem, const 
         bf16x8 o = __builtin_bit_cast(bf16x8, v);
         const bf16x8 r = *reinterpret_cast<const bf16x8*>(p.res + (size_t)m * p.ldr + n);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = f2bf(apply_act<ACT>((float)o[e] + (float)r[e]));
+        for (int e = 0; e < 8; ++e) {
+          if constexpr (ACT == ACT_DRELU) o[e] = (float)r[e] > 0.f ? o[e] : f2bf(0.f);
+          else o[e] = f2bf(apply_act<ACT>((float)o[e] + (float)r[e]));
+        }
         v = __builtin_bit_cast(u32x4, o);
       }
       *reinterpret_cast<u32x4*>(y + (size_t)m * p.ldy + p.y_coff + n) = v;
@@ -351,7 +354,10 @@ __global__ __launch_bounds__(256) void gemm_pp_reduce_kernel(const float* __rest
   if constexpr (HAS_RES) {
     const bf16x8 r = *reinterpret_cast<const bf16x8*>(res + (size_t)m * ldr + n);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += (float)r[e];
+    for (int e = 0; e < 8; ++e) {
+      if constexpr (ACT == ACT_DRELU) v[e] = (float)r[e] > 0.f ? v[e] : 0.f;
+      else v[e] += (float)r[e];
+    }
   }
   bf16x8 o;
 #pragma unroll
@@ -458,6 +464,10 @@ void gemm_pp(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t 
     case ACT_RELU: launch_res<ACT_RELU>(p, splits, wsp, s); break;
     case ACT_GELU_TANH: launch_res<ACT_GELU_TANH>(p, splits, wsp, s); break;
     case ACT_TANH: launch_res<ACT_TANH>(p, splits, wsp, s); break;
+    case ACT_DRELU:
+      if (!res) throw std::invalid_argument("gemm_pp: the drelu epilogue needs the mask operand (res)");
+      launch_pp<ACT_DRELU, true>(p, splits, wsp, s);
+      break;
     default: throw std::invalid_argument("gemm_pp: unsupported activation");
   }
   FTM_CHECK_LAUNCH();

@@ -118,13 +118,16 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
     """Online trainer: ``train_step(records)`` on micro-batches of
     ``(label, dense[13], cats[26], cross[C])`` records; ``predict(records)``."""
 
-    _TRANSIENT = ("_model", "_opt", "_bucketer", "_graph", "_static", "_static_loss")
+    _TRANSIENT = ("_model", "_opt", "_bucketer", "_graph", "_static", "_static_loss", "_fused")
 
-    def __init__(self, cfg: WideDeepConfig | None = None, device=None, seed: int = 0):
+    def __init__(self, cfg: WideDeepConfig | None = None, device=None, seed: int = 0, fused: bool | None = None):
         self.cfg = cfg or WideDeepConfig()
         self.device = device
         self.seed = seed
-        self._model = self._opt = self._bucketer = None
+        # fused: the hand-fused GPU step (models/zoo/wide_deep_fused.py); None = on a GPU
+        # unless FTM_WD_FUSED=0.  False: autograd forward/backward + torch Adam.
+        self.fused = fused
+        self._model = self._opt = self._bucketer = self._fused = None
         self._graph = self._static = self._static_loss = None
         self.steps = 0
 
@@ -133,6 +136,12 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         self._model = WideDeep(self.cfg, dev, self.seed)
         if comm.is_dist():  # identical initial replicas: rank 0's weights to everyone
             comm.broadcast_tensors([p.data for p in self._model.parameters()] + list(self._model.buffers()), 0)
+        use_fused = self.fused if self.fused is not None else os.environ.get("FTM_WD_FUSED", "1") != "0"
+        from .wide_deep_fused import FusedWideDeepStep
+
+        if dev.type == "cuda" and use_fused and FusedWideDeepStep.supports(self.cfg):
+            self._fused = FusedWideDeepStep(self._model, self.cfg.lr_dense, self.cfg.lr_sparse)
+            return
         fused = dev.type == "cuda"  # one multi-tensor Adam launch instead of one per parameter tensor
         self._opt = torch.optim.Adam(self._model.dense_parameters(), lr=self.cfg.lr_dense, fused=fused,
                                      capturable=fused)
@@ -141,7 +150,7 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
     def close(self):
         if self._bucketer is not None:
             self._bucketer.remove()
-        self._model = self._opt = self._bucketer = None
+        self._model = self._opt = self._bucketer = self._fused = None
         self._graph = self._static = self._static_loss = None
 
     @property
@@ -199,6 +208,10 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
     def _step(self, batch):
         m = self._model
         labels, dense, cats, cross = batch
+        if self._fused is not None:
+            loss = self._fused.step(labels, dense, cats, cross)
+            self.steps += 1
+            return loss
         logits = m(dense, cats, cross)
         loss = F.binary_cross_entropy_with_logits(logits, labels)
         self._opt.zero_grad(set_to_none=True)
@@ -220,10 +233,13 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
     def snapshot_state(self, ctx):
         d = model_state_dir(ctx, "widedeep")
         st = {f"model/{k}": v for k, v in self._model.state().items()}
-        for i, s in enumerate(self._opt.state_dict()["state"].values()):
-            for k, v in s.items():
-                if torch.is_tensor(v):
-                    st[f"adam/{i}/{k}"] = v.detach().reshape(v.shape)
+        if self._fused is not None:
+            st.update(self._fused.state())
+        else:
+            for i, s in enumerate(self._opt.state_dict()["state"].values()):
+                for k, v in s.items():
+                    if torch.is_tensor(v):
+                        st[f"adam/{i}/{k}"] = v.detach().reshape(v.shape)
         if d is not None and (not comm.is_dist() or comm.world()[0] == 0):
             bundle.save_tensors(os.path.join(d, "variables"), st)
         ctx.operator_state.blobs["widedeep_steps"] = self.steps
@@ -238,7 +254,13 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
             self.open()
         with bundle.BundleReader(prefix) as r:
             sd = {k[len("model/"):]: r.read(k) for k in r.keys() if k.startswith("model/")}
-        self._model.load_state_dict({k: v.to(self._model.device) for k, v in sd.items()})
+            adam = {k: r.read(k) for k in r.keys() if k.startswith("adam/")}
+        with torch.no_grad():  # in place: the fused step's parameters are views of its flat buffer
+            for k, v in self._model.state_dict().items():
+                if k in sd:
+                    v.copy_(sd[k].to(v.device).reshape(v.shape))
+        if self._fused is not None:
+            self._fused.load_state(adam)
         self.steps = ctx.operator_state.blobs.get("widedeep_steps", 0)
 
 

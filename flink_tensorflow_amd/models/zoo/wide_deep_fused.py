@@ -1,0 +1,188 @@
+"""Fused Wide&Deep training step for the GPU (BASELINE config 4).
+
+The autograd step (``WideDeepTrainer._step``: module forward, ``loss.backward()``, torch
+Adam) launches ~140 kernels per micro-batch, most of them framework elementwise kernels
+(casts, cat/pad, slices, BCE pieces, bias-grad reductions, the Adam multi-tensor kernel,
+bf16 weight copies).  This step computes the same forward, gradients and updates with:
+
+* ``wd_gather`` (``kernels/widedeep.hip``): embedding rows + dense features + zero pad
+  straight into the bf16 MLP input, the wide-part sum, the global embedding ids;
+* the MLP forward on the MFMA GEMM with fused bias + ReLU epilogues (``ops.kernels.gemm``);
+* ``wd_loss``: BCE-with-logits mean, dlogit, the wide gradient rows, the scalar gradients;
+* ``wd_head_bwd`` for the 256 -> 1 head, then per hidden layer the weight gradient as one
+  library TN GEMM with an fp32 result (dW = dA^T . H), the bias gradient as a column sum
+  and dX as a library NN GEMM (dA . W, no transposed weight copy) + ``wd_relu_mask``.
+  (At this batch the backward GEMMs are 4096-row problems of 32-64 256x256 tiles: the
+  ping-pong kernel with its ``drelu`` epilogue uses an eighth of the chip there and
+  measured slower than library GEMM + mask, transposes included);
+* the deterministic row-sparse pipeline (sort + segment sum + sparse Adagrad) as before;
+* ``wd_adam`` over ONE flat fp32 buffer holding every dense parameter (the module's
+  parameters are views of it), writing the bf16 copies the next forward reads.
+
+Under data parallelism the flat gradient buffer is all-reduced in one RCCL call (the
+average folded into Adam) and the sparse rows are all-gathered as before.  The result is
+the autograd step's update up to bf16 rounding (``tests/test_widedeep.py``).
+"""
+from __future__ import annotations
+
+import torch
+
+from ... import _ext
+from ...ops import kernels as K
+from ...ops.embedding import segment_sum, sparse_adagrad
+from ...parallel import comm
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+class _Acts:
+    """Static activations / gradients of one micro-batch size."""
+
+    def __init__(self, step: "FusedWideDeepStep", B: int):
+        dev, m = step.dev, step.m
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.B = B
+        self.x = torch.empty(B, step.XP, **bf)
+        self.h = [torch.empty(B, l.weight.shape[0], **bf) for l in step.layers]
+        self.hd = torch.empty(B, m.head.weight.shape[0], **bf)
+        self.da = [torch.empty(B, l.weight.shape[0], **bf) for l in step.layers]
+        self.de = torch.empty(B, step.F * step.D, **bf)
+        self.wsum = torch.empty(B, dtype=torch.float32, device=dev)
+        self.gids = torch.empty(B * step.F, dtype=torch.int32, device=dev)
+        self.dlogit = torch.empty(B, dtype=torch.float32, device=dev)
+        self.dlogit16 = torch.empty(B, **bf)
+        self.loss = torch.empty((), dtype=torch.float32, device=dev)
+        self.part = torch.empty(2 * (-(-B // 256)), dtype=torch.float32, device=dev)
+        self.C = None
+        self.wgrad = None
+
+
+class FusedWideDeepStep:
+    """``step(labels, dense, cats, cross)`` -> loss (device scalar); activations are kept
+    per micro-batch size.  Owns the Adam state; ``state()`` / ``load_state()`` for
+    checkpoints."""
+
+    @staticmethod
+    def supports(cfg) -> bool:
+        """Shapes the kernels take: hidden widths multiples of 64 (K of the dX GEMMs),
+        embedding rows of 8..512 floats with D/8 a power of two."""
+        d8 = cfg.embed_dim // 8
+        return (all(h % 64 == 0 for h in cfg.hidden) and cfg.embed_dim % 8 == 0 and d8 & (d8 - 1) == 0
+                and d8 <= 64 and (cfg.num_fields * cfg.embed_dim) % 8 == 0)
+
+    def __init__(self, model, lr: float, lr_sparse: float, betas=(0.9, 0.999), eps: float = 1e-8):
+        dev = model.device
+        if dev.type != "cuda":
+            raise ValueError("the fused Wide&Deep step runs on a GPU")
+        self.m, self.cfg, self.dev = model, model.cfg, dev
+        self.lr, self.lr_sparse, self.b1, self.b2, self.eps = lr, lr_sparse, betas[0], betas[1], eps
+        self._H = _ext.hip()
+        cfg = self.cfg
+        # ---- one flat fp32 buffer for every dense parameter; the module's params become views
+        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad and not n.endswith("table")]
+        al = 64  # every parameter starts on a 256-B boundary (16-B vector access of biases)
+        total = sum(-(-p.numel() // al) * al for _, p in named)
+        self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.t = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.g: dict[str, torch.Tensor] = {}
+        self.off: dict[str, tuple[int, int]] = {}
+        o = 0
+        for n, p in named:
+            k = p.numel()
+            self.flat[o:o + k].copy_(p.data.reshape(-1))
+            p.data = self.flat[o:o + k].view_as(p)
+            self.g[n] = self.grad[o:o + k].view(p.shape)
+            self.off[n] = (o, k)
+            o += -(-k // al) * al
+        # ---- bf16 operands of every Linear (rewritten by the Adam kernel)
+        self.layers = list(model.mlp)
+        self.w16 = [l.weight.detach().to(torch.bfloat16) for l in self.layers] + [
+            model.head.weight.detach().to(torch.bfloat16)]
+        names = [f"mlp.{i}.weight" for i in range(len(self.layers))] + ["head.weight"]
+        self.seg = torch.tensor([[self.off[n][0] for n in names], [self.off[n][1] for n in names],
+                                 [w.data_ptr() for w in self.w16]], dtype=torch.int64, device=dev)
+        self.F, self.D, self.ND = cfg.num_fields, cfg.embed_dim, cfg.num_dense
+        self.XP = model.in_pad
+        self._acts: dict[int, _Acts] = {}
+
+    def refresh(self):
+        """Re-derives the bf16 operands from the fp32 masters (after a restore)."""
+        for w, l in zip(self.w16, self.layers + [self.m.head]):
+            w.copy_(l.weight.detach())
+
+    # ------------------------------------------------------------------ the step
+    def step(self, labels, dense, cats, cross) -> torch.Tensor:
+        H, m, cfg = self._H, self.m, self.cfg
+        B = labels.shape[0]
+        a = self._acts.get(B)
+        if a is None:
+            a = self._acts[B] = _Acts(self, B)
+        C = cross.shape[1]
+        WV, WD = m.wide.table.shape
+        if a.wgrad is None or a.C != C:
+            a.C = C
+            a.wgrad = torch.empty(B * C, WD, dtype=torch.float32, device=self.dev)
+        s = _stream()
+        cats, cross = cats.contiguous(), cross.contiguous()
+        dense, labels = dense.contiguous(), labels.contiguous()
+        # forward
+        H.wd_gather(cats.data_ptr(), dense.data_ptr(), cross.data_ptr(), m.emb.table.data_ptr(),
+                    m.wide.table.data_ptr(), a.x.data_ptr(), a.wsum.data_ptr(), a.gids.data_ptr(), B, self.F,
+                    cfg.vocab_per_field, self.D, self.ND, self.XP, C, WV, WD, s)
+        h = a.x
+        for i, l in enumerate(self.layers):
+            h = K.gemm(h, self.w16[i], l.bias, None, "relu", out=a.h[i])
+        K.gemm(h, self.w16[-1], m.head.bias, None, None, out=a.hd)
+        H.wd_loss(a.hd.data_ptr(), a.hd.shape[1], a.wsum.data_ptr(), m.wide_bias.data_ptr(),
+                  labels.data_ptr(), B, a.dlogit.data_ptr(), a.dlogit16.data_ptr(), a.loss.data_ptr(),
+                  self.g["wide_bias"].data_ptr(), self.g["head.bias"].data_ptr(), a.wgrad.data_ptr(), C, WD, a.part.data_ptr(), s)
+        # backward: head (only logit column 0 is used), then the hidden layers
+        last = a.h[-1]
+        self.g["head.weight"][0:1].copy_(torch.mm(a.dlogit16.view(1, B), last, out_dtype=torch.float32))
+        H.wd_head_bwd(last.data_ptr(), a.dlogit.data_ptr(), m.head.weight.data_ptr(), a.da[-1].data_ptr(), B,
+                      last.shape[1], s)
+        for i in range(len(self.layers) - 1, -1, -1):
+            da = a.da[i]
+            inp = a.h[i - 1] if i else a.x
+            self.g[f"mlp.{i}.weight"].copy_(torch.mm(da.t(), inp, out_dtype=torch.float32))
+            torch.sum(da, 0, dtype=torch.float32, out=self.g[f"mlp.{i}.bias"])
+            if i:  # dX, then the ReLU mask of this layer's input
+                torch.mm(da, self.w16[i], out=a.da[i - 1])
+                H.wd_relu_mask(a.da[i - 1].data_ptr(), inp.data_ptr(), inp.numel(), s)
+            else:  # embedding columns of dX only
+                torch.mm(da, self.w16[0][:, : self.F * self.D], out=a.de)
+        # sparse rows
+        ue, re = segment_sum(a.gids, a.de.view(B * self.F, self.D), m.emb.table.shape[0], static=True)
+        uw, rw = segment_sum(cross.view(-1), a.wgrad, WV, static=True)
+        ws = 1
+        if comm.is_dist():
+            from .wide_deep import _sparse_sync
+
+            ue, re = segment_sum(*_sparse_sync(ue, re), m.emb.table.shape[0], static=True)
+            uw, rw = segment_sum(*_sparse_sync(uw, rw), WV, static=True)
+            c = comm.get()
+            c.all_reduce(self.grad)  # one collective for every dense gradient
+            ws = c.size
+        sparse_adagrad(m.emb.table.data, m.emb.accum, ue, re, self.lr_sparse)
+        sparse_adagrad(m.wide.table.data, m.wide.accum, uw, rw, self.lr_sparse)
+        # dense Adam over the flat buffer + the bf16 operands of the next step
+        self.t.add_(1.0)
+        H.wd_adam(self.flat.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                  self.flat.numel(), self.t.data_ptr(), self.lr, self.b1, self.b2, self.eps, 1.0 / ws,
+                  self.seg.data_ptr(), self.seg.shape[1], s)
+        return a.loss
+
+    # ------------------------------------------------------------------ checkpoints
+    def state(self) -> dict[str, torch.Tensor]:
+        return {"adam/exp_avg": self.exp_avg, "adam/exp_avg_sq": self.exp_avg_sq, "adam/step": self.t}
+
+    def load_state(self, st: dict) -> None:
+        for k, dst in self.state().items():
+            if k in st:
+                dst.copy_(st[k].to(dst.device).reshape(dst.shape))
+        self.refresh()

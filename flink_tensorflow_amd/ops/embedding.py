@@ -28,6 +28,9 @@ def embedding_bag(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | No
     return out
 
 
+_SLICE = 32  # sorted rows per lane group in the static segment sum
+
+
 def _segment_sum_static(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L: int):
     """Sync-free, static-shape segment sum on the GPU: outputs are sized by the number of
     keys n (an upper bound of the unique count); unused slots carry uid -1 and zero rows.
@@ -53,8 +56,11 @@ def _segment_sum_static(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L
     if not fp32 and g.dtype != torch.bfloat16:
         g = g.to(torch.bfloat16)
     perm32 = perm.to(torch.int32)
-    _hip().segment_sum_rows(g.data_ptr(), perm32.data_ptr(), seg.data_ptr(), out.data_ptr(), n, D, L, int(fp32),
-                            _stream())
+    # reduce-by-key over fixed slices of the sorted rows + a fix-up pass for the runs that
+    # span slices (hot ids), all in fixed order: see kernels/embedding.hip
+    ws = torch.empty(2 * (-(-n // _SLICE)) * D, dtype=torch.float32, device=rows.device)
+    _hip().segment_sum_sorted(g.data_ptr(), perm32.data_ptr(), seg_id.data_ptr(), seg.data_ptr(), out.data_ptr(),
+                              ws.data_ptr(), n, n, D, L, _SLICE, int(fp32), _stream())
     return uids, out
 
 

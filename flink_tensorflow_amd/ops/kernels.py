@@ -19,9 +19,9 @@ import torch.nn.functional as F
 
 from .. import _ext
 
-ACT_NONE, ACT_RELU, ACT_GELU, ACT_SIGMOID, ACT_TANH, ACT_RELU6 = 0, 1, 2, 3, 4, 5
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_SIGMOID, ACT_TANH, ACT_RELU6, ACT_DRELU = 0, 1, 2, 3, 4, 5, 6
 _ACT_NAMES = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU, "gelu_tanh": ACT_GELU,
-              "sigmoid": ACT_SIGMOID, "tanh": ACT_TANH, "relu6": ACT_RELU6}
+              "sigmoid": ACT_SIGMOID, "tanh": ACT_TANH, "relu6": ACT_RELU6, "drelu": ACT_DRELU}
 
 
 def act_code(act) -> int:
@@ -385,6 +385,11 @@ def gemm_pp(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = Non
     y = x2.float() @ w_nk.float().t()
     if bias is not None:
         y = y + bias.float()
+    if a == ACT_DRELU:  # the residual operand is the ReLU mask source, not an addend
+        if residual is None:
+            raise ValueError("gemm_pp: act 'drelu' needs the mask operand (residual)")
+        out2[:, out_col:out_col + N] = torch.where(residual.reshape(M, N).float() > 0, y, 0.0).to(out.dtype)
+        return out
     if residual is not None:
         y = y + residual.reshape(M, N).float()
     out2[:, out_col:out_col + N] = _apply_act_ref(y, a).to(out.dtype)

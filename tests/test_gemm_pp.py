@@ -120,3 +120,22 @@ def test_gemm_pp_graph_capture():
     graph.replay()
     torch.cuda.synchronize()
     _close(out, _ref(x, w, None, None, None))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("splits", [1, 3])
+def test_gemm_pp_drelu_mask_epilogue(splits):
+    """act='drelu': y = (mask > 0) ? x.w^T + b : 0 — the ReLU backward of a training step's
+    dX GEMM, in the direct epilogue and in the split-K reduction."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    M, N, Kd = 1000, 512, 768
+    x = torch.randn(M, Kd, generator=g, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, Kd, generator=g, device=DEV) / Kd ** 0.5).to(torch.bfloat16)
+    h = torch.randn(M, N, generator=g, device=DEV).to(torch.bfloat16)
+    got = K.gemm_pp(x, w, None, h, "drelu", splits=splits)
+    ref = torch.where(h.float() > 0, x.float() @ w.float().t(), 0.0)
+    torch.cuda.synchronize()
+    assert bool((got[h <= 0] == 0).all())
+    _close(got, ref)
+    host = K.gemm_pp(x.cpu(), w.cpu(), None, h.cpu(), "drelu")
+    _close(host, ref.cpu())
