@@ -21,10 +21,15 @@ namespace {
 
 // G = D/8 lanes per (b, f) embedding row; rows r >= B*F are the per-record rows (dense, pad,
 // wide sum) handled by the G lanes of row B*F + b.
-__global__ __launch_bounds__(256) void wd_gather_kernel(const int* __restrict__ cats, const float* __restrict__ dense,
-                                                        const int* __restrict__ cross, const float* __restrict__ emb,
-                                                        const float* __restrict__ wide, bf16* __restrict__ x,
-                                                        float* __restrict__ wsum, int* __restrict__ gids, int B, int F,
+// cats / dense / cross rows have their own strides (elements): they may be views of one
+// packed record buffer.  wids gets a contiguous copy of the crossed ids (the wide part's
+// sort keys).
+__global__ __launch_bounds__(256) void wd_gather_kernel(const int* __restrict__ cats, int ldc,
+                                                        const float* __restrict__ dense, int ldd,
+                                                        const int* __restrict__ cross, int ldx,
+                                                        const float* __restrict__ emb, const float* __restrict__ wide,
+                                                        bf16* __restrict__ x, float* __restrict__ wsum,
+                                                        int* __restrict__ gids, int* __restrict__ wids, int B, int F,
                                                         int V, int D, int gshift, int ND, int XP, int C, int WV,
                                                         int WD) {
   const long t = (long)blockIdx.x * 256 + threadIdx.x;
@@ -33,7 +38,7 @@ __global__ __launch_bounds__(256) void wd_gather_kernel(const int* __restrict__ 
   const long nemb = (long)B * F;
   if (r < nemb) {
     const int b = (int)(r / F), f = (int)(r - (long)b * F);
-    const int gid = cats[r] + f * V;  // field-local id -> row of the concatenated table
+    const int gid = cats[(size_t)b * ldc + f] + f * V;  // field-local id -> row of the concatenated table
     if (g == 0) gids[r] = gid;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (gid >= 0 && gid < F * V) {
@@ -52,13 +57,14 @@ __global__ __launch_bounds__(256) void wd_gather_kernel(const int* __restrict__ 
     for (int c0 = g * 8; base + c0 < XP; c0 += 8 << gshift) {
       bf16x8 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(c0 + e < ND ? dense[(size_t)b * ND + c0 + e] : 0.f);
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(c0 + e < ND ? dense[(size_t)b * ldd + c0 + e] : 0.f);
       *reinterpret_cast<bf16x8*>(x + (size_t)b * XP + base + c0) = o;
     }
     if (g == 0) {
       float s = 0.f;
       for (int c = 0; c < C; ++c) {
-        const int id = cross[(size_t)b * C + c];
+        const int id = cross[(size_t)b * ldx + c];
+        wids[(size_t)b * C + c] = id;
         if (id >= 0 && id < WV) s += wide[(size_t)id * WD];
       }
       wsum[b] = s;
@@ -70,7 +76,7 @@ __global__ __launch_bounds__(256) void wd_gather_kernel(const int* __restrict__ 
 // and wd_loss_final adds them in block order (deterministic).
 __global__ __launch_bounds__(256) void wd_loss_kernel(const bf16* __restrict__ head, int ldh,
                                                       const float* __restrict__ wsum, const float* __restrict__ wbias,
-                                                      const float* __restrict__ labels, int B,
+                                                      const float* __restrict__ labels, int ldl, int B,
                                                       float* __restrict__ dlogit, bf16* __restrict__ dlogit16,
                                                       float* __restrict__ part, float* __restrict__ wgrad, int C,
                                                       int WD) {
@@ -79,7 +85,7 @@ __global__ __launch_bounds__(256) void wd_loss_kernel(const bf16* __restrict__ h
   float lo = 0.f, d = 0.f;
   if (b < B) {
     const float l = (float)head[(size_t)b * ldh] + wsum[b] + wbias[0];
-    const float y = labels[b];
+    const float y = labels[(size_t)b * ldl];
     lo = fmaxf(l, 0.f) - l * y + log1pf(__expf(-fabsf(l)));
     d = (__builtin_amdgcn_rcpf(1.f + __expf(-l)) - y) / (float)B;
     dlogit[b] = d;
@@ -183,9 +189,9 @@ int pow2_shift(int g) {
 
 }  // namespace
 
-void wd_gather(uintptr_t cats, uintptr_t dense, uintptr_t cross, uintptr_t emb, uintptr_t wide, uintptr_t x,
-               uintptr_t wsum, uintptr_t gids, int B, int F, int V, int D, int ND, int XP, int C, int WV, int WD,
-               uintptr_t stream) {
+void wd_gather(uintptr_t cats, int ldc, uintptr_t dense, int ldd, uintptr_t cross, int ldx, uintptr_t emb,
+               uintptr_t wide, uintptr_t x, uintptr_t wsum, uintptr_t gids, uintptr_t wids, int B, int F, int V, int D,
+               int ND, int XP, int C, int WV, int WD, uintptr_t stream) {
   const int gs = pow2_shift(D / 8);
   if (D % 8 || gs < 0) throw std::invalid_argument("wd_gather: D / 8 must be a power of two <= 64");
   if (XP % 8 || XP < F * D + ND) throw std::invalid_argument("wd_gather: XP must be a multiple of 8 >= F*D + ND");
@@ -194,16 +200,16 @@ void wd_gather(uintptr_t cats, uintptr_t dense, uintptr_t cross, uintptr_t emb, 
   if (B <= 0) return;
   const long threads = ((long)B * F + B) << gs;
   hipLaunchKernelGGL(wd_gather_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const int*>(cats),
-                     reinterpret_cast<const float*>(dense), reinterpret_cast<const int*>(cross),
+                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const int*>(cats), ldc,
+                     reinterpret_cast<const float*>(dense), ldd, reinterpret_cast<const int*>(cross), ldx,
                      reinterpret_cast<const float*>(emb), reinterpret_cast<const float*>(wide),
-                     reinterpret_cast<bf16*>(x), reinterpret_cast<float*>(wsum), reinterpret_cast<int*>(gids), B, F, V,
-                     D, gs, ND, XP, C, WV, WD);
+                     reinterpret_cast<bf16*>(x), reinterpret_cast<float*>(wsum), reinterpret_cast<int*>(gids),
+                     reinterpret_cast<int*>(wids), B, F, V, D, gs, ND, XP, C, WV, WD);
   FTM_CHECK_LAUNCH();
 }
 
 // part: >= 2 * ceil(B / 256) floats of workspace
-void wd_loss(uintptr_t head, int ldh, uintptr_t wsum, uintptr_t wbias, uintptr_t labels, int B, uintptr_t dlogit,
+void wd_loss(uintptr_t head, int ldh, uintptr_t wsum, uintptr_t wbias, uintptr_t labels, int ldl, int B, uintptr_t dlogit,
              uintptr_t dlogit16, uintptr_t loss, uintptr_t g_wbias, uintptr_t g_hb0, uintptr_t wgrad, int C, int WD,
              uintptr_t part, uintptr_t stream) {
   if (B <= 0) throw std::invalid_argument("wd_loss: empty batch");
@@ -212,7 +218,7 @@ void wd_loss(uintptr_t head, int ldh, uintptr_t wsum, uintptr_t wbias, uintptr_t
   const int nb = (B + 255) / 256;
   hipLaunchKernelGGL(wd_loss_kernel, dim3(nb), dim3(256), 0, s, reinterpret_cast<const bf16*>(head), ldh,
                      reinterpret_cast<const float*>(wsum), reinterpret_cast<const float*>(wbias),
-                     reinterpret_cast<const float*>(labels), B, reinterpret_cast<float*>(dlogit),
+                     reinterpret_cast<const float*>(labels), ldl, B, reinterpret_cast<float*>(dlogit),
                      reinterpret_cast<bf16*>(dlogit16), reinterpret_cast<float*>(part), reinterpret_cast<float*>(wgrad),
                      C, WD);
   hipLaunchKernelGGL(wd_loss_final_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<const float*>(part), nb, B,

@@ -98,6 +98,17 @@ class WideDeep(torch.nn.Module):
         return {k: v.detach() for k, v in self.state_dict().items()}
 
 
+def _rebase_view(t: torch.Tensor, base: torch.Tensor, new_base: torch.Tensor) -> torch.Tensor:
+    """The view of ``new_base`` (a same-shape copy of ``base``) that ``t`` is of ``base``."""
+    nb = new_base.view(torch.uint8).reshape(-1)
+    off = t.data_ptr() - base.data_ptr()
+    es = t.element_size()
+    if off % es:
+        raise ValueError("misaligned view")
+    flat = nb[off:].view(t.dtype) if off else nb.view(t.dtype)
+    return flat.as_strided(t.shape, t.stride())
+
+
 def _sparse_sync(uids: torch.Tensor, rows: torch.Tensor):
     """All-gather row-sparse gradients.  The static-shape sparse pipeline pads every rank's
     (uids, rows) to the same length (one slot per looked-up id, uid -1 = empty), so the
@@ -175,8 +186,12 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
     def train_step(self, records=None, batch=None) -> float:
         batch = batch if batch is not None else self.collate(records)
         if self._graph is not None and all(a.shape == b.shape for a, b in zip(batch, self._static)):
-            for dst, src in zip(self._static, batch):  # new micro-batch into the captured inputs
-                dst.copy_(src, non_blocking=True)
+            sp, bp = getattr(self._static, "packed", None), getattr(batch, "packed", None)
+            if sp is not None and bp is not None and sp.shape == bp.shape:
+                sp.copy_(bp, non_blocking=True)  # one copy re-binds all four views
+            else:
+                for dst, src in zip(self._static, batch):  # new micro-batch into the captured inputs
+                    dst.copy_(src, non_blocking=True)
             self._graph.replay()
             self.steps += 1
             return self._static_loss
@@ -192,7 +207,12 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         the row-sparse all-gathers run on the capturing stream, so one replay is one whole
         DP step."""
         dev = self._model.device
-        self._static = tuple(t.to(dev).clone() for t in batch)
+        packed = getattr(batch, "packed", None)
+        if packed is not None:  # static copy of the packed buffer + the same views into it
+            sp = packed.to(dev).clone()
+            self._static = PackedBatch(tuple(_rebase_view(t, packed, sp) for t in batch), sp)
+        else:
+            self._static = tuple(t.to(dev).clone() for t in batch)
         with capture_lock():
             s = torch.cuda.Stream(dev)
             s.wait_stream(torch.cuda.current_stream(dev))
@@ -283,6 +303,16 @@ def pack_click_records(records, cfg: WideDeepConfig, n_cross: int = 8) -> np.nda
     return arr.view(np.uint8).reshape(len(records), lay.itemsize)
 
 
+class PackedBatch(tuple):
+    """``(labels, dense, cats, cross)`` as views of ONE device buffer of packed rows
+    (``.packed``): a captured training step re-binds a batch with a single copy."""
+
+    def __new__(cls, parts, packed):
+        t = super().__new__(cls, parts)
+        t.packed = packed
+        return t
+
+
 class PackedBatchStager:
     """Micro-batch staging of packed click rows: native multithreaded gather into a pinned
     slot, async H2D on the current stream, and device-side views split into (labels,
@@ -321,11 +351,12 @@ class PackedBatchStager:
         o_d = 4
         o_c = o_d + 4 * c.num_dense
         o_x = o_c + 4 * c.num_fields
-        labels = dev[:, 0:4].contiguous().view(torch.float32).reshape(-1)
-        dense = dev[:, o_d:o_c].contiguous().view(torch.float32)
-        cats = dev[:, o_c:o_x].contiguous().view(torch.int32)
-        cross = dev[:, o_x:o_x + 4 * self.n_cross].contiguous().view(torch.int32)
-        return labels, dense, cats, cross
+        # strided views of the packed rows (no splitting copies); ``.packed`` is the buffer
+        labels = dev[:, 0:4].view(torch.float32).reshape(-1)
+        dense = dev[:, o_d:o_c].view(torch.float32)
+        cats = dev[:, o_c:o_x].view(torch.int32)
+        cross = dev[:, o_x:o_x + 4 * self.n_cross].view(torch.int32)
+        return PackedBatch((labels, dense, cats, cross), dev)
 
 
 def synthetic_click_records(n: int, cfg: WideDeepConfig, seed: int = 0, n_cross: int = 8):

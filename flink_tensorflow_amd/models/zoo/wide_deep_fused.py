@@ -51,6 +51,7 @@ class _Acts:
         self.de = torch.empty(B, step.F * step.D, **bf)
         self.wsum = torch.empty(B, dtype=torch.float32, device=dev)
         self.gids = torch.empty(B * step.F, dtype=torch.int32, device=dev)
+        self.wids = None
         self.dlogit = torch.empty(B, dtype=torch.float32, device=dev)
         self.dlogit16 = torch.empty(B, **bf)
         self.loss = torch.empty((), dtype=torch.float32, device=dev)
@@ -127,29 +128,34 @@ class FusedWideDeepStep:
         if a.wgrad is None or a.C != C:
             a.C = C
             a.wgrad = torch.empty(B * C, WD, dtype=torch.float32, device=self.dev)
+            a.wids = torch.empty(B * C, dtype=torch.int32, device=self.dev)
         s = _stream()
-        cats, cross = cats.contiguous(), cross.contiguous()
-        dense, labels = dense.contiguous(), labels.contiguous()
+        # the inputs may be strided views of one packed record buffer (rows of label | dense |
+        # cats | cross): the kernels take row strides, no splitting copies
+        cats, dense, cross = (t if t.stride(-1) == 1 else t.contiguous() for t in (cats, dense, cross))
+        if labels.dim() != 1:
+            labels = labels.reshape(-1)
         # forward
-        H.wd_gather(cats.data_ptr(), dense.data_ptr(), cross.data_ptr(), m.emb.table.data_ptr(),
-                    m.wide.table.data_ptr(), a.x.data_ptr(), a.wsum.data_ptr(), a.gids.data_ptr(), B, self.F,
-                    cfg.vocab_per_field, self.D, self.ND, self.XP, C, WV, WD, s)
+        H.wd_gather(cats.data_ptr(), cats.stride(0), dense.data_ptr(), dense.stride(0), cross.data_ptr(),
+                    cross.stride(0), m.emb.table.data_ptr(), m.wide.table.data_ptr(), a.x.data_ptr(), a.wsum.data_ptr(),
+                    a.gids.data_ptr(), a.wids.data_ptr(), B, self.F, cfg.vocab_per_field, self.D, self.ND, self.XP, C,
+                    WV, WD, s)
         h = a.x
         for i, l in enumerate(self.layers):
             h = K.gemm(h, self.w16[i], l.bias, None, "relu", out=a.h[i])
         K.gemm(h, self.w16[-1], m.head.bias, None, None, out=a.hd)
         H.wd_loss(a.hd.data_ptr(), a.hd.shape[1], a.wsum.data_ptr(), m.wide_bias.data_ptr(),
-                  labels.data_ptr(), B, a.dlogit.data_ptr(), a.dlogit16.data_ptr(), a.loss.data_ptr(),
+                  labels.data_ptr(), labels.stride(0), B, a.dlogit.data_ptr(), a.dlogit16.data_ptr(), a.loss.data_ptr(),
                   self.g["wide_bias"].data_ptr(), self.g["head.bias"].data_ptr(), a.wgrad.data_ptr(), C, WD, a.part.data_ptr(), s)
         # backward: head (only logit column 0 is used), then the hidden layers
         last = a.h[-1]
-        self.g["head.weight"][0:1].copy_(torch.mm(a.dlogit16.view(1, B), last, out_dtype=torch.float32))
+        torch.mm(a.dlogit16.view(1, B), last, out_dtype=torch.float32, out=self.g["head.weight"][0:1])
         H.wd_head_bwd(last.data_ptr(), a.dlogit.data_ptr(), m.head.weight.data_ptr(), a.da[-1].data_ptr(), B,
                       last.shape[1], s)
         for i in range(len(self.layers) - 1, -1, -1):
             da = a.da[i]
             inp = a.h[i - 1] if i else a.x
-            self.g[f"mlp.{i}.weight"].copy_(torch.mm(da.t(), inp, out_dtype=torch.float32))
+            torch.mm(da.t(), inp, out_dtype=torch.float32, out=self.g[f"mlp.{i}.weight"])
             torch.sum(da, 0, dtype=torch.float32, out=self.g[f"mlp.{i}.bias"])
             if i:  # dX, then the ReLU mask of this layer's input
                 torch.mm(da, self.w16[i], out=a.da[i - 1])
@@ -158,7 +164,7 @@ class FusedWideDeepStep:
                 torch.mm(da, self.w16[0][:, : self.F * self.D], out=a.de)
         # sparse rows
         ue, re = segment_sum(a.gids, a.de.view(B * self.F, self.D), m.emb.table.shape[0], static=True)
-        uw, rw = segment_sum(cross.view(-1), a.wgrad, WV, static=True)
+        uw, rw = segment_sum(a.wids, a.wgrad, WV, static=True)
         ws = 1
         if comm.is_dist():
             from .wide_deep import _sparse_sync

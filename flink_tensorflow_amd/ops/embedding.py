@@ -28,39 +28,41 @@ def embedding_bag(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | No
     return out
 
 
-_SLICE = 32  # sorted rows per lane group in the static segment sum
+_SLICE = 8  # sorted rows per lane group in the static segment sum (one batch of 8 loads)
 
 
 def _segment_sum_static(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L: int):
     """Sync-free, static-shape segment sum on the GPU: outputs are sized by the number of
     keys n (an upper bound of the unique count); unused slots carry uid -1 and zero rows.
     No ``.item()`` / ``unique`` host round trip, so a training step stays asynchronous
-    (and capturable)."""
+    (and capturable).  Grouping: ``kernels/sort_segments.hip`` (radix sort over the key
+    bits actually used + run boundaries); sums: ``segment_sum_sorted``."""
     n = keys.numel()
     D = rows.shape[1]
     dev = keys.device
-    flat = keys.reshape(-1).to(torch.int32)
-    key = torch.where((flat >= 0) & (flat < num_rows), flat, torch.full_like(flat, num_rows))  # int32 radix sort
-    sorted_k, perm = torch.sort(key, stable=True)
-    first = torch.ones(n, dtype=torch.bool, device=dev)
-    if n > 1:
-        first[1:] = sorted_k[1:] != sorted_k[:-1]
-    seg_id = torch.cumsum(first.to(torch.int32), 0, dtype=torch.int32) - 1
-    uids = torch.full((n,), -1, dtype=torch.int32, device=dev)
-    seg = torch.full((n + 1,), n, dtype=torch.int32, device=dev)
-    _hip().segment_starts(sorted_k.data_ptr(), seg_id.data_ptr(), seg.data_ptr(), uids.data_ptr(), n, num_rows,
-                          _stream())
+    H = _hip()
+    flat = keys.reshape(-1)
+    if flat.dtype != torch.int32:
+        flat = flat.to(torch.int32)
+    flat = flat.contiguous()
+    i32 = dict(dtype=torch.int32, device=dev)
+    sorted_k, perm, seg_id, uids = (torch.empty(n, **i32) for _ in range(4))
+    seg = torch.empty(n + 1, **i32)
+    work = torch.empty(3 * n, **i32)
+    tb = H.sort_segments_temp_bytes(n, num_rows)
+    temp = torch.empty(tb, dtype=torch.uint8, device=dev)
+    H.sort_segments(flat.data_ptr(), n, num_rows, sorted_k.data_ptr(), perm.data_ptr(), seg_id.data_ptr(),
+                    seg.data_ptr(), uids.data_ptr(), work.data_ptr(), temp.data_ptr(), tb, _stream())
     out = torch.empty((n, D), dtype=torch.float32, device=rows.device)
     g = rows.contiguous()
     fp32 = g.dtype == torch.float32
     if not fp32 and g.dtype != torch.bfloat16:
         g = g.to(torch.bfloat16)
-    perm32 = perm.to(torch.int32)
     # reduce-by-key over fixed slices of the sorted rows + a fix-up pass for the runs that
     # span slices (hot ids), all in fixed order: see kernels/embedding.hip
     ws = torch.empty(2 * (-(-n // _SLICE)) * D, dtype=torch.float32, device=rows.device)
-    _hip().segment_sum_sorted(g.data_ptr(), perm32.data_ptr(), seg_id.data_ptr(), seg.data_ptr(), out.data_ptr(),
-                              ws.data_ptr(), n, n, D, L, _SLICE, int(fp32), _stream())
+    H.segment_sum_sorted(g.data_ptr(), perm.data_ptr(), seg_id.data_ptr(), seg.data_ptr(), out.data_ptr(),
+                         ws.data_ptr(), n, n, D, L, _SLICE, int(fp32), _stream())
     return uids, out
 
 

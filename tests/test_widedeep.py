@@ -177,3 +177,29 @@ def test_fused_step_matches_autograd_gpu():
     lc = [float(cap.train_step(batch=b)) for b in batches[2:]]
     le = [float(eager.train_step(batch=b)) for b in batches[2:]]
     torch.testing.assert_close(torch.tensor(lc), torch.tensor(le), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_fused_step_on_packed_rows_captured_gpu():
+    """The bench path: batches are strided views of one packed device buffer (no split
+    copies), the captured fused step re-binds a batch with one copy, and matches the eager
+    fused step on the same batches."""
+    from flink_tensorflow_amd.models.zoo.wide_deep import PackedBatchStager, pack_click_records
+
+    dev = torch.device("cuda", 0)
+    cfg = WideDeepConfig.tiny(hidden=(128, 64), embed_dim=16)
+    nx = min(8, cfg.num_fields - 1)
+    rows = list(pack_click_records(synthetic_click_records(128 * 6, cfg, seed=4), cfg, n_cross=nx))
+    stager = PackedBatchStager(cfg, 128, dev, n_cross=nx, depth=6)
+    batches = [stager.stage(rows[i * 128:(i + 1) * 128]) for i in range(6)]
+    assert all(getattr(b, "packed", None) is not None and b[2].stride(0) != b[2].shape[1] for b in batches)
+    cap = WideDeepTrainer(cfg, device=dev, seed=2, fused=True)
+    eag = WideDeepTrainer(cfg, device=dev, seed=2, fused=True)
+    cap.open()
+    eag.open()
+    cap.capture(batches[0])          # two warm-up steps on batch 0
+    for _ in range(2):
+        eag.train_step(batch=batches[0])
+    lc = [float(cap.train_step(batch=b)) for b in batches[1:]]
+    le = [float(eag.train_step(batch=b)) for b in batches[1:]]
+    torch.testing.assert_close(torch.tensor(lc), torch.tensor(le), rtol=1e-5, atol=1e-6)
