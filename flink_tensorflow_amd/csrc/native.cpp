@@ -895,16 +895,30 @@ void scatter_into(uintptr_t dst, size_t dst_bytes, const std::vector<size_t>& of
 // Gather-copy of many record payloads into one contiguous destination (a pinned
 // staging slot).  Releases the GIL and fans the copy across threads.
 // ----------------------------------------------------------------------------------
+// Raw CPython buffer views of a batch's records (PyBUF_SIMPLE: contiguous bytes), released
+// with the GIL held (declare before any gil_scoped_release so it is destroyed after it).
+// pybind11's buffer::request() builds a shape/stride buffer_info per object: ~0.4 us per
+// record, which made staging a 4096-record Wide&Deep micro-batch ~1.6 ms.
+struct RawViews {
+  std::vector<Py_buffer> v;
+  size_t n = 0;
+  ~RawViews() {
+    for (size_t i = 0; i < n; ++i) PyBuffer_Release(&v[i]);
+  }
+};
+
 void gather_into(uintptr_t dst, size_t dst_bytes, const py::list& srcs, size_t stride, int nthreads) {
   std::vector<std::pair<const uint8_t*, size_t>> v;
-  std::vector<py::buffer_info> keep;
-  keep.reserve(srcs.size());
+  RawViews keep;
+  keep.v.resize(srcs.size());
+  v.reserve(srcs.size());
   for (auto h : srcs) {
-    keep.emplace_back(h.cast<py::buffer>().request());
-    auto& bi = keep.back();
-    size_t nb = size_t(bi.size * bi.itemsize);
+    Py_buffer& b = keep.v[keep.n];
+    if (PyObject_GetBuffer(h.ptr(), &b, PyBUF_SIMPLE) != 0) throw py::error_already_set();
+    ++keep.n;
+    const size_t nb = size_t(b.len);
     if (nb > stride) throw std::runtime_error("record payload larger than the staging stride");
-    v.emplace_back(static_cast<const uint8_t*>(bi.ptr), nb);
+    v.emplace_back(static_cast<const uint8_t*>(b.buf), nb);
   }
   if (v.size() * stride > dst_bytes) throw std::runtime_error("staging slot too small for the batch");
   uint8_t* d = reinterpret_cast<uint8_t*>(dst);
