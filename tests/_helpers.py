@@ -11,7 +11,7 @@ def _free_port():
     return p
 
 
-def torchrun_smoke(nproc, *args, timeout=180):
+def torchrun_smoke(nproc, *args, timeout=180, script="comm_smoke.py"):
     import json
     import subprocess
     import sys
@@ -20,7 +20,7 @@ def torchrun_smoke(nproc, *args, timeout=180):
     env = dict(os.environ, PYTHONPATH=root, OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(root, "tools", "comm_smoke.py"), *args]
+           os.path.join(root, "tools", script), *args]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     return sorted((json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")), key=lambda d: d["rank"])

@@ -203,3 +203,16 @@ def test_fused_step_on_packed_rows_captured_gpu():
     lc = [float(cap.train_step(batch=b)) for b in batches[1:]]
     le = [float(eag.train_step(batch=b)) for b in batches[1:]]
     torch.testing.assert_close(torch.tensor(lc), torch.tensor(le), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_fused_dp_replicas_stay_identical_gpu():
+    """Two ranks (loopback communicator, both on this GPU) train the fused step on different
+    records: after broadcast init, dense all-reduce and the merged row-sparse updates, every
+    parameter and both embedding tables are bit-identical across the replicas."""
+    from _helpers import torchrun_smoke
+
+    out = torchrun_smoke(2, "--fake", script="wd_dp_check.py", timeout=300)
+    assert [o["rank"] for o in out] == [0, 1] and all(o["fused"] for o in out)
+    assert out[0]["sums"] == out[1]["sums"]
+    assert out[0]["losses"] != out[1]["losses"]  # the ranks did see different data
