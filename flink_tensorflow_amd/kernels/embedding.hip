@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256) void segsum_slices_kernel(const T* __restrict_
                                                             const int* __restrict__ seg_id,
                                                             const int* __restrict__ seg, float* __restrict__ out,
                                                             float* __restrict__ head, float* __restrict__ tail, int n,
-                                                            int D, int L, int S) {
+                                                            int D, int L, int S, int lo, int hi) {
   const long t = (long)blockIdx.x * 256 + threadIdx.x;
   const long k = t / G;
   const int c = (int)(t % G) * 8;
@@ -225,8 +225,9 @@ __global__ __launch_bounds__(256) void segsum_slices_kernel(const T* __restrict_
     for (int j = 0; j < 8; ++j) {  // 8 independent perm -> row loads in flight
       const long i = b0 + j;
       rid[j] = i < i1 ? seg_id[i] : -1;
-      if (i < i1) {
-        const int src = perm[i] / L;
+      const int pi = i < i1 ? perm[i] : lo - 1;
+      if (pi >= lo && pi < hi) {  // rows of another table sharing the key space add nothing
+        const int src = (pi - lo) / L;
         if constexpr (sizeof(T) == 2) {
           const bf16x8 gv = *reinterpret_cast<const bf16x8*>(grad + (size_t)src * D + c);
 #pragma unroll
@@ -237,6 +238,9 @@ __global__ __launch_bounds__(256) void segsum_slices_kernel(const T* __restrict_
           row[j][0] = x[0]; row[j][1] = x[1]; row[j][2] = x[2]; row[j][3] = x[3];
           row[j][4] = y[0]; row[j][5] = y[1]; row[j][6] = y[2]; row[j][7] = y[3];
         }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) row[j][e] = 0.f;
       }
     }
 #pragma unroll
@@ -314,11 +318,12 @@ __global__ __launch_bounds__(256) void segment_starts_kernel(const int* __restri
 // G = D/4 lanes per touched row (a power of two <= 64), 4 elements per lane.
 __global__ __launch_bounds__(256) void sparse_adagrad_kernel(float* __restrict__ table, float* __restrict__ accum,
                                                              const int* __restrict__ uids, const float* __restrict__ g,
-                                                             int U, int D, int V, float lr, float eps, int gshift) {
+                                                             int U, int D, int V, float lr, float eps, int gshift,
+                                                             int off) {
   const int t = blockIdx.x * 256 + threadIdx.x;
   const int u = t >> gshift;
   if (u >= U) return;
-  const int id = uids[u];
+  const int id = uids[u] < 0 ? -1 : uids[u] - off;  // off: this table's base in a shared key space
   if (id < 0 || id >= V) return;  // padding of the static-shape sparse pipeline
   const int c = (t & ((1 << gshift) - 1)) * 4;
   const size_t row = (size_t)id * D;
@@ -397,7 +402,7 @@ void segment_sum_rows(uintptr_t grad, uintptr_t perm, uintptr_t seg, uintptr_t o
 }
 
 void sparse_adagrad(uintptr_t table, uintptr_t accum, uintptr_t uids, uintptr_t g, int U, int D, int V, float lr,
-                    float eps, uintptr_t stream) {
+                    float eps, int off, uintptr_t stream) {
   if (D % 4) throw std::invalid_argument("sparse_adagrad: D % 4 != 0");
   const int gs = pow2_shift(D / 4);
   if (gs < 0) throw std::invalid_argument("sparse_adagrad: D / 4 must be a power of two <= 64");
@@ -407,28 +412,30 @@ void sparse_adagrad(uintptr_t table, uintptr_t accum, uintptr_t uids, uintptr_t 
   hipLaunchKernelGGL(sparse_adagrad_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), reinterpret_cast<float*>(table),
                      reinterpret_cast<float*>(accum), reinterpret_cast<const int*>(uids),
-                     reinterpret_cast<const float*>(g), U, D, V, lr, eps, gs);
+                     reinterpret_cast<const float*>(g), U, D, V, lr, eps, gs, off);
   FTM_CHECK_LAUNCH();
 }
 
 // sorted: int32 keys (a 32-bit radix sort is half the passes of a 64-bit one)
 template <typename T, int G>
 void launch_segsum(const void* grad, const int* P, const int* SID, const int* SEG, float* O, float* ws, int n, int U,
-                   int D, int L, int S, hipStream_t s) {
+                   int D, int L, int S, int lo, int hi, hipStream_t s) {
   const long slices = (n + S - 1) / S;
   float* head = ws;
   float* tail = ws + slices * D;
   const long threads = slices * G;
   hipLaunchKernelGGL((segsum_slices_kernel<T, G>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
-                     reinterpret_cast<const T*>(grad), P, SID, SEG, O, head, tail, n, D, L, S);
+                     reinterpret_cast<const T*>(grad), P, SID, SEG, O, head, tail, n, D, L, S, lo, hi);
   hipLaunchKernelGGL((segsum_fixup_kernel<G>), dim3((unsigned)((U + 3) / 4)), dim3(256), 0, s, SEG, O, head, tail, U,
                      D, S);
 }
 
 // Static-shape deterministic segment sum of sorted rows: seg_id[i] = destination of sorted
-// position i, seg [U + 1] run starts; ws >= 2 * ceil(n / S) * D floats.
+// position i, seg [U + 1] run starts; ws >= 2 * ceil(n / S) * D floats.  Only sorted
+// positions whose perm lies in [lo, hi) contribute (rows (perm - lo) / L of grad): several
+// tables can share one key space and one sort.
 void segment_sum_sorted(uintptr_t grad, uintptr_t perm, uintptr_t seg_id, uintptr_t seg, uintptr_t out, uintptr_t ws,
-                        int n, int U, int D, int L, int S, int grad_is_fp32, uintptr_t stream) {
+                        int n, int U, int D, int L, int S, int grad_is_fp32, int lo, int hi, uintptr_t stream) {
   if (D % 8 || D / 8 > 64 || ((D / 8) & (D / 8 - 1))) throw std::invalid_argument("segment_sum_sorted: D/8 power of 2 <= 64");
   if (S <= 0 || S % 8) throw std::invalid_argument("segment_sum_sorted: slice length must be a positive multiple of 8");
   if (grad % 16 || out % 16 || ws % 16) throw std::invalid_argument("segment_sum_sorted: 16-byte alignment required");
@@ -442,13 +449,13 @@ void segment_sum_sorted(uintptr_t grad, uintptr_t perm, uintptr_t seg_id, uintpt
   const void* g = reinterpret_cast<const void*>(grad);
 #define FTM_SEGSUM(T)                                                                      \
   switch (D / 8) {                                                                         \
-    case 1: launch_segsum<T, 1>(g, P, SID, SEG, O, W, n, U, D, L, S, s); break;            \
-    case 2: launch_segsum<T, 2>(g, P, SID, SEG, O, W, n, U, D, L, S, s); break;            \
-    case 4: launch_segsum<T, 4>(g, P, SID, SEG, O, W, n, U, D, L, S, s); break;            \
-    case 8: launch_segsum<T, 8>(g, P, SID, SEG, O, W, n, U, D, L, S, s); break;            \
-    case 16: launch_segsum<T, 16>(g, P, SID, SEG, O, W, n, U, D, L, S, s); break;          \
-    case 32: launch_segsum<T, 32>(g, P, SID, SEG, O, W, n, U, D, L, S, s); break;          \
-    default: launch_segsum<T, 64>(g, P, SID, SEG, O, W, n, U, D, L, S, s); break;          \
+    case 1: launch_segsum<T, 1>(g, P, SID, SEG, O, W, n, U, D, L, S, lo, hi, s); break;            \
+    case 2: launch_segsum<T, 2>(g, P, SID, SEG, O, W, n, U, D, L, S, lo, hi, s); break;            \
+    case 4: launch_segsum<T, 4>(g, P, SID, SEG, O, W, n, U, D, L, S, lo, hi, s); break;            \
+    case 8: launch_segsum<T, 8>(g, P, SID, SEG, O, W, n, U, D, L, S, lo, hi, s); break;            \
+    case 16: launch_segsum<T, 16>(g, P, SID, SEG, O, W, n, U, D, L, S, lo, hi, s); break;          \
+    case 32: launch_segsum<T, 32>(g, P, SID, SEG, O, W, n, U, D, L, S, lo, hi, s); break;          \
+    default: launch_segsum<T, 64>(g, P, SID, SEG, O, W, n, U, D, L, S, lo, hi, s); break;          \
   }
   if (grad_is_fp32) { FTM_SEGSUM(float) } else { FTM_SEGSUM(bf16) }
 #undef FTM_SEGSUM

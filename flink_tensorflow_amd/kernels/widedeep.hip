@@ -3,14 +3,15 @@
 // framework kernels per step (casts, cat/pad, slices, BCE pieces, Adam, bf16 weight copies):
 //
 //   wd_gather     x[b] = [emb[cats[b,f] + f*V] for f | dense[b] | 0 pad]  (bf16 MLP input)
-//                 wsum[b] = sum_c wide[cross[b,c], 0]; gids[b*F+f] = cats[b,f] + f*V
+//                 wsum[b] = sum_c wide[cross[b,c], 0]; the sparse grouping keys of both tables
 //   wd_loss       logit = deep[b] + wsum[b] + wide_bias, BCE-with-logits mean (block partials
 //                 added in block order), dlogit = (sigmoid - y) / B, wide gradient rows, the
 //                 scalar gradients (wide bias, head bias 0)
 //   wd_head_bwd   dh[b, j] = (h[b, j] > 0) * dlogit[b] * w_head0[j]   (bf16)
 //   wd_adam       Adam over the flat fp32 parameter buffer (device step counter, so a
 //                 captured step replays correctly) + the bf16 copy of every weight segment
-//   wd_relu_mask  the ReLU backward mask of a layer input, in place on the library dX
+//   wd_mask_colsum  the ReLU backward mask of a layer input, in place on the library dX,
+//                 and the bias gradient (column sums, fixed order) in the same pass
 #include <pybind11/pybind11.h>
 
 #include <stdexcept>
@@ -22,14 +23,15 @@ namespace {
 // G = D/8 lanes per (b, f) embedding row; rows r >= B*F are the per-record rows (dense, pad,
 // wide sum) handled by the G lanes of row B*F + b.
 // cats / dense / cross rows have their own strides (elements): they may be views of one
-// packed record buffer.  wids gets a contiguous copy of the crossed ids (the wide part's
-// sort keys).
+// packed record buffer.  keys [B*F + B*C]: the sparse-gradient grouping keys of BOTH
+// tables in one key space — embedding rows as is, wide rows offset by F*V, invalid ids of
+// either table -> F*V + WV (one dropped bucket) — so one radix sort groups both.
 __global__ __launch_bounds__(256) void wd_gather_kernel(const int* __restrict__ cats, int ldc,
                                                         const float* __restrict__ dense, int ldd,
                                                         const int* __restrict__ cross, int ldx,
                                                         const float* __restrict__ emb, const float* __restrict__ wide,
                                                         bf16* __restrict__ x, float* __restrict__ wsum,
-                                                        int* __restrict__ gids, int* __restrict__ wids, int B, int F,
+                                                        int* __restrict__ keys, int B, int F,
                                                         int V, int D, int gshift, int ND, int XP, int C, int WV,
                                                         int WD) {
   const long t = (long)blockIdx.x * 256 + threadIdx.x;
@@ -39,7 +41,8 @@ __global__ __launch_bounds__(256) void wd_gather_kernel(const int* __restrict__ 
   if (r < nemb) {
     const int b = (int)(r / F), f = (int)(r - (long)b * F);
     const int gid = cats[(size_t)b * ldc + f] + f * V;  // field-local id -> row of the concatenated table
-    if (g == 0) gids[r] = gid;
+    const int FV = F * V, BAD = FV + WV;
+    if (g == 0) keys[r] = (gid >= 0 && gid < FV) ? gid : BAD;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (gid >= 0 && gid < F * V) {
       const f32x4* src = reinterpret_cast<const f32x4*>(emb + (size_t)gid * D + g * 8);
@@ -64,8 +67,9 @@ __global__ __launch_bounds__(256) void wd_gather_kernel(const int* __restrict__ 
       float s = 0.f;
       for (int c = 0; c < C; ++c) {
         const int id = cross[(size_t)b * ldx + c];
-        wids[(size_t)b * C + c] = id;
-        if (id >= 0 && id < WV) s += wide[(size_t)id * WD];
+        const bool ok = id >= 0 && id < WV;
+        keys[nemb + (size_t)b * C + c] = ok ? F * V + id : F * V + WV;
+        if (ok) s += wide[(size_t)id * WD];
       }
       wsum[b] = s;
     }
@@ -170,15 +174,44 @@ __global__ __launch_bounds__(256) void wd_adam_kernel(float* __restrict__ p, con
   }
 }
 
-// x[i] = h[i] > 0 ? x[i] : 0 over bf16 vectors of 8 (the ReLU backward mask of a layer input)
-__global__ __launch_bounds__(256) void wd_relu_mask_kernel(bf16* __restrict__ x, const bf16* __restrict__ h, long n8) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n8) return;
-  bf16x8 xv = reinterpret_cast<bf16x8*>(x)[i];
-  const bf16x8 hv = reinterpret_cast<const bf16x8*>(h)[i];
+// db[j] = sum_b x[b, j] (fp32, fixed order), optionally after the ReLU backward mask of the
+// layer input h (x[b, j] = 0 where h[b, j] <= 0, written back).  Block = 16 columns x 128
+// row lanes; each lane sums every 128th row of its 8 columns, then a fixed LDS tree.
+__global__ __launch_bounds__(256) void wd_mask_colsum_kernel(bf16* __restrict__ x, const bf16* __restrict__ h,
+                                                             float* __restrict__ db, int B, int n) {
+  __shared__ float red[128][17];
+  const int chunk = threadIdx.x & 1;      // which 8 of the block's 16 columns
+  const int rl = threadIdx.x >> 1;        // row lane 0..127
+  const int c0 = blockIdx.x * 16 + chunk * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < n) {
+    for (int b = rl; b < B; b += 128) {
+      bf16x8* px = reinterpret_cast<bf16x8*>(x + (size_t)b * n + c0);
+      bf16x8 xv = *px;
+      if (h) {
+        const bf16x8 hv = *reinterpret_cast<const bf16x8*>(h + (size_t)b * n + c0);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) xv[e] = (float)hv[e] > 0.f ? xv[e] : f2bf(0.f);
-  reinterpret_cast<bf16x8*>(x)[i] = xv;
+        for (int e = 0; e < 8; ++e) xv[e] = (float)hv[e] > 0.f ? xv[e] : f2bf(0.f);
+        *px = xv;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += (float)xv[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl][chunk * 8 + e] = acc[e];
+  __syncthreads();
+  for (int w = 64; w > 0; w >>= 1) {
+    if (rl < w) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[rl][chunk * 8 + e] += red[rl + w][chunk * 8 + e];
+    }
+    __syncthreads();
+  }
+  if (rl == 0 && c0 < n) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) db[c0 + e] = red[0][chunk * 8 + e];
+  }
 }
 
 int pow2_shift(int g) {
@@ -190,21 +223,21 @@ int pow2_shift(int g) {
 }  // namespace
 
 void wd_gather(uintptr_t cats, int ldc, uintptr_t dense, int ldd, uintptr_t cross, int ldx, uintptr_t emb,
-               uintptr_t wide, uintptr_t x, uintptr_t wsum, uintptr_t gids, uintptr_t wids, int B, int F, int V, int D,
+               uintptr_t wide, uintptr_t x, uintptr_t wsum, uintptr_t keys, int B, int F, int V, int D,
                int ND, int XP, int C, int WV, int WD, uintptr_t stream) {
   const int gs = pow2_shift(D / 8);
   if (D % 8 || gs < 0) throw std::invalid_argument("wd_gather: D / 8 must be a power of two <= 64");
   if (XP % 8 || XP < F * D + ND) throw std::invalid_argument("wd_gather: XP must be a multiple of 8 >= F*D + ND");
   if (emb % 16 || x % 16) throw std::invalid_argument("wd_gather: 16-byte alignment required");
-  if ((long)F * V >= (1L << 31)) throw std::invalid_argument("wd_gather: table rows must fit int32");
+  if ((long)F * V + WV >= (1L << 30)) throw std::invalid_argument("wd_gather: table rows must fit the key space");
   if (B <= 0) return;
   const long threads = ((long)B * F + B) << gs;
   hipLaunchKernelGGL(wd_gather_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const int*>(cats), ldc,
                      reinterpret_cast<const float*>(dense), ldd, reinterpret_cast<const int*>(cross), ldx,
                      reinterpret_cast<const float*>(emb), reinterpret_cast<const float*>(wide),
-                     reinterpret_cast<bf16*>(x), reinterpret_cast<float*>(wsum), reinterpret_cast<int*>(gids),
-                     reinterpret_cast<int*>(wids), B, F, V, D, gs, ND, XP, C, WV, WD);
+                     reinterpret_cast<bf16*>(x), reinterpret_cast<float*>(wsum), reinterpret_cast<int*>(keys), B, F,
+                     V, D, gs, ND, XP, C, WV, WD);
   FTM_CHECK_LAUNCH();
 }
 
@@ -248,13 +281,11 @@ void wd_adam(uintptr_t p, uintptr_t g, uintptr_t m, uintptr_t v, long n, uintptr
   FTM_CHECK_LAUNCH();
 }
 
-void wd_relu_mask(uintptr_t x, uintptr_t h, long n, uintptr_t stream) {
-  if (n % 8 || x % 16 || h % 16) throw std::invalid_argument("wd_relu_mask: n % 8 and 16-byte alignment");
-  const long n8 = n / 8;
-  if (n8 <= 0) return;
-  hipLaunchKernelGGL(wd_relu_mask_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<bf16*>(x),
-                     reinterpret_cast<const bf16*>(h), n8);
+void wd_mask_colsum(uintptr_t x, uintptr_t h, uintptr_t db, int B, int n, uintptr_t stream) {
+  if (n % 8 || x % 16 || h % 16) throw std::invalid_argument("wd_mask_colsum: n % 8 and 16-byte alignment");
+  if (B <= 0 || n <= 0) return;
+  hipLaunchKernelGGL(wd_mask_colsum_kernel, dim3((n + 15) / 16), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<bf16*>(x), reinterpret_cast<const bf16*>(h), reinterpret_cast<float*>(db), B, n);
   FTM_CHECK_LAUNCH();
 }
 
@@ -263,5 +294,5 @@ void register_widedeep(pybind11::module_& m) {
   m.def("wd_loss", &wd_loss);
   m.def("wd_head_bwd", &wd_head_bwd);
   m.def("wd_adam", &wd_adam);
-  m.def("wd_relu_mask", &wd_relu_mask);
+  m.def("wd_mask_colsum", &wd_mask_colsum);
 }

@@ -11,11 +11,13 @@ bf16 weight copies).  This step computes the same forward, gradients and updates
 * ``wd_loss``: BCE-with-logits mean, dlogit, the wide gradient rows, the scalar gradients;
 * ``wd_head_bwd`` for the 256 -> 1 head, then per hidden layer the weight gradient as one
   library TN GEMM with an fp32 result (dW = dA^T . H), the bias gradient as a column sum
-  and dX as a library NN GEMM (dA . W, no transposed weight copy) + ``wd_relu_mask``.
+  and dX as a library NN GEMM (dA . W, no transposed weight copy) + ``wd_mask_colsum``
+  (the ReLU mask of the layer input and the next bias gradient in one pass).
   (At this batch the backward GEMMs are 4096-row problems of 32-64 256x256 tiles: the
   ping-pong kernel with its ``drelu`` epilogue uses an eighth of the chip there and
   measured slower than library GEMM + mask, transposes included);
-* the deterministic row-sparse pipeline (sort + segment sum + sparse Adagrad) as before;
+* the deterministic row-sparse pipeline: both tables' lookups in one key space, one radix
+  sort, a reduce-by-key per table, sparse Adagrad;
 * ``wd_adam`` over ONE flat fp32 buffer holding every dense parameter (the module's
   parameters are views of it), writing the bf16 copies the next forward reads.
 
@@ -29,7 +31,7 @@ import torch
 
 from ... import _ext
 from ...ops import kernels as K
-from ...ops.embedding import segment_sum, sparse_adagrad
+from ...ops.embedding import group_keys, segment_sum, segment_sum_grouped, sparse_adagrad
 from ...parallel import comm
 
 
@@ -50,8 +52,7 @@ class _Acts:
         self.da = [torch.empty(B, l.weight.shape[0], **bf) for l in step.layers]
         self.de = torch.empty(B, step.F * step.D, **bf)
         self.wsum = torch.empty(B, dtype=torch.float32, device=dev)
-        self.gids = torch.empty(B * step.F, dtype=torch.int32, device=dev)
-        self.wids = None
+        self.keys = None
         self.dlogit = torch.empty(B, dtype=torch.float32, device=dev)
         self.dlogit16 = torch.empty(B, **bf)
         self.loss = torch.empty((), dtype=torch.float32, device=dev)
@@ -128,7 +129,7 @@ class FusedWideDeepStep:
         if a.wgrad is None or a.C != C:
             a.C = C
             a.wgrad = torch.empty(B * C, WD, dtype=torch.float32, device=self.dev)
-            a.wids = torch.empty(B * C, dtype=torch.int32, device=self.dev)
+            a.keys = torch.empty(B * self.F + B * C, dtype=torch.int32, device=self.dev)
         s = _stream()
         # the inputs may be strided views of one packed record buffer (rows of label | dense |
         # cats | cross): the kernels take row strides, no splitting copies
@@ -138,8 +139,7 @@ class FusedWideDeepStep:
         # forward
         H.wd_gather(cats.data_ptr(), cats.stride(0), dense.data_ptr(), dense.stride(0), cross.data_ptr(),
                     cross.stride(0), m.emb.table.data_ptr(), m.wide.table.data_ptr(), a.x.data_ptr(), a.wsum.data_ptr(),
-                    a.gids.data_ptr(), a.wids.data_ptr(), B, self.F, cfg.vocab_per_field, self.D, self.ND, self.XP, C,
-                    WV, WD, s)
+                    a.keys.data_ptr(), B, self.F, cfg.vocab_per_field, self.D, self.ND, self.XP, C, WV, WD, s)
         h = a.x
         for i, l in enumerate(self.layers):
             h = K.gemm(h, self.w16[i], l.bias, None, "relu", out=a.h[i])
@@ -152,30 +152,38 @@ class FusedWideDeepStep:
         torch.mm(a.dlogit16.view(1, B), last, out_dtype=torch.float32, out=self.g["head.weight"][0:1])
         H.wd_head_bwd(last.data_ptr(), a.dlogit.data_ptr(), m.head.weight.data_ptr(), a.da[-1].data_ptr(), B,
                       last.shape[1], s)
+        n_top = a.da[-1].shape[1]
+        H.wd_mask_colsum(a.da[-1].data_ptr(), 0, self.g[f"mlp.{len(self.layers) - 1}.bias"].data_ptr(), B, n_top, s)
         for i in range(len(self.layers) - 1, -1, -1):
-            da = a.da[i]
+            da = a.da[i]  # masked; its column sums are already in the bias gradient
             inp = a.h[i - 1] if i else a.x
             torch.mm(da.t(), inp, out_dtype=torch.float32, out=self.g[f"mlp.{i}.weight"])
-            torch.sum(da, 0, dtype=torch.float32, out=self.g[f"mlp.{i}.bias"])
-            if i:  # dX, then the ReLU mask of this layer's input
+            if i:  # dX, then the ReLU mask of this layer's input + the next bias gradient
                 torch.mm(da, self.w16[i], out=a.da[i - 1])
-                H.wd_relu_mask(a.da[i - 1].data_ptr(), inp.data_ptr(), inp.numel(), s)
+                H.wd_mask_colsum(a.da[i - 1].data_ptr(), inp.data_ptr(), self.g[f"mlp.{i - 1}.bias"].data_ptr(), B,
+                                 inp.shape[1], s)
             else:  # embedding columns of dX only
                 torch.mm(da, self.w16[0][:, : self.F * self.D], out=a.de)
-        # sparse rows
-        ue, re = segment_sum(a.gids, a.de.view(B * self.F, self.D), m.emb.table.shape[0], static=True)
-        uw, rw = segment_sum(a.wids, a.wgrad, WV, static=True)
+        # sparse rows: both tables share one key space (wide ids offset by the embedding
+        # rows) and one radix sort; each table's sums read only its own lookups
+        FV = m.emb.table.shape[0]
+        ne = B * self.F
+        groups = group_keys(a.keys, FV + WV)
+        u = groups[3]
+        re = segment_sum_grouped(groups, a.de.view(ne, self.D), 1, 0, ne)
+        rw = segment_sum_grouped(groups, a.wgrad, 1, ne, ne + B * C)
+        ue = uw = u
         ws = 1
         if comm.is_dist():
             from .wide_deep import _sparse_sync
 
-            ue, re = segment_sum(*_sparse_sync(ue, re), m.emb.table.shape[0], static=True)
-            uw, rw = segment_sum(*_sparse_sync(uw, rw), WV, static=True)
+            ue, re = segment_sum(*_sparse_sync(u, re), FV + WV, static=True)
+            uw, rw = segment_sum(*_sparse_sync(u, rw), FV + WV, static=True)
             c = comm.get()
             c.all_reduce(self.grad)  # one collective for every dense gradient
             ws = c.size
         sparse_adagrad(m.emb.table.data, m.emb.accum, ue, re, self.lr_sparse)
-        sparse_adagrad(m.wide.table.data, m.wide.accum, uw, rw, self.lr_sparse)
+        sparse_adagrad(m.wide.table.data, m.wide.accum, uw, rw, self.lr_sparse, offset=FV)
         # dense Adam over the flat buffer + the bf16 operands of the next step
         self.t.add_(1.0)
         H.wd_adam(self.flat.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),

@@ -31,14 +31,13 @@ def embedding_bag(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | No
 _SLICE = 8  # sorted rows per lane group in the static segment sum (one batch of 8 loads)
 
 
-def _segment_sum_static(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L: int):
-    """Sync-free, static-shape segment sum on the GPU: outputs are sized by the number of
-    keys n (an upper bound of the unique count); unused slots carry uid -1 and zero rows.
-    No ``.item()`` / ``unique`` host round trip, so a training step stays asynchronous
-    (and capturable).  Grouping: ``kernels/sort_segments.hip`` (radix sort over the key
-    bits actually used + run boundaries); sums: ``segment_sum_sorted``."""
+def group_keys(keys: torch.Tensor, num_rows: int):
+    """Static-shape grouping of int32 keys on the GPU (``kernels/sort_segments.hip``: radix
+    sort over the key bits in use + run boundaries; keys outside [0, num_rows) form one
+    dropped bucket).  Returns ``(perm, seg_id, seg, uids)``: the stable sorted order, the
+    run of every sorted position, the run starts (n past the last run) and the run keys
+    (-1 past the runs / for the dropped bucket) — one slot per key, no host sync."""
     n = keys.numel()
-    D = rows.shape[1]
     dev = keys.device
     H = _hip()
     flat = keys.reshape(-1)
@@ -53,17 +52,37 @@ def _segment_sum_static(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L
     temp = torch.empty(tb, dtype=torch.uint8, device=dev)
     H.sort_segments(flat.data_ptr(), n, num_rows, sorted_k.data_ptr(), perm.data_ptr(), seg_id.data_ptr(),
                     seg.data_ptr(), uids.data_ptr(), work.data_ptr(), temp.data_ptr(), tb, _stream())
+    return perm, seg_id, seg, uids
+
+
+def segment_sum_grouped(groups, rows: torch.Tensor, L: int = 1, lo: int = 0, hi: int | None = None) -> torch.Tensor:
+    """Per-run sums (fp32 [n, D], one row per run slot, zero for empty slots) of ``rows``
+    under a ``group_keys`` grouping; only sorted positions whose original index lies in
+    [lo, hi) contribute (row (index - lo) // L): tables sharing one key space share one
+    sort.  Reduce-by-key over fixed slices + a fix-up pass for runs spanning slices (hot
+    ids), all in fixed order (``kernels/embedding.hip``)."""
+    perm, seg_id, seg, _ = groups
+    n = perm.numel()
+    D = rows.shape[1]
+    hi = n if hi is None else hi
     out = torch.empty((n, D), dtype=torch.float32, device=rows.device)
     g = rows.contiguous()
     fp32 = g.dtype == torch.float32
     if not fp32 and g.dtype != torch.bfloat16:
         g = g.to(torch.bfloat16)
-    # reduce-by-key over fixed slices of the sorted rows + a fix-up pass for the runs that
-    # span slices (hot ids), all in fixed order: see kernels/embedding.hip
     ws = torch.empty(2 * (-(-n // _SLICE)) * D, dtype=torch.float32, device=rows.device)
-    H.segment_sum_sorted(g.data_ptr(), perm.data_ptr(), seg_id.data_ptr(), seg.data_ptr(), out.data_ptr(),
-                         ws.data_ptr(), n, n, D, L, _SLICE, int(fp32), _stream())
-    return uids, out
+    _hip().segment_sum_sorted(g.data_ptr(), perm.data_ptr(), seg_id.data_ptr(), seg.data_ptr(), out.data_ptr(),
+                              ws.data_ptr(), n, n, D, L, _SLICE, int(fp32), lo, hi, _stream())
+    return out
+
+
+def _segment_sum_static(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L: int):
+    """Sync-free, static-shape segment sum on the GPU: outputs are sized by the number of
+    keys n (an upper bound of the unique count); unused slots carry uid -1 and zero rows.
+    No ``.item()`` / ``unique`` host round trip, so a training step stays asynchronous
+    (and capturable)."""
+    groups = group_keys(keys, num_rows)
+    return groups[3], segment_sum_grouped(groups, rows, L)
 
 
 def segment_sum(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L: int = 1, static: bool = False):
@@ -118,7 +137,9 @@ def embedding_bag_backward(ids: torch.Tensor, grad_out: torch.Tensor, num_rows: 
 
 
 def sparse_adagrad(table: torch.Tensor, accum: torch.Tensor, uids: torch.Tensor, grads: torch.Tensor, lr: float,
-                   eps: float = 1e-8) -> None:
+                   eps: float = 1e-8, offset: int = 0) -> None:
+    """Adagrad on the rows ``uids - offset`` (``offset``: the table's base in a key space
+    shared with other tables; ids outside the table, and -1, are skipped)."""
     U, D = grads.shape
     if table.is_cuda:
         _check(table, "table", torch.float32, table.device)
@@ -126,9 +147,10 @@ def sparse_adagrad(table: torch.Tensor, accum: torch.Tensor, uids: torch.Tensor,
         _check(grads, "grads", torch.float32, table.device)
         _check(uids, "uids", torch.int32, table.device)
         _hip().sparse_adagrad(table.data_ptr(), accum.data_ptr(), uids.data_ptr(), grads.data_ptr(), U, D,
-                              table.shape[0], float(lr), float(eps), _stream())
+                              table.shape[0], float(lr), float(eps), int(offset), _stream())
         return
-    keep = (uids >= 0) & (uids < table.shape[0])  # static-shape padding slots
+    uids = torch.where(uids >= 0, uids - offset, -1)
+    keep = (uids >= 0) & (uids < table.shape[0])  # static-shape padding slots / other tables
     uids, grads = uids[keep], grads[keep]
     idx = uids.long()
     a = accum[idx] + grads * grads
