@@ -1,0 +1,4 @@
+source tools/gpu_calls/gpu_steps.sh
+step pytest_gpu 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread
+step bert_stream 300 python -u examples/bert_stream.py --records 16384 --batch 256
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
