@@ -216,3 +216,48 @@ def test_fused_dp_replicas_stay_identical_gpu():
     assert [o["rank"] for o in out] == [0, 1] and all(o["fused"] for o in out)
     assert out[0]["sums"] == out[1]["sums"]
     assert out[0]["losses"] != out[1]["losses"]  # the ranks did see different data
+
+
+def test_sparse_adagrad_offset_host():
+    """Two tables in one key space: each table's update takes only its own ids."""
+    ta, tb = torch.zeros(10, 8), torch.zeros(6, 8)
+    aa, ab = torch.full((10, 8), 0.1), torch.full((6, 8), 0.1)
+    uids = torch.tensor([3, 12, -1, 15], dtype=torch.int32)   # 3 -> table a; 12, 15 -> table b rows 2, 5
+    g = torch.ones(4, 8)
+    E.sparse_adagrad(ta, aa, uids, g, 0.5)
+    E.sparse_adagrad(tb, ab, uids, g, 0.5, offset=10)
+    assert ta[3].ne(0).all() and ta.abs().sum(1).ne(0).sum() == 1
+    assert tb[2].ne(0).all() and tb[5].ne(0).all() and tb.abs().sum(1).ne(0).sum() == 2
+
+
+@pytest.mark.gpu
+def test_group_keys_and_grouped_sums_gpu():
+    """``group_keys`` (radix sort over the used bits + runs) == a stable torch sort, invalid
+    keys in one dropped bucket; ``segment_sum_grouped`` with index ranges sums two tables
+    that share the key space from one grouping."""
+    dev = torch.device("cuda", 0)
+    g0 = torch.Generator().manual_seed(3)
+    ka = torch.randint(-2, 500, (3000,), generator=g0, dtype=torch.int32)
+    ka[::7] = 11                                              # hot key
+    kb = torch.randint(0, 300, (1000,), generator=g0, dtype=torch.int32) + 500
+    keys = torch.cat([ka, kb]).to(dev)
+    perm, seg_id, seg, uids = E.group_keys(keys, 800)
+    k = keys.cpu().long()
+    kk = torch.where((k >= 0) & (k < 800), k, torch.full_like(k, 800))
+    sk, sp = torch.sort(kk, stable=True)
+    assert torch.equal(perm.cpu().long(), sp)
+    runs = torch.unique_consecutive(sk)
+    nr = runs.numel()
+    want = torch.where(runs < 800, runs, torch.full_like(runs, -1)).to(torch.int32)
+    assert torch.equal(uids[:nr].cpu(), want) and (uids[nr:] == -1).all()
+    ra = torch.randn(3000, 16, generator=g0).to(torch.bfloat16)
+    rb = torch.randn(1000, 8, generator=g0)
+    sa = E.segment_sum_grouped((perm, seg_id, seg, uids), ra.to(dev), 1, 0, 3000).cpu()
+    sb = E.segment_sum_grouped((perm, seg_id, seg, uids), rb.to(dev), 1, 3000, 4000).cpu()
+    for i in range(nr):
+        key = int(runs[i])
+        ia = [j for j in range(3000) if int(kk[j]) == key]
+        ib = [j - 3000 for j in range(3000, 4000) if int(kk[j]) == key]
+        torch.testing.assert_close(sa[i], ra.float()[ia].sum(0) if ia else torch.zeros(16), rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(sb[i], rb[ib].sum(0) if ib else torch.zeros(8), rtol=1e-4, atol=1e-4)
+    assert sa[nr:].abs().sum() == 0 and sb[nr:].abs().sum() == 0
