@@ -42,8 +42,9 @@ class SignatureBatchedModel(SavedModel_, BatchedGpuModel):
     def __init__(self, path: str, signature: str = SignatureConstants.DEFAULT_SERVING_SIGNATURE_DEF_KEY,
                  input_key: str | None = None, output_keys: Sequence[str] | None = None,
                  record_shape: Sequence[int] | None = None, buckets: Sequence[int] = (64, 256), lanes: int = 2,
-                 depth: int = 3, precision: str = "bf16", tags: Sequence[str] = (TAG_SERVE,), device=None):
-        super().__init__(path, tags, device)
+                 depth: int = 3, precision: str = "bf16", tags: Sequence[str] = (TAG_SERVE,), device=None,
+                 distributed_weights: bool = False):
+        super().__init__(path, tags, device, distributed_weights)
         self.signature = signature
         self.input_key = input_key
         self.output_keys = list(output_keys) if output_keys is not None else None

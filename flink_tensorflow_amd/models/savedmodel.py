@@ -98,7 +98,26 @@ def asset_file_defs(mg: MetaGraphDef) -> list[AssetFileDef]:
     return out
 
 
-def load_bundle(local_dir: str, tags: Sequence[str], device=None) -> SavedModelBundle:
+def _allocate_variables(sess: Session, var_prefix: str) -> bool:
+    """Every variable of the bundle allocated (uninitialised) on the session's device from
+    the index alone — no tensor data read.  False when a variable cannot be received by a
+    broadcast (STRING), in which case the caller restores normally."""
+    from ..io import bundle
+    from ..types.dtypes import DataType
+
+    with bundle.BundleReader(var_prefix) as r:
+        specs = {k: r.dtype_and_shape(k) for k in r.keys()}
+    if any(dt == DataType.STRING for dt, _ in specs.values()):
+        return False
+    dev = sess.device
+    for k, (dt, shape) in specs.items():
+        sess.variables[k] = torch.empty(shape, dtype=dt.torch, device=dev)
+    return True
+
+
+def load_bundle(local_dir: str, tags: Sequence[str], device=None, read_variables: bool = True) -> SavedModelBundle:
+    """``read_variables=False``: variables are only allocated from the checkpoint index (a
+    data-parallel rank that receives rank 0's values by broadcast)."""
     sm = read_saved_model(local_dir)
     mg = select_meta_graph(sm, tags)
     g = Graph.from_graph_def(mg.graph_def)
@@ -106,8 +125,9 @@ def load_bundle(local_dir: str, tags: Sequence[str], device=None) -> SavedModelB
     var_prefix = os.path.join(local_dir, VARIABLES_DIRECTORY, VARIABLES_FILENAME)
     sd = mg.saver_def
     if sd is not None and sd.restore_op_name and os.path.exists(var_prefix + ".index"):
-        sess.run(targets=[sd.restore_op_name.split(":")[0]],
-                 feed_dict={sd.filename_tensor_name: StringTensor(var_prefix.encode())})
+        if read_variables or not _allocate_variables(sess, var_prefix):
+            sess.run(targets=[sd.restore_op_name.split(":")[0]],
+                     feed_dict={sd.filename_tensor_name: StringTensor(var_prefix.encode())})
     asset_feeds = {}
     for a in asset_file_defs(mg):
         asset_feeds[a.tensor_info.name] = StringTensor(os.path.join(local_dir, ASSETS_DIRECTORY, a.filename).encode())
@@ -145,9 +165,9 @@ class DefaultSavedModelLoader(SavedModelLoader):
             self._metagraph = select_meta_graph(read_saved_model(self.export_path), self.tags)
         return self._metagraph
 
-    def load(self, device=None) -> SavedModelBundle:
+    def load(self, device=None, read_variables: bool = True) -> SavedModelBundle:
         local = fs.copy_to_local(self.export_path)
-        return load_bundle(local, self.tags, device=device)
+        return load_bundle(local, self.tags, device=device, read_variables=read_variables)
 
 
 class TensorFlowModel(RichModel, CheckpointedModel):
@@ -155,8 +175,11 @@ class TensorFlowModel(RichModel, CheckpointedModel):
 
     _TRANSIENT = ("_bundle", "_functions")
 
-    def __init__(self, device=None):
+    def __init__(self, device=None, distributed_weights: bool = False):
         self.device = device
+        # data parallel: rank 0 reads the variables, the other ranks receive them (RCCL
+        # broadcast) instead of every rank reading the checkpoint
+        self.distributed_weights = distributed_weights
         self._bundle: SavedModelBundle | None = None
         self._pending_restore: str | None = None
 
@@ -176,7 +199,21 @@ class TensorFlowModel(RichModel, CheckpointedModel):
         if self._bundle is not None:
             raise RuntimeError("model already open")  # checkState(bundle == null)
         dev = self.device if self.device is not None else default_device()
-        self._bundle = self.loader.load(device=dev)
+        from ..parallel import comm
+
+        dist = self.distributed_weights and comm.is_dist()
+        if dist and comm.rank_size()[0] != 0:
+            try:
+                self._bundle = self.loader.load(device=dev, read_variables=False)
+            except TypeError:  # a custom loader without the option: it reads, rank 0's values win
+                self._bundle = self.loader.load(device=dev)
+        else:
+            self._bundle = self.loader.load(device=dev)
+        if dist:
+            vs = self._bundle.session.variables
+            comm.broadcast_tensors([vs[k] for k in sorted(vs) if isinstance(vs[k], torch.Tensor)], src=0)
+            if hasattr(vs, "touch"):
+                vs.touch()
         if self._pending_restore is not None:  # initialize_state ran before open()
             prefix, self._pending_restore = self._pending_restore, None
             self.restore_variables(prefix)
@@ -255,8 +292,9 @@ class TensorFlowModel(RichModel, CheckpointedModel):
 class SavedModel_(TensorFlowModel):
     """Concrete TensorFlowModel over a path (for users who don't subclass)."""
 
-    def __init__(self, path: str, tags: Sequence[str] = (TAG_SERVE,), device: str | torch.device | None = None):
-        super().__init__(device)
+    def __init__(self, path: str, tags: Sequence[str] = (TAG_SERVE,), device: str | torch.device | None = None,
+                 distributed_weights: bool = False):
+        super().__init__(device, distributed_weights)
         self._loader = DefaultSavedModelLoader(path, tags)
 
     @property

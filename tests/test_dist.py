@@ -242,3 +242,38 @@ def test_torchrun_agent_store_rendezvous():
     assert [o["rank"] for o in out] == [0, 1]
     for o in out:
         assert o["bcast"] == [1.0] * 4 and o["sum"] == [3.0] * 3 and o["objs"] == [0, 1]
+
+
+def _savedmodel_rank0_broadcast(paths, dist_weights, rank, world):
+    from flink_tensorflow_amd.models import RegressionMethod, SavedModelModel
+    from flink_tensorflow_amd.types import example, feature
+
+    m = SavedModelModel(paths[rank], device="cpu", distributed_weights=dist_weights)
+    m.open()
+    y = m.function("regress_x_to_y", RegressionMethod()).apply([example(("x", feature(1.0)))])
+    a = float(m.session().variables["a"])
+    m.close()
+    return [float(y.reshape(-1)[0]), a]
+
+
+def test_savedmodel_variables_read_by_rank0_and_broadcast(half_plus_two, tmp_path):
+    """``distributed_weights=True``: rank 0 reads the SavedModel's variables, the other
+    ranks only allocate them from the checkpoint index and receive rank 0's values — rank 1
+    here points at a copy whose ``a`` was re-saved as 3 and still computes 0.5 x + 2."""
+    import functools
+    import shutil
+
+    from flink_tensorflow_amd.io.saver import VariableSaver
+    from flink_tensorflow_amd.models import SavedModelModel
+
+    other = str(tmp_path / "hpt_a3")
+    shutil.copytree(half_plus_two, other)
+    m = SavedModelModel(other, device="cpu")
+    m.open()
+    m.session().variables["a"].fill_(3.0)
+    VariableSaver().save(m.session(), os.path.join(other, "variables", "variables"))
+    m.close()
+    out = _run(functools.partial(_savedmodel_rank0_broadcast, [half_plus_two, other], True))
+    assert out[0] == [2.5, 0.5] and out[1] == [2.5, 0.5], out
+    ctrl = _run(functools.partial(_savedmodel_rank0_broadcast, [half_plus_two, other], False))
+    assert ctrl[1] == [5.0, 3.0], ctrl  # without it, rank 1 serves its own copy
