@@ -21,7 +21,6 @@ write all weights and optimizer state as a TensorBundle V2 into the checkpoint d
 from __future__ import annotations
 
 import os
-import time
 from dataclasses import dataclass
 
 import numpy as np

@@ -18,7 +18,6 @@
 """
 from __future__ import annotations
 
-import abc
 import os
 import time
 
@@ -26,7 +25,7 @@ import numpy as np
 
 from ..models.core import BatchedGpuModel, CheckpointedModel, RichModel  # noqa: F401  (re-exported)
 from . import functions as F
-from .operators import Collector, Operator, Record
+from .operators import Operator, Record
 
 
 
