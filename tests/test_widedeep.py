@@ -261,3 +261,32 @@ def test_group_keys_and_grouped_sums_gpu():
         torch.testing.assert_close(sa[i], ra.float()[ia].sum(0) if ia else torch.zeros(16), rtol=1e-4, atol=1e-4)
         torch.testing.assert_close(sb[i], rb[ib].sum(0) if ib else torch.zeros(8), rtol=1e-4, atol=1e-4)
     assert sa[nr:].abs().sum() == 0 and sb[nr:].abs().sum() == 0
+
+
+@pytest.mark.gpu
+def test_fused_step_checkpoint_roundtrip_gpu(tmp_path):
+    """CheckpointedModel on the fused path: weights, tables and the flat Adam state go into
+    the checkpoint bundle; a fresh trainer restored from it continues exactly like the
+    uninterrupted one."""
+    from flink_tensorflow_amd.runtime.functions import InitializationContext, SnapshotContext
+    from flink_tensorflow_amd.runtime.state import OperatorStateStore
+
+    dev = torch.device("cuda", 0)
+    cfg = WideDeepConfig.tiny(hidden=(128, 64), embed_dim=16)
+    recs = synthetic_click_records(256 * 6, cfg, seed=12)
+    a = WideDeepTrainer(cfg, device=dev, seed=4, fused=True)
+    a.open()
+    batches = [a.collate(recs[i * 256:(i + 1) * 256]) for i in range(6)]
+    for b in batches[:3]:
+        a.train_step(batch=b)
+    ops = OperatorStateStore()
+    a.snapshot_state(SnapshotContext(1, 0.0, ops, str(tmp_path), 0))
+    r = WideDeepTrainer(cfg, device=dev, seed=99, fused=True)  # different init: all of it must come back
+    r.open()
+    r.initialize_state(InitializationContext(ops, True, str(tmp_path), 0))
+    la = [float(a.train_step(batch=b)) for b in batches[3:]]
+    lr = [float(r.train_step(batch=b)) for b in batches[3:]]
+    torch.testing.assert_close(torch.tensor(lr), torch.tensor(la), rtol=1e-5, atol=1e-6)
+    for (k, va), vb in zip(a.model.state_dict().items(), r.model.state_dict().values()):
+        torch.testing.assert_close(vb, va, rtol=1e-5, atol=1e-6, msg=k)
+    assert r.steps == a.steps == 6  # the step counter came back too
