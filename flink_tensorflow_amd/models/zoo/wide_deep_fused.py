@@ -133,6 +133,8 @@ class FusedWideDeepStep:
         s = _stream()
         # the inputs may be strided views of one packed record buffer (rows of label | dense |
         # cats | cross): the kernels take row strides, no splitting copies
+        cats, cross = (t if t.dtype == torch.int32 else t.to(torch.int32) for t in (cats, cross))
+        dense, labels = (t if t.dtype == torch.float32 else t.float() for t in (dense, labels))
         cats, dense, cross = (t if t.stride(-1) == 1 else t.contiguous() for t in (cats, dense, cross))
         if labels.dim() != 1:
             labels = labels.reshape(-1)
