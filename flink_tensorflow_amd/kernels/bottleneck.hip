@@ -21,7 +21,7 @@
 //            and back into Y
 //   phase 2  8 waves over (TP pixels x CN channels), K = 256; + b1, relu -> X region ->
 //            coalesced 16-B y1 stores
-//   the next tile's x2 is loaded into registers during phase 2.
+//   the next tile's x2 and residual rows are loaded into registers during phase 2.
 #include <pybind11/pybind11.h>
 
 #include <stdexcept>
@@ -53,7 +53,8 @@ __global__ __launch_bounds__(NT, 1) void bottleneck_tail_kernel(const bf16* __re
                                                                 const bf16* __restrict__ res,
                                                                 const bf16* __restrict__ w3, const float* __restrict__ b3,
                                                                 const bf16* __restrict__ w1, const float* __restrict__ b1,
-                                                                bf16* __restrict__ y3, bf16* __restrict__ y1, int M) {
+                                                                bf16* __restrict__ y3, bf16* __restrict__ y1, int M,
+                                                                int dec_h, int dec_w) {
   constexpr int CM = DUAL ? 2 * CX : CX;  // GEMM-1 depth
   constexpr int W3_BYTES = CO * CM * 2;
   constexpr int W1_BYTES = CN * CO * 2;
@@ -97,7 +98,23 @@ __global__ __launch_bounds__(NT, 1) void bottleneck_tail_kernel(const bf16* __re
     }
   };
 
+  // residual rows of a tile, 16-B chunks in the pass's thread order; loaded one tile ahead
+  // (during the previous tile's phase 2) so the pass never waits on HBM
+  constexpr int YIT = YCH / NT;
+  static_assert(NT / (CO / 8) == 16, "pass: 16 pixels per iteration");
+  u32x4 rv[YIT];
+  auto load_r = [&](int tt) {
+#pragma unroll
+    for (int it = 0; it < YIT; ++it) {
+      const int q = tid + it * NT;
+      const int px = tt * TP + (q >> 5);
+      rv[it] = (!DUAL && px < M) ? reinterpret_cast<const u32x4*>(res + (size_t)px * CO)[q & 31]
+                                 : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+
   int t = blockIdx.x;
+  load_r(t);
   load_x(t);
   store_x();
   __syncthreads();
@@ -140,14 +157,15 @@ __global__ __launch_bounds__(NT, 1) void bottleneck_tail_kernel(const bf16* __re
     __syncthreads();
     // ---- pass: + residual, relu -> y3 (global) and back into Y (coalesced 16-B chunks)
     {
-      constexpr int YIT = YCH / NT;
-      u32x4 rv[YIT];
-#pragma unroll
-      for (int it = 0; it < YIT; ++it) {  // all residual loads in flight first
-        const int q = tid + it * NT;
-        const int px = p0 + (q >> 5);
-        rv[it] = (!DUAL && px < M) ? reinterpret_cast<const u32x4*>(res + (size_t)px * CO)[q & 31]
-                                   : u32x4{0u, 0u, 0u, 0u};
+      // decimated y3: (n, h, w) of this thread's first pass pixel, advanced by 16 pixels per
+      // iteration (one divide pair per tile, not per store)
+      int dn = 0, dh = 0, dw = 0;
+      if (dec_w) {
+        const int o0 = p0 + (tid >> 5);
+        dw = o0 % dec_w;
+        const int tt = o0 / dec_w;
+        dh = tt % dec_h;
+        dn = tt / dec_h;
       }
 #pragma unroll
       for (int it = 0; it < YIT; ++it) {
@@ -159,12 +177,28 @@ __global__ __launch_bounds__(NT, 1) void bottleneck_tail_kernel(const bf16* __re
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = f2bf(fmaxf((float)v[e] + (float)r[e], 0.f));
         Ys[si] = __builtin_bit_cast(u32x4, v);
-        if (p0 + pl < M) reinterpret_cast<u32x4*>(y3 + (size_t)(p0 + pl) * CO)[c] = __builtin_bit_cast(u32x4, v);
+        int o = p0 + pl;
+        bool st = o < M;
+        if (dec_w) {  // decimated y3: only the even (h, w) pixels, compact [N, H/2, W/2, 256]
+          if (it) {
+            dw += 16;
+            while (dw >= dec_w) {
+              dw -= dec_w;
+              if (++dh == dec_h) { dh = 0; ++dn; }
+            }
+          }
+          st = st && !((dh | dw) & 1);
+          o = (dn * (dec_h >> 1) + (dh >> 1)) * (dec_w >> 1) + (dw >> 1);
+        }
+        if (st) reinterpret_cast<u32x4*>(y3 + (size_t)o * CO)[c] = __builtin_bit_cast(u32x4, v);
       }
     }
     const int tn = t + gridDim.x;
     const bool more = tn < ntiles;
-    if (more) load_x(tn);  // next tile's x2 in flight during phase 2
+    if (more) {  // next tile's x2 and residual in flight during phase 2
+      load_x(tn);
+      if constexpr (!DUAL) load_r(tn);
+    }
     __syncthreads();
     // ---- phase 2: y1 tile = relu(Y . W1^T + b1)  (wave: one 16-pixel fragment, NF2 x 16 channels)
     const int pf = wave / WPG, cbase = (wave % WPG) * NF2 * 16;
@@ -209,7 +243,7 @@ __global__ __launch_bounds__(NT, 1) void bottleneck_tail_kernel(const bf16* __re
 
 template <int TP, int CN, bool DUAL>
 void launch_tail(const bf16* x2, const bf16* xs, const bf16* res, const bf16* w3, const float* b3, const bf16* w1,
-                 const float* b1, bf16* y3, bf16* y1, int M, int num_cu, hipStream_t stream) {
+                 const float* b1, bf16* y3, bf16* y1, int M, int num_cu, hipStream_t stream, int dec_h, int dec_w) {
   constexpr int CM = DUAL ? 2 * CX : CX;
   const int tiles = (M + TP - 1) / TP;
   const int grid = tiles < num_cu ? tiles : num_cu;
@@ -218,7 +252,7 @@ void launch_tail(const bf16* x2, const bf16* xs, const bf16* res, const bf16* w3
   hipFuncSetAttribute((const void*)bottleneck_tail_kernel<TP, CN, DUAL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                       lds);
   hipLaunchKernelGGL((bottleneck_tail_kernel<TP, CN, DUAL>), dim3(grid), dim3(NT), lds, stream, x2, xs, res, w3, b3, w1,
-                     b1, y3, y1, M);
+                     b1, y3, y1, M, dec_h, dec_w);
 }
 
 
@@ -440,22 +474,28 @@ __global__ __launch_bounds__(NT, 1) void bottleneck_tail_wide_kernel(
 // [256, 128] = [W3 | Wsc]), b3 [256], w1 [cn, 256], b1 [cn] -> y3 [M, 256], y1 [M, cn]
 // (all bf16 rows contiguous; biases fp32); cn = 64 or 128 (128: identity residual only).
 void bottleneck_tail_bf16(uintptr_t x2, uintptr_t xs, uintptr_t res, uintptr_t w3, uintptr_t b3, uintptr_t w1,
-                          uintptr_t b1, uintptr_t y3, uintptr_t y1, int M, int cn, int num_cu, uintptr_t stream) {
+                          uintptr_t b1, uintptr_t y3, uintptr_t y1, int M, int cn, int num_cu, uintptr_t stream,
+                          int dec_h, int dec_w) {
   if (M <= 0) throw std::invalid_argument("bottleneck_tail: empty problem");
   if ((long)M * CO >= (1L << 31)) throw std::invalid_argument("bottleneck_tail: tensor too large for 32-bit indexing");
   const bool dual = xs != 0;
   if (dual == (res != 0)) throw std::invalid_argument("bottleneck_tail: pass exactly one of xs (dual) and res");
   for (uintptr_t p : {x2, dual ? xs : res, w3, w1, y3, y1, b3, b1})
     if (!p || p % 16) throw std::invalid_argument("bottleneck_tail: null or non-16-byte-aligned pointer");
+  // dec_h x dec_w > 0: y3 is stored decimated (its only other reader is a stride-2 1x1
+  // projection shortcut, ResNet's stage-1 -> stage-2 boundary): 1/4 of the y3 bytes
+  if (dec_w < 0 || dec_h < 0 || (dec_w > 0) != (dec_h > 0) || dec_w % 2 || dec_h % 2 ||
+      (dec_w > 0 && M % (dec_h * dec_w)))
+    throw std::invalid_argument("bottleneck_tail: decimation needs even H, W dividing the pixel count");
   auto s = reinterpret_cast<hipStream_t>(stream);
   auto bp = [](uintptr_t p) { return reinterpret_cast<bf16*>(p); };
   auto fp = [](uintptr_t p) { return reinterpret_cast<const float*>(p); };
   if (dual && cn == 64)
-    launch_tail<64, 64, true>(bp(x2), bp(xs), nullptr, bp(w3), fp(b3), bp(w1), fp(b1), bp(y3), bp(y1), M, num_cu, s);
+    launch_tail<64, 64, true>(bp(x2), bp(xs), nullptr, bp(w3), fp(b3), bp(w1), fp(b1), bp(y3), bp(y1), M, num_cu, s, dec_h, dec_w);
   else if (!dual && cn == 64)
-    launch_tail<128, 64, false>(bp(x2), nullptr, bp(res), bp(w3), fp(b3), bp(w1), fp(b1), bp(y3), bp(y1), M, num_cu, s);
+    launch_tail<128, 64, false>(bp(x2), nullptr, bp(res), bp(w3), fp(b3), bp(w1), fp(b1), bp(y3), bp(y1), M, num_cu, s, dec_h, dec_w);
   else if (!dual && cn == 128)
-    launch_tail<64, 128, false>(bp(x2), nullptr, bp(res), bp(w3), fp(b3), bp(w1), fp(b1), bp(y3), bp(y1), M, num_cu, s);
+    launch_tail<64, 128, false>(bp(x2), nullptr, bp(res), bp(w3), fp(b3), bp(w1), fp(b1), bp(y3), bp(y1), M, num_cu, s, dec_h, dec_w);
   else
     throw std::invalid_argument("bottleneck_tail: unsupported variant (dual " + std::to_string(dual) + ", cn " +
                                 std::to_string(cn) + ")");

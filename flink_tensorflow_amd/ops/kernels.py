@@ -211,7 +211,7 @@ def conv3x3_c64(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor, act=N
 
 def bottleneck_tail(x2: torch.Tensor, res: torch.Tensor | None, w3: torch.Tensor, b3: torch.Tensor, w1: torch.Tensor,
                     b1: torch.Tensor, y3: torch.Tensor | None = None, y1: torch.Tensor | None = None,
-                    xs: torch.Tensor | None = None):
+                    xs: torch.Tensor | None = None, y3_decimated: bool = False):
     """Fused ResNet bottleneck block boundary (kernels/bottleneck.hip):
     ``y3 = relu(x2 @ w3^T + b3 + res)`` (1x1 expand CX -> 4 CX with residual) and
     ``y1 = relu(y3 @ w1^T + b1)`` (the next block's 1x1 reduce 4 CX -> CN); returns
@@ -220,8 +220,17 @@ def bottleneck_tail(x2: torch.Tensor, res: torch.Tensor | None, w3: torch.Tensor
     projection shortcut): ``xs [..., 64]`` instead of ``res`` and ``w3 [256, 128]`` =
     [expand | projection] — ``y3 = relu([x2 | xs] @ w3^T + b3)`` (CN = 64).  Weights are 1x1
     OHWI squeezed ([out, in]), biases fp32.  GPU: one persistent kernel, y3 reused from LDS;
-    host: the fp32 reference with y3 rounded to the output dtype before the second GEMM."""
+    host: the fp32 reference with y3 rounded to the output dtype before the second GEMM.
+
+    ``y3_decimated``: ``x2`` is ``[N, H, W, 64]`` and only the even-(h, w) pixels of y3 are
+    stored, compact as ``[N, H/2, W/2, 256]`` — for a y3 whose only other reader is a
+    stride-2 1x1 projection shortcut (ResNet v1.5's stage-1 -> stage-2 boundary)."""
     lead = x2.shape[:-1]
+    dec_hw = (0, 0)
+    if y3_decimated:
+        if x2.dim() != 4 or x2.shape[1] % 2 or x2.shape[2] % 2 or x2.shape[-1] != 64:
+            raise ValueError("bottleneck_tail: decimated y3 needs x2 [N, H, W, 64] with even H, W")
+        dec_hw = (x2.shape[1], x2.shape[2])
     dual = xs is not None
     cx = x2.shape[-1]
     co = 4 * cx
@@ -239,9 +248,10 @@ def bottleneck_tail(x2: torch.Tensor, res: torch.Tensor | None, w3: torch.Tensor
     if b3.numel() != co or b1.numel() != cn:
         raise ValueError("bottleneck_tail: bias sizes must match the output channels")
     odt = x2.dtype if x2.is_cuda else torch.float32
-    y3 = torch.empty((*lead, co), dtype=odt, device=x2.device) if y3 is None else y3
+    lead3 = (lead[0], dec_hw[0] // 2, dec_hw[1] // 2) if y3_decimated else lead
+    y3 = torch.empty((*lead3, co), dtype=odt, device=x2.device) if y3 is None else y3
     y1 = torch.empty((*lead, cn), dtype=odt, device=x2.device) if y1 is None else y1
-    if tuple(y3.shape) != (*lead, co) or tuple(y1.shape) != (*lead, cn):
+    if tuple(y3.shape) != (*lead3, co) or tuple(y1.shape) != (*lead, cn):
         raise ValueError("bottleneck_tail: output buffers do not fit")
     M = x2.numel() // cx
     second = xs if dual else res
@@ -254,20 +264,22 @@ def bottleneck_tail(x2: torch.Tensor, res: torch.Tensor | None, w3: torch.Tensor
         if dev not in _NUM_CU:
             _NUM_CU[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
         if cx == 128:
+            if y3_decimated:
+                raise ValueError("bottleneck_tail: decimated y3 is a CX = 64 variant")
             _hip().bottleneck_tail_wide_bf16(x2.data_ptr(), res.data_ptr(), w3.data_ptr(), b3.data_ptr(),
                                              w1.data_ptr(), b1.data_ptr(), y3.data_ptr(), y1.data_ptr(), M,
                                              _NUM_CU[dev], _stream())
         else:
             _hip().bottleneck_tail_bf16(x2.data_ptr(), _ptr(xs), _ptr(res), w3.data_ptr(), b3.data_ptr(),
                                         w1.data_ptr(), b1.data_ptr(), y3.data_ptr(), y1.data_ptr(), M, cn,
-                                        _NUM_CU[dev], _stream())
+                                        _NUM_CU[dev], _stream(), dec_hw[0], dec_hw[1])
         return y3, y1
     xin = torch.cat([x2.reshape(M, cx), xs.reshape(M, cx)], 1) if dual else x2.reshape(M, cx)
     a = xin.float() @ w3.reshape(co, k3).float().t() + b3.float()
     a = a.to(odt).float()  # the kernel rounds acc + bias first
-    a = torch.relu(a if dual else a + res.reshape(M, co).float())
-    y3.copy_(a.reshape(y3.shape).to(y3.dtype))
-    b = torch.relu(y3.reshape(M, co).float() @ w1.reshape(cn, co).float().t() + b1.float())
+    a = torch.relu(a if dual else a + res.reshape(M, co).float()).to(y3.dtype)
+    y3.copy_(a.reshape(*lead, co)[:, ::2, ::2] if y3_decimated else a.reshape(y3.shape))
+    b = torch.relu(a.float() @ w1.reshape(cn, co).float().t() + b1.float())
     y1.copy_(b.reshape(y1.shape).to(y1.dtype))
     return y3, y1
 

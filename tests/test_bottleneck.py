@@ -73,6 +73,9 @@ def _check(r50, dev, wide="0"):
     n = 5 if wide == "1" else 3
     assert fused.summary()["fused_tails"] == n and plain.summary()["fused_tails"] == 0
     assert fused.summary()["fused_shortcuts"] == plain.summary()["fused_shortcuts"] == 4
+    # stage 1 -> stage 2: the tail's 256-channel output is stored decimated (only the
+    # stride-2 projection reads it besides the fused reduce conv)
+    assert fused.summary()["decimated_tails"] == 1 and plain.summary()["decimated_tails"] == 0
     assert len(fused.steps) == len(plain.steps) - n
     # deep-K 1x1 reduce convs (stages 3/4) run on the ping-pong GEMM on the GPU; the FC head
     # too; no library GEMM anywhere
@@ -95,3 +98,33 @@ def test_compiled_resnet50_fuses_block_boundaries_cpu(r50, wide):
 @pytest.mark.parametrize("wide", ["0", "1"])
 def test_compiled_resnet50_fuses_block_boundaries_gpu(r50, wide):
     _check(r50, torch.device("cuda", 0), wide)
+
+
+def _decimated_case(dev):
+    g = torch.Generator().manual_seed(5)
+    x2, res = torch.randn(2, 6, 10, 64, generator=g), torch.randn(2, 6, 10, 256, generator=g)
+    w3, w1 = torch.randn(256, 64, generator=g) / 8, torch.randn(128, 256, generator=g) / 16
+    b3, b1 = torch.randn(256, generator=g), torch.randn(128, generator=g)
+    x2, res, w3, w1 = (t.bfloat16().float() for t in (x2, res, w3, w1))  # exact in bf16
+    full3, full1 = K.bottleneck_tail(x2, res, w3, b3, w1, b1)
+    cast = (lambda t: t.to(dev, torch.bfloat16)) if dev.type == "cuda" else (lambda t: t)
+    fp = (lambda t: t.to(dev)) if dev.type == "cuda" else (lambda t: t)
+    y3, y1 = K.bottleneck_tail(cast(x2), cast(res), cast(w3), fp(b3), cast(w1), fp(b1), y3_decimated=True)
+    assert tuple(y3.shape) == (2, 3, 5, 256) and tuple(y1.shape) == (2, 6, 10, 128)
+    tol = dict(rtol=3e-2, atol=3e-2 * full3.abs().max().item()) if dev.type == "cuda" else {}
+    torch.testing.assert_close(y3.float().cpu(), full3[:, ::2, ::2], **tol)
+    tol1 = dict(rtol=3e-2, atol=3e-2 * full1.abs().max().item()) if dev.type == "cuda" else {}
+    torch.testing.assert_close(y1.float().cpu(), full1, **tol1)
+
+
+def test_decimated_tail_reference():
+    """y3_decimated stores only the even-(h, w) pixels of y3, compact; y1 is unchanged."""
+    _decimated_case(torch.device("cpu"))
+    with pytest.raises(ValueError):
+        K.bottleneck_tail(torch.zeros(1, 5, 4, 64), torch.zeros(1, 5, 4, 256), torch.zeros(256, 64), torch.zeros(256),
+                          torch.zeros(128, 256), torch.zeros(128), y3_decimated=True)  # odd H
+
+
+@pytest.mark.gpu
+def test_decimated_tail_gpu():
+    _decimated_case(torch.device("cuda", 0))
