@@ -756,6 +756,23 @@ class CompiledFunction(TransformerLowering):
                 and self._fuse_block_tail(xin, out, w_ohwi.reshape(w_ohwi.shape[0], -1), w_dev, b_dev, res_val, None, act,
                                       absorbed, last, node.name):
             return
+        if (res_val is not None and pointwise and act == K.ACT_RELU and xin_shape_override is None
+                and out.qscale is None and out.dtype == torch.bfloat16 and (xin.phys_c or Cin) == Cin
+                and Cin in (128, 256) and Cout % 128 == 0 and res_val.qscale is None and res_val.concat_slot is None
+                and tuple(res_val.shape) == tuple(out.shape) and os.environ.get("FTM_PW_RES", "1") != "0"):
+            # identity-residual expansion conv (ResNet stages 2/3): persistent kernel, resident
+            # weight slice, next tile's x / residual prefetched (kernels/pw_res.hip)
+            w_nk = w_dev.reshape(Cout, Cin)
+            bz = b_dev if b_dev is not None else self._dev(torch.zeros(Cout), torch.float32)
+
+            def run_pw(xin=xin, out=out, res_val=res_val, w_nk=w_nk, bz=bz):
+                K.pw_res(xin.buf, w_nk, bz, res_val.buf, out=_target(out), out_channel_offset=_coff(out))
+
+            self._emit(node.name, "conv", run_pw, [xin, res_val], [out], {"impl": "pw_res"})
+            self.pw_res_layers = getattr(self, "pw_res_layers", 0) + 1
+            self.vals[(last.name, 0)] = out
+            self._alias_fused_outputs(absorbed, out)
+            return
 
         def run(xin=xin, out=out, res_val=res_val, w_dev=w_dev, b_dev=b_dev):
             K.conv2d_nhwc(xin.buf, w_dev, b_dev, res_val.buf if res_val is not None else None, (sh, sw),
@@ -1656,7 +1673,7 @@ class CompiledFunction(TransformerLowering):
                 "fp8_layers": self.fp8_layers, "fused_shortcuts": getattr(self, "fused_shortcuts", 0),
                 "fused_tails": getattr(self, "fused_tails", 0), "decimated_tails": getattr(self, "decimated_tails", 0),
                 "fused_pools": getattr(self, "fused_pools", 0), "conv3x3c64": getattr(self, "conv3x3c64", 0),
-                "conv_pp": getattr(self, "conv_pp_layers", 0),
+                "conv_pp": getattr(self, "conv_pp_layers", 0), "pw_res": getattr(self, "pw_res_layers", 0),
                 "activation_bytes": self.activation_bytes,
                 "param_bytes": self.param_bytes()}
 

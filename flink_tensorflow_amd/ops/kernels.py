@@ -931,6 +931,42 @@ def conv1x1_dual(x: torch.Tensor, x2: torch.Tensor, w_cat: torch.Tensor, bias: t
     return out
 
 
+def pw_res(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor, residual: torch.Tensor,
+           out: torch.Tensor | None = None, out_channel_offset: int = 0) -> torch.Tensor:
+    """``relu(x @ w^T + bias + residual)`` for a 1x1 / stride-1 expansion conv over NHWC ``x``
+    ``[..., K]`` (K = 128 or 256), ``w_nk`` ``[N, K]`` (N % 128 == 0), ``residual`` ``[..., N]``.
+    GPU: the persistent kernel with a resident 128-channel weight slice per workgroup and
+    one-tile-ahead x / residual prefetch (kernels/pw_res.hip); host: the fp32 reference."""
+    K_ = x.shape[-1]
+    N = w_nk.shape[0]
+    lead = tuple(x.shape[:-1])
+    if K_ not in (128, 256) or N % 128 or tuple(w_nk.reshape(N, -1).shape) != (N, K_):
+        raise ValueError(f"pw_res: needs x [..., 128|256] and w [N % 128 == 0, K], got {tuple(x.shape)} "
+                         f"{tuple(w_nk.shape)}")
+    if tuple(residual.shape) != (*lead, N) or bias.numel() != N:
+        raise ValueError("pw_res: residual must be [..., N] and bias [N]")
+    if out is None:
+        out = torch.empty((*lead, N), dtype=x.dtype if x.is_cuda else torch.float32, device=x.device)
+        out_channel_offset = 0
+    if tuple(out.shape[:-1]) != lead or out_channel_offset + N > out.shape[-1]:
+        raise ValueError(f"pw_res: out {tuple(out.shape)} cannot hold [..., {N}] at offset {out_channel_offset}")
+    M = x.numel() // K_
+    if x.is_cuda:
+        for t, n in ((x, "x"), (w_nk, "w"), (residual, "residual"), (out, "out")):
+            _check(t, n, device=x.device)
+        _check(bias, "bias", torch.float32, x.device)
+        dev = x.device.index if x.device.index is not None else torch.cuda.current_device()
+        if dev not in _NUM_CU:
+            _NUM_CU[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+        _hip().pw_res_bf16(x.data_ptr(), w_nk.data_ptr(), bias.data_ptr(), residual.data_ptr(), out.data_ptr(), M, N,
+                           K_, out.shape[-1], out_channel_offset, residual.shape[-1], _NUM_CU[dev], _stream())
+        return out
+    y = x.reshape(M, K_).float() @ w_nk.reshape(N, K_).float().t() + bias.float()
+    y = torch.relu(y.to(out.dtype).float() + residual.reshape(M, N).float())
+    out[..., out_channel_offset:out_channel_offset + N] = y.reshape(*lead, N).to(out.dtype)
+    return out
+
+
 # ------------------------------------------------------------------------------ elementwise
 BIN_OPS = {"add": 0, "sub": 1, "mul": 2, "div": 3, "max": 4, "min": 5, "rsub": 6, "rdiv": 7}
 _BIN_REF = {0: lambda a, b: a + b, 1: lambda a, b: a - b, 2: lambda a, b: a * b, 3: lambda a, b: a / b,
