@@ -29,15 +29,16 @@ def time_us(f, reps=5, rounds=9):
 def main():
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
-    for name, (N, H, W, Cin, Cout) in {"s2_expand": (256, 28, 28, 128, 512),
-                                       "s3_expand": (256, 14, 14, 256, 1024)}.items():
+    for name, (N, H, W, Cin, Cout, tp) in {"s2_expand": (256, 28, 28, 128, 512, 0),
+                                           "s3_expand_tp128": (256, 14, 14, 256, 1024, 128),
+                                           "s3_expand": (256, 14, 14, 256, 1024, 0)}.items():
         x = torch.randn(N, H, W, Cin, device=dev, generator=g).bfloat16()
         w = (torch.randn(Cout, Cin, device=dev, generator=g) / Cin ** 0.5).bfloat16()
         b = torch.randn(Cout, device=dev, generator=g)
         r = torch.randn(N, H, W, Cout, device=dev, generator=g).bfloat16()
         o1, o2 = torch.empty_like(r), torch.empty_like(r)
         f_ig = lambda: K.conv2d_nhwc(x, w.reshape(Cout, 1, 1, Cin), b, r, act="relu", out=o1)  # noqa: E731
-        f_pw = lambda: K.pw_res(x, w, b, r, out=o2)  # noqa: E731
+        f_pw = lambda: K.pw_res(x, w, b, r, out=o2, tp=tp)  # noqa: E731
         f_ig(), f_pw()
         torch.cuda.synchronize()
         err = ((o1.float() - o2.float()).abs().max() / o1.float().abs().max()).item()

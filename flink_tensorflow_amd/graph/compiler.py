@@ -732,9 +732,11 @@ class CompiledFunction(TransformerLowering):
         pointwise = (KHe, KWe, sh, sw, pt, pb, pl, pr, dh, dw) == (1, 1, 1, 1, 0, 0, 0, 0, 1, 1)
         if (self.device.type == "cuda" and pointwise and res_val is None and act in (K.ACT_NONE, K.ACT_RELU)
                 and out.qscale is None and xin_shape_override is None and (xin.phys_c or Cin) == Cin
-                and Cin >= 1024 and Cin % 64 == 0 and Cout % 8 == 0 and _coff(out) % 8 == 0):
-            # deep-K 1x1 reduce convs (ResNet stages 3/4: K = 1024 / 2048) are plain GEMMs over
-            # the pixel matrix: the ping-pong 256x256 MFMA kernel (kernels/gemm_pp.hip)
+                and (Cin >= 1024 or (Cin >= _PP_MIN_K and Cout >= 256)) and Cin % 64 == 0 and Cout % 8 == 0
+                and _coff(out) % 8 == 0):
+            # deep-K 1x1 reduce convs (ResNet stages 3/4: K = 1024 / 2048; the stage-3 entry
+            # reduce K = 512 -> 256) are plain GEMMs over the pixel matrix: the ping-pong
+            # 256x256 MFMA kernel (kernels/gemm_pp.hip)
             w_nk = w_dev.reshape(Cout, Cin)
             bz = b_dev if b_dev is not None else self._dev(torch.zeros(Cout), torch.float32)
             M = int(np.prod(xin.shape[:-1]))
@@ -758,7 +760,7 @@ class CompiledFunction(TransformerLowering):
             return
         if (res_val is not None and pointwise and act == K.ACT_RELU and xin_shape_override is None
                 and out.qscale is None and out.dtype == torch.bfloat16 and (xin.phys_c or Cin) == Cin
-                and Cin in (128, 256) and Cout % 128 == 0 and res_val.qscale is None and res_val.concat_slot is None
+                and K.pw_res_ok(Cin, Cout) and res_val.qscale is None and res_val.concat_slot is None
                 and tuple(res_val.shape) == tuple(out.shape) and os.environ.get("FTM_PW_RES", "1") != "0"):
             # identity-residual expansion conv (ResNet stages 2/3): persistent kernel, resident
             # weight slice, next tile's x / residual prefetched (kernels/pw_res.hip)
@@ -1676,6 +1678,9 @@ class CompiledFunction(TransformerLowering):
                 "conv_pp": getattr(self, "conv_pp_layers", 0), "pw_res": getattr(self, "pw_res_layers", 0),
                 "activation_bytes": self.activation_bytes,
                 "param_bytes": self.param_bytes()}
+
+
+_PP_MIN_K = int(os.environ.get("FTM_PP_MIN_K", "512"))
 
 
 def _buf_shape(r: Val) -> tuple:

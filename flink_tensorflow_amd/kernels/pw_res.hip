@@ -27,14 +27,13 @@
 
 namespace {
 
-constexpr int TP = 128;  // pixels per tile
-constexpr int BN = 128;  // output channels per workgroup (resident weight slice)
 constexpr int NT = 512;  // threads (8 waves)
 
 template <int CPR>
-FTM_DEVICE int swz(int row, int c) { return row * CPR + (c ^ (row & 15)); }
+FTM_DEVICE int swz(int row, int c) { return row * CPR + (c ^ (row & (CPR >= 16 ? 15 : CPR - 1))); }
 
-template <int K>
+// K input channels, TP pixels per tile, BN output channels per workgroup (resident slice)
+template <int K, int TP, int BN>
 __global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ x,
                                                                       const bf16* __restrict__ w,
                                                                       const float* __restrict__ bias,
@@ -45,7 +44,9 @@ __global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ 
   constexpr int XIT = TP * KC / NT;     // x chunks per thread per tile
   constexpr int OC = BN / 8;            // 16-B chunks per output row
   constexpr int RIT = TP * OC / NT;     // output / residual chunks per thread per tile
-  static_assert(XIT * NT == TP * KC && RIT * NT == TP * OC && NT / OC == 32, "tile shape");
+  constexpr int I = BN / 64, J = TP / 32;  // per wave: I x 16 channels, J x 16 pixels
+  static_assert(XIT * NT == TP * KC && RIT * NT == TP * OC && I >= 1 && J >= 1, "tile shape");
+  static_assert((size_t)TP * K >= (size_t)TP * BN, "output tile must fit the x tile region");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   u32x4* Ws = reinterpret_cast<u32x4*>(smem);
   u32x4* Xs = reinterpret_cast<u32x4*>(smem + BN * K * 2);  // x tile, then the output tile
@@ -85,8 +86,8 @@ __global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ 
   auto load_r = [&](int tt) {
 #pragma unroll
     for (int it = 0; it < RIT; ++it) {
-      const int q = tid + it * NT, px = tt * TP + (q >> 4);
-      rv[it] = px < M ? reinterpret_cast<const u32x4*>(res + (size_t)px * ldr + n0)[q & 15] : u32x4{0u, 0u, 0u, 0u};
+      const int q = tid + it * NT, px = tt * TP + q / OC;
+      rv[it] = px < M ? reinterpret_cast<const u32x4*>(res + (size_t)px * ldr + n0)[q % OC] : u32x4{0u, 0u, 0u, 0u};
     }
   };
 
@@ -96,41 +97,41 @@ __global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ 
   int tn = t + ngroups;
   if (tn < tiles) load_x(tn);
   __syncthreads();
-  f32x4 bv[2];
+  f32x4 bv[I];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) bv[i] = *reinterpret_cast<const f32x4*>(bias + n0 + wc * 32 + i * 16 + kg * 4);
+  for (int i = 0; i < I; ++i) bv[i] = *reinterpret_cast<const f32x4*>(bias + n0 + wc * (BN / 4) + i * 16 + kg * 4);
 
   while (true) {
-    // ---- MFMA: acc[i][j] = channels 32 wc + 16 i + 4 kg .. +4 of pixel 64 wp + 16 j + prow
-    f32x4 acc[2][4];
+    // ---- MFMA: acc[i][j] = channels BN/4 wc + 16 i + 4 kg .. +4 of pixel TP/2 wp + 16 j + prow
+    f32x4 acc[I][J];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < I; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < K / 32; ++ks) {
       const int c = ks * 4 + kg;
-      bf16x8 a[2], bb[4];
+      bf16x8 a[I], bb[J];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = __builtin_bit_cast(bf16x8, Ws[swz<KC>(wc * 32 + i * 16 + prow, c)]);
+      for (int i = 0; i < I; ++i) a[i] = __builtin_bit_cast(bf16x8, Ws[swz<KC>(wc * (BN / 4) + i * 16 + prow, c)]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bb[j] = __builtin_bit_cast(bf16x8, Xs[swz<KC>(wp * 64 + j * 16 + prow, c)]);
+      for (int j = 0; j < J; ++j) bb[j] = __builtin_bit_cast(bf16x8, Xs[swz<KC>(wp * (TP / 2) + j * 16 + prow, c)]);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < I; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();  // x tile fully read: its LDS becomes the output tile
     // ---- acc + bias -> bf16 output tile [TP][BN]
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int co = wc * 32 + i * 16 + kg * 4;
+    for (int i = 0; i < I; ++i) {
+      const int co = wc * (BN / 4) + i * 16 + kg * 4;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < J; ++j) {
         bf16x4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[i][j][r] + bv[i][r]);
-        bf16* chunk = reinterpret_cast<bf16*>(Xs + swz<OC>(wp * 64 + j * 16 + prow, co >> 3));
+        bf16* chunk = reinterpret_cast<bf16*>(Xs + swz<OC>(wp * (TP / 2) + j * 16 + prow, co >> 3));
         *reinterpret_cast<bf16x4*>(chunk + (co & 7)) = o;
       }
     }
@@ -139,7 +140,7 @@ __global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ 
     const int p0 = t * TP;
 #pragma unroll
     for (int it = 0; it < RIT; ++it) {
-      const int q = tid + it * NT, pl = q >> 4, c = q & 15;
+      const int q = tid + it * NT, pl = q / OC, c = q % OC;
       bf16x8 v = __builtin_bit_cast(bf16x8, Xs[swz<OC>(pl, c)]);
       const bf16x8 r = __builtin_bit_cast(bf16x8, rv[it]);
 #pragma unroll
@@ -159,27 +160,32 @@ __global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ 
   }
 }
 
-template <int K>
+template <int K, int TP, int BN>
 void launch(const bf16* x, const bf16* w, const float* b, const bf16* r, bf16* y, int M, int N, int ldy, int y_coff,
             int ldr, int num_cu, hipStream_t s) {
+  if (N % BN) throw std::invalid_argument("pw_res: N must be a multiple of " + std::to_string(BN));
   const int S = N / BN;
   constexpr int occ = 1;  // one 8-wave workgroup per CU (2 waves per SIMD: <= 256 VGPRs, no spills)
   const int G = (num_cu * occ) / (8 * S) * (8 * S);
   if (G <= 0) throw std::invalid_argument("pw_res: too few CUs for the channel slices");
   constexpr size_t lds = (size_t)BN * K * 2 + (size_t)TP * K * 2;
   static_assert(lds <= 160 * 1024, "LDS");
-  hipFuncSetAttribute((const void*)pw_res_kernel<K>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL(pw_res_kernel<K>, dim3(G), dim3(NT), lds, s, x, w, b, r, y, M, S, ldy, y_coff, ldr);
+  hipFuncSetAttribute((const void*)pw_res_kernel<K, TP, BN>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL((pw_res_kernel<K, TP, BN>), dim3(G), dim3(NT), lds, s, x, w, b, r, y, M, S, ldy, y_coff, ldr);
 }
 
 }  // namespace
 
 // x [M, K] (rows contiguous), w [N, K], bias [N] fp32, res [M, ldr] -> y [M, ldy] at channel
-// offset y_coff: y = relu(x . w^T + bias + res).  K = 128 or 256, N % 128 == 0.
+// offset y_coff: y = relu(x . w^T + bias + res).  Tiles of 128 output channels; pixels per
+// tile (tp = 0: default): K 128 -> 128, K 256 -> 64 (tp = 128 selectable).  Measured
+// (bench/pw_res_bench.py): K 256 at 64 px 47.4 µs vs 54.0 µs at 128 px (twice the tiles per
+// workgroup: less tail imbalance); a K 512 / 64 x 64 variant lost to the igemm kernel
+// (54 vs 48 µs: 32 channel slices re-read each x tile from L2) and was dropped.
 void pw_res_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int M, int N, int K, int ldy,
-                 int y_coff, int ldr, int num_cu, uintptr_t stream) {
+                 int y_coff, int ldr, int num_cu, uintptr_t stream, int tp) {
   if (K != 128 && K != 256) throw std::invalid_argument("pw_res: K must be 128 or 256");
-  if (M <= 0 || N <= 0 || N % BN) throw std::invalid_argument("pw_res: N must be a positive multiple of 128");
+  if (M <= 0 || N <= 0) throw std::invalid_argument("pw_res: empty problem");
   if (ldy % 8 || y_coff % 8 || ldr % 8 || ldr < N || ldy < y_coff + N)
     throw std::invalid_argument("pw_res: output / residual strides");
   if ((long)M * (ldy > ldr ? ldy : ldr) >= (1L << 31) || (long)M * K >= (1L << 31))
@@ -187,11 +193,14 @@ void pw_res_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintpt
   for (uintptr_t p : {x, w, bias, res, y})
     if (!p || p % 16) throw std::invalid_argument("pw_res: null or non-16-byte-aligned pointer");
   auto bp = [](uintptr_t p) { return reinterpret_cast<bf16*>(p); };
+  auto fb = reinterpret_cast<const float*>(bias);
   auto s = reinterpret_cast<hipStream_t>(stream);
   if (K == 128)
-    launch<128>(bp(x), bp(w), reinterpret_cast<const float*>(bias), bp(res), bp(y), M, N, ldy, y_coff, ldr, num_cu, s);
+    launch<128, 128, 128>(bp(x), bp(w), fb, bp(res), bp(y), M, N, ldy, y_coff, ldr, num_cu, s);
+  else if (tp == 128)
+    launch<256, 128, 128>(bp(x), bp(w), fb, bp(res), bp(y), M, N, ldy, y_coff, ldr, num_cu, s);
   else
-    launch<256>(bp(x), bp(w), reinterpret_cast<const float*>(bias), bp(res), bp(y), M, N, ldy, y_coff, ldr, num_cu, s);
+    launch<256, 64, 128>(bp(x), bp(w), fb, bp(res), bp(y), M, N, ldy, y_coff, ldr, num_cu, s);
   FTM_CHECK_LAUNCH();
 }
 

@@ -931,18 +931,24 @@ def conv1x1_dual(x: torch.Tensor, x2: torch.Tensor, w_cat: torch.Tensor, bias: t
     return out
 
 
+def pw_res_ok(K_: int, N: int, num_cu: int = 256) -> bool:
+    """Shapes ``pw_res`` takes: K = 128 / 256, N in 128-channel slices, every slice group
+    of the 8 XCDs resident at once."""
+    return K_ in (128, 256) and N % 128 == 0 and 8 * (N // 128) <= num_cu
+
+
 def pw_res(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor, residual: torch.Tensor,
-           out: torch.Tensor | None = None, out_channel_offset: int = 0) -> torch.Tensor:
+           out: torch.Tensor | None = None, out_channel_offset: int = 0, tp: int = 0) -> torch.Tensor:
     """``relu(x @ w^T + bias + residual)`` for a 1x1 / stride-1 expansion conv over NHWC ``x``
-    ``[..., K]`` (K = 128 or 256), ``w_nk`` ``[N, K]`` (N % 128 == 0), ``residual`` ``[..., N]``.
+    ``[..., K]`` (``pw_res_ok``: K = 128 / 256, N % 128 == 0), ``w_nk`` ``[N, K]``, ``residual``
+    ``[..., N]``; ``tp`` = pixels per tile for K 256 (0: the measured default, 64).
     GPU: the persistent kernel with a resident 128-channel weight slice per workgroup and
     one-tile-ahead x / residual prefetch (kernels/pw_res.hip); host: the fp32 reference."""
     K_ = x.shape[-1]
     N = w_nk.shape[0]
     lead = tuple(x.shape[:-1])
-    if K_ not in (128, 256) or N % 128 or tuple(w_nk.reshape(N, -1).shape) != (N, K_):
-        raise ValueError(f"pw_res: needs x [..., 128|256] and w [N % 128 == 0, K], got {tuple(x.shape)} "
-                         f"{tuple(w_nk.shape)}")
+    if not pw_res_ok(K_, N) or tuple(w_nk.reshape(N, -1).shape) != (N, K_):
+        raise ValueError(f"pw_res: unsupported shapes x {tuple(x.shape)}, w {tuple(w_nk.shape)}")
     if tuple(residual.shape) != (*lead, N) or bias.numel() != N:
         raise ValueError("pw_res: residual must be [..., N] and bias [N]")
     if out is None:
@@ -959,7 +965,7 @@ def pw_res(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor, residual: to
         if dev not in _NUM_CU:
             _NUM_CU[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
         _hip().pw_res_bf16(x.data_ptr(), w_nk.data_ptr(), bias.data_ptr(), residual.data_ptr(), out.data_ptr(), M, N,
-                           K_, out.shape[-1], out_channel_offset, residual.shape[-1], _NUM_CU[dev], _stream())
+                           K_, out.shape[-1], out_channel_offset, residual.shape[-1], _NUM_CU[dev], _stream(), tp)
         return out
     y = x.reshape(M, K_).float() @ w_nk.reshape(N, K_).float().t() + bias.float()
     y = torch.relu(y.to(out.dtype).float() + residual.reshape(M, N).float())

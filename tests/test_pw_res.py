@@ -29,12 +29,13 @@ def test_pw_res_host_reference():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M,K_,N", [(25088, 128, 512), (12544 + 77, 256, 1024), (300, 128, 128), (1000, 256, 384)])
-def test_pw_res_gpu(M, K_, N):
+@pytest.mark.parametrize("M,K_,N,tp", [(25088, 128, 512, 0), (12544 + 77, 256, 1024, 0), (300, 128, 128, 0),
+                                       (1000, 256, 384, 128), (5000 + 3, 256, 512, 128), (12544, 256, 1024, 128)])
+def test_pw_res_gpu(M, K_, N, tp):
     g = torch.Generator().manual_seed(M + N)
     x, w, b, r = _case(M, K_, N, g)
     dev = torch.device("cuda", 0)
-    got = K.pw_res(x.to(dev), w.to(dev), b.to(dev), r.to(dev)).float().cpu()
+    got = K.pw_res(x.to(dev), w.to(dev), b.to(dev), r.to(dev), tp=tp).float().cpu()
     ref = _ref(x, w, b, r)
     torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
 
