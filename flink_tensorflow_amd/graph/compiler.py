@@ -838,8 +838,17 @@ class CompiledFunction(TransformerLowering):
             return True
 
         s2cfg = {"s2": s2}  # _decimate_tails: x2 stored already decimated -> stride 1
+        # stride 1 over a same-size x2 (the decimated stage-1 -> 2 hand-over): opt-in
+        # (FTM_PW_DUAL=1) persistent prefetching kernel (kernels/pw_res.hip, dual form) — 10 %
+        # faster alone (124 vs 139 µs) but 0.2-0.4 % slower end to end next to the sibling
+        # lane (profiles/r02_pw_res2)
+        use_pw = (act == K.ACT_RELU and K.pw_dual_ok(K1, C2, Cout) and (xin.phys_c or K1) == K1
+                  and (x2.phys_c or C2) == C2 and os.environ.get("FTM_PW_DUAL", "0") == "1")
 
-        def run(xin=xin, x2=x2, out=out, w_dev=w_dev, b_dev=b_dev, s2cfg=s2cfg):
+        def run(xin=xin, x2=x2, out=out, w_dev=w_dev, b_dev=b_dev, s2cfg=s2cfg, use_pw=use_pw):
+            if use_pw and s2cfg["s2"] == 1 and tuple(x2.buf.shape[:3]) == tuple(xin.buf.shape[:3]):
+                K.pw_dual(xin.buf, x2.buf, w_dev, b_dev, out=_target(out), out_channel_offset=_coff(out))
+                return
             K.conv1x1_dual(xin.buf, x2.buf, w_dev, b_dev, s2cfg["s2"], act, out=_target(out),
                            out_channel_offset=_coff(out))
 

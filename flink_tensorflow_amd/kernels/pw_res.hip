@@ -32,15 +32,18 @@ constexpr int NT = 512;  // threads (8 waves)
 template <int CPR>
 FTM_DEVICE int swz(int row, int c) { return row * CPR + (c ^ (row & (CPR >= 16 ? 15 : CPR - 1))); }
 
-// K input channels, TP pixels per tile, BN output channels per workgroup (resident slice)
-template <int K, int TP, int BN>
-__global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ x,
-                                                                      const bf16* __restrict__ w,
-                                                                      const float* __restrict__ bias,
-                                                                      const bf16* __restrict__ res,
-                                                                      bf16* __restrict__ y, int M, int S, int ldy,
-                                                                      int y_coff, int ldr) {
+// K = K1 + K2 input channels (K2 > 0: DUAL, a second [M, K2] source x2 — a 1x1 conv with its
+// stride-1 projection shortcut, no residual), TP pixels per tile, BN output channels per
+// workgroup (resident slice)
+template <int K1, int K2, int TP, int BN>
+__global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ x, const bf16* __restrict__ x2,
+                                                       const bf16* __restrict__ w, const float* __restrict__ bias,
+                                                       const bf16* __restrict__ res, bf16* __restrict__ y, int M,
+                                                       int S, int ldy, int y_coff, int ldr) {
+  constexpr int K = K1 + K2;
+  constexpr bool DUAL = K2 > 0;
   constexpr int KC = K / 8;             // 16-B chunks per x / W row
+  constexpr int KC1 = K1 / 8;
   constexpr int XIT = TP * KC / NT;     // x chunks per thread per tile
   constexpr int OC = BN / 8;            // 16-B chunks per output row
   constexpr int RIT = TP * OC / NT;     // output / residual chunks per thread per tile
@@ -72,8 +75,10 @@ __global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ 
   auto load_x = [&](int tt) {
 #pragma unroll
     for (int it = 0; it < XIT; ++it) {
-      const int q = tid + it * NT, px = tt * TP + q / KC;
-      xr[it] = px < M ? reinterpret_cast<const u32x4*>(x + (size_t)px * K)[q % KC] : u32x4{0u, 0u, 0u, 0u};
+      const int q = tid + it * NT, px = tt * TP + q / KC, c = q % KC;
+      const u32x4* src = (!DUAL || c < KC1) ? reinterpret_cast<const u32x4*>(x + (size_t)px * K1) + c
+                                            : reinterpret_cast<const u32x4*>(x2 + (size_t)px * K2) + (c - KC1);
+      xr[it] = px < M ? *src : u32x4{0u, 0u, 0u, 0u};
     }
   };
   auto store_x = [&]() {
@@ -84,6 +89,7 @@ __global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ 
     }
   };
   auto load_r = [&](int tt) {
+    if constexpr (DUAL) return;  // no residual
 #pragma unroll
     for (int it = 0; it < RIT; ++it) {
       const int q = tid + it * NT, px = tt * TP + q / OC;
@@ -142,9 +148,14 @@ __global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ 
     for (int it = 0; it < RIT; ++it) {
       const int q = tid + it * NT, pl = q / OC, c = q % OC;
       bf16x8 v = __builtin_bit_cast(bf16x8, Xs[swz<OC>(pl, c)]);
-      const bf16x8 r = __builtin_bit_cast(bf16x8, rv[it]);
+      if constexpr (DUAL) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = f2bf(fmaxf((float)v[e] + (float)r[e], 0.f));
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(fmaxf((float)v[e], 0.f));
+      } else {
+        const bf16x8 r = __builtin_bit_cast(bf16x8, rv[it]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(fmaxf((float)v[e] + (float)r[e], 0.f));
+      }
       if (p0 + pl < M)
         *reinterpret_cast<u32x4*>(y + (size_t)(p0 + pl) * ldy + y_coff + n0 + c * 8) = __builtin_bit_cast(u32x4, v);
     }
@@ -160,9 +171,10 @@ __global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ 
   }
 }
 
-template <int K, int TP, int BN>
-void launch(const bf16* x, const bf16* w, const float* b, const bf16* r, bf16* y, int M, int N, int ldy, int y_coff,
-            int ldr, int num_cu, hipStream_t s) {
+template <int K1, int K2, int TP, int BN>
+void launch(const bf16* x, const bf16* x2, const bf16* w, const float* b, const bf16* r, bf16* y, int M, int N,
+            int ldy, int y_coff, int ldr, int num_cu, hipStream_t s) {
+  constexpr int K = K1 + K2;
   if (N % BN) throw std::invalid_argument("pw_res: N must be a multiple of " + std::to_string(BN));
   const int S = N / BN;
   constexpr int occ = 1;  // one 8-wave workgroup per CU (2 waves per SIMD: <= 256 VGPRs, no spills)
@@ -170,8 +182,10 @@ void launch(const bf16* x, const bf16* w, const float* b, const bf16* r, bf16* y
   if (G <= 0) throw std::invalid_argument("pw_res: too few CUs for the channel slices");
   constexpr size_t lds = (size_t)BN * K * 2 + (size_t)TP * K * 2;
   static_assert(lds <= 160 * 1024, "LDS");
-  hipFuncSetAttribute((const void*)pw_res_kernel<K, TP, BN>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL((pw_res_kernel<K, TP, BN>), dim3(G), dim3(NT), lds, s, x, w, b, r, y, M, S, ldy, y_coff, ldr);
+  (void)hipFuncSetAttribute((const void*)pw_res_kernel<K1, K2, TP, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            lds);
+  hipLaunchKernelGGL((pw_res_kernel<K1, K2, TP, BN>), dim3(G), dim3(NT), lds, s, x, x2, w, b, r, y, M, S, ldy, y_coff,
+                     ldr);
 }
 
 }  // namespace
@@ -196,12 +210,33 @@ void pw_res_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintpt
   auto fb = reinterpret_cast<const float*>(bias);
   auto s = reinterpret_cast<hipStream_t>(stream);
   if (K == 128)
-    launch<128, 128, 128>(bp(x), bp(w), fb, bp(res), bp(y), M, N, ldy, y_coff, ldr, num_cu, s);
+    launch<128, 0, 128, 128>(bp(x), nullptr, bp(w), fb, bp(res), bp(y), M, N, ldy, y_coff, ldr, num_cu, s);
   else if (tp == 128)
-    launch<256, 128, 128>(bp(x), bp(w), fb, bp(res), bp(y), M, N, ldy, y_coff, ldr, num_cu, s);
+    launch<256, 0, 128, 128>(bp(x), nullptr, bp(w), fb, bp(res), bp(y), M, N, ldy, y_coff, ldr, num_cu, s);
   else
-    launch<256, 64, 128>(bp(x), bp(w), fb, bp(res), bp(y), M, N, ldy, y_coff, ldr, num_cu, s);
+    launch<256, 0, 64, 128>(bp(x), nullptr, bp(w), fb, bp(res), bp(y), M, N, ldy, y_coff, ldr, num_cu, s);
   FTM_CHECK_LAUNCH();
 }
 
-void register_pw_res(pybind11::module_& m) { m.def("pw_res_bf16", &pw_res_bf16); }
+// y = relu([x | x2] . w^T + bias): x [M, 128], x2 [M, 256] (rows contiguous), w [N, 384] —
+// ResNet's stage-2 entry expand conv with its projection shortcut, whose input the stage-1
+// tail stored already decimated (compiler._decimate_tails), so both sources are plain
+// pixel matrices.  N % 128 == 0.
+void pw_dual_bf16(uintptr_t x, uintptr_t x2, uintptr_t w, uintptr_t bias, uintptr_t y, int M, int N, int K1, int K2,
+                  int ldy, int y_coff, int num_cu, uintptr_t stream) {
+  if (K1 != 128 || K2 != 256) throw std::invalid_argument("pw_dual: sources must have 128 and 256 channels");
+  if (M <= 0 || N <= 0) throw std::invalid_argument("pw_dual: empty problem");
+  if (ldy % 8 || y_coff % 8 || ldy < y_coff + N) throw std::invalid_argument("pw_dual: output stride");
+  if ((long)M * (ldy > K2 ? ldy : K2) >= (1L << 31)) throw std::invalid_argument("pw_dual: tensor too large");
+  for (uintptr_t p : {x, x2, w, bias, y})
+    if (!p || p % 16) throw std::invalid_argument("pw_dual: null or non-16-byte-aligned pointer");
+  auto bp = [](uintptr_t p) { return reinterpret_cast<bf16*>(p); };
+  launch<128, 256, 64, 128>(bp(x), bp(x2), bp(w), reinterpret_cast<const float*>(bias), nullptr, bp(y), M, N, ldy,
+                            y_coff, N, num_cu, reinterpret_cast<hipStream_t>(stream));
+  FTM_CHECK_LAUNCH();
+}
+
+void register_pw_res(pybind11::module_& m) {
+  m.def("pw_res_bf16", &pw_res_bf16);
+  m.def("pw_dual_bf16", &pw_dual_bf16);
+}

@@ -973,6 +973,41 @@ def pw_res(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor, residual: to
     return out
 
 
+def pw_dual_ok(K1: int, C2: int, N: int, num_cu: int = 256) -> bool:
+    """Shapes ``pw_dual`` takes (ResNet's stage-2 entry expand + projection)."""
+    return K1 == 128 and C2 == 256 and N % 128 == 0 and 8 * (N // 128) <= num_cu
+
+
+def pw_dual(x: torch.Tensor, x2: torch.Tensor, w_cat: torch.Tensor, bias: torch.Tensor,
+            out: torch.Tensor | None = None, out_channel_offset: int = 0) -> torch.Tensor:
+    """``relu([x | x2] @ w_cat^T + bias)`` with ``x`` ``[..., 128]`` and ``x2`` ``[..., 256]`` on
+    the same pixels (a 1x1 expand conv with its stride-1 — or already decimated — projection
+    shortcut, no residual).  GPU: the persistent ``pw_res`` kernel in its dual-source form
+    (kernels/pw_res.hip); host: ``conv1x1_dual``."""
+    K1, C2 = x.shape[-1], x2.shape[-1]
+    N = w_cat.shape[0]
+    lead = tuple(x.shape[:-1])
+    if not pw_dual_ok(K1, C2, N) or tuple(x2.shape[:-1]) != lead or tuple(w_cat.shape) != (N, K1 + C2):
+        raise ValueError(f"pw_dual: unsupported shapes x {tuple(x.shape)}, x2 {tuple(x2.shape)}, "
+                         f"w {tuple(w_cat.shape)}")
+    if not x.is_cuda:
+        return conv1x1_dual(x, x2, w_cat, bias, 1, "relu", out=out, out_channel_offset=out_channel_offset)
+    if out is None:
+        out = torch.empty((*lead, N), dtype=x.dtype, device=x.device)
+        out_channel_offset = 0
+    if tuple(out.shape[:-1]) != lead or out_channel_offset + N > out.shape[-1]:
+        raise ValueError(f"pw_dual: out {tuple(out.shape)} cannot hold [..., {N}] at offset {out_channel_offset}")
+    for t, n in ((x, "x"), (x2, "x2"), (w_cat, "w"), (out, "out")):
+        _check(t, n, device=x.device)
+    _check(bias, "bias", torch.float32, x.device)
+    dev = x.device.index if x.device.index is not None else torch.cuda.current_device()
+    if dev not in _NUM_CU:
+        _NUM_CU[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+    _hip().pw_dual_bf16(x.data_ptr(), x2.data_ptr(), w_cat.data_ptr(), bias.data_ptr(), out.data_ptr(),
+                        x.numel() // K1, N, K1, C2, out.shape[-1], out_channel_offset, _NUM_CU[dev], _stream())
+    return out
+
+
 # ------------------------------------------------------------------------------ elementwise
 BIN_OPS = {"add": 0, "sub": 1, "mul": 2, "div": 3, "max": 4, "min": 5, "rsub": 6, "rdiv": 7}
 _BIN_REF = {0: lambda a, b: a + b, 1: lambda a, b: a - b, 2: lambda a, b: a * b, 3: lambda a, b: a / b,
