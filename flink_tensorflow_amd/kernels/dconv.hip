@@ -14,7 +14,10 @@
 //   3. stages the [256 px][BN] result through LDS and stores 16-B row segments (bf16 or
 //      e4m3 with the successor's scale), channel-offset capable (concat slices).
 // Output tile: 16 x 16 pixels of one image (wave w owns tile rows 4w..4w+3 = 4 fragments),
-// BN = 32 or 64 channels.  Weights are pre-arranged by the host: row pitch WP bytes =
+// BN = 32 or 64 channels.  Pooled (stem) tiles are 17 conv columns wide: 4 waves cover 7 x 8
+// pooled pixels, 8 waves (pool_rows = 14) 14 x 8 — the filter bank DMA (34 KB for the
+// ResNet s2d stem, an L2 hit but the largest per-workgroup transfer) is then paid once per
+// 112 pooled pixels instead of 56: 181 -> 161 us for the B=256 stem (bench/stem_ab.py).  Weights are pre-arranged by the host: row pitch WP bytes =
 // round_up(KH*KW*Cin*ES, 4*KL) + 16 (the +16 keeps the 16 rows of a fragment read on
 // different banks).
 #include <pybind11/pybind11.h>
@@ -90,8 +93,11 @@ FTM_DEVICE u16x8 pool3x3_max(const uint8_t* base, int row_bytes, int px_bytes) {
   return m;
 }
 
-template <int ES, int BN, int ACT, bool OUT_FP8, bool POOL = false>
-__global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
+template <int ES, int BN, int ACT, bool OUT_FP8, bool POOL = false, int WAVES = 4>
+__global__ __launch_bounds__(WAVES * 64) void dconv_kernel(DconvParams p) {
+  static_assert(WAVES == 4 || (POOL && WAVES == 8), "8-wave tiles are pooled-only");
+  constexpr int NTH = WAVES * 64;
+  constexpr int PTH = WAVES == 8 ? 14 : 7;  // pooled rows per tile
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int KL = ES == 2 ? 16 : 32;  // K bytes per lane per MFMA
   constexpr int I = BN / 16;             // channel fragments
@@ -107,7 +113,7 @@ __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
   const int th = b % p.tiles_h;
   const int n = b / p.tiles_h;
   constexpr int TPW = POOL ? 17 : TW;  // conv tile width (pixel p of the tile = row p / TPW, col p % TPW)
-  const int oy0 = POOL ? th * 14 - p.ppt : th * TH, ox0 = POOL ? tw * 16 - p.ppl : tw * TW, n0 = tn * BN;
+  const int oy0 = POOL ? th * (2 * PTH) - p.ppt : th * TH, ox0 = POOL ? tw * 16 - p.ppl : tw * TW, n0 = tn * BN;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int patch_bytes = p.PH * p.PW * p.RB;
@@ -120,7 +126,7 @@ __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
     const int nchunks = p.PH * p.PW * cpr;
     const int iy0 = oy0 * p.S - p.ph, ix0 = ox0 * p.S - p.pw;
     const uint8_t* xb = p.x + (size_t)n * p.H * p.W * p.RB;
-    for (int q0 = wave * 64; q0 < nchunks; q0 += NT) {
+    for (int q0 = wave * 64; q0 < nchunks; q0 += NTH) {
       const int q = q0 + lane;
       const int r = q / cpr, c = q - r * cpr;
       const int py = r / p.PW, px = r - py * p.PW;
@@ -131,7 +137,7 @@ __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
     }
     const int wchunks = BN * (p.WP >> 4);
     const uint8_t* wb = p.w + (size_t)n0 * p.WP;
-    for (int q0 = wave * 64; q0 < wchunks; q0 += NT) {
+    for (int q0 = wave * 64; q0 < wchunks; q0 += NTH) {
       const int q = q0 + lane;
       const void* src = q < wchunks ? (const void*)(wb + (size_t)q * 16) : (const void*)g_zero16;
       glds16(src, Wsm + q0 * 16);
@@ -226,7 +232,7 @@ __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
   constexpr int CPR = BN / EPO;
   if constexpr (POOL) {
     static_assert(!OUT_FP8, "pooled epilogue is bf16");
-    for (int q = tid; q < 56 * CPR; q += NT) {
+    for (int q = tid; q < PTH * 8 * CPR; q += NTH) {
       const int pp = q / CPR, cc = q % CPR;
       const int pyl = pp >> 3, pxl = pp & 7;
       const int py = (oy0 + p.ppt) / 2 + pyl, px = (ox0 + p.ppl) / 2 + pxl;
@@ -250,18 +256,22 @@ __global__ __launch_bounds__(NT) void dconv_kernel(DconvParams p) {
 }
 
 template <int ES, int BN, bool OUT_FP8>
-void launch_act(const DconvParams& p, int act, size_t lds, hipStream_t s) {
+void launch_act(const DconvParams& p, int act, size_t lds, hipStream_t s, int pool_rows) {
   dim3 grid(p.N * p.tiles_h * p.tiles_w * p.tiles_n), block(NT);
   if constexpr (ES == 2 && !OUT_FP8) {
     if (p.Hp > 0) {  // fused max pool (ReLU stems)
       if (act != ACT_RELU) throw std::invalid_argument("dconv: fused pool needs a ReLU conv");
       static bool done = false;
       if (!done) {
-        hipFuncSetAttribute((const void*)dconv_kernel<ES, BN, ACT_RELU, false, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        for (auto f : {(const void*)dconv_kernel<ES, BN, ACT_RELU, false, true>,
+                       (const void*)dconv_kernel<ES, BN, ACT_RELU, false, true, 8>})
+          hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         done = true;
       }
-      hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_RELU, false, true>), grid, block, lds, s, p);
+      if (pool_rows == 14)  // 8 waves, 14 x 8 pooled pixels: the filter bank is fetched once per 112 outputs
+        hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_RELU, false, true, 8>), grid, dim3(512), lds, s, p);
+      else
+        hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_RELU, false, true>), grid, block, lds, s, p);
       return;
     }
   } else {
@@ -289,12 +299,16 @@ void set_lds_limit() {
 
 }  // namespace
 
-int lds_bytes(int es, int bn, int KH, int KW, int S, int Cin, int wp, bool pool) {
-  const int PH = (TH - 1) * S + KH, PW = (pool ? TW : TW - 1) * S + KW;
+// patch rows of a tile: pooled tiles are 17 conv columns wide and hold npx = 64 * waves
+// fragment pixels (the last fragment row is (npx - 1) / 17)
+int patch_rows(int KH, int S, bool pool, int npx) { return (pool ? (npx - 1) / 17 : TH - 1) * S + KH; }
+
+int lds_bytes(int es, int bn, int KH, int KW, int S, int Cin, int wp, bool pool, int npx = TH * TW) {
+  const int PH = patch_rows(KH, S, pool, npx), PW = (pool ? TW : TW - 1) * S + KW;
   const int patch = PH * PW * Cin * es;
   const int ob = 2;  // bound by the bf16 output tile
   int need = ((patch + 1023) & ~1023) + bn * wp + 1024;  // + slack for a short last DMA
-  const int epi = TH * TW * (bn * ob + 16);
+  const int epi = npx * (bn * ob + 16);
   return need > epi ? need : epi;
 }
 
@@ -305,7 +319,8 @@ int dconv_lds_bytes(int es, int bn, int KH, int KW, int S, int Cin, int wp) {
 // x: NHWC (bf16 es=2 / e4m3 es=1); w: host-arranged [Cout_pad][wp] bytes.
 void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t y, int es, int N, int H, int W,
            int Cin, int Cout, int KH, int KW, int S, int ph, int pw, int Ho, int Wo, int wp, int ldy, int y_coff,
-           int out_fp8, float out_q, int act, int bn, uintptr_t stream, int Hp, int Wp, int ppt, int ppl) {
+           int out_fp8, float out_q, int act, int bn, uintptr_t stream, int Hp, int Wp, int ppt, int ppl,
+           int pool_rows) {
   const int KL = es == 2 ? 16 : 32;
   if (es != 1 && es != 2) throw std::invalid_argument("dconv: es must be 1 or 2");
   if ((Cin * es) % KL) throw std::invalid_argument("dconv: Cin*es must be a multiple of " + std::to_string(KL));
@@ -318,7 +333,10 @@ void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t 
   if (S != 1 && S != 2) throw std::invalid_argument("dconv: stride must be 1 or 2");
   if (!bias || (es == 1 && !scale)) throw std::invalid_argument("dconv: bias (and fp8 scale) required");
   if (x % 16 || w % 16 || y % 16 || bias % 16 || (scale && scale % 16)) throw std::invalid_argument("dconv: alignment");
-  const int lds = lds_bytes(es, bn, KH, KW, S, Cin, wp, Hp > 0);
+  if (Hp > 0 && pool_rows != 7 && pool_rows != 14) throw std::invalid_argument("dconv: pool_rows must be 7 or 14");
+  if (Hp <= 0) pool_rows = 7;
+  const int npx = pool_rows == 14 ? 512 : TH * TW;
+  const int lds = lds_bytes(es, bn, KH, KW, S, Cin, wp, Hp > 0, npx);
   if (lds > 160 * 1024) throw std::invalid_argument("dconv: tile does not fit LDS (" + std::to_string(lds) + " B)");
   DconvParams p{};
   p.x = reinterpret_cast<const uint8_t*>(x);
@@ -333,7 +351,7 @@ void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t 
   p.WP = wp;
   p.ksteps = kpad / (4 * KL);
   if (p.ksteps > 64) throw std::invalid_argument("dconv: more than 64 K-steps");
-  p.PH = (TH - 1) * S + KH;
+  p.PH = patch_rows(KH, S, Hp > 0, npx);
   p.PW = (Hp > 0 ? TW : TW - 1) * S + KW;  // pooled tiles are 17 conv columns wide
   p.ldy = ldy; p.y_coff = y_coff;
   p.Hp = Hp; p.Wp = Wp; p.ppt = ppt; p.ppl = ppl;
@@ -346,11 +364,11 @@ void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t 
       const int dy = tap / KW, dx = tap - dy * KW;
       p.koff[st * 4 + fq] = (dy * p.PW + dx) * p.RB + cb;
     }
-  if (Hp > 0) {  // pooled tiles of 7 x 8 (15 x 17 conv pixels)
+  if (Hp > 0) {  // pooled tiles of 7 x 8 (15 x 17 conv pixels) or 14 x 8 (29 x 17)
     if (ppt < 0 || ppt > 1 || ppl < 0 || ppl > 1) throw std::invalid_argument("dconv: pool padding must be 0/1");
     if ((Hp - 1) * 2 + 3 > Ho + ppt + 1 || (Wp - 1) * 2 + 3 > Wo + ppl + 1)
       throw std::invalid_argument("dconv: pooled shape inconsistent with conv output");
-    p.tiles_h = (Hp + 6) / 7;
+    p.tiles_h = (Hp + pool_rows - 1) / pool_rows;
     p.tiles_w = (Wp + 7) / 8;
   } else {
     p.tiles_h = (Ho + TH - 1) / TH;
@@ -361,7 +379,7 @@ void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t 
 #define FTM_DCONV(ES_, BN_, OF_)            \
   do {                                      \
     set_lds_limit<ES_, BN_, OF_>();         \
-    launch_act<ES_, BN_, OF_>(p, act, lds, s); \
+    launch_act<ES_, BN_, OF_>(p, act, lds, s, pool_rows); \
   } while (0)
   if (es == 2) {
     if (bn == 32) { if (out_fp8) FTM_DCONV(2, 32, true); else FTM_DCONV(2, 32, false); }

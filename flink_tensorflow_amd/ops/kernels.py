@@ -14,6 +14,8 @@ stream, so the ops are hipGraph-capturable.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -868,12 +870,14 @@ def dconv_bf16_weight_bytes(w_ohwi: torch.Tensor, bn: int) -> torch.Tensor:
 def conv2d_direct(x: torch.Tensor, w_arr: torch.Tensor, kshape, Cout: int, bias: torch.Tensor, stride=(1, 1),
                   pad=(0, 0, 0, 0), act=None, out: torch.Tensor | None = None, out_channel_offset: int = 0,
                   bn: int = 64, chan_scale: torch.Tensor | None = None, out_scale: float | None = None,
-                  maxpool_pad: tuple | None = None) -> torch.Tensor:
+                  maxpool_pad: tuple | None = None, pool_rows: int | None = None) -> torch.Tensor:
     """Direct conv on device: ``x`` NHWC bf16 (``chan_scale`` None) or e4m3 bytes (uint8, with
     the per-channel dequant scale ``chan_scale``); ``w_arr`` from :func:`dconv_weights`;
     ``out_scale`` → e4m3 output.  ``maxpool_pad = (top, bottom, left, right)`` fuses a 3x3 /
-    stride-2 max pool of the ReLU output (ResNet stem → pool1).  Device-only (the host
-    paths use the reference convs)."""
+    stride-2 max pool of the ReLU output (ResNet stem → pool1); ``pool_rows`` (7 or 14,
+    default ``FTM_STEM_POOL_ROWS`` or 14) is the pooled tile height — 14 runs 8-wave
+    workgroups that fetch the filter bank once per 14 x 8 pooled pixels.  Device-only (the
+    host paths use the reference convs)."""
     N, H, W, Cin = x.shape
     KH, KW = kshape
     s = stride[0]
@@ -899,7 +903,8 @@ def conv2d_direct(x: torch.Tensor, w_arr: torch.Tensor, kshape, Cout: int, bias:
     _check(bias, "bias", torch.float32, x.device)
     _hip().dconv(x.data_ptr(), w_arr.data_ptr(), _ptr(chan_scale), bias.data_ptr(), out.data_ptr(), es, N, H, W, Cin,
                  Cout, KH, KW, s, pt, pl, Ho, Wo, w_arr.shape[1], out.shape[3], out_channel_offset, int(out_fp8),
-                 1.0 / out_scale if out_fp8 else 1.0, act_code(act), bn, _stream(), Hp, Wp, ppt, ppl)
+                 1.0 / out_scale if out_fp8 else 1.0, act_code(act), bn, _stream(), Hp, Wp, ppt, ppl,
+                 int(pool_rows or os.environ.get("FTM_STEM_POOL_ROWS", "14")))
     return out
 
 

@@ -95,10 +95,12 @@ POOL_CASES = [  # N, H, W, Cin, Cout, (kh, kw), stride, pad, pool padding (TF "S
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pool_rows", [7, 14])
 @pytest.mark.parametrize("case", POOL_CASES)
-def test_dconv_maxpool_gpu(case):
+def test_dconv_maxpool_gpu(case, pool_rows):
     """Stem conv + ReLU + fused 3x3/s2 max pool == conv then pool (the same bf16 values
-    are compared inside the max, so the results are exact up to conv rounding)."""
+    are compared inside the max, so the results are exact up to conv rounding); both pooled
+    tile heights (7 rows / 4 waves, 14 rows / 8 waves)."""
     N, H, W, Cin, Cout, (kh, kw), s, pad, ppad, bn = case
     torch.manual_seed(H * W + Cin)
     x = torch.randn(N, H, W, Cin).to(torch.bfloat16)
@@ -115,6 +117,6 @@ def test_dconv_maxpool_gpu(case):
     ref = K.pool2d_nhwc(conv, (3, 3), (2, 2), mp, "max")
     arr = K.dconv_bf16_weight_bytes(w.float(), bn).to(DEV)
     got = K.conv2d_direct(x.to(DEV), arr, (kh, kw), Cout, b.to(DEV), (s, s), pad, "relu", bn=bn,
-                          maxpool_pad=mp).cpu()
+                          maxpool_pad=mp, pool_rows=pool_rows).cpu()
     assert got.shape == ref.shape
     torch.testing.assert_close(got.float(), ref.float(), rtol=2e-2, atol=2e-2 * ref.abs().max().item())
