@@ -2,6 +2,7 @@
 // Every kernel moves bf16 as 16-byte vectors (8 channels per lane) — guide Guideline 13.
 #include <pybind11/pybind11.h>
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -90,6 +91,80 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restri
       o[3] = o[4] = o[5] = o[6] = o[7] = f2bf(0.f);
       *reinterpret_cast<bf16x8*>(dst + (size_t)idx * 8) = o;
     }
+  }
+}
+
+// Row-staged space-to-depth form (the ResNet stem input): one workgroup per output block
+// row (2 output rows).  The <= 4 source rows its bilinear taps touch are copied into LDS
+// with coalesced dword loads, then every thread interpolates its 2x2 output pixels from
+// LDS.  The one-thread-per-pixel kernel above issues 48 scattered byte loads per thread
+// (each wave instruction touching ~4 cache lines); here global traffic is the source rows
+// once plus the 32-B output stores.  Same arithmetic as resize_pixel, so the results are
+// identical.  Needs dword-aligned rows (host check) and Wi * 3 <= ROW_MAX bytes.
+constexpr int PRE_ROW_MAX = 4096;
+constexpr int PRE_NT = 128;
+
+__global__ __launch_bounds__(PRE_NT) void preprocess_s2d_rows_kernel(const uint8_t* __restrict__ src,
+                                                                     bf16* __restrict__ dst, PreParams q) {
+  __shared__ __attribute__((aligned(16))) uint8_t rows[4][PRE_ROW_MAX];
+  const int Wo2 = (q.Wo + 1) / 2, Ho2 = (q.Ho + 1) / 2;
+  const int oy2 = blockIdx.x % Ho2, b = blockIdx.x / Ho2;
+  const uint8_t* img = src + (size_t)b * q.src_stride;
+  const int rb = q.Wi * 3;
+  // source rows of output rows 2*oy2 + dy: slot 2*dy (y0) and 2*dy + 1 (y1), + their weights
+  int ys[4];
+  float wy[2];
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy) {
+    const int oy = min(2 * oy2 + dy, q.Ho - 1);  // a row past the image is zero-filled below
+    const float fy = q.half_pixel ? (oy + 0.5f) * q.sy - 0.5f : oy * q.sy;
+    const float fy0 = floorf(fy);
+    const int y0 = max((int)fy0, 0);
+    ys[2 * dy] = y0;
+    ys[2 * dy + 1] = min(y0 + 1, q.Hi - 1);
+    wy[dy] = fminf(fmaxf(fy - (q.half_pixel ? (float)y0 : fy0), 0.f), 1.f);
+  }
+  const int rw = rb >> 2;  // dwords per row
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t* srow = reinterpret_cast<const uint32_t*>(img + (size_t)ys[r] * rb);
+    uint32_t* drow = reinterpret_cast<uint32_t*>(rows[r]);
+    for (int i = threadIdx.x; i < rw; i += PRE_NT) drow[i] = srow[i];
+  }
+  __syncthreads();
+  for (int ox2 = threadIdx.x; ox2 < Wo2; ox2 += PRE_NT) {
+    float pix[4][3];
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const int ox = 2 * ox2 + dx;
+      const float fx = q.half_pixel ? (ox + 0.5f) * q.sx - 0.5f : ox * q.sx;
+      const float fx0 = floorf(fx);
+      const int x0 = max((int)fx0, 0), x1 = min(x0 + 1, q.Wi - 1);
+      const float wx = fminf(fmaxf(fx - (q.half_pixel ? (float)x0 : fx0), 0.f), 1.f);
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy) {
+        const uint8_t* r0 = rows[2 * dy];
+        const uint8_t* r1 = rows[2 * dy + 1];
+        const bool live = 2 * oy2 + dy < q.Ho && ox < q.Wo;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const float p00 = r0[x0 * 3 + c], p01 = r0[x1 * 3 + c], p10 = r1[x0 * 3 + c], p11 = r1[x1 * 3 + c];
+          const float top = p00 + (p01 - p00) * wx;
+          const float bot = p10 + (p11 - p10) * wx;
+          pix[dy * 2 + dx][c] = live ? (top + (bot - top) * wy[dy] - q.m[c]) * q.s[c] : 0.f;
+        }
+      }
+    }
+    bf16x8 o0, o1;
+    o0[0] = f2bf(pix[0][0]); o0[1] = f2bf(pix[0][1]); o0[2] = f2bf(pix[0][2]);
+    o0[3] = f2bf(pix[1][0]); o0[4] = f2bf(pix[1][1]); o0[5] = f2bf(pix[1][2]);
+    o0[6] = f2bf(pix[2][0]); o0[7] = f2bf(pix[2][1]);
+    o1[0] = f2bf(pix[2][2]);
+    o1[1] = f2bf(pix[3][0]); o1[2] = f2bf(pix[3][1]); o1[3] = f2bf(pix[3][2]);
+    o1[4] = o1[5] = o1[6] = o1[7] = f2bf(0.f);
+    bf16x8* d = reinterpret_cast<bf16x8*>(dst + ((size_t)blockIdx.x * Wo2 + ox2) * 16);
+    d[0] = o0;
+    d[1] = o1;
   }
 }
 
@@ -235,6 +310,12 @@ int grid_for(long work, int block) {
   return (int)(g < 1 ? 1 : (g > 2048 * 8 ? 2048 * 8 : g));
 }
 
+// FTM_PREPROCESS_PIXEL=1 keeps the one-thread-per-pixel s2d kernel (A/B and tests)
+bool preprocess_pixel_form() {
+  const char* e = std::getenv("FTM_PREPROCESS_PIXEL");
+  return e && e[0] == '1';
+}
+
 }  // namespace
 
 void preprocess_u8_to_bf16(uintptr_t src, uintptr_t dst, int B, int Hi, int Wi, int Ho, int Wo, int align_corners,
@@ -255,7 +336,11 @@ void preprocess_u8_to_bf16(uintptr_t src, uintptr_t dst, int B, int Hi, int Wi, 
   auto s = reinterpret_cast<hipStream_t>(stream);
   auto S = reinterpret_cast<const uint8_t*>(src);
   auto D = reinterpret_cast<bf16*>(dst);
-  if (s2d) hipLaunchKernelGGL(preprocess_kernel<1>, dim3(grid_for(work, 256)), dim3(256), 0, s, S, D, B, q);
+  const bool rows_ok = s2d && Wi * 3 <= PRE_ROW_MAX && (Wi * 3) % 4 == 0 && src % 4 == 0 && src_stride % 4 == 0 &&
+                       !preprocess_pixel_form();
+  if (rows_ok)
+    hipLaunchKernelGGL(preprocess_s2d_rows_kernel, dim3(B * ((Ho + 1) / 2)), dim3(PRE_NT), 0, s, S, D, q);
+  else if (s2d) hipLaunchKernelGGL(preprocess_kernel<1>, dim3(grid_for(work, 256)), dim3(256), 0, s, S, D, B, q);
   else hipLaunchKernelGGL(preprocess_kernel<0>, dim3(grid_for(work, 256)), dim3(256), 0, s, S, D, B, q);
   FTM_CHECK_LAUNCH();
 }
