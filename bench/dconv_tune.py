@@ -1,4 +1,4 @@
-"""Direct conv (kernels/dconv.hip, BN 32/64) vs the implicit-GEMM auto path on the narrow
+"""Direct conv (kernels/dconv.hip, BN 32/64, 4- or 8-wave tiles) vs the implicit-GEMM auto path on the narrow
 layers of ResNet-50 and Inception-v3 at B=256 (random data, interleaved rounds)."""
 import json
 import sys
@@ -49,8 +49,9 @@ def main():
             fns = {"auto": lambda: K.conv2d_nhwc(x, w, b, None, (s, s), pad, (1, 1), "relu", out=y)}
             for bn in (32, 64):
                 arr = K.dconv_bf16_weight_bytes(w.float(), bn)
-                fns[f"d{bn}"] = (lambda arr=arr, bn=bn: K.conv2d_direct(x, arr, (kh, kw), Cout, b, (s, s), pad, "relu",
-                                                                       out=y, bn=bn))
+                for wv in (4, 8):
+                    fns[f"d{bn}w{wv}"] = (lambda arr=arr, bn=bn, wv=wv: K.conv2d_direct(
+                        x, arr, (kh, kw), Cout, b, (s, s), pad, "relu", out=y, bn=bn, waves=wv))
         else:
             x = torch.randint(0, 120, (B, H, W, Cin), dtype=torch.uint8, device=dev)
             wq = torch.randint(0, 120, (Cout, kh * kw * Cin), dtype=torch.uint8, device=dev)
@@ -61,8 +62,10 @@ def main():
                                                      out_scale=0.05, out=y, chan_scale=cs)}
             for bn in (32, 64):
                 arr = K.dconv_weights(wq, Cout, 1, bn)
-                fns[f"d{bn}"] = (lambda arr=arr, bn=bn: K.conv2d_direct(x, arr, (kh, kw), Cout, b, (s, s), pad, "relu",
-                                                                       out=y, bn=bn, chan_scale=cs, out_scale=0.05))
+                for wv in (4, 8):
+                    fns[f"d{bn}w{wv}"] = (lambda arr=arr, bn=bn, wv=wv: K.conv2d_direct(
+                        x, arr, (kh, kw), Cout, b, (s, s), pad, "relu", out=y, bn=bn, chan_scale=cs, out_scale=0.05,
+                        waves=wv))
         for f in fns.values():
             f()
         torch.cuda.synchronize()

@@ -13,8 +13,8 @@
 //      im2col happens in the LDS address, never in memory traffic,
 //   3. stages the [256 px][BN] result through LDS and stores 16-B row segments (bf16 or
 //      e4m3 with the successor's scale), channel-offset capable (concat slices).
-// Output tile: 16 x 16 pixels of one image (wave w owns tile rows 4w..4w+3 = 4 fragments),
-// BN = 32 or 64 channels.  Pooled (stem) tiles are 17 conv columns wide: 4 waves cover 7 x 8
+// Output tile: 16 x 16 pixels of one image with 4 waves, 32 x 16 with 8 (wave w owns tile
+// rows 4w..4w+3 = 4 fragments), BN = 32 or 64 channels.  Pooled (stem) tiles are 17 conv columns wide: 4 waves cover 7 x 8
 // pooled pixels, 8 waves (pool_rows = 14) 14 x 8 — the filter bank DMA (34 KB for the
 // ResNet s2d stem, an L2 hit but the largest per-workgroup transfer) is then paid once per
 // 112 pooled pixels instead of 56: 181 -> 161 us for the B=256 stem (bench/stem_ab.py).  Weights are pre-arranged by the host: row pitch WP bytes =
@@ -33,7 +33,7 @@ namespace {
 
 __device__ __attribute__((aligned(16))) uint32_t g_zero16[4];
 
-constexpr int TH = 16, TW = 16, NT = 256;
+constexpr int TH = 16, TW = 16;  // 4-wave tile (8 waves: 32 x 16)
 
 struct DconvParams {
   const uint8_t* x;    // [N, H, W, Cin] (bf16 or e4m3)
@@ -95,9 +95,10 @@ FTM_DEVICE u16x8 pool3x3_max(const uint8_t* base, int row_bytes, int px_bytes) {
 
 template <int ES, int BN, int ACT, bool OUT_FP8, bool POOL = false, int WAVES = 4>
 __global__ __launch_bounds__(WAVES * 64) void dconv_kernel(DconvParams p) {
-  static_assert(WAVES == 4 || (POOL && WAVES == 8), "8-wave tiles are pooled-only");
+  static_assert(WAVES == 4 || WAVES == 8, "4 or 8 waves");
   constexpr int NTH = WAVES * 64;
   constexpr int PTH = WAVES == 8 ? 14 : 7;  // pooled rows per tile
+  constexpr int THE = TH * WAVES / 4;       // conv rows per (unpooled) tile: 16 or 32
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int KL = ES == 2 ? 16 : 32;  // K bytes per lane per MFMA
   constexpr int I = BN / 16;             // channel fragments
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(WAVES * 64) void dconv_kernel(DconvParams p) {
   const int th = b % p.tiles_h;
   const int n = b / p.tiles_h;
   constexpr int TPW = POOL ? 17 : TW;  // conv tile width (pixel p of the tile = row p / TPW, col p % TPW)
-  const int oy0 = POOL ? th * (2 * PTH) - p.ppt : th * TH, ox0 = POOL ? tw * 16 - p.ppl : tw * TW, n0 = tn * BN;
+  const int oy0 = POOL ? th * (2 * PTH) - p.ppt : th * THE, ox0 = POOL ? tw * 16 - p.ppl : tw * TW, n0 = tn * BN;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int patch_bytes = p.PH * p.PW * p.RB;
@@ -244,7 +245,7 @@ __global__ __launch_bounds__(WAVES * 64) void dconv_kernel(DconvParams p) {
     }
     return;
   }
-  for (int q = tid; q < TH * TW * CPR; q += NT) {
+  for (int q = tid; q < THE * TW * CPR; q += NTH) {
     const int pl = q / CPR, cc = q % CPR;
     const int oy = oy0 + pl / TW, ox = ox0 + pl % TW;
     const int c = n0 + cc * EPO;
@@ -255,23 +256,19 @@ __global__ __launch_bounds__(WAVES * 64) void dconv_kernel(DconvParams p) {
   }
 }
 
-template <int ES, int BN, bool OUT_FP8>
-void launch_act(const DconvParams& p, int act, size_t lds, hipStream_t s, int pool_rows) {
-  dim3 grid(p.N * p.tiles_h * p.tiles_w * p.tiles_n), block(NT);
+template <int ES, int BN, bool OUT_FP8, int WAVES>
+void launch_act(const DconvParams& p, int act, size_t lds, hipStream_t s) {
+  dim3 grid(p.N * p.tiles_h * p.tiles_w * p.tiles_n), block(WAVES * 64);
   if constexpr (ES == 2 && !OUT_FP8) {
     if (p.Hp > 0) {  // fused max pool (ReLU stems)
       if (act != ACT_RELU) throw std::invalid_argument("dconv: fused pool needs a ReLU conv");
       static bool done = false;
       if (!done) {
-        for (auto f : {(const void*)dconv_kernel<ES, BN, ACT_RELU, false, true>,
-                       (const void*)dconv_kernel<ES, BN, ACT_RELU, false, true, 8>})
-          hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)dconv_kernel<ES, BN, ACT_RELU, false, true, WAVES>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         done = true;
       }
-      if (pool_rows == 14)  // 8 waves, 14 x 8 pooled pixels: the filter bank is fetched once per 112 outputs
-        hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_RELU, false, true, 8>), grid, dim3(512), lds, s, p);
-      else
-        hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_RELU, false, true>), grid, block, lds, s, p);
+      hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_RELU, false, true, WAVES>), grid, block, lds, s, p);
       return;
     }
   } else {
@@ -279,20 +276,21 @@ void launch_act(const DconvParams& p, int act, size_t lds, hipStream_t s, int po
   }
   switch (act) {
     case ACT_NONE:
-      hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_NONE, OUT_FP8>), grid, block, lds, s, p);
+      hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_NONE, OUT_FP8, false, WAVES>), grid, block, lds, s, p);
       break;
     case ACT_RELU:
-      hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_RELU, OUT_FP8>), grid, block, lds, s, p);
+      hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_RELU, OUT_FP8, false, WAVES>), grid, block, lds, s, p);
       break;
     default: throw std::invalid_argument("dconv: activation must be none/relu");
   }
 }
 
-template <int ES, int BN, bool OUT_FP8>
+template <int ES, int BN, bool OUT_FP8, int WAVES>
 void set_lds_limit() {
   static bool done = false;
   if (done) return;
-  for (auto f : {(const void*)dconv_kernel<ES, BN, ACT_NONE, OUT_FP8>, (const void*)dconv_kernel<ES, BN, ACT_RELU, OUT_FP8>})
+  for (auto f : {(const void*)dconv_kernel<ES, BN, ACT_NONE, OUT_FP8, false, WAVES>,
+                 (const void*)dconv_kernel<ES, BN, ACT_RELU, OUT_FP8, false, WAVES>})
     hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   done = true;
 }
@@ -301,7 +299,7 @@ void set_lds_limit() {
 
 // patch rows of a tile: pooled tiles are 17 conv columns wide and hold npx = 64 * waves
 // fragment pixels (the last fragment row is (npx - 1) / 17)
-int patch_rows(int KH, int S, bool pool, int npx) { return (pool ? (npx - 1) / 17 : TH - 1) * S + KH; }
+int patch_rows(int KH, int S, bool pool, int npx) { return (pool ? (npx - 1) / 17 : npx / TW - 1) * S + KH; }
 
 int lds_bytes(int es, int bn, int KH, int KW, int S, int Cin, int wp, bool pool, int npx = TH * TW) {
   const int PH = patch_rows(KH, S, pool, npx), PW = (pool ? TW : TW - 1) * S + KW;
@@ -320,7 +318,7 @@ int dconv_lds_bytes(int es, int bn, int KH, int KW, int S, int Cin, int wp) {
 void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t y, int es, int N, int H, int W,
            int Cin, int Cout, int KH, int KW, int S, int ph, int pw, int Ho, int Wo, int wp, int ldy, int y_coff,
            int out_fp8, float out_q, int act, int bn, uintptr_t stream, int Hp, int Wp, int ppt, int ppl,
-           int pool_rows) {
+           int waves) {
   const int KL = es == 2 ? 16 : 32;
   if (es != 1 && es != 2) throw std::invalid_argument("dconv: es must be 1 or 2");
   if ((Cin * es) % KL) throw std::invalid_argument("dconv: Cin*es must be a multiple of " + std::to_string(KL));
@@ -333,9 +331,10 @@ void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t 
   if (S != 1 && S != 2) throw std::invalid_argument("dconv: stride must be 1 or 2");
   if (!bias || (es == 1 && !scale)) throw std::invalid_argument("dconv: bias (and fp8 scale) required");
   if (x % 16 || w % 16 || y % 16 || bias % 16 || (scale && scale % 16)) throw std::invalid_argument("dconv: alignment");
-  if (Hp > 0 && pool_rows != 7 && pool_rows != 14) throw std::invalid_argument("dconv: pool_rows must be 7 or 14");
-  if (Hp <= 0) pool_rows = 7;
-  const int npx = pool_rows == 14 ? 512 : TH * TW;
+  if (waves != 4 && waves != 8) throw std::invalid_argument("dconv: waves must be 4 or 8");
+  if (waves == 8 && lds_bytes(es, bn, KH, KW, S, Cin, wp, Hp > 0, 512) > 160 * 1024) waves = 4;  // wide patches
+  const int npx = waves * 64;                // fragment pixels per tile
+  const int pool_rows = waves == 8 ? 14 : 7;  // pooled tiles: 7 or 14 x 8 pooled pixels
   const int lds = lds_bytes(es, bn, KH, KW, S, Cin, wp, Hp > 0, npx);
   if (lds > 160 * 1024) throw std::invalid_argument("dconv: tile does not fit LDS (" + std::to_string(lds) + " B)");
   DconvParams p{};
@@ -371,15 +370,20 @@ void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t 
     p.tiles_h = (Hp + pool_rows - 1) / pool_rows;
     p.tiles_w = (Wp + 7) / 8;
   } else {
-    p.tiles_h = (Ho + TH - 1) / TH;
+    p.tiles_h = (Ho + npx / TW - 1) / (npx / TW);
     p.tiles_w = (Wo + TW - 1) / TW;
   }
   p.tiles_n = (Cout + bn - 1) / bn;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-#define FTM_DCONV(ES_, BN_, OF_)            \
-  do {                                      \
-    set_lds_limit<ES_, BN_, OF_>();         \
-    launch_act<ES_, BN_, OF_>(p, act, lds, s, pool_rows); \
+#define FTM_DCONV(ES_, BN_, OF_)                                                   \
+  do {                                                                             \
+    if (waves == 8) {                                                              \
+      set_lds_limit<ES_, BN_, OF_, 8>();                                           \
+      launch_act<ES_, BN_, OF_, 8>(p, act, lds, s);                                \
+    } else {                                                                       \
+      set_lds_limit<ES_, BN_, OF_, 4>();                                           \
+      launch_act<ES_, BN_, OF_, 4>(p, act, lds, s);                                \
+    }                                                                              \
   } while (0)
   if (es == 2) {
     if (bn == 32) { if (out_fp8) FTM_DCONV(2, 32, true); else FTM_DCONV(2, 32, false); }

@@ -867,17 +867,30 @@ def dconv_bf16_weight_bytes(w_ohwi: torch.Tensor, bn: int) -> torch.Tensor:
     return dconv_weights(wb, Cout, 2, bn)
 
 
+def _dconv_waves(waves, pool_rows, bn) -> int:
+    """8-wave tiles pay where the filter-bank fetch dominates: BN = 64 (ResNet stem 180 -> 174 µs,
+    Inception 2b 251 -> 223 µs); BN = 32 tiles lose occupancy for little weight saving (2a 148 ->
+    156 µs) and stay at 4 waves (``bench/dconv_tune.py``, profiles/r02_dconv_waves)."""
+    if waves is None and pool_rows is not None:
+        waves = {7: 4, 14: 8}[int(pool_rows)]
+    if waves is None and os.environ.get("FTM_DCONV_WAVES"):
+        waves = int(os.environ["FTM_DCONV_WAVES"])
+    return int(waves or (8 if bn == 64 else 4))
+
+
 def conv2d_direct(x: torch.Tensor, w_arr: torch.Tensor, kshape, Cout: int, bias: torch.Tensor, stride=(1, 1),
                   pad=(0, 0, 0, 0), act=None, out: torch.Tensor | None = None, out_channel_offset: int = 0,
                   bn: int = 64, chan_scale: torch.Tensor | None = None, out_scale: float | None = None,
-                  maxpool_pad: tuple | None = None, pool_rows: int | None = None) -> torch.Tensor:
+                  maxpool_pad: tuple | None = None, pool_rows: int | None = None,
+                  waves: int | None = None) -> torch.Tensor:
     """Direct conv on device: ``x`` NHWC bf16 (``chan_scale`` None) or e4m3 bytes (uint8, with
     the per-channel dequant scale ``chan_scale``); ``w_arr`` from :func:`dconv_weights`;
     ``out_scale`` → e4m3 output.  ``maxpool_pad = (top, bottom, left, right)`` fuses a 3x3 /
-    stride-2 max pool of the ReLU output (ResNet stem → pool1); ``pool_rows`` (7 or 14,
-    default ``FTM_STEM_POOL_ROWS`` or 14) is the pooled tile height — 14 runs 8-wave
-    workgroups that fetch the filter bank once per 14 x 8 pooled pixels.  Device-only (the
-    host paths use the reference convs)."""
+    stride-2 max pool of the ReLU output (ResNet stem → pool1).  ``waves`` (4 or 8, default
+    ``FTM_DCONV_WAVES``, else 8 for ``bn=64`` and 4 for ``bn=32``) sets the workgroup / tile size: 8 waves cover 32 x 16 conv
+    pixels (pooled: 14 x 8 pooled pixels, ``pool_rows=14``; 4 waves = 16 x 16 / 7 x 8) and
+    fetch the filter bank half as often; tiles whose patch would not fit LDS fall back to 4.
+    Device-only (the host paths use the reference convs)."""
     N, H, W, Cin = x.shape
     KH, KW = kshape
     s = stride[0]
@@ -904,7 +917,7 @@ def conv2d_direct(x: torch.Tensor, w_arr: torch.Tensor, kshape, Cout: int, bias:
     _hip().dconv(x.data_ptr(), w_arr.data_ptr(), _ptr(chan_scale), bias.data_ptr(), out.data_ptr(), es, N, H, W, Cin,
                  Cout, KH, KW, s, pt, pl, Ho, Wo, w_arr.shape[1], out.shape[3], out_channel_offset, int(out_fp8),
                  1.0 / out_scale if out_fp8 else 1.0, act_code(act), bn, _stream(), Hp, Wp, ppt, ppl,
-                 int(pool_rows or os.environ.get("FTM_STEM_POOL_ROWS", "14")))
+                 _dconv_waves(waves, pool_rows, bn))
     return out
 
 

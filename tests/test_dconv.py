@@ -29,8 +29,9 @@ BF16_CASES = [  # N, H, W, Cin, Cout, (kh, kw), stride, pad, bn, out_fp8
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("waves", [4, 8])
 @pytest.mark.parametrize("case", BF16_CASES)
-def test_dconv_bf16_gpu(case):
+def test_dconv_bf16_gpu(case, waves):
     N, H, W, Cin, Cout, (kh, kw), s, pad, bn, out_fp8 = case
     torch.manual_seed(hash(case) % 1000)
     x = torch.randn(N, H, W, Cin).to(torch.bfloat16)
@@ -39,7 +40,8 @@ def test_dconv_bf16_gpu(case):
     so = 0.01 if out_fp8 else None
     ref = K.conv2d_nhwc(x, w, b, None, (s, s), pad, (1, 1), "relu", out_scale=so)
     arr = K.dconv_bf16_weight_bytes(w.float(), bn).to(DEV)
-    got = K.conv2d_direct(x.to(DEV), arr, (kh, kw), Cout, b.to(DEV), (s, s), pad, "relu", bn=bn, out_scale=so).cpu()
+    got = K.conv2d_direct(x.to(DEV), arr, (kh, kw), Cout, b.to(DEV), (s, s), pad, "relu", bn=bn, out_scale=so,
+                          waves=waves).cpu()
     if out_fp8:
         gd, rd = Q.from_fp8_bytes(got), Q.from_fp8_bytes(ref)
         assert ((gd - rd).abs() <= 0.13 * rd.abs() + 1e-3).all()
@@ -57,8 +59,9 @@ FP8_CASES = [  # N, H, W, Cin, Cout, k, stride, pad, bn, offset, extra
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("waves", [4, 8])
 @pytest.mark.parametrize("case", FP8_CASES)
-def test_dconv_fp8_gpu(case):
+def test_dconv_fp8_gpu(case, waves):
     N, H, W, Cin, Cout, k, s, pad, bn, off, extra = case
     kh, kw = (k, k) if isinstance(k, int) else k
     torch.manual_seed(Cin * 7 + Cout + kh)
@@ -73,7 +76,7 @@ def test_dconv_fp8_gpu(case):
     out = torch.zeros((N, Ho, Wo, Cout + extra), dtype=torch.uint8, device=DEV)
     arr = K.dconv_weights(wq, Cout, 1, bn).to(DEV)
     K.conv2d_direct(xq.to(DEV), arr, (kh, kw), Cout, b.to(DEV), (s, s), pad, "relu", out=out, out_channel_offset=off,
-                    bn=bn, chan_scale=(ws * sx).to(DEV), out_scale=so)
+                    bn=bn, chan_scale=(ws * sx).to(DEV), out_scale=so, waves=waves)
     got = out[..., off:off + Cout].cpu()
     gd, rd = Q.from_fp8_bytes(got.contiguous()), Q.from_fp8_bytes(ref)
     # raw e4m3 units: one step (2^-3 relative) of slack for accumulation-order rounding flips;
