@@ -35,6 +35,30 @@ def main():
             if rnd:
                 times[form].append(e0.elapsed_time(e1) / 10 * 1e3)
     nbytes = img.numel() + out.numel() * 2
+    # Inception-v3 form: 299 x 299 -> 299 x 299 (897-byte, unaligned rows), s2d [B,150,150,16]
+    img2 = torch.randint(0, 256, (B, 299, 299, 3), dtype=torch.uint8, device=dev)
+    out2 = torch.empty((B, 150, 150, 16), dtype=torch.bfloat16, device=dev)
+    t2 = {"rows": [], "pixel": []}
+    for rnd in range(8):
+        for form in ("rows", "pixel"):
+            if form == "pixel":
+                os.environ["FTM_PREPROCESS_PIXEL"] = "1"
+            else:
+                os.environ.pop("FTM_PREPROCESS_PIXEL", None)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                K.preprocess_images(img2, (299, 299), mean, std, out=out2, s2d=True)
+            e1.record()
+            e1.synchronize()
+            res[form + "299"] = out2.clone()
+            if rnd:
+                t2[form].append(e0.elapsed_time(e1) / 10 * 1e3)
+    os.environ.pop("FTM_PREPROCESS_PIXEL", None)
+    for form, ts in t2.items():
+        us = sorted(ts)[len(ts) // 2]
+        print(json.dumps({"batch": B, "hw": 299, "form": form, "us": round(us, 1),
+                          "max_abs_diff_vs_pixel": float((res[form + "299"].float() - res["pixel299"].float()).abs().max())}))
     for form, ts in times.items():
         us = sorted(ts)[len(ts) // 2]
         print(json.dumps({"batch": B, "form": form, "us": round(us, 1), "TB_s": round(nbytes / us / 1e6, 2),

@@ -100,7 +100,9 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restri
 // LDS.  The one-thread-per-pixel kernel above issues 48 scattered byte loads per thread
 // (each wave instruction touching ~4 cache lines); here global traffic is the source rows
 // once plus the 32-B output stores.  Same arithmetic as resize_pixel, so the results are
-// identical.  Needs dword-aligned rows (host check) and Wi * 3 <= ROW_MAX bytes.
+// identical.  Rows need not be dword-aligned (Inception's 299 x 3 = 897-byte rows): each
+// slot keeps its row's misalignment and the copy starts at the dword below (reading at most
+// 3 bytes past the last row, inside the allocation granule).  Needs Wi * 3 + 3 <= ROW_MAX.
 constexpr int PRE_ROW_MAX = 4096;
 constexpr int PRE_NT = 128;
 
@@ -124,11 +126,14 @@ __global__ __launch_bounds__(PRE_NT) void preprocess_s2d_rows_kernel(const uint8
     ys[2 * dy + 1] = min(y0 + 1, q.Hi - 1);
     wy[dy] = fminf(fmaxf(fy - (q.half_pixel ? (float)y0 : fy0), 0.f), 1.f);
   }
-  const int rw = rb >> 2;  // dwords per row
+  int sh[4];  // byte misalignment of each staged row
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const uint32_t* srow = reinterpret_cast<const uint32_t*>(img + (size_t)ys[r] * rb);
+    const uint8_t* rowp = img + (size_t)ys[r] * rb;
+    sh[r] = (int)(reinterpret_cast<uintptr_t>(rowp) & 3);
+    const uint32_t* srow = reinterpret_cast<const uint32_t*>(rowp - sh[r]);
     uint32_t* drow = reinterpret_cast<uint32_t*>(rows[r]);
+    const int rw = (sh[r] + rb + 3) >> 2;  // dwords covering the row
     for (int i = threadIdx.x; i < rw; i += PRE_NT) drow[i] = srow[i];
   }
   __syncthreads();
@@ -143,8 +148,8 @@ __global__ __launch_bounds__(PRE_NT) void preprocess_s2d_rows_kernel(const uint8
       const float wx = fminf(fmaxf(fx - (q.half_pixel ? (float)x0 : fx0), 0.f), 1.f);
 #pragma unroll
       for (int dy = 0; dy < 2; ++dy) {
-        const uint8_t* r0 = rows[2 * dy];
-        const uint8_t* r1 = rows[2 * dy + 1];
+        const uint8_t* r0 = rows[2 * dy] + sh[2 * dy];
+        const uint8_t* r1 = rows[2 * dy + 1] + sh[2 * dy + 1];
         const bool live = 2 * oy2 + dy < q.Ho && ox < q.Wo;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -336,8 +341,7 @@ void preprocess_u8_to_bf16(uintptr_t src, uintptr_t dst, int B, int Hi, int Wi, 
   auto s = reinterpret_cast<hipStream_t>(stream);
   auto S = reinterpret_cast<const uint8_t*>(src);
   auto D = reinterpret_cast<bf16*>(dst);
-  const bool rows_ok = s2d && Wi * 3 <= PRE_ROW_MAX && (Wi * 3) % 4 == 0 && src % 4 == 0 && src_stride % 4 == 0 &&
-                       !preprocess_pixel_form();
+  const bool rows_ok = s2d && Wi * 3 + 3 <= PRE_ROW_MAX && !preprocess_pixel_form();
   if (rows_ok)
     hipLaunchKernelGGL(preprocess_s2d_rows_kernel, dim3(B * ((Ho + 1) / 2)), dim3(PRE_NT), 0, s, S, D, q);
   else if (s2d) hipLaunchKernelGGL(preprocess_kernel<1>, dim3(grid_for(work, 256)), dim3(256), 0, s, S, D, B, q);

@@ -107,6 +107,7 @@ def test_preprocess(hw_in, hw_out, half):
 @pytest.mark.parametrize("hw_in,hw_out,half,align", [((256, 256), (224, 224), False, False),
                                                      ((100, 120), (75, 75), False, False),  # odd: zero-filled edge
                                                      ((320, 300), (299, 299), True, False),
+                                                     ((299, 299), (299, 299), False, False),  # 897-B rows
                                                      ((64, 96), (33, 47), False, True)])
 def test_preprocess_s2d_row_staged(hw_in, hw_out, half, align, monkeypatch):
     """The row-staged (LDS) s2d preprocess kernel vs the one-thread-per-pixel kernel (same
