@@ -23,5 +23,20 @@ def torchrun_smoke(nproc, *args, timeout=180, script="comm_smoke.py"):
            os.path.join(root, "tools", script), *args]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
-    return sorted((json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")), key=lambda d: d["rank"])
+    return sorted(_rank_records(r.stdout), key=lambda d: d["rank"])
+
+
+def _rank_records(text):
+    """Every ``{"rank": ...}`` JSON object in the ranks' merged stdout.  Ranks share torchrun's
+    stdout pipe, so two records can land on one line (a rank's text and its newline are
+    separate writes): decode objects wherever they start instead of line by line."""
+    import json
+
+    dec = json.JSONDecoder()
+    out, i = [], text.find('{"rank"')
+    while i >= 0:
+        obj, end = dec.raw_decode(text, i)
+        out.append(obj)
+        i = text.find('{"rank"', end)
+    return out
 

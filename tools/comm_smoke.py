@@ -34,8 +34,9 @@ def main():
     c.all_reduce(y)
     objs = comm.all_gather_object({"rank": rank})
     comm.barrier()
-    print(json.dumps({"rank": rank, "ws": ws, "bcast": x.tolist(), "sum": y.tolist(),
-                      "objs": [o["rank"] for o in objs]}), flush=True)
+    sys.stdout.write(json.dumps({"rank": rank, "ws": ws, "bcast": x.tolist(), "sum": y.tolist(),
+                                 "objs": [o["rank"] for o in objs]}) + "\n")  # one write per record
+    sys.stdout.flush()
     comm.destroy()
 
 

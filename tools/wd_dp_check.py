@@ -39,7 +39,8 @@ def main():
     torch.cuda.synchronize(dev)
     sd = tr.model.state_dict()
     sums = {k: [float(v.double().sum()), float(v.double().abs().sum())] for k, v in sorted(sd.items())}
-    print(json.dumps({"rank": rank, "fused": tr._fused is not None, "losses": losses, "sums": sums}), flush=True)
+    sys.stdout.write(json.dumps({"rank": rank, "fused": tr._fused is not None, "losses": losses, "sums": sums}) + "\n")  # one write per record
+    sys.stdout.flush()
     tr.close()
     comm.destroy()
 
