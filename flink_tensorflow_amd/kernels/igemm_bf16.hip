@@ -24,6 +24,7 @@
 // remapped XCD-aware so the channel tiles of one pixel tile share an L2 (guide T1).
 #include <pybind11/pybind11.h>
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -47,6 +48,7 @@ struct IgemmParams {
   int ldr;          // residual pixel stride
   int tiles_m, tiles_n;
   int kq, kr;  // CONV: divmod(BK, Cin), the (tap, channel) advance of one K tile
+  int prio;    // raise the wave priority around each MFMA cluster (igemm_prio)
   // DUAL (pointwise GEMM + fused strided 1x1 shortcut): K = K1 + C2; k >= K1 reads the
   // second source x2 [N, H2, W2, C2] at pixel (n, ho*s2, wo*s2) of output pixel (n, ho, wo)
   const bf16* x2;
@@ -248,6 +250,7 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
     if (kt + 1 < nk) load_tile((kt + 1) * BK);
     const bf16* xs = Xs + buf * BM * BK;
     const bf16* ws = Ws + buf * BN * BK;
+    if (p.prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 a[4], b[J];
@@ -261,6 +264,7 @@ __global__ __launch_bounds__(NT, 2) void igemm_bf16_kernel(IgemmParams p) {
 #pragma unroll
         for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
+    if (p.prio) __builtin_amdgcn_s_setprio(0);
     if (kt + 1 < nk) {
       if constexpr (STAGES == 1) __syncthreads();  // single buffer: everyone done reading
       store_tile(STAGES == 2 ? (buf ^ 1) : 0);
@@ -388,6 +392,19 @@ void launch(const IgemmParams& p, int act, int cfg, hipStream_t s) {
   FTM_CHECK_LAUNCH();
 }
 
+// s_setprio(1) around each K-tile's MFMA cluster (FTM_IGEMM_PRIO=0 turns it off).  With two
+// compute lanes a CU holds this kernel's waves next to the sibling lane's (loads, LDS
+// stores, epilogues): raising the MFMA phase's priority keeps the matrix cores fed.  Single
+// lane it is neutral (3861 vs 3863 µs per 256 images); end to end +1.0 % (79.7k -> 80.5k,
+// profiles/r02_igemm_prio).
+int igemm_prio() {
+  static const int v = [] {
+    const char* e = std::getenv("FTM_IGEMM_PRIO");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return v;
+}
+
 // No allocation in the launch path (it may be captured into a hipGraph): a layer without
 // bias passes a zero vector owned by the caller.
 void require_bias(const float* b) {
@@ -417,6 +434,7 @@ void conv2d_nhwc_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, u
   if (bias) check_align(bias, 16, "bias");
   if (res) check_align(res, 16, "residual");
   IgemmParams p{};
+  p.prio = igemm_prio();
   p.x = reinterpret_cast<const bf16*>(x);
   p.w = reinterpret_cast<const bf16*>(w);
   p.bias = reinterpret_cast<const float*>(bias);
@@ -450,6 +468,7 @@ void gemm_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_
   if (bias) check_align(bias, 16, "bias");
   if (res) check_align(res, 16, "residual");
   IgemmParams p{};
+  p.prio = igemm_prio();
   p.x = reinterpret_cast<const bf16*>(x);
   p.w = reinterpret_cast<const bf16*>(w);
   p.bias = reinterpret_cast<const float*>(bias);
@@ -479,6 +498,7 @@ void conv1x1_dual_bf16(uintptr_t x, uintptr_t x2, uintptr_t w, uintptr_t bias, u
   check_align(y, 16, "y");
   check_align(bias, 16, "bias");
   IgemmParams p{};
+  p.prio = igemm_prio();
   p.x = reinterpret_cast<const bf16*>(x);
   p.x2 = reinterpret_cast<const bf16*>(x2);
   p.w = reinterpret_cast<const bf16*>(w);
