@@ -59,7 +59,7 @@ FTM_DEVICE Tile tile_of(int t, int tiles_y, int tiles_x, int H, int W) {
 template <int ACT>
 __global__ __launch_bounds__(NT, 1) void conv3x3c64_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                           const float* __restrict__ bias, bf16* __restrict__ y,
-                                                          int N, int H, int W, int ldy, int y_coff) {
+                                                          int N, int H, int W, int ldy, int y_coff, int prio) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   u32x4* Ws = reinterpret_cast<u32x4*>(smem);
   u32x4* Ps = reinterpret_cast<u32x4*>(smem + W_BYTES);
@@ -124,6 +124,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3c64_kernel(const bf16* __restric
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    FTM_PRIO_HI(prio);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int kh = tap / 3, kw = tap - kh * 3;
@@ -145,6 +146,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3c64_kernel(const bf16* __restric
           for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
       }
     }
+    FTM_PRIO_LO(prio);
     // ---- epilogue: lane holds channels 16i + 4*kg + r of pixel (wave, 16j + prow)
     {
       const int oy = cur.y0 + wave;
@@ -191,10 +193,12 @@ void conv3x3c64_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int 
   auto Y = reinterpret_cast<bf16*>(y);
   if (act == ACT_RELU) {
     hipFuncSetAttribute((const void*)conv3x3c64_kernel<ACT_RELU>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(conv3x3c64_kernel<ACT_RELU>, dim3(grid), dim3(NT), lds, s, X, Wt, B, Y, N, H, W, ldy, y_coff);
+    hipLaunchKernelGGL(conv3x3c64_kernel<ACT_RELU>, dim3(grid), dim3(NT), lds, s, X, Wt, B, Y, N, H, W, ldy, y_coff,
+                       ftm_mfma_prio());
   } else if (act == ACT_NONE) {
     hipFuncSetAttribute((const void*)conv3x3c64_kernel<ACT_NONE>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(conv3x3c64_kernel<ACT_NONE>, dim3(grid), dim3(NT), lds, s, X, Wt, B, Y, N, H, W, ldy, y_coff);
+    hipLaunchKernelGGL(conv3x3c64_kernel<ACT_NONE>, dim3(grid), dim3(NT), lds, s, X, Wt, B, Y, N, H, W, ldy, y_coff,
+                       ftm_mfma_prio());
   } else {
     throw std::invalid_argument("conv3x3c64: act must be none or relu");
   }

@@ -49,6 +49,7 @@ struct DconvParams {
   int PH, PW;  // patch rows / cols
   int ldy, y_coff;
   int tiles_h, tiles_w, tiles_n;
+  int prio;  // s_setprio(1) around the K loop (ftm_mfma_prio)
   // POOL: fused 3x3 / stride-2 max pool of the (ReLU) conv output.  A workgroup owns a
   // 7 x 8 pooled tile, i.e. a 15 x 17 conv tile (255 of the 256 fragment pixels, rows
   // 14t - ppt.., cols 16t - ppl..); out-of-range conv positions enter the max as 0
@@ -162,6 +163,7 @@ __global__ __launch_bounds__(WAVES * 64) void dconv_kernel(DconvParams p) {
     prow0[j] = (r * p.S) * p.PW + c * p.S;
   }
 
+  FTM_PRIO_HI(p.prio);
   for (int s = 0; s < p.ksteps; ++s) {
     const int kb = s * 4 * KL + fq * KL;  // this lane group's K byte offset
     const int bo = koff_of(p, s, fq);
@@ -196,6 +198,7 @@ __global__ __launch_bounds__(WAVES * 64) void dconv_kernel(DconvParams p) {
           acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], bb[j], acc[i][j], 0, 0, 0, 127, 0, 127);
     }
   }
+  FTM_PRIO_LO(p.prio);
   __syncthreads();  // everyone done with the patch: reuse LDS for the output tile
 
   // ---- 3. epilogue: [dequant] + bias + act -> LDS [256 px][BN] -> 16-B row segments
@@ -353,6 +356,7 @@ void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t 
   p.PH = patch_rows(KH, S, Hp > 0, npx);
   p.PW = (Hp > 0 ? TW : TW - 1) * S + KW;  // pooled tiles are 17 conv columns wide
   p.ldy = ldy; p.y_coff = y_coff;
+  p.prio = ftm_mfma_prio();
   p.Hp = Hp; p.Wp = Wp; p.ppt = ppt; p.ppl = ppl;
   for (int st = 0; st < p.ksteps; ++st)
     for (int fq = 0; fq < 4; ++fq) {

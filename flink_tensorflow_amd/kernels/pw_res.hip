@@ -39,7 +39,7 @@ template <int K1, int K2, int TP, int BN>
 __global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ x, const bf16* __restrict__ x2,
                                                        const bf16* __restrict__ w, const float* __restrict__ bias,
                                                        const bf16* __restrict__ res, bf16* __restrict__ y, int M,
-                                                       int S, int ldy, int y_coff, int ldr) {
+                                                       int S, int ldy, int y_coff, int ldr, int prio) {
   constexpr int K = K1 + K2;
   constexpr bool DUAL = K2 > 0;
   constexpr int KC = K / 8;             // 16-B chunks per x / W row
@@ -114,6 +114,7 @@ __global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ 
     for (int i = 0; i < I; ++i)
 #pragma unroll
       for (int j = 0; j < J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    FTM_PRIO_HI(prio);
 #pragma unroll
     for (int ks = 0; ks < K / 32; ++ks) {
       const int c = ks * 4 + kg;
@@ -127,6 +128,7 @@ __global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ 
 #pragma unroll
         for (int j = 0; j < J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
     }
+    FTM_PRIO_LO(prio);
     __syncthreads();  // x tile fully read: its LDS becomes the output tile
     // ---- acc + bias -> bf16 output tile [TP][BN]
 #pragma unroll
@@ -185,7 +187,7 @@ void launch(const bf16* x, const bf16* x2, const bf16* w, const float* b, const 
   (void)hipFuncSetAttribute((const void*)pw_res_kernel<K1, K2, TP, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             lds);
   hipLaunchKernelGGL((pw_res_kernel<K1, K2, TP, BN>), dim3(G), dim3(NT), lds, s, x, x2, w, b, r, y, M, S, ldy, y_coff,
-                     ldr);
+                     ldr, ftm_mfma_prio());
 }
 
 }  // namespace
