@@ -21,6 +21,7 @@
 // pooling fp8 -> bf16 (classifier input).
 #include <pybind11/pybind11.h>
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -75,9 +76,22 @@ struct Fp8Params {
   int ldx;          // GEMM mode: row stride of X in elements
   int ldy, y_coff;  // output pixel stride / channel offset (elements)
   int tiles_m, tiles_n;
+  int prio;  // s_setprio(1) around each K-tile's MFMA cluster (fp8_prio)
 };
 
 FTM_DEVICE int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 4); }
+
+// FTM_FP8_PRIO=1 raises the wave priority for the MFMA phase, as igemm_bf16 does by default
+// (profiles/r02_igemm_prio).  Here it measured SLOWER (Inception-v3 fp8 61.2k -> 60.4k
+// static, 54.4k -> 53.1k dynamic): an fp8 K-tile is 128 deep, so the MFMA cluster is long
+// and prioritising it starves the sibling lane's loads.  Off by default.
+int fp8_prio() {
+  static const int v = [] {
+    const char* e = std::getenv("FTM_FP8_PRIO");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return v;
+}
 
 template <int BM, int BN, bool CONV, bool IN_BF16, bool OUT_FP8, int ACT>
 __global__ __launch_bounds__(NT, 2) void igemm_fp8_kernel(Fp8Params p) {
@@ -214,6 +228,7 @@ __global__ __launch_bounds__(NT, 2) void igemm_fp8_kernel(Fp8Params p) {
 
   for (int kt = 0; kt < nk; ++kt) {
     if (kt + 1 < nk) load_tile((kt + 1) * BK);
+    if (p.prio) __builtin_amdgcn_s_setprio(1);
     i32x8 a[4], b[J];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -235,6 +250,7 @@ __global__ __launch_bounds__(NT, 2) void igemm_fp8_kernel(Fp8Params p) {
       for (int j = 0; j < J; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, E8M0_ONE, 0,
                                                                      E8M0_ONE);
+    if (p.prio) __builtin_amdgcn_s_setprio(0);
     if (kt + 1 < nk) {
       __syncthreads();  // single LDS stage: everyone is done reading it
       store_tile();
@@ -500,6 +516,7 @@ void conv2d_nhwc_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, 
   check_align(scale, 16, "scale");
   check_align(bias, 16, "bias");
   Fp8Params p{};
+  p.prio = fp8_prio();
   p.x = reinterpret_cast<const uint8_t*>(x);
   p.w = reinterpret_cast<const uint8_t*>(w);
   p.scale = reinterpret_cast<const float*>(scale);
@@ -533,6 +550,7 @@ void gemm_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr
   check_align(scale, 16, "scale");
   check_align(bias, 16, "bias");
   Fp8Params p{};
+  p.prio = fp8_prio();
   p.x = reinterpret_cast<const uint8_t*>(x);
   p.w = reinterpret_cast<const uint8_t*>(w);
   p.scale = reinterpret_cast<const float*>(scale);
