@@ -37,6 +37,57 @@ METRIC_BERT = "records/sec (whole node) + p50 per-record latency, BERT-base text
 METRIC_INCEPTION = "records/sec (whole node) + p50 per-record latency, Inception-v3 fp8 image stream"
 
 
+def self_launch(args) -> int | None:
+    """``--gpus N`` (N > 1) outside a launcher: start N ranks ourselves, one per GPU.
+
+    The reference's data parallelism is operator parallelism — every subtask opens its own
+    model (``inception.scala:21-22``, ``DefaultSavedModelLoader.scala:40-56``); here a
+    subtask is a process bound to one GPU.  This parent never touches HIP (only
+    ``torch.cuda.device_count()``, which does not initialise the runtime on ROCm): it
+    checks that N GPUs are visible, runs ``torch.distributed.run`` as a CHILD process with
+    the same arguments (the ranks then see WORLD_SIZE and take the normal path, exactly as
+    under the driver's own torchrun) and exits with the child's status; rank 0's JSON line
+    reaches our stdout unchanged.  Returns None when no launch is needed."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import socket
+    import subprocess
+
+    if not args.rehearse_fake_comm:
+        import torch
+
+        n = torch.cuda.device_count()
+        if n < args.gpus:
+            print(f"[bench] --gpus {args.gpus} but {n} GPU(s) visible: refusing (no silent fallback to fewer "
+                  "ranks)", file=sys.stderr)
+            return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    return subprocess.call(cmd, env=env)
+
+
+def run_launch_check(args, comm, rank, ws):
+    """Rendezvous + one object exchange; rank 0 prints the world every rank reported."""
+    import torch
+
+    seen = comm.all_gather_object({"rank": rank, "world": ws, "pid": os.getpid(),
+                                   "local_rank": int(os.environ.get("LOCAL_RANK", 0)),
+                                   "gpus_visible": torch.cuda.device_count()})
+    comm.barrier()
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": args.gpus, "world_size": ws,
+                          "comm_world_size": comm.rank_size()[1], "ranks": [s["rank"] for s in seen],
+                          "pids_distinct": len({s["pid"] for s in seen}) == ws,
+                          "communicator": type(comm.get()).__name__ if comm.is_dist() else None}), flush=True)
+    comm.destroy()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -76,7 +127,14 @@ def main():
     ap.add_argument("--lanes", type=int, default=None,
                     help="compute lanes: independent plan instances on their own HIP streams, batches round-robin "
                          "(default: 3 for bert, 2 otherwise; measured in profiles/r01_lanes)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, rendezvous, exchange one object per rank and print the world the "
+                         "communicator sees (no model; with --rehearse-fake-comm it runs on a CPU-only box)")
     args = ap.parse_args()
+
+    rc = self_launch(args)
+    if rc is not None:
+        raise SystemExit(rc)
 
     import torch
 
@@ -95,11 +153,16 @@ def main():
     else:
         comm.init_distributed()
     rank, ws, local = comm.world()
-    if ws != args.gpus:
-        if rank == 0:
-            print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={ws}; using WORLD_SIZE", file=sys.stderr)
+    if ws != args.gpus:  # never report a different world than the one asked for
+        raise SystemExit(f"[bench] --gpus {args.gpus} but WORLD_SIZE={ws}: refusing to measure another world size")
+    if comm.rank_size()[1] != ws:
+        raise SystemExit(f"[bench] communicator holds {comm.rank_size()[1]} ranks, WORLD_SIZE={ws}")
+    if args.launch_check:
+        return run_launch_check(args, comm, rank, ws)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
+    if not args.rehearse_fake_comm and comm.gpu_count() < ws:
+        raise SystemExit(f"[bench] WORLD_SIZE={ws} but only {comm.gpu_count()} GPU(s) visible to rank {rank}")
     dev = torch.device("cuda", comm.local_device(local))
     torch.cuda.set_device(dev)
     numa = comm.bind_to_gpu_numa(dev) if ws > 1 else None  # DP ranks stage records on their GPU's socket
@@ -216,7 +279,12 @@ def main():
     params = list({t.data_ptr(): t for t in params}.values())  # interned / shared: each storage once
     # rank 0's weights to all ranks over RCCL (one flattened buffer per dtype); in place,
     # so the captured hipGraphs stay valid
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    tb = time.perf_counter()
     nbytes = comm.broadcast_tensors(params, src=0)
+    torch.cuda.synchronize(dev)
+    bcast_s = time.perf_counter() - tb
     compile_s = time.perf_counter() - t0
 
     records = [pool[i] for i in range(args.pool)]
@@ -276,6 +344,7 @@ def main():
     n_rec = n_sub if args.dynamic else B * args.steps
     per_gpu = n_rec / elapsed
     total = comm.all_reduce_scalar(float(n_rec), "sum", device=dev) / elapsed_max
+    per_rank = comm.all_gather_object(round(per_gpu, 1))
     flops = flops_per_record * total
     if rank == 0:
         out = {
@@ -300,9 +369,12 @@ def main():
             "p50_latency_ms": round(node_lat["p50"] * 1e3, 3),
             "p99_latency_ms": round(node_lat["p99"] * 1e3, 3),
             "per_gpu_records_per_s": round(per_gpu, 1),
+            "per_rank_records_per_s": per_rank,
+            "comm_world_size": comm.rank_size()[1],
             "model_tflops_per_s": round(flops / 1e12, 1),
             "compile_s": round(compile_s, 2),
             "weights_broadcast_bytes": nbytes,
+            "weights_broadcast_s": round(bcast_s, 4),
             "plan": plan.summary() if hasattr(plan, "summary") else {"hip_graph": plan.graph is not None},
             "arena": arena.stats() if args.model not in ("bert",) else None,
             "numa_binding_rank0": numa,

@@ -71,3 +71,36 @@ def _silent_exit(rank, world, attempt):
 def test_clean_exit_without_result_is_a_failure():
     with pytest.raises(WorkerFailure, match="without a result"):
         launch(_silent_exit, 2, communicator=FakeCommunicator, max_restarts=0, timeout=60)
+
+
+# ---------------------------------------------------------------- bench.py self-launch
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*argv, timeout=240):
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *argv], capture_output=True,
+                          text=True, timeout=timeout, env=env, cwd=ROOT)
+
+
+def test_bench_spawns_its_own_ranks():
+    """``python bench.py --gpus 2`` outside any launcher starts 2 rank processes itself
+    (torch.distributed.run as a child), they rendezvous and rank 0 prints the world."""
+    p = _bench("--gpus", "2", "--rehearse-fake-comm", "--launch-check")
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["world_size"] == 2 and out["comm_world_size"] == 2
+    assert out["ranks"] == [0, 1] and out["pids_distinct"]
+
+
+def test_bench_refuses_missing_gpus():
+    """Asking for more GPUs than are visible fails loudly instead of measuring fewer."""
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("box has 2+ GPUs")
+    p = _bench("--gpus", "2", timeout=120)
+    assert p.returncode != 0
+    assert "refusing" in p.stderr
