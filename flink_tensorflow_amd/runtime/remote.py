@@ -41,7 +41,6 @@ import traceback
 import uuid
 
 import collections
-import sys
 import weakref
 
 import cloudpickle
@@ -167,17 +166,21 @@ class TensorSlab:
         _, start, pos, end, shape, dtype, _kind, _tvd = ref
         o = self.HDR + pos % self.cap
         dt = np.dtype(dtype)
-        n = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
-        arr = self.mem[o:o + n].view(dt).reshape(shape)
+        n = int(np.prod(shape, dtype=np.int64))
+        # the record's OWN base array: its base is a memoryview (not another ndarray), so
+        # every view derived from the record (reshape, slices, .view(dtype)) collapses onto
+        # it and keeps it alive — the release below cannot fire while any view survives
+        base = np.frombuffer(memoryview(self._mm)[o:o + n * dt.itemsize], dt, n)
         with self._lock:
             self._pending.append((start, end))
         if track:
-            self.track(arr, start)
-        return arr
+            self.track(base, start)
+        return base.reshape(shape)
 
-    def track(self, arr, start: int) -> None:
-        """Releases the record's space when ``arr`` (and every view of it) is collected."""
-        weakref.finalize(arr, self._drop, start)
+    def track(self, base, start: int) -> None:
+        """Releases the record's space when ``base`` (and therefore every view of it) is
+        collected.  ``base`` must be the array returned by ``np.frombuffer`` in ``view``."""
+        weakref.finalize(base, self._drop, start)
 
     def _drop(self, start):
         with self._lock:
@@ -369,16 +372,11 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
             if kind == "recs":
                 for value, ts, idx in msg[1]:
                     if slab is not None and _is_ref(value) and value[6] == "np":
-                        # plain ndarray records: if the operator kept no reference once
-                        # process() returns (maps, batch staging copies), release at once;
-                        # otherwise (windows, pending micro-batches) when it is collected
-                        v = slab.view(value, track=False)
-                        op.process(Record(v, ts), idx)
-                        if sys.getrefcount(v) <= 2:
-                            slab._drop(value[1])
-                        else:
-                            slab.track(v, value[1])
-                        del v
+                        # plain ndarray records: released when the last view of the record
+                        # is collected — at once when the operator kept nothing (maps, batch
+                        # staging copies), later when it kept the record or any view derived
+                        # from it (windows, keyed state, pending micro-batches)
+                        op.process(Record(slab.view(value), ts), idx)
                     else:
                         op.process(Record(_from_slab(value, slab) if slab is not None else value, ts), idx)
                     metrics.inc("records_in")
@@ -462,7 +460,7 @@ class RemoteOperatorProxy:
         tag = f"/ftm-{os.getpid()}-{uuid.uuid4().hex[:10]}"
         self.to_worker = ShmChannel(tag + "-in", True, self.ring_bytes)
         self.from_worker = ShmChannel(tag + "-out", True, self.ring_bytes)
-        self.slab = TensorSlab(tag + "-slab", True) if _SLAB_BYTES > 0 else None
+        self.slab = TensorSlab(tag + "-slab", True, _SLAB_BYTES) if _SLAB_BYTES > 0 else None
         self.proc = mp.get_context("spawn").Process(target=_worker_main, name=f"ftm-{self.node.name}-{self.subtask}",
                                                     args=(self.to_worker.name, self.from_worker.name,
                                                           self.slab.name if self.slab else None), daemon=True)

@@ -221,3 +221,37 @@ def test_tensor_slab_full_falls_back_to_pickle(monkeypatch):
     env = StreamExecutionEnvironment.get_execution_environment()
     got = env.from_collection(vals).count_window_all(40).apply(_WinSum()).run_in_processes().execute_and_collect()
     assert got == [sum(int(v.astype(np.int64).sum()) for v in vals)]
+
+
+class _KeepDerived:
+    """Keeps only DERIVED views of every record (``reshape(-1)``, a column slice) and,
+    every 25th record, returns the checksum over everything kept so far."""
+
+    def __init__(self):
+        self.kept = []
+
+    def __call__(self, v):
+        self.kept.append(v.reshape(-1))
+        self.kept.append(v[:, 0])
+        if len(self.kept) % 50:
+            return None
+        return int(sum(int(k.astype("int64").sum()) for k in self.kept))
+
+
+def test_tensor_slab_keeps_records_alive_through_derived_views(monkeypatch):
+    """An operator that stores only views derived from slab records (not the records
+    themselves) must still see their bytes intact after later batches wrap the slab."""
+    import numpy as np
+
+    from flink_tensorflow_amd.runtime import remote
+
+    monkeypatch.setattr(remote, "_SLAB_BYTES", 4 << 20)
+    rng = np.random.default_rng(2)
+    vals = [rng.integers(0, 256, (64, 64, 4), dtype=np.uint8) for _ in range(400)]  # 16 KB: 6.4 MB in all
+    want, acc = [], 0
+    for i, v in enumerate(vals):
+        acc += int(v.astype(np.int64).sum()) + int(v[:, 0].astype(np.int64).sum())
+        want.append(acc if (i + 1) % 25 == 0 else None)
+    env = StreamExecutionEnvironment.get_execution_environment()
+    got = env.from_collection(vals).map(_KeepDerived()).run_in_processes().execute_and_collect()
+    assert got == want
