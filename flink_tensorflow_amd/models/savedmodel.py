@@ -98,21 +98,111 @@ def asset_file_defs(mg: MetaGraphDef) -> list[AssetFileDef]:
     return out
 
 
-def _allocate_variables(sess: Session, var_prefix: str) -> bool:
-    """Every variable of the bundle allocated (uninitialised) on the session's device from
-    the index alone — no tensor data read.  False when a variable cannot be received by a
-    broadcast (STRING), in which case the caller restores normally."""
+def restore_targets(g: Graph, restore_op: str) -> dict[str, tuple[str, str]] | None:
+    """``{variable node: (checkpoint key, shape_and_slice)}`` as the SaverDef's restore op
+    assigns them: the ``Assign`` nodes reachable from ``restore_op`` through control
+    dependencies whose value is output ``i`` of a ``RestoreV2``, keyed by that op's constant
+    ``tensor_names[i]``.  None when the restore subgraph has another shape (then a rank
+    cannot know what rank 0's restore would produce without running it)."""
+    from ..graph.tensor_proto import tensor_from_proto
+
+    def const_strs(name):
+        n = g.nodes.get(name)
+        if n is None or n.op != "Const":
+            return None
+        t = tensor_from_proto(n.tensor_attr("value"))
+        arr = getattr(t, "array", None)
+        return None if arr is None else [bytes(v).decode() for v in arr.reshape(-1)]
+
+    out, seen, stack = {}, set(), [restore_op.split(":")[0]]
+    while stack:
+        name = stack.pop()
+        if name in seen or name not in g.nodes:
+            continue
+        seen.add(name)
+        n = g.nodes[name]
+        if n.op in ("Assign", "AssignVariableOp") and len(n.inputs) >= 2:
+            var, (src, idx) = n.inputs[0][0], n.inputs[1]
+            vn = g.nodes.get(var)
+            var = (vn.attr("shared_name") or var) if vn is not None else var  # the session's key
+            while g.nodes.get(src) is not None and g.nodes[src].op == "Identity":
+                src, idx = g.nodes[src].inputs[0]
+            r = g.nodes.get(src)
+            if r is None or r.op != "RestoreV2" or len(r.inputs) < 3:
+                return None
+            keys, slices = const_strs(r.inputs[1][0]), const_strs(r.inputs[2][0])
+            if keys is None or slices is None or idx >= len(keys):
+                return None
+            out[var] = (keys[idx], slices[idx])
+        stack.extend(n.control_inputs)
+        stack.extend(i for i, _ in n.inputs if g.nodes.get(i) is not None and g.nodes[i].op in ("NoOp",))
+    return out or None
+
+
+def _allocate_variables(sess: Session, var_prefix: str, restore_op: str) -> bool:
+    """Every variable the SaverDef's restore op would assign, allocated (uninitialised) on
+    the session's device under the SAME variable-node name rank 0's restore gives it, with
+    the shape of its checkpoint entry — no tensor data read.  False when that mapping
+    cannot be derived or a variable cannot be received by a broadcast (STRING, sliced
+    partitions): the caller then restores normally."""
     from ..io import bundle
     from ..types.dtypes import DataType
 
+    targets = restore_targets(sess.graph, restore_op)
+    if targets is None:
+        return False
     with bundle.BundleReader(var_prefix) as r:
-        specs = {k: r.dtype_and_shape(k) for k in r.keys()}
+        specs = {}
+        for var, (key, slc) in targets.items():
+            if slc or key not in r:
+                return False
+            specs[var] = r.dtype_and_shape(key)
     if any(dt == DataType.STRING for dt, _ in specs.values()):
         return False
     dev = sess.device
-    for k, (dt, shape) in specs.items():
-        sess.variables[k] = torch.empty(shape, dtype=dt.torch, device=dev)
+    for var, (dt, shape) in specs.items():
+        sess.variables[var] = torch.empty(shape, dtype=dt.torch, device=dev)
     return True
+
+
+def _hashable(v):
+    """Option values as a cache key: lists/dicts (YAML, ``config.to_dict()``) -> tuples."""
+    if isinstance(v, (list, tuple)):
+        return tuple(_hashable(x) for x in v)
+    if isinstance(v, dict):
+        return tuple(sorted((k, _hashable(x)) for k, x in v.items()))
+    try:
+        hash(v)
+        return v
+    except TypeError:
+        return repr(v)
+
+
+def _link_bundle(src: str, dst: str) -> bool:
+    """Hard-links (or copies, across filesystems) bundle ``src``'s index + data files to
+    prefix ``dst``; False when ``src`` is gone."""
+    import glob
+    import shutil
+
+    files = glob.glob(glob.escape(src) + ".data-*") + [src + ".index"]
+    if not all(os.path.exists(f) for f in files):
+        return False
+    os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
+    for f in files:
+        out = dst + f[len(src):]
+        if os.path.exists(out):
+            os.remove(out)
+        try:
+            os.link(f, out)
+        except OSError:
+            shutil.copyfile(f, out)
+    return True
+
+
+def variables_signature(sess: Session) -> list[tuple[str, tuple, str]]:
+    """(name, shape, dtype) of every tensor variable, sorted: what a weight broadcast sends."""
+    vs = sess.variables
+    return [(k, tuple(vs[k].shape), str(vs[k].dtype)) for k in sorted(vs) if isinstance(vs[k], torch.Tensor)]
 
 
 def load_bundle(local_dir: str, tags: Sequence[str], device=None, read_variables: bool = True) -> SavedModelBundle:
@@ -125,7 +215,7 @@ def load_bundle(local_dir: str, tags: Sequence[str], device=None, read_variables
     var_prefix = os.path.join(local_dir, VARIABLES_DIRECTORY, VARIABLES_FILENAME)
     sd = mg.saver_def
     if sd is not None and sd.restore_op_name and os.path.exists(var_prefix + ".index"):
-        if read_variables or not _allocate_variables(sess, var_prefix):
+        if read_variables or not _allocate_variables(sess, var_prefix, sd.restore_op_name):
             sess.run(targets=[sd.restore_op_name.split(":")[0]],
                      feed_dict={sd.filename_tensor_name: StringTensor(var_prefix.encode())})
     asset_feeds = {}
@@ -173,7 +263,7 @@ class DefaultSavedModelLoader(SavedModelLoader):
 class TensorFlowModel(RichModel, CheckpointedModel):
     """A SavedModel-backed model.  Subclasses define ``loader``."""
 
-    _TRANSIENT = ("_bundle", "_functions")
+    _TRANSIENT = ("_bundle", "_functions", "_pristine_version", "_last_snapshot")
 
     def __init__(self, device=None, distributed_weights: bool = False):
         self.device = device
@@ -182,6 +272,11 @@ class TensorFlowModel(RichModel, CheckpointedModel):
         self.distributed_weights = distributed_weights
         self._bundle: SavedModelBundle | None = None
         self._pending_restore: str | None = None
+        # checkpoint bookkeeping: the variables' version while they still equal the
+        # SavedModel's (None once restored from a checkpoint), and (version, prefix) of the
+        # last bundle a snapshot wrote or a restore read
+        self._pristine_version: int | None = None
+        self._last_snapshot: tuple[int, str] | None = None
 
     @property
     @abc.abstractmethod
@@ -211,9 +306,18 @@ class TensorFlowModel(RichModel, CheckpointedModel):
             self._bundle = self.loader.load(device=dev)
         if dist:
             vs = self._bundle.session.variables
-            comm.broadcast_tensors([vs[k] for k in sorted(vs) if isinstance(vs[k], torch.Tensor)], src=0)
+            sig = variables_signature(self._bundle.session)
+            sigs = comm.all_gather_object(sig)  # every rank must broadcast the same list
+            bad = [r for r, other in enumerate(sigs) if other != sigs[0]]
+            if bad:
+                diff = sorted(set(map(repr, sigs[0])) ^ set(map(repr, sigs[bad[0]])))[:6]
+                raise RuntimeError(f"distributed_weights: ranks {bad} hold different variables than rank 0 "
+                                   f"(first differences: {diff}); refusing a mismatched broadcast")
+            comm.broadcast_tensors([vs[k] for k, _, _ in sig], src=0)
             if hasattr(vs, "touch"):
                 vs.touch()
+        self._pristine_version = self._var_version()
+        self._last_snapshot = None
         if self._pending_restore is not None:  # initialize_state ran before open()
             prefix, self._pending_restore = self._pending_restore, None
             self.restore_variables(prefix)
@@ -241,7 +345,7 @@ class TensorFlowModel(RichModel, CheckpointedModel):
         """The ``ModelFunction`` of ``signature`` (cached per signature / method type /
         options, so its compiled plans live as long as the open model).  ``options`` go to
         ``ModelFunction`` (``compile``, ``batch_buckets``, ``precision``, ``strict``)."""
-        key = (signature, type(method), tuple(sorted(options.items())))
+        key = (signature, type(method), tuple(sorted((k, _hashable(v)) for k, v in options.items())))
         fns = self.__dict__.get("_functions")
         if fns is None:  # first use, or a descriptor unpickled in a subtask (transient field)
             fns = self.__dict__["_functions"] = {}
@@ -269,13 +373,37 @@ class TensorFlowModel(RichModel, CheckpointedModel):
         from ..io.saver import VariableSaver
 
         VariableSaver().restore(self.session(), prefix)
+        self._pristine_version = None
+        self._last_snapshot = (self._var_version(), prefix)
+
+    def _var_version(self) -> int:
+        return getattr(self.session().variables, "version", 0)
 
     def snapshot_state(self, ctx) -> None:
+        """Writes the session variables into the checkpoint only when they changed.
+
+        The reference's ``TensorFlowModel`` takes no part in checkpoints; here it is a
+        ``CheckpointedModel`` so models trained or assigned in a stream survive restarts.
+        A read-only inference model must not pay a D2H copy + bundle write of all its
+        weights at every barrier, so: variables still equal to the SavedModel's -> nothing
+        is written (a restore then keeps the freshly loaded values); unchanged since the
+        last written / restored bundle -> that bundle's files are hard-linked into this
+        checkpoint (no copy; it stays valid when the old checkpoint is pruned); changed ->
+        written."""
         from ..runtime.model_functions import model_state_dir
 
         d = model_state_dir(ctx, STATE_NAME)
-        if d is not None and self.is_open and self.session().variables:
-            self.save_variables(os.path.join(d, "variables"))
+        if d is None or not self.is_open or not self.session().variables:
+            return
+        v = self._var_version()
+        if v == self._pristine_version:
+            return
+        prefix = os.path.join(d, "variables")
+        last = self._last_snapshot
+        if last is not None and last[0] == v and _link_bundle(last[1], prefix):
+            return
+        self.save_variables(prefix)
+        self._last_snapshot = (v, prefix)
 
     def initialize_state(self, ctx) -> None:
         if not ctx.is_restored() or ctx.checkpoint_dir is None:

@@ -40,9 +40,13 @@ def group_keys(keys: torch.Tensor, num_rows: int):
     n = keys.numel()
     dev = keys.device
     H = _hip()
+    if num_rows >= (1 << 30):
+        raise ValueError(f"group_keys: tables of 2^30 rows or more are not supported (got {num_rows})")
     flat = keys.reshape(-1)
     if flat.dtype != torch.int32:
-        flat = flat.to(torch.int32)
+        # out-of-range wide ids go to the dropped bucket BEFORE narrowing: an int64 id at or
+        # above 2^31 must not wrap into [0, num_rows) and update a valid row
+        flat = torch.where((flat >= 0) & (flat < num_rows), flat, num_rows).to(torch.int32)
     flat = flat.contiguous()
     i32 = dict(dtype=torch.int32, device=dev)
     sorted_k, perm, seg_id, uids = (torch.empty(n, **i32) for _ in range(4))

@@ -277,3 +277,60 @@ def test_savedmodel_variables_read_by_rank0_and_broadcast(half_plus_two, tmp_pat
     assert out[0] == [2.5, 0.5] and out[1] == [2.5, 0.5], out
     ctrl = _run(functools.partial(_savedmodel_rank0_broadcast, [half_plus_two, other], False))
     assert ctrl[1] == [5.0, 3.0], ctrl  # without it, rank 1 serves its own copy
+
+
+def test_restore_targets_map_variables_to_checkpoint_keys(half_plus_two):
+    """A receiving rank allocates exactly the variables rank 0's SaverDef restore assigns,
+    under the same names (not the raw index keys)."""
+    from flink_tensorflow_amd.graph.graph import Graph
+    from flink_tensorflow_amd.models.savedmodel import read_saved_model, restore_targets, select_meta_graph
+
+    mg = select_meta_graph(read_saved_model(half_plus_two), ["serve"])
+    t = restore_targets(Graph.from_graph_def(mg.graph_def), mg.saver_def.restore_op_name)
+    assert t == {"a": ("a", ""), "b": ("b", ""), "c": ("c", "")}
+
+
+class _ExtraVarLoader:
+    """Loads half_plus_two; on rank 1 the session gains a variable rank 0 does not have."""
+
+    def __init__(self, path):
+        from flink_tensorflow_amd.models.savedmodel import DefaultSavedModelLoader
+
+        self.inner = DefaultSavedModelLoader(path)
+
+    @property
+    def metagraph(self):
+        return self.inner.metagraph
+
+    def load(self, device=None, read_variables=True):
+        import torch
+
+        from flink_tensorflow_amd.parallel import comm
+
+        b = self.inner.load(device=device, read_variables=read_variables)
+        if comm.rank_size()[0] == 1:
+            b.session.variables["extra"] = torch.zeros(2)
+        return b
+
+
+def _mismatched_open(path, rank, world):
+    from flink_tensorflow_amd.models.savedmodel import TensorFlowModel
+
+    class M(TensorFlowModel):
+        loader = _ExtraVarLoader(path)
+
+    m = M(device="cpu", distributed_weights=True)
+    try:
+        m.open()
+    except RuntimeError as e:
+        return "refused" if "refusing a mismatched broadcast" in str(e) else f"other: {e}"
+    return "opened"
+
+
+def test_distributed_weights_refuse_mismatched_variable_sets(half_plus_two):
+    """Ranks whose sessions hold different variable lists raise before any broadcast
+    (instead of issuing mismatched RCCL broadcasts that hang or corrupt)."""
+    import functools
+
+    out = _run(functools.partial(_mismatched_open, half_plus_two))
+    assert out == {0: "refused", 1: "refused"}, out

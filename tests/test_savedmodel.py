@@ -230,3 +230,51 @@ def test_asset_init_op_ran(model):
 
 def teardown_module(module):
     shutil.rmtree("/tmp/ftm-none", ignore_errors=True)
+
+
+def test_snapshot_writes_variables_only_when_changed(half_plus_two, tmp_path):
+    """A read-only model writes nothing at a checkpoint; a changed one writes its bundle;
+    an unchanged-since-last-bundle one hard-links that bundle (no D2H, no rewrite)."""
+    import os
+    from types import SimpleNamespace
+
+    import torch
+
+    from flink_tensorflow_amd.models import SavedModelModel
+
+    m = SavedModelModel(half_plus_two, device="cpu")
+    m.open()
+
+    def snap(i):
+        ctx = SimpleNamespace(checkpoint_dir=str(tmp_path / f"chk-{i}"), subtask_index=0)
+        m.snapshot_state(ctx)
+        return str(tmp_path / f"chk-{i}" / "models")
+
+    d1 = snap(1)
+    assert not any(f.startswith("variables") for _, _, fs in os.walk(d1) for f in fs)  # pristine: nothing
+    m.session().run(targets=["a/Assign"], feed_dict={"a/initial_value:0": torch.tensor(3.0)})
+    d2 = snap(2)
+    idx2 = [os.path.join(r, f) for r, _, fs in os.walk(d2) for f in fs if f.endswith(".index")]
+    assert len(idx2) == 1
+    d3 = snap(3)
+    idx3 = [os.path.join(r, f) for r, _, fs in os.walk(d3) for f in fs if f.endswith(".index")]
+    assert len(idx3) == 1 and os.path.samefile(idx2[0], idx3[0])  # linked, not rewritten
+    # a restore from the linked bundle gives the changed value
+    m2 = SavedModelModel(half_plus_two, device="cpu")
+    m2.open()
+    m2.restore_variables(idx3[0][: -len(".index")])
+    assert float(m2.session().variables["a"]) == 3.0
+    m.close()
+    m2.close()
+
+
+def test_function_cache_accepts_unhashable_options(half_plus_two):
+    """``batch_buckets`` as a list (what YAML / ``config.to_dict()`` produce) still caches."""
+    from flink_tensorflow_amd.models import PredictMethod, SavedModelModel
+
+    m = SavedModelModel(half_plus_two, device="cpu")
+    m.open()
+    f1 = m.function("serving_default", PredictMethod(), batch_buckets=[1, 4])
+    f2 = m.function("serving_default", PredictMethod(), batch_buckets=[1, 4])
+    assert f1 is f2
+    m.close()

@@ -290,3 +290,14 @@ def test_fused_step_checkpoint_roundtrip_gpu(tmp_path):
     for (k, va), vb in zip(a.model.state_dict().items(), r.model.state_dict().values()):
         torch.testing.assert_close(vb, va, rtol=1e-5, atol=1e-6, msg=k)
     assert r.steps == a.steps == 6  # the step counter came back too
+
+
+@pytest.mark.gpu
+def test_group_keys_int64_out_of_range_ids_are_dropped_gpu():
+    """int64 ids at or above 2^31 (or negative) land in the dropped bucket; before the fix
+    they wrapped on the int32 cast and could alias valid rows."""
+    dev = torch.device("cuda", 0)
+    keys = torch.tensor([5, (1 << 32) + 5, 7, -(1 << 33) + 7, 5, (1 << 31)], dtype=torch.int64, device=dev)
+    perm, seg_id, seg, uids = E.group_keys(keys, 100)
+    assert uids[:3].cpu().tolist() == [5, 7, -1]  # runs: 5 (x2), 7 (x1), dropped (x3)
+    assert perm[:3].cpu().tolist() == [0, 4, 2]
