@@ -20,6 +20,7 @@ void register_conv_pp(pybind11::module_& m);
 void register_widedeep(pybind11::module_& m);
 void register_sort_segments(pybind11::module_& m);
 void register_pw_res(pybind11::module_& m);
+void register_gemm_train(pybind11::module_& m);
 
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "flink_tensorflow_amd CDNA4 (gfx950) kernels";
@@ -40,4 +41,5 @@ PYBIND11_MODULE(_hip, m) {
   register_widedeep(m);
   register_sort_segments(m);
   register_pw_res(m);
+  register_gemm_train(m);
 }

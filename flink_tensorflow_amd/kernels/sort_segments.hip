@@ -1,18 +1,23 @@
 // Static-shape key grouping for the row-sparse gradient pipeline (ops/embedding.py):
-// keys -> (stable order, run boundaries, unique keys) in five launches, no host sync.
+// keys -> (stable order, run boundaries, unique keys), no host sync, no library kernels.
 //
-//   prep      key' = key in [0, num_rows) ? key : num_rows (one bucket for invalid ids),
-//             iota, seg[] = n, uids[] = -1
-//   radix     hipcub::DeviceRadixSort::SortPairs over ceil(log2(num_rows + 1)) bits only
-//             (stable LSD radix: the same order as a stable comparison sort)
-//   flags     first[i] = sorted[i] != sorted[i - 1]
-//   scan      hipcub::DeviceScan::InclusiveSum -> run index + 1 of every sorted position
-//   starts    seg[run] = i, uids[run] = key (or -1 for the invalid bucket) at run starts
+// In-tree LSD radix sort over the key bits in use (ceil(log2(num_rows + 1)), 8-bit digits:
+// 3 passes for the 3.6M-row Wide&Deep key space), 2048-key tiles of 256 threads:
 //
-// Replaces a chain of ~25 framework kernels per table (where/compare/fill/sort merge passes,
-// cumsum, dtype copies).  Temp storage and buffers are caller-allocated (stream-ordered
-// allocator; inside hipGraph capture they come from the graph's pool).
-#include <hipcub/hipcub.hpp>
+//   count0    per-tile digit counts of pass 0 (keys clamped: ids outside [0, num_rows) form
+//             one bucket, num_rows); zeroes the later passes' counters; seg[] = n, uids[] = -1
+//   scatter   per pass: every tile derives its digit offsets itself from the pass's
+//             [digit][tile] counts (its predecessors' counts + the global digit totals: 256
+//             threads x ntiles L2 reads, no scan launch), ranks its keys stably (per wave,
+//             64-key rounds in tile order: lanes with the same digit found by 9 ballots, the
+//             leader advances the wave's LDS digit counter), scatters (key, index) and counts
+//             the NEXT pass's digits of what landed in each destination tile (global atomics
+//             on integer counters: order-independent, so the result stays deterministic)
+//   runs      count of run starts per tile, then run index (tile prefix + block scan), run
+//             starts and run keys (-1 for the invalid bucket)
+//
+// Stable: equal keys keep their input order (same result as a stable comparison sort), so
+// every reduce-by-key downstream sums in a fixed order.  6 launches for 3 passes.
 #include <pybind11/pybind11.h>
 
 #include <stdexcept>
@@ -21,39 +26,11 @@
 
 namespace {
 
-__global__ __launch_bounds__(256) void seg_prep_kernel(const int* __restrict__ keys, int* __restrict__ kq,
-                                                       int* __restrict__ iota, int* __restrict__ seg,
-                                                       int* __restrict__ uids, int n, int num_rows) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) {
-    const int k = keys[i];
-    kq[i] = (k >= 0 && k < num_rows) ? k : num_rows;
-    iota[i] = i;
-    uids[i] = -1;
-  }
-  if (i <= n) seg[i] = n;
-}
-
-__global__ __launch_bounds__(256) void seg_flags_kernel(const int* __restrict__ sorted, int* __restrict__ first,
-                                                        int n) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) first[i] = (i == 0 || sorted[i] != sorted[i - 1]) ? 1 : 0;
-}
-
-// run index r = incl[i] - 1; the first position of each run writes its start and key
-__global__ __launch_bounds__(256) void seg_starts_kernel(const int* __restrict__ sorted, const int* __restrict__ incl,
-                                                         int* __restrict__ seg_id, int* __restrict__ seg,
-                                                         int* __restrict__ uids, int n, int num_rows) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const int r = incl[i] - 1;
-  seg_id[i] = r;
-  const int k = sorted[i];
-  if (i == 0 || sorted[i - 1] != k) {
-    seg[r] = i;
-    uids[r] = k >= num_rows ? -1 : k;
-  }
-}
+constexpr int RT = 256;             // threads per tile
+constexpr int KPT = 8;              // keys per thread
+constexpr int TILE = RT * KPT;      // 2048 keys: wave w, round r, lane l -> key w*512 + r*64 + l
+constexpr int RADIX = 256;
+constexpr int MAXP = 4;             // num_rows < 2^30 -> at most 4 passes of 8 bits
 
 int key_bits(int num_rows) {
   int b = 1;
@@ -61,15 +38,196 @@ int key_bits(int num_rows) {
   return b;
 }
 
+FTM_DEVICE int clamp_key(int k, int num_rows) { return (k >= 0 && k < num_rows) ? k : num_rows; }
+
+__global__ __launch_bounds__(RT) void rs_count0_kernel(const int* __restrict__ keys, int n, int num_rows,
+                                                       int* __restrict__ hist0, int* __restrict__ hist_rest,
+                                                       int rest_len, int* __restrict__ seg, int* __restrict__ uids,
+                                                       int ntiles) {
+  __shared__ int cnt[RADIX];
+  const int t = blockIdx.x;
+  cnt[threadIdx.x] = 0;
+  // grid-stride init of the later passes' counters and of the run outputs
+  for (int i = t * RT + threadIdx.x; i < rest_len; i += ntiles * RT) hist_rest[i] = 0;
+  for (int i = t * RT + threadIdx.x; i <= n; i += ntiles * RT) {
+    seg[i] = n;
+    if (i < n) uids[i] = -1;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const int i = t * TILE + j * RT + threadIdx.x;
+    if (i < n) atomicAdd(&cnt[clamp_key(keys[i], num_rows) & (RADIX - 1)], 1);
+  }
+  __syncthreads();
+  hist0[threadIdx.x * ntiles + t] = cnt[threadIdx.x];
+}
+
+// One radix pass.  vin == nullptr: values are the input indices (first pass; keys clamped).
+__global__ __launch_bounds__(RT) void rs_scatter_kernel(const int* __restrict__ kin, const int* __restrict__ vin,
+                                                        int* __restrict__ kout, int* __restrict__ vout, int n,
+                                                        int num_rows, int shift, const int* __restrict__ hist,
+                                                        int* __restrict__ hist_next, int shift_next, int ntiles) {
+  __shared__ int goff[RADIX];
+  __shared__ int tot[RADIX];
+  __shared__ int wcnt[4][RADIX + 1];  // per-wave digit counters (+1: the out-of-range slot)
+  const int t = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  {  // this tile's offset for every digit: digits below it everywhere + this digit in earlier tiles
+    const int d = threadIdx.x;
+    int total = 0, pre = 0;
+    for (int u = 0; u < ntiles; ++u) {
+      const int c = hist[d * ntiles + u];
+      total += c;
+      pre += u < t ? c : 0;
+    }
+    tot[d] = total;
+    goff[d] = pre;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) wcnt[ww][d] = 0;
+    if (d < 4) wcnt[d][RADIX] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {  // exclusive scan of the 256 digit totals by wave 0 (4 per lane)
+    int v[4], s = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = s;
+      s += tot[lane * 4 + e];
+    }
+    int incl = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    const int base = incl - s;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) goff[lane * 4 + e] += base + v[e];
+  }
+  // stable ranks: wave w owns tile keys [w*512, w*512 + 512) in 8 rounds of 64
+  int key[KPT], val[KPT], dig[KPT], rank[KPT];
+  const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int r = 0; r < KPT; ++r) {
+    const int i = t * TILE + w * 512 + r * 64 + lane;
+    const bool ok = i < n;
+    int k = ok ? kin[i] : 0;
+    if (!vin) k = clamp_key(k, num_rows);
+    key[r] = k;
+    val[r] = ok ? (vin ? vin[i] : i) : 0;
+    const int d = ok ? ((k >> shift) & (RADIX - 1)) : RADIX;  // 9-bit digit: RADIX = not a key
+    dig[r] = d;
+    unsigned long long m = ~0ull;
+#pragma unroll
+    for (int b = 0; b < 9; ++b) {
+      const unsigned long long bal = __ballot((d >> b) & 1);
+      m &= ((d >> b) & 1) ? bal : ~bal;
+    }
+    const int leader = __ffsll((long long)m) - 1;
+    int old = 0;
+    if (lane == leader) {
+      old = wcnt[w][d];
+      wcnt[w][d] = old + __popcll(m);
+    }
+    old = __shfl(old, leader, 64);
+    rank[r] = old + __popcll(m & lt);
+  }
+  __syncthreads();
+  {  // exclusive prefix over waves per digit
+    const int d = threadIdx.x;
+    int s = 0;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const int c = wcnt[ww][d];
+      wcnt[ww][d] = s;
+      s += c;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < KPT; ++r) {
+    const int d = dig[r];
+    if (d == RADIX) continue;
+    const int pos = goff[d] + wcnt[w][d] + rank[r];
+    kout[pos] = key[r];
+    vout[pos] = val[r];
+    if (hist_next) atomicAdd(&hist_next[((key[r] >> shift_next) & (RADIX - 1)) * ntiles + pos / TILE], 1);
+  }
+}
+
+// number of run starts (sorted[i] != sorted[i - 1]) per tile
+__global__ __launch_bounds__(RT) void rs_runs_count_kernel(const int* __restrict__ s, int n, int* __restrict__ tcount) {
+  __shared__ int red[RT / 64];
+  const int t = blockIdx.x;
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const int i = t * TILE + threadIdx.x * KPT + j;
+    if (i < n) c += (i == 0 || s[i] != s[i - 1]) ? 1 : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) tcount[t] = red[0] + red[1] + red[2] + red[3];
+}
+
+// run index of every sorted position (earlier tiles' runs + block scan), run starts, run keys
+__global__ __launch_bounds__(RT) void rs_runs_write_kernel(const int* __restrict__ s, int n, int num_rows,
+                                                           const int* __restrict__ tcount, int* __restrict__ seg_id,
+                                                           int* __restrict__ seg, int* __restrict__ uids) {
+  __shared__ int wsum[RT / 64];
+  __shared__ int base_s;
+  const int t = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    int b = 0;
+    for (int u = 0; u < t; ++u) b += tcount[u];
+    base_s = b;
+  }
+  int f[KPT], c = 0;
+  const int i0 = t * TILE + threadIdx.x * KPT;
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const int i = i0 + j;
+    f[j] = (i < n && (i == 0 || s[i] != s[i - 1])) ? 1 : 0;
+    c += f[j];
+  }
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int before = base_s;
+  for (int ww = 0; ww < w; ++ww) before += wsum[ww];
+  int run = before + incl - c;  // runs started before this thread's first position
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const int i = i0 + j;
+    if (i >= n) break;
+    run += f[j];
+    const int r = run - 1;
+    seg_id[i] = r;
+    if (f[j]) {
+      const int k = s[i];
+      seg[r] = i;
+      uids[r] = k >= num_rows ? -1 : k;
+    }
+  }
+}
+
+int passes_for(int num_rows) { return (key_bits(num_rows) + 7) / 8; }
+
 }  // namespace
 
-// bytes of hipcub temp storage for n keys below num_rows + 1
+// bytes of scratch (digit counters of every pass + per-tile run counts) for n keys
 size_t sort_segments_temp_bytes(int n, int num_rows) {
-  size_t a = 0, b = 0;
-  hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const int*)nullptr, (int*)nullptr, (const int*)nullptr, (int*)nullptr,
-                                     n, 0, key_bits(num_rows));
-  hipcub::DeviceScan::InclusiveSum(nullptr, b, (const int*)nullptr, (int*)nullptr, n);
-  return (a > b ? a : b) + 256;
+  const size_t ntiles = (size_t)(n + TILE - 1) / TILE;
+  return (size_t)passes_for(num_rows) * RADIX * ntiles * 4 + ntiles * 4 + 256;
 }
 
 // keys int32 [n] -> sorted int32 [n], perm int32 [n] (stable), seg_id int32 [n],
@@ -81,24 +239,34 @@ void sort_segments(uintptr_t keys, int n, int num_rows, uintptr_t sorted, uintpt
   if (n <= 0) return;
   if (num_rows < 0 || num_rows >= (1 << 30)) throw std::invalid_argument("sort_segments: num_rows out of range");
   if (temp_bytes < sort_segments_temp_bytes(n, num_rows)) throw std::invalid_argument("sort_segments: temp too small");
+  if (temp % 4) throw std::invalid_argument("sort_segments: temp alignment");
   auto s = reinterpret_cast<hipStream_t>(stream);
-  int* kq = reinterpret_cast<int*>(work);
-  int* iota = kq + n;
-  int* tmp = iota + n;
-  const dim3 grid((n + 256) / 256), block(256);
-  hipLaunchKernelGGL(seg_prep_kernel, grid, block, 0, s, reinterpret_cast<const int*>(keys), kq, iota,
-                     reinterpret_cast<int*>(seg), reinterpret_cast<int*>(uids), n, num_rows);
-  size_t tb = temp_bytes;
-  if (hipcub::DeviceRadixSort::SortPairs(reinterpret_cast<void*>(temp), tb, kq, reinterpret_cast<int*>(sorted), iota,
-                                         reinterpret_cast<int*>(perm), n, 0, key_bits(num_rows), s) != hipSuccess)
-    throw std::runtime_error("sort_segments: radix sort failed");
-  hipLaunchKernelGGL(seg_flags_kernel, grid, block, 0, s, reinterpret_cast<const int*>(sorted), tmp, n);
-  tb = temp_bytes;
-  if (hipcub::DeviceScan::InclusiveSum(reinterpret_cast<void*>(temp), tb, tmp, kq, n, s) != hipSuccess)
-    throw std::runtime_error("sort_segments: scan failed");
-  hipLaunchKernelGGL(seg_starts_kernel, grid, block, 0, s, reinterpret_cast<const int*>(sorted), kq,
-                     reinterpret_cast<int*>(seg_id), reinterpret_cast<int*>(seg), reinterpret_cast<int*>(uids), n,
-                     num_rows);
+  const int ntiles = (n + TILE - 1) / TILE;
+  const int P = passes_for(num_rows);
+  int* hist = reinterpret_cast<int*>(temp);  // [P][RADIX][ntiles]
+  int* tcount = hist + (size_t)P * RADIX * ntiles;
+  const size_t hs = (size_t)RADIX * ntiles;
+  int* wk = reinterpret_cast<int*>(work);
+  int *ks = reinterpret_cast<int*>(sorted), *vs = reinterpret_cast<int*>(perm);
+  // the last pass must land in (sorted, perm): alternate from there backwards
+  int* kb[2] = {ks, wk};
+  int* vb[2] = {vs, wk + n};
+  hipLaunchKernelGGL(rs_count0_kernel, dim3(ntiles), dim3(RT), 0, s, reinterpret_cast<const int*>(keys), n, num_rows,
+                     hist, hist + hs, (int)((P - 1) * hs), reinterpret_cast<int*>(seg), reinterpret_cast<int*>(uids),
+                     ntiles);
+  const int* kin = reinterpret_cast<const int*>(keys);
+  const int* vin = nullptr;
+  for (int p = 0; p < P; ++p) {
+    const int o = (P - 1 - p) & 1;  // pass P-1 writes buffer set 0 = (sorted, perm)
+    int* hn = p + 1 < P ? hist + (size_t)(p + 1) * hs : nullptr;
+    hipLaunchKernelGGL(rs_scatter_kernel, dim3(ntiles), dim3(RT), 0, s, kin, vin, kb[o], vb[o], n, num_rows, 8 * p,
+                       hist + (size_t)p * hs, hn, 8 * (p + 1), ntiles);
+    kin = kb[o];
+    vin = vb[o];
+  }
+  hipLaunchKernelGGL(rs_runs_count_kernel, dim3(ntiles), dim3(RT), 0, s, ks, n, tcount);
+  hipLaunchKernelGGL(rs_runs_write_kernel, dim3(ntiles), dim3(RT), 0, s, ks, n, num_rows, tcount,
+                     reinterpret_cast<int*>(seg_id), reinterpret_cast<int*>(seg), reinterpret_cast<int*>(uids));
   FTM_CHECK_LAUNCH();
 }
 

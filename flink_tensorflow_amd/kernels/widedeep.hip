@@ -150,6 +150,52 @@ __global__ __launch_bounds__(256) void wd_head_bwd_kernel(const bf16* __restrict
   *reinterpret_cast<bf16x8*>(dh + (size_t)b * H + c) = o;
 }
 
+// Head backward in one pass over the top hidden activations h [B, H] (only logit column 0
+// of the 8-row head is used): dh = (h > 0) ? dlogit[b] * wh0 : 0 (bf16), plus this block's
+// column partials of dh (-> the top layer's bias gradient) and of dlogit[b] * h (-> the head
+// weight row): part[blk][0..H) and part[blk][H..2H), summed in fixed order by colsum_reduce.
+// Thread t: 8-column chunk t % CH, row lane t / CH (CH = H / 8 chunks, 256 / CH row lanes).
+__global__ __launch_bounds__(256) void wd_head_bwd2_kernel(const bf16* __restrict__ h, const float* __restrict__ dlogit,
+                                                           const float* __restrict__ wh0, bf16* __restrict__ dh,
+                                                           float* __restrict__ part, int B, int H, int rows_per_blk) {
+  __shared__ float red[256 * 16];
+  const int CH = H >> 3, RL = 256 / CH;
+  const int c = threadIdx.x % CH, rl = threadIdx.x / CH;
+  float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, dw[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (rl < RL) {
+    f32x4 w0 = *reinterpret_cast<const f32x4*>(wh0 + c * 8), w1 = *reinterpret_cast<const f32x4*>(wh0 + c * 8 + 4);
+    const float wv[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+    const int b0 = blockIdx.x * rows_per_blk, b1 = min(B, b0 + rows_per_blk);
+    for (int b = b0 + rl; b < b1; b += RL) {
+      const float d = dlogit[b];
+      const bf16x8 hv = *reinterpret_cast<const bf16x8*>(h + (size_t)b * H + c * 8);
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = (float)hv[e];
+        o[e] = f2bf(x > 0.f ? d * wv[e] : 0.f);
+        db[e] += (float)o[e];
+        dw[e] += d * x;
+      }
+      *reinterpret_cast<bf16x8*>(dh + (size_t)b * H + c * 8) = o;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[threadIdx.x * 16 + e] = db[e];
+    red[threadIdx.x * 16 + 8 + e] = dw[e];
+  }
+  __syncthreads();
+  float* out = part + (size_t)blockIdx.x * 2 * H;
+  for (int j = threadIdx.x; j < 2 * H; j += 256) {
+    const int col = j % H, kind = j / H;  // kind 0: bias, 1: weight
+    const int cj = col >> 3, e = col & 7;
+    float a = 0.f;
+    for (int r = 0; r < RL; ++r) a += red[(r * CH + cj) * 16 + kind * 8 + e];
+    out[j] = a;
+  }
+}
+
 // seg: int64 [3, nseg] = (flat offset, element count, bf16 copy pointer) per weight segment
 __global__ __launch_bounds__(256) void wd_adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                       float* __restrict__ m, float* __restrict__ v, long n,
@@ -270,6 +316,19 @@ void wd_head_bwd(uintptr_t h, uintptr_t dlogit, uintptr_t wh0, uintptr_t dh, int
   FTM_CHECK_LAUNCH();
 }
 
+void wd_head_bwd2(uintptr_t h, uintptr_t dlogit, uintptr_t wh0, uintptr_t dh, uintptr_t part, int B, int H, int blocks,
+                  uintptr_t stream) {
+  if (H % 8 || H > 2048 || 256 % (H / 8) || h % 16 || dh % 16 || wh0 % 16)
+    throw std::invalid_argument("wd_head_bwd2: H / 8 must divide 256; 16-byte alignment");
+  if (B <= 0 || blocks <= 0) return;
+  const int rows = (B + blocks - 1) / blocks;
+  hipLaunchKernelGGL(wd_head_bwd2_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const bf16*>(h), reinterpret_cast<const float*>(dlogit),
+                     reinterpret_cast<const float*>(wh0), reinterpret_cast<bf16*>(dh), reinterpret_cast<float*>(part),
+                     B, H, rows);
+  FTM_CHECK_LAUNCH();
+}
+
 void wd_adam(uintptr_t p, uintptr_t g, uintptr_t m, uintptr_t v, long n, uintptr_t step, float lr, float b1, float b2,
              float eps, float gscale, uintptr_t seg, int nseg, uintptr_t stream) {
   if (n <= 0) return;
@@ -293,6 +352,7 @@ void register_widedeep(pybind11::module_& m) {
   m.def("wd_gather", &wd_gather);
   m.def("wd_loss", &wd_loss);
   m.def("wd_head_bwd", &wd_head_bwd);
+  m.def("wd_head_bwd2", &wd_head_bwd2);
   m.def("wd_adam", &wd_adam);
   m.def("wd_mask_colsum", &wd_mask_colsum);
 }

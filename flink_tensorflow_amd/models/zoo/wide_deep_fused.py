@@ -7,23 +7,26 @@ bf16 weight copies).  This step computes the same forward, gradients and updates
 
 * ``wd_gather`` (``kernels/widedeep.hip``): embedding rows + dense features + zero pad
   straight into the bf16 MLP input, the wide-part sum, the global embedding ids;
-* the MLP forward on the MFMA GEMM with fused bias + ReLU epilogues (``ops.kernels.gemm``);
-* ``wd_loss``: BCE-with-logits mean, dlogit, the wide gradient rows, the scalar gradients;
-* ``wd_head_bwd`` for the 256 -> 1 head, then per hidden layer the weight gradient as one
-  library TN GEMM with an fp32 result (dW = dA^T . H), the bias gradient as a column sum
-  and dX as a library NN GEMM (dA . W, no transposed weight copy) + ``wd_mask_colsum``
-  (the ReLU mask of the layer input and the next bias gradient in one pass).
-  (At this batch the backward GEMMs are 4096-row problems of 32-64 256x256 tiles: the
-  ping-pong kernel with its ``drelu`` epilogue uses an eighth of the chip there and
-  measured slower than library GEMM + mask, transposes included);
+* every dense GEMM on the layout-general MFMA training GEMM (``ops.kernels.gemm_train``,
+  ``kernels/gemm_train.hip``): the forward with fused bias + ReLU epilogues, per hidden
+  layer the weight gradient dW = dA^T . H straight from the row-major activations (both
+  operands K-major, hardware transpose reads, split-K with a fixed-order reduction) into
+  the flat fp32 gradient buffer, and dX = dA . W with the ReLU mask of the layer input in
+  the epilogue and the next bias gradient as per-tile column sums (no transposed copies, no
+  library GEMM, no separate mask / column-sum pass);
+* ``wd_head_bwd2`` for the 256 -> 1 head: dh, the top bias gradient and the head weight
+  gradient in one pass over the activations;
 * the deterministic row-sparse pipeline: both tables' lookups in one key space, one radix
   sort, a reduce-by-key per table, sparse Adagrad;
 * ``wd_adam`` over ONE flat fp32 buffer holding every dense parameter (the module's
   parameters are views of it), writing the bf16 copies the next forward reads.
 
-Under data parallelism the flat gradient buffer is all-reduced in one RCCL call (the
-average folded into Adam) and the sparse rows are all-gathered as before.  The result is
-the autograd step's update up to bf16 rounding (``tests/test_widedeep.py``).
+Under data parallelism the flat gradient buffer is all-reduced in two chunks on the
+communicator's stream while the step goes on: everything but the first layer's weight
+gradient as soon as the second layer's backward is done, the first layer's weights right
+after its dW GEMM — both overlap the remaining GEMMs and the sparse grouping; Adam waits
+for them (the average is folded into Adam).  The sparse rows are all-gathered as before.
+The result is the autograd step's update up to bf16 rounding (``tests/test_widedeep.py``).
 """
 from __future__ import annotations
 
@@ -68,11 +71,14 @@ class FusedWideDeepStep:
 
     @staticmethod
     def supports(cfg) -> bool:
-        """Shapes the kernels take: hidden widths multiples of 64 (K of the dX GEMMs),
-        embedding rows of 8..512 floats with D/8 a power of two."""
+        """Shapes the kernels take: hidden widths multiples of 8 (GEMM K / N), the top one
+        with width / 8 dividing 256 (head backward), embedding rows of 8..512 floats with D/8
+        a power of two."""
         d8 = cfg.embed_dim // 8
-        return (all(h % 64 == 0 for h in cfg.hidden) and cfg.embed_dim % 8 == 0 and d8 & (d8 - 1) == 0
-                and d8 <= 64 and (cfg.num_fields * cfg.embed_dim) % 8 == 0)
+        top8 = cfg.hidden[-1] // 8
+        return (all(h % 8 == 0 for h in cfg.hidden) and 0 < top8 <= 256 and 256 % top8 == 0
+                and cfg.embed_dim % 8 == 0 and d8 & (d8 - 1) == 0 and d8 <= 64
+                and (cfg.num_fields * cfg.embed_dim) % 8 == 0)
 
     def __init__(self, model, lr: float, lr_sparse: float, betas=(0.9, 0.999), eps: float = 1e-8):
         dev = model.device
@@ -108,6 +114,10 @@ class FusedWideDeepStep:
         names = [f"mlp.{i}.weight" for i in range(len(self.layers))] + ["head.weight"]
         self.seg = torch.tensor([[self.off[n][0] for n in names], [self.off[n][1] for n in names],
                                  [w.data_ptr() for w in self.w16]], dtype=torch.int64, device=dev)
+        # all-reduce chunking: [0, _chunk) = mlp.0.weight (ready last), [_chunk, end) = the rest
+        # (another parameter order: one late all-reduce of everything)
+        o0, k0 = self.off["mlp.0.weight"]
+        self._chunk = min(total, -(-k0 // al) * al) if o0 == 0 else total
         self.F, self.D, self.ND = cfg.num_fields, cfg.embed_dim, cfg.num_dense
         self.XP = model.in_pad
         self._acts: dict[int, _Acts] = {}
@@ -118,12 +128,31 @@ class FusedWideDeepStep:
             w.copy_(l.weight.detach())
 
     # ------------------------------------------------------------------ the step
+    def _bwd_buffers(self, a: "_Acts"):
+        """Split-K workspaces of the dW GEMMs, column-sum partials of the dX GEMMs and of the
+        head backward (allocated once per micro-batch size)."""
+        if getattr(a, "ws", None) is not None:
+            return
+        dev, B = self.dev, a.B
+        a.splits, a.ws = [], []
+        for i, l in enumerate(self.layers):
+            n_out, k_in = l.weight.shape
+            s = K.gemm_train_splits(n_out, k_in, B)
+            a.splits.append(s)
+            a.ws.append(torch.empty(max(1, s) * n_out * k_in if s > 1 else 1, dtype=torch.float32, device=dev))
+        a.colsum = [torch.empty(-(-B // 128), l.weight.shape[1], dtype=torch.float32, device=dev)
+                    for l in self.layers[1:]]
+        self.head_blocks = 64
+        H = a.h[-1].shape[1]
+        a.head_part = torch.empty(self.head_blocks, 2 * H, dtype=torch.float32, device=dev)
+
     def step(self, labels, dense, cats, cross) -> torch.Tensor:
         H, m, cfg = self._H, self.m, self.cfg
         B = labels.shape[0]
         a = self._acts.get(B)
         if a is None:
             a = self._acts[B] = _Acts(self, B)
+        self._bwd_buffers(a)
         C = cross.shape[1]
         WV, WD = m.wide.table.shape
         if a.wgrad is None or a.C != C:
@@ -138,34 +167,42 @@ class FusedWideDeepStep:
         cats, dense, cross = (t if t.stride(-1) == 1 else t.contiguous() for t in (cats, dense, cross))
         if labels.dim() != 1:
             labels = labels.reshape(-1)
+        dist = comm.is_dist()
         # forward
         H.wd_gather(cats.data_ptr(), cats.stride(0), dense.data_ptr(), dense.stride(0), cross.data_ptr(),
                     cross.stride(0), m.emb.table.data_ptr(), m.wide.table.data_ptr(), a.x.data_ptr(), a.wsum.data_ptr(),
                     a.keys.data_ptr(), B, self.F, cfg.vocab_per_field, self.D, self.ND, self.XP, C, WV, WD, s)
         h = a.x
         for i, l in enumerate(self.layers):
-            h = K.gemm(h, self.w16[i], l.bias, None, "relu", out=a.h[i])
-        K.gemm(h, self.w16[-1], m.head.bias, None, None, out=a.hd)
+            h = K.gemm_train(h, self.w16[i], bias=l.bias, act="relu", out=a.h[i])
+        K.gemm_train(h, self.w16[-1], bias=m.head.bias, out=a.hd)
         H.wd_loss(a.hd.data_ptr(), a.hd.shape[1], a.wsum.data_ptr(), m.wide_bias.data_ptr(),
                   labels.data_ptr(), labels.stride(0), B, a.dlogit.data_ptr(), a.dlogit16.data_ptr(), a.loss.data_ptr(),
                   self.g["wide_bias"].data_ptr(), self.g["head.bias"].data_ptr(), a.wgrad.data_ptr(), C, WD, a.part.data_ptr(), s)
-        # backward: head (only logit column 0 is used), then the hidden layers
+        # backward: head (only logit column 0 is used) -> dh, top bias and head weight gradients
         last = a.h[-1]
-        torch.mm(a.dlogit16.view(1, B), last, out_dtype=torch.float32, out=self.g["head.weight"][0:1])
-        H.wd_head_bwd(last.data_ptr(), a.dlogit.data_ptr(), m.head.weight.data_ptr(), a.da[-1].data_ptr(), B,
-                      last.shape[1], s)
-        n_top = a.da[-1].shape[1]
-        H.wd_mask_colsum(a.da[-1].data_ptr(), 0, self.g[f"mlp.{len(self.layers) - 1}.bias"].data_ptr(), B, n_top, s)
-        for i in range(len(self.layers) - 1, -1, -1):
+        Hl = last.shape[1]
+        top = len(self.layers) - 1
+        H.wd_head_bwd2(last.data_ptr(), a.dlogit.data_ptr(), m.head.weight.data_ptr(), a.da[-1].data_ptr(),
+                       a.head_part.data_ptr(), B, Hl, self.head_blocks, s)
+        K.colsum_reduce(a.head_part[:, :Hl], self.g[f"mlp.{top}.bias"])
+        K.colsum_reduce(a.head_part[:, Hl:], self.g["head.weight"][0])
+        works = []
+        for i in range(top, -1, -1):
             da = a.da[i]  # masked; its column sums are already in the bias gradient
             inp = a.h[i - 1] if i else a.x
-            torch.mm(da.t(), inp, out_dtype=torch.float32, out=self.g[f"mlp.{i}.weight"])
-            if i:  # dX, then the ReLU mask of this layer's input + the next bias gradient
-                torch.mm(da, self.w16[i], out=a.da[i - 1])
-                H.wd_mask_colsum(a.da[i - 1].data_ptr(), inp.data_ptr(), self.g[f"mlp.{i - 1}.bias"].data_ptr(), B,
-                                 inp.shape[1], s)
-            else:  # embedding columns of dX only
-                torch.mm(da, self.w16[0][:, : self.F * self.D], out=a.de)
+            K.gemm_train(da, inp, x_t=True, w_t=True, out=self.g[f"mlp.{i}.weight"], splits=a.splits[i], ws=a.ws[i])
+            if i:  # dX with the ReLU mask of this layer's input; the next bias gradient from its column sums
+                K.gemm_train(da, self.w16[i], w_t=True, mask=inp, out=a.da[i - 1], colsum=a.colsum[i - 1])
+                K.colsum_reduce(a.colsum[i - 1], self.g[f"mlp.{i - 1}.bias"])
+                if i == 1 and dist and self._chunk < self.grad.numel():
+                    # every dense gradient but mlp.0.weight is final: reduce it now
+                    works.append(comm.get().all_reduce_async(self.grad[self._chunk:]))
+            else:
+                if dist:  # mlp.0.weight (and all the rest, unless it went early)
+                    works.append(comm.get().all_reduce_async(self.grad[:self._chunk] if works else self.grad))
+                # embedding columns of dX only
+                K.gemm_train(da, self.w16[0][:, : self.F * self.D], w_t=True, out=a.de)
         # sparse rows: both tables share one key space (wide ids offset by the embedding
         # rows) and one radix sort; each table's sums read only its own lookups
         FV = m.emb.table.shape[0]
@@ -176,16 +213,16 @@ class FusedWideDeepStep:
         rw = segment_sum_grouped(groups, a.wgrad, 1, ne, ne + B * C)
         ue = uw = u
         ws = 1
-        if comm.is_dist():
+        if dist:
             from .wide_deep import _sparse_sync
 
             ue, re = segment_sum(*_sparse_sync(u, re), FV + WV, static=True)
             uw, rw = segment_sum(*_sparse_sync(u, rw), FV + WV, static=True)
-            c = comm.get()
-            c.all_reduce(self.grad)  # one collective for every dense gradient
-            ws = c.size
+            ws = comm.get().size
         sparse_adagrad(m.emb.table.data, m.emb.accum, ue, re, self.lr_sparse)
         sparse_adagrad(m.wide.table.data, m.wide.accum, uw, rw, self.lr_sparse, offset=FV)
+        for w in works:  # dense gradients reduced (overlapped with the GEMMs + sparse pipeline)
+            w.wait()
         # dense Adam over the flat buffer + the bf16 operands of the next step
         self.t.add_(1.0)
         H.wd_adam(self.flat.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),

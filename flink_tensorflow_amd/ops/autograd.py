@@ -1,14 +1,16 @@
-"""Autograd wrappers over the MFMA GEMM kernel (online-training path).
+"""Autograd wrappers over the hand-written MFMA training GEMM (online-training path).
 
-``linear(x, w, b, act)`` computes ``act(x @ w^T + b)`` with the fused-epilogue GEMM in the
-forward pass; the backward pass is three more MFMA GEMM launches:
+``linear(x, w, b, act)`` computes ``act(x @ w^T + b)``; on the GPU all three GEMMs of the
+layer run on ``kernels/gemm_train.hip`` (``ops.kernels.gemm_train``), none on a library:
 
-* dact  = dy * act'(pre)   (elementwise, recomputed from the saved output for ReLU/sigmoid)
-* dx    = dact · W         → gemm(dact[M,N], W^T[K,N])
-* dW    = dactᵀ · x        → gemm(dactᵀ[N,M], xᵀ[K,M])
-* db    = Σ_rows dact
+* forward  y  = act(x · Wᵀ + b)      gemm_train(x, W)            fused bias + activation
+* dact     = dy * act'(y)            elementwise, from the saved output (ReLU / sigmoid / tanh)
+* dx       = dact · W                gemm_train(dact, W, w_t)    W read K-major (transpose reads)
+* dW       = dactᵀ · x               gemm_train(dact, x, x_t, w_t) fp32 result for the fp32 master
+* db       = Σ_rows dact             fp32 column sum
 
-On host tensors the same math runs through the fp32 reference ops.
+Shapes the kernel does not take (K or N not a multiple of 8) use the older igemm forward
+and fp32 host-reference GEMMs; on host tensors the same math runs in fp32.
 """
 from __future__ import annotations
 
@@ -30,23 +32,24 @@ def _act_grad(y: torch.Tensor, dy: torch.Tensor, act: int) -> torch.Tensor:
     raise NotImplementedError(f"backward of activation {act}")
 
 
-def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """``a @ b`` with an fp32 result: bf16 operands accumulate in fp32 and are written as
-    fp32 by the library GEMM itself (no bf16 rounding of the weight gradient, no cast)."""
-    if a.is_cuda and a.dtype != torch.float32:
-        return torch.mm(a, b, out_dtype=torch.float32)
-    return torch.mm(a.float(), b.float())
+def _train_ok(x2: torch.Tensor, wc: torch.Tensor) -> bool:
+    return (x2.is_cuda and x2.dtype == torch.bfloat16 and wc.dtype == torch.bfloat16 and x2.shape[1] % 8 == 0
+            and wc.shape[0] % 8 == 0)
 
 
 class _Linear(torch.autograd.Function):
-    """Forward on the hand-written MFMA GEMM with the fused bias + activation epilogue.
-    Backward: the activation mask, then two plain GEMMs on the library (dX = dA.W, NN;
-    dW = dA^T.X, TN with an fp32 result for the fp32 master weight — no transposed copies,
-    no cast kernels) and the bias gradient as one fp32 column sum."""
+    """Forward and backward on the layout-general MFMA training GEMM (no transposed copies,
+    fp32 weight gradient written by the GEMM itself, no cast kernels)."""
 
     @staticmethod
     def forward(ctx, x, w, w_compute, b, act):
-        y = K.gemm(x, w_compute, b, None, act)
+        lead = x.shape[:-1]
+        x2 = x.reshape(-1, x.shape[-1])
+        if _train_ok(x2, w_compute):
+            x2 = x2 if x2.stride(1) == 1 else x2.contiguous()
+            y = K.gemm_train(x2, w_compute, bias=b, act=act).reshape(*lead, w_compute.shape[0])
+        else:
+            y = K.gemm(x, w_compute, b, None, act)
         ctx.act = act
         ctx.w_dtype = w.dtype
         ctx.save_for_backward(x, w_compute, y)
@@ -61,10 +64,21 @@ class _Linear(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         da2 = da.reshape(-1, da.shape[-1])
         dx = dw = db = None
+        gpu = _train_ok(x2, wc)
+        if gpu:
+            da2 = da2.to(torch.bfloat16)
+            da2 = da2 if da2.stride(1) == 1 else da2.contiguous()
+            x2 = x2 if x2.stride(1) == 1 else x2.contiguous()
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(da2.to(wc.dtype), wc).to(x.dtype).reshape(*lead, x.shape[-1])
+            if gpu:
+                dx = K.gemm_train(da2, wc, w_t=True).to(x.dtype).reshape(*lead, x.shape[-1])
+            else:
+                dx = (da2.float() @ wc.float()).to(x.dtype).reshape(*lead, x.shape[-1])
         if ctx.needs_input_grad[1]:
-            dw = _mm_f32(da2.t(), x2).to(ctx.w_dtype)
+            if gpu:
+                dw = K.gemm_train(da2, x2, x_t=True, w_t=True, out_dtype=torch.float32).to(ctx.w_dtype)
+            else:
+                dw = (da2.float().t() @ x2.float()).to(ctx.w_dtype)
         if ctx.has_b and ctx.needs_input_grad[3]:
             db = da2.sum(0, dtype=torch.float32)
         return dx, dw, None, db, None

@@ -328,6 +328,117 @@ def gemm(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = None, 
     return out
 
 
+# ------------------------------------------------------------------------------ gemm_train
+_TR_KTILE_US = 0.45   # one 128x128x64 K step with two workgroups sharing a CU
+_TR_SLOTS = 512       # resident 128x128 workgroups (2 per CU)
+
+
+def gemm_train_splits(M: int, N: int, K: int) -> int:
+    """Split-K factor for ``gemm_train``: rounds of resident 128x128 workgroups times K
+    steps, plus the fp32 slab round trip of the reduction and its launch."""
+    tiles = -(-M // 128) * -(-N // 128)
+    nk = -(-K // 64)
+    best_s, best_t = 1, -(-tiles // _TR_SLOTS) * nk * _TR_KTILE_US
+    for s in (2, 3, 4, 6, 8, 12, 16, 24, 32):
+        if s > nk:
+            break
+        per = -(-nk // s)
+        se = -(-nk // per)
+        t = -(-tiles * se // _TR_SLOTS) * per * _TR_KTILE_US + se * M * N * 8 / _PP_SPLIT_BW + 2.0
+        if t < 0.9 * best_t:
+            best_s, best_t = se, t
+    return best_s
+
+
+def gemm_train(x: torch.Tensor, w: torch.Tensor, *, x_t: bool = False, w_t: bool = False,
+               bias: torch.Tensor | None = None, mask: torch.Tensor | None = None, act=None,
+               out: torch.Tensor | None = None, out_dtype=torch.bfloat16, splits: int | None = None,
+               ws: torch.Tensor | None = None, colsum: torch.Tensor | None = None) -> torch.Tensor:
+    """``epi(X @ W^T)`` on the layout-general training GEMM (``kernels/gemm_train.hip``).
+
+    ``X`` is ``x`` [M, K] (K-contiguous) or, with ``x_t``, ``x`` stored [K, M]; ``W`` is
+    ``w`` [N, K] or, with ``w_t``, ``w`` stored [K, N] — so a dense layer's three GEMMs need
+    no transposed copies: forward ``gemm_train(h, W)``, dX ``gemm_train(dA, W, w_t=True)``,
+    dW ``gemm_train(dA, h, x_t=True, w_t=True, out_dtype=torch.float32)``.  ``mask`` (bf16
+    [M, N], e.g. the layer input) applies the ReLU backward ``mask > 0 ? y : 0``; ``out`` may
+    be a row-strided view.  fp32 output takes no activation.  ``splits`` > 1 runs split-K
+    (None: cost model) with an fp32 workspace ``ws`` (>= splits*M*N floats).  ``colsum``
+    (fp32 [ceil(M/128), N], bf16 output, no split) receives every 128-row tile's column sums
+    of the stored values — ``colsum_reduce`` turns them into the next layer's bias gradient.
+    K must be a multiple of 8 (a partial last K tile reads zeros)."""
+    a = act_code(act)
+    if mask is not None:
+        a = ACT_DRELU
+    M, K = (x.shape[1], x.shape[0]) if x_t else (x.shape[0], x.shape[1])
+    N, K2 = (w.shape[1], w.shape[0]) if w_t else (w.shape[0], w.shape[1])
+    if K != K2:
+        raise ValueError(f"gemm_train: K mismatch {K} vs {K2}")
+    if out is None:
+        out = torch.empty((M, N), dtype=out_dtype, device=x.device)
+    if tuple(out.shape) != (M, N):
+        raise ValueError(f"gemm_train: out shape {tuple(out.shape)} != {(M, N)}")
+    f32 = out.dtype == torch.float32
+    if not x.is_cuda:  # reference path (CPU): same math in fp32
+        X = x.float().t() if x_t else x.float()
+        W = w.float() if w_t else w.float().t()
+        y = X @ W
+        if bias is not None:
+            y = y + bias.float()
+        if mask is not None:
+            y = torch.where(mask.float() > 0, y, torch.zeros_like(y))
+        else:
+            y = _apply_act_ref(y, a)
+        out.copy_(y.to(out.dtype))
+        if colsum is not None:
+            yq = out.float()
+            for t in range(colsum.shape[0]):
+                colsum[t].copy_(yq[t * 128:(t + 1) * 128].sum(0))
+        return out
+    for t, nm in ((x, "x"), (w, "w")):
+        _check(t, nm, device=x.device)
+        if t.stride(1) != 1:
+            raise ValueError(f"gemm_train: {nm} rows must be contiguous")
+    if out.stride(1) != 1:
+        raise ValueError("gemm_train: out rows must be contiguous")
+    if bias is not None:
+        _check(bias, "bias", torch.float32, x.device)
+    if mask is not None:
+        _check(mask, "mask", device=x.device)
+        if tuple(mask.shape) != (M, N) or mask.stride(1) != 1:
+            raise ValueError("gemm_train: mask must be [M, N] with contiguous rows")
+    if colsum is not None:
+        if f32 or tuple(colsum.shape) != (-(-M // 128), N) or colsum.dtype != torch.float32 or not colsum.is_contiguous():
+            raise ValueError("gemm_train: colsum must be contiguous fp32 [ceil(M/128), N] with bf16 output")
+        splits = 1
+    s = gemm_train_splits(M, N, K) if splits is None else int(splits)
+    s = _hip().gemm_train_splits(K, s)
+    wsp = 0
+    if s > 1:
+        need = s * M * N
+        if ws is None or ws.numel() < need:
+            ws = torch.empty(need, dtype=torch.float32, device=x.device)
+        wsp = ws.data_ptr()
+    _hip().gemm_train(x.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(mask), out.data_ptr(), M, N, K, x.stride(0),
+                      w.stride(0), out.stride(0), mask.stride(0) if mask is not None else 0, bool(x_t), bool(w_t), a,
+                      f32, s, wsp, _ptr(colsum), _stream())
+    return out
+
+
+def colsum_reduce(part: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """``out[n] = sum_t part[t, n]`` in fixed order (``gemm_train``'s per-tile column sums ->
+    a bias gradient); ``part`` may be a column slice of a wider partial buffer."""
+    T, N = part.shape
+    if out.numel() != N:
+        raise ValueError("colsum_reduce: out must hold N floats")
+    if not part.is_cuda:
+        out.copy_(part.sum(0).reshape(out.shape))
+        return out
+    if part.stride(1) != 1 or not out.is_contiguous():
+        raise ValueError("colsum_reduce: contiguous rows / output")
+    _hip().colsum_reduce(part.data_ptr(), T, part.stride(0), N, out.data_ptr(), _stream())
+    return out
+
+
 # ------------------------------------------------------------------------------ gemm_pp
 _PP_KTILE_US = 1.5    # one 256x256x64 K step of one workgroup (measured: 1.39 PF at 8192^3)
 _PP_SPLIT_BW = 5.0e6  # bytes per microsecond of the fp32 partial round trip (write + read)
