@@ -136,3 +136,19 @@ def test_bert_stream_over_a_savedmodel(tmp_path):
     assert [lab for lab, _ in got] == p.argmax(-1).tolist()
     np.testing.assert_allclose([c for _, c in got], p.max(-1).values.numpy(), rtol=1e-5)
     m.close()
+
+
+def test_widedeep_online_example_cpu():
+    """examples/widedeep_online.py on the host: the co-process job trains every click
+    record in micro-batches and answers the control stream's eval ticks."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "examples", "widedeep_online.py"), "--cpu",
+                        "--eval-every", "0.5"], capture_output=True, text=True, timeout=300, cwd=root)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["records_trained"] == 2048 and out["steps"] >= 8 and out["eval_losses"]
