@@ -168,33 +168,41 @@ def _as_string(ctx, node, x):
 
 
 # ------------------------------------------------------------------ checkpoints
-def _slices_ok(ss):
-    for s in _strs(ss):
-        if s:
-            raise NotImplementedError("partitioned variable slices in SaveV2/RestoreV2")
-
-
 @register("SaveV2")
 def _save_v2(ctx, node, prefix, names, shape_and_slices, *tensors):
-    _slices_ok(shape_and_slices)
+    """Whole tensors under their names; partitioned-variable slices (``shape_and_slices``
+    ``"full shape start,len:..."``) as slice entries of the full variable."""
     p = _str(prefix)
     w = bundle.BundleWriter(p)
     vals = []
-    for n, t in zip(_strs(names), tensors):
+    for n, ss, t in zip(_strs(names), _strs(shape_and_slices), tensors):
         if hasattr(t, "read"):
             t = t.read()
-        vals.append((n.decode(), t))
-    for n, t in sorted(vals):
-        w.add(n, t)
+        vals.append((n.decode(), ss.decode(), t))
+    for n, ss, t in sorted(vals, key=lambda v: (v[0], v[1])):
+        spec = bundle.parse_shape_and_slice(ss)
+        if spec is None:
+            w.add(n, t)
+        else:
+            w.add_slice(n, spec[0], spec[1], t)
     w.finish()
     return ()
 
 
 @register("RestoreV2")
 def _restore_v2(ctx, node, prefix, names, shape_and_slices):
-    _slices_ok(shape_and_slices)
+    out = []
     with bundle.BundleReader(_str(prefix)) as r:
-        return tuple(r.read(n.decode(), device=ctx.device) for n in _strs(names))
+        for n, ss in zip(_strs(names), _strs(shape_and_slices)):
+            spec = bundle.parse_shape_and_slice(ss.decode())
+            if spec is None:
+                out.append(r.read(n.decode(), device=ctx.device))
+            else:
+                e = r.entries.get(n.decode())
+                if e is not None and [int(d) for d in (e.shape.as_list() or [])] != spec[0]:
+                    raise ValueError(f"RestoreV2: {n.decode()!r} has shape {e.shape.as_list()}, slice spec says {spec[0]}")
+                out.append(r.read_slice(n.decode(), spec[1], device=ctx.device))
+    return tuple(out)
 
 
 @register("MergeV2Checkpoints")
