@@ -76,7 +76,8 @@ class PipelinedGpuRunner:
     """
 
     def __init__(self, plans, feed: str, fetch_bufs: Callable[[Any], Sequence[torch.Tensor]],
-                 record_shape, record_dtype=torch.uint8, depth: int = 3, device=None, gather_threads: int = 8):
+                 record_shape, record_dtype=torch.uint8, depth: int = 3, device=None, gather_threads: int = 8,
+                 stage_chunk: int = 64):
         lanes = plans if isinstance(plans, (list, tuple)) else [plans]
         self.lanes = [dict(sorted(p.items())) for p in lanes]
         self.plans = self.lanes[0]
@@ -93,6 +94,7 @@ class PipelinedGpuRunner:
         self.compute_streams = [torch.cuda.Stream(self.device) for _ in self.lanes]
         self.compute_stream = self.compute_streams[0]
         self.gather_threads = gather_threads
+        self.stage_chunk = stage_chunk  # records per gather + H2D piece (0: whole batch at once)
         # FTM_HEAD_BYPASS=0: always D2D-copy the staged batch into the plan input (A/B switch)
         self.head_bypass = os.environ.get("FTM_HEAD_BYPASS", "1") != "0"
         self._native = _ext.native()
@@ -127,13 +129,24 @@ class PipelinedGpuRunner:
         t0 = time.perf_counter()
         finished = self._harvest_through(slot) if slot.busy else []
         t1 = time.perf_counter()
-        # host gather into the pinned slot (zero padding rows only when needed)
+        # host gather into the pinned slot in pieces, each piece's H2D issued as soon as it is
+        # staged (the DMA of piece i overlaps the gather of piece i+1: a batch reaches the GPU
+        # one piece after its last record is gathered, not one whole-batch copy later); the
+        # padding rows of a short batch are zeroed only when needed
+        rb = self.record_bytes
+        base, cap = slot.pinned_in.data_ptr(), slot.pinned_in.numel() * slot.pinned_in.element_size()
+        step = self.stage_chunk if 0 < self.stage_chunk < n else n
+        payloads = list(payloads)
         with trace_range(f"gather[{n}/{b}]"):
-            self._native.gather_into(slot.pinned_in.data_ptr(),
-                                     slot.pinned_in.numel() * slot.pinned_in.element_size(), list(payloads),
-                                     self.record_bytes, self.gather_threads)
+            for lo in range(0, n, step):
+                hi = min(n, lo + step)
+                self._native.gather_into(base + lo * rb, cap - lo * rb, payloads[lo:hi], rb, self.gather_threads)
+                with torch.cuda.stream(self.copy_stream):
+                    slot.dev_in[lo:hi].copy_(slot.pinned_in[lo:hi], non_blocking=True)
             if n < b:
                 slot.pinned_in[n:].zero_()
+                with torch.cuda.stream(self.copy_stream):
+                    slot.dev_in[n:].copy_(slot.pinned_in[n:], non_blocking=True)
         t2 = time.perf_counter()
         lane = self._lane
         self._lane = (self._lane + 1) % len(self.lanes)
@@ -143,8 +156,7 @@ class PipelinedGpuRunner:
             plan = select(slot.pinned_in, n)
         t3 = time.perf_counter()
         stream = self.compute_streams[lane]
-        with trace_range("h2d"), torch.cuda.stream(self.copy_stream):
-            slot.dev_in.copy_(slot.pinned_in, non_blocking=True)
+        with torch.cuda.stream(self.copy_stream):
             slot.h2d.record(self.copy_stream)
         with torch.cuda.stream(stream):
             stream.wait_event(slot.h2d)

@@ -41,10 +41,17 @@ constexpr int NT = 256;
 constexpr int TILE = 128 * 128;       // one operand tile: 128 x 64 bf16 (either image)
 constexpr int STAGE = 2 * TILE;       // X tile + W tile
 constexpr int OPITCH = 128 * 2 + 16;  // bf16 epilogue row pitch (bytes)
-constexpr int LDS_MAIN = 2 * STAGE;
 constexpr int LDS_EPI = 128 * OPITCH;
-constexpr int LDS_BYTES = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
-static_assert(LDS_BYTES <= 64 * 1024, "two workgroups per CU");
+constexpr int LDS_RED = 4 * 16 * 8 * 4;  // column-sum partials after the epilogue tile
+// STAGES = 2: 64 KiB, two workgroups per CU (grids wider than the chip); STAGES = 4: 128
+// KiB, one workgroup per CU with three K tiles in flight across every barrier (small
+// grids, where nothing else hides the DMA latency)
+template <int STAGES>
+constexpr int lds_bytes() {
+  return STAGES * STAGE > LDS_EPI + LDS_RED ? STAGES * STAGE : LDS_EPI + LDS_RED;
+}
+static_assert(lds_bytes<2>() <= 64 * 1024, "two workgroups per CU");
+static_assert(lds_bytes<4>() <= 160 * 1024, "LDS budget");
 
 typedef short v4s __attribute__((ext_vector_type(4)));
 
@@ -147,9 +154,9 @@ struct Operand {
   }
 };
 
-template <bool XT, bool WT, int ACT, bool F32, bool HAS_RES, bool SPLIT>
-__global__ __launch_bounds__(NT, 2) void gemm_train_kernel(TrParams p) {
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[LDS_BYTES];
+template <bool XT, bool WT, int ACT, bool F32, bool HAS_RES, bool SPLIT, int STAGES>
+__global__ __launch_bounds__(NT, STAGES == 2 ? 2 : 1) void gemm_train_kernel(TrParams p) {
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[lds_bytes<STAGES>()];
   const int tile = xcd_remap(blockIdx.x, p.tiles_m * p.tiles_n);
   const int tm = tile / p.tiles_n;
   const int tn = tile - tm * p.tiles_n;
@@ -181,12 +188,21 @@ __global__ __launch_bounds__(NT, 2) void gemm_train_kernel(TrParams p) {
     ow.dma(smem + s * STAGE + TILE, wave, kt0 + kt);
   };
 
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // K tiles t+1 .. t+STAGES-1 are in flight while tile t is consumed; 8 DMA instructions
+  // per wave per K tile, so "tile t+1 has landed" is vmcnt(8 * tiles issued after it)
+  auto wait_next = [&](int after) {  // after = tiles issued after the one waited for
+    if (STAGES >= 4 && after >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (STAGES >= 3 && after >= 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+#pragma unroll
+  for (int j = 0; j < STAGES - 1; ++j)
+    if (j < nk) stage(j, j);
+  wait_next(min(STAGES - 2, nk - 1));
   TR_BARRIER();
   for (int t = 0; t < nk; ++t) {
-    const int s = t & 1;
-    if (t + 1 < nk) stage(t + 1, s ^ 1);
+    const int s = t % STAGES;
+    if (t + STAGES - 1 < nk) stage(t + STAGES - 1, (t + STAGES - 1) % STAGES);  // buffer read in t-1
     const uint8_t* tx = smem + s * STAGE;
     const uint8_t* tw = tx + TILE;
 #pragma unroll
@@ -203,7 +219,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_train_kernel(TrParams p) {
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wait_next(min(STAGES - 2, nk - 2 - t));  // tile t+1 landed (tiles after it may fly on)
     TR_BARRIER();
   }
 
@@ -300,14 +316,29 @@ __global__ __launch_bounds__(NT, 2) void gemm_train_kernel(TrParams p) {
   }
 }
 
-// out[n] = sum_t part[t * ldp + n], t in fixed order (column-sum partials -> bias gradient).
+// out[n] = sum_t part[t * ldp + n] in a fixed order (column-sum partials -> bias gradient):
+// a block owns 64 columns, wave w sums rows t = w, w + 4, ... (8 independent loads in
+// flight per lane), then the 4 wave partials are added in wave order.
 __global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ part, int T, int ldp, int N,
                                                             float* __restrict__ out) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + lane;
   float a = 0.f;
-  for (int t = 0; t < T; ++t) a += part[(size_t)t * ldp + n];
-  out[n] = a;
+  if (n < N) {
+    int t = w;
+    for (; t + 28 < T; t += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(t + 4 * u) * ldp + n];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a += v[u];
+    }
+    for (; t < T; t += 4) a += part[(size_t)t * ldp + n];
+  }
+  red[w][lane] = a;
+  __syncthreads();
+  if (w == 0 && n < N) out[n] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
 
 // Split-K reduction: sum the fp32 slabs in slab order (deterministic), + bias, then fp32
@@ -346,16 +377,31 @@ __global__ __launch_bounds__(256) void gemm_train_reduce_kernel(const float* __r
   }
 }
 
+int cu_count() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v;
+  }();
+  return n;
+}
+
 template <bool XT, bool WT, int ACT, bool F32, bool HAS_RES>
 void launch_tr(const TrParams& p, int splits, float* ws, hipStream_t s) {
   const int tiles = p.tiles_m * p.tiles_n;
+  const bool deep = tiles * (splits > 1 ? splits : 1) <= cu_count();  // one workgroup per CU
   if (splits <= 1) {
-    hipLaunchKernelGGL((gemm_train_kernel<XT, WT, ACT, F32, HAS_RES, false>), dim3(tiles), dim3(NT), 0, s, p);
+    if (deep) hipLaunchKernelGGL((gemm_train_kernel<XT, WT, ACT, F32, HAS_RES, false, 4>), dim3(tiles), dim3(NT), 0, s, p);
+    else hipLaunchKernelGGL((gemm_train_kernel<XT, WT, ACT, F32, HAS_RES, false, 2>), dim3(tiles), dim3(NT), 0, s, p);
     return;
   }
   TrParams q = p;
   q.y = ws;
-  hipLaunchKernelGGL((gemm_train_kernel<XT, WT, ACT_NONE, true, false, true>), dim3(tiles, splits), dim3(NT), 0, s, q);
+  if (deep)
+    hipLaunchKernelGGL((gemm_train_kernel<XT, WT, ACT_NONE, true, false, true, 4>), dim3(tiles, splits), dim3(NT), 0, s, q);
+  else
+    hipLaunchKernelGGL((gemm_train_kernel<XT, WT, ACT_NONE, true, false, true, 2>), dim3(tiles, splits), dim3(NT), 0, s, q);
   const long work = (long)p.M * (p.N >> 2);
   hipLaunchKernelGGL((gemm_train_reduce_kernel<ACT, F32, HAS_RES>), dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
                      s, ws, splits, p.split_stride, p.bias, p.res, p.ldr, p.y, p.ldy, p.M, p.N);
@@ -448,7 +494,7 @@ void gemm_train(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr
 // out[n] = sum over T rows of part (row stride ldp): the per-tile column sums -> bias gradient
 void colsum_reduce(uintptr_t part, int T, int ldp, int N, uintptr_t out, uintptr_t stream) {
   if (T <= 0 || N <= 0) return;
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3((N + 63) / 64), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      reinterpret_cast<const float*>(part), T, ldp, N, reinterpret_cast<float*>(out));
   FTM_CHECK_LAUNCH();
 }

@@ -4,20 +4,21 @@
 // In-tree LSD radix sort over the key bits in use (ceil(log2(num_rows + 1)), 8-bit digits:
 // 3 passes for the 3.6M-row Wide&Deep key space), 2048-key tiles of 256 threads:
 //
-//   count0    per-tile digit counts of pass 0 (keys clamped: ids outside [0, num_rows) form
-//             one bucket, num_rows); zeroes the later passes' counters; seg[] = n, uids[] = -1
-//   scatter   per pass: every tile derives its digit offsets itself from the pass's
-//             [digit][tile] counts (its predecessors' counts + the global digit totals: 256
-//             threads x ntiles L2 reads, no scan launch), ranks its keys stably (per wave,
-//             64-key rounds in tile order: lanes with the same digit found by 9 ballots, the
-//             leader advances the wave's LDS digit counter), scatters (key, index) and counts
-//             the NEXT pass's digits of what landed in each destination tile (global atomics
-//             on integer counters: order-independent, so the result stays deterministic)
+//   count     per pass, per-tile digit counts [digit][tile] (LDS atomics; the first pass
+//             clamps keys: ids outside [0, num_rows) form one bucket, num_rows, and sets
+//             seg[] = n, uids[] = -1)
+//   scatter   per pass: every tile derives its digit offsets itself from the pass's counts
+//             (its predecessors' counts + the global digit totals: 256 threads x ntiles L2
+//             reads, no scan launch), ranks its keys stably (per wave, 64-key rounds in tile
+//             order: lanes with the same digit found by 9 ballots, the leader advances the
+//             wave's LDS digit counter) and scatters (key, index)
 //   runs      count of run starts per tile, then run index (tile prefix + block scan), run
 //             starts and run keys (-1 for the invalid bucket)
 //
 // Stable: equal keys keep their input order (same result as a stable comparison sort), so
-// every reduce-by-key downstream sums in a fixed order.  6 launches for 3 passes.
+// every reduce-by-key downstream sums in a fixed order.  8 launches for 3 passes.  (Counting
+// the next pass's digits inside the scatter with global atomics was tried: a hot id makes
+// thousands of atomics on one counter, 150-330 us per pass.)
 #include <pybind11/pybind11.h>
 
 #include <stdexcept>
@@ -40,34 +41,37 @@ int key_bits(int num_rows) {
 
 FTM_DEVICE int clamp_key(int k, int num_rows) { return (k >= 0 && k < num_rows) ? k : num_rows; }
 
-__global__ __launch_bounds__(RT) void rs_count0_kernel(const int* __restrict__ keys, int n, int num_rows,
-                                                       int* __restrict__ hist0, int* __restrict__ hist_rest,
-                                                       int rest_len, int* __restrict__ seg, int* __restrict__ uids,
-                                                       int ntiles) {
+// first: keys are the raw input (clamped here); also initialises the run outputs
+__global__ __launch_bounds__(RT) void rs_count_kernel(const int* __restrict__ keys, int n, int num_rows, int shift,
+                                                      bool first, int* __restrict__ hist, int* __restrict__ seg,
+                                                      int* __restrict__ uids, int ntiles) {
   __shared__ int cnt[RADIX];
   const int t = blockIdx.x;
   cnt[threadIdx.x] = 0;
-  // grid-stride init of the later passes' counters and of the run outputs
-  for (int i = t * RT + threadIdx.x; i < rest_len; i += ntiles * RT) hist_rest[i] = 0;
-  for (int i = t * RT + threadIdx.x; i <= n; i += ntiles * RT) {
-    seg[i] = n;
-    if (i < n) uids[i] = -1;
+  if (first) {  // grid-stride init of the run outputs
+    for (int i = t * RT + threadIdx.x; i <= n; i += ntiles * RT) {
+      seg[i] = n;
+      if (i < n) uids[i] = -1;
+    }
   }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
     const int i = t * TILE + j * RT + threadIdx.x;
-    if (i < n) atomicAdd(&cnt[clamp_key(keys[i], num_rows) & (RADIX - 1)], 1);
+    if (i < n) {
+      const int k = first ? clamp_key(keys[i], num_rows) : keys[i];
+      atomicAdd(&cnt[(k >> shift) & (RADIX - 1)], 1);
+    }
   }
   __syncthreads();
-  hist0[threadIdx.x * ntiles + t] = cnt[threadIdx.x];
+  hist[threadIdx.x * ntiles + t] = cnt[threadIdx.x];
 }
 
 // One radix pass.  vin == nullptr: values are the input indices (first pass; keys clamped).
 __global__ __launch_bounds__(RT) void rs_scatter_kernel(const int* __restrict__ kin, const int* __restrict__ vin,
                                                         int* __restrict__ kout, int* __restrict__ vout, int n,
                                                         int num_rows, int shift, const int* __restrict__ hist,
-                                                        int* __restrict__ hist_next, int shift_next, int ntiles) {
+                                                        int ntiles) {
   __shared__ int goff[RADIX];
   __shared__ int tot[RADIX];
   __shared__ int wcnt[4][RADIX + 1];  // per-wave digit counters (+1: the out-of-range slot)
@@ -152,7 +156,6 @@ __global__ __launch_bounds__(RT) void rs_scatter_kernel(const int* __restrict__ 
     const int pos = goff[d] + wcnt[w][d] + rank[r];
     kout[pos] = key[r];
     vout[pos] = val[r];
-    if (hist_next) atomicAdd(&hist_next[((key[r] >> shift_next) & (RADIX - 1)) * ntiles + pos / TILE], 1);
   }
 }
 
@@ -251,16 +254,15 @@ void sort_segments(uintptr_t keys, int n, int num_rows, uintptr_t sorted, uintpt
   // the last pass must land in (sorted, perm): alternate from there backwards
   int* kb[2] = {ks, wk};
   int* vb[2] = {vs, wk + n};
-  hipLaunchKernelGGL(rs_count0_kernel, dim3(ntiles), dim3(RT), 0, s, reinterpret_cast<const int*>(keys), n, num_rows,
-                     hist, hist + hs, (int)((P - 1) * hs), reinterpret_cast<int*>(seg), reinterpret_cast<int*>(uids),
-                     ntiles);
   const int* kin = reinterpret_cast<const int*>(keys);
   const int* vin = nullptr;
   for (int p = 0; p < P; ++p) {
     const int o = (P - 1 - p) & 1;  // pass P-1 writes buffer set 0 = (sorted, perm)
-    int* hn = p + 1 < P ? hist + (size_t)(p + 1) * hs : nullptr;
+    int* hp = hist + (size_t)p * hs;
+    hipLaunchKernelGGL(rs_count_kernel, dim3(ntiles), dim3(RT), 0, s, kin, n, num_rows, 8 * p, p == 0, hp,
+                       reinterpret_cast<int*>(seg), reinterpret_cast<int*>(uids), ntiles);
     hipLaunchKernelGGL(rs_scatter_kernel, dim3(ntiles), dim3(RT), 0, s, kin, vin, kb[o], vb[o], n, num_rows, 8 * p,
-                       hist + (size_t)p * hs, hn, 8 * (p + 1), ntiles);
+                       hp, ntiles);
     kin = kb[o];
     vin = vb[o];
   }

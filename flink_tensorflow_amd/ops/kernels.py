@@ -329,8 +329,16 @@ def gemm(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = None, 
 
 
 # ------------------------------------------------------------------------------ gemm_train
-_TR_KTILE_US = 0.45   # one 128x128x64 K step with two workgroups sharing a CU
-_TR_SLOTS = 512       # resident 128x128 workgroups (2 per CU)
+_TR_KTILE_US = 0.45       # one 128x128x64 K step, two workgroups sharing a CU (2-stage ring)
+_TR_KTILE_DEEP_US = 0.3   # the same with the CU to itself (4-stage ring, grids <= one per CU)
+_TR_SLOTS = 512           # resident 128x128 workgroups (2 per CU)
+
+
+def _tr_time(tiles: int, per: int, se: int, num_cu: int = 256) -> float:
+    wgs = tiles * se
+    if wgs <= num_cu:
+        return per * _TR_KTILE_DEEP_US
+    return -(-wgs // _TR_SLOTS) * per * _TR_KTILE_US
 
 
 def gemm_train_splits(M: int, N: int, K: int) -> int:
@@ -338,13 +346,13 @@ def gemm_train_splits(M: int, N: int, K: int) -> int:
     steps, plus the fp32 slab round trip of the reduction and its launch."""
     tiles = -(-M // 128) * -(-N // 128)
     nk = -(-K // 64)
-    best_s, best_t = 1, -(-tiles // _TR_SLOTS) * nk * _TR_KTILE_US
+    best_s, best_t = 1, _tr_time(tiles, nk, 1)
     for s in (2, 3, 4, 6, 8, 12, 16, 24, 32):
         if s > nk:
             break
         per = -(-nk // s)
         se = -(-nk // per)
-        t = -(-tiles * se // _TR_SLOTS) * per * _TR_KTILE_US + se * M * N * 8 / _PP_SPLIT_BW + 2.0
+        t = _tr_time(tiles, per, se) + se * M * N * 8 / _PP_SPLIT_BW + 2.0
         if t < 0.9 * best_t:
             best_s, best_t = se, t
     return best_s
@@ -394,10 +402,9 @@ def gemm_train(x: torch.Tensor, w: torch.Tensor, *, x_t: bool = False, w_t: bool
             for t in range(colsum.shape[0]):
                 colsum[t].copy_(yq[t * 128:(t + 1) * 128].sum(0))
         return out
-    for t, nm in ((x, "x"), (w, "w")):
-        _check(t, nm, device=x.device)
-        if t.stride(1) != 1:
-            raise ValueError(f"gemm_train: {nm} rows must be contiguous")
+    for t, nm in ((x, "x"), (w, "w")):  # row-strided views are fine (ld = stride(0))
+        if t.dtype != torch.bfloat16 or t.device != x.device or t.dim() != 2 or t.stride(1) != 1:
+            raise ValueError(f"gemm_train: {nm} must be a bf16 [rows, cols] view with contiguous rows on {x.device}")
     if out.stride(1) != 1:
         raise ValueError("gemm_train: out rows must be contiguous")
     if bias is not None:
