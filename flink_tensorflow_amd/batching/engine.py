@@ -19,7 +19,6 @@ compiled bucket ≥ n (padding rows are zero and their outputs discarded).
 from __future__ import annotations
 
 import bisect
-import os
 import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Sequence
@@ -95,8 +94,6 @@ class PipelinedGpuRunner:
         self.compute_stream = self.compute_streams[0]
         self.gather_threads = gather_threads
         self.stage_chunk = stage_chunk  # records per gather + H2D piece (0: whole batch at once)
-        # FTM_HEAD_BYPASS=0: always D2D-copy the staged batch into the plan input (A/B switch)
-        self.head_bypass = os.environ.get("FTM_HEAD_BYPASS", "1") != "0"
         self._native = _ext.native()
         depth = max(depth, len(self.lanes) + 2)  # every lane busy + one batch being staged
         self.slots: dict[int, list[_Slot]] = {}
@@ -161,7 +158,7 @@ class PipelinedGpuRunner:
         with torch.cuda.stream(stream):
             stream.wait_event(slot.h2d)
             with trace_range(f"forward[{b}]@lane{lane}"):
-                replay_from = getattr(plan, "replay_from", None) if self.head_bypass else None
+                replay_from = getattr(plan, "replay_from", None)
                 if replay_from is not None:  # head kernel reads the staging slot: no D2D copy
                     replay_from(self.feed, slot.dev_in)
                 else:

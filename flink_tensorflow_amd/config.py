@@ -12,6 +12,7 @@ every operator as ``parameters.engine`` in ``open(parameters)``
 from __future__ import annotations
 
 import argparse
+import contextlib
 import dataclasses
 import os
 from dataclasses import dataclass, field
@@ -36,6 +37,15 @@ class EngineConfig:
     restart_delay_s: float = 0.0
     channel_capacity: int = 1024
     log_level: str = "INFO"
+    # ---- compiler / kernel selection (measured choices; FT_<NAME> env vars or YAML)
+    conv_impl: str = "incumbent"       # implicit-GEMM convs: incumbent | auto (probe conv_pp) | pp
+    fuse_block_tails: bool = True      # ResNet block boundary: expand + next reduce in one kernel
+    fuse_wide_tails: bool = False      # ... also for stage 2 (weights streamed; measured no gain)
+    decimate_tails: bool = True        # stage-1 tail output stored at the stride-2 reader's pixels
+    pw_res_kernel: bool = True         # identity-residual expand convs on the persistent kernel
+    pw_dual_kernel: bool = False       # stage-2 projection+expand on the persistent dual kernel
+    conv3x3c64_kernel: bool = True     # 64-channel 3x3 convs with the filter bank in LDS
+    wd_fused_step: bool = True         # Wide&Deep: hand-fused GPU step instead of autograd
     extra: dict = field(default_factory=dict)
 
     # ------------------------------------------------------------------ sources
@@ -118,6 +128,8 @@ class EngineConfig:
             raise ValueError("max_batch >= 1 and max_delay_ms >= 0 required")
         if self.precision not in ("bf16", "fp8"):
             raise ValueError("precision must be bf16 or fp8")
+        if self.conv_impl not in ("incumbent", "auto", "pp"):
+            raise ValueError("conv_impl must be incumbent, auto or pp")
         if not 0 < self.arena_fraction <= 1:
             raise ValueError("arena_fraction must be in (0, 1]")
         if self.batch_buckets and sorted(self.batch_buckets) != list(self.batch_buckets):
@@ -139,6 +151,7 @@ class EngineConfig:
         """Configures a ``StreamExecutionEnvironment`` and exposes the config to operators."""
         from .runtime.checkpoint import RestartStrategy
 
+        set_current(self)
         env.set_parallelism(self.parallelism)
         env.config.channel_capacity = self.channel_capacity
         env.config.global_job_parameters["engine"] = self
@@ -155,3 +168,34 @@ class EngineConfig:
         d = dataclasses.asdict(self)
         d["batch_buckets"] = list(self.batch_buckets)
         return d
+
+
+_CURRENT: EngineConfig | None = None
+
+
+def current() -> EngineConfig:
+    """The process's engine configuration: the one last applied to an environment, else
+    defaults + ``FT_*`` environment variables (read once).  The graph compiler and the
+    model zoo read their kernel-selection fields from here."""
+    global _CURRENT
+    if _CURRENT is None:
+        _CURRENT = EngineConfig.from_env()
+    return _CURRENT
+
+
+def set_current(cfg: EngineConfig | None) -> None:
+    global _CURRENT
+    _CURRENT = cfg
+
+
+@contextlib.contextmanager
+def override(**fields):
+    """Temporarily replaces fields of the current configuration (tests, A/B benches)."""
+    old = current()
+    new = dataclasses.replace(old, extra=dict(old.extra))
+    new.update(fields)
+    set_current(new)
+    try:
+        yield new
+    finally:
+        set_current(old)

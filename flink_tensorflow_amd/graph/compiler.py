@@ -106,6 +106,12 @@ def _time_launch(fn, dev, reps: int = 5) -> float:
     return e0.elapsed_time(e1) * 1e3 / reps
 
 
+
+def _cfg():
+    from ..config import current
+
+    return current()
+
 class CompileError(RuntimeError):
     pass
 
@@ -277,7 +283,7 @@ class CompiledFunction(TransformerLowering):
         the bytes (ResNet v1.5's stage-1 -> stage-2 boundary: 308 MB less HBM write traffic
         per 256 images); the projection then reads it at stride 1."""
         self.decimated_tails = 0
-        if os.environ.get("FTM_TAIL_DECIMATE", "1") == "0":
+        if not _cfg().decimate_tails:
             return
         fetched = {id(_root(self.vals[(TensorName.parse(f).name, TensorName.parse(f).index)]))
                    for f in self.fetch_names}
@@ -714,7 +720,7 @@ class CompiledFunction(TransformerLowering):
             return
 
         if (res_val is None and out.qscale is None and xin_shape_override is None and (xin.phys_c or Cin) == Cin
-                and os.environ.get("FTM_CONV3X3C64", "1") != "0"
+                and _cfg().conv3x3c64_kernel
                 and K.conv3x3_c64_eligible(tuple(xin.shape), tuple(w_ohwi.shape), (sh, sw), (pt, pb, pl, pr), (dh, dw),
                                            None, act)):
             # 64-channel 3x3 (ResNet stage 1): persistent kernel, filter bank resident in LDS
@@ -761,7 +767,7 @@ class CompiledFunction(TransformerLowering):
         if (res_val is not None and pointwise and act == K.ACT_RELU and xin_shape_override is None
                 and out.qscale is None and out.dtype == torch.bfloat16 and (xin.phys_c or Cin) == Cin
                 and K.pw_res_ok(Cin, Cout) and res_val.qscale is None and res_val.concat_slot is None
-                and tuple(res_val.shape) == tuple(out.shape) and os.environ.get("FTM_PW_RES", "1") != "0"):
+                and tuple(res_val.shape) == tuple(out.shape) and _cfg().pw_res_kernel):
             # identity-residual expansion conv (ResNet stages 2/3): persistent kernel, resident
             # weight slice, next tile's x / residual prefetched (kernels/pw_res.hip)
             w_nk = w_dev.reshape(Cout, Cin)
@@ -839,11 +845,11 @@ class CompiledFunction(TransformerLowering):
 
         s2cfg = {"s2": s2}  # _decimate_tails: x2 stored already decimated -> stride 1
         # stride 1 over a same-size x2 (the decimated stage-1 -> 2 hand-over): opt-in
-        # (FTM_PW_DUAL=1) persistent prefetching kernel (kernels/pw_res.hip, dual form) — 10 %
+        # (EngineConfig.pw_dual_kernel) persistent prefetching kernel (kernels/pw_res.hip, dual form) — 10 %
         # faster alone (124 vs 139 µs) but 0.2-0.4 % slower end to end next to the sibling
         # lane (profiles/r02_pw_res2)
         use_pw = (act == K.ACT_RELU and K.pw_dual_ok(K1, C2, Cout) and (xin.phys_c or K1) == K1
-                  and (x2.phys_c or C2) == C2 and os.environ.get("FTM_PW_DUAL", "0") == "1")
+                  and (x2.phys_c or C2) == C2 and _cfg().pw_dual_kernel)
 
         def run(xin=xin, x2=x2, out=out, w_dev=w_dev, b_dev=b_dev, s2cfg=s2cfg, use_pw=use_pw):
             if use_pw and s2cfg["s2"] == 1 and tuple(x2.buf.shape[:3]) == tuple(xin.buf.shape[:3]):
@@ -876,13 +882,13 @@ class CompiledFunction(TransformerLowering):
         (CX = 64, reduce to 64 or 128) and stage 2 (CX = 128, reduce to 128).  ``w3`` is the
         host [4 CX, K] expand weight; with ``xs_val`` (stage 1's first block) K = 64 + 64
         covers the stride-1 projection shortcut of ``xs_val`` too."""
-        if os.environ.get("FTM_TAIL_FUSE", "1") == "0" or self.precision == "fp8":
+        if not _cfg().fuse_block_tails or self.precision == "fp8":
             return False
         cx = xin.shape[-1]
         co = 4 * cx
         # stage 2 (weights streamed through LDS) measured no faster than the two convs it
         # replaces (profiles/r01_tail): opt-in only
-        wide = os.environ.get("FTM_TAIL_WIDE", "0") == "1"
+        wide = _cfg().fuse_wide_tails
         widths = {64: (64, 128), 128: (128,) if wide else ()}.get(cx, ()) if xs_val is None \
             else ((64,) if cx == 64 else ())
 
@@ -955,11 +961,11 @@ class CompiledFunction(TransformerLowering):
         The choice is measured, not guessed: both candidates (and both conv_pp tile shapes)
         run a few times on scratch tensors of the layer's shapes on this device, and the
         result is cached per layer signature for the process (every bucket plan and lane of
-        a model reuses it).  Default off (``FTM_CONV_IMPL=incumbent``): with two compute
+        a model reuses it).  Default off (``EngineConfig.conv_impl = "incumbent"``): with two compute
         lanes the probe-selected layers measured ~1 % slower end to end
-        (profiles/r02_conv_pp); ``FTM_CONV_IMPL=auto`` enables the probe, ``=pp`` forces
+        (profiles/r02_conv_pp); ``conv_impl = "auto"`` enables the probe, ``"pp"`` forces
         conv_pp wherever eligible."""
-        force = os.environ.get("FTM_CONV_IMPL", "incumbent")
+        force = _cfg().conv_impl
         if self.device.type != "cuda" or force == "incumbent" or self.precision == "fp8":
             return None
         if any(s[0][3] % 64 for s in srcs) or Cout % 8 or _coff(out) % 8 or out.dtype != torch.bfloat16:
@@ -1689,7 +1695,7 @@ class CompiledFunction(TransformerLowering):
                 "param_bytes": self.param_bytes()}
 
 
-_PP_MIN_K = int(os.environ.get("FTM_PP_MIN_K", "512"))
+_PP_MIN_K = 512
 
 
 def _buf_shape(r: Val) -> tuple:

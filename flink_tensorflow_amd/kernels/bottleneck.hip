@@ -268,7 +268,7 @@ void launch_tail(const bf16* x2, const bf16* xs, const bf16* res, const bf16* w3
 // (32-channel quarters of the chunk's 128 outputs); the next tile's residual and x2 loads
 // are issued during phase 2.  Measured 166 µs per boundary at micro-batch 256 — no faster
 // than the expand + reduce convs it replaces (the weight stream's L2 latency is exposed
-// with only two chunks in flight), so the compiler uses it only with FTM_TAIL_WIDE=1.
+// with only two chunks in flight), so the compiler uses it only with EngineConfig.fuse_wide_tails.
 constexpr int WX = 128, WO = 512, WTP = 64;
 constexpr int WCHUNK = 128 * 128 / 8;  // 16-B pieces of one weight chunk
 constexpr int WIT = WCHUNK / NT;       // 4 per thread
@@ -474,16 +474,6 @@ __global__ __launch_bounds__(NT, 1) void bottleneck_tail_wide_kernel(
 // x2 [M, 64], res [M, 256] (or, dual: xs [M, 64] and no residual), w3 [256, 64] (dual:
 // [256, 128] = [W3 | Wsc]), b3 [256], w1 [cn, 256], b1 [cn] -> y3 [M, 256], y1 [M, cn]
 // (all bf16 rows contiguous; biases fp32); cn = 64 or 128 (128: identity residual only).
-// FTM_TAIL_TP64=1: 64-pixel tiles for the residual CN-64 tail (104 KB of LDS instead of 144):
-// leaves room for one implicit-GEMM workgroup of the sibling compute lane on the CU
-int tail_tp64() {
-  static const int v = [] {
-    const char* e = std::getenv("FTM_TAIL_TP64");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return v;
-}
-
 void bottleneck_tail_bf16(uintptr_t x2, uintptr_t xs, uintptr_t res, uintptr_t w3, uintptr_t b3, uintptr_t w1,
                           uintptr_t b1, uintptr_t y3, uintptr_t y1, int M, int cn, int num_cu, uintptr_t stream,
                           int dec_h, int dec_w) {
@@ -503,8 +493,6 @@ void bottleneck_tail_bf16(uintptr_t x2, uintptr_t xs, uintptr_t res, uintptr_t w
   auto fp = [](uintptr_t p) { return reinterpret_cast<const float*>(p); };
   if (dual && cn == 64)
     launch_tail<64, 64, true>(bp(x2), bp(xs), nullptr, bp(w3), fp(b3), bp(w1), fp(b1), bp(y3), bp(y1), M, num_cu, s, dec_h, dec_w);
-  else if (!dual && cn == 64 && tail_tp64())
-    launch_tail<64, 64, false>(bp(x2), nullptr, bp(res), bp(w3), fp(b3), bp(w1), fp(b1), bp(y3), bp(y1), M, num_cu, s, dec_h, dec_w);
   else if (!dual && cn == 64)
     launch_tail<128, 64, false>(bp(x2), nullptr, bp(res), bp(w3), fp(b3), bp(w1), fp(b1), bp(y3), bp(y1), M, num_cu, s, dec_h, dec_w);
   else if (!dual && cn == 128)

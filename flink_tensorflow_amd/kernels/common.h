@@ -9,18 +9,11 @@
 
 #include <cstdlib>
 
-// Host: FTM_MFMA_PRIO=1 raises the wave priority (s_setprio 1) around the MFMA clusters of
-// the persistent / direct conv kernels (conv3x3c64, pw_res, dconv), as igemm / gemm_pp /
-// conv_pp do by default.  Measured neutral for these (ResNet-50 78.36k vs 78.30k, 3 pairs;
-// these kernels hold most of a CU's LDS, so little of the sibling lane co-resides with
-// them: profiles/r02_igemm_prio), so it is off by default.
-inline int ftm_mfma_prio() {
-  static const int v = [] {
-    const char* e = std::getenv("FTM_MFMA_PRIO");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return v;
-}
+// Wave priority (s_setprio 1) around the MFMA clusters of the persistent / direct conv
+// kernels (conv3x3c64, pw_res, dconv) stays off: measured neutral for these (ResNet-50
+// 78.36k vs 78.30k, 3 pairs; they hold most of a CU's LDS, so little of the sibling lane
+// co-resides with them: profiles/r02_igemm_prio), unlike igemm / gemm_pp / conv_pp.
+constexpr int ftm_mfma_prio() { return 0; }
 #define FTM_PRIO_HI(p)                          \
   do {                                          \
     if (p) __builtin_amdgcn_s_setprio(1);       \

@@ -81,17 +81,10 @@ struct Fp8Params {
 
 FTM_DEVICE int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 4); }
 
-// FTM_FP8_PRIO=1 raises the wave priority for the MFMA phase, as igemm_bf16 does by default
-// (profiles/r02_igemm_prio).  Here it measured SLOWER (Inception-v3 fp8 61.2k -> 60.4k
-// static, 54.4k -> 53.1k dynamic): an fp8 K-tile is 128 deep, so the MFMA cluster is long
-// and prioritising it starves the sibling lane's loads.  Off by default.
-int fp8_prio() {
-  static const int v = [] {
-    const char* e = std::getenv("FTM_FP8_PRIO");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return v;
-}
+// No wave-priority raise around the MFMA phase (igemm_bf16 has one): here it measured SLOWER
+// (Inception-v3 fp8 61.2k -> 60.4k static, 54.4k -> 53.1k dynamic): an fp8 K-tile is 128
+// deep, so the MFMA cluster is long and prioritising it starves the sibling lane's loads.
+constexpr int fp8_prio() { return 0; }
 
 template <int BM, int BN, bool CONV, bool IN_BF16, bool OUT_FP8, int ACT>
 __global__ __launch_bounds__(NT, 2) void igemm_fp8_kernel(Fp8Params p) {

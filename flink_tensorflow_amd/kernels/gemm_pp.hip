@@ -306,25 +306,10 @@ __device__ __forceinline__ void pp_tile(const PPParams& p, uint8_t* smem, const 
   }
 }
 
-// PERSIST: a grid of (at most) one workgroup per CU walks the tiles (id += gridDim.x; the
-// grid is a multiple of 8, so every id of a workgroup stays on its XCD and the XCD remap
-// keeps each XCD on a contiguous tile range).  The CUs drift apart instead of starting
-// every tile round together, so the epilogue stores and the next prologue's loads of
-// different CUs no longer all hit HBM in the same microseconds, and no workgroup is
-// dispatched per tile.  Every workgroup exits after its last tile: no inter-workgroup
-// waits.
-template <int ACT, bool HAS_RES, bool SPLIT, bool PERSIST>
+template <int ACT, bool HAS_RES, bool SPLIT>
 __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PPParams p) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[LDS_BYTES];
-  const int nwg = p.tiles_m * p.tiles_n;
-  if constexpr (PERSIST) {
-    for (int id = blockIdx.x; id < nwg; id += gridDim.x) {
-      pp_tile<ACT, HAS_RES, SPLIT>(p, smem, xcd_remap(id, nwg));
-      __syncthreads();  // the epilogue's LDS reads retired before the next tile's DMA
-    }
-  } else {
-    pp_tile<ACT, HAS_RES, SPLIT>(p, smem, xcd_remap(blockIdx.x, nwg));
-  }
+  pp_tile<ACT, HAS_RES, SPLIT>(p, smem, xcd_remap(blockIdx.x, p.tiles_m * p.tiles_n));
 }
 
 // Split-K reduction: y = act(sum_s part[s] + bias (+ res)), 8 columns per thread.
@@ -365,42 +350,18 @@ __global__ __launch_bounds__(256) void gemm_pp_reduce_kernel(const float* __rest
   *reinterpret_cast<bf16x8*>(y + (size_t)m * ldy + y_coff + n) = o;
 }
 
-// 0: one workgroup per tile; 1: persistent (FTM_GEMM_PERSIST, read once)
-int persist_mode() {
-  static const int mode = [] {
-    const char* e = std::getenv("FTM_GEMM_PERSIST");
-    return e ? std::atoi(e) : 0;
-  }();
-  return mode;
-}
-
-int cu_count() {
-  static const int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return v;
-  }();
-  return n;
-}
-
 template <int ACT, bool HAS_RES>
 void launch_pp(const PPParams& p, int splits, float* ws, hipStream_t s) {
   dim3 block(NT);
   const int tiles = p.tiles_m * p.tiles_n;
   if (splits <= 1) {
-    const int cus = cu_count() & ~7;
-    if (persist_mode() == 1 && tiles > cus) {
-      hipLaunchKernelGGL((gemm_pp_kernel<ACT, HAS_RES, false, true>), dim3(cus), block, 0, s, p);
-    } else {
-      hipLaunchKernelGGL((gemm_pp_kernel<ACT, HAS_RES, false, false>), dim3(tiles), block, 0, s, p);
-    }
+    hipLaunchKernelGGL((gemm_pp_kernel<ACT, HAS_RES, false>), dim3(tiles), block, 0, s, p);
     return;
   }
   PPParams q = p;
   q.y = ws;
   dim3 grid(tiles, splits);
-  hipLaunchKernelGGL((gemm_pp_kernel<ACT_NONE, false, true, false>), grid, block, 0, s, q);
+  hipLaunchKernelGGL((gemm_pp_kernel<ACT_NONE, false, true>), grid, block, 0, s, q);
   const long work = (long)p.M * (p.N >> 3);
   hipLaunchKernelGGL((gemm_pp_reduce_kernel<ACT, HAS_RES>), dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
                      ws, splits, p.split_stride, p.bias, p.res, p.ldr, reinterpret_cast<bf16*>(p.y), p.ldy, p.y_coff,

@@ -392,18 +392,12 @@ void launch(const IgemmParams& p, int act, int cfg, hipStream_t s) {
   FTM_CHECK_LAUNCH();
 }
 
-// s_setprio(1) around each K-tile's MFMA cluster (FTM_IGEMM_PRIO=0 turns it off).  With two
+// s_setprio(1) around each K-tile's MFMA cluster.  With two
 // compute lanes a CU holds this kernel's waves next to the sibling lane's (loads, LDS
 // stores, epilogues): raising the MFMA phase's priority keeps the matrix cores fed.  Single
 // lane it is neutral (3861 vs 3863 µs per 256 images); end to end +1.0 % (79.7k -> 80.5k,
 // profiles/r02_igemm_prio).
-int igemm_prio() {
-  static const int v = [] {
-    const char* e = std::getenv("FTM_IGEMM_PRIO");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  return v;
-}
+constexpr int igemm_prio() { return 1; }
 
 // No allocation in the launch path (it may be captured into a hipGraph): a layer without
 // bias passes a zero vector owned by the caller.

@@ -315,11 +315,6 @@ int grid_for(long work, int block) {
   return (int)(g < 1 ? 1 : (g > 2048 * 8 ? 2048 * 8 : g));
 }
 
-// FTM_PREPROCESS_PIXEL=1 keeps the one-thread-per-pixel s2d kernel (A/B and tests)
-bool preprocess_pixel_form() {
-  const char* e = std::getenv("FTM_PREPROCESS_PIXEL");
-  return e && e[0] == '1';
-}
 
 }  // namespace
 
@@ -341,7 +336,7 @@ void preprocess_u8_to_bf16(uintptr_t src, uintptr_t dst, int B, int Hi, int Wi, 
   auto s = reinterpret_cast<hipStream_t>(stream);
   auto S = reinterpret_cast<const uint8_t*>(src);
   auto D = reinterpret_cast<bf16*>(dst);
-  const bool rows_ok = s2d && Wi * 3 + 3 <= PRE_ROW_MAX && !preprocess_pixel_form();
+  const bool rows_ok = s2d && Wi * 3 + 3 <= PRE_ROW_MAX;
   if (rows_ok)
     hipLaunchKernelGGL(preprocess_s2d_rows_kernel, dim3(B * ((Ho + 1) / 2)), dim3(PRE_NT), 0, s, S, D, q);
   else if (s2d) hipLaunchKernelGGL(preprocess_kernel<1>, dim3(grid_for(work, 256)), dim3(256), 0, s, S, D, B, q);

@@ -135,7 +135,7 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         self.device = device
         self.seed = seed
         # fused: the hand-fused GPU step (models/zoo/wide_deep_fused.py); None = on a GPU
-        # unless FTM_WD_FUSED=0.  False: autograd forward/backward + torch Adam.
+        # unless EngineConfig.wd_fused_step is off.  False: autograd forward/backward + torch Adam.
         self.fused = fused
         self._model = self._opt = self._bucketer = self._fused = None
         self._graph = self._static = self._static_loss = None
@@ -146,7 +146,9 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         self._model = WideDeep(self.cfg, dev, self.seed)
         if comm.is_dist():  # identical initial replicas: rank 0's weights to everyone
             comm.broadcast_tensors([p.data for p in self._model.parameters()] + list(self._model.buffers()), 0)
-        use_fused = self.fused if self.fused is not None else os.environ.get("FTM_WD_FUSED", "1") != "0"
+        from ...config import current
+
+        use_fused = self.fused if self.fused is not None else current().wd_fused_step
         from .wide_deep_fused import FusedWideDeepStep
 
         if dev.type == "cuda" and use_fused and FusedWideDeepStep.supports(self.cfg):

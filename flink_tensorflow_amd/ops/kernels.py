@@ -991,8 +991,6 @@ def _dconv_waves(waves, pool_rows, bn) -> int:
     156 µs) and stay at 4 waves (``bench/dconv_tune.py``, profiles/r02_dconv_waves)."""
     if waves is None and pool_rows is not None:
         waves = {7: 4, 14: 8}[int(pool_rows)]
-    if waves is None and os.environ.get("FTM_DCONV_WAVES"):
-        waves = int(os.environ["FTM_DCONV_WAVES"])
     return int(waves or (8 if bn == 64 else 4))
 
 
@@ -1005,7 +1003,7 @@ def conv2d_direct(x: torch.Tensor, w_arr: torch.Tensor, kshape, Cout: int, bias:
     the per-channel dequant scale ``chan_scale``); ``w_arr`` from :func:`dconv_weights`;
     ``out_scale`` → e4m3 output.  ``maxpool_pad = (top, bottom, left, right)`` fuses a 3x3 /
     stride-2 max pool of the ReLU output (ResNet stem → pool1).  ``waves`` (4 or 8, default
-    ``FTM_DCONV_WAVES``, else 8 for ``bn=64`` and 4 for ``bn=32``) sets the workgroup / tile size: 8 waves cover 32 x 16 conv
+    default 8 for ``bn=64`` and 4 for ``bn=32``) sets the workgroup / tile size: 8 waves cover 32 x 16 conv
     pixels (pooled: 14 x 8 pooled pixels, ``pool_rows=14``; 4 waves = 16 x 16 / 7 x 8) and
     fetch the filter bank half as often; tiles whose patch would not fit LDS fall back to 4.
     Device-only (the host paths use the reference convs)."""

@@ -48,17 +48,10 @@ def test_host_reference_matches_two_convs():
 
 
 def _compile(g, dev, fuse, wide="0"):
-    env = {"FTM_TAIL_FUSE": "1" if fuse else "0", "FTM_TAIL_WIDE": wide}
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
+    from flink_tensorflow_amd.config import override
+
+    with override(fuse_block_tails=fuse, fuse_wide_tails=wide == "1"):
         return CompiledFunction(g, {"images:0": ((2, 64, 64, 3), "UINT8")}, ["logits:0"], dev, strict=True)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k)
-            else:
-                os.environ[k] = v
 
 
 @pytest.fixture(scope="module")
@@ -69,7 +62,7 @@ def r50():
 def _check(r50, dev, wide="0"):
     fused, plain = _compile(r50, dev, True, wide=wide), _compile(r50, dev, False)
     # stage 1: block 1 (dual: projection shortcut) -> 2 -> 3 -> stage 2 block 1; opt-in
-    # (FTM_TAIL_WIDE=1), stage 2: block 2 -> 3 -> 4 (weights streamed through LDS)
+    # (fuse_wide_tails), stage 2: block 2 -> 3 -> 4 (weights streamed through LDS)
     n = 5 if wide == "1" else 3
     assert fused.summary()["fused_tails"] == n and plain.summary()["fused_tails"] == 0
     assert fused.summary()["fused_shortcuts"] == plain.summary()["fused_shortcuts"] == 4

@@ -46,3 +46,21 @@ def test_operators_see_engine_config(tmp_path):
     assert env.parallelism == 2 and env.restart_strategy.attempts == 2 and env.checkpoint_interval == 0.05
     out = env.from_collection(list(range(10))).map(_Probe()).execute_and_collect()
     assert sorted(out) == [(i, 17) for i in range(10)]
+
+
+def test_kernel_selection_lives_in_engine_config(monkeypatch):
+    """The compiler's kernel-selection switches are typed EngineConfig fields (FT_* env,
+    YAML, CLI, or ``override``), not ad-hoc environment variables."""
+    from flink_tensorflow_amd import config
+
+    monkeypatch.setenv("FT_CONV_IMPL", "auto")
+    monkeypatch.setenv("FT_FUSE_BLOCK_TAILS", "0")
+    config.set_current(None)
+    try:
+        cfg = config.current()
+        assert cfg.conv_impl == "auto" and cfg.fuse_block_tails is False
+        with config.override(fuse_block_tails=True, pw_res_kernel=False):
+            assert config.current().fuse_block_tails and not config.current().pw_res_kernel
+        assert config.current() is cfg
+    finally:
+        config.set_current(None)

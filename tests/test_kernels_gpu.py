@@ -109,16 +109,12 @@ def test_preprocess(hw_in, hw_out, half):
                                                      ((320, 300), (299, 299), True, False),
                                                      ((299, 299), (299, 299), False, False),  # 897-B rows
                                                      ((64, 96), (33, 47), False, True)])
-def test_preprocess_s2d_row_staged(hw_in, hw_out, half, align, monkeypatch):
-    """The row-staged (LDS) s2d preprocess kernel vs the one-thread-per-pixel kernel (same
-    arithmetic: equal up to one bf16 ulp from contraction) and vs the fp32 host path."""
+def test_preprocess_s2d_row_staged(hw_in, hw_out, half, align):
+    """The row-staged (LDS) s2d preprocess kernel vs the fp32 host path."""
     img = torch.randint(0, 256, (4, *hw_in, 3), dtype=torch.uint8)
     mean, std = (123.68, 116.78, 103.94), (58.4, 57.12, 57.38)
     got = K.preprocess_images(img.to(DEV), hw_out, mean, std, align, half, s2d=True)
-    monkeypatch.setenv("FTM_PREPROCESS_PIXEL", "1")
-    pix = K.preprocess_images(img.to(DEV), hw_out, mean, std, align, half, s2d=True)
     ref = K.preprocess_images(img, hw_out, mean, std, align, half, s2d=True)
-    torch.testing.assert_close(got.float(), pix.float(), rtol=8e-3, atol=1e-2)
     _close(got, ref, rtol=1e-2, atol_scale=1e-2)
     assert (got[..., 12:] == 0).all()
 
