@@ -38,7 +38,6 @@ pools requantise on the fly; anything else reads a dequantised bf16 copy.
 from __future__ import annotations
 
 import logging
-import os
 import types
 from dataclasses import dataclass, field
 from typing import Any, Callable
