@@ -105,7 +105,7 @@ def main():
                          "widedeep = Wide&Deep online training (DP gradient all-reduce); "
                          "inception_v3 = fp8 Inception-v3 stream with bucketed dynamic batching; bert_graph = "
                          "the BERT-base classifier as a TF GraphDef (modeling.py layout) through the graph "
-                         "compiler (padded batches)")
+                         "compiler (token-packed unless --no-pack)")
     ap.add_argument("--seq-len", type=int, default=128)
     ap.add_argument("--precision", default=None, choices=["bf16", "fp8"],
                     help="compute precision of the compiled CNN plan (inception_v3 default fp8)")
@@ -119,7 +119,7 @@ def main():
                          "--max-delay-ms) and p50/p99 are arrival -> result on host.  Runs --steps x --batch "
                          "arrivals after --warmup x --batch warm-up arrivals")
     ap.add_argument("--max-delay-ms", type=float, default=2.0, help="MicroBatcher deadline (offered-rate mode)")
-    ap.add_argument("--no-pack", action="store_true", help="bert: run padded batches (no token packing)")
+    ap.add_argument("--no-pack", action="store_true", help="bert / bert_graph: run padded batches (no token packing)")
     ap.add_argument("--rehearse-fake-comm", action="store_true",
                     help="REHEARSAL ONLY: several ranks on one GPU exchange through the test loopback "
                          "communicator (host-staged) instead of RCCL, to exercise the multi-rank control flow "
@@ -233,8 +233,15 @@ def main():
         graph = Graph.from_graph_def(gd)
         for lane in range(lanes):
             arena = DeviceArena(dev, budget, name=f"rank{rank}/lane{lane}")
-            p = CompiledFunction(graph, {"input_ids:0": ((B, seq), "INT32")}, ["logits:0"], dev,
-                                 use_graph=not args.no_graph, strict=True, arena=arena)
+            if args.no_pack:
+                p = CompiledFunction(graph, {"input_ids:0": ((B, seq), "INT32")}, ["logits:0"], dev,
+                                     use_graph=not args.no_graph, strict=True, arena=arena)
+            else:  # padding-free: one plan per token capacity, picked per micro-batch on the host
+                from flink_tensorflow_amd.graph.packed import PackedFunction, default_granule
+
+                p = PackedFunction(graph, {"input_ids:0": ((B, seq), "INT32")}, ["logits:0"], dev,
+                                   use_graph=not args.no_graph, strict=True, arena=arena,
+                                   granule=default_granule(B, seq))
             lane_plans.append({B: p})
             params += p.params
         feed, rec_shape, rec_dtype = "input_ids:0", (seq,), torch.int32
@@ -245,10 +252,12 @@ def main():
             pool[i, n:] = 0
         pool[:, 0] = 101
         h, it = cfg.hidden, cfg.intermediate
-        flops_per_record = 2.0 * seq * cfg.layers * (4 * h * h + 2 * h * it) + 4.0 * seq * seq * h * cfg.layers
+        L = lens if not args.no_pack else np.full(args.pool, seq)  # useful work: real tokens only
+        flops_per_record = float(np.mean(2.0 * L * cfg.layers * (4 * h * h + 2 * h * it)
+                                         + 4.0 * L * L * h * cfg.layers))
         model_name = "BERT-base (seq classification), TF GraphDef through the graph compiler"
         data = (f"synthetic token ids, seq {seq} (real lengths U[{seq // 2},{seq}]), random-init weights, "
-                "padded execution")
+                + ("padded execution" if args.no_pack else "padding-free (token-packed) compiled plans"))
     else:
         from flink_tensorflow_amd.models.zoo.bert import (BertConfig, BertDeviceWeights, BertEncoderPlan,
                                                           PackedBertEncoder, init_bert_weights)

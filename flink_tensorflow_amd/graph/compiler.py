@@ -128,6 +128,12 @@ class Val:
     last_use: int = -1
     concat_slot: tuple | None = None  # (target Val, channel offset) for concat-by-stride-write
     qscale: float | None = None  # fp8 e4m3 storage (uint8 buffer) with this per-tensor scale
+    # token-packed plans (``token_capacity``): "packed" = one row per real token (the plan's
+    # token capacity T rows), "cls" = one row per sequence (its first token); ``shape`` is
+    # then the physical [rows, D] and ``lshape`` the graph's logical shape ([B*S, D] or
+    # [B, S, D]) that Reshape / StridedSlice reason about
+    rows: str | None = None
+    lshape: tuple | None = None
 
     @property
     def is_const(self):
@@ -156,11 +162,17 @@ class CompiledFunction(TransformerLowering):
     def __init__(self, graph: Graph, feeds: dict[str, tuple[tuple, Any]], fetches: list[str], device,
                  variables: dict | None = None, use_graph: bool = True, strict: bool = False,
                  topk_fetch: bool = True, precision: str = "bf16", calibration: dict | None = None,
-                 arena=None):
+                 arena=None, token_capacity: int | None = None):
         if precision not in ("bf16", "fp8"):
             raise ValueError(f"precision must be bf16 or fp8, not {precision!r}")
         self.graph = graph
         self.arena = arena  # subtask DeviceArena (shared slab + interned weights) or None
+        # padding-free transformer plan: token rows packed into this capacity (graph/packed.py)
+        self.token_cap = token_capacity
+        self._pack: dict | None = None
+        self._cls_nodes: set[str] = set()
+        self._cur_cls = False
+        self._cls_cache: dict[int, Val] = {}
         self.activation_bytes = 0
         self.precision = precision
         self.device = torch.device(device)
@@ -228,6 +240,8 @@ class CompiledFunction(TransformerLowering):
                 self.cons.setdefault(s, []).append(n)
         self._groups = {}
         self._prematch_transformer()  # layer_norm / attention / embedding patterns (BERT graphs)
+        if self.token_cap is not None:
+            self._setup_packing()  # CompileError when the graph cannot run token-packed
         for f in fed:
             shape, dt = self.feed_specs[str(f)]
             dt = DataType.of(dt).torch
@@ -273,6 +287,8 @@ class CompiledFunction(TransformerLowering):
             tn = TensorName.parse(f)
             if (tn.name, tn.index) not in self.vals:
                 raise CompileError(f"fetch {f} was not produced by the plan")
+            if self.vals[(tn.name, tn.index)].rows is not None:
+                raise CompileError(f"fetch {f} is a token-packed tensor (fetch a per-sequence output)")
         self._decimate_tails()
 
     def _decimate_tails(self):
@@ -367,6 +383,8 @@ class CompiledFunction(TransformerLowering):
 
     def _get(self, src: tuple[str, int]) -> Val | None:
         v = self.vals.get(src)
+        if v is not None and self._cur_cls and v.rows == "packed":
+            return self._cls_gather(v)  # first-token-only region: read each sequence's first row
         return v if v is not None else self._const_val(src)
 
     def _single_consumer(self, name: str) -> Node | None:
@@ -453,9 +471,23 @@ class CompiledFunction(TransformerLowering):
     def _lower(self, node: Node):
         if self._fold(node):
             return
+        self._cur_cls = node.name in self._cls_nodes
+        try:
+            self._lower_node(node)
+        finally:
+            self._cur_cls = False
+
+    _ROW_OPS = ("MatMul", "Reshape", "StridedSlice", "Identity", "StopGradient", "Snapshot", "NoOp")
+
+    def _lower_node(self, node: Node):
         grp = self._groups.get(node.name)
         if grp is not None and not grp["done"] and self._lower_group(grp):
             return
+        if self._pack is not None and node.op not in self._ROW_OPS:
+            for s in node.inputs:  # packed rows reach only row-wise lowerings
+                v = self.vals.get(s)
+                if v is not None and v.rows is not None:
+                    raise CompileError(f"{node.op} {node.name} reads token-packed rows; no packed lowering")
         op = node.op
         if op == "Conv2D":
             return self._lower_conv(node)
@@ -1154,9 +1186,14 @@ class CompiledFunction(TransformerLowering):
         b_dev = self._dev(bias, torch.float32) if bias is not None else None
         self.params += [w_dev] + ([b_dev] if b_dev is not None else [])
         out = self._new((a.shape[0], N), phys_c=n_pad if n_pad != N else None)
+        out.rows = a.rows
+        out.lshape = (*a.lshape[:-1], N) if a.lshape else None
         if n_pad != N:
             out.buf_shape = (a.shape[0], n_pad)
-        res_val = self.vals[residual[0].inputs[residual[1]]] if residual is not None else None
+        res_val = self._get(residual[0].inputs[residual[1]]) if residual is not None else None
+        if res_val is not None and (res_val.rows != a.rows or tuple(res_val.shape) != tuple(out.shape)):
+            if a.rows is not None or res_val.rows is not None:
+                raise CompileError(f"{node.name}: residual rows do not match the packed GEMM rows")
         xin = self._as_bf16(a, node.name)
         for n in absorbed:
             self._fused.add(n.name)
@@ -1359,6 +1396,8 @@ class CompiledFunction(TransformerLowering):
         if sv is None or not sv.is_const or x.phys_c:
             return self._lower_glue(node)
         shape = [int(v) for v in sv.const.reshape(-1).tolist()]
+        if x.rows is not None:
+            return self._reshape_rows(node, x, shape)
         n = int(np.prod(x.shape))
         if -1 in shape:
             i = shape.index(-1)
@@ -1419,6 +1458,8 @@ class CompiledFunction(TransformerLowering):
         return v.shape[-1] % 8 == 0 and v.dtype == torch.bfloat16 and src_node in self.cons
 
     def _lower_glue(self, node: Node):
+        if any(self.vals.get(s) is not None and self.vals[s].rows is not None for s in node.inputs):
+            raise CompileError(f"{node.op} {node.name} reads token-packed rows; no packed lowering")
         if self.strict:
             raise CompileError(f"op {node.op} ({node.name}) has no CDNA4 lowering (strict mode)")
         self.glue_ops.append(node.op)
@@ -1691,7 +1732,9 @@ class CompiledFunction(TransformerLowering):
                 "fused_pools": getattr(self, "fused_pools", 0), "conv3x3c64": getattr(self, "conv3x3c64", 0),
                 "conv_pp": getattr(self, "conv_pp_layers", 0), "pw_res": getattr(self, "pw_res_layers", 0),
                 "activation_bytes": self.activation_bytes,
-                "param_bytes": self.param_bytes()}
+                "param_bytes": self.param_bytes(),
+                **({"token_capacity": self.token_cap, "first_token_only_nodes": len(self._cls_nodes)}
+                   if self._pack is not None else {})}
 
 
 _PP_MIN_K = 512

@@ -20,6 +20,20 @@ Google's ``modeling.py``) arrives as decomposed ops.  Before lowering, the compi
 Every match is structural (op types, single-consumer chains, constant operands) and is
 re-validated at lowering time against the folded constants; anything that does not match
 lowers op by op as before.
+
+**Token packing** (``CompiledFunction(token_capacity=T)``, driven by ``graph/packed.py``):
+when the attention masks are ``NotEqual(input_ids, 0)`` of the fed ids (the mask-from-ids
+layout) the plan runs padding-free — the embedding group becomes ``pack_tokens`` (real
+tokens compacted into T rows, their in-sequence positions and per-sequence offsets on the
+device) + ``embed_layernorm`` at those positions; every row-wise op (projections with their
+fused bias / GELU / residual epilogues, LayerNorms, reshapes) runs on the T packed rows;
+attention runs per packed sequence (``cu_seqlens``).  The pooler's first-token
+``StridedSlice`` marks a **first-token-only region**: every node whose values reach the
+fetches only through that slice (the final layer after its QKV projection) runs on one row
+per sequence — ``cls_attention`` (first query over the sequence's keys), then the output
+projection, residual LayerNorm, FFN and LayerNorm on B rows, with each packed operand read
+through a first-row gather.  The reference product path this accelerates is
+``ModelFunction`` over a loaded signature (``ModelFunction.scala:34-79``).
 """
 from __future__ import annotations
 
@@ -267,6 +281,137 @@ class TransformerLowering:
                     self._fused.add(n)
                     changed = True
 
+    # ------------------------------------------------------------------ token packing
+    _ROWWISE = ("MatMul", "BiasAdd", "Add", "AddV2", "Sub", "Mul", "Pow", "Tanh", "Identity", "Reshape",
+                "RealDiv", "Relu", "Sigmoid")
+
+    def _setup_packing(self):
+        """Validates that the graph can run token-packed and finds the first-token-only region
+        (``self._cls_nodes``); raises ``CompileError`` otherwise."""
+        from ..types.names import TensorName
+        from .compiler import CompileError
+
+        grps = list({id(g): g for g in self._groups.values()}.values())
+        embs = [g for g in grps if g["kind"] == "emb"]
+        attns = [g for g in grps if g["kind"] == "attn"]
+        if len(embs) != 1 or not attns:
+            raise CompileError("token packing needs one embedding group and fused attention")
+        ids_src = embs[0]["ids"]
+        feed = next((f for f in self.feed_names if (TensorName.parse(f).name, TensorName.parse(f).index) == ids_src),
+                    None)
+        if feed is None:
+            raise CompileError("token packing needs the embedding ids to be a feed")
+        shape, _ = self.feed_specs[feed]
+        if len(shape) != 2:
+            raise CompileError("token packing needs [batch, seq] ids")
+        B, S = (int(v) for v in shape)
+        for g in attns:  # every attention mask must be "id != 0" of these ids
+            if g["mask"] != ids_src or not any(self.graph[n].op == "NotEqual" for n in g["mask_chain"]):
+                raise CompileError("token packing needs attention masks computed from the ids (NotEqual(ids, 0))")
+        T = int(self.token_cap)
+        if not 0 < T <= B * S:
+            raise CompileError(f"token capacity {T} outside (0, {B * S}]")
+        self._pack = {"ids": ids_src, "feed": feed, "B": B, "S": S, "T": T, "pad": 0, "cu": None, "cls": None}
+        # first-token-only region: nodes whose every consumer is in the region or is the
+        # pooler's first-token slice (reverse topological order: consumers first)
+        starts = {n for n in self.order if self.graph[n].op == "StridedSlice" and self._first_token_spec(self.graph[n])}
+        if not starts:
+            return
+        attn_out = {g["out"]: g for g in attns}
+        fed = {TensorName.parse(f).name for f in self.feed_names}
+        region: set[str] = set()
+        barrier: set[str] = set()
+        for n in reversed(self.order):
+            if n in region or n in fed or n in starts or self._fetched(n):
+                continue
+            cons = self._consumers(n)
+            if not cons or any(c in barrier for c in cons) or not all(c in region or c in starts for c in cons):
+                continue
+            grp = self._groups.get(n)
+            if n in attn_out:  # the attention itself: first query only, over all keys
+                g = attn_out[n]
+                g["cls"] = True
+                region |= g["members"]
+                barrier |= g["members"]  # its input keeps every row (keys / values)
+                continue
+            if grp is not None and grp["kind"] == "attn":
+                continue
+            op = self.graph[n].op
+            in_ln = grp is not None and grp["kind"] == "ln"
+            if op not in self._ROWWISE and not (in_ln and op in ("Mean", "SquaredDifference", "Rsqrt",
+                                                                  "StopGradient")):
+                continue
+            if self._is_const_node((n, 0)):
+                continue
+            region.add(n)
+        self._cls_nodes = region
+
+    def _first_token_spec(self, node) -> bool:
+        """``x[:, 0:1, :]`` / ``x[:, 0, :]`` of a rank-3 tensor (constant bounds, unit strides)."""
+        if len(node.inputs) != 4 or node.attr("ellipsis_mask", 0) or node.attr("new_axis_mask", 0):
+            return False
+        if self._is_const_node(node.inputs[0]):
+            return False
+        b, e, s = (self._const_of(node.inputs[i]) for i in (1, 2, 3))
+        if b is None or e is None or s is None:
+            return False
+        b, e, s = (t.reshape(-1).tolist() for t in (b, e, s))
+        if len(b) != 3 or any(v != 1 for v in s):
+            return False
+        bm, em, shrink = node.attr("begin_mask", 0), node.attr("end_mask", 0), node.attr("shrink_axis_mask", 0)
+        full = all((bm >> d & 1 or b[d] == 0) and em >> d & 1 and not shrink >> d & 1 for d in (0, 2))
+        first = not bm >> 1 & 1 and b[1] == 0 and (shrink >> 1 & 1 or (not em >> 1 & 1 and e[1] == 1))
+        return full and first
+
+    def _cls_gather(self, v):
+        """(B, D) rows of each sequence's first token of the packed ``v`` (one gather step,
+        cached per value)."""
+        from .compiler import _view
+
+        hit = self._cls_cache.get(id(v))
+        if hit is not None:
+            return hit
+        pk = self._pack
+        out = self._new((pk["B"], v.shape[-1]), v.dtype)
+        out.rows, out.lshape = "cls", v.lshape
+        cls = pk["cls"]
+
+        def run(v=v, out=out, cls=cls):
+            torch.index_select(_view(v), 0, cls.buf.long() if not cls.buf.is_cuda else cls.buf, out=out.buf)
+
+        self._emit(f"first_token_gather/{len(self._cls_cache)}", "gather", run, [v, cls], [out])
+        self._cls_cache[id(v)] = out
+        return out
+
+    def _reshape_rows(self, node, x, shape):
+        """Reshape of packed / first-token rows: only the row split ([B*S, D] <-> [B, S, D])
+        may change; the physical rows stay."""
+        from .compiler import CompileError, Val
+
+        pk = self._pack
+        D = x.shape[-1]
+        n = pk["B"] * pk["S"] * D
+        if -1 in shape:
+            i = shape.index(-1)
+            rest = int(np.prod([v for j, v in enumerate(shape) if j != i]))
+            shape[i] = n // max(rest, 1)
+        if shape[-1] != D or int(np.prod(shape)) != n or list(shape[:-1]) not in ([pk["B"] * pk["S"]],
+                                                                                   [pk["B"], pk["S"]]):
+            raise CompileError(f"reshape {node.name} of packed token rows to {shape}")
+        self.vals[(node.name, 0)] = Val(tuple(x.shape), x.dtype, alias_of=x, rows=x.rows, lshape=tuple(shape))
+
+    def _slice_first_token(self, node, x) -> bool:
+        from .compiler import CompileError, Val
+
+        if not self._first_token_spec(node) or x.lshape is None or len(x.lshape) != 3:
+            raise CompileError(f"StridedSlice {node.name} of packed token rows is not a first-token slice")
+        if x.rows == "packed":
+            x = self._cls_gather(x)
+        B, D = self._pack["B"], x.shape[-1]
+        shp = (B, D) if node.attr("shrink_axis_mask", 0) >> 1 & 1 else (B, 1, D)
+        self.vals[(node.name, 0)] = Val(shp, x.dtype, alias_of=x)
+        return True
+
     # ------------------------------------------------------------------ lowering
     def _lower_group(self, grp) -> bool:
         """Lowers a matched group (False: its constants do not validate -> op by op)."""
@@ -304,6 +449,7 @@ class TransformerLowering:
         g_dev, b_dev = self._dev(gamma, torch.float32), self._dev(beta, torch.float32)
         self.params += [g_dev, b_dev]
         out = self._new(x.shape)
+        out.rows, out.lshape = x.rows, x.lshape
 
         def run(xin=xin, out=out, g=g_dev, b=b_dev, eps=eps, D=D):
             K.layernorm(_rows(xin, D), g, b, eps=eps, out=out.buf.view(-1, D))
@@ -337,6 +483,29 @@ class TransformerLowering:
         ids32 = ids
         if ids.dtype != torch.int32:
             return False
+        pk = self._pack
+        if pk is not None and (grp["ids"] == pk["ids"]):
+            if (B, S) != (pk["B"], pk["S"]):
+                return False
+            T = pk["T"]
+            pids, ppos = self._new((T,), torch.int32), self._new((T,), torch.int32)
+            cu, cls = self._new((B + 1,), torch.int32), self._new((B,), torch.int32)
+            pk["cu"], pk["cls"] = cu, cls
+
+            def run_pack(ids=ids32, pids=pids, ppos=ppos, cu=cu, cls=cls):
+                K.pack_tokens(_view_(ids).reshape(B, S), pk["pad"], T, pids.buf, ppos.buf, cu.buf, cls.buf)
+
+            self._emit(grp["out"] + "/pack_tokens", "pack", run_pack, [ids32], [pids, ppos, cu, cls])
+            out = self._new((T, D))
+            out.rows, out.lshape = "packed", (B, S, D)
+
+            def run_p(pids=pids, ppos=ppos, out=out):
+                K.embed_layernorm(pids.buf, None, w_dev, pos_dev, typ_dev, g_dev, b_dev, S, eps, out=out.buf,
+                                  pos_ids=ppos.buf)
+
+            self._emit(grp["out"], "embed_ln", run_p, [pids, ppos], [out])
+            self.vals[(grp["out"], 0)] = out
+            return True
         out = self._new((B, S, D))
 
         def run(ids=ids32, out=out):
@@ -348,9 +517,11 @@ class TransformerLowering:
         return True
 
     def _lower_attn_group(self, grp) -> bool:
-        x = self._get(grp["x"])
+        x = self.vals.get(grp["x"])  # never first-token gathered: keys / values need every row
         mask = self._get(grp["mask"])
         if x is None or x.is_const or len(x.shape) != 2 or mask is None or mask.is_const:
+            return False
+        if x.rows is not None and x.rows != "packed":
             return False
         if mask.dtype != torch.int32 or len(mask.shape) != 2:
             return False
@@ -377,15 +548,23 @@ class TransformerLowering:
         T, Din = x.shape
         _, S, nh, dh = shp
         H = nh * dh
-        B = T // S
-        if dh != 64 or B * S != T or tuple(mask.shape) != (B, S) or any(w.shape != (H, Din) for w in ws):
+        pk = self._pack if x.rows == "packed" else None
+        B = pk["B"] if pk is not None else T // S
+        if pk is not None and (S != pk["S"] or pk["cu"] is None):
+            return False
+        if dh != 64 or (pk is None and B * S != T) or tuple(mask.shape) != (B, S) or \
+                any(w.shape != (H, Din) for w in ws):
             return False
         w_qkv = self._dev(torch.cat(ws, 0), torch.bfloat16)
         b_qkv = self._dev(torch.cat(bs, 0), torch.float32)
         self.params += [w_qkv, b_qkv]
         xin = self._as_bf16(x, grp["out"])
         qkv = self._new((T, 3 * H))
-        ctx = self._new((T, H))
+        cls_only = pk is not None and grp.get("cls", False)
+        ctx = self._new((B, H) if cls_only else (T, H))
+        if pk is not None:
+            qkv.rows = "packed"
+            ctx.rows, ctx.lshape = ("cls" if cls_only else "packed"), (B * S, H)
         sc = float(scale.float().reshape(-1)[0])
         gpu = self.device.type == "cuda"
         splits = K.gemm_pp_splits(T, 3 * H, Din) if gpu and Din % 64 == 0 else 1
@@ -400,8 +579,18 @@ class TransformerLowering:
         def run_attn(qkv=qkv, ctx=ctx, mask=mask):
             K.attention(qkv.buf, _view_(mask).reshape(-1), B, S, nh, pad_id=0, scale=sc, out=ctx.buf)
 
+        if pk is not None:
+            cu = pk["cu"]
+
+            def run_attn(qkv=qkv, ctx=ctx, cu=cu):  # noqa: F811
+                if cls_only:  # first query of each sequence only (the pooler reads nothing else)
+                    K.cls_attention(qkv.buf, cu.buf, B, nh, scale=sc, out=ctx.buf)
+                else:
+                    K.attention(qkv.buf, None, B, S, nh, scale=sc, out=ctx.buf, cu_seqlens=cu.buf)
+
+            mask = cu
         self._emit(grp["out"] + "/qkv", "gemm", run_qkv, [xin], [qkv], {"impl": "gemm_pp", "fused": "qkv"})
-        self._emit(grp["out"], "attention", run_attn, [qkv, mask], [ctx])
+        self._emit(grp["out"], "cls_attention" if cls_only else "attention", run_attn, [qkv, mask], [ctx])
         self.vals[(grp["out"], 0)] = ctx
         return True
 
@@ -450,6 +639,9 @@ class TransformerLowering:
 
     # ---- StridedSlice / Squeeze / ExpandDims
     def _lower_strided_slice(self, node) -> bool:
+        x = self.vals.get(node.inputs[0])
+        if x is not None and x.rows is not None:
+            return self._slice_first_token(node, x)
         x = self._get(node.inputs[0])
         if x is None or x.is_const or x.phys_c or x.qscale is not None:
             return False

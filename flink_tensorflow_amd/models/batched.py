@@ -43,8 +43,11 @@ class SignatureBatchedModel(SavedModel_, BatchedGpuModel):
                  input_key: str | None = None, output_keys: Sequence[str] | None = None,
                  record_shape: Sequence[int] | None = None, buckets: Sequence[int] = (64, 256), lanes: int = 2,
                  depth: int = 3, precision: str = "bf16", tags: Sequence[str] = (TAG_SERVE,), device=None,
-                 distributed_weights: bool = False):
+                 distributed_weights: bool = False, pack_tokens: bool | None = None):
         super().__init__(path, tags, device, distributed_weights)
+        # token-id signatures (BERT-style, mask computed from the ids): padding-free plans
+        # (graph/packed.py).  None = whenever the graph allows it, False = padded plans
+        self.pack_tokens = pack_tokens
         self.signature = signature
         self.input_key = input_key
         self.output_keys = list(output_keys) if output_keys is not None else None
@@ -91,14 +94,26 @@ class SignatureBatchedModel(SavedModel_, BatchedGpuModel):
         from ..batching.engine import PipelinedGpuRunner
         from ..config import EngineConfig
         from ..graph.compiler import CompiledFunction
+        from ..graph.packed import default_granule, try_packed
 
         sess = self.session()
         dev = sess.device
         budget = EngineConfig().arena_bytes(dev) // self.lanes
         self._arena = [DeviceArena(dev, budget, name=f"{self.signature}/lane{i}") for i in range(self.lanes)]
-        lanes = [{b: CompiledFunction(sess.graph, {self._feed: ((b, *self._shape), self._dtype.name)}, self._fetches,
-                                      dev, sess.variables, strict=False, precision=self.precision, arena=arena)
-                  for b in sorted(self.buckets, reverse=True)} for arena in self._arena]
+
+        def plan(b, arena):
+            spec = {self._feed: ((b, *self._shape), self._dtype.name)}
+            if self.pack_tokens is not False and self.precision == "bf16":
+                p = try_packed(sess.graph, spec, self._fetches, dev, variables=sess.variables, arena=arena,
+                               granule=default_granule(b, self._shape[0]) if self._shape else 2048)
+                if p is not None:
+                    return p
+                if self.pack_tokens:
+                    raise ValueError(f"signature {self.signature!r} cannot run token-packed")
+            return CompiledFunction(sess.graph, spec, self._fetches, dev, sess.variables, strict=False,
+                                    precision=self.precision, arena=arena)
+
+        lanes = [{b: plan(b, arena) for b in sorted(self.buckets, reverse=True)} for arena in self._arena]
         self._plans = lanes[0]
         glue = sorted({g for p in self._plans.values() for g in p.glue_ops})
         if glue:

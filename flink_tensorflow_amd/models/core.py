@@ -155,7 +155,7 @@ class ModelFunction:
     def __init__(self, session_provider: Callable[[], Session] | Session, signature_def: SignatureDef,
                  method: GraphMethod, check_method_name: bool = True, compile: bool | None = None,
                  batch_buckets: tuple[int, ...] | None = DEFAULT_BATCH_BUCKETS, precision: str = "bf16",
-                 strict: bool = False):
+                 strict: bool = False, pack_tokens: bool | None = None):
         if check_method_name and method.name and signature_def.method_name != method.name:
             raise ValueError(f"signature method name {signature_def.method_name!r} does not match "
                              f"method {method.name!r}")
@@ -168,6 +168,9 @@ class ModelFunction:
         self.batch_buckets = tuple(sorted(batch_buckets)) if batch_buckets else None
         self.precision = precision
         self.strict = strict
+        # token-id signatures whose attention masks come from the ids: padding-free plans
+        # (graph/packed.py); None = whenever the graph allows it
+        self.pack_tokens = pack_tokens
         self._plans: dict = {}          # feed-spec key -> (CompiledFunction, variables version, staging)
         self._interpret_reason: str | None = None
         self.last_plan = None
@@ -214,7 +217,16 @@ class ModelFunction:
         hit = self._plans.get(key)
         if hit is not None and hit[1] == version:
             return hit
-        plan = compile_signature(sess, specs, self._fetch_names, strict=self.strict, precision=self.precision)
+        plan = None
+        if self.pack_tokens is not False and self.precision == "bf16" and bucket:
+            from ..graph.packed import default_granule, try_packed
+
+            (shape, _), = specs.values() if len(specs) == 1 else ((None, None),)
+            if shape is not None and len(shape) == 2:
+                plan = try_packed(sess.graph, specs, self._fetch_names, sess.device, variables=sess.variables,
+                                  strict=self.strict, granule=default_granule(shape[0], shape[1]))
+        if plan is None:
+            plan = compile_signature(sess, specs, self._fetch_names, strict=self.strict, precision=self.precision)
         if plan.glue_ops:
             LOG.info("signature %s: ops run as PyTorch glue in the compiled plan: %s",
                      self.signature_def.method_name, sorted(set(plan.glue_ops)))
@@ -247,8 +259,11 @@ class ModelFunction:
             if bucket:
                 n = int(v.shape[0])
                 st[:n].copy_(v)
+                st[n:].zero_()  # no stale rows of an earlier, larger batch (packing counts tokens)
             else:
                 st.copy_(v)
+            if hasattr(plan, "select"):  # token-packed: capacity from the host-side ids
+                plan.select(st, n)
             plan.input_buffer(k).copy_(st, non_blocking=True)
         outs = plan(None)
         if bucket:

@@ -99,3 +99,93 @@ def test_bert_base_savedmodel_compiled_on_gpu(tmp_path):
     print(f"\n[bert_graph] base seq128 b32: max |logit err| / max |logit| = {err:.4f}")
     assert err < 0.05, err
     m.close()
+
+
+def test_packed_compiled_graph_matches_padded():
+    """Token packing of a mask-from-ids BERT graph (``graph/packed.py``): pack_tokens +
+    packed projections / LayerNorms, varlen attention, and the final layer after its QKV
+    projection on each sequence's first row only — same logits as the fp32 reference, on
+    mixed-length batches and every capacity a batch can select."""
+    from flink_tensorflow_amd.graph.packed import PackedFunction
+
+    cfg = BertConfig.tiny()
+    B, S = 4, 16
+    gd, w = bert_graph_def(cfg, S, seed=3, mask_from_ids=True)
+    pf = PackedFunction(Graph.from_graph_def(gd), {"input_ids:0": ((B, S), "INT32")}, ["logits:0", "probs:0"],
+                        "cpu", strict=True, granule=16)
+    assert pf.caps == [16, 32, 48, 64]
+    s = pf.plans[64].summary()
+    assert s["glue_ops"] == [] and s["token_capacity"] == 64
+    # last layer: first-query attention, everything after its QKV projection on B rows
+    assert s["kinds"]["cls_attention"] == 1 and s["kinds"]["attention"] == cfg.layers - 1, s
+    assert s["kinds"]["pack"] == 1 and s["first_token_only_nodes"] > 20, s
+    for seed in range(3):
+        ids = _ids(B, S, cfg.vocab_size, seed=10 + seed)
+        n_tok = int((ids != 0).sum())
+        logits, probs = pf({"input_ids:0": ids})
+        assert pf.current.token_cap == pf.capacity_for(n_tok) and pf.current.token_cap < B * S
+        ref = reference_forward(w, cfg, ids)
+        torch.testing.assert_close(logits, ref, atol=2e-3, rtol=2e-2)
+        torch.testing.assert_close(probs, torch.softmax(ref, -1), atol=2e-3, rtol=2e-2)
+
+
+def test_packing_refuses_a_fed_mask():
+    """A separately fed attention mask is not "id != pad": packing is refused (the padded
+    plan stays the path)."""
+    from flink_tensorflow_amd.graph.packed import try_packed
+
+    cfg = BertConfig.tiny()
+    gd, _ = bert_graph_def(cfg, 16, seed=3, mask_from_ids=False)
+    spec = {"input_ids:0": ((2, 16), "INT32"), "input_mask:0": ((2, 16), "INT32")}
+    assert try_packed(Graph.from_graph_def(gd), spec, ["logits:0"], "cpu", strict=True) is None
+
+
+def test_bert_savedmodel_model_function_packed(tmp_path):
+    """A mask-from-ids BERT SavedModel served through ``ModelFunction`` compiles token-packed
+    (the reference's product path, ``ModelFunction.scala:34-79``) and matches fp32."""
+    from flink_tensorflow_amd.models import PredictMethod, SavedModelModel
+    from flink_tensorflow_amd.models.zoo.bert import init_bert_weights
+
+    cfg = BertConfig.tiny()
+    d = export_bert_saved_model(str(tmp_path / "bert"), cfg, 16, seed=6, mask_from_ids=True)
+    m = SavedModelModel(d, device="cpu")
+    m.open()
+    fn = m.function("serving_default", PredictMethod(), compile=True)
+    ref_w = init_bert_weights(cfg, 6)
+    for seed, n in ((3, 4), (4, 3)):
+        ids = _ids(n, 16, cfg.vocab_size, seed=seed)
+        out = fn.apply({"input_ids": ids})
+        s = fn.plan_summary()
+        assert s["packed"] and s["glue_ops"] == [] and s["kinds"]["cls_attention"] == 1, s
+        torch.testing.assert_close(out["logits"], reference_forward(ref_w, cfg, ids), atol=2e-3, rtol=2e-2)
+    m.close()
+
+
+@pytest.mark.gpu
+def test_bert_base_savedmodel_packed_on_gpu(tmp_path):
+    """BERT-base seq 128 SavedModel, mask from the ids, mixed-length batches: ModelFunction
+    compiles it token-packed on the GPU (pack_tokens, varlen attention, first-token-only
+    final layer, no glue) and the logits match the fp32 PyTorch BERT."""
+    from flink_tensorflow_amd.models import PredictMethod, SavedModelModel
+    from flink_tensorflow_amd.models.zoo.bert import init_bert_weights
+
+    cfg = BertConfig.base()
+    d = export_bert_saved_model(str(tmp_path / "bert"), cfg, 128, seed=9, mask_from_ids=True)
+    m = SavedModelModel(d, device="cuda:0")
+    m.open()
+    fn = m.function("serving_default", PredictMethod())
+    host = init_bert_weights(cfg, 9)
+    dev_w = {k: v.cuda() for k, v in host.items()}
+    for seed, n in ((5, 64), (6, 50)):
+        ids = _ids(n, 128, cfg.vocab_size, seed=seed)
+        out = fn.apply({"input_ids": ids})
+        s = fn.plan_summary()
+        assert s["packed"] and s["glue_ops"] == [] and s["hip_graph"], s
+        assert s["kinds"]["cls_attention"] == 1 and s["kinds"]["attention"] == cfg.layers - 1, s
+        ref = reference_forward(dev_w, cfg, ids.cuda()).float().cpu()
+        got = out["logits"].float().cpu()
+        err = (got - ref).abs().max().item() / ref.abs().max().item()
+        print(f"\n[bert_graph packed] base seq128 b{n}: capacity {fn.last_plan.current.token_cap}, "
+              f"tokens {int((ids != 0).sum())}, max |logit err| / max |logit| = {err:.4f}")
+        assert err < 0.05, err
+    m.close()
