@@ -52,7 +52,7 @@ def step_work(plan, step):
             return m * n * k, n * k
         return None, 0
     kh, kw, cin, cout = f
-    out = step.outputs[0].shape
+    out = step.meta.get("conv_out") or step.outputs[0].shape  # fused-pool stem: pre-pool grid
     m = _elems(out) // out[-1]
     macs, wel = m * cout * kh * kw * cin, kh * kw * cin * cout
     if len(step.inputs) > 1 and step.inputs[1].shape[-1] != out[-1]:  # fused projection shortcut

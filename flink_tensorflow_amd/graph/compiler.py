@@ -741,7 +741,8 @@ class CompiledFunction(TransformerLowering):
                                 out=_target(out), out_channel_offset=_coff(out), bn=bn,
                                 out_scale=_eff_scale(out) if out.qscale is not None else None, maxpool_pad=mpad)
 
-            self._emit(node.name, "conv", run_d, [xin], [out])
+            # the MACs of a pool-fused stem are those of its full-resolution (pre-pool) output
+            self._emit(node.name, "conv", run_d, [xin], [out], {"conv_out": (N, Ho, Wo, Cout)} if pool else None)
             if pool is not None:
                 self.vals[(pool[0].name, 0)] = out
                 self.fused_pools = getattr(self, "fused_pools", 0) + 1

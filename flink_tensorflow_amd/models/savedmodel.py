@@ -344,7 +344,7 @@ class TensorFlowModel(RichModel, CheckpointedModel):
     def function(self, signature: str, method, **options) -> ModelFunction:
         """The ``ModelFunction`` of ``signature`` (cached per signature / method type /
         options, so its compiled plans live as long as the open model).  ``options`` go to
-        ``ModelFunction`` (``compile``, ``batch_buckets``, ``precision``, ``strict``)."""
+        ``ModelFunction`` (``compile``, ``batch_buckets``, ``precision``, ``strict``, ``pack_tokens``)."""
         key = (signature, type(method), tuple(sorted((k, _hashable(v)) for k, v in options.items())))
         fns = self.__dict__.get("_functions")
         if fns is None:  # first use, or a descriptor unpickled in a subtask (transient field)

@@ -127,7 +127,8 @@ def test_widedeep_dp_step_captured_with_rccl(rccl_comm):
     recs = synthetic_click_records(64 * 8, cfg, seed=5)
     rows = list(pack_click_records(recs, cfg, nx))
     stager = PackedBatchStager(cfg, 64, dev, n_cross=nx)
-    a, b = WideDeepTrainer(cfg, device=dev, seed=1), WideDeepTrainer(cfg, device=dev, seed=1)
+    # the autograd DP step (the fused step has its own chunked all-reduce: test_widedeep.py)
+    a, b = WideDeepTrainer(cfg, device=dev, seed=1, fused=False), WideDeepTrainer(cfg, device=dev, seed=1, fused=False)
     a.open()
     b.open()
     assert a._bucketer.active and b._bucketer.active  # the RCCL communicator is installed

@@ -1,7 +1,7 @@
 # round 3 (session 2): GPU suite on the restored tree (gemm_train, LDS radix sort, knob
 # cleanup, pinned bundle staging), default bench, W&D bench, kernel stats of both
 source tools/gpu_calls/gpu_steps.sh
-step pytest_gpu 900 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread
+step pytest_gpu 900 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread
 step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
 step bench_resnet_default 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
 step bench_wd 300 python -u bench.py --model widedeep --steps 50 --warmup 10
