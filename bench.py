@@ -107,6 +107,8 @@ def main():
                          "the BERT-base classifier as a TF GraphDef (modeling.py layout) through the graph "
                          "compiler (token-packed unless --no-pack)")
     ap.add_argument("--seq-len", type=int, default=128)
+    ap.add_argument("--token-granule", type=int, default=2048,
+                    help="bert_graph: token-capacity step of the packed plans (0: graph/packed.default_granule)")
     ap.add_argument("--precision", default=None, choices=["bf16", "fp8"],
                     help="compute precision of the compiled CNN plan (inception_v3 default fp8)")
     ap.add_argument("--buckets", default=None,
@@ -126,7 +128,7 @@ def main():
                          "of this script where there is one GPU; numbers from such runs are not results")
     ap.add_argument("--lanes", type=int, default=None,
                     help="compute lanes: independent plan instances on their own HIP streams, batches round-robin "
-                         "(default: 3 for bert, 2 otherwise; measured in profiles/r01_lanes)")
+                         "(default: 3 for bert / bert_graph, 2 otherwise; measured in profiles/r01_lanes)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, rendezvous, exchange one object per rank and print the world the "
                          "communicator sees (no model; with --rehearse-fake-comm it runs on a CPU-only box)")
@@ -176,7 +178,7 @@ def main():
     from flink_tensorflow_amd.batching.arena import DeviceArena
     from flink_tensorflow_amd.config import EngineConfig
 
-    lanes = args.lanes or (3 if args.model == "bert" else 2)
+    lanes = args.lanes or (3 if args.model in ("bert", "bert_graph") else 2)
     budget = EngineConfig().arena_bytes(dev) // lanes  # this subtask's HBM share, split over its lanes
     lane_plans, params = [], []
     if args.model == "inception_v3":
@@ -241,7 +243,7 @@ def main():
 
                 p = PackedFunction(graph, {"input_ids:0": ((B, seq), "INT32")}, ["logits:0"], dev,
                                    use_graph=not args.no_graph, strict=True, arena=arena,
-                                   granule=default_granule(B, seq))
+                                   granule=args.token_granule or default_granule(B, seq))
             lane_plans.append({B: p})
             params += p.params
         feed, rec_shape, rec_dtype = "input_ids:0", (seq,), torch.int32

@@ -27,6 +27,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <tuple>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
@@ -854,6 +857,111 @@ std::vector<std::pair<py::bytes, py::bytes>> sstable_parse(const py::buffer& buf
 }
 
 // ----------------------------------------------------------------------------------
+// Persistent copy pool: the staging copies (gather into a pinned slot, scatter into a
+// worker slab) run on long-lived threads instead of spawning threads per call — a
+// ResNet-50 micro-batch is gathered in 64-record pieces (each piece's H2D overlaps the
+// next piece's gather), and spawning 8 threads per piece cost more than the copy.
+// One job at a time; the calling thread works on the job too.
+// ----------------------------------------------------------------------------------
+class CopyPool {
+ public:
+  static CopyPool& get() {
+    static CopyPool* p = new CopyPool();  // never destroyed: workers may outlive static teardown
+    return *p;
+  }
+  // fn(i) for i in [0, n), spread over up to `threads` threads (caller included)
+  template <typename F>
+  void run(int n, int threads, const F& fn) {
+    threads = std::max(1, std::min({threads, n, kMax}));
+    if (threads == 1) {
+      for (int i = 0; i < n; ++i) fn(i);
+      return;
+    }
+    std::unique_lock<std::mutex> job_lock(job_mu_);  // one job at a time
+    ensure(threads - 1);
+    std::function<void(int)> f = fn;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &f;
+      n_ = n;
+      next_.store(0);
+      done_.store(0);
+      helpers_ = threads - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return done_.load() == n_ && active_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  static constexpr int kMax = 64;
+  void ensure(int k) {
+    std::lock_guard<std::mutex> lk(mu_);
+    while ((int)threads_.size() < k) threads_.emplace_back([this, id = (int)threads_.size()] { loop(id); });
+  }
+  void work() {
+    for (;;) {
+      int i = next_.fetch_add(1);
+      if (i >= n_) break;
+      (*job_)(i);
+      done_.fetch_add(1);
+    }
+  }
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (id >= helpers_ || job_ == nullptr) continue;  // this job wants fewer helpers
+        ++active_;
+      }
+      work();
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        --active_;
+      }
+      done_cv_.notify_all();
+    }
+  }
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> threads_;
+  const std::function<void(int)>* job_ = nullptr;
+  int n_ = 0, helpers_ = 0, active_ = 0;
+  uint64_t gen_ = 0;
+  std::atomic<int> next_{0}, done_{0};
+};
+
+// Byte-balanced parallel copy of (dst, src, bytes) pieces: large records are split into
+// 256 KiB slices so a few big records still spread over every thread.
+void parallel_copy(const std::vector<std::tuple<uint8_t*, const uint8_t*, size_t>>& pieces, int nthreads) {
+  constexpr size_t kSlice = 256 << 10;
+  std::vector<std::tuple<uint8_t*, const uint8_t*, size_t>> w;
+  size_t total = 0;
+  for (auto& p : pieces) total += std::get<2>(p);
+  if (nthreads <= 1 || total < (1u << 20)) {
+    for (auto& p : pieces) std::memcpy(std::get<0>(p), std::get<1>(p), std::get<2>(p));
+    return;
+  }
+  w.reserve(pieces.size() + total / kSlice + 1);
+  for (auto& p : pieces) {
+    for (size_t o = 0; o < std::get<2>(p); o += kSlice)
+      w.emplace_back(std::get<0>(p) + o, std::get<1>(p) + o, std::min(kSlice, std::get<2>(p) - o));
+  }
+  const int nt = std::min<int>(nthreads, (int)w.size());
+  const size_t per = (w.size() + nt - 1) / nt;  // contiguous runs: each thread streams its own range
+  CopyPool::get().run(nt, nt, [&](int t) {
+    const size_t lo = t * per, hi = std::min(w.size(), lo + per);
+    for (size_t i = lo; i < hi; ++i) std::memcpy(std::get<0>(w[i]), std::get<1>(w[i]), std::get<2>(w[i]));
+  });
+}
+
+// ----------------------------------------------------------------------------------
 // Copy of many payloads to per-payload offsets of one destination region (the
 // worker-process tensor slab: a micro-batch of records of any sizes in one call).
 // ----------------------------------------------------------------------------------
@@ -873,22 +981,12 @@ void scatter_into(uintptr_t dst, size_t dst_bytes, const std::vector<size_t>& of
     total += nb;
   }
   uint8_t* d = reinterpret_cast<uint8_t*>(dst);
+  std::vector<std::tuple<uint8_t*, const uint8_t*, size_t>> pieces;
+  pieces.reserve(v.size());
+  for (size_t i = 0; i < v.size(); ++i) pieces.emplace_back(d + offs[i], v[i].first, v[i].second);
+  (void)total;
   py::gil_scoped_release nogil;
-  auto work = [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; ++i) std::memcpy(d + offs[i], v[i].first, v[i].second);
-  };
-  int nt = std::max(1, std::min<int>(nthreads, int(v.size())));
-  if (nt == 1 || total < (1u << 20)) {
-    work(0, v.size());
-    return;
-  }
-  std::vector<std::thread> th;
-  size_t chunk = (v.size() + nt - 1) / nt;
-  for (int t = 0; t < nt; ++t) {
-    size_t lo = t * chunk, hi = std::min(v.size(), lo + chunk);
-    if (lo < hi) th.emplace_back(work, lo, hi);
-  }
-  for (auto& t : th) t.join();
+  parallel_copy(pieces, nthreads);
 }
 
 // ----------------------------------------------------------------------------------
@@ -922,23 +1020,11 @@ void gather_into(uintptr_t dst, size_t dst_bytes, const py::list& srcs, size_t s
   }
   if (v.size() * stride > dst_bytes) throw std::runtime_error("staging slot too small for the batch");
   uint8_t* d = reinterpret_cast<uint8_t*>(dst);
+  std::vector<std::tuple<uint8_t*, const uint8_t*, size_t>> pieces;
+  pieces.reserve(v.size());
+  for (size_t i = 0; i < v.size(); ++i) pieces.emplace_back(d + i * stride, v[i].first, v[i].second);
   py::gil_scoped_release nogil;
-  auto work = [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; ++i) std::memcpy(d + i * stride, v[i].first, v[i].second);
-  };
-  int nt = std::max(1, std::min<int>(nthreads, int(v.size())));
-  size_t total = v.size() * stride;
-  if (nt == 1 || total < (1u << 20)) {
-    work(0, v.size());
-    return;
-  }
-  std::vector<std::thread> th;
-  size_t chunk = (v.size() + nt - 1) / nt;
-  for (int t = 0; t < nt; ++t) {
-    size_t lo = t * chunk, hi = std::min(v.size(), lo + chunk);
-    if (lo < hi) th.emplace_back(work, lo, hi);
-  }
-  for (auto& t : th) t.join();
+  parallel_copy(pieces, nthreads);
 }
 
 }  // namespace
