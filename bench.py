@@ -97,6 +97,8 @@ def main():
     ap.add_argument("--image-hw", type=int, default=None,
                     help="decoded source image size (resnet50: 256 resized to 224; inception_v3: 299)")
     ap.add_argument("--depth", type=int, default=3, help="pipeline slots")
+    ap.add_argument("--gather-threads", type=int, default=8, help="native copy threads staging a micro-batch")
+    ap.add_argument("--no-numa", action="store_true", help="do not pin this rank to its GPU's NUMA node")
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
     ap.add_argument("--pool", type=int, default=512, help="distinct synthetic records cycled by the source")
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert", "bert_graph", "widedeep",
@@ -167,7 +169,9 @@ def main():
         raise SystemExit(f"[bench] WORLD_SIZE={ws} but only {comm.gpu_count()} GPU(s) visible to rank {rank}")
     dev = torch.device("cuda", comm.local_device(local))
     torch.cuda.set_device(dev)
-    numa = comm.bind_to_gpu_numa(dev) if ws > 1 else None  # DP ranks stage records on their GPU's socket
+    # stage records on the GPU's socket (every rank, DP=1 included): the gather threads and
+    # the pinned slots they write are first-touched there
+    numa = comm.bind_to_gpu_numa(dev) if not args.no_numa else None
 
     if args.model == "widedeep":
         return run_widedeep(args, dev, rank, ws)
@@ -300,7 +304,7 @@ def main():
 
     records = [pool[i] for i in range(args.pool)]
     runner = PipelinedGpuRunner(lane_plans, feed, lambda p: p.output_tensors(), rec_shape, rec_dtype,
-                                depth=args.depth, device=dev)
+                                depth=args.depth, device=dev, gather_threads=args.gather_threads)
 
     if args.offered_rate:
         return run_offered(args, runner, records, B, rank, ws, dev, comm, MetricGroup, model_name, data, lanes,
