@@ -51,6 +51,7 @@ class _Slot:
         self.dev_in = torch.empty((bucket, *rec_shape), dtype=rec_dtype, device=device)
         self.pinned_out = [torch.empty(s, dtype=d, pin_memory=pin) for s, d in out_shapes]
         self.h2d = torch.cuda.Event()
+        self.h2d_parts: list[torch.cuda.Event] = []  # one per staged piece (chunked head launch)
         self.done = torch.cuda.Event()
         self.busy = False
         self.n = 0
@@ -134,16 +135,19 @@ class PipelinedGpuRunner:
         base, cap = slot.pinned_in.data_ptr(), slot.pinned_in.numel() * slot.pinned_in.element_size()
         step = self.stage_chunk if 0 < self.stage_chunk < n else n
         payloads = list(payloads)
+        pieces = [(lo, min(n, lo + step)) for lo in range(0, n, step)]
+        while len(slot.h2d_parts) < len(pieces):
+            slot.h2d_parts.append(torch.cuda.Event())
         with trace_range(f"gather[{n}/{b}]"):
-            for lo in range(0, n, step):
-                hi = min(n, lo + step)
+            for i, (lo, hi) in enumerate(pieces):
                 self._native.gather_into(base + lo * rb, cap - lo * rb, payloads[lo:hi], rb, self.gather_threads)
+                if n < b and hi == n:  # the padding rows of a short batch travel with the last piece
+                    slot.pinned_in[n:].zero_()
+                    hi = b
+                    pieces[i] = (lo, b)
                 with torch.cuda.stream(self.copy_stream):
                     slot.dev_in[lo:hi].copy_(slot.pinned_in[lo:hi], non_blocking=True)
-            if n < b:
-                slot.pinned_in[n:].zero_()
-                with torch.cuda.stream(self.copy_stream):
-                    slot.dev_in[n:].copy_(slot.pinned_in[n:], non_blocking=True)
+                    slot.h2d_parts[i].record(self.copy_stream)
         t2 = time.perf_counter()
         lane = self._lane
         self._lane = (self._lane + 1) % len(self.lanes)
@@ -156,14 +160,19 @@ class PipelinedGpuRunner:
         with torch.cuda.stream(self.copy_stream):
             slot.h2d.record(self.copy_stream)
         with torch.cuda.stream(stream):
-            stream.wait_event(slot.h2d)
             with trace_range(f"forward[{b}]@lane{lane}"):
-                replay_from = getattr(plan, "replay_from", None)
-                if replay_from is not None:  # head kernel reads the staging slot: no D2D copy
-                    replay_from(self.feed, slot.dev_in)
-                else:
-                    plan.input_buffer(self.feed).copy_(slot.dev_in, non_blocking=True)
-                    plan.replay()
+                chunked = getattr(plan, "replay_from_chunks", None)
+                # head kernel per staged piece: the GPU starts on the first piece while the
+                # later ones are still in flight (shortens the pipeline fill)
+                if not (len(pieces) > 1 and chunked is not None and chunked(
+                        self.feed, slot.dev_in, pieces, lambda i: stream.wait_event(slot.h2d_parts[i]))):
+                    stream.wait_event(slot.h2d)
+                    replay_from = getattr(plan, "replay_from", None)
+                    if replay_from is not None:  # head kernel reads the staging slot: no D2D copy
+                        replay_from(self.feed, slot.dev_in)
+                    else:
+                        plan.input_buffer(self.feed).copy_(slot.dev_in, non_blocking=True)
+                        plan.replay()
             with trace_range("d2h"):
                 for dst, src in zip(slot.pinned_out, self.fetch_bufs(plan)):
                     dst.copy_(src, non_blocking=True)

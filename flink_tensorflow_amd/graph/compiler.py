@@ -1686,6 +1686,26 @@ class CompiledFunction(TransformerLowering):
         h[1].fn(x=types.SimpleNamespace(buf=src))
         self._graph_tail.replay()
 
+    def replay_from_chunks(self, feed: str, src: torch.Tensor, chunks, wait) -> bool:
+        """``replay_from`` for a batch that reaches the device in pieces: the head
+        preprocess kernel runs per piece ``chunks[i] = (lo, hi)`` right after ``wait(i)``
+        (the current stream waits for that piece's H2D), so the GPU starts on the first
+        records while the rest are still being gathered / copied; then the graph of the
+        remaining steps.  False (nothing launched) when the plan has no such head."""
+        h = self._head
+        buf = self.input_buffer(feed)
+        if (h is None or self._graph_tail is None or h[0] != str(TensorName.parse(feed))
+                or src.shape != buf.shape or src.dtype != buf.dtype or src.device != buf.device
+                or not src.is_contiguous() or len(h[1].outputs) != 1):
+            return False
+        st = h[1]
+        out = _root(st.outputs[0]).buf
+        for i, (lo, hi) in enumerate(chunks):
+            wait(i)
+            st.fn(x=types.SimpleNamespace(buf=src[lo:hi]), out=types.SimpleNamespace(buf=out[lo:hi]))
+        self._graph_tail.replay()
+        return True
+
     def replay(self):
         """Runs the plan on the current input buffers (no host synchronisation)."""
         if self._graph_obj is not None:
