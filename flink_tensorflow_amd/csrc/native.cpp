@@ -869,7 +869,9 @@ class CopyPool {
     static CopyPool* p = new CopyPool();  // never destroyed: workers may outlive static teardown
     return *p;
   }
-  // fn(i) for i in [0, n), spread over up to `threads` threads (caller included)
+  // fn(i) for i in [0, n) on up to `threads` threads (the caller included).  Jobs from
+  // several caller threads (e.g. the per-edge slab writers of several worker subtasks) run
+  // concurrently: each job is a queue entry the idle workers claim indices from.
   template <typename F>
   void run(int n, int threads, const F& fn) {
     threads = std::max(1, std::min({threads, n, kMax}));
@@ -877,64 +879,65 @@ class CopyPool {
       for (int i = 0; i < n; ++i) fn(i);
       return;
     }
-    std::unique_lock<std::mutex> job_lock(job_mu_);  // one job at a time
-    ensure(threads - 1);
+    Job job;
     std::function<void(int)> f = fn;
+    job.fn = &f;
+    job.n = n;
+    job.helpers = threads - 1;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      job_ = &f;
-      n_ = n;
-      next_.store(0);
-      done_.store(0);
-      helpers_ = threads - 1;
-      ++gen_;
+      ensure(threads - 1);
+      jobs_.push_back(&job);
     }
     cv_.notify_all();
-    work();
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return done_.load() == n_ && active_ == 0; });
-    job_ = nullptr;
+    job.work();
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      jobs_.erase(std::find(jobs_.begin(), jobs_.end(), &job));  // no new helper joins now
+      done_cv_.wait(lk, [&] { return job.active == 0; });
+    }
   }
 
  private:
   static constexpr int kMax = 64;
-  void ensure(int k) {
-    std::lock_guard<std::mutex> lk(mu_);
-    while ((int)threads_.size() < k) threads_.emplace_back([this, id = (int)threads_.size()] { loop(id); });
-  }
-  void work() {
-    for (;;) {
-      int i = next_.fetch_add(1);
-      if (i >= n_) break;
-      (*job_)(i);
-      done_.fetch_add(1);
+  struct Job {
+    const std::function<void(int)>* fn = nullptr;
+    int n = 0;
+    int helpers = 0;  // worker threads that may still join
+    int active = 0;   // worker threads inside work() (guarded by mu_)
+    std::atomic<int> next{0};
+    void work() {
+      for (int i = next.fetch_add(1); i < n; i = next.fetch_add(1)) (*fn)(i);
     }
+  };
+  void ensure(int k) {  // mu_ held
+    while ((int)threads_.size() < k) threads_.emplace_back([this] { loop(); });
   }
-  void loop(int id) {
-    uint64_t seen = 0;
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (id >= helpers_ || job_ == nullptr) continue;  // this job wants fewer helpers
-        ++active_;
-      }
-      work();
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        --active_;
-      }
+      Job* j = nullptr;
+      cv_.wait(lk, [&] {
+        for (Job* c : jobs_)
+          if (c->helpers > 0 && c->next.load() < c->n) {
+            j = c;
+            return true;
+          }
+        return false;
+      });
+      --j->helpers;
+      ++j->active;
+      lk.unlock();
+      j->work();
+      lk.lock();
+      --j->active;
       done_cv_.notify_all();
     }
   }
-  std::mutex job_mu_, mu_;
+  std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   std::vector<std::thread> threads_;
-  const std::function<void(int)>* job_ = nullptr;
-  int n_ = 0, helpers_ = 0, active_ = 0;
-  uint64_t gen_ = 0;
-  std::atomic<int> next_{0}, done_{0};
+  std::vector<Job*> jobs_;
 };
 
 // Byte-balanced parallel copy of (dst, src, bytes) pieces: large records are split into
