@@ -58,6 +58,7 @@ struct CPParams {
   void* y;
   int M, N, K;
   int OH, OW;
+  int KW, dh, dw;  // source 0's filter width and dilation (conv_lite walks K without ktab)
   int ldw, ldy, y_coff, ldr;
   int tiles_m, tiles_n;
   int kt_per_split;
@@ -375,6 +376,176 @@ __global__ __launch_bounds__(NT, 1) void conv_pp_kernel(CPParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// conv_lite: the same im2col-in-the-DMA-address loader for a 128x128 tile of FOUR waves
+// (2 x 2, 64 x 64 outputs each) on two 32 KiB LDS stages — 64 KiB, so two workgroups (or
+// one plus a sibling lane's kernel) share a CU, where conv_pp's 128-160 KiB tiles hold it
+// alone.  Both operands stream global -> LDS by buffer_load ... lds (no VGPR staging, no
+// ds_write: the register-staged igemm spends ~20 % of its wave cycles stalled on LDS issue,
+// profiles/r03_conv); one barrier per K-tile: wait for this stage's DMA, barrier (which
+// also retires every wave's reads of the other stage), issue the next K-tile's DMA into
+// the other stage, then 2 x 16 MFMAs on this one — the DMA of tile t+1 overlaps the MFMAs
+// of tile t.  Epilogue as igemm: + bias -> bf16 LDS tile -> coalesced 16-B row segments
+// (+ residual, act).
+// ---------------------------------------------------------------------------------------
+template <int ACT, bool HAS_RES>
+__global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
+  constexpr int BM = 128, BN = 128;
+  constexpr int XB = BM * 128, WB = BN * 128, STG = XB + WB;
+  constexpr int OPITCH = BN * 2 + 16;
+  constexpr int LDS = 2 * STG > BM * OPITCH ? 2 * STG : BM * OPITCH;
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[LDS];
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int tm = tile / p.tiles_n;
+  const int tn = tile - tm * p.tiles_n;
+  const int m0 = tm * BM;
+  const int n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave & 1;   // pixel half of the tile
+  const int wn = wave >> 1;  // channel half
+
+  // DMA roles: wave w stages image rows 8 * (4 w + q) + (lane >> 3), q = 0..3, of both the
+  // X (pixel) and W (channel) images; the lane's 16-B chunk is pre-swizzled on the source
+  const int drow = lane >> 3;
+  const int dchunk = (lane & 7) ^ drow;
+  const unsigned nimg = (unsigned)p.M / (unsigned)(p.OH * p.OW);
+  const CSrc& S = p.s[0];
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)S.x, 0, (int)(nimg * (unsigned)(S.H * S.W) * (unsigned)S.C * 2u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.w, 0, (int)((unsigned)p.N * (unsigned)p.ldw * 2u), 0x00020000);
+  int pb[4], hw[4];
+  unsigned offw[4];
+  const int ohw = p.OH * p.OW;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 8 * (4 * wave + q) + drow;
+    const int m = m0 + r;
+    const bool live = m < p.M;
+    const int n = live ? m / ohw : 0;
+    const int rem = live ? m - n * ohw : 0;
+    const int oh = rem / p.OW;
+    const int ow = rem - oh * p.OW;
+    const int ih0 = live ? oh * S.sh - S.ph : -16384;
+    const int iw0 = ow * S.sw - S.pw;
+    pb[q] = ((n * S.H + ih0) * S.W + iw0) * S.C * 2 + dchunk * 16;
+    hw[q] = (ih0 << 16) | (iw0 & 0xFFFF);
+    const unsigned co = n0 + r;
+    offw[q] = co < (unsigned)p.N ? (co * p.ldw + dchunk * 8) * 2u : 0x80000000u;
+  }
+  // The K walk (channel chunk, filter column, filter row) advances incrementally in scalar
+  // registers: no table read inside the loop (a ktab load there is a vector load — the
+  // LDS-DMA in the loop defeats the scalar-load analysis — and stalled every K-tile).
+  const int c64 = S.C >> 6;
+  int cc = 0, kw = 0, kh = 0;
+  auto dma = [&](int kt, int stage) {
+    const int dih = kh * p.dh, diw = kw * p.dw;
+    const int delta = ((dih * S.W + diw) * S.C + cc * 64) * 2;
+    if (++cc == c64) {
+      cc = 0;
+      if (++kw == p.KW) {
+        kw = 0;
+        ++kh;
+      }
+    }
+    uint8_t* bx = smem + stage * STG + 4 * wave * 8 * 128;
+    uint8_t* bw = bx + XB;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ih = (hw[q] >> 16) + dih;
+      const int iw = ((hw[q] << 16) >> 16) + diw;
+      const bool ok = (unsigned)ih < (unsigned)S.H && (unsigned)iw < (unsigned)S.W;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(bx + q * 8 * 128), 16,
+                                               ok ? (unsigned)(pb[q] + delta) : 0x80000000u, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 8 * 128), 16,
+                                               offw[q], (unsigned)kt * 128u, 0, 0);
+    }
+  };
+
+  const int frow = lane & 15;
+  const int fq = lane >> 4;
+  f32x4 acc[4][4];  // [channel fragment i][pixel fragment j]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K >> 6;
+  dma(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) dma(kt + 1, st ^ 1);
+    const uint8_t* xs = smem + st * STG;
+    const uint8_t* ws = xs + XB;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int slot = ((ks * 4 + fq) ^ (frow & 7)) << 4;
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ws + (wn * 64 + i * 16 + frow) * 128 + slot);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(xs + (wm * 64 + j * 16 + frow) * 128 + slot);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  __syncthreads();  // every wave is done with the stage images: the epilogue tile reuses them
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int cl = wn * 64 + i * 16 + fq * 4;
+    f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias && n0 + cl < p.N) bv = *reinterpret_cast<const f32x4*>(p.bias + n0 + cl);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pl = wm * 64 + j * 16 + frow;
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[i][j][r] + bv[r];
+        if constexpr (!HAS_RES) v = apply_act<ACT>(v);
+        o[r] = f2bf(v);
+      }
+      *reinterpret_cast<bf16x4*>(smem + pl * OPITCH + cl * 2) = o;
+    }
+  }
+  __syncthreads();
+  bf16* y = reinterpret_cast<bf16*>(p.y);
+  constexpr int SEGS = BN / 8;
+#pragma unroll 4
+  for (int q = threadIdx.x; q < BM * SEGS; q += 256) {
+    const int ml = q / SEGS;
+    const int cc = q - ml * SEGS;
+    const int m = m0 + ml;
+    const int n = n0 + cc * 8;
+    if (m >= p.M || n >= p.N) continue;
+    u32x4 v = *reinterpret_cast<const u32x4*>(smem + ml * OPITCH + cc * 16);
+    if constexpr (HAS_RES) {
+      bf16x8 o = __builtin_bit_cast(bf16x8, v);
+      const bf16x8 r = *reinterpret_cast<const bf16x8*>(p.res + (size_t)m * p.ldr + n);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(apply_act<ACT>((float)o[e] + (float)r[e]));
+      v = __builtin_bit_cast(u32x4, o);
+    }
+    *reinterpret_cast<u32x4*>(y + (size_t)m * p.ldy + p.y_coff + n) = v;
+  }
+}
+
+template <int ACT>
+void launch_lite(const CPParams& p, hipStream_t s) {
+  if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true>), dim3(p.tiles_m * p.tiles_n), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((conv_lite_kernel<ACT, false>), dim3(p.tiles_m * p.tiles_n), dim3(256), 0, s, p);
+}
+
 template <int ACT, bool HAS_RES>
 __global__ __launch_bounds__(256) void conv_pp_reduce_kernel(const float* __restrict__ part, int splits,
                                                              long split_stride, const float* __restrict__ bias,
@@ -481,6 +652,11 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
     need(S.H < 16384 && S.W < 16384 && S.ph < 1024 && S.pw < 1024, "spatial size");
     need((KH - 1) * dh < 1024 && (KW - 1) * dw < 1024, "receptive field");
     K += (long)KH * KW * S.C;
+    if (i == 0) {
+      p.KW = KW;
+      p.dh = dh;
+      p.dw = dw;
+    }
   }
   for (int i = ns; i < 2; ++i) p.s[i] = p.s[0];
   need(Cout % 8 == 0 && ldy % 8 == 0 && y_coff % 8 == 0, "Cout / ldy / y_coff must be multiples of 8");
@@ -497,7 +673,9 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   p.K = (int)K;
   p.OH = OH; p.OW = OW;
   p.ldw = (int)K; p.ldy = ldy; p.y_coff = y_coff; p.ldr = ldr;
-  const int BM = tile == 1 ? 512 : 256, BN = tile == 1 ? 128 : 256;
+  need(tile >= 0 && tile <= 2, "tile must be 0 (256x256), 1 (512x128) or 2 (128x128, 4 waves)");
+  need(tile != 2 || (ns == 1 && splits <= 1), "the 4-wave tile takes one source and no split-K");
+  const int BM = tile == 1 ? 512 : tile == 2 ? 128 : 256, BN = tile == 1 ? 128 : tile == 2 ? 128 : 256;
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (Cout + BN - 1) / BN;
   const int nk = p.K / 64;
@@ -511,7 +689,13 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   float* wsp = reinterpret_cast<float*>(ws);
-  if (tile == 1) launch_tile<512, 128>(p, splits, wsp, ns == 2, act, s);
+  if (tile == 2) {
+    switch (act) {
+      case ACT_NONE: launch_lite<ACT_NONE>(p, s); break;
+      case ACT_RELU: launch_lite<ACT_RELU>(p, s); break;
+      default: throw std::invalid_argument("conv_pp: unsupported activation");
+    }
+  } else if (tile == 1) launch_tile<512, 128>(p, splits, wsp, ns == 2, act, s);
   else launch_tile<256, 256>(p, splits, wsp, ns == 2, act, s);
   FTM_CHECK_LAUNCH();
 }

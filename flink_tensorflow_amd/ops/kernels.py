@@ -543,7 +543,7 @@ def conv_pp_ktab(srcs) -> torch.Tensor:
 
 def conv_pp_tile(Cout: int) -> int:
     """0 = 256x256 tiles, 1 = 512x128 tiles (channel counts that would waste half of a
-    256-wide tile)."""
+    256-wide tile); 2 (never chosen here) = the 4-wave 128x128 ``conv_lite`` tile."""
     return 1 if Cout <= 128 or (Cout % 256 and Cout % 128 == 0) else 0
 
 
@@ -583,7 +583,10 @@ class ConvPP:
             raise ValueError("conv_pp: Cout % 8")
         self.M = self.N * self.OH * self.OW
         self.tile = conv_pp_tile(Cout) if tile is None else tile
-        self.splits = conv_pp_splits(self.M, Cout, self.K, self.tile) if splits is None else splits
+        if self.tile == 2 and len(self.srcs) != 1:
+            raise ValueError("conv_pp: the 4-wave 128x128 tile takes one source")
+        self.splits = (1 if self.tile == 2 else conv_pp_splits(self.M, Cout, self.K, self.tile)) if splits is None \
+            else splits
         self.ktab = conv_pp_ktab([(xs[1], xs[2], xs[3], k[0], k[1], dl[0], dl[1])
                                   for xs, k, _, _, dl in self.srcs]).to(device)
         self.ws = (torch.empty(self.splits * self.M * Cout, dtype=torch.float32, device=device)
