@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--workers", type=int, default=8)
     ap.add_argument("--records", type=int, default=40000)
     ap.add_argument("--hw", type=int, default=256)
+    ap.add_argument("--remote-source", action="store_true",
+                    help="the parallel source runs inside the worker processes, chained with the map "
+                         "(records are produced where they are consumed; nothing crosses the coordinator)")
     a = ap.parse_args()
     from flink_tensorflow_amd.runtime import StreamExecutionEnvironment
     from flink_tensorflow_amd.runtime.sources import ThroughputSink
@@ -29,14 +32,23 @@ def main():
     pool = [np.random.default_rng(i).integers(0, 256, (a.hw, a.hw, 3), dtype=np.uint8) for i in range(64)]
     n = a.records
 
+    hw = a.hw
+
     def images(idx, par, start):
-        for i in range(start, n):
-            if i % par == idx:
-                yield pool[i % len(pool)]
+        # this subtask's share of the n records; ``start`` = how many of them it already emitted
+        import numpy as _np
+
+        local = [_np.random.default_rng(i).integers(0, 256, (hw, hw, 3), dtype=_np.uint8) for i in range(16)]
+        for k, i in enumerate(range(idx, n, par)):
+            if k >= start:
+                yield local[i % len(local)].copy()  # a freshly produced record (decode / read), not a shared buffer
 
     env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(a.workers)
     sink = ThroughputSink(every=512)
-    env.generate(images).map(_touch).run_in_processes().add_sink(sink, parallelism=1)
+    src = env.generate(images)
+    if a.remote_source:
+        src = src.run_in_processes()
+    src.map(_touch).run_in_processes().add_sink(sink, parallelism=1)
     t0 = time.perf_counter()
     env.execute("transport")
     el = time.perf_counter() - t0
@@ -45,7 +57,8 @@ def main():
     print(json.dumps({"workers": a.workers, "records": got, "record_bytes": pool[0].nbytes, "seconds": round(el, 3),
                       "steady_records_per_s": round(steady, 1),
                       "steady_GB_per_s": round(steady * pool[0].nbytes / 1e9, 2),
-                      "slab": os.environ.get("FTM_SLAB_BYTES", "default") != "0", "cpus": os.cpu_count()}),
+                      "slab": os.environ.get("FTM_SLAB_BYTES", "default") != "0", "cpus": os.cpu_count(),
+                      "mode": "in-worker parallel source" if a.remote_source else "coordinator source -> workers"}),
           flush=True)
     assert got == n
 

@@ -38,7 +38,9 @@ class EngineConfig:
     channel_capacity: int = 1024
     log_level: str = "INFO"
     # ---- compiler / kernel selection (measured choices; FT_<NAME> env vars or YAML)
-    conv_impl: str = "incumbent"       # implicit-GEMM convs: incumbent | auto (probe conv_pp) | pp
+    conv_impl: str = "lite"            # implicit-GEMM convs: lite (4-wave LDS-DMA conv_lite) | incumbent
+    #                                    (register-staged igemm) | auto (probe conv_pp) | pp
+    conv_lite_pointwise: bool = True   # deep-K 1x1 reduces (K >= 1024) on conv_lite instead of gemm_pp
     fuse_block_tails: bool = True      # ResNet block boundary: expand + next reduce in one kernel
     fuse_wide_tails: bool = False      # ... also for stage 2 (weights streamed; measured no gain)
     decimate_tails: bool = True        # stage-1 tail output stored at the stride-2 reader's pixels
@@ -128,8 +130,8 @@ class EngineConfig:
             raise ValueError("max_batch >= 1 and max_delay_ms >= 0 required")
         if self.precision not in ("bf16", "fp8"):
             raise ValueError("precision must be bf16 or fp8")
-        if self.conv_impl not in ("incumbent", "auto", "pp"):
-            raise ValueError("conv_impl must be incumbent, auto or pp")
+        if self.conv_impl not in ("lite", "incumbent", "auto", "pp"):
+            raise ValueError("conv_impl must be lite, incumbent, auto or pp")
         if not 0 < self.arena_fraction <= 1:
             raise ValueError("arena_fraction must be in (0, 1]")
         if self.batch_buckets and sorted(self.batch_buckets) != list(self.batch_buckets):

@@ -778,6 +778,20 @@ class CompiledFunction(TransformerLowering):
             w_nk = w_dev.reshape(Cout, Cin)
             bz = b_dev if b_dev is not None else self._dev(torch.zeros(Cout), torch.float32)
             M = int(np.prod(xin.shape[:-1]))
+            if _cfg().conv_impl == "lite" and _cfg().conv_lite_pointwise and Cin >= 1024 and len(xin.shape) == 4:
+                # stage 3/4 reduces: the 4-wave LDS-DMA tile beats the 256x256 ping-pong GEMM
+                # (stage 3: 37.8 vs 43.5 µs, profiles/r03_conv) and leaves room on the CU
+                cl = K.ConvPP([(tuple(xin.shape), (1, 1), (1, 1), (0, 0), (1, 1))], Cout, tuple(out.shape[1:3]),
+                              self.device, tile=2)
+
+                def run_cl(xin=xin, out=out, cl=cl, w_nk=w_nk, bz=bz, act=act):
+                    cl([xin.buf], w_nk, bz, None, act, out=_target(out), out_channel_offset=_coff(out))
+
+                self._emit(node.name, "conv", run_cl, [xin], [out], {"impl": "conv_lite"})
+                self.conv_lite_layers = getattr(self, "conv_lite_layers", 0) + 1
+                self.vals[(last.name, 0)] = out
+                self._alias_fused_outputs(absorbed, out)
+                return
             splits = K.gemm_pp_splits(M, Cout, Cin)
             ws = torch.empty(splits * M * Cout, dtype=torch.float32, device=self.device) if splits > 1 else None
 
@@ -819,7 +833,26 @@ class CompiledFunction(TransformerLowering):
                           (pt, pb, pl, pr), (dh, dw), act, out=_target(out), out_channel_offset=_coff(out),
                           out_scale=_eff_scale(out) if out.qscale is not None else None)
 
-        if out.qscale is None and xin_shape_override is None and (xin.phys_c or Cin) == Cin:
+        lite = (self.device.type == "cuda" and _cfg().conv_impl == "lite" and out.qscale is None
+                and xin_shape_override is None and (xin.phys_c or Cin) == Cin and Cin % 64 == 0 and Cout % 8 == 0
+                and _coff(out) % 8 == 0 and out.dtype == torch.bfloat16 and xin.dtype == torch.bfloat16
+                and not pointwise and act in (K.ACT_NONE, K.ACT_RELU)
+                and (res_val is None or (res_val.concat_slot is None and res_val.qscale is None
+                                         and tuple(res_val.shape) == tuple(out.shape) and res_val.alias_of is None))
+                and max(pt, pb) < 1024 and max(pl, pr) < 1024)
+        if lite:
+            # KxK convs (stage 2-4 3x3): 4-wave 128x128 implicit GEMM on two LDS-DMA stages
+            # (kernels/conv_pp.hip conv_lite): 6-24 % faster than the register-staged igemm
+            # per layer and 64 KiB of LDS, so it shares a CU with the sibling lane
+            cl = K.ConvPP([(tuple(xin.shape), (KHe, KWe), (sh, sw), (pt, pl), (dh, dw))], Cout, tuple(out.shape[1:3]),
+                          self.device, tile=2)
+
+            def run(xin=xin, out=out, res_val=res_val, cl=cl, w2=w_dev.reshape(Cout, -1), b_dev=b_dev):  # noqa: F811
+                cl([xin.buf], w2, b_dev, res_val.buf if res_val is not None else None, act, out=_target(out),
+                   out_channel_offset=_coff(out))
+
+            self.conv_lite_layers = getattr(self, "conv_lite_layers", 0) + 1
+        elif out.qscale is None and xin_shape_override is None and (xin.phys_c or Cin) == Cin:
             pp = self._conv_pp_choice(node.name, [(tuple(xin.shape), (KHe, KWe), (sh, sw), (pt, pl), (dh, dw))],
                                       Cout, out, res_val, act, w_dev, b_dev,
                                       lambda xs, o, r: K.conv2d_nhwc(xs[0], w_dev, b_dev, r, (sh, sw),
@@ -998,7 +1031,7 @@ class CompiledFunction(TransformerLowering):
         (profiles/r02_conv_pp); ``conv_impl = "auto"`` enables the probe, ``"pp"`` forces
         conv_pp wherever eligible."""
         force = _cfg().conv_impl
-        if self.device.type != "cuda" or force == "incumbent" or self.precision == "fp8":
+        if self.device.type != "cuda" or force in ("incumbent", "lite") or self.precision == "fp8":
             return None
         if any(s[0][3] % 64 for s in srcs) or Cout % 8 or _coff(out) % 8 or out.dtype != torch.bfloat16:
             return None
@@ -1752,6 +1785,7 @@ class CompiledFunction(TransformerLowering):
                 "fused_tails": getattr(self, "fused_tails", 0), "decimated_tails": getattr(self, "decimated_tails", 0),
                 "fused_pools": getattr(self, "fused_pools", 0), "conv3x3c64": getattr(self, "conv3x3c64", 0),
                 "conv_pp": getattr(self, "conv_pp_layers", 0), "pw_res": getattr(self, "pw_res_layers", 0),
+                "conv_lite": getattr(self, "conv_lite_layers", 0),
                 "activation_bytes": self.activation_bytes,
                 "param_bytes": self.param_bytes(),
                 **({"token_capacity": self.token_cap, "first_token_only_nodes": len(self._cls_nodes)}

@@ -278,6 +278,56 @@ class _SourceTask(_Task):
         self.writer.emit(END)
 
 
+class _RemoteSourceTask(_Task):
+    """A source subtask running in a worker process together with its chained worker
+    operators (``runtime/remote.py`` ``RemoteChainProxy``).  This coordinator thread only
+    forwards checkpoint triggers and waits for the end of input; the proxy's drainer
+    emits the chain's output, acks the members' snapshots and forwards barriers."""
+
+    def __init__(self, job, node, subtask, writer, restore, chain: list):
+        super().__init__(job, node, subtask, writer, restore)
+        from .remote import RemoteChainProxy
+
+        self.pending_trigger: deque[int] = deque()
+        self.chain = chain
+        self.op = RemoteChainProxy([node] + [t.node for t in chain], subtask, job)
+        self.op.fn = self.op  # job.fail() cancels sources through ``op.fn.cancel()``
+        for t in chain:  # members live in the worker: notifications go through the proxy
+            t.op = _WorkerMember()
+
+    def run(self):
+        proxy = self.op
+        proxy.setup(self.runtime_context(), Output(self.writer.emit, self.writer.emit_side))
+        contexts = [self.runtime_context()] + [t.runtime_context() for t in self.chain]
+        proxy.start_chain(contexts, [self.restore] + [t.restore for t in self.chain], self.job.restore_dir)
+        try:
+            def poll():
+                while self.pending_trigger:
+                    cid = self.pending_trigger.popleft()
+                    proxy.trigger(cid, self.job.chk_dir(cid))
+                if self.job.cancel.is_set():
+                    proxy.cancel()
+                    raise JobCancelled()
+
+            self.final_state = proxy.wait_source_end(poll)
+        except BaseException:
+            proxy._shutdown()
+            raise
+        proxy.close()  # the drainer has re-emitted everything up to the source's end
+        for t, m in zip(self.chain, getattr(proxy, "member_metrics", [])):
+            t.op.worker_metrics = m
+        self.writer.emit(END)
+
+
+class _WorkerMember:
+    """Stand-in operator of a chain member that runs inside a worker-process source chain."""
+
+    worker_metrics = None
+
+    def notify_checkpoint_complete(self, checkpoint_id):
+        pass  # the chain's proxy notifies the whole worker chain once
+
+
 class _ChainedTask(_Task):
     """A subtask chained into its upstream subtask's thread (Flink's operator chaining:
     forward edge, equal parallelism, single input, single consumer).  It has no thread and
@@ -513,6 +563,8 @@ class LocalExecutor:
         ops = {(n.uid, i): n.make_operator() for n in nodes if not n.is_source and not getattr(n, "remote", False)
                for i in range(n.parallelism)}
         chained_to = self._chains(nodes, ops)  # downstream uid -> upstream node it runs inside
+        remote_chained = self._remote_source_chains(nodes)  # chained into a worker-process source
+        chained_to.update(remote_chained)
         gates: dict[tuple[str, int], InputGate] = {}
         chan_of: dict[tuple[str, int], list] = {}
         for n in nodes:
@@ -552,6 +604,14 @@ class LocalExecutor:
             for i in range(n.parallelism):
                 w = RecordWriter(out_edges[(tail.uid, i)], i, self.cancel)
                 rs = restore_states.get((n.uid, i)) if restore_states else None
+                if n.is_source and getattr(n, "remote", False):
+                    chain = [_ChainedTask(self, m, i, restore_states.get((m.uid, i)) if restore_states else None, None)
+                             for m in members]
+                    t = _RemoteSourceTask(self, n, i, w, rs, chain)
+                    self.sources.append(t)
+                    self.tasks.append(t)
+                    self.tasks.extend(chain)
+                    continue
                 if n.is_source:
                     t = _SourceTask(self, n, i, w, rs)
                     self.sources.append(t)
@@ -562,6 +622,32 @@ class LocalExecutor:
                 self.tasks.append(_OpTask(self, n, i, w, rs, gates[(n.uid, i)], chan_of[(n.uid, i)],
                                           ops.get((n.uid, i)), chain))
                 self.tasks.extend(chain)
+
+    def _remote_source_chains(self, nodes) -> dict:
+        """Worker-process sources: the downstream worker operators they run together with
+        (forward edge, equal parallelism, single input, single consumer, chaining allowed)
+        — ``member uid -> upstream node``."""
+        consumers: dict[str, int] = {}
+        for n in nodes:
+            for up, _, _ in n.inputs:
+                consumers[up.uid] = consumers.get(up.uid, 0) + 1
+        out = {}
+        for src in nodes:
+            if not (src.is_source and getattr(src, "remote", False)):
+                continue
+            cur = src
+            while consumers.get(cur.uid) == 1:
+                nxt = next(n for n in nodes if any(up is cur for up, _, _ in n.inputs))
+                if len(nxt.inputs) != 1:
+                    break
+                up, part, side_tag = nxt.inputs[0]
+                if not (getattr(nxt, "remote", False) and side_tag is None and part.kind == "forward"
+                        and nxt.parallelism == cur.parallelism and getattr(nxt, "chaining", True)
+                        and not getattr(nxt, "chain_head", False)):
+                    break
+                out[nxt.uid] = cur
+                cur = nxt
+        return out
 
     def _chains(self, nodes, ops) -> dict:
         """Operator chaining (Flink's ``StreamingJobGraphGenerator.isChainable``): a node runs

@@ -21,14 +21,26 @@ shape, dtype) crosses the ring; the worker hands the operator a zero-copy view o
 returns the space when the view is garbage collected.  Small values, object payloads and a
 full slab fall back to the pickle.
 
+**Remote source chains** (``env.generate(...).run_in_processes()``): a source subtask can
+run in the worker too, with the forward-connected, equal-parallelism worker operators
+downstream of it chained into the same process (Flink's chained source in a task slot).
+Records are then produced, mapped and consumed inside the worker — nothing crosses the
+coordinator — so a parallel source feeds N model workers at the rate of N processes, not
+of one coordinator thread.  Checkpoint triggers travel to the worker, which snapshots the
+source offset and every chained operator between two records and sends the states and
+the barrier INLINE in its output stream (ordered after everything emitted before it).
+
 Messages (cloudpickle, fragmented when larger than half a ring):
 
 =====================  ==============================================================
 coordinator → worker   ``init`` (operator factory, context, restore state), ``recs``
                        [(value, ts, input)], ``wm`` ts, ``snap`` (id, dir), ``notify``
-                       id, ``end``, ``close``
+                       id, ``end``, ``close``; source chains: ``init_chain`` (factories,
+                       contexts, restore states), ``trigger`` (id, dir), ``cancel``
 worker → coordinator   ``out`` [elements], ``side`` [(tag, value)], ``state`` (id, state),
-                       ``ended``, ``closed`` (metrics), ``error`` (message, traceback)
+                       ``ended``, ``closed`` (metrics), ``error`` (message, traceback);
+                       source chains: ``barrier`` (id, ts, [state per chain member]),
+                       ``source_end`` (final source state)
 =====================  ==============================================================
 """
 from __future__ import annotations
@@ -337,6 +349,10 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
                 break
             if not parent_alive():
                 return  # coordinator gone
+        if msg[0] == "init_chain":
+            _run_source_chain(msg, inp, out, emit, flush, parent_alive)
+            op = None
+            return
         kind, factory, spec, restore, restore_dir = msg
         assert kind == "init", kind
         from .functions import RuntimeContext
@@ -417,6 +433,152 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
                 pass
         out.close()
 
+
+
+class _ChainCancelled(Exception):
+    pass
+
+
+def _worker_device(spec):
+    if not spec["gpu"]:
+        return None
+    import torch
+
+    if not torch.cuda.is_available():
+        return None
+    from ..parallel.comm import gpu_count
+
+    device = torch.device("cuda", spec["subtask"] % max(1, gpu_count()))
+    torch.cuda.set_device(device)
+    return device
+
+
+def _run_source_chain(msg, inp, out, emit, flush, parent_alive):
+    """Worker side of a remote source chain: the source function runs here and every record
+    goes straight through the chained operators; only the chain's output leaves."""
+    from .functions import RuntimeContext, SourceContext
+    from ..utils.metrics import MetricGroup
+
+    _, factories, specs, restores, restore_dir = msg
+    ops = [cloudpickle.loads(f)() for f in factories]
+    metrics = []
+    device = _worker_device(specs[0]) if any(sp["gpu"] for sp in specs) else None
+
+    def side(tag, v):
+        flush()
+        out.send(("side", [(tag, v)]), alive=parent_alive)
+
+    def into(nxt):
+        def e(elem):
+            if type(elem) is Record:
+                nxt.process(elem, 0)
+            elif isinstance(elem, Watermark):
+                nxt.process_watermark(elem, 0)
+            else:
+                raise TypeError(f"operators emit records and watermarks, not {type(elem).__name__}")
+        return e
+
+    for i, (op, sp) in enumerate(zip(ops, specs)):
+        mg = MetricGroup(f"{sp['name']}[{sp['subtask']}]")
+        metrics.append(mg)
+        ctx = RuntimeContext(sp["name"], sp["subtask"], sp["parallelism"], device if sp["gpu"] else None,
+                             sp["attempt"], mg, sp["config"], None)
+        ctx.global_index, ctx.global_parallelism = sp["global_index"], sp["global_parallelism"]
+        ctx.worker_pid = os.getpid()
+        op.setup(ctx, Output(into(ops[i + 1]) if i + 1 < len(ops) else emit, side))
+        op.initialize(restores[i], restore_dir)
+    for op in reversed(ops):
+        op.open()
+    head = into(ops[1]) if len(ops) > 1 else emit
+    src, fn = ops[0], ops[0].fn
+    lock = threading.RLock()
+    last = [time.perf_counter()]
+    recs_out = [0]
+
+    def control(m):
+        kind = m[0]
+        if kind == "trigger":
+            cid, d = m[1], m[2]
+            with lock:
+                for o in ops[1:]:
+                    o.prepare_snapshot()
+                states = [o.snapshot_state(cid, d) for o in ops]
+                flush()
+                out.send(("barrier", cid, time.time(), states), alive=parent_alive)
+        elif kind == "notify":
+            for o in ops:
+                o.notify_checkpoint_complete(m[1])
+        elif kind == "cancel":
+            fn.cancel()
+            raise _ChainCancelled()
+        else:
+            raise RemoteTaskError(f"unexpected {kind!r} while the source runs")
+
+    def poll(force=False):
+        now = time.perf_counter()
+        if not force and now - last[0] < 1e-3:
+            return
+        last[0] = now
+        while True:
+            m = inp.recv(0.0)
+            if m is None:
+                break
+            control(m)
+        if not parent_alive():
+            raise _ChainCancelled()
+        for o in ops[1:]:
+            o.on_idle(time.time())
+        flush()
+
+    class Ctx(SourceContext):
+        @property
+        def checkpoint_lock(self):
+            return lock
+
+        def collect(self, value, timestamp=None):
+            poll()
+            head(Record(value, timestamp))
+            recs_out[0] += 1
+
+        def emit_watermark(self, ts):
+            head(Watermark(ts))
+
+    try:
+        fn.run(Ctx())
+        with lock:
+            poll(force=True)  # triggers that arrived before the end still get their barrier
+            final = src.snapshot_state(-1, None)
+        head(Watermark(float("inf")))
+        for o in ops[1:]:
+            o.end_input()
+        flush()
+        out.send(("source_end", final), alive=parent_alive)
+        while True:  # late notifications, then close
+            m = inp.recv(_IDLE_S)
+            if m is None:
+                if not parent_alive():
+                    return
+                continue
+            if m[0] == "notify":
+                for o in ops:
+                    o.notify_checkpoint_complete(m[1])
+            elif m[0] == "close":
+                break
+            elif m[0] == "cancel":
+                return
+        for o in ops:
+            o.close()
+        ops = []
+        metrics[0].inc("records_out", recs_out[0])
+        out.send(("closed", [mg.snapshot() for mg in metrics]), alive=parent_alive)
+    except _ChainCancelled:
+        pass
+    finally:
+        for o in ops:
+            try:
+                o.close()
+            except Exception:  # noqa: BLE001
+                pass
 
 # ------------------------------------------------------------------ coordinator side
 class RemoteOperatorProxy:
@@ -548,6 +710,9 @@ class RemoteOperatorProxy:
     def notify_checkpoint_complete(self, checkpoint_id: int):
         self._send(("notify", checkpoint_id))
 
+    def _on_barrier(self, msg):
+        raise RemoteTaskError(f"{self.node.name}[{self.subtask}]: unexpected barrier from an operator worker")
+
     # ---- plumbing
     def _alive(self) -> bool:
         return self.proc is not None and self.proc.is_alive()
@@ -615,6 +780,8 @@ class RemoteOperatorProxy:
                 elif kind == "error":
                     self._error = (msg[1], msg[2])
                     return
+                elif kind == "barrier":
+                    self._on_barrier(msg)
                 else:
                     if kind == "closed":
                         self.worker_metrics = msg[1]
@@ -624,3 +791,93 @@ class RemoteOperatorProxy:
             except Exception as e:  # noqa: BLE001 - e.g. a cancelled downstream
                 self._error = (f"{type(e).__name__}: {e}", traceback.format_exc())
                 return
+
+
+class RemoteChainProxy(RemoteOperatorProxy):
+    """Coordinator side of a remote source chain (``nodes[0]`` the source, then the chained
+    worker operators).  The drainer re-emits the chain's output, acknowledges each member's
+    snapshot and forwards the barrier when the worker's inline ``barrier`` message arrives."""
+
+    def __init__(self, nodes, subtask: int, job, ring_bytes: int = _RING_BYTES):
+        super().__init__(nodes[0], subtask, job, ring_bytes)
+        self.nodes = list(nodes)
+        self.final_state = None
+
+    def start_chain(self, contexts, restores, checkpoint_dir):
+        try:
+            self._start_chain(contexts, restores, checkpoint_dir)
+        except BaseException:
+            self._shutdown()
+            raise
+
+    def _start_chain(self, contexts, restores, checkpoint_dir):
+        import multiprocessing as mp
+
+        tag = f"/ftm-{os.getpid()}-{uuid.uuid4().hex[:10]}"
+        self.to_worker = ShmChannel(tag + "-in", True, self.ring_bytes)
+        self.from_worker = ShmChannel(tag + "-out", True, self.ring_bytes)
+        name = "+".join(n.name for n in self.nodes)
+        self.proc = mp.get_context("spawn").Process(target=_worker_main, name=f"ftm-{name}-{self.subtask}",
+                                                    args=(self.to_worker.name, self.from_worker.name, None),
+                                                    daemon=True)
+        self.proc.start()
+        self._drainer = threading.Thread(target=self._drain, name=f"drain-{name}-{self.subtask}", daemon=True)
+        self._drainer.start()
+        self._wait("attached", 120.0)
+        self.to_worker.unlink()
+        self.from_worker.unlink()
+        specs = [{"name": n.name, "subtask": self.subtask, "parallelism": n.parallelism, "gpu": bool(n.uses_gpu),
+                  "attempt": self.job.attempt, "config": self.job.config, "global_index": c.global_index,
+                  "global_parallelism": c.global_parallelism} for n, c in zip(self.nodes, contexts)]
+        self._send(("init_chain", [cloudpickle.dumps(n.factory) for n in self.nodes], specs, list(restores),
+                    checkpoint_dir))
+
+    def trigger(self, checkpoint_id: int, checkpoint_dir):
+        self._send(("trigger", checkpoint_id, checkpoint_dir))
+
+    def cancel(self):
+        if self._alive():
+            try:
+                self.to_worker.send(("cancel",), timeout_s=1.0)
+            except Exception:  # noqa: BLE001
+                pass
+
+    def wait_source_end(self, cancel) -> object:
+        """Blocks until the worker's source finished (its final state), raising on a worker
+        failure or a cancelled job; ``cancel()`` is polled between waits."""
+        while True:
+            self._check()
+            try:
+                msg = self._replies.get(timeout=0.05)
+            except queue.Empty:
+                cancel()
+                continue
+            if msg[0] != "source_end":
+                raise RemoteTaskError(f"{self.node.name}[{self.subtask}]: expected 'source_end', got {msg[0]!r}")
+            self.final_state = msg[1]
+            return msg[1]
+
+    def close(self):
+        graceful = False
+        try:
+            if self._alive() and self._error is None and not self.job.cancel.is_set():
+                self._send(("close",))
+                self._wait("closed", 60.0)
+                graceful = True
+        finally:
+            self._shutdown(graceful)
+
+    def _drain(self):
+        super()._drain()
+        m = self.worker_metrics  # the chain sends one snapshot per member: the source's is the proxy's
+        if isinstance(m, list):
+            self.member_metrics = m[1:]
+            self.worker_metrics = m[0] if m else None
+
+    def _on_barrier(self, msg):
+        from .operators import Barrier
+
+        _, cid, ts, states = msg
+        for n, st in zip(self.nodes, states):
+            self.job.ack(cid, (n.uid, self.subtask), st)
+        self.out._emit(Barrier(cid, ts))

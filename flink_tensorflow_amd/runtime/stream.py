@@ -183,9 +183,13 @@ class DataStream:
 
     def run_in_processes(self, enable: bool = True) -> "DataStream":
         """Runs each subtask of this operator in its own worker process (one per GPU for
-        model operators), fed through shared-memory rings (``runtime/remote.py``)."""
-        if self.node.is_source:
-            raise ValueError("sources run in the coordinator process")
+        model operators), fed through shared-memory rings (``runtime/remote.py``).
+
+        On a source, the source subtasks run in the workers too, and every downstream
+        operator that also runs in processes and is forward-connected with equal parallelism
+        (single input, single consumer) is chained into the same worker: records are
+        produced and consumed there and never cross the coordinator (a parallel source
+        feeding one model worker per GPU)."""
         self.node.remote = bool(enable)
         return self
 

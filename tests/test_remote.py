@@ -255,3 +255,46 @@ def test_tensor_slab_keeps_records_alive_through_derived_views(monkeypatch):
     env = StreamExecutionEnvironment.get_execution_environment()
     got = env.from_collection(vals).map(_KeepDerived()).run_in_processes().execute_and_collect()
     assert got == want
+
+
+def _own_partition(n, delay_s=0.0):
+    def gen(idx, par, start):
+        import time as _t
+
+        for v in [i for i in range(1, n + 1) if i % par == idx][start:]:
+            if delay_s:
+                _t.sleep(delay_s)
+            yield v
+    return gen
+
+
+def test_remote_source_chain_runs_in_workers():
+    """A worker-process source with its worker-process map chained into the same process:
+    records are produced and mapped in the workers (never through the coordinator); only
+    the map's output comes back."""
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    out = env.generate(_own_partition(400)).run_in_processes() \
+        .map(lambda v: (os.getpid(), v * 3)).run_in_processes().execute_and_collect()
+    assert sorted(v for _, v in out) == [3 * i for i in range(1, 401)]
+    pids = {p for p, _ in out}
+    assert len(pids) == 2 and os.getpid() not in pids
+
+
+def test_remote_source_chain_checkpoint_restart(tmp_path):
+    """Checkpoints of a worker-process source chain: triggers reach the worker, which
+    snapshots the source offset and the chained operators between two records and sends
+    the barrier inline; after a failure inside the chain the job restarts from the last
+    checkpoint and every keyed running sum downstream is exact (no record lost or
+    duplicated)."""
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    env.enable_checkpointing(0.05, str(tmp_path / "chk"))
+    env.set_restart_strategy(RestartStrategy.fixed_delay(2, 0.0))
+    sink = env.generate(_own_partition(300, delay_s=0.002)).run_in_processes() \
+        .map(FailAfter(100, attempts=(0,))).run_in_processes() \
+        .key_by(lambda v: v % 3).process(_RunningSum()).collect_into()
+    res = env.execute("remote-source-recover")
+    assert res.attempts == 1 and len(res.checkpoints) >= 1
+    final = {}
+    for k, t in sink.results():
+        final[k] = max(final.get(k, 0), t)
+    assert final == {k: sum(v for v in range(1, 301) if v % 3 == k) for k in range(3)}
