@@ -40,7 +40,8 @@ class EngineConfig:
     # ---- compiler / kernel selection (measured choices; FT_<NAME> env vars or YAML)
     conv_impl: str = "lite"            # implicit-GEMM convs: lite (4-wave LDS-DMA conv_lite) | incumbent
     #                                    (register-staged igemm) | auto (probe conv_pp) | pp
-    conv_lite_pointwise: bool = True   # deep-K 1x1 reduces (K >= 1024) on conv_lite instead of gemm_pp
+    conv_lite_pointwise: bool = False  # deep-K 1x1 reduces (K >= 1024) on conv_lite instead of gemm_pp
+    conv_lite_max_m: int = 0           # conv_lite only for layers of at most this many output pixels (0: any)
     fuse_block_tails: bool = True      # ResNet block boundary: expand + next reduce in one kernel
     fuse_wide_tails: bool = False      # ... also for stage 2 (weights streamed; measured no gain)
     decimate_tails: bool = True        # stage-1 tail output stored at the stride-2 reader's pixels

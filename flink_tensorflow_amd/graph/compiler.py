@@ -839,7 +839,8 @@ class CompiledFunction(TransformerLowering):
                 and not pointwise and act in (K.ACT_NONE, K.ACT_RELU)
                 and (res_val is None or (res_val.concat_slot is None and res_val.qscale is None
                                          and tuple(res_val.shape) == tuple(out.shape) and res_val.alias_of is None))
-                and max(pt, pb) < 1024 and max(pl, pr) < 1024)
+                and max(pt, pb) < 1024 and max(pl, pr) < 1024
+                and (not _cfg().conv_lite_max_m or int(np.prod(out.shape[:3])) <= _cfg().conv_lite_max_m))
         if lite:
             # KxK convs (stage 2-4 3x3): 4-wave 128x128 implicit GEMM on two LDS-DMA stages
             # (kernels/conv_pp.hip conv_lite): 6-24 % faster than the register-staged igemm
@@ -1149,11 +1150,18 @@ class CompiledFunction(TransformerLowering):
             self._alias_fused_outputs(absorbed, out)
             return
 
-        def run(x=x, out=out, wq=wq_dev, ws=ws_dev, cs=cs_dev, b=b_dev, x_scale=x_scale):
-            F8.conv2d_nhwc_fp8(_view(x), x_scale, wq, (KH, KW), ws, b, stride, pads, dil, act,
-                               out_scale=_eff_scale(out), out=_target(out), out_channel_offset=_coff(out), chan_scale=cs)
+        # fp8 input: the 4-wave LDS-DMA tile (kernels/fp8.hip conv_lite_fp8, cfg 8); a bf16
+        # input (the layer after the stem) is quantised on load by the register-staged kernel
+        cfg = 8 if (x.qscale is not None and _cfg().conv_impl == "lite") else -1
 
-        self._emit(node.name, "conv_fp8", run, [x], [out])
+        def run(x=x, out=out, wq=wq_dev, ws=ws_dev, cs=cs_dev, b=b_dev, x_scale=x_scale, cfg=cfg):
+            F8.conv2d_nhwc_fp8(_view(x), x_scale, wq, (KH, KW), ws, b, stride, pads, dil, act,
+                               out_scale=_eff_scale(out), out=_target(out), out_channel_offset=_coff(out), chan_scale=cs,
+                               cfg=cfg)
+
+        self._emit(node.name, "conv_fp8", run, [x], [out], {"impl": "conv_lite_fp8"} if cfg == 8 else None)
+        if cfg == 8:
+            self.conv_lite_layers = getattr(self, "conv_lite_layers", 0) + 1
         self.vals[(last.name, 0)] = out
         self._alias_fused_outputs(absorbed, out)
 

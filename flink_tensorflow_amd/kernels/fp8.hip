@@ -328,6 +328,200 @@ void launch_tile(const Fp8Params& p, int act, int cfg, hipStream_t s) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// conv_lite_fp8: the fp8 counterpart of conv_pp.hip's conv_lite — a 128x128 tile of four
+// waves (64 x 64 outputs each, one v_mfma_scale_f32_16x16x128_f8f6f4 per fragment pair
+// and K-tile) on two 32 KiB LDS stages filled by buffer_load ... lds (no VGPR staging, no
+// ds_write), one barrier per K-tile, so two workgroups (or one and a sibling lane's
+// kernel) share a CU.  The K walk is per lane: each lane stages one fixed logical 16-B
+// chunk of every K-tile (the XOR swizzle is applied on the source address), so any
+// Cin % 16 == 0 works (Inception's 192 / 288 / 768 ...): the lane's (filter tap, channel)
+// advances by divmod(128, Cin) per K-tile — no divides in the loop — and chunks past K or
+// in the zero padding read zeros through the buffer range check.  Epilogue as
+// igemm_fp8_kernel (per-channel dequant scale + bias + act, e4m3 or bf16 output at a
+// channel offset of a wider buffer).
+// ---------------------------------------------------------------------------------------
+template <bool OUT_FP8, int ACT>
+__global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p) {
+  constexpr int BM = 128, BN = 128;
+  constexpr int XB = BM * BK, WB = BN * BK, STG = XB + WB;
+  constexpr int OB = OUT_FP8 ? 1 : 2;
+  constexpr int OLD = BN * OB + 16;
+  constexpr int LDS = 2 * STG > BM * OLD ? 2 * STG : BM * OLD;
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[LDS];
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int tm = tile / p.tiles_n;
+  const int tn = tile - tm * p.tiles_n;
+  const int m0 = tm * BM;
+  const int n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+
+  const int drow = lane >> 3;
+  const int dchunk = (lane & 7) ^ drow;  // this lane's logical 16-B chunk of every K-tile
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.x, 0, (int)((unsigned)p.N * (unsigned)(p.H * p.W) * (unsigned)p.Cin), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.w, 0, (int)((unsigned)p.Cout * (unsigned)p.K), 0x00020000);
+  int pb[4], ihw[4];
+  unsigned wrow[4];
+  const int ohw = p.Ho * p.Wo;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 8 * (4 * wave + q) + drow;
+    const int m = m0 + r;
+    const bool live = m < p.M;
+    const int n = live ? m / ohw : 0;
+    const int rem = live ? m - n * ohw : 0;
+    const int oh = rem / p.Wo;
+    const int ow = rem - oh * p.Wo;
+    const int ih0 = live ? oh * p.sh - p.ph : -16384;
+    const int iw0 = ow * p.sw - p.pw;
+    pb[q] = ((n * p.H + ih0) * p.W + iw0) * p.Cin;
+    ihw[q] = (ih0 << 16) | (iw0 & 0xFFFF);
+    const unsigned co = n0 + r;
+    wrow[q] = co < (unsigned)p.Cout ? co * (unsigned)p.K : 0x80000000u;
+  }
+  // K walk of this lane's chunk: k = kt * 128 + dchunk * 16 -> (tap, ci), tap -> (kh, kw)
+  const int ntaps = p.KH * p.KW;
+  const int kq = BK / p.Cin, kr = BK - kq * p.Cin;
+  int k = dchunk * 16;
+  int tap = k / p.Cin;
+  int ci = k - tap * p.Cin;
+  int kh = tap / p.KW;
+  int kw = tap - kh * p.KW;
+  auto dma = [&](int stage) {
+    const bool kin = tap < ntaps;
+    const int dih = kh * p.dh, diw = kw * p.dw;
+    const int toff = (dih * p.W + diw) * p.Cin + ci;
+    uint8_t* bx = smem + stage * STG + 4 * wave * 8 * BK;
+    uint8_t* bw = bx + XB;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ih = (ihw[q] >> 16) + dih;
+      const int iw = ((ihw[q] << 16) >> 16) + diw;
+      const bool ok = kin && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(bx + q * 8 * BK), 16,
+                                               ok ? (unsigned)(pb[q] + toff) : 0x80000000u, 0, 0, 0);
+      const unsigned wo = (k < p.K && wrow[q] != 0x80000000u) ? wrow[q] + (unsigned)k : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 8 * BK), 16,
+                                               wo, 0, 0, 0);
+    }
+    // advance to the next K-tile
+    k += BK;
+    ci += kr;
+    int dt = kq;
+    if (ci >= p.Cin) {
+      ci -= p.Cin;
+      ++dt;
+    }
+    tap += dt;
+    kw += dt;
+    while (kw >= p.KW) {
+      kw -= p.KW;
+      ++kh;
+    }
+  };
+
+  const int frow = lane & 15;
+  const int c0 = 2 * (lane >> 4);
+  const int sl0 = (c0 ^ (frow & 7)) << 4, sl1 = ((c0 + 1) ^ (frow & 7)) << 4;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BK - 1) / BK;
+  dma(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) dma(st ^ 1);
+    const uint8_t* xs = smem + st * STG;
+    const uint8_t* ws = xs + XB;
+    i32x8 a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint8_t* r = ws + (wn * 64 + i * 16 + frow) * BK;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(r + sl0), hi = *reinterpret_cast<const u32x4*>(r + sl1);
+      a[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint8_t* r = xs + (wm * 64 + j * 16 + frow) * BK;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(r + sl0), hi = *reinterpret_cast<const u32x4*>(r + sl1);
+      b[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, E8M0_ONE, 0,
+                                                                     E8M0_ONE);
+  }
+  __syncthreads();  // the epilogue tile reuses the stage images
+
+  uint8_t* Os = smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int cl = wn * 64 + i * 16 + (lane >> 4) * 4;
+    f32x4 sv = {0.f, 0.f, 0.f, 0.f}, bv = {0.f, 0.f, 0.f, 0.f};
+    if (n0 + cl < p.Cout) {
+      sv = *reinterpret_cast<const f32x4*>(p.scale + n0 + cl);
+      bv = *reinterpret_cast<const f32x4*>(p.bias + n0 + cl);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pl = wm * 64 + j * 16 + frow;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act<ACT>(acc[i][j][r] * sv[r] + bv[r]);
+      if constexpr (OUT_FP8) {
+        *reinterpret_cast<uint32_t*>(Os + pl * OLD + cl) =
+            pack4(v[0] * p.out_q, v[1] * p.out_q, v[2] * p.out_q, v[3] * p.out_q);
+      } else {
+        bf16x4 o;
+        o[0] = f2bf(v[0]); o[1] = f2bf(v[1]); o[2] = f2bf(v[2]); o[3] = f2bf(v[3]);
+        *reinterpret_cast<bf16x4*>(Os + pl * OLD + cl * 2) = o;
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int EPC = 16 / OB;
+  constexpr int CPR = BN / EPC;
+#pragma unroll 4
+  for (int q = threadIdx.x; q < BM * CPR; q += 256) {
+    const int pl = q / CPR;
+    const int cc = q % CPR;
+    const int m = m0 + pl;
+    const int c = n0 + cc * EPC;
+    if (m >= p.M || c >= p.Cout) continue;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(Os + pl * OLD + cc * 16);
+    *reinterpret_cast<u32x4*>(p.y + ((size_t)m * p.ldy + p.y_coff + c) * OB) = v;
+  }
+}
+
+template <bool OUT_FP8>
+void launch_lite_fp8(const Fp8Params& p0, int act, hipStream_t s) {
+  Fp8Params p = p0;
+  p.tiles_m = (p.M + 127) / 128;
+  p.tiles_n = (p.Cout + 127) / 128;
+  dim3 grid(p.tiles_m * p.tiles_n), block(256);
+  switch (act) {
+    case ACT_NONE: hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_NONE>), grid, block, 0, s, p); break;
+    case ACT_RELU: hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_RELU>), grid, block, 0, s, p); break;
+    default: throw std::invalid_argument("fp8 conv_lite: activation must be none/relu");
+  }
+}
+
+// cfg value selecting conv_lite_fp8 (fp8 input only; any conv geometry with Cin % 16 == 0)
+constexpr int LITE_CFG = 8;
+
 template <bool CONV>
 void launch_io(const Fp8Params& p, bool in_bf16, bool out_fp8, int act, int cfg, hipStream_t s) {
   if (in_bf16) {
@@ -524,6 +718,15 @@ void conv2d_nhwc_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, 
   p.ldx = Cin;
   p.ldy = ldy; p.y_coff = y_coff;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (cfg == LITE_CFG) {
+    if (in_bf16) throw std::invalid_argument("conv2d_nhwc_fp8: the conv_lite tile takes fp8 input");
+    if (ph >= 1024 || pw >= 1024 || H >= 16384 || W >= 16384) throw std::invalid_argument("conv2d_nhwc_fp8: geometry");
+    if ((long)Cout * p.K >= (1L << 31)) throw std::invalid_argument("conv2d_nhwc_fp8: weights larger than 2 GiB");
+    if (out_fp8) launch_lite_fp8<true>(p, act, s);
+    else launch_lite_fp8<false>(p, act, s);
+    FTM_CHECK_LAUNCH();
+    return;
+  }
   const bool pointwise = KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
   if (pointwise) launch_io<false>(p, in_bf16, out_fp8, act, cfg, s);
   else launch_io<true>(p, in_bf16, out_fp8, act, cfg, s);

@@ -98,11 +98,23 @@ def _conv_case(cin, cout, k, stride, pads, in_bf16, out_fp8, cfg, offset=0, extr
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [0, 1, 2, 16, 17])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 8, 16, 17])
 def test_conv_fp8_configs_gpu(cfg):
     _conv_case(32, 64, 3, 1, (1, 1, 1, 1), False, True, cfg)
     _conv_case(64, 192, 3, 2, (0, 0, 0, 0), False, False, cfg)
     _conv_case(48, 96, (1, 7), 1, (0, 0, 3, 3), False, True, cfg, offset=32, extra=64)
+
+
+@pytest.mark.gpu
+def test_conv_fp8_lite_shapes_gpu():
+    """conv_lite_fp8 (cfg 8, the 4-wave LDS-DMA tile): Cin not a multiple of the 128-byte
+    K-tile (288, 192, 80), K tails, Cout tails, 1x1 / 7x1 / strided, fp8 and bf16 output at a
+    concat offset."""
+    _conv_case(288, 384, 3, 2, (0, 0, 0, 0), False, True, 8, N=2, H=17, W=17)
+    _conv_case(192, 80, (7, 1), 1, (3, 3, 0, 0), False, False, 8, N=3, H=9, W=9)
+    _conv_case(80, 192, 3, 1, (1, 1, 1, 1), False, True, 8, offset=64, extra=128)
+    _conv_case(768, 128, 1, 1, (0, 0, 0, 0), False, True, 8, N=4, H=9, W=9)
+    _conv_case(16, 32, 3, 1, (1, 1, 1, 1), False, False, 8)
 
 
 @pytest.mark.gpu
