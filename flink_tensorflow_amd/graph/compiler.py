@@ -846,7 +846,7 @@ class CompiledFunction(TransformerLowering):
             # (kernels/conv_pp.hip conv_lite): 6-24 % faster than the register-staged igemm
             # per layer and 64 KiB of LDS, so it shares a CU with the sibling lane
             cl = K.ConvPP([(tuple(xin.shape), (KHe, KWe), (sh, sw), (pt, pl), (dh, dw))], Cout, tuple(out.shape[1:3]),
-                          self.device, tile=2)
+                          self.device, tile=3 if _cfg().conv_lite_bk == 32 else 2)
 
             def run(xin=xin, out=out, res_val=res_val, cl=cl, w2=w_dev.reshape(Cout, -1), b_dev=b_dev):  # noqa: F811
                 cl([xin.buf], w2, b_dev, res_val.buf if res_val is not None else None, act, out=_target(out),

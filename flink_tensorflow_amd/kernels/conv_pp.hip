@@ -388,13 +388,25 @@ __global__ __launch_bounds__(NT, 1) void conv_pp_kernel(CPParams p) {
 // of tile t.  Epilogue as igemm: + bias -> bf16 LDS tile -> coalesced 16-B row segments
 // (+ residual, act).
 // ---------------------------------------------------------------------------------------
-template <int ACT, bool HAS_RES>
+template <int ACT, bool HAS_RES, int BK>
 __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
+  // BK = 64: 128-B LDS rows, 2 x 32 KiB stages, 2 MFMA steps per K-tile.
+  // BK = 32: 64-B rows, 2 x 16 KiB stages (the igemm's footprint: four workgroups per CU),
+  //          1 MFMA step per K-tile; 16-B chunk slot = chunk ^ ((row >> 2) & 3) keeps the
+  //          16-lane ds_read_b128 groups on distinct banks.
   constexpr int BM = 128, BN = 128;
-  constexpr int XB = BM * 128, WB = BN * 128, STG = XB + WB;
+  constexpr int ROWB = BK * 2;             // LDS row bytes
+  constexpr int CPR = ROWB / 16;           // 16-B chunks per row
+  constexpr int RPI = 1024 / ROWB;         // rows per DMA wave-instruction
+  constexpr int QX = BM / RPI / 4;         // DMA instructions per wave per operand
+  constexpr int XB = BM * ROWB, WB = BN * ROWB, STG = XB + WB;
   constexpr int OPITCH = BN * 2 + 16;
   constexpr int LDS = 2 * STG > BM * OPITCH ? 2 * STG : BM * OPITCH;
   __shared__ __attribute__((aligned(1024))) uint8_t smem[LDS];
+  auto slot_of = [](int row, int chunk) {
+    if constexpr (CPR == 8) return chunk ^ (row & 7);
+    else return chunk ^ ((row >> 2) & 3);
+  };
 
   const int nwg = p.tiles_m * p.tiles_n;
   const int tile = xcd_remap(blockIdx.x, nwg);
@@ -407,22 +419,22 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
   const int wm = wave & 1;   // pixel half of the tile
   const int wn = wave >> 1;  // channel half
 
-  // DMA roles: wave w stages image rows 8 * (4 w + q) + (lane >> 3), q = 0..3, of both the
-  // X (pixel) and W (channel) images; the lane's 16-B chunk is pre-swizzled on the source
-  const int drow = lane >> 3;
-  const int dchunk = (lane & 7) ^ drow;
+  // DMA roles: wave w stages image rows RPI * (QX w + q) + lane / CPR of both the X (pixel)
+  // and W (channel) images; the lane's 16-B chunk is pre-swizzled on the source
+  const int drow = lane / CPR;
+  const int dchunk = slot_of(drow, lane % CPR);  // (row mod the swizzle period == drow's)
   const unsigned nimg = (unsigned)p.M / (unsigned)(p.OH * p.OW);
   const CSrc& S = p.s[0];
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)S.x, 0, (int)(nimg * (unsigned)(S.H * S.W) * (unsigned)S.C * 2u), 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)p.w, 0, (int)((unsigned)p.N * (unsigned)p.ldw * 2u), 0x00020000);
-  int pb[4], hw[4];
-  unsigned offw[4];
+  int pb[QX], hw[QX];
+  unsigned offw[QX];
   const int ohw = p.OH * p.OW;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = 8 * (4 * wave + q) + drow;
+  for (int q = 0; q < QX; ++q) {
+    const int r = RPI * (QX * wave + q) + drow;
     const int m = m0 + r;
     const bool live = m < p.M;
     const int n = live ? m / ohw : 0;
@@ -439,29 +451,31 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
   // The K walk (channel chunk, filter column, filter row) advances incrementally in scalar
   // registers: no table read inside the loop (a ktab load there is a vector load — the
   // LDS-DMA in the loop defeats the scalar-load analysis — and stalled every K-tile).
-  const int c64 = S.C >> 6;
-  int cc = 0, kw = 0, kh = 0;
-  auto dma = [&](int kt, int stage) {
+  const int cpt = S.C / BK;  // K-tiles per filter tap
+  int cc = 0, kw = 0, kh = 0, kt_dma = 0;
+  auto dma = [&](int stage) {
     const int dih = kh * p.dh, diw = kw * p.dw;
-    const int delta = ((dih * S.W + diw) * S.C + cc * 64) * 2;
-    if (++cc == c64) {
+    const int delta = ((dih * S.W + diw) * S.C + cc * BK) * 2;
+    const unsigned woff = (unsigned)kt_dma * (unsigned)ROWB;
+    ++kt_dma;
+    if (++cc == cpt) {
       cc = 0;
       if (++kw == p.KW) {
         kw = 0;
         ++kh;
       }
     }
-    uint8_t* bx = smem + stage * STG + 4 * wave * 8 * 128;
+    uint8_t* bx = smem + stage * STG + QX * wave * RPI * ROWB;
     uint8_t* bw = bx + XB;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < QX; ++q) {
       const int ih = (hw[q] >> 16) + dih;
       const int iw = ((hw[q] << 16) >> 16) + diw;
       const bool ok = (unsigned)ih < (unsigned)S.H && (unsigned)iw < (unsigned)S.W;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(bx + q * 8 * 128), 16,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(bx + q * 1024), 16,
                                                ok ? (unsigned)(pb[q] + delta) : 0x80000000u, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 8 * 128), 16,
-                                               offw[q], (unsigned)kt * 128u, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 1024), 16,
+                                               offw[q], woff, 0, 0);
     }
   };
 
@@ -473,24 +487,24 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = p.K >> 6;
-  dma(0, 0);
+  const int nk = p.K / BK;
+  dma(0);
   for (int kt = 0; kt < nk; ++kt) {
     const int st = kt & 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (kt + 1 < nk) dma(kt + 1, st ^ 1);
+    if (kt + 1 < nk) dma(st ^ 1);
     const uint8_t* xs = smem + st * STG;
     const uint8_t* ws = xs + XB;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int slot = ((ks * 4 + fq) ^ (frow & 7)) << 4;
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int sl = slot_of(frow, ks * 4 + fq) << 4;
       bf16x8 a[4], b[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ws + (wn * 64 + i * 16 + frow) * 128 + slot);
+      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ws + (wn * 64 + i * 16 + frow) * ROWB + sl);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(xs + (wm * 64 + j * 16 + frow) * 128 + slot);
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(xs + (wm * 64 + j * 16 + frow) * ROWB + sl);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -524,11 +538,11 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
 #pragma unroll 4
   for (int q = threadIdx.x; q < BM * SEGS; q += 256) {
     const int ml = q / SEGS;
-    const int cc = q - ml * SEGS;
+    const int ccol = q - ml * SEGS;
     const int m = m0 + ml;
-    const int n = n0 + cc * 8;
+    const int n = n0 + ccol * 8;
     if (m >= p.M || n >= p.N) continue;
-    u32x4 v = *reinterpret_cast<const u32x4*>(smem + ml * OPITCH + cc * 16);
+    u32x4 v = *reinterpret_cast<const u32x4*>(smem + ml * OPITCH + ccol * 16);
     if constexpr (HAS_RES) {
       bf16x8 o = __builtin_bit_cast(bf16x8, v);
       const bf16x8 r = *reinterpret_cast<const bf16x8*>(p.res + (size_t)m * p.ldr + n);
@@ -540,10 +554,11 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
   }
 }
 
-template <int ACT>
+// lite_bk: 64 (tile 2) or 32 (tile 3)
+template <int ACT, int BK>
 void launch_lite(const CPParams& p, hipStream_t s) {
-  if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true>), dim3(p.tiles_m * p.tiles_n), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL((conv_lite_kernel<ACT, false>), dim3(p.tiles_m * p.tiles_n), dim3(256), 0, s, p);
+  if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, BK>), dim3(p.tiles_m * p.tiles_n), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, BK>), dim3(p.tiles_m * p.tiles_n), dim3(256), 0, s, p);
 }
 
 template <int ACT, bool HAS_RES>
@@ -673,9 +688,11 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   p.K = (int)K;
   p.OH = OH; p.OW = OW;
   p.ldw = (int)K; p.ldy = ldy; p.y_coff = y_coff; p.ldr = ldr;
-  need(tile >= 0 && tile <= 2, "tile must be 0 (256x256), 1 (512x128) or 2 (128x128, 4 waves)");
-  need(tile != 2 || (ns == 1 && splits <= 1), "the 4-wave tile takes one source and no split-K");
-  const int BM = tile == 1 ? 512 : tile == 2 ? 128 : 256, BN = tile == 1 ? 128 : tile == 2 ? 128 : 256;
+  need(tile >= 0 && tile <= 3, "tile must be 0 (256x256), 1 (512x128), 2 / 3 (128x128, 4 waves, K-tile 64 / 32)");
+  const bool lite = tile >= 2;
+  need(!lite || (ns == 1 && splits <= 1), "the 4-wave tile takes one source and no split-K");
+  need(tile != 3 || p.s[0].C % 32 == 0, "the 32-deep 4-wave tile needs Cin % 32 == 0");
+  const int BM = tile == 1 ? 512 : lite ? 128 : 256, BN = tile == 1 ? 128 : lite ? 128 : 256;
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (Cout + BN - 1) / BN;
   const int nk = p.K / 64;
@@ -689,10 +706,12 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   float* wsp = reinterpret_cast<float*>(ws);
-  if (tile == 2) {
-    switch (act) {
-      case ACT_NONE: launch_lite<ACT_NONE>(p, s); break;
-      case ACT_RELU: launch_lite<ACT_RELU>(p, s); break;
+  if (lite) {
+    switch (act * 2 + (tile == 3)) {
+      case ACT_NONE * 2: launch_lite<ACT_NONE, 64>(p, s); break;
+      case ACT_NONE * 2 + 1: launch_lite<ACT_NONE, 32>(p, s); break;
+      case ACT_RELU * 2: launch_lite<ACT_RELU, 64>(p, s); break;
+      case ACT_RELU * 2 + 1: launch_lite<ACT_RELU, 32>(p, s); break;
       default: throw std::invalid_argument("conv_pp: unsupported activation");
     }
   } else if (tile == 1) launch_tile<512, 128>(p, splits, wsp, ns == 2, act, s);

@@ -543,7 +543,8 @@ def conv_pp_ktab(srcs) -> torch.Tensor:
 
 def conv_pp_tile(Cout: int) -> int:
     """0 = 256x256 tiles, 1 = 512x128 tiles (channel counts that would waste half of a
-    256-wide tile); 2 (never chosen here) = the 4-wave 128x128 ``conv_lite`` tile."""
+    256-wide tile); 2 / 3 (never chosen here) = the 4-wave 128x128 ``conv_lite`` tile with a
+    64- / 32-deep K-tile (64 / 32 KiB of LDS)."""
     return 1 if Cout <= 128 or (Cout % 256 and Cout % 128 == 0) else 0
 
 
@@ -583,9 +584,9 @@ class ConvPP:
             raise ValueError("conv_pp: Cout % 8")
         self.M = self.N * self.OH * self.OW
         self.tile = conv_pp_tile(Cout) if tile is None else tile
-        if self.tile == 2 and len(self.srcs) != 1:
+        if self.tile in (2, 3) and len(self.srcs) != 1:
             raise ValueError("conv_pp: the 4-wave 128x128 tile takes one source")
-        self.splits = (1 if self.tile == 2 else conv_pp_splits(self.M, Cout, self.K, self.tile)) if splits is None \
+        self.splits = (1 if self.tile in (2, 3) else conv_pp_splits(self.M, Cout, self.K, self.tile)) if splits is None \
             else splits
         self.ktab = conv_pp_ktab([(xs[1], xs[2], xs[3], k[0], k[1], dl[0], dl[1])
                                   for xs, k, _, _, dl in self.srcs]).to(device)
