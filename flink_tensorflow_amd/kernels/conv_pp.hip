@@ -388,6 +388,13 @@ __global__ __launch_bounds__(NT, 1) void conv_pp_kernel(CPParams p) {
 // of tile t.  Epilogue as igemm: + bias -> bf16 LDS tile -> coalesced 16-B row segments
 // (+ residual, act).
 // ---------------------------------------------------------------------------------------
+// 16-B chunk slot of (row, chunk) in a conv_lite LDS image with CPR chunks per row
+template <int CPR>
+FTM_DEVICE int lite_slot(int row, int chunk) {
+  if constexpr (CPR == 8) return chunk ^ (row & 7);
+  else return chunk ^ ((row >> 2) & 3);
+}
+
 template <int ACT, bool HAS_RES, int BK>
 __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
   // BK = 64: 128-B LDS rows, 2 x 32 KiB stages, 2 MFMA steps per K-tile.
@@ -403,10 +410,6 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
   constexpr int OPITCH = BN * 2 + 16;
   constexpr int LDS = 2 * STG > BM * OPITCH ? 2 * STG : BM * OPITCH;
   __shared__ __attribute__((aligned(1024))) uint8_t smem[LDS];
-  auto slot_of = [](int row, int chunk) {
-    if constexpr (CPR == 8) return chunk ^ (row & 7);
-    else return chunk ^ ((row >> 2) & 3);
-  };
 
   const int nwg = p.tiles_m * p.tiles_n;
   const int tile = xcd_remap(blockIdx.x, nwg);
@@ -422,15 +425,17 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
   // DMA roles: wave w stages image rows RPI * (QX w + q) + lane / CPR of both the X (pixel)
   // and W (channel) images; the lane's 16-B chunk is pre-swizzled on the source
   const int drow = lane / CPR;
-  const int dchunk = slot_of(drow, lane % CPR);  // (row mod the swizzle period == drow's)
+  const int dchunk = lite_slot<CPR>(drow, lane % CPR);  // (row mod the swizzle period == drow's)
   const unsigned nimg = (unsigned)p.M / (unsigned)(p.OH * p.OW);
   const CSrc& S = p.s[0];
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)S.x, 0, (int)(nimg * (unsigned)(S.H * S.W) * (unsigned)S.C * 2u), 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)p.w, 0, (int)((unsigned)p.N * (unsigned)p.ldw * 2u), 0x00020000);
-  int pb[QX], hw[QX];
-  unsigned offw[QX];
+  // fixed-size (QX <= 4): arrays sized by the template-dependent QX made hipcc's host pass
+  // drop the kernel by SFINAE (an undefined device stub at load time)
+  int pb[4], hw[4];
+  unsigned offw[4];
   const int ohw = p.OH * p.OW;
 #pragma unroll
   for (int q = 0; q < QX; ++q) {
@@ -499,7 +504,7 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
-      const int sl = slot_of(frow, ks * 4 + fq) << 4;
+      const int sl = lite_slot<CPR>(frow, ks * 4 + fq) << 4;
       bf16x8 a[4], b[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ws + (wn * 64 + i * 16 + frow) * ROWB + sl);
