@@ -37,12 +37,17 @@ def main():
                          "through SignatureBatchedModel (the path a user's own SavedModel takes)")
     ap.add_argument("--processes", action="store_true",
                     help="run the model operator in a worker process (records cross through the tensor slab)")
+    ap.add_argument("--worker-source", action="store_true",
+                    help="run the source inside the model's worker process too (a chained source: records are "
+                         "produced where the GPU operator consumes them; implies --processes)")
     a = ap.parse_args()
-    pool = np.random.default_rng(0).integers(0, 256, (256, a.hw, a.hw, 3), dtype=np.uint8)
+    hw, n_rec = a.hw, a.records
 
     def images(idx, par, start):
-        for i in range(start, a.records):
-            if i % par == idx:
+        # built where the source runs (the coordinator, or the worker with --worker-source)
+        pool = np.random.default_rng(idx).integers(0, 256, (256, hw, hw, 3), dtype=np.uint8)
+        for k, i in enumerate(range(idx, n_rec, par)):
+            if k >= start:
                 yield pool[i % len(pool)]
 
     env = StreamExecutionEnvironment.get_execution_environment()
@@ -57,9 +62,11 @@ def main():
         model = SignatureBatchedModel(d, buckets=(a.batch,), output_keys=["classes", "scores"])
     else:
         model = ResNet50Model(image_hw=(a.hw, a.hw), buckets=(a.batch,), depth_layers=a.depth_layers)
-    op = env.generate(images).map_with_model_batched(model, None, max_batch=a.batch, max_delay_ms=a.delay_ms,
-                                                     name="resnet50")
-    if a.processes:
+    src = env.generate(images)
+    if a.worker_source:
+        src = src.run_in_processes()
+    op = src.map_with_model_batched(model, None, max_batch=a.batch, max_delay_ms=a.delay_ms, name="resnet50")
+    if a.processes or a.worker_source:
         op = op.run_in_processes()
     op.add_sink(sink := ThroughputSink())
     t0 = time.time()
@@ -67,7 +74,8 @@ def main():
     el = time.time() - t0
     m = [v for k, v in res.metrics.items() if k.startswith("resnet50")][0]
     steady = sink.rate(0.2)  # steady state: skip the first fifth (compile, capture, pipeline fill)
-    print(json.dumps({"records": a.records, "savedmodel": a.savedmodel, "worker_process": a.processes, "seconds": round(el, 3), "records_per_s": round(a.records / el, 1),
+    print(json.dumps({"records": a.records, "savedmodel": a.savedmodel, "worker_process": a.processes or a.worker_source,
+                      "worker_source": a.worker_source, "seconds": round(el, 3), "records_per_s": round(a.records / el, 1),
                       "steady_records_per_s": round(steady, 1) if steady else None,
                       "latency_s": m["histograms"].get("latency_s"), "batch": m["histograms"].get("batch_size")}))
 
