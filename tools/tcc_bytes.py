@@ -31,6 +31,10 @@ def last_batch(rows, marker="preprocess"):
     return [i for i in ids if i >= s]
 
 
+def _short(name: str) -> str:
+    return name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:70]
+
+
 def main():
     fetch = load(sys.argv[1], "FETCH_SIZE")
     write = load(sys.argv[2], "WRITE_SIZE")
@@ -38,11 +42,11 @@ def main():
     ids_w = last_batch(write)
     agg = defaultdict(lambda: [0.0, 0.0, 0])
     for i in ids_f:
-        n = fetch[i][0].split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")[:70]
+        n = _short(fetch[i][0])
         agg[n][0] += fetch[i][1] * 1024
         agg[n][2] += 1
     for i in ids_w:
-        n = write[i][0].split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")[:70]
+        n = _short(write[i][0])
         agg[n][1] += write[i][1] * 1024
     tot_r = sum(v[0] for v in agg.values())
     tot_w = sum(v[1] for v in agg.values())
