@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--worker-source", action="store_true",
                     help="run the source inside the model's worker process too (a chained source: records are "
                          "produced where the GPU operator consumes them; implies --processes)")
+    ap.add_argument("--no-chain", action="store_true",
+                    help="disable operator chaining: the in-process source runs in its own thread and hands "
+                         "records to the model thread through a queue")
     a = ap.parse_args()
     hw, n_rec = a.hw, a.records
 
@@ -51,6 +54,8 @@ def main():
                 yield pool[i % len(pool)]
 
     env = StreamExecutionEnvironment.get_execution_environment()
+    if a.no_chain:
+        env.disable_operator_chaining()
     if a.savedmodel:
         import tempfile
 
@@ -75,7 +80,7 @@ def main():
     m = [v for k, v in res.metrics.items() if k.startswith("resnet50")][0]
     steady = sink.rate(0.2)  # steady state: skip the first fifth (compile, capture, pipeline fill)
     print(json.dumps({"records": a.records, "savedmodel": a.savedmodel, "worker_process": a.processes or a.worker_source,
-                      "worker_source": a.worker_source, "seconds": round(el, 3), "records_per_s": round(a.records / el, 1),
+                      "worker_source": a.worker_source, "chained": not a.no_chain, "seconds": round(el, 3), "records_per_s": round(a.records / el, 1),
                       "steady_records_per_s": round(steady, 1) if steady else None,
                       "latency_s": m["histograms"].get("latency_s"), "batch": m["histograms"].get("batch_size")}))
 

@@ -191,12 +191,15 @@ class _SourceCtx(SourceContext):
         return self._lock
 
     def collect(self, value, timestamp=None):
-        self.task.check_trigger()
-        self.task.writer.emit(Record(value, timestamp))
-        self.task.metrics.inc("records_out")
+        task = self.task
+        with self._lock:  # re-entrant: sources normally hold it already (chain timer excluded)
+            task.check_trigger()
+            task.head_emit(Record(value, timestamp))
+        task.metrics.inc("records_out")
 
     def emit_watermark(self, ts):
-        self.task.writer.emit(Watermark(ts))
+        with self._lock:
+            self.task.head_emit(Watermark(ts))
 
 
 # ------------------------------------------------------------------ tasks
@@ -245,35 +248,98 @@ class _Task:
 
 
 class _SourceTask(_Task):
-    def __init__(self, *a, **kw):
-        super().__init__(*a, **kw)
+    """A source subtask, with the operators chained into it (Flink chains a source with
+    its forward, equal-parallelism consumers: records go from ``SourceContext.collect``
+    straight into the first member's ``process`` on this thread, no queue hand-off).
+
+    Chain members get their time-driven work (``on_idle``: a micro-batch whose
+    ``max_delay`` expired, completed GPU batches) from the collect path at most every
+    millisecond, and from a timer thread under the checkpoint lock while the source
+    function is not emitting (Flink's processing-time service fires under the same lock)."""
+
+    def __init__(self, job, node, subtask, writer, restore, chain: list | None = None):
+        super().__init__(job, node, subtask, writer, restore)
         self.pending_trigger: deque[int] = deque()
         self.op = self.node.make_operator()
+        self.chain = chain or []
+        self.head_emit = writer.emit if writer is not None else None
+        self._last_poll = time.perf_counter()
 
     def check_trigger(self):
         while self.pending_trigger:
             cid = self.pending_trigger.popleft()
-            state = self.op.snapshot_state(cid, self.job.chk_dir(cid))
-            self.job.ack(cid, (self.uid, self.subtask), state)
+            d = self.job.chk_dir(cid)
+            self.job.ack(cid, (self.uid, self.subtask), self.op.snapshot_state(cid, d))
+            for t in self.chain:  # in chain order: each flush reaches the next before it snapshots
+                t.op.prepare_snapshot()
+                self.job.ack(cid, (t.uid, t.subtask), t.op.snapshot_state(cid, d))
             self.writer.emit(Barrier(cid, time.time()))
         if self.job.cancel.is_set():
             raise JobCancelled()
+        if self.chain:
+            now = time.perf_counter()
+            if now - self._last_poll >= 1e-3:
+                self._poll_chain(now)
+
+    def _poll_chain(self, now):
+        self._last_poll = now
+        wall = time.time()
+        for t in self.chain:
+            t.op.on_idle(wall)
+        self.writer.flush()
+
+    def _chain_timer(self, lock, stop: threading.Event):
+        try:
+            while True:
+                with lock:
+                    dls = [d for d in (t.op.next_deadline() for t in self.chain) if d is not None]
+                wait = 0.01 if not dls else min(0.01, max(2e-4, min(dls) - time.time()))
+                if stop.wait(wait):
+                    return
+                if time.perf_counter() - self._last_poll < wait:
+                    continue  # the source is emitting: the collect path polls
+                with lock:
+                    if stop.is_set():
+                        return
+                    self._poll_chain(time.perf_counter())
+        except BaseException as e:  # noqa: BLE001
+            self.job.fail(self, e, traceback.format_exc())
 
     def run(self):
         fn = self.op.fn
-        ctx = self.runtime_context()
-        self.op.setup(ctx, Output(self.writer.emit, self.writer.emit_side))
-        self.op.initialize(self.restore, self.job.restore_dir)
-        self.op.open()
+        tasks = [self] + self.chain
+        for i, t in enumerate(tasks):
+            nxt = tasks[i + 1] if i + 1 < len(tasks) else None
+            out = Output(_chain_emit(nxt), _drop_side) if nxt else Output(self.writer.emit, self.writer.emit_side)
+            t.op.setup(t.runtime_context(), out)
+            t.op.initialize(t.restore, self.job.restore_dir)
+        for t in reversed(tasks):  # downstream first: ready before anything is emitted into it
+            t.op.open()
+        if self.chain:
+            self.head_emit = _chain_emit(self.chain[0])
         sctx = _SourceCtx(self)
+        stop = threading.Event()
+        timer = None
+        if self.chain:
+            timer = threading.Thread(target=self._chain_timer, args=(sctx.checkpoint_lock, stop),
+                                     name=f"{self.node.name}-{self.subtask}-timer", daemon=True)
+            timer.start()
         try:
             fn.run(sctx)
             with sctx.checkpoint_lock:
+                stop.set()
                 self.check_trigger()
                 # end-of-input offsets: later checkpoints restore this source as exhausted
                 self.final_state = self.op.snapshot_state(-1, None)
+            if timer is not None:
+                timer.join()
+                self.head_emit(Watermark(float("inf")))
+                for t in self.chain:  # in chain order: each flush reaches the next operator
+                    t.op.end_input()
         finally:
-            self.op.close()
+            stop.set()
+            for t in tasks:
+                t.op.close()
         self.writer.emit(Watermark(float("inf")))
         self.writer.emit(END)
 
@@ -612,13 +678,14 @@ class LocalExecutor:
                     self.tasks.append(t)
                     self.tasks.extend(chain)
                     continue
-                if n.is_source:
-                    t = _SourceTask(self, n, i, w, rs)
-                    self.sources.append(t)
-                    self.tasks.append(t)
-                    continue
                 chain = [_ChainedTask(self, m, i, restore_states.get((m.uid, i)) if restore_states else None,
                                       ops[(m.uid, i)]) for m in members]
+                if n.is_source:
+                    t = _SourceTask(self, n, i, w, rs, chain)
+                    self.sources.append(t)
+                    self.tasks.append(t)
+                    self.tasks.extend(chain)
+                    continue
                 self.tasks.append(_OpTask(self, n, i, w, rs, gates[(n.uid, i)], chan_of[(n.uid, i)],
                                           ops.get((n.uid, i)), chain))
                 self.tasks.extend(chain)
@@ -653,8 +720,9 @@ class LocalExecutor:
         """Operator chaining (Flink's ``StreamingJobGraphGenerator.isChainable``): a node runs
         inside its upstream's thread when the edge is forward, both have the same
         parallelism, it has exactly that one input, the upstream has no other consumer, and
-        neither side is a source, a worker-process operator, an operator that cannot chain
-        (two-input) or a node marked ``start_new_chain`` / ``disable_chaining``."""
+        neither side is a worker-process operator, an operator that cannot chain (two-input)
+        or a node marked ``start_new_chain`` / ``disable_chaining``.  A source heads a chain
+        (``_SourceTask`` runs its members), it never joins one."""
         if not getattr(self.env, "chaining", True):
             return {}
         consumers: dict[str, int] = {}
@@ -662,9 +730,10 @@ class LocalExecutor:
             for up, _, _ in n.inputs:
                 consumers[up.uid] = consumers.get(up.uid, 0) + 1
 
-        def ok(n):
-            return (not n.is_source and not getattr(n, "remote", False) and getattr(n, "chaining", True)
-                    and ops[(n.uid, 0)].chainable)
+        def ok(n, head=False):
+            if n.is_source:  # a source heads a chain; it never joins one
+                return head and not getattr(n, "remote", False) and getattr(n, "chaining", True)
+            return not getattr(n, "remote", False) and getattr(n, "chaining", True) and ops[(n.uid, 0)].chainable
 
         out = {}
         for n in nodes:
@@ -672,7 +741,7 @@ class LocalExecutor:
                 continue
             up, part, side_tag = n.inputs[0]
             if (side_tag is None and part.kind == "forward" and up.parallelism == n.parallelism
-                    and consumers.get(up.uid) == 1 and ok(up) and ok(n)):
+                    and consumers.get(up.uid) == 1 and ok(up, head=True) and ok(n)):
                 out[n.uid] = up
         return out
 

@@ -302,14 +302,14 @@ def test_operator_chaining_forms_chains_and_keeps_per_operator_metrics():
     env, sink = _chain_job()
     ex = LocalExecutor(env, "chained")
     res = ex.execute()
-    assert ex.chains == [["inc", "even", "x10", "collect"]]
-    assert sum(t.thread is not None for t in ex.tasks) == 2   # the source + one chain
+    assert ex.chains == [["collection", "inc", "even", "x10", "collect"]]  # the source heads the chain
+    assert sum(t.thread is not None for t in ex.tasks) == 1   # one thread runs the whole job
     assert sink.results() == [10 * x for x in range(2, 1001, 2)]
     assert res.metrics["x10[0]"]["counters"]["records_in"] == 500
 
 
-@pytest.mark.parametrize("mark,chains", [("new_chain", [["even", "x10", "collect"]]),   # "even" starts a chain
-                                         ("no_chain", [["x10", "collect"]]),            # "even" chains with nothing
+@pytest.mark.parametrize("mark,chains", [("new_chain", [["collection", "inc"], ["even", "x10", "collect"]]),
+                                         ("no_chain", [["collection", "inc"], ["x10", "collect"]]),  # "even" alone
                                          ("env_off", [])])
 def test_chaining_controls(mark, chains):
     from flink_tensorflow_amd.runtime.executor import LocalExecutor
@@ -321,6 +321,40 @@ def test_chaining_controls(mark, chains):
     ex.execute()
     assert ex.chains == chains
     assert sink.results() == [10 * x for x in range(2, 1001, 2)]
+
+
+def test_source_chain_flushes_micro_batches_while_the_source_is_idle():
+    """A micro-batching operator chained into its source still honours ``max_delay_ms``
+    while the source function sleeps between records (the chain timer flushes it), and a
+    checkpoint taken mid-stream acks the source and every chain member."""
+    from flink_tensorflow_amd.runtime.executor import LocalExecutor
+    from flink_tensorflow_amd.runtime.functions import SourceFunction
+
+    class Bursty(SourceFunction):
+        def run(self, ctx):
+            for burst in range(3):
+                with ctx.checkpoint_lock:
+                    for i in range(3):
+                        ctx.collect(burst * 3 + i)
+                time.sleep(0.25)  # far longer than max_delay: the batch must not wait for this
+
+    def run_batch(model, vals):  # (value, batch contents, flush time); the function is cloned
+        t = time.perf_counter()
+        return [(v * 2, tuple(vals), t) for v in vals]
+
+    env = StreamExecutionEnvironment.get_execution_environment()
+    sink = env.add_source(Bursty(), "bursty").map_with_model_batched(
+        object(), run_batch, max_batch=64, max_delay_ms=5, name="batched").collect_into()
+    ex = LocalExecutor(env, "idle-flush")
+    t0 = time.perf_counter()
+    ex.execute()
+    assert ex.chains == [["bursty", "batched", "collect"]]
+    out = sink.results()
+    assert sorted(v for v, _, _ in out) == [2 * i for i in range(9)]
+    batches = sorted({(t, b) for _, b, t in out})
+    assert [b for _, b in batches] == [(0, 1, 2), (3, 4, 5), (6, 7, 8)]
+    # each burst was flushed by the timer long before the next burst arrived
+    assert batches[0][0] - t0 < 0.2 and batches[1][0] - batches[0][0] < 0.45
 
 
 def test_key_by_and_fan_out_break_chains():
