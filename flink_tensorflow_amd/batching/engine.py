@@ -26,6 +26,7 @@ from typing import Any, Callable, Sequence
 import numpy as np
 import torch
 
+from ..utils.streams import dedicated_stream
 from ..utils.tracing import capture_lock, trace_range
 
 from .. import _ext
@@ -90,8 +91,10 @@ class PipelinedGpuRunner:
         self.record_shape = tuple(record_shape)
         self.record_dtype = record_dtype
         self.record_bytes = int(np.prod(record_shape)) * torch.empty((), dtype=record_dtype).element_size()
-        self.copy_stream = torch.cuda.Stream(self.device)
-        self.compute_streams = [torch.cuda.Stream(self.device) for _ in self.lanes]
+        # framework-owned streams, not torch's pool (a pooled stream can be the one a sibling
+        # subtask thread is capturing a hipGraph on: utils/streams.py)
+        self.copy_stream = dedicated_stream(self.device, owner=self)
+        self.compute_streams = [dedicated_stream(self.device, owner=self) for _ in self.lanes]
         self.compute_stream = self.compute_streams[0]
         self.gather_threads = gather_threads
         self.stage_chunk = stage_chunk  # records per gather + H2D piece (0: whole batch at once)

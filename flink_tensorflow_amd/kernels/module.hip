@@ -3,6 +3,11 @@
 // (passed as an integer from torch.cuda.current_stream().cuda_stream), so every launch
 // lands on the caller's stream and is captured by hipGraph capture.
 #include <pybind11/pybind11.h>
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
 
 void register_igemm(pybind11::module_& m);
 void register_nn_misc(pybind11::module_& m);
@@ -42,4 +47,17 @@ PYBIND11_MODULE(_hip, m) {
   register_sort_segments(m);
   register_pw_res(m);
   register_gemm_train(m);
+  // Streams owned by the framework (not torch's round-robin pool of 32 per device): a pooled
+  // stream handed to a runner can be the very stream another thread is capturing a hipGraph
+  // on, and then that thread's launches land in the capture (or are rejected).
+  m.def("stream_create", [](int priority) {
+    hipStream_t s = nullptr;
+    hipError_t e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority);
+    if (e != hipSuccess) throw std::runtime_error(std::string("hipStreamCreateWithPriority: ") + hipGetErrorString(e));
+    return reinterpret_cast<std::uintptr_t>(s);
+  }, pybind11::arg("priority") = 0);
+  m.def("stream_destroy", [](std::uintptr_t s) {
+    hipError_t e = hipStreamDestroy(reinterpret_cast<hipStream_t>(s));
+    if (e != hipSuccess) throw std::runtime_error(std::string("hipStreamDestroy: ") + hipGetErrorString(e));
+  });
 }

@@ -87,12 +87,17 @@ def graph_capture(graph, stream=None, pool=None):
 
     import torch
 
+    from .streams import capture_stream
+
     lock = capture_lock()
 
     @contextlib.contextmanager
     def _cm():
         with lock:
-            with torch.cuda.graph(graph, pool=pool, stream=stream, capture_error_mode="thread_local"):
+            # a framework-owned capture stream: torch's default capture stream comes from the
+            # stream pool and can coincide with a sibling subtask's replay stream (utils/streams.py)
+            s = stream if stream is not None else capture_stream()
+            with torch.cuda.graph(graph, pool=pool, stream=s, capture_error_mode="thread_local"):
                 yield
 
     return _cm()
