@@ -679,7 +679,8 @@ class LocalExecutor:
                     self.tasks.extend(chain)
                     continue
                 chain = [_ChainedTask(self, m, i, restore_states.get((m.uid, i)) if restore_states else None,
-                                      ops[(m.uid, i)]) for m in members]
+                                      ops[(m.uid, i)] if (m.uid, i) in ops else self._remote_proxy(m, i))
+                         for m in members]
                 if n.is_source:
                     t = _SourceTask(self, n, i, w, rs, chain)
                     self.sources.append(t)
@@ -689,6 +690,11 @@ class LocalExecutor:
                 self.tasks.append(_OpTask(self, n, i, w, rs, gates[(n.uid, i)], chan_of[(n.uid, i)],
                                           ops.get((n.uid, i)), chain))
                 self.tasks.extend(chain)
+
+    def _remote_proxy(self, node, subtask):
+        from .remote import RemoteOperatorProxy
+
+        return RemoteOperatorProxy(node, subtask, self)
 
     def _remote_source_chains(self, nodes) -> dict:
         """Worker-process sources: the downstream worker operators they run together with
@@ -720,9 +726,11 @@ class LocalExecutor:
         """Operator chaining (Flink's ``StreamingJobGraphGenerator.isChainable``): a node runs
         inside its upstream's thread when the edge is forward, both have the same
         parallelism, it has exactly that one input, the upstream has no other consumer, and
-        neither side is a worker-process operator, an operator that cannot chain (two-input)
-        or a node marked ``start_new_chain`` / ``disable_chaining``.  A source heads a chain
-        (``_SourceTask`` runs its members), it never joins one."""
+        neither side is an operator that cannot chain (two-input) or a node marked
+        ``start_new_chain`` / ``disable_chaining``.  A source heads a chain (``_SourceTask``
+        runs its members), it never joins one; a worker-process operator's proxy can only be
+        a chain's last member (records go from the upstream's thread straight into its slab
+        batches, no queue hand-off)."""
         if not getattr(self.env, "chaining", True):
             return {}
         consumers: dict[str, int] = {}
@@ -731,9 +739,16 @@ class LocalExecutor:
                 consumers[up.uid] = consumers.get(up.uid, 0) + 1
 
         def ok(n, head=False):
+            if not getattr(n, "chaining", True):
+                return False
+            if getattr(n, "remote", False):
+                # a worker-process operator can END a chain (its drainer thread emits into the
+                # thread-safe record writer), never feed a chained successor; remote sources
+                # chain inside their worker instead (_remote_source_chains)
+                return not head and not n.is_source
             if n.is_source:  # a source heads a chain; it never joins one
-                return head and not getattr(n, "remote", False) and getattr(n, "chaining", True)
-            return not getattr(n, "remote", False) and getattr(n, "chaining", True) and ops[(n.uid, 0)].chainable
+                return head
+            return ops[(n.uid, 0)].chainable
 
         out = {}
         for n in nodes:
