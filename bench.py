@@ -117,6 +117,9 @@ def main():
                     help="comma-separated extra batch buckets compiled next to --batch; with --dynamic the "
                          "per-step batch size varies and each micro-batch runs on the smallest bucket")
     ap.add_argument("--dynamic", action="store_true", help="variable micro-batch sizes (uniform in [B/4, B])")
+    ap.add_argument("--bucket-step", type=int, default=8,
+                    help="with --dynamic (and no --buckets): a compiled bucket every this many records from "
+                         "B/4 to B (padding to the bucket is the cost of dynamic sizes; plans share one arena)")
     ap.add_argument("--offered-rate", type=float, default=None,
                     help="open-loop latency mode: records ARRIVE at this rate (records/s per GPU, Poisson); "
                          "each is stamped at its arrival, micro-batches form in a MicroBatcher (--batch, "
@@ -190,7 +193,8 @@ def main():
 
         graph = Graph.from_graph_def(inception_v3_graph_def(image_hw=(HW, HW), top_k=5, seed=0))
         sizes = sorted({B} | {int(b) for b in (args.buckets or "").split(",") if b}
-                       | (set(range(max(32, B // 4), B, 32)) if args.dynamic and not args.buckets else set()))
+                       | (set(range(max(args.bucket_step, B // 4), B, args.bucket_step))
+                          if args.dynamic and not args.buckets else set()))
         rng = np.random.default_rng(1234 + rank)
         pool = rng.integers(0, 256, size=(args.pool, HW, HW, 3), dtype=np.uint8)
         calib = torch.from_numpy(pool[: min(64, args.pool)])
@@ -213,7 +217,8 @@ def main():
         gd = resnet50_graph_def(image_hw=(HW, HW), top_k=5, seed=0)
         graph = Graph.from_graph_def(gd)
         sizes = sorted({B} | {int(b) for b in (args.buckets or "").split(",") if b}
-                       | (set(range(max(32, B // 4), B, 32)) if args.dynamic and not args.buckets else set()))
+                       | (set(range(max(args.bucket_step, B // 4), B, args.bucket_step))
+                          if args.dynamic and not args.buckets else set()))
         for lane in range(lanes):
             arena = DeviceArena(dev, budget, name=f"rank{rank}/lane{lane}")
             plans = {}

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--remote-source", action="store_true",
                     help="the parallel source runs inside the worker processes, chained with the map "
                          "(records are produced where they are consumed; nothing crosses the coordinator)")
+    ap.add_argument("--no-chain", action="store_true", help="disable operator chaining (source and proxy threads)")
     a = ap.parse_args()
     from flink_tensorflow_amd.runtime import StreamExecutionEnvironment
     from flink_tensorflow_amd.runtime.sources import ThroughputSink
@@ -44,6 +45,8 @@ def main():
                 yield local[i % len(local)].copy()  # a freshly produced record (decode / read), not a shared buffer
 
     env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(a.workers)
+    if a.no_chain:
+        env.disable_operator_chaining()
     sink = ThroughputSink(every=512)
     src = env.generate(images)
     if a.remote_source:
@@ -58,7 +61,8 @@ def main():
                       "steady_records_per_s": round(steady, 1),
                       "steady_GB_per_s": round(steady * pool[0].nbytes / 1e9, 2),
                       "slab": os.environ.get("FTM_SLAB_BYTES", "default") != "0", "cpus": os.cpu_count(),
-                      "mode": "in-worker parallel source" if a.remote_source else "coordinator source -> workers"}),
+                      "mode": "in-worker parallel source" if a.remote_source else "coordinator source -> workers",
+                      "chained": not a.no_chain}),
           flush=True)
     assert got == n
 

@@ -100,6 +100,10 @@ class PipelinedGpuRunner:
         self.stage_chunk = stage_chunk  # records per gather + H2D piece (0: whole batch at once)
         self._native = _ext.native()
         depth = max(depth, len(self.lanes) + 2)  # every lane busy + one batch being staged
+        # batches in flight over ALL buckets (each bucket has its own ``depth`` slots): with
+        # many buckets (dynamic batch sizes) the host could otherwise run dozens of batches
+        # ahead of the GPU, adding queueing latency without adding throughput
+        self.max_inflight = depth
         self.slots: dict[int, list[_Slot]] = {}
         for b, plan in self.plans.items():
             outs = [(tuple(t.shape), t.dtype) for t in fetch_bufs(plan)]
@@ -129,6 +133,8 @@ class PipelinedGpuRunner:
         self._next[b] = (self._next[b] + 1) % len(slots)
         t0 = time.perf_counter()
         finished = self._harvest_through(slot) if slot.busy else []
+        while len(self._inflight) >= self.max_inflight:
+            finished.append(self._harvest(self._inflight[0]))
         t1 = time.perf_counter()
         # host gather into the pinned slot in pieces, each piece's H2D issued as soon as it is
         # staged (the DMA of piece i overlaps the gather of piece i+1: a batch reaches the GPU

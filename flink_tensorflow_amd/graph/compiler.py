@@ -1354,6 +1354,8 @@ class CompiledFunction(TransformerLowering):
         Ho = (H + pt + pb - kh) // sh + 1
         Wo = (W + pl + pr - kw) // sw + 1
         mode = "max" if node.op == "MaxPool" else "avg"
+        if mode == "avg" and (sh, sw) == (1, 1) and self._commute_avgpool(node, x, (kh, kw), (pt, pb, pl, pr)):
+            return
         if x.qscale is not None and C % 16 == 0:
             # pooled values stay within the input range: keep the input scale, requantise
             # only when written into a concat buffer of another scale
@@ -1376,6 +1378,79 @@ class CompiledFunction(TransformerLowering):
 
         self._emit(node.name, "pool", run, [xin], [out])
         self.vals[(node.name, 0)] = out
+
+    def _commute_avgpool(self, node: Node, x: Val, ksize, pads) -> bool:
+        """AvgPool(stride 1) -> 1x1 Conv2D (+ BN/bias, ReLU) lowered as 1x1 conv (no bias or
+        act, bf16 out) -> avgpool with the bias + act + fp8 quantisation in its epilogue.
+        Both operators are linear and the conv is pointwise, so they commute exactly (the
+        pool's count-excluding-padding divisor depends on the position only); the pool then
+        runs over Cout instead of Cin channels (Inception's pool branches: 32-192 vs
+        192-2048), and in fp8 the pooled value is no longer rounded to e4m3 before the
+        conv.  Taken when Cout <= Cin / 2 (the extra bf16 round trip of the conv output is
+        cheaper than pooling the wide input)."""
+        c = self._single_consumer(node.name)
+        if c is None or c.op != "Conv2D" or c.inputs[0][0] != node.name or c.attr("data_format", "NHWC") != "NHWC":
+            return False
+        if list(c.attr("strides") or [1, 1, 1, 1]) != [1, 1, 1, 1] or list(c.attr("dilations") or [1, 1, 1, 1]) != [1, 1, 1, 1]:
+            return False
+        wv = self._get(c.inputs[1])
+        if wv is None or not wv.is_const or tuple(wv.const.shape[:2]) != (1, 1) or x.phys_c or x.concat_slot is not None:
+            return False
+        N, H, W, C = x.shape
+        w = wv.const.float()
+        Cin, Cout = w.shape[2], w.shape[3]
+        if Cin != C or C % 16 or Cout % 16 or 2 * Cout > C or x.rows is not None:
+            return False
+        last, scale, bias, residual, act, absorbed = self._conv_chain(c)
+        if residual is not None or act not in (K.ACT_NONE, K.ACT_RELU):
+            return False
+        fp8_in = x.qscale is not None
+        if not fp8_in and x.dtype != torch.bfloat16:
+            return False
+        if scale is not None:
+            w = w * scale
+        w_ohwi = w.permute(3, 0, 1, 2).contiguous()
+        b_dev = self._dev(bias if bias is not None else torch.zeros(Cout), torch.float32)
+        y = self._new((N, H, W, Cout))  # the conv's output before bias / act (bf16, real units)
+        o_scale = self._qscale(last.name) if (self.precision == "fp8" and self._fp8_consumers_ok(last.name)) else None
+        out = self._new((N, H, W, Cout), torch.uint8 if o_scale is not None else torch.bfloat16)
+        out.qscale = o_scale
+        zero = self._dev(torch.zeros(Cout), torch.float32)
+        if fp8_in:
+            wq, ws = F8.quantize_weight(w_ohwi)
+            wq_dev, ws_dev, cs_dev = self._dev(wq), self._dev(ws), self._dev(ws * x.qscale, torch.float32)
+            self.params += [wq_dev, cs_dev, zero, b_dev]
+            self.fp8_layers += 1
+            cfg = 8 if (self.device.type == "cuda" and _cfg().conv_impl == "lite") else -1
+
+            def run_conv(x=x, y=y, wq=wq_dev, ws=ws_dev, cs=cs_dev, zero=zero, cfg=cfg, xs=x.qscale):
+                F8.conv2d_nhwc_fp8(_view(x), xs, wq, (1, 1), ws, zero, act=K.ACT_NONE, out=y.buf, chan_scale=cs,
+                                   cfg=cfg)
+
+            self._emit(c.name, "conv_fp8", run_conv, [x], [y], {"impl": "pointwise_before_avgpool"})
+        else:
+            w_dev = self._dev(w_ohwi, torch.bfloat16)
+            self.params += [w_dev, zero, b_dev]
+
+            def run_conv(x=x, y=y, w_dev=w_dev, zero=zero):  # noqa: F811
+                K.conv2d_nhwc(x.buf, w_dev, zero, None, (1, 1), (0, 0, 0, 0), (1, 1), K.ACT_NONE, out=y.buf)
+
+            self._emit(c.name, "conv", run_conv, [x], [y], {"impl": "pointwise_before_avgpool"})
+
+        def run_pool(y=y, out=out, b=b_dev, act=act, ksize=tuple(ksize), pads=tuple(pads)):
+            F8.avgpool_bias_act(y.buf, ksize, (1, 1), pads, b, act,
+                                out_scale=_eff_scale(out) if out.qscale is not None else None, out=_target(out),
+                                out_channel_offset=_coff(out))
+
+        self._emit(node.name, "pool_fp8" if o_scale is not None else "pool", run_pool, [y], [out],
+                   {"impl": "avgpool_bias_act"})
+        self._fused.add(c.name)
+        for a in absorbed:
+            self._fused.add(a.name)
+        self.vals[(last.name, 0)] = out
+        self._alias_fused_outputs(absorbed, out)
+        self.commuted_pools = getattr(self, "commuted_pools", 0) + 1
+        return True
 
     def _lower_mean(self, node: Node) -> bool:
         x = self._in(node, 0)
@@ -1794,6 +1869,7 @@ class CompiledFunction(TransformerLowering):
                 "fused_pools": getattr(self, "fused_pools", 0), "conv3x3c64": getattr(self, "conv3x3c64", 0),
                 "conv_pp": getattr(self, "conv_pp_layers", 0), "pw_res": getattr(self, "pw_res_layers", 0),
                 "conv_lite": getattr(self, "conv_lite_layers", 0),
+                "commuted_pools": getattr(self, "commuted_pools", 0),
                 "activation_bytes": self.activation_bytes,
                 "param_bytes": self.param_bytes(),
                 **({"token_capacity": self.token_cap, "first_token_only_nodes": len(self._cls_nodes)}

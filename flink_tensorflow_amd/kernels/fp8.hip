@@ -645,6 +645,94 @@ __global__ __launch_bounds__(256) void pool_fp8_kernel(const uint8_t* __restrict
   }
 }
 
+// Average pool (TF SAME: the sum divided by the in-bounds count) over a bf16 NHWC tensor,
+// then the bias + activation of the conv that PRODUCED it, written as fp8 (sat(y * out_q))
+// or bf16 into a (concat) buffer at a channel offset.  Inception's AvgPool(3x3/1) -> 1x1
+// conv branches run as 1x1 conv (no bias / act, bf16 out) -> this kernel: pool and
+// pointwise conv are both linear, so they commute, and the pool then reads Cout (32-192)
+// channels instead of Cin (192-2048).  16 channels x PX adjacent outputs per thread.
+template <bool OUT_FP8, int ACT, int PX>
+__global__ __launch_bounds__(256) void avgpool_epi_kernel(const bf16* __restrict__ x, const float* __restrict__ bias,
+                                                          uint8_t* __restrict__ y, int N, int H, int W, int C, int Ho,
+                                                          int Wo, int kh, int kw, int sh, int sw, int ph, int pw,
+                                                          int ldy, int y_coff, float out_q) {
+  const int cchunks = C / 16;
+  const int wgroups = (Wo + PX - 1) / PX;
+  const long total = (long)N * Ho * wgroups * cchunks;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int cc = idx % cchunks;
+    long t = idx / cchunks;
+    const int oxg = t % wgroups;
+    t /= wgroups;
+    const int oy = t % Ho;
+    const int n = t / Ho;
+    const int ox0 = oxg * PX;
+    float acc[PX][16];
+    int cnt_w[PX];
+#pragma unroll
+    for (int p = 0; p < PX; ++p) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[p][e] = 0.f;
+      const int lo = max((ox0 + p) * sw - pw, 0), hi = min((ox0 + p) * sw - pw + kw, W);
+      cnt_w[p] = max(hi - lo, 0);
+    }
+    int cnt_h = 0;
+    const int iy0 = oy * sh - ph, ixs = ox0 * sw - pw;
+    const int ncols = (PX - 1) * sw + kw;
+    for (int dy = 0; dy < kh; ++dy) {
+      const int iy = iy0 + dy;
+      if ((unsigned)iy >= (unsigned)H) continue;
+      ++cnt_h;
+      const bf16* row = x + ((size_t)n * H + iy) * W * C + cc * 16;
+      for (int c = 0; c < ncols; ++c) {
+        const int ix = ixs + c;
+        if ((unsigned)ix >= (unsigned)W) continue;
+        const bf16x8* src = reinterpret_cast<const bf16x8*>(row + (size_t)ix * C);
+        const bf16x8 a = src[0], b = src[1];
+#pragma unroll
+        for (int p = 0; p < PX; ++p) {
+          const int rel = c - p * sw;  // column inside output p's window?
+          if (rel < 0 || rel >= kw) continue;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            acc[p][e] += (float)a[e];
+            acc[p][8 + e] += (float)b[e];
+          }
+        }
+      }
+    }
+    float bv[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) bv[e] = bias[cc * 16 + e];
+#pragma unroll
+    for (int p = 0; p < PX; ++p) {
+      const int ox = ox0 + p;
+      if (ox >= Wo) break;
+      const float inv = 1.f / (float)max(cnt_h * cnt_w[p], 1);
+      float v[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = apply_act<ACT>(__builtin_fmaf(acc[p][e], inv, bv[e]));
+      const size_t o = (((size_t)n * Ho + oy) * Wo + ox) * ldy + y_coff + cc * 16;
+      if constexpr (OUT_FP8) {
+        u32x4 q;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) q[w] = pack4(v[4 * w] * out_q, v[4 * w + 1] * out_q, v[4 * w + 2] * out_q, v[4 * w + 3] * out_q);
+        *reinterpret_cast<u32x4*>(y + o) = q;
+      } else {
+        bf16x8 o0, o1;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          o0[e] = f2bf(v[e]);
+          o1[e] = f2bf(v[8 + e]);
+        }
+        bf16x8* dst = reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(y) + o);
+        dst[0] = o0;
+        dst[1] = o1;
+      }
+    }
+  }
+}
+
 // [N, HW, C] fp8 -> [N, C] bf16 mean * s.  One block per image, 16 channels per thread.
 __global__ __launch_bounds__(256) void gap_fp8_kernel(const uint8_t* __restrict__ x, bf16* __restrict__ y, int HW, int C,
                                                       float s) {
@@ -808,6 +896,47 @@ void pool2d_nhwc_fp8(uintptr_t x, uintptr_t y, int N, int H, int W, int C, int H
   FTM_CHECK_LAUNCH();
 }
 
+template <bool OUT_FP8, int ACT>
+void launch_avgpool_epi(const bf16* X, const float* B, uint8_t* Y, int N, int H, int W, int C, int Ho, int Wo, int kh,
+                        int kw, int sh, int sw, int ph, int pw, int ldy, int y_coff, float out_q, hipStream_t s) {
+  if (sw == 1) {
+    const long work = (long)N * Ho * ((Wo + 1) / 2) * (C / 16);
+    hipLaunchKernelGGL((avgpool_epi_kernel<OUT_FP8, ACT, 2>), dim3(grid_for(work, 256)), dim3(256), 0, s, X, B, Y, N, H,
+                       W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, ldy, y_coff, out_q);
+  } else {
+    const long work = (long)N * Ho * Wo * (C / 16);
+    hipLaunchKernelGGL((avgpool_epi_kernel<OUT_FP8, ACT, 1>), dim3(grid_for(work, 256)), dim3(256), 0, s, X, B, Y, N, H,
+                       W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, ldy, y_coff, out_q);
+  }
+}
+
+// y[.., y_coff:y_coff+C] = act(avgpool(x) + bias) (* out_q as fp8 when out_fp8, else bf16);
+// x bf16 [N, H, W, C], bias fp32 [C], act NONE or RELU.
+void avgpool_bias_act(uintptr_t x, uintptr_t bias, uintptr_t y, int N, int H, int W, int C, int Ho, int Wo, int kh,
+                      int kw, int sh, int sw, int ph, int pw, int ldy, int y_coff, int out_fp8, float out_q, int act,
+                      uintptr_t stream) {
+  if (C % 16 || ldy % 16 || y_coff % 16) throw std::invalid_argument("avgpool_bias_act: C/ldy/y_coff % 16 != 0");
+  if (act != ACT_NONE && act != ACT_RELU) throw std::invalid_argument("avgpool_bias_act: act must be NONE or RELU");
+  if (N <= 0 || Ho <= 0 || Wo <= 0 || kh <= 0 || kw <= 0 || sh <= 0 || sw <= 0)
+    throw std::invalid_argument("avgpool_bias_act: empty problem");
+  if (y_coff + C > ldy) throw std::invalid_argument("avgpool_bias_act: channel slot exceeds the output row");
+  check_align(x, 16, "x");
+  check_align(y, 16, "y");
+  if (!bias) throw std::invalid_argument("avgpool_bias_act: bias pointer is required");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  auto X = reinterpret_cast<const bf16*>(x);
+  auto B = reinterpret_cast<const float*>(bias);
+  auto Y = reinterpret_cast<uint8_t*>(y);
+  if (out_fp8) {
+    if (act == ACT_RELU) launch_avgpool_epi<true, ACT_RELU>(X, B, Y, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, ldy, y_coff, out_q, s);
+    else launch_avgpool_epi<true, ACT_NONE>(X, B, Y, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, ldy, y_coff, out_q, s);
+  } else {
+    if (act == ACT_RELU) launch_avgpool_epi<false, ACT_RELU>(X, B, Y, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, ldy, y_coff, out_q, s);
+    else launch_avgpool_epi<false, ACT_NONE>(X, B, Y, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, ldy, y_coff, out_q, s);
+  }
+  FTM_CHECK_LAUNCH();
+}
+
 void global_avgpool_fp8(uintptr_t x, uintptr_t y, int N, int HW, int C, float s, uintptr_t stream) {
   if (C % 16) throw std::invalid_argument("global_avgpool_fp8: C % 16 != 0");
   check_align(x, 16, "x");
@@ -824,5 +953,6 @@ void register_fp8(pybind11::module_& m) {
   m.def("dequantize_fp8_bf16", &dequantize_fp8_bf16);
   m.def("pool2d_nhwc_fp8", &pool2d_nhwc_fp8);
   m.def("global_avgpool_fp8", &global_avgpool_fp8);
+  m.def("avgpool_bias_act", &avgpool_bias_act);
   m.attr("fp8_igemm_num_configs") = NCFG;
 }

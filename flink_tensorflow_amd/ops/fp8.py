@@ -183,6 +183,44 @@ def pool2d_nhwc_fp8(x: torch.Tensor, ksize, stride, pad=(0, 0, 0, 0), mode="max"
     return out
 
 
+def avgpool_bias_act(x: torch.Tensor, ksize, stride, pad, bias: torch.Tensor, act=None, out_scale: float | None = None,
+                     out: torch.Tensor | None = None, out_channel_offset: int = 0) -> torch.Tensor:
+    """``act(avgpool(x) + bias)`` over bf16 NHWC ``x`` (TF SAME average: divided by the
+    in-bounds count), written as fp8 bytes of scale ``out_scale`` or as bf16 (None), into
+    ``out`` at ``out_channel_offset`` (a concat buffer).  The second half of an
+    AvgPool -> pointwise-conv branch computed as conv -> pool (``kernels/fp8.hip``
+    ``avgpool_epi_kernel``)."""
+    N, H, W, C = x.shape
+    kh, kw = ksize
+    sh, sw = stride
+    pt, pb, pl, pr = pad
+    Ho = (H + pt + pb - kh) // sh + 1
+    Wo = (W + pl + pr - kw) // sw + 1
+    a = act_code(act)
+    out_fp8 = out_scale is not None
+    if out is None:
+        out = torch.empty((N, Ho, Wo, C), dtype=torch.uint8 if out_fp8 else (torch.bfloat16 if x.is_cuda else
+                                                                               torch.float32), device=x.device)
+        out_channel_offset = 0
+    if tuple(out.shape[:3]) != (N, Ho, Wo) or out_channel_offset + C > out.shape[3]:
+        raise ValueError(f"avgpool_bias_act: out {tuple(out.shape)} cannot hold [{N},{Ho},{Wo},{C}] at "
+                         f"offset {out_channel_offset}")
+    if x.is_cuda:
+        _check(x, "x", torch.bfloat16, x.device)
+        _check(bias, "bias", torch.float32, x.device)
+        _check(out, "out", torch.uint8 if out_fp8 else torch.bfloat16, x.device)
+        _hip().avgpool_bias_act(x.data_ptr(), bias.data_ptr(), out.data_ptr(), N, H, W, C, Ho, Wo, kh, kw, sh, sw, pt,
+                                pl, out.shape[-1], out_channel_offset, int(out_fp8),
+                                1.0 / out_scale if out_fp8 else 1.0, a, _stream())
+        return out
+    xf = x.float().permute(0, 3, 1, 2)
+    s = F.avg_pool2d(F.pad(xf, (pl, pr, pt, pb)), (kh, kw), (sh, sw), divisor_override=1)
+    cnt = F.avg_pool2d(F.pad(torch.ones_like(xf[:, :1]), (pl, pr, pt, pb)), (kh, kw), (sh, sw), divisor_override=1)
+    y = _apply_act_ref((s / cnt).permute(0, 2, 3, 1)[:, :Ho, :Wo] + bias.float(), a)
+    out[..., out_channel_offset:out_channel_offset + C] = to_fp8_bytes(y / out_scale) if out_fp8 else y.to(out.dtype)
+    return out
+
+
 def global_avgpool_fp8(x: torch.Tensor, scale: float, out=None) -> torch.Tensor:
     """[N, H, W, C] fp8 → [N, C] bf16 (device) / fp32 (host) mean * scale."""
     N, H, W, C = x.shape

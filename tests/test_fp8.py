@@ -50,6 +50,8 @@ def test_inception_v3_fp8_plan_host():
     g, p16, p8 = _inception_plans("cpu")
     s8 = p8.summary()
     assert s8["glue_ops"] == [] and s8["fp8_layers"] == 93
+    # every AvgPool(3x3/1) -> 1x1 conv branch runs as 1x1 conv -> pool (+ bias/ReLU/quantise)
+    assert s8["commuted_pools"] == 9 and p16.summary()["commuted_pools"] == 9
     assert "concat" not in s8["kinds"] and "dequant" not in s8["kinds"]  # stride-written fp8 concats
     img = torch.randint(0, 256, (2, 75, 75, 3), dtype=torch.uint8)
     l16, _ = p16({"images:0": img})
@@ -159,6 +161,29 @@ def test_pool_fp8_gpu(mode):
     ref = Q.global_avgpool_fp8(x, 0.01)
     got = Q.global_avgpool_fp8(x.to(DEV), 0.01).float().cpu()
     torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("out_fp8", [True, False])
+def test_avgpool_bias_act_gpu(out_fp8):
+    """The pool half of a commuted AvgPool -> 1x1 conv branch: bf16 in, TF SAME average,
+    bias + ReLU, fp8 (or bf16) into a concat slot; against the fp32 host reference."""
+    torch.manual_seed(4)
+    x = (torch.randn(3, 17, 17, 64) * 2).to(torch.bfloat16)
+    b = torch.randn(64) * 0.5
+    so = 0.02 if out_fp8 else None
+    for ks, st, pad in (((3, 3), (1, 1), (1, 1, 1, 1)), ((3, 3), (2, 2), (0, 0, 0, 0))):
+        ref = Q.avgpool_bias_act(x.float(), ks, st, pad, b, "relu", out_scale=so)
+        Ho, Wo = ref.shape[1:3]
+        out = torch.zeros((3, Ho, Wo, 96), dtype=torch.uint8 if out_fp8 else torch.bfloat16, device=DEV)
+        Q.avgpool_bias_act(x.to(DEV), ks, st, pad, b.to(DEV), "relu", out_scale=so, out=out, out_channel_offset=32)
+        got = out.cpu()
+        assert (got[..., :32] == 0).all()
+        if out_fp8:
+            gd, rd = Q.from_fp8_bytes(got[..., 32:].contiguous()) * so, Q.from_fp8_bytes(ref) * so
+            assert ((gd - rd).abs() <= 0.13 * rd.abs() + 1e-3).all()
+        else:
+            torch.testing.assert_close(got[..., 32:].float(), ref.float(), rtol=1e-2, atol=1e-2)
 
 
 @pytest.mark.gpu

@@ -52,19 +52,19 @@ def test_remote_map_runs_in_worker_processes():
     assert len(pids) == 2 and os.getpid() not in pids
 
 
-def test_worker_operator_ends_a_chain():
-    """A worker-process operator's proxy is chained as the LAST member of its upstream's
-    chain (records go from the source thread straight into the slab batches); nothing is
-    chained behind it, and the operator still runs in the worker."""
+def test_worker_operator_is_not_chained():
+    """A worker-process operator's proxy keeps its own coordinator thread: chained behind
+    its upstream, producing records and scattering them into the slab would serialise on
+    one thread (profiles/r03_transport).  Operators around it still chain."""
     from flink_tensorflow_amd.runtime.executor import LocalExecutor
 
     env = StreamExecutionEnvironment.get_execution_environment()
     s = env.from_collection(list(range(500))).map(lambda v: v + 1).name("inc")
     s = s.map(lambda v: (os.getpid(), v)).name("remote").run_in_processes()
     sink = s.map(lambda pv: pv).name("after").collect_into()
-    ex = LocalExecutor(env, "remote-tail")
+    ex = LocalExecutor(env, "remote-alone")
     ex.execute()
-    assert ex.chains == [["collection", "inc", "remote"], ["after", "collect"]]
+    assert ex.chains == [["collection", "inc"], ["after", "collect"]]
     out = sink.results()
     assert sorted(v for _, v in out) == list(range(1, 501))
     assert {p for p, _ in out} != {os.getpid()} and len({p for p, _ in out}) == 1
