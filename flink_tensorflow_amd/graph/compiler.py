@@ -1079,11 +1079,15 @@ class CompiledFunction(TransformerLowering):
         del xs, o, o2, r
         return best
 
-    def _fusable_maxpool(self, last: Node, act, out: Val):
+    def _fusable_maxpool(self, last: Node, act, out: Val, fp8: bool = False):
         """The single consumer of a ReLU conv chain when it is a 3x3 / stride-2 NHWC
-        MaxPool whose padding is at most one row/column per side (ResNet's pool1):
+        MaxPool whose padding is at most one row/column per side (ResNet's pool1; with
+        ``fp8``, Inception's MaxPool_3a after an fp8 -> fp8 direct conv):
         ``(pool node, (top, bottom, left, right), (Hp, Wp))`` or None."""
-        if act != K.ACT_RELU or out.qscale is not None or out.dtype != torch.bfloat16:
+        if act != K.ACT_RELU:
+            return None
+        if (out.qscale is not None or out.dtype != torch.bfloat16) if not fp8 else \
+                (out.qscale is None or out.dtype != torch.uint8):
             return None
         if any(TensorName.parse(f).name == last.name for f in self.fetch_names):
             return None
@@ -1140,12 +1144,28 @@ class CompiledFunction(TransformerLowering):
             bn = 64 if Cout >= 64 else 32
             w_arr = self._dev(K.dconv_weights(wq, Cout, 1, bn))
             self.params.append(w_arr)
+            pool = self._fusable_maxpool(last, act, out, fp8=True) if stride == (1, 1) else None
+            mpad = None
+            if pool is not None:
+                # fp8 ReLU conv + 3x3/s2 max pool in one kernel (Inception's Conv2d_2b ->
+                # MaxPool_3a): the pre-pool output never reaches HBM; the pooled values keep
+                # the conv output's scale (a max never leaves the input range)
+                pnode, mpad, (Hp, Wp) = pool
+                q = out.qscale
+                out = self._new((out_nhw[0], Hp, Wp, Cout), torch.uint8)
+                out.qscale = q
+                self._fused.add(pnode.name)
 
-            def run_d(x=x, out=out, w_arr=w_arr, cs=cs_dev, b=b_dev, bn=bn):
+            def run_d(x=x, out=out, w_arr=w_arr, cs=cs_dev, b=b_dev, bn=bn, mpad=mpad):
                 K.conv2d_direct(_view(x), w_arr, (KH, KW), Cout, b, stride, pads, act, out=_target(out),
-                                out_channel_offset=_coff(out), bn=bn, chan_scale=cs, out_scale=_eff_scale(out))
+                                out_channel_offset=_coff(out), bn=bn, chan_scale=cs, out_scale=_eff_scale(out),
+                                maxpool_pad=mpad)
 
-            self._emit(node.name, "conv_fp8", run_d, [x], [out])
+            self._emit(node.name, "conv_fp8", run_d, [x], [out], {"conv_out": (*out_nhw, Cout)} if pool else None)
+            if pool is not None:
+                self.vals[(pool[0].name, 0)] = out
+                self.fused_pools = getattr(self, "fused_pools", 0) + 1
+                return
             self.vals[(last.name, 0)] = out
             self._alias_fused_outputs(absorbed, out)
             return

@@ -79,6 +79,7 @@ FTM_DEVICE uint32_t pack4_fp8(float a, float b, float c, float d) {
 }
 
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned char u8x16 __attribute__((ext_vector_type(16)));
 
 // 3x3 max over bf16 rows of the LDS output tile.  The pooled convs are ReLU convs, so every
 // value is +0 or positive (out-of-image positions enter as +0) and the bf16 bit patterns
@@ -91,6 +92,20 @@ FTM_DEVICE u16x8 pool3x3_max(const uint8_t* base, int row_bytes, int px_bytes) {
 #pragma unroll
     for (int dx = 0; dx < 3; ++dx)
       if (dy | dx) m = __builtin_elementwise_max(m, *reinterpret_cast<const u16x8*>(base + dy * row_bytes + dx * px_bytes));
+  return m;
+}
+
+// The same over e4m3 bytes (fp8 chains, e.g. Inception's Conv2d_2b -> MaxPool_3a): a ReLU
+// output is +0 or positive and saturated below the NaN code, so the e4m3 bytes order like
+// the values too: an unsigned byte max of the already-quantised tile (exactly the max pool
+// of the fp8 values the unfused layers would store).
+FTM_DEVICE u8x16 pool3x3_max_u8(const uint8_t* base, int row_bytes, int px_bytes) {
+  u8x16 m = *reinterpret_cast<const u8x16*>(base);
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx)
+      if (dy | dx) m = __builtin_elementwise_max(m, *reinterpret_cast<const u8x16*>(base + dy * row_bytes + dx * px_bytes));
   return m;
 }
 
@@ -235,16 +250,18 @@ __global__ __launch_bounds__(WAVES * 64) void dconv_kernel(DconvParams p) {
   constexpr int EPO = 16 / OB;
   constexpr int CPR = BN / EPO;
   if constexpr (POOL) {
-    static_assert(!OUT_FP8, "pooled epilogue is bf16");
     for (int q = tid; q < PTH * 8 * CPR; q += NTH) {
       const int pp = q / CPR, cc = q % CPR;
       const int pyl = pp >> 3, pxl = pp & 7;
       const int py = (oy0 + p.ppt) / 2 + pyl, px = (ox0 + p.ppl) / 2 + pxl;
       const int c = n0 + cc * EPO;
       if (py >= p.Hp || px >= p.Wp || c >= p.Cout) continue;
-      const u16x8 m = pool3x3_max(Os + ((2 * pyl) * TPW + 2 * pxl) * OLD + cc * 16, TPW * OLD, OLD);
+      const uint8_t* src = Os + ((2 * pyl) * TPW + 2 * pxl) * OLD + cc * 16;
       const size_t mo = ((size_t)n * p.Hp + py) * p.Wp + px;
-      *reinterpret_cast<u16x8*>(p.y + (mo * p.ldy + p.y_coff + c) * 2) = m;
+      if constexpr (OUT_FP8)
+        *reinterpret_cast<u8x16*>(p.y + mo * p.ldy + p.y_coff + c) = pool3x3_max_u8(src, TPW * OLD, OLD);
+      else
+        *reinterpret_cast<u16x8*>(p.y + (mo * p.ldy + p.y_coff + c) * 2) = pool3x3_max(src, TPW * OLD, OLD);
     }
     return;
   }
@@ -262,8 +279,8 @@ __global__ __launch_bounds__(WAVES * 64) void dconv_kernel(DconvParams p) {
 template <int ES, int BN, bool OUT_FP8, int WAVES>
 void launch_act(const DconvParams& p, int act, size_t lds, hipStream_t s) {
   dim3 grid(p.N * p.tiles_h * p.tiles_w * p.tiles_n), block(WAVES * 64);
-  if constexpr (ES == 2 && !OUT_FP8) {
-    if (p.Hp > 0) {  // fused max pool (ReLU stems)
+  if constexpr ((ES == 2 && !OUT_FP8) || (ES == 1 && OUT_FP8)) {
+    if (p.Hp > 0) {  // fused max pool (ReLU stems; fp8 -> fp8 chains)
       if (act != ACT_RELU) throw std::invalid_argument("dconv: fused pool needs a ReLU conv");
       static bool done = false;
       if (!done) {
@@ -275,7 +292,7 @@ void launch_act(const DconvParams& p, int act, size_t lds, hipStream_t s) {
       return;
     }
   } else {
-    if (p.Hp > 0) throw std::invalid_argument("dconv: fused pool is bf16-only");
+    if (p.Hp > 0) throw std::invalid_argument("dconv: fused pool needs bf16 -> bf16 or fp8 -> fp8");
   }
   switch (act) {
     case ACT_NONE:

@@ -123,3 +123,41 @@ def test_dconv_maxpool_gpu(case, pool_rows):
                           maxpool_pad=mp, pool_rows=pool_rows).cpu()
     assert got.shape == ref.shape
     torch.testing.assert_close(got.float(), ref.float(), rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+
+
+FP8_POOL_CASES = [  # N, H, W, Cin, Cout, stride-1 3x3 pad, pool padding, bn
+    (2, 37, 37, 32, 64, (0, 0, 0, 0), "VALID", 64),  # Inception Conv2d_2b -> MaxPool_3a at 1/4 scale
+    (1, 30, 41, 32, 32, (1, 1, 1, 1), "SAME", 32),
+    (2, 33, 33, 64, 64, (1, 1, 1, 1), "VALID", 64),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pool_rows", [7, 14])
+@pytest.mark.parametrize("case", FP8_POOL_CASES)
+def test_dconv_fp8_maxpool_gpu(case, pool_rows):
+    """fp8 -> fp8 direct conv + ReLU + fused 3x3/s2 max pool == the same kernel unpooled,
+    then the fp8 pool kernel: bit-exact (the max runs over the same quantised bytes)."""
+    N, H, W, Cin, Cout, pad, ppad, bn = case
+    torch.manual_seed(H + Cin + Cout)
+    x = torch.randn(N, H, W, Cin).relu()
+    sx = Q.scale_for(x.max())
+    xq = Q.quantize(x, sx).to(DEV)
+    wq, ws = Q.quantize_weight(torch.randn(Cout, 3, 3, Cin) / (9 * Cin) ** 0.5)
+    b = (torch.randn(Cout) * 0.1).to(DEV)
+    arr = K.dconv_weights(wq, Cout, 1, bn).to(DEV)
+    cs = (ws * sx).to(DEV)
+    so = 0.02
+    conv = K.conv2d_direct(xq, arr, (3, 3), Cout, b, (1, 1), pad, "relu", bn=bn, chan_scale=cs, out_scale=so)
+    Ho, Wo = conv.shape[1:3]
+    if ppad == "SAME":
+        ph = max((-(-Ho // 2) - 1) * 2 + 3 - Ho, 0)
+        pw = max((-(-Wo // 2) - 1) * 2 + 3 - Wo, 0)
+        mp = (ph // 2, ph - ph // 2, pw // 2, pw - pw // 2)
+    else:
+        mp = (0, 0, 0, 0)
+    ref = Q.pool2d_nhwc_fp8(conv, (3, 3), (2, 2), mp, "max").cpu()
+    got = K.conv2d_direct(xq, arr, (3, 3), Cout, b, (1, 1), pad, "relu", bn=bn, chan_scale=cs, out_scale=so,
+                          maxpool_pad=mp, pool_rows=pool_rows).cpu()
+    assert got.shape == ref.shape and got.dtype == torch.uint8
+    assert torch.equal(got, ref)

@@ -195,6 +195,7 @@ def test_inception_v3_fp8_plan_gpu():
     host = CompiledFunction(g, feeds, ["logits:0"], "cpu", strict=True, precision="fp8", calibration=calib)
     dev = CompiledFunction(g, feeds, ["logits:0"], DEV, strict=True, precision="fp8", calibration=calib)
     assert dev.summary()["hip_graph"] and dev.summary()["fp8_layers"] == 93
+    assert dev.summary()["fused_pools"] == 1  # Conv2d_2b (fp8 direct conv) + MaxPool_3a
     lh = host({"images:0": img})[0]
     ld = dev({"images:0": img.to(DEV)})[0].cpu()
     assert F.cosine_similarity(lh.flatten(), ld.flatten(), dim=0) > 0.99
