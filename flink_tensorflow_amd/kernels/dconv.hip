@@ -284,11 +284,11 @@ void launch_act(const DconvParams& p, int act, size_t lds, hipStream_t s) {
       if (act != ACT_RELU) throw std::invalid_argument("dconv: fused pool needs a ReLU conv");
       static bool done = false;
       if (!done) {
-        hipFuncSetAttribute((const void*)dconv_kernel<ES, BN, ACT_RELU, false, true, WAVES>,
+        hipFuncSetAttribute((const void*)dconv_kernel<ES, BN, ACT_RELU, OUT_FP8, true, WAVES>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         done = true;
       }
-      hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_RELU, false, true, WAVES>), grid, block, lds, s, p);
+      hipLaunchKernelGGL((dconv_kernel<ES, BN, ACT_RELU, OUT_FP8, true, WAVES>), grid, block, lds, s, p);
       return;
     }
   } else {

@@ -1034,6 +1034,7 @@ def conv2d_direct(x: torch.Tensor, w_arr: torch.Tensor, kshape, Cout: int, bias:
     _check(x, "x", x.dtype, x.device)
     _check(w_arr, "w", torch.uint8, x.device)
     _check(bias, "bias", torch.float32, x.device)
+    _check(out, "out", torch.uint8 if out_fp8 else torch.bfloat16, x.device)  # the kernel writes out_fp8 ? 1 : 2 B
     _hip().dconv(x.data_ptr(), w_arr.data_ptr(), _ptr(chan_scale), bias.data_ptr(), out.data_ptr(), es, N, H, W, Cin,
                  Cout, KH, KW, s, pt, pl, Ho, Wo, w_arr.shape[1], out.shape[3], out_channel_offset, int(out_fp8),
                  1.0 / out_scale if out_fp8 else 1.0, act_code(act), bn, _stream(), Hp, Wp, ppt, ppl,

@@ -1,4 +1,4 @@
-# round 3 (session 2) Q: fp8 direct conv + fused 3x3/s2 max pool (Inception Conv2d_2b ->
+# round 3 (session 2) Q (rerun after the pooled fp8 template fix): fp8 direct conv + fused 3x3/s2 max pool (Inception Conv2d_2b ->
 # MaxPool_3a); stream --processes re-measured
 source tools/gpu_calls/gpu_steps.sh
 step pytest_q 300 python -u -m pytest tests/test_dconv.py tests/test_fp8.py -m gpu -x -q --timeout 120 --timeout-method thread
