@@ -1145,6 +1145,16 @@ class CompiledFunction(TransformerLowering):
             w_arr = self._dev(K.dconv_weights(wq, Cout, 1, bn))
             self.params.append(w_arr)
             pool = self._fusable_maxpool(last, act, out, fp8=True) if stride == (1, 1) else None
+            if pool is not None:
+                # pooled tiles cover 14 x 8 pooled pixels with 8 waves x 64 conv pixels; fuse
+                # only when that tiling wastes little conv work (Inception's 73x73 pool rounds to
+                # 84 x 80 and costs 1.42x the convs: 445 µs fused vs 236 + 132 µs apart)
+                _, Hp_, Wp_ = pool[0], *pool[2]
+                waves = K._dconv_waves(None, None, bn)
+                pr_ = 14 if waves == 8 else 7
+                work = -(-Hp_ // pr_) * -(-Wp_ // 8) * 64 * waves
+                if work > 1.15 * out_nhw[1] * out_nhw[2]:
+                    pool = None
             mpad = None
             if pool is not None:
                 # fp8 ReLU conv + 3x3/s2 max pool in one kernel (Inception's Conv2d_2b ->

@@ -341,13 +341,20 @@ void launch_tile(const Fp8Params& p, int act, int cfg, hipStream_t s) {
 // igemm_fp8_kernel (per-channel dequant scale + bias + act, e4m3 or bf16 output at a
 // channel offset of a wider buffer).
 // ---------------------------------------------------------------------------------------
-template <bool OUT_FP8, int ACT>
+// BN_ = 64 halves the channel tile for Cout that 128 would pad badly (192 = 3 x 64 instead
+// of 2 x 128; 160, 320, 448 ...); NSTG = 1 (a single LDS stage) when the whole K fits one
+// K-tile (K <= 128: no prefetch to overlap, and half the LDS lets more workgroups hide the
+// load latency of these streaming layers).
+template <bool OUT_FP8, int ACT, int BN_ = 128, int NSTG = 2>
 __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p) {
-  constexpr int BM = 128, BN = 128;
+  static_assert(BN_ == 128 || BN_ == 64, "channel tile 128 or 64");
+  constexpr int BM = 128, BN = BN_;
+  constexpr int NI = BN / 32;  // weight fragments per wave (a wave covers BN / 2 channels)
+  constexpr int WQ = BN / 32;  // weight DMA rows-of-8 per wave
   constexpr int XB = BM * BK, WB = BN * BK, STG = XB + WB;
   constexpr int OB = OUT_FP8 ? 1 : 2;
   constexpr int OLD = BN * OB + 16;
-  constexpr int LDS = 2 * STG > BM * OLD ? 2 * STG : BM * OLD;
+  constexpr int LDS = NSTG * STG > BM * OLD ? NSTG * STG : BM * OLD;
   __shared__ __attribute__((aligned(1024))) uint8_t smem[LDS];
 
   const int nwg = p.tiles_m * p.tiles_n;
@@ -382,8 +389,8 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p) {
     const int iw0 = ow * p.sw - p.pw;
     pb[q] = ((n * p.H + ih0) * p.W + iw0) * p.Cin;
     ihw[q] = (ih0 << 16) | (iw0 & 0xFFFF);
-    const unsigned co = n0 + r;
-    wrow[q] = co < (unsigned)p.Cout ? co * (unsigned)p.K : 0x80000000u;
+    const unsigned co = n0 + 8 * (WQ * wave + q) + drow;  // weight rows: WQ rows-of-8 per wave
+    wrow[q] = (q < WQ && co < (unsigned)p.Cout) ? co * (unsigned)p.K : 0x80000000u;
   }
   // K walk of this lane's chunk: k = kt * 128 + dchunk * 16 -> (tap, ci), tap -> (kh, kw)
   const int ntaps = p.KH * p.KW;
@@ -398,7 +405,7 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p) {
     const int dih = kh * p.dh, diw = kw * p.dw;
     const int toff = (dih * p.W + diw) * p.Cin + ci;
     uint8_t* bx = smem + stage * STG + 4 * wave * 8 * BK;
-    uint8_t* bw = bx + XB;
+    uint8_t* bw = smem + stage * STG + XB + WQ * wave * 8 * BK;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int ih = (ihw[q] >> 16) + dih;
@@ -406,9 +413,11 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p) {
       const bool ok = kin && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(bx + q * 8 * BK), 16,
                                                ok ? (unsigned)(pb[q] + toff) : 0x80000000u, 0, 0, 0);
-      const unsigned wo = (k < p.K && wrow[q] != 0x80000000u) ? wrow[q] + (unsigned)k : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 8 * BK), 16,
-                                               wo, 0, 0, 0);
+      if (q < WQ) {
+        const unsigned wo = (k < p.K && wrow[q] != 0x80000000u) ? wrow[q] + (unsigned)k : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 8 * BK), 16,
+                                                 wo, 0, 0, 0);
+      }
     }
     // advance to the next K-tile
     k += BK;
@@ -429,25 +438,25 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p) {
   const int frow = lane & 15;
   const int c0 = 2 * (lane >> 4);
   const int sl0 = (c0 ^ (frow & 7)) << 4, sl1 = ((c0 + 1) ^ (frow & 7)) << 4;
-  f32x4 acc[4][4];
+  f32x4 acc[NI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (p.K + BK - 1) / BK;
+  const int nk = NSTG == 1 ? 1 : (p.K + BK - 1) / BK;  // NSTG 1: the host guarantees K <= BK
   dma(0);
   for (int kt = 0; kt < nk; ++kt) {
-    const int st = kt & 1;
+    const int st = NSTG == 1 ? 0 : (kt & 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (kt + 1 < nk) dma(st ^ 1);
+    if (NSTG > 1 && kt + 1 < nk) dma(st ^ 1);
     const uint8_t* xs = smem + st * STG;
     const uint8_t* ws = xs + XB;
-    i32x8 a[4], b[4];
+    i32x8 a[NI], b[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint8_t* r = ws + (wn * 64 + i * 16 + frow) * BK;
+    for (int i = 0; i < NI; ++i) {
+      const uint8_t* r = ws + (wn * (BN / 2) + i * 16 + frow) * BK;
       const u32x4 lo = *reinterpret_cast<const u32x4*>(r + sl0), hi = *reinterpret_cast<const u32x4*>(r + sl1);
       a[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
@@ -458,7 +467,7 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p) {
       b[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, E8M0_ONE, 0,
@@ -468,8 +477,8 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p) {
 
   uint8_t* Os = smem;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int cl = wn * 64 + i * 16 + (lane >> 4) * 4;
+  for (int i = 0; i < NI; ++i) {
+    const int cl = wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
     f32x4 sv = {0.f, 0.f, 0.f, 0.f}, bv = {0.f, 0.f, 0.f, 0.f};
     if (n0 + cl < p.Cout) {
       sv = *reinterpret_cast<const f32x4*>(p.scale + n0 + cl);
@@ -506,16 +515,31 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p) {
   }
 }
 
-template <bool OUT_FP8>
-void launch_lite_fp8(const Fp8Params& p0, int act, hipStream_t s) {
-  Fp8Params p = p0;
+template <bool OUT_FP8, int BN_, int NSTG>
+void launch_lite_fp8_t(Fp8Params p, int act, hipStream_t s) {
   p.tiles_m = (p.M + 127) / 128;
-  p.tiles_n = (p.Cout + 127) / 128;
+  p.tiles_n = (p.Cout + BN_ - 1) / BN_;
   dim3 grid(p.tiles_m * p.tiles_n), block(256);
   switch (act) {
-    case ACT_NONE: hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_NONE>), grid, block, 0, s, p); break;
-    case ACT_RELU: hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_RELU>), grid, block, 0, s, p); break;
+    case ACT_NONE: hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_NONE, BN_, NSTG>), grid, block, 0, s, p); break;
+    case ACT_RELU: hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_RELU, BN_, NSTG>), grid, block, 0, s, p); break;
     default: throw std::invalid_argument("fp8 conv_lite: activation must be none/relu");
+  }
+}
+
+// channel tile: 64 when it pads Cout less than 128 (Cout % 128 in (0, 64]: 192, 320, 448,
+// <= 64); one LDS stage when K fits one K-tile.  ``bn`` > 0 forces the channel tile.
+template <bool OUT_FP8>
+void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, int bn = 0) {
+  const int r = p.Cout % 128;
+  const bool n64 = bn ? bn == 64 : (r > 0 && r <= 64);
+  const bool one = p.K <= BK;
+  if (n64) {
+    if (one) launch_lite_fp8_t<OUT_FP8, 64, 1>(p, act, s);
+    else launch_lite_fp8_t<OUT_FP8, 64, 2>(p, act, s);
+  } else {
+    if (one) launch_lite_fp8_t<OUT_FP8, 128, 1>(p, act, s);
+    else launch_lite_fp8_t<OUT_FP8, 128, 2>(p, act, s);
   }
 }
 

@@ -117,6 +117,11 @@ def test_conv_fp8_lite_shapes_gpu():
     _conv_case(80, 192, 3, 1, (1, 1, 1, 1), False, True, 8, offset=64, extra=128)
     _conv_case(768, 128, 1, 1, (0, 0, 0, 0), False, True, 8, N=4, H=9, W=9)
     _conv_case(16, 32, 3, 1, (1, 1, 1, 1), False, False, 8)
+    # channel tile 64 (Cout % 128 in (0, 64]) and the single-stage K <= 128 variants
+    _conv_case(64, 80, 1, 1, (0, 0, 0, 0), False, True, 8, N=3, H=13, W=13)      # K 64: one stage, BN 128
+    _conv_case(64, 192, 1, 1, (0, 0, 0, 0), False, True, 8, offset=64, extra=128)  # one stage, BN 64
+    _conv_case(32, 320, 3, 1, (1, 1, 1, 1), False, False, 8)                     # BN 64, 5 tiles
+    _conv_case(128, 448, 1, 1, (0, 0, 0, 0), False, True, 8, N=2, H=9, W=9)      # K 128 exactly, BN 64
 
 
 @pytest.mark.gpu
@@ -195,7 +200,8 @@ def test_inception_v3_fp8_plan_gpu():
     host = CompiledFunction(g, feeds, ["logits:0"], "cpu", strict=True, precision="fp8", calibration=calib)
     dev = CompiledFunction(g, feeds, ["logits:0"], DEV, strict=True, precision="fp8", calibration=calib)
     assert dev.summary()["hip_graph"] and dev.summary()["fp8_layers"] == 93
-    assert dev.summary()["fused_pools"] == 1  # Conv2d_2b (fp8 direct conv) + MaxPool_3a
+    # Conv2d_2b + MaxPool_3a stay apart: the pooled tiling would waste > 15 % of the conv work
+    assert dev.summary()["fused_pools"] == 0
     lh = host({"images:0": img})[0]
     ld = dev({"images:0": img.to(DEV)})[0].cpu()
     assert F.cosine_similarity(lh.flatten(), ld.flatten(), dim=0) > 0.99
