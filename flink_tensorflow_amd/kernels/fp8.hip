@@ -341,13 +341,13 @@ void launch_tile(const Fp8Params& p, int act, int cfg, hipStream_t s) {
 // igemm_fp8_kernel (per-channel dequant scale + bias + act, e4m3 or bf16 output at a
 // channel offset of a wider buffer).
 // ---------------------------------------------------------------------------------------
-// BN_ = 64 halves the channel tile for Cout that 128 would pad badly (192 = 3 x 64 instead
-// of 2 x 128; 160, 320, 448 ...); NSTG = 1 (a single LDS stage) when the whole K fits one
+// BN_ = 96 / 64 for Cout that a 128-wide channel tile would pad badly (96, 192 = 2 x 96,
+// 80, 160, 288 on 96; 320, 448, <= 64 on 64); NSTG = 1 (a single LDS stage) when the whole K fits one
 // K-tile (K <= 128: no prefetch to overlap, and half the LDS lets more workgroups hide the
 // load latency of these streaming layers).
 template <bool OUT_FP8, int ACT, int BN_ = 128, int NSTG = 2>
 __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p) {
-  static_assert(BN_ == 128 || BN_ == 64, "channel tile 128 or 64");
+  static_assert(BN_ == 128 || BN_ == 96 || BN_ == 64, "channel tile 128, 96 or 64");
   constexpr int BM = 128, BN = BN_;
   constexpr int NI = BN / 32;  // weight fragments per wave (a wave covers BN / 2 channels)
   constexpr int WQ = BN / 32;  // weight DMA rows-of-8 per wave
@@ -527,20 +527,30 @@ void launch_lite_fp8_t(Fp8Params p, int act, hipStream_t s) {
   }
 }
 
-// channel tile: 64 when it pads Cout less than 128 (Cout % 128 in (0, 64]: 192, 320, 448,
-// <= 64); one LDS stage when K fits one K-tile.  ``bn`` > 0 forces the channel tile.
+// channel tile: the one of 128 / 96 / 64 that pads Cout least (ties go to the wider tile:
+// more reuse of each pixel row); one LDS stage when K fits one K-tile.  ``bn`` > 0 forces it.
+int lite_fp8_bn(int Cout) {
+  int best = 128, pad = (Cout + 127) / 128 * 128;
+  for (int bn : {96, 64}) {
+    const int pd = (Cout + bn - 1) / bn * bn;
+    if (pd < pad) best = bn, pad = pd;
+  }
+  return best;
+}
+
 template <bool OUT_FP8>
 void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, int bn = 0) {
-  const int r = p.Cout % 128;
-  const bool n64 = bn ? bn == 64 : (r > 0 && r <= 64);
+  const int b = bn ? bn : lite_fp8_bn(p.Cout);
   const bool one = p.K <= BK;
-  if (n64) {
-    if (one) launch_lite_fp8_t<OUT_FP8, 64, 1>(p, act, s);
-    else launch_lite_fp8_t<OUT_FP8, 64, 2>(p, act, s);
-  } else {
-    if (one) launch_lite_fp8_t<OUT_FP8, 128, 1>(p, act, s);
-    else launch_lite_fp8_t<OUT_FP8, 128, 2>(p, act, s);
-  }
+#define FTM_LITE(BN_)                                                     \
+  do {                                                                    \
+    if (one) launch_lite_fp8_t<OUT_FP8, BN_, 1>(p, act, s);               \
+    else launch_lite_fp8_t<OUT_FP8, BN_, 2>(p, act, s);                   \
+  } while (0)
+  if (b == 64) FTM_LITE(64);
+  else if (b == 96) FTM_LITE(96);
+  else FTM_LITE(128);
+#undef FTM_LITE
 }
 
 // cfg value selecting conv_lite_fp8 (fp8 input only; any conv geometry with Cin % 16 == 0)

@@ -122,6 +122,8 @@ def test_conv_fp8_lite_shapes_gpu():
     _conv_case(64, 192, 1, 1, (0, 0, 0, 0), False, True, 8, offset=64, extra=128)  # one stage, BN 64
     _conv_case(32, 320, 3, 1, (1, 1, 1, 1), False, False, 8)                     # BN 64, 5 tiles
     _conv_case(128, 448, 1, 1, (0, 0, 0, 0), False, True, 8, N=2, H=9, W=9)      # K 128 exactly, BN 64
+    _conv_case(96, 96, 3, 1, (1, 1, 1, 1), False, True, 8, offset=32, extra=64)   # BN 96
+    _conv_case(48, 160, (1, 7), 1, (0, 0, 3, 3), False, False, 8, N=2, H=9, W=9)  # BN 96, 2 tiles
 
 
 @pytest.mark.gpu
