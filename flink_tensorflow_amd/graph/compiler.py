@@ -924,6 +924,32 @@ class CompiledFunction(TransformerLowering):
             K.conv1x1_dual(xin.buf, x2.buf, w_dev, b_dev, s2cfg["s2"], act, out=_target(out),
                            out_channel_offset=_coff(out))
 
+        if (self.device.type == "cuda" and _cfg().conv_impl == "lite" and not use_pw and K1 % 64 == 0
+                and C2 % 64 == 0 and (xin.phys_c or K1) == K1 and (x2.phys_c or C2) == C2
+                and act in (K.ACT_NONE, K.ACT_RELU) and out.dtype == torch.bfloat16 and out.qscale is None
+                and _coff(out) % 8 == 0 and len(xin.shape) == 4):
+            # expand + projection shortcut as one 4-wave LDS-DMA implicit GEMM over two
+            # sources (kernels/conv_pp.hip conv_lite, DUAL); planned for x2 as it is and, when
+            # _decimate_tails later stores x2 decimated, for the compact stride-1 layout
+            xs0 = (tuple(xin.shape), (1, 1), (1, 1), (0, 0), (1, 1))
+            lite = {s2: K.ConvPP([xs0, (tuple(x2.shape), (1, 1), (s2, s2), (0, 0), (1, 1))], Cout, (Ho, Wo),
+                                 self.device, tile=2)}
+            N2, H2, W2, _ = x2.shape
+            if s2 == 2 and H2 % 2 == 0 and W2 % 2 == 0:
+                lite[1] = K.ConvPP([xs0, ((N2, H2 // 2, W2 // 2, C2), (1, 1), (1, 1), (0, 0), (1, 1))], Cout, (Ho, Wo),
+                                   self.device, tile=2)
+
+            def run(xin=xin, x2=x2, out=out, w_dev=w_dev, b_dev=b_dev, s2cfg=s2cfg, lite=lite):  # noqa: F811
+                lite[s2cfg["s2"]]([xin.buf, x2.buf], w_dev, b_dev, None, act, out=_target(out),
+                                  out_channel_offset=_coff(out))
+
+            self._emit(node.name, "conv", run, [xin, x2], [out], {"s2cfg": s2cfg, "impl": "conv_lite_dual"})
+            self.conv_lite_layers = getattr(self, "conv_lite_layers", 0) + 1
+            self.vals[(last.name, 0)] = out
+            self._alias_fused_outputs(absorbed, out)
+            self.fused_shortcuts = getattr(self, "fused_shortcuts", 0) + 1
+            return True
+
         pp = None
         if (xin.phys_c or K1) == K1 and (x2.phys_c or C2) == C2:
             pp = self._conv_pp_choice(node.name, [(tuple(xin.shape), (1, 1), (1, 1), (0, 0), (1, 1)),

@@ -63,6 +63,7 @@ struct CPParams {
   int tiles_m, tiles_n;
   int kt_per_split;
   long split_stride;
+  int nk0;  // conv_lite with two sources: K-tiles of source 0 (source 1 follows, pointwise)
 };
 
 #define CP_FENCE() __builtin_amdgcn_sched_barrier(0)
@@ -395,7 +396,10 @@ FTM_DEVICE int lite_slot(int row, int chunk) {
   else return chunk ^ ((row >> 2) & 3);
 }
 
-template <int ACT, bool HAS_RES, int BK>
+// DUAL: a second, pointwise and unpadded source (the strided projection input of a ResNet
+// block's first expand: y = x W_e + x2[::s] W_p in one K loop); its K-tiles follow source
+// 0's, the weight rows are [W_e | W_p].
+template <int ACT, bool HAS_RES, int BK, bool DUAL = false>
 __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
   // BK = 64: 128-B LDS rows, 2 x 32 KiB stages, 2 MFMA steps per K-tile.
   // BK = 32: 64-B rows, 2 x 16 KiB stages (the igemm's footprint: four workgroups per CU),
@@ -434,8 +438,13 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
       (void*)p.w, 0, (int)((unsigned)p.N * (unsigned)p.ldw * 2u), 0x00020000);
   // fixed-size (QX <= 4): arrays sized by the template-dependent QX made hipcc's host pass
   // drop the kernel by SFINAE (an undefined device stub at load time)
-  int pb[4], hw[4];
+  int pb[4], hw[4], pb1[4];
   unsigned offw[4];
+  const CSrc& S1 = p.s[1];
+  __amdgpu_buffer_rsrc_t rx1 = rx;
+  if constexpr (DUAL)
+    rx1 = __builtin_amdgcn_make_buffer_rsrc((void*)S1.x, 0, (int)(nimg * (unsigned)(S1.H * S1.W) * (unsigned)S1.C * 2u),
+                                            0x00020000);
   const int ohw = p.OH * p.OW;
 #pragma unroll
   for (int q = 0; q < QX; ++q) {
@@ -450,6 +459,7 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
     const int iw0 = ow * S.sw - S.pw;
     pb[q] = ((n * S.H + ih0) * S.W + iw0) * S.C * 2 + dchunk * 16;
     hw[q] = (ih0 << 16) | (iw0 & 0xFFFF);
+    if constexpr (DUAL) pb1[q] = live ? ((n * S1.H + oh * S1.sh) * S1.W + ow * S1.sw) * S1.C * 2 + dchunk * 16 : -1;
     const unsigned co = n0 + r;
     offw[q] = co < (unsigned)p.N ? (co * p.ldw + dchunk * 8) * 2u : 0x80000000u;
   }
@@ -459,9 +469,25 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
   const int cpt = S.C / BK;  // K-tiles per filter tap
   int cc = 0, kw = 0, kh = 0, kt_dma = 0;
   auto dma = [&](int stage) {
+    const unsigned woff = (unsigned)kt_dma * (unsigned)ROWB;
+    if constexpr (DUAL) {
+      if (kt_dma >= p.nk0) {  // source 1 (uniform branch: kt_dma is wave-uniform)
+        const int delta1 = (kt_dma - p.nk0) * BK * 2;
+        ++kt_dma;
+        uint8_t* bx = smem + stage * STG + QX * wave * RPI * ROWB;
+        uint8_t* bw = bx + XB;
+#pragma unroll
+        for (int q = 0; q < QX; ++q) {
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rx1, (__attribute__((address_space(3))) void*)(bx + q * 1024), 16,
+                                                   pb1[q] >= 0 ? (unsigned)(pb1[q] + delta1) : 0x80000000u, 0, 0, 0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 1024), 16,
+                                                   offw[q], woff, 0, 0);
+        }
+        return;
+      }
+    }
     const int dih = kh * p.dh, diw = kw * p.dw;
     const int delta = ((dih * S.W + diw) * S.C + cc * BK) * 2;
-    const unsigned woff = (unsigned)kt_dma * (unsigned)ROWB;
     ++kt_dma;
     if (++cc == cpt) {
       cc = 0;
@@ -561,9 +587,17 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
 
 // lite_bk: 64 (tile 2) or 32 (tile 3)
 template <int ACT, int BK>
-void launch_lite(const CPParams& p, hipStream_t s) {
-  if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, BK>), dim3(p.tiles_m * p.tiles_n), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, BK>), dim3(p.tiles_m * p.tiles_n), dim3(256), 0, s, p);
+void launch_lite(const CPParams& p, hipStream_t s, bool dual = false) {
+  const dim3 grid(p.tiles_m * p.tiles_n), block(256);
+  if constexpr (BK == 64) {
+    if (dual) {
+      if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, BK, true>), grid, block, 0, s, p);
+      else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, BK, true>), grid, block, 0, s, p);
+      return;
+    }
+  }
+  if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, BK>), grid, block, 0, s, p);
+  else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, BK>), grid, block, 0, s, p);
 }
 
 template <int ACT, bool HAS_RES>
@@ -676,6 +710,10 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
       p.KW = KW;
       p.dh = dh;
       p.dw = dw;
+      p.nk0 = (int)(K / 64);
+    } else if (tile == 2) {  // conv_lite's second source: pointwise, unpadded, in range
+      need(KH == 1 && KW == 1 && S.ph == 0 && S.pw == 0, "the 4-wave tile's second source must be 1x1 unpadded");
+      need((OH - 1) * S.sh < S.H && (OW - 1) * S.sw < S.W, "second source smaller than the output grid");
     }
   }
   for (int i = ns; i < 2; ++i) p.s[i] = p.s[0];
@@ -695,7 +733,7 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   p.ldw = (int)K; p.ldy = ldy; p.y_coff = y_coff; p.ldr = ldr;
   need(tile >= 0 && tile <= 3, "tile must be 0 (256x256), 1 (512x128), 2 / 3 (128x128, 4 waves, K-tile 64 / 32)");
   const bool lite = tile >= 2;
-  need(!lite || (ns == 1 && splits <= 1), "the 4-wave tile takes one source and no split-K");
+  need(!lite || ((ns == 1 || tile == 2) && splits <= 1), "the 4-wave tile takes no split-K (two sources: tile 2)");
   need(tile != 3 || p.s[0].C % 32 == 0, "the 32-deep 4-wave tile needs Cin % 32 == 0");
   const int BM = tile == 1 ? 512 : lite ? 128 : 256, BN = tile == 1 ? 128 : lite ? 128 : 256;
   p.tiles_m = (p.M + BM - 1) / BM;
@@ -713,9 +751,9 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   float* wsp = reinterpret_cast<float*>(ws);
   if (lite) {
     switch (act * 2 + (tile == 3)) {
-      case ACT_NONE * 2: launch_lite<ACT_NONE, 64>(p, s); break;
+      case ACT_NONE * 2: launch_lite<ACT_NONE, 64>(p, s, ns == 2); break;
       case ACT_NONE * 2 + 1: launch_lite<ACT_NONE, 32>(p, s); break;
-      case ACT_RELU * 2: launch_lite<ACT_RELU, 64>(p, s); break;
+      case ACT_RELU * 2: launch_lite<ACT_RELU, 64>(p, s, ns == 2); break;
       case ACT_RELU * 2 + 1: launch_lite<ACT_RELU, 32>(p, s); break;
       default: throw std::invalid_argument("conv_pp: unsupported activation");
     }

@@ -48,6 +48,11 @@ CASES = [
     ("lite_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (7, 7), True, "relu", 2, None),
     ("lite_1x1", [((2, 14, 14, 256), (1, 1), (1, 1), (0, 0), (1, 1))], 1024, (14, 14), True, None, 2, None),
     ("lite_dil", [((2, 17, 17, 64), (5, 5), (1, 1), (4, 4), (2, 2))], 192, (17, 17), False, "relu", 2, None),
+    # two sources on the 4-wave tile (expand + strided projection shortcut), M tail, N tail
+    ("lite_dual", [((2, 14, 14, 128), (1, 1), (1, 1), (0, 0), (1, 1)),
+                   ((2, 28, 28, 256), (1, 1), (2, 2), (0, 0), (1, 1))], 512, (14, 14), False, "relu", 2, None),
+    ("lite_dual_s1", [((3, 7, 7, 64), (1, 1), (1, 1), (0, 0), (1, 1)),
+                      ((3, 7, 7, 128), (1, 1), (1, 1), (0, 0), (1, 1))], 200, (7, 7), False, None, 2, None),
     # the same tile with a 32-deep K-tile (32 KiB of LDS)
     ("lite32_3x3", [((4, 28, 28, 128), (3, 3), (1, 1), (1, 1), (1, 1))], 128, (28, 28), False, "relu", 3, None),
     ("lite32_3x3s2", [((3, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 3, None),
