@@ -927,10 +927,12 @@ class CompiledFunction(TransformerLowering):
         if (self.device.type == "cuda" and _cfg().conv_impl == "lite" and not use_pw and K1 % 64 == 0
                 and C2 % 64 == 0 and (xin.phys_c or K1) == K1 and (x2.phys_c or C2) == C2
                 and act in (K.ACT_NONE, K.ACT_RELU) and out.dtype == torch.bfloat16 and out.qscale is None
-                and _coff(out) % 8 == 0 and len(xin.shape) == 4):
+                and _coff(out) % 8 == 0 and len(xin.shape) == 4 and N * Ho * Wo <= 65536):
             # expand + projection shortcut as one 4-wave LDS-DMA implicit GEMM over two
             # sources (kernels/conv_pp.hip conv_lite, DUAL); planned for x2 as it is and, when
-            # _decimate_tails later stores x2 decimated, for the compact stride-1 layout
+            # _decimate_tails later stores x2 decimated, for the compact stride-1 layout.
+            # Stages 3/4 only (ResNet-50 B=256: 111 / 100 µs vs 114 / 111 on the dual igemm);
+            # stage 2's 200k-row GEMM stays on the igemm (141 vs 158 µs, profiles/r03_operating_points)
             xs0 = (tuple(xin.shape), (1, 1), (1, 1), (0, 0), (1, 1))
             lite = {s2: K.ConvPP([xs0, (tuple(x2.shape), (1, 1), (s2, s2), (0, 0), (1, 1))], Cout, (Ho, Wo),
                                  self.device, tile=2)}
