@@ -653,6 +653,8 @@ class CompiledFunction(TransformerLowering):
         return cur, scale, bias, residual, act, absorbed
 
     def _lower_conv(self, node: Node):
+        if self.precision == "fp8" and self._lower_sibling_group(node):
+            return
         x = self._in(node, 0)
         wv = self._in(node, 1)
         if not wv.is_const:
@@ -1412,6 +1414,8 @@ class CompiledFunction(TransformerLowering):
         Ho = (H + pt + pb - kh) // sh + 1
         Wo = (W + pl + pr - kw) // sw + 1
         mode = "max" if node.op == "MaxPool" else "avg"
+        if mode == "avg" and self.precision == "fp8" and self._lower_sibling_group(node):
+            return
         if mode == "avg" and (sh, sw) == (1, 1) and self._commute_avgpool(node, x, (kh, kw), (pt, pb, pl, pr)):
             return
         if x.qscale is not None and C % 16 == 0:
@@ -1436,6 +1440,131 @@ class CompiledFunction(TransformerLowering):
 
         self._emit(node.name, "pool", run, [xin], [out])
         self.vals[(node.name, 0)] = out
+
+    # ---- horizontal fusion of sibling pointwise convs (Inception module heads)
+    def _pw_member(self, c: Node, x: Val, src, max_cout: int | None = None):
+        """``c`` as a member of a sibling group: a 1x1 / stride-1 Conv2D of ``src`` with a
+        constant filter and a chain without residual ending in ReLU or nothing."""
+        if c.op != "Conv2D" or c.name in self._fused or c.inputs[0] != src or c.attr("data_format", "NHWC") != "NHWC":
+            return None
+        if list(c.attr("strides") or [1, 1, 1, 1]) != [1, 1, 1, 1] or list(c.attr("dilations") or [1, 1, 1, 1]) != [1, 1, 1, 1]:
+            return None
+        wv = self._get(c.inputs[1])
+        if wv is None or not wv.is_const or tuple(wv.const.shape[:3]) != (1, 1, x.shape[-1]):
+            return None
+        Cout = int(wv.const.shape[3])
+        if Cout % 16 or (max_cout is not None and Cout > max_cout):
+            return None
+        last, scale, bias, residual, act, absorbed = self._conv_chain(c)
+        if residual is not None or act not in (K.ACT_NONE, K.ACT_RELU):
+            return None
+        w = wv.const.float()
+        if scale is not None:
+            w = w * scale
+        return {"conv": c, "w": w.reshape(-1, Cout).t().contiguous(), "bias": bias, "act": act, "last": last,
+                "absorbed": absorbed, "Cout": Cout}
+
+    def _lower_sibling_group(self, entry: Node) -> bool:
+        """The 1x1 convs that read one fp8 value — an Inception module's branch heads, and
+        its AvgPool(3x3/1) -> 1x1 branch commuted to 1x1 -> pool — run as ONE implicit GEMM
+        over their concatenated filters (``conv2d_nhwc_fp8_multi``): the input is read once
+        instead of 3-4 times, and the combined channel count tiles better than 32-64-channel
+        GEMMs.  Its epilogue sends each branch's channels to that branch's destination (a
+        concat slot, an fp8 buffer with its own scale, or the bf16 pre-pool value)."""
+        src = entry.inputs[0] if entry.inputs else None
+        x = self.vals.get(src) if src is not None else None
+        if x is None or x.qscale is None or x.phys_c or x.rows is not None or len(x.shape) != 4 or x.shape[-1] % 16:
+            return False
+        N, H, W, C = x.shape
+        members = []
+        for cname in dict.fromkeys(self.cons.get(src[0], [])):
+            c = self.graph[cname]
+            if c.name in self._fused or not c.inputs or c.inputs[0] != src or any(i == src for i in c.inputs[1:]):
+                continue
+            if c.op == "Conv2D":
+                m = self._pw_member(c, x, src)
+                if m is not None:
+                    m["kind"], m["entry"] = "conv", c.name
+                    members.append(m)
+            elif c.op == "AvgPool" and c.attr("data_format", "NHWC") == "NHWC" and list(c.attr("ksize")) == [1, 3, 3, 1] \
+                    and list(c.attr("strides")) == [1, 1, 1, 1]:
+                pc = self._single_consumer(c.name)
+                if pc is None:
+                    continue
+                m = self._pw_member(pc, x, (c.name, 0), max_cout=C // 2)
+                if m is None:
+                    continue
+                if c.attr("padding", "VALID") == "SAME":
+                    pads = (*same_pads(H, 3, 1), *same_pads(W, 3, 1))
+                else:
+                    continue  # a VALID 3x3/1 pool changes the spatial size: not a sibling of the 1x1s
+                m["kind"], m["entry"], m["pool"], m["pads"] = "pool", c.name, c, pads
+                members.append(m)
+        if len(members) < 2 or entry.name not in {m["entry"] for m in members} or len(members) > 6:
+            return False
+        xs = x.qscale
+        ws_rows, bias_parts, lo_parts, segs, pool_steps = [], [], [], [], []
+        c0 = 0
+        for m in members:
+            Cout = m["Cout"]
+            ws_rows.append(m["w"])
+            if m["kind"] == "conv":
+                last = m["last"]
+                o_scale = self._qscale(last.name) if self._fp8_consumers_ok(last.name) else None
+                out = self._new((N, H, W, Cout), torch.uint8 if o_scale is not None else torch.bfloat16)
+                out.qscale = o_scale
+                bias_parts.append(m["bias"] if m["bias"] is not None else torch.zeros(Cout))
+                lo_parts.append(torch.full((Cout,), 0.0 if m["act"] == K.ACT_RELU else float("-inf")))
+                m["out"] = out
+                segs.append((out, c0, c0 + Cout))
+            else:
+                y = self._new((N, H, W, Cout))  # pre-bias conv output, pooled next
+                bias_parts.append(torch.zeros(Cout))
+                lo_parts.append(torch.full((Cout,), float("-inf")))
+                last = m["last"]
+                o_scale = self._qscale(last.name) if self._fp8_consumers_ok(last.name) else None
+                out = self._new((N, H, W, Cout), torch.uint8 if o_scale is not None else torch.bfloat16)
+                out.qscale = o_scale
+                m["y"], m["out"] = y, out
+                segs.append((y, c0, c0 + Cout))
+            c0 += Cout
+        wq, wsc = F8.quantize_weight(torch.cat(ws_rows, 0))
+        wq_dev, ws_dev = self._dev(wq), self._dev(wsc)
+        cs_dev = self._dev(wsc * xs, torch.float32)
+        b_dev = self._dev(torch.cat(bias_parts), torch.float32)
+        lo_dev = self._dev(torch.cat(lo_parts), torch.float32)
+        self.params += [wq_dev, cs_dev, b_dev, lo_dev]
+        self.fp8_layers += len(members)
+
+        def run(x=x, segs=segs, wq=wq_dev, ws=ws_dev, cs=cs_dev, b=b_dev, lo=lo_dev, xs=xs):
+            F8.conv2d_nhwc_fp8_multi(_view(x), xs, wq, (1, 1), ws, b, lo,
+                                     [(_target(v), a, e, _coff(v), _eff_scale(v) if v.qscale is not None else None)
+                                      for v, a, e in segs], chan_scale=cs)
+
+        self._emit("+".join(m["conv"].name for m in members), "conv_fp8", run, [x], [v for v, _, _ in segs],
+                   {"impl": "conv_lite_fp8_multi", "multi_out": True})
+        for m in members:
+            self._fused.add(m["conv"].name)
+            for a in m["absorbed"]:
+                self._fused.add(a.name)
+            if m["kind"] == "pool":
+                self._fused.add(m["pool"].name)
+                y, out, act = m["y"], m["out"], m["act"]
+                bp = self._dev(m["bias"] if m["bias"] is not None else torch.zeros(m["Cout"]), torch.float32)
+                self.params.append(bp)
+
+                def run_pool(y=y, out=out, b=bp, act=act, pads=m["pads"]):
+                    F8.avgpool_bias_act(y.buf, (3, 3), (1, 1), pads, b, act,
+                                        out_scale=_eff_scale(out) if out.qscale is not None else None,
+                                        out=_target(out), out_channel_offset=_coff(out))
+
+                self._emit(m["pool"].name, "pool_fp8" if out.qscale is not None else "pool", run_pool, [y], [out],
+                           {"impl": "avgpool_bias_act"})
+                self.commuted_pools = getattr(self, "commuted_pools", 0) + 1
+            self.vals[(m["last"].name, 0)] = m["out"]
+            self._alias_fused_outputs(m["absorbed"], m["out"])
+        self.sibling_groups = getattr(self, "sibling_groups", 0) + 1
+        return True
 
     def _commute_avgpool(self, node: Node, x: Val, ksize, pads) -> bool:
         """AvgPool(stride 1) -> 1x1 Conv2D (+ BN/bias, ReLU) lowered as 1x1 conv (no bias or
@@ -1618,7 +1747,7 @@ class CompiledFunction(TransformerLowering):
         # consumed by nothing but this concat, and not fetched
         prods = [s for s in self.steps if any(o is v for o in s.outputs)]
         if len(prods) != 1 or prods[0].kind not in ("conv", "pool", "conv_fp8", "pool_fp8") or v.concat_slot is not None \
-                or len(prods[0].outputs) != 1:
+                or (len(prods[0].outputs) != 1 and not prods[0].meta.get("multi_out")):
             return False
         if v.alias_of is not None or v.phys_c:
             return False
@@ -1928,6 +2057,7 @@ class CompiledFunction(TransformerLowering):
                 "conv_pp": getattr(self, "conv_pp_layers", 0), "pw_res": getattr(self, "pw_res_layers", 0),
                 "conv_lite": getattr(self, "conv_lite_layers", 0),
                 "commuted_pools": getattr(self, "commuted_pools", 0),
+                "sibling_groups": getattr(self, "sibling_groups", 0),
                 "activation_bytes": self.activation_bytes,
                 "param_bytes": self.param_bytes(),
                 **({"token_capacity": self.token_cap, "first_token_only_nodes": len(self._cls_nodes)}

@@ -79,6 +79,20 @@ struct Fp8Params {
   int prio;  // s_setprio(1) around each K-tile's MFMA cluster (fp8_prio)
 };
 
+// Multi-output epilogue of conv_lite_fp8 (horizontally fused sibling 1x1 convs of one
+// input): output channels [c0[s], c0[s+1]) go to destination s — its own buffer, pixel
+// stride, channel offset and e4m3 scale (or bf16) — and each channel has its own lower
+// clamp (0 = ReLU, -inf = none).  Passed by value (a captured launch keeps it).
+constexpr int MAX_SEGS = 6;
+struct Fp8Segs {
+  uint8_t* y[MAX_SEGS];
+  int c0[MAX_SEGS + 1];
+  int ld[MAX_SEGS], off[MAX_SEGS], bf16[MAX_SEGS];
+  float q[MAX_SEGS];
+  const float* lo;  // per output channel lower clamp
+  int n;
+};
+
 FTM_DEVICE int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 4); }
 
 // No wave-priority raise around the MFMA phase (igemm_bf16 has one): here it measured SLOWER
@@ -345,14 +359,14 @@ void launch_tile(const Fp8Params& p, int act, int cfg, hipStream_t s) {
 // 80, 160, 288 on 96; 320, 448, <= 64 on 64); NSTG = 1 (a single LDS stage) when the whole K fits one
 // K-tile (K <= 128: no prefetch to overlap, and half the LDS lets more workgroups hide the
 // load latency of these streaming layers).
-template <bool OUT_FP8, int ACT, int BN_ = 128, int NSTG = 2>
-__global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p) {
+template <bool OUT_FP8, int ACT, int BN_ = 128, int NSTG = 2, bool MULTI = false>
+__global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8Segs sg) {
   static_assert(BN_ == 128 || BN_ == 96 || BN_ == 64, "channel tile 128, 96 or 64");
   constexpr int BM = 128, BN = BN_;
   constexpr int NI = BN / 32;  // weight fragments per wave (a wave covers BN / 2 channels)
   constexpr int WQ = BN / 32;  // weight DMA rows-of-8 per wave
   constexpr int XB = BM * BK, WB = BN * BK, STG = XB + WB;
-  constexpr int OB = OUT_FP8 ? 1 : 2;
+  constexpr int OB = (OUT_FP8 && !MULTI) ? 1 : 2;  // MULTI stages bf16, quantises per segment at the store
   constexpr int OLD = BN * OB + 16;
   constexpr int LDS = NSTG * STG > BM * OLD ? NSTG * STG : BM * OLD;
   __shared__ __attribute__((aligned(1024))) uint8_t smem[LDS];
@@ -479,18 +493,22 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p) {
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int cl = wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
-    f32x4 sv = {0.f, 0.f, 0.f, 0.f}, bv = {0.f, 0.f, 0.f, 0.f};
+    f32x4 sv = {0.f, 0.f, 0.f, 0.f}, bv = {0.f, 0.f, 0.f, 0.f}, lv = {0.f, 0.f, 0.f, 0.f};
     if (n0 + cl < p.Cout) {
       sv = *reinterpret_cast<const f32x4*>(p.scale + n0 + cl);
       bv = *reinterpret_cast<const f32x4*>(p.bias + n0 + cl);
+      if constexpr (MULTI) lv = *reinterpret_cast<const f32x4*>(sg.lo + n0 + cl);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int pl = wm * 64 + j * 16 + frow;
       float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = apply_act<ACT>(acc[i][j][r] * sv[r] + bv[r]);
-      if constexpr (OUT_FP8) {
+      for (int r = 0; r < 4; ++r) {
+        if constexpr (MULTI) v[r] = fmaxf(acc[i][j][r] * sv[r] + bv[r], lv[r]);
+        else v[r] = apply_act<ACT>(acc[i][j][r] * sv[r] + bv[r]);
+      }
+      if constexpr (OUT_FP8 && !MULTI) {
         *reinterpret_cast<uint32_t*>(Os + pl * OLD + cl) =
             pack4(v[0] * p.out_q, v[1] * p.out_q, v[2] * p.out_q, v[3] * p.out_q);
       } else {
@@ -501,6 +519,32 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p) {
     }
   }
   __syncthreads();
+  if constexpr (MULTI) {
+    constexpr int CPR16 = BN / 16;  // 16-channel chunks (32 B of the bf16 tile) per row
+#pragma unroll 2
+    for (int q = threadIdx.x; q < BM * CPR16; q += 256) {
+      const int pl = q / CPR16;
+      const int cc = q % CPR16;
+      const int m = m0 + pl;
+      const int c = n0 + cc * 16;
+      if (m >= p.M || c >= p.Cout) continue;
+      int sgi = 0;
+#pragma unroll
+      for (int t = 1; t < MAX_SEGS; ++t) sgi += (t < sg.n && c >= sg.c0[t]) ? 1 : 0;
+      const int cl = c - sg.c0[sgi];
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(Os + pl * OLD + cc * 32);
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(Os + pl * OLD + cc * 32 + 16);
+      const size_t e = (size_t)m * sg.ld[sgi] + sg.off[sgi] + cl;  // elements of that destination
+      if (sg.bf16[sgi]) {
+        u32x4* dst = reinterpret_cast<u32x4*>(sg.y[sgi] + e * 2);
+        dst[0] = lo;
+        dst[1] = hi;
+      } else {
+        *reinterpret_cast<u32x4*>(sg.y[sgi] + e) = quant16(lo, hi, sg.q[sgi]);
+      }
+    }
+    return;
+  }
   constexpr int EPC = 16 / OB;
   constexpr int CPR = BN / EPC;
 #pragma unroll 4
@@ -515,14 +559,18 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p) {
   }
 }
 
-template <bool OUT_FP8, int BN_, int NSTG>
-void launch_lite_fp8_t(Fp8Params p, int act, hipStream_t s) {
+template <bool OUT_FP8, int BN_, int NSTG, bool MULTI = false>
+void launch_lite_fp8_t(Fp8Params p, int act, hipStream_t s, const Fp8Segs& sg) {
   p.tiles_m = (p.M + 127) / 128;
   p.tiles_n = (p.Cout + BN_ - 1) / BN_;
   dim3 grid(p.tiles_m * p.tiles_n), block(256);
+  if constexpr (MULTI) {  // the per-channel clamp replaces the activation
+    hipLaunchKernelGGL((conv_lite_fp8_kernel<false, ACT_NONE, BN_, NSTG, true>), grid, block, 0, s, p, sg);
+    return;
+  }
   switch (act) {
-    case ACT_NONE: hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_NONE, BN_, NSTG>), grid, block, 0, s, p); break;
-    case ACT_RELU: hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_RELU, BN_, NSTG>), grid, block, 0, s, p); break;
+    case ACT_NONE: hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_NONE, BN_, NSTG>), grid, block, 0, s, p, sg); break;
+    case ACT_RELU: hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_RELU, BN_, NSTG>), grid, block, 0, s, p, sg); break;
     default: throw std::invalid_argument("fp8 conv_lite: activation must be none/relu");
   }
 }
@@ -538,14 +586,14 @@ int lite_fp8_bn(int Cout) {
   return best;
 }
 
-template <bool OUT_FP8>
-void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, int bn = 0) {
+template <bool OUT_FP8, bool MULTI = false>
+void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, const Fp8Segs& sg = Fp8Segs{}, int bn = 0) {
   const int b = bn ? bn : lite_fp8_bn(p.Cout);
   const bool one = p.K <= BK;
 #define FTM_LITE(BN_)                                                     \
   do {                                                                    \
-    if (one) launch_lite_fp8_t<OUT_FP8, BN_, 1>(p, act, s);               \
-    else launch_lite_fp8_t<OUT_FP8, BN_, 2>(p, act, s);                   \
+    if (one) launch_lite_fp8_t<OUT_FP8, BN_, 1, MULTI>(p, act, s, sg);    \
+    else launch_lite_fp8_t<OUT_FP8, BN_, 2, MULTI>(p, act, s, sg);        \
   } while (0)
   if (b == 64) FTM_LITE(64);
   else if (b == 96) FTM_LITE(96);
@@ -854,6 +902,64 @@ void conv2d_nhwc_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, 
   else launch_io<true>(p, in_bf16, out_fp8, act, cfg, s);
 }
 
+// Horizontally fused sibling convs on the conv_lite_fp8 tile: one implicit GEMM over the
+// concatenated filters [Cout_total][K], whose output channel ranges go to different
+// destinations.  segs: [(y, c0, c1, ldy, y_coff, is_bf16, out_q)] covering [0, Cout) in
+// order, every bound a multiple of 16; lo: fp32 [Cout] lower clamp (0 ReLU / -inf none).
+void conv2d_nhwc_fp8_multi(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t lo, int N, int H,
+                           int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw,
+                           int Ho, int Wo, pybind11::list segs, uintptr_t stream) {
+  const int ns = (int)pybind11::len(segs);
+  if (ns < 1 || ns > MAX_SEGS) throw std::invalid_argument("conv2d_nhwc_fp8_multi: 1.." + std::to_string(MAX_SEGS) + " segments");
+  if (Cin % 16 || Cout % 16) throw std::invalid_argument("conv2d_nhwc_fp8_multi: Cin / Cout % 16 != 0");
+  if (N <= 0 || Ho <= 0 || Wo <= 0) throw std::invalid_argument("conv2d_nhwc_fp8_multi: empty problem");
+  if ((long)N * H * W * Cin >= (1L << 31) || (long)N * Ho * Wo >= (1L << 31))
+    throw std::invalid_argument("conv2d_nhwc_fp8_multi: tensor too large for 32-bit indexing");
+  if (ph >= 1024 || pw >= 1024 || H >= 16384 || W >= 16384) throw std::invalid_argument("conv2d_nhwc_fp8_multi: geometry");
+  if (!scale || !bias || !lo) throw std::invalid_argument("conv2d_nhwc_fp8_multi: scale, bias and clamp pointers required");
+  check_align(x, 16, "x");
+  check_align(w, 16, "w");
+  check_align(scale, 16, "scale");
+  check_align(bias, 16, "bias");
+  check_align(lo, 16, "lo");
+  Fp8Segs sg{};
+  sg.n = ns;
+  sg.lo = reinterpret_cast<const float*>(lo);
+  int expect = 0;
+  for (int i = 0; i < ns; ++i) {
+    pybind11::tuple t = segs[i].cast<pybind11::tuple>();
+    if (t.size() != 7) throw std::invalid_argument("segment tuple (y, c0, c1, ldy, y_coff, is_bf16, out_q)");
+    const uintptr_t y = t[0].cast<uintptr_t>();
+    const int c0 = t[1].cast<int>(), c1 = t[2].cast<int>(), ld = t[3].cast<int>(), off = t[4].cast<int>();
+    const int isb = t[5].cast<int>();
+    if (c0 != expect || c1 <= c0 || c0 % 16 || c1 % 16) throw std::invalid_argument("conv2d_nhwc_fp8_multi: segments must tile [0, Cout) in 16s");
+    if (ld % 16 || off % 16 || off + (c1 - c0) > ld) throw std::invalid_argument("conv2d_nhwc_fp8_multi: segment pitch / offset");
+    check_align(y, 16, "segment y");
+    sg.y[i] = reinterpret_cast<uint8_t*>(y);
+    sg.c0[i] = c0;
+    sg.ld[i] = ld;
+    sg.off[i] = off;
+    sg.bf16[i] = isb;
+    sg.q[i] = t[6].cast<float>();
+    expect = c1;
+  }
+  if (expect != Cout) throw std::invalid_argument("conv2d_nhwc_fp8_multi: segments do not cover Cout");
+  sg.c0[ns] = Cout;
+  Fp8Params p{};
+  p.x = reinterpret_cast<const uint8_t*>(x);
+  p.w = reinterpret_cast<const uint8_t*>(w);
+  p.scale = reinterpret_cast<const float*>(scale);
+  p.bias = reinterpret_cast<const float*>(bias);
+  p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout;
+  p.KH = KH; p.KW = KW; p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
+  p.M = N * Ho * Wo;
+  p.K = KH * KW * Cin;
+  p.ldx = Cin;
+  if ((long)Cout * p.K >= (1L << 31)) throw std::invalid_argument("conv2d_nhwc_fp8_multi: weights larger than 2 GiB");
+  launch_lite_fp8<false, true>(p, ACT_NONE, reinterpret_cast<hipStream_t>(stream), sg);
+  FTM_CHECK_LAUNCH();
+}
+
 // Y[M, N] = act(Xq[M, K] . Wq[N, K]^T * scale + bias)
 void gemm_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t y, int M, int N, int K, int ldx,
               int ldy, int in_bf16, float in_q, int out_fp8, float out_q, int act, uintptr_t stream, int cfg) {
@@ -988,5 +1094,6 @@ void register_fp8(pybind11::module_& m) {
   m.def("pool2d_nhwc_fp8", &pool2d_nhwc_fp8);
   m.def("global_avgpool_fp8", &global_avgpool_fp8);
   m.def("avgpool_bias_act", &avgpool_bias_act);
+  m.def("conv2d_nhwc_fp8_multi", &conv2d_nhwc_fp8_multi);
   m.attr("fp8_igemm_num_configs") = NCFG;
 }

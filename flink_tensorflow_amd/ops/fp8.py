@@ -142,6 +142,49 @@ def conv2d_nhwc_fp8(x: torch.Tensor, x_scale: float, wq: torch.Tensor, kshape, w
     return out
 
 
+def conv2d_nhwc_fp8_multi(x: torch.Tensor, x_scale: float, wq: torch.Tensor, kshape, w_scale: torch.Tensor,
+                          bias: torch.Tensor, lo: torch.Tensor, segs, stride=(1, 1), pad=(0, 0, 0, 0), dilation=(1, 1),
+                          chan_scale: torch.Tensor | None = None) -> None:
+    """Horizontally fused sibling convs (``kernels/fp8.hip`` conv_lite_fp8, multi-output
+    epilogue): one implicit GEMM over the concatenated filters ``wq`` [Cout_total, K]; output
+    channels are clamped below by ``lo`` (0 = ReLU, -inf = none) and split into ``segs``:
+    ``[(out, c0, c1, out_channel_offset, out_scale)]`` in channel order, ``out`` an NHWC
+    buffer (e4m3 bytes with ``out_scale``, or bf16 when ``out_scale`` is None).  The tile is
+    staged in bf16 and quantised per segment at the store."""
+    N, H, W, Cin = x.shape
+    Cout = wq.shape[0]
+    KH, KW = kshape
+    sh, sw = stride
+    pt, pb, pl, pr = pad
+    dh, dw = dilation
+    Ho, Wo = conv_out_hw(H, W, KH, KW, sh, sw, pt, pl, dh, dw, pb, pr)
+    for out, c0, c1, off, osc in segs:
+        if tuple(out.shape[:3]) != (N, Ho, Wo) or off + (c1 - c0) > out.shape[3]:
+            raise ValueError(f"conv2d_nhwc_fp8_multi: segment out {tuple(out.shape)} cannot hold [{c0}, {c1}) at {off}")
+        if out.dtype != (torch.uint8 if osc is not None else (torch.bfloat16 if x.is_cuda else out.dtype)):
+            raise ValueError("conv2d_nhwc_fp8_multi: segment dtype does not match its scale")
+    if x.is_cuda:
+        _check(x, "x", torch.uint8, x.device)
+        _check(wq, "wq", torch.uint8, x.device)
+        if wq.shape[1] != KH * KW * Cin:
+            raise ValueError(f"conv2d_nhwc_fp8_multi: weight K {wq.shape[1]} != {KH}*{KW}*{Cin}")
+        if chan_scale is None:
+            chan_scale = (w_scale.float() * x_scale).contiguous()
+        for t, nm in ((chan_scale, "chan_scale"), (bias, "bias"), (lo, "lo")):
+            _check(t, nm, torch.float32, x.device)
+        _hip().conv2d_nhwc_fp8_multi(
+            x.data_ptr(), wq.data_ptr(), chan_scale.data_ptr(), bias.data_ptr(), lo.data_ptr(), N, H, W, Cin, Cout, KH,
+            KW, sh, sw, pt, pl, dh, dw, Ho, Wo,
+            [(o.data_ptr(), c0, c1, o.shape[-1], off, int(osc is None), 1.0 / osc if osc is not None else 1.0)
+             for o, c0, c1, off, osc in segs], _stream())
+        return
+    y = conv2d_nhwc_fp8(x, x_scale, wq, kshape, w_scale, bias, stride, pad, dilation, None)  # fp32, no act
+    y = torch.maximum(y, lo.float()).to(torch.bfloat16).float()  # the kernel stages the tile in bf16
+    for out, c0, c1, off, osc in segs:
+        v = y[..., c0:c1]
+        out[..., off:off + c1 - c0] = to_fp8_bytes(v / osc) if osc is not None else v.to(out.dtype)
+
+
 def gemm_fp8(x: torch.Tensor, x_scale: float, wq: torch.Tensor, w_scale: torch.Tensor, bias=None, act=None,
              out_scale: float | None = None, out: torch.Tensor | None = None, cfg: int = -1,
              chan_scale: torch.Tensor | None = None) -> torch.Tensor:

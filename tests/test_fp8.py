@@ -52,6 +52,8 @@ def test_inception_v3_fp8_plan_host():
     assert s8["glue_ops"] == [] and s8["fp8_layers"] == 93
     # every AvgPool(3x3/1) -> 1x1 conv branch runs as 1x1 conv -> pool (+ bias/ReLU/quantise)
     assert s8["commuted_pools"] == 9 and p16.summary()["commuted_pools"] == 9
+    # each module's sibling 1x1 convs (and its commuted pool branch) run as one multi-output GEMM
+    assert s8["sibling_groups"] == 10 and p16.summary()["sibling_groups"] == 0
     assert "concat" not in s8["kinds"] and "dequant" not in s8["kinds"]  # stride-written fp8 concats
     img = torch.randint(0, 256, (2, 75, 75, 3), dtype=torch.uint8)
     l16, _ = p16({"images:0": img})
@@ -191,6 +193,47 @@ def test_avgpool_bias_act_gpu(out_fp8):
             assert ((gd - rd).abs() <= 0.13 * rd.abs() + 1e-3).all()
         else:
             torch.testing.assert_close(got[..., 32:].float(), ref.float(), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.gpu
+def test_conv_fp8_multi_output_gpu():
+    """Sibling 1x1 convs as one GEMM with a multi-destination epilogue: fp8 segments of
+    different scales (one at a concat offset), a bf16 segment, ReLU and no-act channels;
+    against the host reference of the same kernel."""
+    torch.manual_seed(6)
+    N, H, W, C = 2, 13, 11, 96
+    x = torch.randn(N, H, W, C).relu()
+    sx = Q.scale_for(x.abs().max())
+    xq = Q.quantize(x, sx)
+    couts = (64, 48, 32, 16)
+    w = torch.randn(sum(couts), C) / C ** 0.5
+    wq, ws = Q.quantize_weight(w)
+    b = torch.randn(sum(couts)) * 0.1
+    lo = torch.tensor([0.0] * (64 + 48) + [float("-inf")] * 48)
+
+    def outs(dev):
+        return [torch.zeros((N, H, W, 128), dtype=torch.uint8, device=dev),   # concat slot at 32
+                torch.zeros((N, H, W, 48), dtype=torch.uint8, device=dev),
+                torch.zeros((N, H, W, 32), dtype=torch.bfloat16 if dev != "cpu" else torch.float32, device=dev),
+                torch.zeros((N, H, W, 16), dtype=torch.uint8, device=dev)]
+
+    def segs(o):
+        return [(o[0], 0, 64, 32, 0.02), (o[1], 64, 112, 0, 0.05), (o[2], 112, 144, 0, None), (o[3], 144, 160, 0, 0.01)]
+
+    ref = outs("cpu")
+    Q.conv2d_nhwc_fp8_multi(xq, sx, wq, (1, 1), ws, b, lo, segs(ref))
+    got = outs(DEV)
+    Q.conv2d_nhwc_fp8_multi(xq.to(DEV), sx, wq.to(DEV), (1, 1), ws.to(DEV), b.to(DEV), lo.to(DEV), segs(got))
+    torch.cuda.synchronize()
+    for i, (r, g) in enumerate(zip(ref, got)):
+        g = g.cpu()
+        if r.dtype == torch.uint8:
+            rd, gd = Q.from_fp8_bytes(r), Q.from_fp8_bytes(g)
+            assert ((gd - rd).abs() <= 0.13 * rd.abs() + 1e-3).all(), i
+        else:
+            torch.testing.assert_close(g.float(), r.float(), rtol=2e-2, atol=2e-2)
+    assert (got[0][..., :32] == 0).all() and (got[0][..., 96:] == 0).all()
+    assert (Q.from_fp8_bytes(got[3].cpu()) < 0).any()  # the no-act channels keep their negatives
 
 
 @pytest.mark.gpu
