@@ -41,8 +41,7 @@ class EngineConfig:
     conv_impl: str = "lite"            # implicit-GEMM convs: lite (4-wave LDS-DMA conv_lite) | incumbent
     #                                    (register-staged igemm) | auto (probe conv_pp) | pp
     conv_lite_pointwise: bool = False  # deep-K 1x1 reduces (K >= 1024) on conv_lite instead of gemm_pp
-    conv_lite_max_m: int = 0           # conv_lite only for layers of at most this many output pixels (0: any)
-    conv_lite_bk: int = 64             # conv_lite K-tile depth: 64 (64 KiB LDS) or 32 (32 KiB, igemm footprint)
+    sibling_conv_fusion: bool = True   # fp8: an Inception module's sibling 1x1 convs as one multi-output GEMM
     fuse_block_tails: bool = True      # ResNet block boundary: expand + next reduce in one kernel
     fuse_wide_tails: bool = False      # ... also for stage 2 (weights streamed; measured no gain)
     decimate_tails: bool = True        # stage-1 tail output stored at the stride-2 reader's pixels

@@ -841,14 +841,13 @@ class CompiledFunction(TransformerLowering):
                 and not pointwise and act in (K.ACT_NONE, K.ACT_RELU)
                 and (res_val is None or (res_val.concat_slot is None and res_val.qscale is None
                                          and tuple(res_val.shape) == tuple(out.shape) and res_val.alias_of is None))
-                and max(pt, pb) < 1024 and max(pl, pr) < 1024
-                and (not _cfg().conv_lite_max_m or int(np.prod(out.shape[:3])) <= _cfg().conv_lite_max_m))
+                and max(pt, pb) < 1024 and max(pl, pr) < 1024)
         if lite:
             # KxK convs (stage 2-4 3x3): 4-wave 128x128 implicit GEMM on two LDS-DMA stages
             # (kernels/conv_pp.hip conv_lite): 6-24 % faster than the register-staged igemm
             # per layer and 64 KiB of LDS, so it shares a CU with the sibling lane
             cl = K.ConvPP([(tuple(xin.shape), (KHe, KWe), (sh, sw), (pt, pl), (dh, dw))], Cout, tuple(out.shape[1:3]),
-                          self.device, tile=3 if _cfg().conv_lite_bk == 32 else 2)
+                          self.device, tile=2)  # the 32-deep K-tile (tile 3) measured slower: profiles/r03_conv
 
             def run(xin=xin, out=out, res_val=res_val, cl=cl, w2=w_dev.reshape(Cout, -1), b_dev=b_dev):  # noqa: F811
                 cl([xin.buf], w2, b_dev, res_val.buf if res_val is not None else None, act, out=_target(out),
@@ -1471,6 +1470,8 @@ class CompiledFunction(TransformerLowering):
         instead of 3-4 times, and the combined channel count tiles better than 32-64-channel
         GEMMs.  Its epilogue sends each branch's channels to that branch's destination (a
         concat slot, an fp8 buffer with its own scale, or the bf16 pre-pool value)."""
+        if not _cfg().sibling_conv_fusion:
+            return False
         src = entry.inputs[0] if entry.inputs else None
         x = self.vals.get(src) if src is not None else None
         if x is None or x.qscale is None or x.phys_c or x.rows is not None or len(x.shape) != 4 or x.shape[-1] % 16:
