@@ -98,6 +98,8 @@ def main():
                     help="decoded source image size (resnet50: 256 resized to 224; inception_v3: 299)")
     ap.add_argument("--depth", type=int, default=3, help="pipeline slots")
     ap.add_argument("--gather-threads", type=int, default=8, help="native copy threads staging a micro-batch")
+    ap.add_argument("--stagger-lanes", action="store_true",
+                    help="start lane k >= 1 only when lane 0's first batch is done (lanes half a period apart)")
     ap.add_argument("--no-numa", action="store_true", help="do not pin this rank to its GPU's NUMA node")
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
     ap.add_argument("--pool", type=int, default=512, help="distinct synthetic records cycled by the source")
@@ -309,7 +311,8 @@ def main():
 
     records = [pool[i] for i in range(args.pool)]
     runner = PipelinedGpuRunner(lane_plans, feed, lambda p: p.output_tensors(), rec_shape, rec_dtype,
-                                depth=args.depth, device=dev, gather_threads=args.gather_threads)
+                                depth=args.depth, device=dev, gather_threads=args.gather_threads,
+                                stagger=args.stagger_lanes)
 
     if args.offered_rate:
         return run_offered(args, runner, records, B, rank, ws, dev, comm, MetricGroup, model_name, data, lanes,

@@ -78,7 +78,7 @@ class PipelinedGpuRunner:
 
     def __init__(self, plans, feed: str, fetch_bufs: Callable[[Any], Sequence[torch.Tensor]],
                  record_shape, record_dtype=torch.uint8, depth: int = 3, device=None, gather_threads: int = 8,
-                 stage_chunk: int = 64):
+                 stage_chunk: int = 64, stagger: bool = False):
         lanes = plans if isinstance(plans, (list, tuple)) else [plans]
         self.lanes = [dict(sorted(p.items())) for p in lanes]
         self.plans = self.lanes[0]
@@ -115,6 +115,13 @@ class PipelinedGpuRunner:
         # thread's time goes when the GPU is not saturated
         self.host_s = {"gather": 0.0, "select": 0.0, "launch": 0.0, "wait": 0.0}
         self.batches = 0
+        # stagger: when the pipeline starts from empty, lane k >= 1 starts its first batch
+        # only when lane 0's first batch is done, so the lanes run half a period apart (one
+        # lane's memory-bound layers against the other's compute-bound ones) instead of
+        # in step
+        self.stagger = stagger and len(self.lanes) > 1
+        self._stagger_evt = None
+        self._started: set[int] = set()
 
     def bucket_for(self, n: int) -> int:
         i = bisect.bisect_left(self.buckets, n)
@@ -166,6 +173,13 @@ class PipelinedGpuRunner:
             plan = select(slot.pinned_in, n)
         t3 = time.perf_counter()
         stream = self.compute_streams[lane]
+        if self.stagger:
+            if not self._inflight:  # the pipeline restarts from empty
+                self._started.clear()
+                self._stagger_evt = None
+            if lane not in self._started and lane != 0 and self._stagger_evt is not None:
+                stream.wait_event(self._stagger_evt)
+            self._started.add(lane)
         with torch.cuda.stream(self.copy_stream):
             slot.h2d.record(self.copy_stream)
         with torch.cuda.stream(stream):
@@ -186,6 +200,8 @@ class PipelinedGpuRunner:
                 for dst, src in zip(slot.pinned_out, self.fetch_bufs(plan)):
                     dst.copy_(src, non_blocking=True)
             slot.done.record(stream)
+        if self.stagger and lane == 0 and self._stagger_evt is None:
+            self._stagger_evt = slot.done
         slot.busy = True
         slot.n = n
         slot.ts = ingest_ts
