@@ -316,3 +316,37 @@ def test_remote_source_chain_checkpoint_restart(tmp_path):
     for k, t in sink.results():
         final[k] = max(final.get(k, 0), t)
     assert final == {k: sum(v for v in range(1, 301) if v % 3 == k) for k in range(3)}
+
+
+def test_tensor_slab_view_batch_releases_with_the_last_view():
+    """The worker maps a message's slab records as slices of one base array: contents and
+    dtypes round-trip, a surviving derived view of ANY record holds the whole span, and the
+    span is released (header advanced) once the last view is gone."""
+    import gc
+
+    import numpy as np
+
+    from flink_tensorflow_amd.runtime.remote import TensorSlab
+
+    tag = f"/ftm-vb-{os.getpid()}"
+    co = TensorSlab(tag, True, 1 << 22)
+    wk = TensorSlab(tag, False)
+    try:
+        rng = np.random.default_rng(3)
+        vals = [rng.integers(0, 256, (64, 96), dtype=np.uint8), rng.standard_normal((33, 65)).astype(np.float32),
+                rng.integers(-999, 999, (7, 301), dtype=np.int16)]
+        out = co.put_batch([(v, None, 0) for v in vals])
+        arrs = wk.view_batch([r for r, _, _ in out])
+        for a, v in zip(arrs, vals):
+            assert a.dtype == v.dtype and a.shape == v.shape and np.array_equal(a, v)
+        keep = arrs[2][3:, ::2]  # a view derived from the LAST record only
+        del a, arrs
+        gc.collect()
+        assert int(wk.hdr[0]) == 0  # still held by the derived view
+        del keep
+        gc.collect()
+        assert int(wk.hdr[0]) == out[-1][0][3]  # the whole span released
+    finally:
+        wk.close()
+        co.unlink()
+        co.close()
