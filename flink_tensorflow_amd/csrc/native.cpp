@@ -41,6 +41,7 @@
 #include <vector>
 
 #if defined(__SSE4_2__)
+#include <immintrin.h>
 #include <nmmintrin.h>
 #endif
 
@@ -940,6 +941,38 @@ class CopyPool {
   std::vector<Job*> jobs_;
 };
 
+// Streaming copy for staging destinations the CPU does not read back (the pinned H2D slots,
+// the worker slab): non-temporal 32-B stores skip the read-for-ownership of every
+// destination line that plain stores pay — a third of the memory traffic of the copy.
+__attribute__((target("avx2"))) void stream_copy_avx2(uint8_t* d, const uint8_t* s, size_t n) {
+  size_t head = (32 - (reinterpret_cast<uintptr_t>(d) & 31)) & 31;
+  if (head > n) head = n;
+  std::memcpy(d, s, head);
+  d += head;
+  s += head;
+  n -= head;
+  size_t i = 0;
+  for (; i + 128 <= n; i += 128) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 32));
+    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 64));
+    const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 96));
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i), a);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 32), b);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 64), c);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 96), e);
+  }
+  std::memcpy(d + i, s + i, n - i);
+}
+
+const bool kHasAvx2 = __builtin_cpu_supports("avx2");
+
+// one staging piece; callers fence (sfence) before they publish the destination
+inline void staging_copy(uint8_t* d, const uint8_t* s, size_t n) {
+  if (kHasAvx2 && n >= 4096) stream_copy_avx2(d, s, n);
+  else std::memcpy(d, s, n);
+}
+
 // Byte-balanced parallel copy of (dst, src, bytes) pieces: large records are split into
 // 256 KiB slices so a few big records still spread over every thread.
 void parallel_copy(const std::vector<std::tuple<uint8_t*, const uint8_t*, size_t>>& pieces, int nthreads) {
@@ -948,7 +981,8 @@ void parallel_copy(const std::vector<std::tuple<uint8_t*, const uint8_t*, size_t
   size_t total = 0;
   for (auto& p : pieces) total += std::get<2>(p);
   if (nthreads <= 1 || total < (1u << 20)) {
-    for (auto& p : pieces) std::memcpy(std::get<0>(p), std::get<1>(p), std::get<2>(p));
+    for (auto& p : pieces) staging_copy(std::get<0>(p), std::get<1>(p), std::get<2>(p));
+    _mm_sfence();
     return;
   }
   w.reserve(pieces.size() + total / kSlice + 1);
@@ -960,7 +994,8 @@ void parallel_copy(const std::vector<std::tuple<uint8_t*, const uint8_t*, size_t
   const size_t per = (w.size() + nt - 1) / nt;  // contiguous runs: each thread streams its own range
   CopyPool::get().run(nt, nt, [&](int t) {
     const size_t lo = t * per, hi = std::min(w.size(), lo + per);
-    for (size_t i = lo; i < hi; ++i) std::memcpy(std::get<0>(w[i]), std::get<1>(w[i]), std::get<2>(w[i]));
+    for (size_t i = lo; i < hi; ++i) staging_copy(std::get<0>(w[i]), std::get<1>(w[i]), std::get<2>(w[i]));
+    _mm_sfence();  // this thread's streaming stores are globally visible before the join
   });
 }
 
