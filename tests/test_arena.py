@@ -1,5 +1,6 @@
 """Tensor arena: native liveness offset planner, first-fit allocator, and compiled plans
 sharing one subtask arena (activation slab + interned weights)."""
+import numpy as np
 import pytest
 import torch
 from hypothesis import given, settings
@@ -130,3 +131,22 @@ def test_two_compute_lanes_keep_order_gpu(small_graph):
     for a, b in zip(one, two):
         torch.testing.assert_close(a.outputs[0], b.outputs[0])
         assert torch.equal(a.outputs[1], b.outputs[1])
+
+
+@pytest.mark.parametrize("stride,nbytes,threads", [(5003, 5003, 8), (196608, 196608, 8), (4099, 4000, 1),
+                                                   (300000, 262145, 4), (64, 48, 8)])
+def test_staging_gather_streaming_copy_exact(stride, nbytes, threads):
+    """The staging gather's streaming (non-temporal) copy: odd sizes, unaligned destination
+    rows, slices that cross the 256 KiB split, the single-thread and small-copy paths."""
+    from flink_tensorflow_amd import _ext
+
+    nat = _ext.native()
+    rng = np.random.default_rng(7)
+    recs = [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(37)]
+    dst = np.zeros(1 + stride * len(recs) + 64, np.uint8)
+    base = dst.ctypes.data + 1  # every row starts off 32-B alignment
+    nat.gather_into(base, stride * len(recs), recs, stride, threads)
+    for i, r in enumerate(recs):
+        np.testing.assert_array_equal(dst[1 + i * stride:1 + i * stride + nbytes], r)
+        assert not dst[1 + i * stride + nbytes:1 + (i + 1) * stride].any()  # nothing past the payload
+    assert dst[0] == 0 and not dst[1 + stride * len(recs):].any()
