@@ -99,7 +99,7 @@ class PipelinedGpuRunner:
         self.gather_threads = gather_threads
         self.stage_chunk = stage_chunk  # records per gather + H2D piece (0: whole batch at once)
         self._native = _ext.native()
-        depth = max(depth, len(self.lanes) + 2)  # every lane busy + one batch being staged
+        depth = max(depth, len(self.lanes) + 1)  # every lane busy + one batch being staged
         # batches in flight over ALL buckets (each bucket has its own ``depth`` slots): with
         # many buckets (dynamic batch sizes) the host could otherwise run dozens of batches
         # ahead of the GPU, adding queueing latency without adding throughput
