@@ -41,7 +41,6 @@ class EngineConfig:
     conv_impl: str = "lite"            # implicit-GEMM convs: lite (4-wave LDS-DMA conv_lite) | incumbent
     #                                    (register-staged igemm) | auto (probe conv_pp) | pp
     conv_lite_pointwise: bool = False  # deep-K 1x1 reduces (K >= 1024) on conv_lite instead of gemm_pp
-    conv_lite_wide: bool = False       # conv_lite's 8-wave 256x128 tile where the grid stays >= 2.5 waves
     sibling_conv_fusion: bool = True   # fp8: an Inception module's sibling 1x1 convs as one multi-output GEMM
     fuse_block_tails: bool = True      # ResNet block boundary: expand + next reduce in one kernel
     fuse_wide_tails: bool = False      # ... also for stage 2 (weights streamed; measured no gain)

@@ -846,12 +846,8 @@ class CompiledFunction(TransformerLowering):
             # KxK convs (stage 2-4 3x3): 4-wave 128x128 implicit GEMM on two LDS-DMA stages
             # (kernels/conv_pp.hip conv_lite): 6-24 % faster than the register-staged igemm
             # per layer and 64 KiB of LDS, so it shares a CU with the sibling lane
-            # the 8-wave 256x128 form (tile 4) where it still makes >= 2.5 waves of tiles
-            # (a quarter fewer LDS image bytes per MFMA; stage-2 3x3s at B = 256)
-            M = int(np.prod(out.shape[:3]))
-            wide = _cfg().conv_lite_wide and -(-M // 256) * -(-Cout // 128) >= 640
             cl = K.ConvPP([(tuple(xin.shape), (KHe, KWe), (sh, sw), (pt, pl), (dh, dw))], Cout, tuple(out.shape[1:3]),
-                          self.device, tile=4 if wide else 2)  # the 32-deep K-tile (tile 3) measured slower
+                          self.device, tile=2)  # the 32-deep K-tile (tile 3) measured slower: profiles/r03_conv
 
             def run(xin=xin, out=out, res_val=res_val, cl=cl, w2=w_dev.reshape(Cout, -1), b_dev=b_dev):  # noqa: F811
                 cl([xin.buf], w2, b_dev, res_val.buf if res_val is not None else None, act, out=_target(out),

@@ -399,26 +399,17 @@ FTM_DEVICE int lite_slot(int row, int chunk) {
 // DUAL: a second, pointwise and unpadded source (the strided projection input of a ResNet
 // block's first expand: y = x W_e + x2[::s] W_p in one K loop); its K-tiles follow source
 // 0's, the weight rows are [W_e | W_p].
-// BM = 256 (tile 4): eight waves as 4 (pixels) x 2 (channels) over a 256x128 tile on two
-// 48 KiB stages (96 KiB: one workgroup per CU, 64 KiB left for a sibling lane's conv_lite).
-// The LDS image bytes per MFMA drop by a quarter against 128x128 — the 4-wave tile moves
-// ~25 B/clk/CU from L2 into LDS at ~35 % MFMA busy, about what one CU's L2->LDS path
-// delivers (MI355X_MICROARCH.md, "gather into LDS": 66-73 GB/s per CU).
-template <int ACT, bool HAS_RES, int BK, bool DUAL = false, int BM = 128>
-__global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_lite_kernel(CPParams p) {
+template <int ACT, bool HAS_RES, int BK, bool DUAL = false>
+__global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
   // BK = 64: 128-B LDS rows, 2 x 32 KiB stages, 2 MFMA steps per K-tile.
   // BK = 32: 64-B rows, 2 x 16 KiB stages (the igemm's footprint: four workgroups per CU),
   //          1 MFMA step per K-tile; 16-B chunk slot = chunk ^ ((row >> 2) & 3) keeps the
   //          16-lane ds_read_b128 groups on distinct banks.
-  constexpr int BN = 128;
-  constexpr int NW = BM / 32;              // waves: 4 (128x128) or 8 (256x128)
-  constexpr int WM = BM / 64;              // wave rows over the pixels
-  static_assert((BM == 128 || BM == 256) && (BM == 128 || (BK == 64 && !DUAL)), "conv_lite tile");
+  constexpr int BM = 128, BN = 128;
   constexpr int ROWB = BK * 2;             // LDS row bytes
   constexpr int CPR = ROWB / 16;           // 16-B chunks per row
   constexpr int RPI = 1024 / ROWB;         // rows per DMA wave-instruction
-  constexpr int QX = BM / RPI / NW;        // DMA instructions per wave for the X image
-  constexpr int QW = BN / RPI / NW;        // ... for the W image
+  constexpr int QX = BM / RPI / 4;         // DMA instructions per wave per operand
   constexpr int XB = BM * ROWB, WB = BN * ROWB, STG = XB + WB;
   constexpr int OPITCH = BN * 2 + 16;
   constexpr int LDS = 2 * STG > BM * OPITCH ? 2 * STG : BM * OPITCH;
@@ -432,8 +423,8 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_lite_kernel(CP
   const int n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave % WM;  // pixel quarter / half of the tile
-  const int wn = wave / WM;  // channel half
+  const int wm = wave & 1;   // pixel half of the tile
+  const int wn = wave >> 1;  // channel half
 
   // DMA roles: wave w stages image rows RPI * (QX w + q) + lane / CPR of both the X (pixel)
   // and W (channel) images; the lane's 16-B chunk is pre-swizzled on the source
@@ -449,7 +440,6 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_lite_kernel(CP
   // drop the kernel by SFINAE (an undefined device stub at load time)
   int pb[4], hw[4], pb1[4];
   unsigned offw[4];
-  static_assert(QX <= 4 && QW <= 4, "per-lane DMA row arrays");
   const CSrc& S1 = p.s[1];
   __amdgpu_buffer_rsrc_t rx1 = rx;
   if constexpr (DUAL)
@@ -470,10 +460,7 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_lite_kernel(CP
     pb[q] = ((n * S.H + ih0) * S.W + iw0) * S.C * 2 + dchunk * 16;
     hw[q] = (ih0 << 16) | (iw0 & 0xFFFF);
     if constexpr (DUAL) pb1[q] = live ? ((n * S1.H + oh * S1.sh) * S1.W + ow * S1.sw) * S1.C * 2 + dchunk * 16 : -1;
-  }
-#pragma unroll
-  for (int q = 0; q < QW; ++q) {
-    const unsigned co = n0 + RPI * (QW * wave + q) + drow;
+    const unsigned co = n0 + r;
     offw[q] = co < (unsigned)p.N ? (co * p.ldw + dchunk * 8) * 2u : 0x80000000u;
   }
   // The K walk (channel chunk, filter column, filter row) advances incrementally in scalar
@@ -488,15 +475,14 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_lite_kernel(CP
         const int delta1 = (kt_dma - p.nk0) * BK * 2;
         ++kt_dma;
         uint8_t* bx = smem + stage * STG + QX * wave * RPI * ROWB;
-        uint8_t* bw = smem + stage * STG + XB + QW * wave * RPI * ROWB;
+        uint8_t* bw = bx + XB;
 #pragma unroll
-        for (int q = 0; q < QX; ++q)
+        for (int q = 0; q < QX; ++q) {
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rx1, (__attribute__((address_space(3))) void*)(bx + q * 1024), 16,
                                                    pb1[q] >= 0 ? (unsigned)(pb1[q] + delta1) : 0x80000000u, 0, 0, 0);
-#pragma unroll
-        for (int q = 0; q < QW; ++q)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 1024), 16,
                                                    offw[q], woff, 0, 0);
+        }
         return;
       }
     }
@@ -511,7 +497,7 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_lite_kernel(CP
       }
     }
     uint8_t* bx = smem + stage * STG + QX * wave * RPI * ROWB;
-    uint8_t* bw = smem + stage * STG + XB + QW * wave * RPI * ROWB;
+    uint8_t* bw = bx + XB;
 #pragma unroll
     for (int q = 0; q < QX; ++q) {
       const int ih = (hw[q] >> 16) + dih;
@@ -519,9 +505,8 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_lite_kernel(CP
       const bool ok = (unsigned)ih < (unsigned)S.H && (unsigned)iw < (unsigned)S.W;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(bx + q * 1024), 16,
                                                ok ? (unsigned)(pb[q] + delta) : 0x80000000u, 0, 0, 0);
-      if (q < QW)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 1024), 16,
-                                                 offw[q], woff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 1024), 16,
+                                               offw[q], woff, 0, 0);
     }
   };
 
@@ -582,7 +567,7 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_lite_kernel(CP
   bf16* y = reinterpret_cast<bf16*>(p.y);
   constexpr int SEGS = BN / 8;
 #pragma unroll 4
-  for (int q = threadIdx.x; q < BM * SEGS; q += NW * 64) {
+  for (int q = threadIdx.x; q < BM * SEGS; q += 256) {
     const int ml = q / SEGS;
     const int ccol = q - ml * SEGS;
     const int m = m0 + ml;
@@ -600,16 +585,11 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_lite_kernel(CP
   }
 }
 
-// lite_bk: 64 (tile 2) or 32 (tile 3); tile 4: the 256x128 eight-wave tile (K-tile 64)
+// lite_bk: 64 (tile 2) or 32 (tile 3)
 template <int ACT, int BK>
-void launch_lite(const CPParams& p, hipStream_t s, bool dual = false, bool wide = false) {
-  const dim3 grid(p.tiles_m * p.tiles_n), block(wide ? 512 : 256);
+void launch_lite(const CPParams& p, hipStream_t s, bool dual = false) {
+  const dim3 grid(p.tiles_m * p.tiles_n), block(256);
   if constexpr (BK == 64) {
-    if (wide) {
-      if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, BK, false, 256>), grid, block, 0, s, p);
-      else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, BK, false, 256>), grid, block, 0, s, p);
-      return;
-    }
     if (dual) {
       if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, BK, true>), grid, block, 0, s, p);
       else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, BK, true>), grid, block, 0, s, p);
@@ -751,12 +731,11 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   p.K = (int)K;
   p.OH = OH; p.OW = OW;
   p.ldw = (int)K; p.ldy = ldy; p.y_coff = y_coff; p.ldr = ldr;
-  need(tile >= 0 && tile <= 4,
-       "tile must be 0 (256x256), 1 (512x128), 2 / 3 (128x128, 4 waves, K-tile 64 / 32), 4 (256x128, 8 waves)");
+  need(tile >= 0 && tile <= 3, "tile must be 0 (256x256), 1 (512x128), 2 / 3 (128x128, 4 waves, K-tile 64 / 32)");
   const bool lite = tile >= 2;
-  need(!lite || ((ns == 1 || tile == 2) && splits <= 1), "the lite tiles take no split-K (two sources: tile 2)");
+  need(!lite || ((ns == 1 || tile == 2) && splits <= 1), "the 4-wave tile takes no split-K (two sources: tile 2)");
   need(tile != 3 || p.s[0].C % 32 == 0, "the 32-deep 4-wave tile needs Cin % 32 == 0");
-  const int BM = tile == 1 ? 512 : tile == 4 ? 256 : lite ? 128 : 256, BN = tile == 1 ? 128 : lite ? 128 : 256;
+  const int BM = tile == 1 ? 512 : lite ? 128 : 256, BN = tile == 1 ? 128 : lite ? 128 : 256;
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (Cout + BN - 1) / BN;
   const int nk = p.K / 64;
@@ -772,9 +751,9 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   float* wsp = reinterpret_cast<float*>(ws);
   if (lite) {
     switch (act * 2 + (tile == 3)) {
-      case ACT_NONE * 2: launch_lite<ACT_NONE, 64>(p, s, ns == 2, tile == 4); break;
+      case ACT_NONE * 2: launch_lite<ACT_NONE, 64>(p, s, ns == 2); break;
       case ACT_NONE * 2 + 1: launch_lite<ACT_NONE, 32>(p, s); break;
-      case ACT_RELU * 2: launch_lite<ACT_RELU, 64>(p, s, ns == 2, tile == 4); break;
+      case ACT_RELU * 2: launch_lite<ACT_RELU, 64>(p, s, ns == 2); break;
       case ACT_RELU * 2 + 1: launch_lite<ACT_RELU, 32>(p, s); break;
       default: throw std::invalid_argument("conv_pp: unsupported activation");
     }

@@ -58,12 +58,6 @@ CASES = [
     ("lite32_3x3s2", [((3, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 3, None),
     ("lite32_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (7, 7), True, "relu", 3, None),
     ("lite32_1x1", [((2, 14, 14, 256), (1, 1), (1, 1), (0, 0), (1, 1))], 1024, (14, 14), True, None, 3, None),
-    # the 8-wave 256x128 form of the tile (96 KiB): M tails, N tail, residual, stride, dilation
-    ("lite256_3x3", [((4, 28, 28, 128), (3, 3), (1, 1), (1, 1), (1, 1))], 128, (28, 28), False, "relu", 4, None),
-    ("lite256_3x3s2", [((3, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 4, None),
-    ("lite256_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (7, 7), True, "relu", 4, None),
-    ("lite256_1x1", [((2, 14, 14, 256), (1, 1), (1, 1), (0, 0), (1, 1))], 1024, (14, 14), True, None, 4, None),
-    ("lite256_dil", [((2, 17, 17, 64), (5, 5), (1, 1), (4, 4), (2, 2))], 192, (17, 17), False, "relu", 4, None),
 ]
 
 
