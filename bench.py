@@ -102,6 +102,8 @@ def main():
                     help="start lane k >= 1 only when lane 0's first batch is done (lanes half a period apart)")
     ap.add_argument("--no-numa", action="store_true", help="do not pin this rank to its GPU's NUMA node")
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
+    ap.add_argument("--no-gc-freeze", action="store_true",
+                    help="leave the setup objects to the cyclic GC (A/B of the runner's gc.freeze)")
     ap.add_argument("--pool", type=int, default=512, help="distinct synthetic records cycled by the source")
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert", "bert_graph", "widedeep",
                                                            "inception_v3"],
@@ -312,7 +314,7 @@ def main():
     records = [pool[i] for i in range(args.pool)]
     runner = PipelinedGpuRunner(lane_plans, feed, lambda p: p.output_tensors(), rec_shape, rec_dtype,
                                 depth=args.depth, device=dev, gather_threads=args.gather_threads,
-                                stagger=args.stagger_lanes)
+                                stagger=args.stagger_lanes, freeze_gc=not args.no_gc_freeze)
 
     if args.offered_rate:
         return run_offered(args, runner, records, B, rank, ws, dev, comm, MetricGroup, model_name, data, lanes,
@@ -513,6 +515,10 @@ def run_widedeep(args, dev, rank, ws):
                   file=sys.stderr)
             tr._graph = None
             torch.cuda.synchronize(dev)
+    from flink_tensorflow_amd.utils.gcfreeze import freeze_setup_objects
+
+    if not args.no_gc_freeze:
+        freeze_setup_objects()  # as the pipelined runner does after its plans compile
 
     for _ in range(args.warmup):
         step()

@@ -78,7 +78,7 @@ class PipelinedGpuRunner:
 
     def __init__(self, plans, feed: str, fetch_bufs: Callable[[Any], Sequence[torch.Tensor]],
                  record_shape, record_dtype=torch.uint8, depth: int = 3, device=None, gather_threads: int = 8,
-                 stage_chunk: int = 64, stagger: bool = False):
+                 stage_chunk: int = 64, stagger: bool = False, freeze_gc: bool = True):
         lanes = plans if isinstance(plans, (list, tuple)) else [plans]
         self.lanes = [dict(sorted(p.items())) for p in lanes]
         self.plans = self.lanes[0]
@@ -122,6 +122,10 @@ class PipelinedGpuRunner:
         self.stagger = stagger and len(self.lanes) > 1
         self._stagger_evt = None
         self._started: set[int] = set()
+        if freeze_gc:  # the plans are compiled: keep the GC's full passes off them
+            from ..utils.gcfreeze import freeze_setup_objects
+
+            freeze_setup_objects()
 
     def bucket_for(self, n: int) -> int:
         i = bisect.bisect_left(self.buckets, n)
