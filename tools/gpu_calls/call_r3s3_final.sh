@@ -1,4 +1,4 @@
-# round 3 (session 3) final: the committed tree — GPU suite, smoke, the driver's bench (x2),
+# round 3 (session 3) final (re-run after the gc.freeze change): the committed tree — GPU suite, smoke, the driver's bench (x2),
 # ResNet-50 kernel stats, Inception-v3 fp8 / BERT graph / W&D benches, ResNet stream job
 source tools/gpu_calls/gpu_steps.sh
 step pytest_gpu 900 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread
