@@ -7,7 +7,11 @@ runner that is a host stall long enough to let the compute lanes run dry (measur
 3-4 ms gap in the submit loop of a 20-batch window, `profiles/r03_s3_window`).  After setup
 ``freeze_setup_objects()`` collects once and moves every surviving object into the
 permanent generation (``gc.freeze``), so later collections scan only what the stream
-itself allocates."""
+itself allocates.
+
+Frozen objects are still freed by reference counting; only reference cycles among them
+are no longer reclaimed until ``gc.unfreeze()``.  A process that rebuilds its plans many
+times can call ``unfreeze_setup_objects()`` when it tears a runner down."""
 from __future__ import annotations
 
 import gc
@@ -24,3 +28,10 @@ def freeze_setup_objects(collect: bool = True) -> int:
             gc.collect()
         gc.freeze()
         return gc.get_freeze_count()
+
+
+def unfreeze_setup_objects() -> None:
+    """Returns the frozen objects to the oldest generation (their cycles become collectable
+    again)."""
+    with _lock:
+        gc.unfreeze()
