@@ -150,3 +150,16 @@ def test_staging_gather_streaming_copy_exact(stride, nbytes, threads):
         np.testing.assert_array_equal(dst[1 + i * stride:1 + i * stride + nbytes], r)
         assert not dst[1 + i * stride + nbytes:1 + (i + 1) * stride].any()  # nothing past the payload
     assert dst[0] == 0 and not dst[1 + stride * len(recs):].any()
+
+
+def test_gc_freeze_moves_setup_objects_out_of_collection():
+    import gc
+
+    from flink_tensorflow_amd.utils.gcfreeze import freeze_setup_objects, unfreeze_setup_objects
+
+    try:
+        n = freeze_setup_objects(collect=False)
+        assert n > 0 and gc.get_freeze_count() == n
+    finally:
+        unfreeze_setup_objects()
+    assert gc.get_freeze_count() == 0
