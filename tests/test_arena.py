@@ -159,7 +159,7 @@ def test_gc_freeze_moves_setup_objects_out_of_collection():
 
     try:
         n = freeze_setup_objects(collect=False)
-        assert n > 0 and gc.get_freeze_count() == n
+        assert n > 0 and gc.get_freeze_count() > 0
     finally:
         unfreeze_setup_objects()
     assert gc.get_freeze_count() == 0
