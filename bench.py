@@ -42,9 +42,9 @@ def self_launch(args) -> int | None:
 
     The reference's data parallelism is operator parallelism — every subtask opens its own
     model (``inception.scala:21-22``, ``DefaultSavedModelLoader.scala:40-56``); here a
-    subtask is a process bound to one GPU.  This parent never touches HIP (only
-    ``torch.cuda.device_count()``, which does not initialise the runtime on ROCm): it
-    checks that N GPUs are visible, runs ``torch.distributed.run`` as a CHILD process with
+    subtask is a process bound to one GPU.  This parent never touches HIP (it does not
+    even import torch: GPUs are counted from the KFD topology in sysfs,
+    ``utils/gpus.py``): it checks that N GPUs are visible, runs ``torch.distributed.run`` as a CHILD process with
     the same arguments (the ranks then see WORLD_SIZE and take the normal path, exactly as
     under the driver's own torchrun) and exits with the child's status; rank 0's JSON line
     reaches our stdout unchanged.  Returns None when no launch is needed."""
@@ -54,9 +54,9 @@ def self_launch(args) -> int | None:
     import subprocess
 
     if not args.rehearse_fake_comm:
-        import torch
+        from flink_tensorflow_amd.utils.gpus import sysfs_gpu_count
 
-        n = torch.cuda.device_count()
+        n = sysfs_gpu_count()
         if n < args.gpus:
             print(f"[bench] --gpus {args.gpus} but {n} GPU(s) visible: refusing (no silent fallback to fewer "
                   "ranks)", file=sys.stderr)

@@ -162,6 +162,71 @@ class GraphBuilder:
     def no_op(self, name, control=()) -> str:
         return self.op("NoOp", [], name=name, control=control)
 
+    # ------------------------------------------------------------------ TF1 control flow
+    def placeholder_with_default(self, default, name: str, shape=None) -> str:
+        return self.op("PlaceholderWithDefault", [default], name=name, dtype=self._dtype_of(default),
+                       shape=TensorShapeProto.of(shape) if shape is not None else TensorShapeProto(unknown_rank=True))
+
+    def _dtype_of(self, t: str) -> DataType:
+        nd = next(n for n in self.nodes if n.name == t.split(":")[0])
+        a = nd.attr.get("dtype") or nd.attr.get("T")
+        return DataType(a.type) if a is not None else DataType.FLOAT
+
+    def _guard_new_nodes(self, start: int, pivot: str):
+        """Input-less nodes made inside a branch / loop body get a control edge on the pivot
+        (as TF's CondContext / WhileContext add), so they live in its frame and die with it."""
+        p = "^" + pivot.split(":")[0]
+        for nd in self.nodes[start:]:
+            if not nd.input:
+                nd.input.append(p)
+
+    def cond(self, pred: str, true_fn, false_fn, inputs=(), name: str = "cond") -> str:
+        """``tf.cond`` as TF1 emits it: ``Switch`` every input on ``pred``, build each branch
+        on its Switch output, ``Merge`` the two results (output 0).  ``true_fn`` / ``false_fn``
+        take the switched inputs and return one tensor."""
+        with self.name_scope(name):
+            sw = self.op("Switch", [pred, pred], name="Switch")
+            swn = sw.split(":")[0]
+            pivot_t = self.op("Identity", [f"{swn}:1"], name="switch_t")
+            pivot_f = self.op("Identity", [f"{swn}:0"], name="switch_f")
+            xs = [self.op("Switch", [x, pred], name="Switch").split(":")[0] for x in inputs]
+            start = len(self.nodes)
+            t = true_fn(*[f"{x}:1" for x in xs])
+            self._guard_new_nodes(start, pivot_t)
+            start = len(self.nodes)
+            f = false_fn(*[f"{x}:0" for x in xs])
+            self._guard_new_nodes(start, pivot_f)
+            return self.op("Merge", [f, t], name="Merge", N=2)
+
+    def while_loop(self, cond_fn, body_fn, loop_vars, invariants=(), name: str = "while") -> list[str]:
+        """``tf.while_loop`` as TF1 emits it: ``Enter`` → ``Merge`` (with the back edge) →
+        ``LoopCond`` → ``Switch``; the true side runs the body into ``NextIteration``, the
+        false side leaves through ``Exit``.  ``invariants`` enter as loop constants.
+        ``cond_fn`` / ``body_fn`` take (*loop vars, *invariants); returns the Exit tensors."""
+        with self.name_scope(name):
+            frame = "/".join(self._scope)
+            enters = [self.op("Enter", [v], name="Enter", frame_name=frame, is_constant=False, parallel_iterations=10)
+                      for v in loop_vars]
+            invs = [self.op("Enter", [v], name="Enter", frame_name=frame, is_constant=True, parallel_iterations=10)
+                    for v in invariants]
+            merges = [self.op("Merge", [e, e], name="Merge", N=2) for e in enters]  # back edge patched below
+            start = len(self.nodes)
+            c = cond_fn(*merges, *invs)
+            self._guard_new_nodes(start, merges[0])
+            lc = self.op("LoopCond", [c], name="LoopCond")
+            sws = [self.op("Switch", [m, lc], name="Switch").split(":")[0] for m in merges]
+            exits = [self.op("Exit", [f"{sw}:0"], name="Exit") for sw in sws]
+            body_in = [self.op("Identity", [f"{sw}:1"], name="Identity") for sw in sws]
+            start = len(self.nodes)
+            outs = body_fn(*body_in, *invs)
+            outs = [outs] if isinstance(outs, str) else list(outs)
+            self._guard_new_nodes(start, body_in[0])
+            nexts = [self.op("NextIteration", [o], name="NextIteration") for o in outs]
+            for m, nx in zip(merges, nexts):
+                nd = next(n for n in self.nodes if n.name == m.split(":")[0])
+                nd.input[1] = nx.split(":")[0]
+            return exits
+
     # ------------------------------------------------------------------ output
     def build_graph_def(self) -> GraphDef:
         return GraphDef(node=list(self.nodes), versions=VersionDef(producer=26))

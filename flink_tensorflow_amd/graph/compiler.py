@@ -165,6 +165,11 @@ class CompiledFunction(TransformerLowering):
                  arena=None, token_capacity: int | None = None):
         if precision not in ("bf16", "fp8"):
             raise ValueError(f"precision must be bf16 or fp8, not {precision!r}")
+        from .control_flow import fold_static_control_flow
+
+        # TF1 conds on compile-time-constant predicates (an exported ``is_training`` switch
+        # left at its default) resolve before lowering: the plan is the cond-free one
+        graph = fold_static_control_flow(graph, list(feeds), list(fetches))
         self.graph = graph
         self.arena = arena  # subtask DeviceArena (shared slab + interned weights) or None
         # padding-free transformer plan: token rows packed into this capacity (graph/packed.py)

@@ -177,7 +177,10 @@ class Graph:
                 state[name] = 1
                 stack.append((name, True))
                 node = self.nodes[name]
+                merge = node.op in ("Merge", "RefMerge")
                 for dep in [s for s, _ in node.inputs] + node.control_inputs:
+                    if merge and self.nodes[dep].op in ("NextIteration", "RefNextIteration"):
+                        continue  # a loop's back edge: the Merge does not wait for it
                     if dep in needed and state.get(dep, 0) == 0:
                         stack.append((dep, False))
                     elif dep in needed and state.get(dep) == 1 and not _is_loop_edge(self, dep, name):

@@ -24,7 +24,7 @@ import torch
 from ..proto.messages import DeviceStepStats, NodeExecStats, RunMetadata, StepStats
 from ..types.names import TensorName
 from ..types.tensor import StringTensor, as_tensor
-from . import ops_core, ops_io, ops_nn  # noqa: F401  (register kernels)
+from . import control_flow, ops_core, ops_io, ops_nn  # noqa: F401  (register kernels)
 from .graph import Graph
 from .op_registry import REF_INPUT_OPS, OpContext, lookup
 
@@ -33,6 +33,8 @@ from .op_registry import REF_INPUT_OPS, OpContext, lookup
 class _Plan:
     order: list[str]
     fed_nodes: frozenset
+    control_flow: bool = False  # Switch/Merge/Enter/...: tagged-token dataflow (control_flow.py)
+    topology: Any = None
 
 
 class Run:
@@ -107,7 +109,7 @@ class Session:
                 stack.append(src)
             stack.extend(node.control_inputs)
         order = self.graph.topo_order(needed)
-        p = _Plan(order, fed_nodes)
+        p = _Plan(order, fed_nodes, control_flow.plan_has_control_flow(self.graph, order))
         self._plans[key] = p
         return p
 
@@ -131,7 +133,9 @@ class Session:
             values: dict[tuple[str, int], Any] = dict(feeds)
             ctx = OpContext(self, self.device)
             stats = [] if run_metadata else None
-            for name in plan.order:
+            if plan.control_flow:
+                values = control_flow.run_dataflow(self, plan, values, ctx, stats, lookup, ops_core.VarRef)
+            for name in ([] if plan.control_flow else plan.order):
                 if name in plan.fed_nodes:
                     continue
                 node = self.graph.nodes[name]
@@ -165,7 +169,11 @@ class Session:
                 try:
                     v = values[(f.name, f.index)]
                 except KeyError:
+                    if values.get((f.name, -1)) is control_flow.DEAD:
+                        raise RuntimeError(f"fetch {f} is dead: it lies in a branch the run did not take") from None
                     raise KeyError(f"fetch {f} was not produced (node has {self._num_outputs(f.name)} outputs)") from None
+                if v is control_flow.DEAD:
+                    raise RuntimeError(f"fetch {f} is dead: it lies in a branch the run did not take")
                 if isinstance(v, ops_core.VarRef):
                     v = v.read()
                 result.append(v)

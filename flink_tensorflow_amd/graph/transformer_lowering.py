@@ -376,8 +376,11 @@ class TransformerLowering:
         out.rows, out.lshape = "cls", v.lshape
         cls = pk["cls"]
 
+        from ..ops import kernels as K
+
         def run(v=v, out=out, cls=cls):
-            torch.index_select(_view(v), 0, cls.buf.long() if not cls.buf.is_cuda else cls.buf, out=out.buf)
+            src = _view(v)
+            K.gather_rows(src.reshape(-1, src.shape[-1]), cls.buf, out=out.buf)
 
         self._emit(f"first_token_gather/{len(self._cls_cache)}", "gather", run, [v, cls], [out])
         self._cls_cache[id(v)] = out

@@ -273,6 +273,11 @@ class BundleReader:
         if self._stager is None:
             self._stager = _PinnedStager()
         out = torch.empty(shape, dtype=dt.torch, device=device)
+        if e.size != out.numel() * out.element_size():
+            # the CRC covers only the stored bytes: a short entry would leave the tail of the
+            # device tensor uninitialised (the host path fails the same input in reshape)
+            raise DataLossError(f"tensor {name!r} in {self.prefix}: entry holds {e.size} bytes, "
+                                f"shape {list(shape)} of {dt.name} needs {out.numel() * out.element_size()}")
         if e.size == 0:
             return out
         dst = out.view(-1).view(torch.uint8) if out.numel() else out
@@ -367,7 +372,12 @@ def merge_bundles(src_prefixes: Iterable[str], dst_prefix: str, delete_old_dirs:
             if k in merged and not (e.slices and merged[k].slices):
                 raise ValueError(f"duplicate tensor {k!r} across shards")
             if k in merged:  # a partitioned variable saved by several shards: union of its slices
-                merged[k].slices.extend(e.slices)
+                m = merged[k]
+                if (m.dtype != e.dtype or list(m.shape.as_list() or []) != list(e.shape.as_list() or [])):
+                    # MergeV2Checkpoints rejects slices of one variable that disagree
+                    raise ValueError(f"partitioned tensor {k!r}: shards disagree on its full shape / dtype "
+                                     f"({m.shape.as_list()}/{m.dtype} vs {e.shape.as_list()}/{e.dtype})")
+                m.slices.extend(e.slices)
                 continue
             if not e.slices:
                 e.shard_id = base + e.shard_id

@@ -158,7 +158,33 @@ void lrn_bf16(uintptr_t x, uintptr_t y, long P, int C, int r, float bias, float 
   FTM_CHECK_LAUNCH();
 }
 
+// Row gather out[r] = x[idx[r]] (rows of `row_bytes`, a multiple of 16): the first-token
+// (CLS) rows of a token-packed encoder.  One thread per 16-byte chunk; an index outside
+// [0, n_src) writes zeros (a padded batch row has no token).
+namespace {
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint4* __restrict__ x, const int* __restrict__ idx,
+                                                          uint4* __restrict__ y, int n_out, int n_src, int chunks) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= (long)n_out * chunks) return;
+  const int r = (int)(i / chunks), c = (int)(i % chunks);
+  const int src = idx[r];
+  y[i] = (src >= 0 && src < n_src) ? x[(long)src * chunks + c] : make_uint4(0u, 0u, 0u, 0u);
+}
+}  // namespace
+
+void gather_rows(uintptr_t x, uintptr_t idx, uintptr_t y, int n_out, int n_src, long row_bytes, uintptr_t stream) {
+  if (row_bytes % 16 || row_bytes <= 0) throw std::invalid_argument("gather_rows: row bytes must be a positive multiple of 16");
+  if (x % 16 || y % 16 || idx % 4) throw std::invalid_argument("gather_rows: 16-byte aligned rows, 4-byte indices");
+  if (n_out <= 0) return;
+  const int chunks = (int)(row_bytes / 16);
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)(((long)n_out * chunks + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const uint4*>(x),
+                     reinterpret_cast<const int*>(idx), reinterpret_cast<uint4*>(y), n_out, n_src, chunks);
+  FTM_CHECK_LAUNCH();
+}
+
 void register_elementwise(pybind11::module_& m) {
+  m.def("gather_rows", &gather_rows);
   m.def("binary_bf16", &binary_bf16);
   m.def("lrn_bf16", &lrn_bf16);
 }

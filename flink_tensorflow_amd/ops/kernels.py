@@ -1186,6 +1186,25 @@ def binary(a: torch.Tensor, b, op: str, act=None, out: torch.Tensor | None = Non
     return out
 
 
+def gather_rows(x: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``out[r] = x[idx[r]]`` over the rows of a 2-D tensor (int32 indices; an index out of
+    range gives a zero row).  On the GPU one HIP kernel (16-byte chunks), no ATen gather."""
+    n = idx.numel()
+    if out is None:
+        out = torch.empty((n, x.shape[-1]), dtype=x.dtype, device=x.device)
+    if x.is_cuda:
+        _check(x, "x", x.dtype, x.device)
+        _check(out, "out", x.dtype, x.device)
+        _check(idx, "idx", torch.int32, x.device)
+        rb = x.shape[-1] * x.element_size()
+        _hip().gather_rows(x.data_ptr(), idx.data_ptr(), out.data_ptr(), n, x.shape[0], rb, _stream())
+        return out
+    ok = (idx >= 0) & (idx < x.shape[0])
+    out.zero_()
+    out[ok] = x[idx[ok].long()]
+    return out
+
+
 def lrn(x: torch.Tensor, depth_radius: int = 5, bias: float = 1.0, alpha: float = 1.0, beta: float = 0.5,
         out: torch.Tensor | None = None) -> torch.Tensor:
     """TF ``LRN`` on NHWC (normalisation across channels)."""

@@ -315,6 +315,7 @@ class _SourceTask(_Task):
             t.op.initialize(t.restore, self.job.restore_dir)
         for t in reversed(tasks):  # downstream first: ready before anything is emitted into it
             t.op.open()
+        self.job.wait_all_opened()
         if self.chain:
             self.head_emit = _chain_emit(self.chain[0])
         sctx = _SourceCtx(self)
@@ -366,6 +367,7 @@ class _RemoteSourceTask(_Task):
         proxy.setup(self.runtime_context(), Output(self.writer.emit, self.writer.emit_side))
         contexts = [self.runtime_context()] + [t.runtime_context() for t in self.chain]
         proxy.start_chain(contexts, [self.restore] + [t.restore for t in self.chain], self.job.restore_dir)
+        self.job.wait_all_opened()
         try:
             def poll():
                 while self.pending_trigger:
@@ -451,6 +453,7 @@ class _OpTask(_Task):
             t.op.initialize(t.restore, self.job.restore_dir)
         for t in reversed(tasks):  # downstream first: ready before anything is emitted into it
             t.op.open()
+        self.job.wait_all_opened()
         ops = [t.op for t in tasks]
         channels = set(self.channel_input)
         finished: set[int] = set()
@@ -571,6 +574,22 @@ class LocalExecutor:
         self.restore_dir: str | None = None
         self.rank, self.world_size = env.rank, env.world_size
         self._lock = threading.Lock()
+        self._opened: threading.Barrier | None = None
+
+    def wait_all_opened(self):
+        """Start barrier: a task thread emits or processes its first record only after
+        every task thread of the attempt has opened its operators.  GPU subtasks that share
+        this process compile and capture their hipGraphs in ``open()``; without the barrier
+        one subtask replays (and allocates, frees pinned blocks, runs the GC) on its streams
+        while a sibling is still inside a stream capture, which the HIP runtime does not
+        isolate per thread (``test_remote_batched_resnet_gpu``, round-3 driver abort)."""
+        b = self._opened
+        if b is None:
+            return
+        try:
+            b.wait()
+        except threading.BrokenBarrierError:
+            raise JobCancelled() from None
 
     # ---- device binding: one model subtask per GPU
     def device_for(self, node, subtask):
@@ -616,6 +635,8 @@ class LocalExecutor:
         if self.coordinator is not None:
             self.coordinator.abort_pending()  # no checkpoint of a failed attempt may complete
         self.cancel.set()
+        if self._opened is not None:
+            self._opened.abort()  # tasks still waiting for their siblings' open() give up
         for s in self.sources:
             try:
                 s.op.fn.cancel()
@@ -778,6 +799,7 @@ class LocalExecutor:
                 self.coordinator.start({(t.uid, t.subtask) for t in self.tasks})
             if self.env.fault_injector is not None:
                 self.env.fault_injector.arm(self)
+            self._opened = threading.Barrier(sum(1 for t in self.tasks if not isinstance(t, _ChainedTask)))
             for t in self.tasks:
                 t.start()
             stop_flush = threading.Event()

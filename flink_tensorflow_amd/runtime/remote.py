@@ -494,7 +494,9 @@ def _run_source_chain(msg, inp, out, emit, flush, parent_alive):
     _, factories, specs, restores, restore_dir = msg
     ops = [cloudpickle.loads(f)() for f in factories]
     metrics = []
-    device = _worker_device(specs[0]) if any(sp["gpu"] for sp in specs) else None
+    # the source node itself never uses the GPU: bind the device of the first GPU member
+    gpu_spec = next((sp for sp in specs if sp["gpu"]), None)
+    device = _worker_device(gpu_spec) if gpu_spec is not None else None
 
     def side(tag, v):
         flush()
@@ -568,15 +570,51 @@ def _run_source_chain(msg, inp, out, emit, flush, parent_alive):
             return lock
 
         def collect(self, value, timestamp=None):
-            poll()
-            head(Record(value, timestamp))
+            with lock:  # re-entrant: sources normally hold it already (chain timer excluded)
+                poll()
+                head(Record(value, timestamp))
             recs_out[0] += 1
 
         def emit_watermark(self, ts):
-            head(Watermark(ts))
+            with lock:
+                head(Watermark(ts))
 
+    stop = threading.Event()
+    timer_error: list = []
+
+    def chain_timer():
+        # the local chain's ``_chain_timer`` (executor.py): while the source blocks between
+        # records (slow generator, file-monitor sleep) the chained operators still get their
+        # deadlines (micro-batch max_delay, completed GPU batches) and checkpoint triggers
+        # still get their barrier; the collect path polls while records flow
+        try:
+            while True:
+                with lock:
+                    dls = [d for d in (o.next_deadline() for o in ops[1:]) if d is not None]
+                wait = 0.01 if not dls else min(0.01, max(2e-4, min(dls) - time.time()))
+                if stop.wait(wait):
+                    return
+                if time.perf_counter() - last[0] < wait:
+                    continue  # the source is emitting: the collect path polls
+                with lock:
+                    if stop.is_set():
+                        return
+                    poll(force=True)
+        except BaseException as e:  # noqa: BLE001 - _ChainCancelled included: re-raised after the source returns
+            timer_error.append(e)
+            fn.cancel()
+
+    timer = threading.Thread(target=chain_timer, name="worker-chain-timer", daemon=True)
+    timer.start()
     try:
-        fn.run(Ctx())
+        try:
+            fn.run(Ctx())
+        finally:
+            with lock:
+                stop.set()
+            timer.join()
+        if timer_error:
+            raise timer_error[0]
         with lock:
             poll(force=True)  # triggers that arrived before the end still get their barrier
             final = src.snapshot_state(-1, None)

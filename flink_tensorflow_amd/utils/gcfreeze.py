@@ -23,7 +23,12 @@ _lock = threading.Lock()
 def freeze_setup_objects(collect: bool = True) -> int:
     """One collection (optional), then ``gc.freeze()``.  Returns the number of frozen
     objects.  Idempotent; cheap to call again after more setup."""
-    with _lock:
+    from .tracing import capture_lock
+
+    # under the capture lock: a collection finalises whatever became garbage anywhere in
+    # the process (old plans' hipGraphs, arenas, pinned blocks) and must not do so while a
+    # sibling subtask thread is inside a stream capture
+    with capture_lock(), _lock:
         if collect:
             gc.collect()
         gc.freeze()

@@ -93,11 +93,22 @@ def graph_capture(graph, stream=None, pool=None):
 
     @contextlib.contextmanager
     def _cm():
+        import gc
+
         with lock:
             # a framework-owned capture stream: torch's default capture stream comes from the
             # stream pool and can coincide with a sibling subtask's replay stream (utils/streams.py)
             s = stream if stream is not None else capture_stream()
-            with torch.cuda.graph(graph, pool=pool, stream=s, capture_error_mode="thread_local"):
-                yield
+            # no automatic collection while capturing: a collection triggered by ANY thread
+            # runs finalisers (graph / arena / pinned-block teardown) in the middle of the
+            # capture (explicit collections take the capture lock: utils/gcfreeze.py)
+            was_enabled = gc.isenabled()
+            gc.disable()
+            try:
+                with torch.cuda.graph(graph, pool=pool, stream=s, capture_error_mode="thread_local"):
+                    yield
+            finally:
+                if was_enabled:
+                    gc.enable()
 
     return _cm()

@@ -40,3 +40,23 @@ def _rank_records(text):
         i = text.find('{"rank"', end)
     return out
 
+
+
+def run_isolated(target, timeout=240):
+    """Runs ``"module:function"`` (a module under tests/) in a fresh Python process with
+    ``faulthandler`` on for all threads.  Tests that put several GPU subtasks into one
+    process use it: a native abort (SIGABRT / SIGSEGV) then fails that one test, with every
+    thread's Python stack in the failure message, instead of killing the whole pytest run."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mod, fn = target.split(":")
+    code = (f"import sys; sys.path[:0] = [{root!r}, {os.path.join(root, 'tests')!r}]\n"
+            f"import {mod}\n{mod}.{fn}()\nprint('__ISOLATED_OK__', flush=True)\n")
+    env = dict(os.environ, PYTHONFAULTHANDLER="1", PYTHONUNBUFFERED="1")
+    r = subprocess.run([sys.executable, "-X", "faulthandler", "-c", code], stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=timeout, env=env, cwd=root)
+    out = r.stdout or ""
+    assert r.returncode == 0 and "__ISOLATED_OK__" in out, f"{target} exited with {r.returncode}:\n{out[-12000:]}"
+    return out

@@ -44,7 +44,7 @@ class _Writer:
 def _task(op):
     job = SimpleNamespace(cancel=threading.Event(), attempt=0, config=None, rank=0, world_size=1, restore_dir=None,
                           coordinator=None, device_for=lambda node, st: None, chk_dir=lambda cid: None,
-                          ack=lambda cid, key, state: None)
+                          ack=lambda cid, key, state: None, wait_all_opened=lambda: None)
     node = SimpleNamespace(uid="op", name="op", parallelism=1, remote=False, make_operator=lambda: op)
     gate = InputGate(64)
     t = _OpTask(job, node, 0, _Writer(), None, gate, [(0, 0), (1, 0)])

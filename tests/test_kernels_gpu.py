@@ -322,3 +322,20 @@ def test_bottleneck_tail_wide_kernel(M):
     torch.cuda.synchronize()
     _close(y3, y3_ref)
     _close(y1, y1_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,dtype", [(768, torch.bfloat16), (64, torch.float32)])
+def test_gather_rows_kernel(D, dtype):
+    """First-token (CLS) row gather of the packed encoder: == torch indexing; an index
+    out of range gives a zero row."""
+    from flink_tensorflow_amd.ops import kernels as K
+
+    dev = torch.device("cuda", 0)
+    x = torch.randn(1000, D, device=dev).to(dtype)
+    idx = torch.tensor([0, 999, 5, 5, -1, 1000, 17], dtype=torch.int32, device=dev)
+    got = K.gather_rows(x, idx)
+    want = torch.zeros_like(got)
+    ok = (idx >= 0) & (idx < 1000)
+    want[ok] = x[idx[ok].long()]
+    assert torch.equal(got, want)

@@ -104,3 +104,20 @@ def test_bench_refuses_missing_gpus():
     p = _bench("--gpus", "2", timeout=120)
     assert p.returncode != 0
     assert "refusing" in p.stderr
+
+
+def test_sysfs_gpu_count_reads_kfd_topology(tmp_path, monkeypatch):
+    """GPUs are counted from the KFD topology (nodes with SIMDs), narrowed by a visibility
+    mask, without loading any GPU library."""
+    from flink_tensorflow_amd.utils.gpus import sysfs_gpu_count
+
+    for i, simds in enumerate([0, 1024, 1024, 0, 1024]):  # CPU nodes have simd_count 0
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count 8\nsimd_count {simds}\nmem_banks_count 1\n")
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert sysfs_gpu_count(str(tmp_path)) == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
+    assert sysfs_gpu_count(str(tmp_path)) == 1
+    assert sysfs_gpu_count(str(tmp_path / "missing")) == 0

@@ -144,10 +144,8 @@ def test_remote_error_propagates():
         env.execute("remote-boom")
 
 
-@pytest.mark.gpu
-def test_remote_batched_resnet_gpu():
-    """Two ResNet subtasks as worker processes sharing the box's GPU (one per GPU on a
-    node), each with its own arena, pinned ring and captured plans."""
+def _two_gpu_subtasks_resnet():
+    """Body of ``test_remote_batched_resnet_gpu`` (runs in its own process)."""
     import numpy as np
 
     from flink_tensorflow_amd.models.zoo.image_classifier import ResNet50Model
@@ -166,8 +164,34 @@ def test_remote_batched_resnet_gpu():
 
     local, remote = run(False), run(True)
     assert len(remote) == len(local) == 40
+    # numerics: the fp32 interpreter on the host over the same images (results arrive in
+    # any order: compare the sorted top-1 probabilities and the multiset of top-1 labels)
+    ref = ResNet50Model(image_hw=(64, 64), buckets=(8, 16), top_k=3, depth_layers=26, device="cpu")
+    ref.open()
+    want = ref.label(imgs)
+    ref.close()
+    for got in (local, remote):
+        p_got = np.sort([r[0][0] for r in got])
+        p_want = np.sort([r[0][0] for r in want])
+        assert np.abs(p_got - p_want).max() < 0.01, (p_got, p_want)
+        lab_got = sorted(r[0][1] for r in got)
+        lab_want = sorted(r[0][1] for r in want)
+        common = sum(min(lab_got.count(x), lab_want.count(x)) for x in set(lab_want))
+        assert common >= 36, (lab_got, lab_want)
     top1 = lambda res: sorted(r[0][1] for r in res)  # noqa: E731 - each result: top-k (prob, label)
     assert top1(remote) == top1(local)
+
+
+@pytest.mark.gpu
+def test_remote_batched_resnet_gpu():
+    """Two ResNet subtasks, first as two threads of one process (each with its own runner,
+    arena and captured plans: the start barrier keeps every capture ahead of the first
+    replay), then as worker processes sharing the box's GPU (one per GPU on a node); both
+    checked against the fp32 interpreter.  Runs in a child process (a native abort fails
+    this test with every thread's stack, not the suite)."""
+    from _helpers import run_isolated
+
+    run_isolated("test_remote:_two_gpu_subtasks_resnet", timeout=300)
 
 
 def _digest(v):
@@ -350,3 +374,71 @@ def test_tensor_slab_view_batch_releases_with_the_last_view():
         wk.close()
         co.unlink()
         co.close()
+
+
+def _slow_stamped(n, gap_s):
+    def gen(idx, par, start):
+        import time as _t
+
+        for i in [i for i in range(n) if i % par == idx][start:]:
+            _t.sleep(gap_s)
+            yield (i, _t.time())
+    return gen
+
+
+def _stamp_batch(model, vals):
+    import time as _t
+
+    now = _t.time()
+    return [(i, now - t) for i, t in vals]
+
+
+def test_worker_source_chain_timer_fires_deadlines(tmp_path):
+    """A worker-process source that blocks between records (longer than the micro-batch
+    ``max_delay``): the worker's chain timer still flushes every partial batch on its
+    deadline (latency ~ max_delay, not the source's gap) and checkpoints still complete
+    while the source sleeps."""
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(1)
+    env.enable_checkpointing(0.05, str(tmp_path / "chk"))
+    sink = env.generate(_slow_stamped(8, 0.25)).run_in_processes() \
+        .map_with_model_batched(object(), _stamp_batch, max_batch=64, max_delay_ms=5).run_in_processes() \
+        .collect_into()
+    res = env.execute("slow-worker-source")
+    out = sorted(sink.results())
+    assert [i for i, _ in out] == list(range(8))
+    assert max(lat for _, lat in out) < 0.15, out  # without the timer: ~0.25 s (the next record)
+    assert len(res.checkpoints) >= 2
+
+
+class _DeviceProbe:
+    """A model that is a RichFunction: the batched operator hands it the runtime context."""
+
+    def set_runtime_context(self, ctx):
+        self.ctx = ctx
+
+
+def _device_of(model, vals):
+    import torch
+
+    c = model.ctx
+    want = torch.device("cuda", c.subtask_index % torch.cuda.device_count())
+    return [(c.subtask_index, str(c.device), str(want), str(torch.cuda.current_device())) for _ in vals]
+
+
+@pytest.mark.gpu
+def test_worker_source_chain_binds_gpu_member_device():
+    """In a worker-process source chain the source node itself uses no GPU: the chained GPU
+    operator still gets ``ctx.device = cuda:(subtask % gpus)`` and the worker's current
+    device is set to it (the device used to come from the source's spec)."""
+    from flink_tensorflow_amd.runtime import functions as F
+
+    class Probe(_DeviceProbe, F.RichFunction):
+        pass
+
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    out = env.generate(_own_partition(20)).run_in_processes() \
+        .map_with_model_batched(Probe(), _device_of, max_batch=4, max_delay_ms=2).run_in_processes() \
+        .execute_and_collect()
+    assert len(out) == 20
+    for sub, dev, want, cur in out:
+        assert dev == want and dev.endswith(":" + cur), (sub, dev, want, cur)

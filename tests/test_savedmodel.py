@@ -365,3 +365,28 @@ def test_bundle_reads_into_hbm_through_pinned_staging_gpu(tmp_path):
     with bundle.BundleReader(prefix) as r:
         with pytest.raises(bundle.DataLossError):
             r.read("big", device=dev)
+    # an entry whose stored size disagrees with its shape fails loudly (the CRC alone covers
+    # only the stored bytes: the device tensor's tail would stay uninitialised)
+    bundle.save_tensors(prefix, {"big": big, "small": small})
+    with bundle.BundleReader(prefix) as r:
+        r.entries["small"].size -= 4
+        with pytest.raises(bundle.DataLossError, match="needs"):
+            r.read("small", device=dev)
+
+
+def test_merge_rejects_partitions_that_disagree_on_the_full_shape(tmp_path):
+    """MergeV2Checkpoints of two shards holding slices of one partitioned variable whose
+    full shapes disagree is an error (TF rejects it too)."""
+    from types import SimpleNamespace
+
+    import flink_tensorflow_amd.graph.ops_io  # noqa: F401  (registers the checkpoint ops)
+    from flink_tensorflow_amd.graph.op_registry import lookup as get_op
+    from flink_tensorflow_amd.types.tensor import StringTensor
+
+    ctx = SimpleNamespace(device=torch.device("cpu"))
+    save = get_op("SaveV2")
+    p0, p1 = str(tmp_path / "s0" / "ckpt"), str(tmp_path / "s1" / "ckpt")
+    save(ctx, None, StringTensor(p0), StringTensor(["w"]), StringTensor(["6 4 0,2:-"]), torch.ones(2, 4))
+    save(ctx, None, StringTensor(p1), StringTensor(["w"]), StringTensor(["8 4 2,4:-"]), torch.ones(4, 4))
+    with pytest.raises(ValueError, match="disagree"):
+        bundle.merge_bundles([p0, p1], str(tmp_path / "m" / "ckpt"))
