@@ -49,6 +49,10 @@ class EngineConfig:
     pw_dual_kernel: bool = False       # stage-2 projection+expand on the persistent dual kernel
     conv3x3c64_kernel: bool = True     # 64-channel 3x3 convs with the filter bank in LDS
     wd_fused_step: bool = True         # Wide&Deep: hand-fused GPU step instead of autograd
+    # Wide&Deep under DP: "owner" = deduplicated rows to their owner rank (row % world),
+    # owner-side Adagrad, updated rows back (parallel/sparse_exchange.py); "allgather" = the
+    # padded all-gather of one row per lookup (sync-free: the DP step stays capturable)
+    wd_sparse_exchange: str = "owner"
     extra: dict = field(default_factory=dict)
 
     # ------------------------------------------------------------------ sources

@@ -92,6 +92,16 @@ class Comm {
     check(ncclReduceScatter(P(send), P(recv), recvcount, dtype_of(dt), op_of(op), comm_, S(stream)),
           "ncclReduceScatter");
   }
+  // point-to-point (inside a group_start / group_end pair: an all-to-all with per-peer
+  // counts is one send + one recv per peer, all in one group)
+  void send(std::uintptr_t buf, size_t count, int dt, int peer, std::uintptr_t stream) {
+    live();
+    check(ncclSend(P(buf), count, dtype_of(dt), peer, comm_, S(stream)), "ncclSend");
+  }
+  void recv(std::uintptr_t buf, size_t count, int dt, int peer, std::uintptr_t stream) {
+    live();
+    check(ncclRecv(P(buf), count, dtype_of(dt), peer, comm_, S(stream)), "ncclRecv");
+  }
   // returns "" while healthy, else RCCL's error string (peer failure, network error)
   std::string async_error() {
     if (comm_ == nullptr) return "communicator destroyed";
@@ -150,6 +160,8 @@ PYBIND11_MODULE(_rccl, m) {
       .def("all_reduce", &Comm::all_reduce)
       .def("all_gather", &Comm::all_gather)
       .def("reduce_scatter", &Comm::reduce_scatter)
+      .def("send", &Comm::send)
+      .def("recv", &Comm::recv)
       .def("async_error", &Comm::async_error)
       .def("abort", &Comm::abort)
       .def("destroy", &Comm::destroy)

@@ -246,8 +246,8 @@ class DefaultSavedModelLoader(SavedModelLoader):
         self.tags = tuple(tags)
         self._metagraph: MetaGraphDef | None = None
 
-    def __getstate__(self):
-        return {"export_path": self.export_path, "tags": self.tags, "_metagraph": None}
+    def __getstate__(self):  # the parsed MetaGraphDef is transient (subclass fields travel)
+        return {**self.__dict__, "_metagraph": None}
 
     @property
     def metagraph(self) -> MetaGraphDef:

@@ -128,7 +128,7 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
     """Online trainer: ``train_step(records)`` on micro-batches of
     ``(label, dense[13], cats[26], cross[C])`` records; ``predict(records)``."""
 
-    _TRANSIENT = ("_model", "_opt", "_bucketer", "_graph", "_static", "_static_loss", "_fused")
+    _TRANSIENT = ("_model", "_opt", "_bucketer", "_graph", "_static", "_static_loss", "_fused", "_exchange")
 
     def __init__(self, cfg: WideDeepConfig | None = None, device=None, seed: int = 0, fused: bool | None = None):
         self.cfg = cfg or WideDeepConfig()
@@ -137,6 +137,7 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         # fused: the hand-fused GPU step (models/zoo/wide_deep_fused.py); None = on a GPU
         # unless EngineConfig.wd_fused_step is off.  False: autograd forward/backward + torch Adam.
         self.fused = fused
+        self._exchange = None  # owner-based sparse exchange under DP (parallel/sparse_exchange.py)
         self._model = self._opt = self._bucketer = self._fused = None
         self._graph = self._static = self._static_loss = None
         self.steps = 0
@@ -149,10 +150,14 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         from ...config import current
 
         use_fused = self.fused if self.fused is not None else current().wd_fused_step
+        if comm.is_dist() and current().wd_sparse_exchange == "owner":
+            from ...parallel.sparse_exchange import OwnerSparseExchange
+
+            self._exchange = OwnerSparseExchange(comm.get())
         from .wide_deep_fused import FusedWideDeepStep
 
         if dev.type == "cuda" and use_fused and FusedWideDeepStep.supports(self.cfg):
-            self._fused = FusedWideDeepStep(self._model, self.cfg.lr_dense, self.cfg.lr_sparse)
+            self._fused = FusedWideDeepStep(self._model, self.cfg.lr_dense, self.cfg.lr_sparse, exchange=self._exchange)
             return
         fused = dev.type == "cuda"  # one multi-tensor Adam launch instead of one per parameter tensor
         self._opt = torch.optim.Adam(self._model.dense_parameters(), lr=self.cfg.lr_dense, fused=fused,
@@ -162,8 +167,13 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
     def close(self):
         if self._bucketer is not None:
             self._bucketer.remove()
-        self._model = self._opt = self._bucketer = self._fused = None
+        self._model = self._opt = self._bucketer = self._fused = self._exchange = None
         self._graph = self._static = self._static_loss = None
+
+    @property
+    def exchange_stats(self):
+        """Bytes sent / received by the last step's owner exchange (None without one)."""
+        return self._exchange.stats if self._exchange is not None else None
 
     @property
     def is_open(self):
@@ -208,6 +218,8 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         the row-sparse all-gathers run on the capturing stream, so one replay is one whole
         DP step."""
         dev = self._model.device
+        if self._exchange is not None:
+            return  # the owner exchange sizes its messages on the host: steps run uncaptured
         packed = getattr(batch, "packed", None)
         if packed is not None:  # static copy of the packed buffer + the same views into it
             sp = packed.to(dev).clone()
@@ -233,6 +245,9 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
             loss = self._fused.step(labels, dense, cats, cross)
             self.steps += 1
             return loss
+        if self._exchange is not None:
+            self._exchange.begin_step()
+            self.pull_rows(cats, cross)
         logits = m(dense, cats, cross)
         loss = F.binary_cross_entropy_with_logits(logits, labels)
         self._opt.zero_grad(set_to_none=True)
@@ -240,20 +255,34 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         self._bucketer.synchronize()  # dense grads: bucketed all-reduce launched during backward
         self._opt.step()
         sync = _sparse_sync if comm.is_dist() else None
-        m.emb.apply_updates(self.cfg.lr_sparse, sync)
-        m.wide.apply_updates(self.cfg.lr_sparse, sync)
+        m.emb.apply_updates(self.cfg.lr_sparse, sync, self._exchange)
+        m.wide.apply_updates(self.cfg.lr_sparse, sync, self._exchange)
         self.steps += 1
         return loss.detach()
+
+    def pull_rows(self, cats, cross) -> None:
+        """Owner exchange: refreshes the embedding / wide rows this batch looks up from their
+        owners (the rows a rank does not own are a cache, ``parallel/sparse_exchange.py``)."""
+        m, cfg = self._model, self.cfg
+        offs = torch.arange(cfg.num_fields, device=cats.device, dtype=torch.int64) * cfg.vocab_per_field
+        self._exchange.pull_lookups(m.emb.table.data, cats.to(torch.int64) + offs)
+        self._exchange.pull_lookups(m.wide.table.data, cross)
 
     @torch.no_grad()
     def predict(self, records) -> list[float]:
         _, dense, cats, cross = self.collate(records)
+        if self._exchange is not None:
+            self.pull_rows(cats, cross)
         return torch.sigmoid(self._model(dense, cats, cross)).tolist()
 
     # ---- CheckpointedModel
     def snapshot_state(self, ctx):
         d = model_state_dir(ctx, "widedeep")
         st = {f"model/{k}": v for k, v in self._model.state().items()}
+        if self._exchange is not None:  # owner-authoritative rows and Adagrad state: merge the shards
+            for name, e in (("emb", self._model.emb), ("wide", self._model.wide)):
+                st[f"model/{name}.table"] = self._exchange.merge_owner_shards(e.table.data)
+                st[f"model/{name}.accum"] = self._exchange.merge_owner_shards(e.accum)
         if self._fused is not None:
             st.update(self._fused.state())
         else:
@@ -261,7 +290,7 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
                 for k, v in s.items():
                     if torch.is_tensor(v):
                         st[f"adam/{i}/{k}"] = v.detach().reshape(v.shape)
-        if d is not None and (not comm.is_dist() or comm.world()[0] == 0):
+        if d is not None and comm.rank_size()[0] == 0:
             bundle.save_tensors(os.path.join(d, "variables"), st)
         ctx.operator_state.blobs["widedeep_steps"] = self.steps
 

@@ -80,8 +80,9 @@ class FusedWideDeepStep:
                 and cfg.embed_dim % 8 == 0 and d8 & (d8 - 1) == 0 and d8 <= 64
                 and (cfg.num_fields * cfg.embed_dim) % 8 == 0)
 
-    def __init__(self, model, lr: float, lr_sparse: float, betas=(0.9, 0.999), eps: float = 1e-8):
+    def __init__(self, model, lr: float, lr_sparse: float, betas=(0.9, 0.999), eps: float = 1e-8, exchange=None):
         dev = model.device
+        self.exchange = exchange  # OwnerSparseExchange under DP (else the padded all-gather)
         if dev.type != "cuda":
             raise ValueError("the fused Wide&Deep step runs on a GPU")
         self.m, self.cfg, self.dev = model, model.cfg, dev
@@ -168,6 +169,11 @@ class FusedWideDeepStep:
         if labels.dim() != 1:
             labels = labels.reshape(-1)
         dist = comm.is_dist()
+        if dist and self.exchange is not None:  # fresh copies of the rows this batch reads
+            self.exchange.begin_step()
+            offs = torch.arange(self.F, device=cats.device, dtype=torch.int64) * cfg.vocab_per_field
+            self.exchange.pull_lookups(m.emb.table.data, cats.to(torch.int64) + offs)
+            self.exchange.pull_lookups(m.wide.table.data, cross)
         # forward
         H.wd_gather(cats.data_ptr(), cats.stride(0), dense.data_ptr(), dense.stride(0), cross.data_ptr(),
                     cross.stride(0), m.emb.table.data_ptr(), m.wide.table.data_ptr(), a.x.data_ptr(), a.wsum.data_ptr(),
@@ -213,14 +219,20 @@ class FusedWideDeepStep:
         rw = segment_sum_grouped(groups, a.wgrad, 1, ne, ne + B * C)
         ue = uw = u
         ws = 1
-        if dist:
+        if dist and self.exchange is not None:
+            # deduplicated rows to their owners, owner-side Adagrad, updated rows back
+            ws = comm.get().size
+            self.exchange.apply(m.emb.table.data, m.emb.accum, u, re, self.lr_sparse)
+            self.exchange.apply(m.wide.table.data, m.wide.accum, u, rw, self.lr_sparse, offset=FV)
+        elif dist:
             from .wide_deep import _sparse_sync
 
             ue, re = segment_sum(*_sparse_sync(u, re), FV + WV, static=True)
             uw, rw = segment_sum(*_sparse_sync(u, rw), FV + WV, static=True)
             ws = comm.get().size
-        sparse_adagrad(m.emb.table.data, m.emb.accum, ue, re, self.lr_sparse)
-        sparse_adagrad(m.wide.table.data, m.wide.accum, uw, rw, self.lr_sparse, offset=FV)
+        if not (dist and self.exchange is not None):
+            sparse_adagrad(m.emb.table.data, m.emb.accum, ue, re, self.lr_sparse)
+            sparse_adagrad(m.wide.table.data, m.wide.accum, uw, rw, self.lr_sparse, offset=FV)
         for w in works:  # dense gradients reduced (overlapped with the GEMMs + sparse pipeline)
             w.wait()
         # dense Adam over the flat buffer + the bf16 operands of the next step

@@ -196,14 +196,21 @@ class SparseEmbedding(torch.nn.Module):
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
         return EmbeddingBagFunction.apply(ids, self.table, self.anchor, self)
 
-    def apply_updates(self, lr: float, sync=None):
-        """Applies the step's sparse gradients (optionally synchronised across ranks)."""
+    def apply_updates(self, lr: float, sync=None, exchange=None):
+        """Applies the step's sparse gradients (optionally synchronised across ranks:
+        ``sync`` all-gathers them for every replica to apply; ``exchange`` — an
+        ``parallel.sparse_exchange.OwnerSparseExchange`` — sends them to the rows' owners)."""
         if not self.sparse_grads:
             return 0
         several = len(self.sparse_grads) > 1
         uids = torch.cat([u for u, _ in self.sparse_grads])
         rows = torch.cat([r for _, r in self.sparse_grads])
         self.sparse_grads.clear()
+        if exchange is not None:
+            if several:  # one row per id on this rank before the exchange
+                uids, rows = segment_sum(uids, rows, self.table.shape[0], static=True)
+            exchange.apply(self.table.data, self.accum, uids, rows, lr)
+            return int(uids.numel())
         if sync is not None:
             uids, rows = sync(uids, rows)
         # merge duplicate rows (several lookups, several ranks) with the deterministic

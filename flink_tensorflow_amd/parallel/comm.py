@@ -165,6 +165,13 @@ class Communicator(abc.ABC):
         self.all_reduce(t, op)
         return Work()
 
+    def all_to_all_v(self, out: torch.Tensor, out_splits: Sequence[int], inp: torch.Tensor,
+                     in_splits: Sequence[int]) -> None:
+        """Personalised exchange along dim 0: rows ``in_splits[r]`` of ``inp`` (in rank
+        order) go to rank r; ``out`` receives ``out_splits[r]`` rows from rank r, in rank
+        order.  The splits are host integers every pair agrees on."""
+        raise NotImplementedError
+
     def group(self):
         """Context manager fusing the collectives issued inside into one launch."""
         import contextlib
@@ -255,6 +262,24 @@ class RcclCommunicator(Communicator):
             raise ValueError("reduce_scatter: inp must hold size x out elements of out's dtype")
         self._c.reduce_scatter(inp.data_ptr(), out.data_ptr(), out.numel(), self._dt(out), _NCCL_OP[op],
                                self._cur())
+
+    def all_to_all_v(self, out, out_splits, inp, in_splits):
+        _check(out, self.device)
+        _check(inp, self.device)
+        row = int(np.prod(inp.shape[1:])) if inp.dim() > 1 else 1
+        dt, st = self._dt(inp), self._cur()
+        esz = inp.element_size()
+        with self.group():  # one send + one recv per peer, one launch
+            o = 0
+            for r, n in enumerate(in_splits):
+                if n:
+                    self._c.send(inp.data_ptr() + o * row * esz, n * row, dt, r, st)
+                o += n
+            o = 0
+            for r, n in enumerate(out_splits):
+                if n:
+                    self._c.recv(out.data_ptr() + o * row * esz, n * row, dt, r, st)
+                o += n
 
     def all_reduce_async(self, t, op="sum") -> Work:
         _check(t, self.device)

@@ -108,6 +108,26 @@ class FakeCommunicator(Communicator):
         n = out.numel()
         out.copy_(red[self.rank * n:(self.rank + 1) * n].view(out.shape))
 
+    def all_to_all_v(self, out, out_splits, inp, in_splits):
+        # one round: every rank publishes its whole send buffer; each takes its slice from
+        # every peer (rank order), as RCCL's grouped send/recv delivers it
+        offs = np.concatenate([[0], np.cumsum(list(in_splits))]).tolist()
+        meta = np.asarray(offs, np.int64).tobytes()
+        got = self._exchange(meta + self._bytes(inp))
+        host = inp.detach().to("cpu")
+        row = int(np.prod(inp.shape[1:])) if inp.dim() > 1 else 1
+        nmeta = 8 * (self.size + 1)
+        parts = []
+        for r, b in enumerate(got):
+            o = np.frombuffer(b[:nmeta], np.int64)
+            flat = torch.from_numpy(np.frombuffer(b[nmeta:], np.uint8).copy()).view(host.dtype)
+            part = flat[o[self.rank] * row:o[self.rank + 1] * row]
+            if part.numel() != out_splits[r] * row:
+                raise ValueError(f"all_to_all_v: rank {r} sends {part.numel() // max(row, 1)} rows, expected "
+                                 f"{out_splits[r]}")
+            parts.append(part)
+        out.copy_(torch.cat(parts).view(out.shape) if parts else out)
+
     def all_gather_object(self, obj):
         import pickle
 

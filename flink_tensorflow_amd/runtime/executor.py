@@ -575,6 +575,42 @@ class LocalExecutor:
         self.rank, self.world_size = env.rank, env.world_size
         self._lock = threading.Lock()
         self._opened: threading.Barrier | None = None
+        self._groups: dict = {}
+
+    def operator_group(self, node) -> dict | None:
+        """The rendezvous of a worker-process GPU operator's subtasks (one
+        subtask per GPU, rank 0 loads, RCCL broadcast): a key/value store hosted here in the
+        coordinator, under an attempt-scoped prefix.  Each worker opens its communicator on
+        it (subtask = rank) before ``op.open()``; rank 0 publishes the RCCL unique id.  None
+        when the operator does not form one: SPMD jobs (each rank runs its own subtasks
+        and already has the global communicator), host operators, or fewer GPUs than
+        subtasks (RCCL needs one GPU per rank).  GPUs are counted from sysfs: the
+        coordinator never initialises HIP for this."""
+        mode = getattr(self.env, "job_communicator", "auto")
+        test_cls = getattr(self.env, "test_communicator", None)
+        if not mode or self.world_size > 1 or not node.uses_gpu:
+            return None
+        if mode == "auto" and node.parallelism <= 1:
+            return None
+        if test_cls is None:
+            from ..utils.gpus import sysfs_gpu_count
+
+            if sysfs_gpu_count() < node.parallelism:
+                return None
+        with self._lock:
+            g = self._groups.get(node.uid)
+            if g is None:
+                import datetime
+
+                from torch.distributed import TCPStore
+
+                store = TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False,
+                                 timeout=datetime.timedelta(seconds=600))
+                g = self._groups[node.uid] = {"addr": "127.0.0.1", "port": store.port, "size": node.parallelism,
+                                              "prefix": f"ftm-op/{node.uid}/{self.attempt}/",
+                                              "cls": cloudpickle.dumps(test_cls) if test_cls is not None else None,
+                                              "_store": store}
+        return {k: v for k, v in g.items() if not k.startswith("_")}
 
     def wait_all_opened(self):
         """Start barrier: a task thread emits or processes its first record only after
@@ -645,6 +681,7 @@ class LocalExecutor:
 
     # ---- build + run
     def _build(self, restore_states: dict | None):
+        self._groups = {}  # a restarted attempt rendezvouses afresh (new store, new prefix)
         nodes = self.env._topo_nodes()
         cap = self.config.channel_capacity
         ops = {(n.uid, i): n.make_operator() for n in nodes if not n.is_source and not getattr(n, "remote", False)

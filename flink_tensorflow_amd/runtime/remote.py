@@ -345,11 +345,49 @@ class ShmChannel:
 
 
 # ------------------------------------------------------------------ worker side
+def _open_group(spec, device):
+    """Joins the operator's communicator (``LocalExecutor.operator_group``) and installs it
+    as this process's ``parallel.comm`` communicator: RCCL on the subtask's GPU, or the
+    test implementation the job injected."""
+    g = spec.get("group")
+    if not g:
+        return None
+    import datetime
+
+    from torch.distributed import PrefixStore, TCPStore
+
+    from ..parallel import comm
+
+    if not g.get("cls") and (device is None or device.type != "cuda"):
+        return None
+    store = PrefixStore(g["prefix"], TCPStore(g["addr"], g["port"], g["size"], is_master=False,
+                                              timeout=datetime.timedelta(seconds=600)))
+    if g.get("cls"):
+        c = cloudpickle.loads(g["cls"])(spec["subtask"], g["size"], device or "cpu", store)
+    else:
+        c = comm.RcclCommunicator(spec["subtask"], g["size"], device, store)
+    comm.set_communicator(c)
+    return c
+
+
+def _close_group(c, abort: bool) -> None:
+    if c is None:
+        return
+    from ..parallel import comm
+
+    try:
+        comm.set_communicator(None)
+        c.destroy(abort=abort)  # a failed subtask aborts: the restarted attempt builds a new group
+    except Exception:  # noqa: BLE001
+        pass
+
+
 def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
     inp = ShmChannel(in_name, create=False)
     out = ShmChannel(out_name, create=False)
     slab = TensorSlab(slab_name, create=False) if slab_name else None
     op = None
+    group = None
     pending: list = []
     parent = os.getppid()
 
@@ -397,6 +435,7 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
                              spec["config"], None)
         ctx.global_index, ctx.global_parallelism = spec["global_index"], spec["global_parallelism"]
         ctx.worker_pid = os.getpid()
+        group = _open_group(spec, device)
         op = cloudpickle.loads(factory)()
         op.setup(ctx, Output(emit, lambda tag, v: (flush(), out.send(("side", [(tag, v)]), alive=parent_alive))))
         op.initialize(restore, restore_dir)
@@ -446,6 +485,8 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
             elif kind == "close":
                 op.close()
                 op = None
+                _close_group(group, abort=False)
+                group = None
                 flush()
                 out.send(("closed", metrics.snapshot()), alive=parent_alive)
                 break
@@ -463,6 +504,7 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
                 op.close()
             except Exception:  # noqa: BLE001
                 pass
+        _close_group(group, abort=True)
         out.close()
 
 
@@ -512,6 +554,7 @@ def _run_source_chain(msg, inp, out, emit, flush, parent_alive):
                 raise TypeError(f"operators emit records and watermarks, not {type(elem).__name__}")
         return e
 
+    group = _open_group(gpu_spec, device) if gpu_spec is not None else None
     for i, (op, sp) in enumerate(zip(ops, specs)):
         mg = MetricGroup(f"{sp['name']}[{sp['subtask']}]")
         metrics.append(mg)
@@ -639,6 +682,8 @@ def _run_source_chain(msg, inp, out, emit, flush, parent_alive):
         for o in ops:
             o.close()
         ops = []
+        _close_group(group, abort=False)
+        group = None
         metrics[0].inc("records_out", recs_out[0])
         out.send(("closed", [mg.snapshot() for mg in metrics]), alive=parent_alive)
     except _ChainCancelled:
@@ -649,8 +694,14 @@ def _run_source_chain(msg, inp, out, emit, flush, parent_alive):
                 o.close()
             except Exception:  # noqa: BLE001
                 pass
+        _close_group(group, abort=True)
 
 # ------------------------------------------------------------------ coordinator side
+def _job_group(job, node):
+    f = getattr(job, "operator_group", None)
+    return f(node) if f is not None and getattr(node, "uses_gpu", False) else None
+
+
 class RemoteOperatorProxy:
     """Stands in for the operator inside the coordinator's task loop."""
 
@@ -707,7 +758,8 @@ class RemoteOperatorProxy:
             self.slab.unlink()
         spec = {"name": self.node.name, "subtask": self.subtask, "parallelism": self.node.parallelism,
                 "gpu": bool(self.node.uses_gpu), "attempt": self.job.attempt, "config": self.job.config,
-                "global_index": self.ctx.global_index, "global_parallelism": self.ctx.global_parallelism}
+                "global_index": self.ctx.global_index, "global_parallelism": self.ctx.global_parallelism,
+                "group": _job_group(self.job, self.node)}
         self._send(("init", cloudpickle.dumps(self.node.factory), spec, snapshot, checkpoint_dir))
 
     def open(self):
@@ -898,7 +950,8 @@ class RemoteChainProxy(RemoteOperatorProxy):
         self.from_worker.unlink()
         specs = [{"name": n.name, "subtask": self.subtask, "parallelism": n.parallelism, "gpu": bool(n.uses_gpu),
                   "attempt": self.job.attempt, "config": self.job.config, "global_index": c.global_index,
-                  "global_parallelism": c.global_parallelism} for n, c in zip(self.nodes, contexts)]
+                  "global_parallelism": c.global_parallelism, "group": _job_group(self.job, n)}
+                 for n, c in zip(self.nodes, contexts)]
         self._send(("init_chain", [cloudpickle.dumps(n.factory) for n in self.nodes], specs, list(restores),
                     checkpoint_dir))
 

@@ -82,6 +82,10 @@ class StreamExecutionEnvironment:
         self.restart_strategy = RestartStrategy.no_restart()
         self.fault_injector = None
         self.chaining = True
+        # one communicator per worker-process GPU operator (runtime/remote.py): "auto" forms it
+        # when the operator runs P > 1 subtasks and the node has >= P GPUs; True also for P = 1
+        self.job_communicator: bool | str = "auto"
+        self.test_communicator = None  # test-only injection (parallel/fake.py), never set by product code
         from ..parallel.comm import world
 
         self.rank, self.world_size, _ = world()
@@ -99,6 +103,16 @@ class StreamExecutionEnvironment:
 
     def get_parallelism(self) -> int:
         return self.parallelism
+
+    def enable_job_communicator(self, on: bool | str = True, communicator=None) -> "StreamExecutionEnvironment":
+        """Data parallelism inside one job: the P worker-process subtasks of a GPU operator
+        form one communicator (RCCL over xGMI, subtask = rank, one GPU per subtask), so a
+        model opened with ``distributed_weights=True`` is read by subtask 0 only and
+        broadcast, and a ``ModelCoProcessFunction`` trainer all-reduces its gradients with
+        ``parallel.comm.get()``.  ``communicator`` injects a test implementation."""
+        self.job_communicator = on
+        self.test_communicator = communicator
+        return self
 
     def disable_operator_chaining(self) -> "StreamExecutionEnvironment":
         """Every operator runs in its own subtask thread (records cross a channel between

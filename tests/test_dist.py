@@ -129,7 +129,13 @@ def _widedeep(rank, world):
     recs = synthetic_click_records(256, t.cfg, seed=100 + rank)  # different data per rank
     for i in range(4):
         t.train_step(recs[i * 64:(i + 1) * 64])
-    sd = {k: v.detach().numpy().copy() for k, v in t.model.state_dict().items()}  # plain arrays over the queue
+    sd = dict(t.model.state_dict())
+    if t._exchange is not None:  # owner exchange: rows / Adagrad state are authoritative at their owner
+        for name in ("emb", "wide"):
+            e = getattr(t.model, name)
+            sd[f"{name}.table"] = t._exchange.merge_owner_shards(e.table.data)
+            sd[f"{name}.accum"] = t._exchange.merge_owner_shards(e.accum)
+    sd = {k: v.detach().numpy().copy() for k, v in sd.items()}  # plain arrays over the queue
     t.close()
     return sd
 

@@ -1,0 +1,106 @@
+"""Data parallelism inside ONE streaming job (SURVEY §2.12 "one subtask per GPU, rank 0
+loads, RCCL broadcast"): the P worker-process subtasks of a GPU operator form one
+communicator (``LocalExecutor.operator_group`` → ``runtime/remote.py::_open_group``).
+
+Reference: parallel subtasks are the reference's execution model
+(``flink-tensorflow-examples/.../inception/inception.scala:22-23``); there every subtask
+reads the model itself (``DefaultSavedModelLoader.scala:40-56``).  Here only subtask 0
+reads the variables and the others receive them; CPU tests inject the loopback
+communicator, the GPU test runs through RCCL."""
+import os
+
+import pytest
+import torch
+
+from flink_tensorflow_amd.models.savedmodel import DefaultSavedModelLoader, TensorFlowModel
+from flink_tensorflow_amd.runtime import StreamExecutionEnvironment
+
+
+class _RecordingLoader(DefaultSavedModelLoader):
+    """Marks, per process, whether it read the variables from the bundle."""
+
+    def __init__(self, path, marks):
+        super().__init__(path, ("serve",))
+        self.marks = marks
+
+    def load(self, device=None, read_variables: bool = True):
+        if read_variables:
+            open(os.path.join(self.marks, f"read-{os.getpid()}"), "w").close()
+        return super().load(device=device, read_variables=read_variables)
+
+
+class _HalfPlusTwo(TensorFlowModel):
+    def __init__(self, path, marks):
+        super().__init__(None, distributed_weights=True)
+        self._loader = _RecordingLoader(path, marks)
+
+    @property
+    def loader(self):
+        return self._loader
+
+
+def _variables_of(value, model):
+    from flink_tensorflow_amd.parallel import comm
+
+    vs = model.session().variables
+    return (os.getpid(), comm.rank_size(), {k: float(vs[k].reshape(-1)[0]) for k in ("a", "b", "c")}, value)
+
+
+def test_p4_job_reads_once_and_broadcasts(tmp_path, half_plus_two):
+    """A P=4 job of worker-process model subtasks: only subtask 0 reads the bundle's
+    variables; all four serve bit-identical values after the in-job broadcast."""
+    from flink_tensorflow_amd.parallel.fake import FakeCommunicator
+
+    marks = tmp_path / "marks"
+    marks.mkdir()
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(4)
+    env.enable_job_communicator(True, communicator=FakeCommunicator)
+    model = _HalfPlusTwo(half_plus_two, str(marks))
+    out = env.from_collection(list(range(40))).rebalance().map_with_model(model, _variables_of) \
+        .run_in_processes().execute_and_collect()
+    assert sorted(o[3] for o in out) == list(range(40))
+    pids = {o[0] for o in out}
+    assert len(pids) == 4 and os.getpid() not in pids
+    assert {o[1] for o in out} == {(r, 4) for r in range(4)}  # every subtask is a rank of one group
+    assert {tuple(o[2].items()) for o in out} == {(("a", 0.5), ("b", 2.0), ("c", 3.0))}
+    readers = [f for f in os.listdir(marks)]
+    assert len(readers) == 1, readers  # subtask 0 only
+
+
+def test_no_group_without_enough_gpus_or_for_host_operators(tmp_path, half_plus_two):
+    """Without an injected communicator the group is formed only when the node has a GPU
+    per subtask: on this host the subtasks run without one (each reads its own model)."""
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    marks = tmp_path / "marks"
+    marks.mkdir()
+    out = env.from_collection(list(range(10))).rebalance().map_with_model(_HalfPlusTwo(half_plus_two, str(marks)),
+                                                                          _variables_of) \
+        .run_in_processes().execute_and_collect()
+    if torch.cuda.device_count() < 2:
+        assert {o[1] for o in out} == {(0, 1)} and len(os.listdir(marks)) == 2
+
+
+def _rccl_probe(value, model):
+    from flink_tensorflow_amd.parallel import comm
+
+    c = comm.get()
+    t = torch.full((4,), float(c.rank + 1), device=c.device)
+    c.all_reduce(t)
+    return (type(c).__name__, c.size, str(c.device), float(t[0].item()),
+            float(model.session().variables["a"].reshape(-1)[0]))
+
+
+@pytest.mark.gpu
+def test_p1_job_communicator_runs_through_rccl_gpu(tmp_path, half_plus_two):
+    """P = 1 with the job communicator on: the worker subtask opens an RCCL communicator on
+    its GPU, the distributed-weights open goes through it, and an all-reduce works."""
+    marks = tmp_path / "marks"
+    marks.mkdir()
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(1)
+    env.enable_job_communicator(True)
+    model = _HalfPlusTwo(half_plus_two, str(marks))
+    model.device = torch.device("cuda", 0)
+    out = env.from_collection(list(range(3))).map_with_model(model, _rccl_probe).run_in_processes() \
+        .execute_and_collect()
+    assert out and all(o == ("RcclCommunicator", 1, "cuda:0", 1.0, 0.5) for o in out), out
+    assert len(os.listdir(marks)) == 1

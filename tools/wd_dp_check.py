@@ -3,7 +3,9 @@ every rank trains the fused GPU step on its own synthetic records for a few step
 given communicator (``--fake``: the loopback test communicator, so several ranks can share
 one GPU; default RCCL on ``cuda:LOCAL_RANK``), then prints one JSON line with checksums of
 all dense parameters and both embedding tables.  Replicas must agree bit for bit: dense
-gradients are all-reduced, row-sparse gradients all-gathered and merged deterministically."""
+gradients are all-reduced; row-sparse gradients go to the rows' owners (the owner exchange,
+``parallel/sparse_exchange.py``: tables compared as merged owner shards) or are all-gathered
+and merged deterministically (``FT_WD_SPARSE_EXCHANGE=allgather``)."""
 import argparse
 import json
 import os
@@ -37,7 +39,12 @@ def main():
     recs = synthetic_click_records(256 * a.steps, cfg, seed=100 + rank)
     losses = [float(tr.train_step(recs[i * 256:(i + 1) * 256])) for i in range(a.steps)]
     torch.cuda.synchronize(dev)
-    sd = tr.model.state_dict()
+    sd = dict(tr.model.state_dict())
+    if tr._exchange is not None:  # owner-authoritative rows / Adagrad state: the merged shards
+        for name in ("emb", "wide"):
+            e = getattr(tr.model, name)
+            sd[f"{name}.table"] = tr._exchange.merge_owner_shards(e.table.data)
+            sd[f"{name}.accum"] = tr._exchange.merge_owner_shards(e.accum)
     sums = {k: [float(v.double().sum()), float(v.double().abs().sum())] for k, v in sorted(sd.items())}
     sys.stdout.write(json.dumps({"rank": rank, "fused": tr._fused is not None, "losses": losses, "sums": sums}) + "\n")  # one write per record
     sys.stdout.flush()
