@@ -1,6 +1,9 @@
 """Coordinator -> worker-process record transport: decoded-image records (256x256x3 uint8,
 196 KB) streamed through ``run_in_processes()`` subtasks (tensor slab: payload written once
 into shared memory, descriptors through the ring) vs the pickle path (FTM_SLAB_BYTES=0).
+The generator source is splittable, so by default the executor relocates it into the
+worker processes (``LocalExecutor._relocate_sources``: records are produced where they are
+consumed); ``--no-relocate`` measures the coordinator -> slab -> worker copy path.
 Prints one JSON line: aggregate GB/s and records/s of the whole job."""
 import argparse
 import json
@@ -26,6 +29,9 @@ def main():
                     help="the parallel source runs inside the worker processes, chained with the map "
                          "(records are produced where they are consumed; nothing crosses the coordinator)")
     ap.add_argument("--no-chain", action="store_true", help="disable operator chaining (source and proxy threads)")
+    ap.add_argument("--no-relocate", action="store_true",
+                    help="keep the generator source in the coordinator (env.relocate_sources = False): every "
+                         "record is produced there and copied into the workers' slabs")
     a = ap.parse_args()
     from flink_tensorflow_amd.runtime import StreamExecutionEnvironment
     from flink_tensorflow_amd.runtime.sources import ThroughputSink
@@ -47,13 +53,17 @@ def main():
     env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(a.workers)
     if a.no_chain:
         env.disable_operator_chaining()
+    env.relocate_sources = not a.no_relocate
     sink = ThroughputSink(every=512)
     src = env.generate(images)
     if a.remote_source:
         src = src.run_in_processes()
     src.map(_touch).run_in_processes().add_sink(sink, parallelism=1)
+    from flink_tensorflow_amd.runtime.executor import LocalExecutor
+
     t0 = time.perf_counter()
-    env.execute("transport")
+    ex = LocalExecutor(env, "transport")
+    ex.execute()
     el = time.perf_counter() - t0
     got = sink.count() if hasattr(sink, "count") else n
     steady = sink.rate(0.3)  # after worker spawn / import and pipeline fill
@@ -62,7 +72,7 @@ def main():
                       "steady_GB_per_s": round(steady * pool[0].nbytes / 1e9, 2),
                       "slab": os.environ.get("FTM_SLAB_BYTES", "default") != "0", "cpus": os.cpu_count(),
                       "mode": "in-worker parallel source" if a.remote_source else "coordinator source -> workers",
-                      "chained": not a.no_chain}),
+                      "relocated_sources": ex.relocated, "chained": not a.no_chain}),
           flush=True)
     assert got == n
 

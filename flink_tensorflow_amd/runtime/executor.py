@@ -683,6 +683,7 @@ class LocalExecutor:
     def _build(self, restore_states: dict | None):
         self._groups = {}  # a restarted attempt rendezvouses afresh (new store, new prefix)
         nodes = self.env._topo_nodes()
+        self.relocated = self._relocate_sources(nodes)
         cap = self.config.channel_capacity
         ops = {(n.uid, i): n.make_operator() for n in nodes if not n.is_source and not getattr(n, "remote", False)
                for i in range(n.parallelism)}
@@ -753,6 +754,56 @@ class LocalExecutor:
         from .remote import RemoteOperatorProxy
 
         return RemoteOperatorProxy(node, subtask, self)
+
+    def _relocate_sources(self, nodes) -> list[str]:
+        """Moves relocatable sources into the worker processes of their consumer: a source
+        whose function is splittable by subtask (``relocatable``), feeding exactly one
+        worker-process operator of the same parallelism (forward or rebalance edge, single
+        input), becomes a worker-process source chained with that operator — each worker
+        produces its own share of the records where they are consumed, instead of the
+        coordinator producing every record and copying it across (a rebalance between
+        equal-parallelism splits becomes forward: each split's records stay with their
+        worker, which is the even distribution rebalance asks for).  Returns the relocated
+        source names."""
+        if not getattr(self.env, "relocate_sources", True) or self.world_size > 1:
+            return []
+        consumers: dict[str, list] = {}
+        for n in nodes:
+            for i, (up, part, side_tag) in enumerate(n.inputs):
+                consumers.setdefault(up.uid, []).append((n, i, part, side_tag))
+        moved = []
+        for src in nodes:
+            fn = getattr(src, "source_fn", None)
+            if not src.is_source or getattr(src, "remote", False) or not getattr(fn, "relocatable", False):
+                continue
+            path = [src]  # src -> [rebalance pass-through] -> worker operator
+            ok = True
+            while ok:
+                cs = consumers.get(path[-1].uid, [])
+                if len(cs) != 1:
+                    ok = False
+                    break
+                dst, i, part, side_tag = cs[0]
+                ok = (side_tag is None and len(dst.inputs) == 1 and dst.parallelism == src.parallelism
+                      and part.kind in ("forward", "rebalance") and getattr(dst, "chaining", True)
+                      and not getattr(dst, "chain_head", False))
+                if not ok:
+                    break
+                path.append(dst)
+                if getattr(dst, "remote", False):
+                    break
+                if getattr(dst, "passthrough", None) != "rebalance":
+                    ok = False
+            if not ok or not getattr(path[-1], "remote", False):
+                continue
+            for a, b in zip(path, path[1:]):  # forward edges, every hop in the worker
+                up, part, side_tag = b.inputs[0]
+                if part.kind != "forward":
+                    b.inputs[0] = (up, Partitioner("forward"), side_tag)
+                a.remote = True
+            src.relocated = True
+            moved.append(src.name)
+        return moved
 
     def _remote_source_chains(self, nodes) -> dict:
         """Worker-process sources: the downstream worker operators they run together with

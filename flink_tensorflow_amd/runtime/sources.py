@@ -73,7 +73,12 @@ class CollectionSource(SourceFunction, CheckpointedFunction):
 
 
 class GeneratorSource(SourceFunction, CheckpointedFunction):
-    """Records from ``factory(subtask_index, parallelism, start_offset)`` (an iterator)."""
+    """Records from ``factory(subtask_index, parallelism, start_offset)`` (an iterator).
+
+    Relocatable: a subtask's records depend only on its index, so the subtask can run in
+    whichever process consumes them (``LocalExecutor._relocate_sources``)."""
+
+    relocatable = True
 
     def __init__(self, factory: Callable[[int, int, int], Iterable], limit: int | None = None):
         super().__init__()

@@ -84,6 +84,11 @@ class StreamExecutionEnvironment:
         self.chaining = True
         # one communicator per worker-process GPU operator (runtime/remote.py): "auto" forms it
         # when the operator runs P > 1 subtasks and the node has >= P GPUs; True also for P = 1
+        # a splittable source (GeneratorSource: each subtask generates its own share) whose only
+        # consumer is a worker-process operator of equal parallelism runs INSIDE the workers,
+        # chained with it, instead of producing in the coordinator and shipping every record
+        # across (executor.py ``_relocate_sources``)
+        self.relocate_sources = True
         self.job_communicator: bool | str = "auto"
         self.test_communicator = None  # test-only injection (parallel/fake.py), never set by product code
         from ..parallel.comm import world
@@ -143,6 +148,7 @@ class StreamExecutionEnvironment:
             return Operator(clone_function(proto), name)
 
         node = _Node(name, factory, parallelism or self.parallelism, is_source=True)
+        node.source_fn = proto  # inspected by the executor (worker-local source relocation)
         self.nodes.append(node)
         return DataStream(self, node)
 
@@ -231,7 +237,9 @@ class DataStream:
 
     # ---- partitioning
     def _repartition(self, kind: str) -> "DataStream":
-        return self._add(kind, lambda: UnionOperator(None, kind), partitioner=Partitioner(kind))
+        ds = self._add(kind, lambda: UnionOperator(None, kind), partitioner=Partitioner(kind))
+        ds.node.passthrough = kind  # a pass-through node that only repartitions
+        return ds
 
     def rebalance(self):
         return self._repartition("rebalance")

@@ -442,3 +442,35 @@ def test_worker_source_chain_binds_gpu_member_device():
     assert len(out) == 20
     for sub, dev, want, cur in out:
         assert dev == want and dev.endswith(":" + cur), (sub, dev, want, cur)
+
+
+def _pid_records(n):
+    def gen(idx, par, start):
+        import os as _os
+
+        for i in [i for i in range(n) if i % par == idx][start:]:
+            yield (_os.getpid(), i)
+    return gen
+
+
+def test_splittable_source_relocates_into_its_worker_consumer():
+    """A generator source feeding (rebalance) a worker-process map of equal parallelism runs
+    inside the workers, chained with the map: every record is produced in the process that
+    maps it, none crosses the coordinator.  ``relocate_sources = False`` keeps the old
+    layout (produced in the coordinator, shipped to the workers)."""
+    from flink_tensorflow_amd.runtime.executor import LocalExecutor
+
+    for relocate in (True, False):
+        env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+        env.relocate_sources = relocate
+        sink = env.generate(_pid_records(300)).rebalance().map(lambda r: (r[0], os.getpid(), r[1])) \
+            .run_in_processes().collect_into()
+        ex = LocalExecutor(env, "relocate")
+        ex.execute()
+        out = sink.results()
+        assert sorted(v for _, _, v in out) == list(range(300))
+        if relocate:
+            assert ex.relocated == ["generator"]
+            assert all(src == mapper != os.getpid() for src, mapper, _ in out)
+        else:
+            assert ex.relocated == [] and {src for src, _, _ in out} == {os.getpid()}
