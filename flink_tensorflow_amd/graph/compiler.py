@@ -176,9 +176,13 @@ class CompiledFunction(TransformerLowering):
         if precision not in ("bf16", "fp8"):
             raise ValueError(f"precision must be bf16 or fp8, not {precision!r}")
         from .control_flow import fold_static_control_flow
+        from .functions import has_functional_ops, lower_functional_ops
 
-        # TF1 conds on compile-time-constant predicates (an exported ``is_training`` switch
-        # left at its default) resolve before lowering: the plan is the cond-free one
+        # function calls / functional If / While inline into plain dataflow first; then TF1
+        # conds on compile-time-constant predicates (an exported ``is_training`` switch left
+        # at its default) resolve before lowering: the plan is the cond-free one
+        if has_functional_ops(graph):
+            graph = lower_functional_ops(graph)
         graph = fold_static_control_flow(graph, list(feeds), list(fetches))
         self.graph = graph
         self.arena = arena  # subtask DeviceArena (shared slab + interned weights) or None
@@ -519,6 +523,10 @@ class CompiledFunction(TransformerLowering):
             return self._lower_softmax(node)
         if op in ("Identity", "StopGradient", "Snapshot"):
             self.vals[(node.name, 0)] = self._in(node, 0)
+            return
+        if op == "IdentityN":  # e.g. an inlined function call's outputs (graph/functions.py)
+            for i in range(len(node.inputs)):
+                self.vals[(node.name, i)] = self._in(node, i)
             return
         if op == "Reshape":
             return self._lower_reshape(node)

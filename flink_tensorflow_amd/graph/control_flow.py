@@ -281,7 +281,8 @@ def run_dataflow(session, plan, feeds: dict, ctx, stats: list | None, lookup, va
             else:
                 args = st.inputs if st is not None else []
                 deref = op not in REF_INPUT_OPS
-                args = [a.read() if isinstance(a, var_ref_type) and (deref or i > 0) else a for i, a in enumerate(args)]
+                args = [a.read() if isinstance(a, var_ref_type) and not a.resource and (deref or i > 0) else a
+                        for i, a in enumerate(args)]
                 try:
                     outs = tuple(lookup(op)(ctx, node, *args))
                 except (ValueError, TypeError, KeyError, RuntimeError, NotImplementedError) as e:

@@ -76,6 +76,7 @@ class Graph:
     def __init__(self):
         self.nodes: dict[str, Node] = {}
         self.versions = None
+        self.library: dict = {}  # function name -> FunctionDef (GraphDef.library; graph/functions.py)
         self._consumers: dict[str, list[str]] | None = None
 
     # ------------------------------------------------------------------ construction
@@ -114,6 +115,9 @@ class Graph:
             self.nodes[name] = Node(name, nd.op, data, ctrl, dict(nd.attr), nd.device, nd)
         if gd.versions is not None:
             self.versions = gd.versions
+        if gd.library is not None:
+            for f in gd.library.function:
+                self.library[f.signature.name] = f
         self._consumers = None
 
     def add_node(self, node: Node) -> Node:
@@ -124,7 +128,10 @@ class Graph:
         return node
 
     def to_graph_def(self) -> GraphDef:
-        return GraphDef(node=[n.to_node_def() for n in self.nodes.values()], versions=self.versions)
+        from ..proto.messages import FunctionDefLibrary
+
+        lib = FunctionDefLibrary(function=list(self.library.values())) if self.library else None
+        return GraphDef(node=[n.to_node_def() for n in self.nodes.values()], versions=self.versions, library=lib)
 
     # ------------------------------------------------------------------ queries
     def __contains__(self, name: str) -> bool:

@@ -18,10 +18,14 @@ class FailedPreconditionError(RuntimeError):
 class VarRef:
     """A reference to a session variable (the output of VariableV2 / VarHandleOp)."""
 
-    __slots__ = ("session", "name", "dtype", "shape")
+    __slots__ = ("session", "name", "dtype", "shape", "resource")
 
-    def __init__(self, session, name, dtype, shape):
+    def __init__(self, session, name, dtype, shape, resource: bool = False):
         self.session, self.name, self.dtype, self.shape = session, name, dtype, shape
+        # a resource handle (VarHandleOp) is never read implicitly: only ReadVariableOp /
+        # Assign*VariableOp / ResourceGather touch it; pass-through ops (Identity, function
+        # arguments) forward the handle
+        self.resource = resource
 
     def read(self):
         v = self.session.variables.get(self.name)
@@ -99,7 +103,7 @@ def _variable(ctx, node):
     name = node.attr("shared_name") or node.name
     dt = node.attr("dtype")
     shape = node.shape_attr("shape")
-    return (VarRef(ctx.session, name, dt, shape),)
+    return (VarRef(ctx.session, name, dt, shape, resource=node.op == "VarHandleOp"),)
 
 
 @register("Assign")

@@ -62,7 +62,10 @@ class VariableStore(dict):
 
 class Session:
     def __init__(self, graph: Graph, device: str | torch.device | None = None):
-        self.graph = graph
+        from .functions import has_functional_ops, lower_functional_ops
+
+        # function calls / functional If / While (GraphDef.library) run as plain dataflow
+        self.graph = lower_functional_ops(graph) if has_functional_ops(graph) else graph
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.variables: VariableStore = VariableStore()
         self._const_cache: dict = {}
@@ -146,7 +149,7 @@ class Session:
                         v = values[(src, k)]
                     except KeyError:
                         raise RuntimeError(f"input {src}:{k} of {name} was not computed") from None
-                    if isinstance(v, ops_core.VarRef) and (deref or i > 0):
+                    if isinstance(v, ops_core.VarRef) and not v.resource and (deref or i > 0):
                         v = v.read()
                     args.append(v)
                 fn = lookup(node.op)

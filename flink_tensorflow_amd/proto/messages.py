@@ -154,9 +154,48 @@ class OpList(Message):
     FIELDS = [F(1, "op", "message", repeated=True, msg=OpDefRaw)]
 
 
+class ArgDef(Message):
+    """``OpDef.ArgDef``: one input / output argument of an op or function signature."""
+
+    FIELDS = [F(1, "name", "string"), F(2, "description", "string"), F(3, "type", "enum"),
+              F(4, "type_attr", "string"), F(5, "number_attr", "string"), F(6, "type_list_attr", "string"),
+              F(16, "is_ref", "bool")]
+
+
+class AttrDef(Message):
+    FIELDS = [F(1, "name", "string"), F(2, "type", "string"), F(3, "default_value", "message", msg=AttrValue)]
+
+
+class OpDef(Message):
+    """A function signature (``FunctionDef.signature``)."""
+
+    FIELDS = [F(1, "name", "string"), F(2, "input_arg", "message", repeated=True, msg=ArgDef),
+              F(3, "output_arg", "message", repeated=True, msg=ArgDef),
+              F(4, "attr", "message", repeated=True, msg=AttrDef), F(16, "is_stateful", "bool"),
+              F(20, "control_output", "string", repeated=True)]
+
+
+class FunctionDef(Message):
+    """``tensorflow/core/framework/function.proto``: a function body.  Inside it, inputs
+    name the signature's arguments (``"x"``) or node outputs as ``"node:out_arg:index"``."""
+
+    FIELDS = [F(1, "signature", "message", msg=OpDef), F(3, "node_def", "message", repeated=True, msg=NodeDef),
+              F(4, "ret", "map", value_kind="string"), F(5, "attr", "map", msg=AttrValue),
+              F(6, "control_ret", "map", value_kind="string")]
+
+
+class GradientDef(Message):
+    FIELDS = [F(1, "function_name", "string"), F(2, "gradient_func", "string")]
+
+
+class FunctionDefLibrary(Message):
+    FIELDS = [F(1, "function", "message", repeated=True, msg=FunctionDef),
+              F(2, "gradient", "message", repeated=True, msg=GradientDef)]
+
+
 class GraphDef(Message):
-    FIELDS = [F(1, "node", "message", repeated=True, msg=NodeDef), F(3, "version", "int32"),
-              F(4, "versions", "message", msg=VersionDef)]
+    FIELDS = [F(1, "node", "message", repeated=True, msg=NodeDef), F(2, "library", "message", msg=FunctionDefLibrary),
+              F(3, "version", "int32"), F(4, "versions", "message", msg=VersionDef)]
 
 
 # ----------------------------------------------------------------------------- meta graph

@@ -77,5 +77,45 @@ for t in ts:
     t.start()
 for t in ts:
     t.join()
+
+# the persistent copy pool (CopyPool in csrc/native.cpp) driven by two runner-like threads
+# at once: micro-batches of 196 KB records (above the 1 MiB single-thread cut-off) gathered
+# into staging slots in 64-record pieces with 8 helper threads each, while a third thread
+# scatters records into a slab — concurrent jobs on one pool (round-3 driver abort suspect)
+big = [np.full(196608, i % 251, dtype=np.uint8) for i in range(64)]
+errors = []
+
+
+def runner(k):
+    try:
+        slot = np.empty(64 * 196608, dtype=np.uint8)
+        for it in range(12):
+            for lo in range(0, 64, 16):
+                N.gather_into(slot.ctypes.data + lo * 196608, slot.nbytes - lo * 196608, big[lo:lo + 16], 196608, 8)
+            v = slot.reshape(64, 196608)
+            if not all(v[i, 0] == i % 251 and v[i, -1] == i % 251 for i in range(64)):
+                errors.append(f"runner {k} iteration {it}: wrong bytes")
+    except Exception as e:  # noqa: BLE001
+        errors.append(repr(e))
+
+
+def scatterer():
+    try:
+        slab = np.empty(32 * 196608, dtype=np.uint8)
+        offs = [i * 196608 for i in range(32)]
+        for it in range(12):
+            N.scatter_into(slab.ctypes.data, slab.nbytes, offs, big[:32], 4)
+            if slab[5 * 196608] != 5:
+                errors.append(f"scatter iteration {it}: wrong bytes")
+    except Exception as e:  # noqa: BLE001
+        errors.append(repr(e))
+
+
+ts = [threading.Thread(target=runner, args=(k,)) for k in range(2)] + [threading.Thread(target=scatterer)]
+for t in ts:
+    t.start()
+for t in ts:
+    t.join()
+assert not errors, errors
 print("native exercise ok")
 sys.stdout.flush()
