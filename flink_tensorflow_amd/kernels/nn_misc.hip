@@ -106,9 +106,12 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restri
 constexpr int PRE_ROW_MAX = 4096;
 constexpr int PRE_NT = 128;
 
+// ROWB: LDS bytes per staged row (1024 for sources up to 340 pixels wide: 4 KiB per
+// workgroup instead of 16 KiB, so LDS no longer caps the workgroups resident per CU).
+template <int ROWB>
 __global__ __launch_bounds__(PRE_NT) void preprocess_s2d_rows_kernel(const uint8_t* __restrict__ src,
                                                                      bf16* __restrict__ dst, PreParams q) {
-  __shared__ __attribute__((aligned(16))) uint8_t rows[4][PRE_ROW_MAX];
+  __shared__ __attribute__((aligned(16))) uint8_t rows[4][ROWB];
   const int Wo2 = (q.Wo + 1) / 2, Ho2 = (q.Ho + 1) / 2;
   const int oy2 = blockIdx.x % Ho2, b = blockIdx.x / Ho2;
   const uint8_t* img = src + (size_t)b * q.src_stride;
@@ -337,8 +340,10 @@ void preprocess_u8_to_bf16(uintptr_t src, uintptr_t dst, int B, int Hi, int Wi, 
   auto S = reinterpret_cast<const uint8_t*>(src);
   auto D = reinterpret_cast<bf16*>(dst);
   const bool rows_ok = s2d && Wi * 3 + 3 <= PRE_ROW_MAX;
-  if (rows_ok)
-    hipLaunchKernelGGL(preprocess_s2d_rows_kernel, dim3(B * ((Ho + 1) / 2)), dim3(PRE_NT), 0, s, S, D, q);
+  if (rows_ok && Wi * 3 + 3 <= 1024)
+    hipLaunchKernelGGL(preprocess_s2d_rows_kernel<1024>, dim3(B * ((Ho + 1) / 2)), dim3(PRE_NT), 0, s, S, D, q);
+  else if (rows_ok)
+    hipLaunchKernelGGL(preprocess_s2d_rows_kernel<PRE_ROW_MAX>, dim3(B * ((Ho + 1) / 2)), dim3(PRE_NT), 0, s, S, D, q);
   else if (s2d) hipLaunchKernelGGL(preprocess_kernel<1>, dim3(grid_for(work, 256)), dim3(256), 0, s, S, D, B, q);
   else hipLaunchKernelGGL(preprocess_kernel<0>, dim3(grid_for(work, 256)), dim3(256), 0, s, S, D, B, q);
   FTM_CHECK_LAUNCH();

@@ -108,7 +108,8 @@ def test_preprocess(hw_in, hw_out, half):
                                                      ((100, 120), (75, 75), False, False),  # odd: zero-filled edge
                                                      ((320, 300), (299, 299), True, False),
                                                      ((299, 299), (299, 299), False, False),  # 897-B rows
-                                                     ((64, 96), (33, 47), False, True)])
+                                                     ((64, 96), (33, 47), False, True),
+                                                     ((400, 480), (224, 224), False, False)])  # 4 KiB rows
 def test_preprocess_s2d_row_staged(hw_in, hw_out, half, align):
     """The row-staged (LDS) s2d preprocess kernel vs the fp32 host path."""
     img = torch.randint(0, 256, (4, *hw_in, 3), dtype=torch.uint8)
