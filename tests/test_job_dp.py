@@ -104,3 +104,65 @@ def test_p1_job_communicator_runs_through_rccl_gpu(tmp_path, half_plus_two):
         .execute_and_collect()
     assert out and all(o == ("RcclCommunicator", 1, "cuda:0", 1.0, 0.5) for o in out), out
     assert len(os.listdir(marks)) == 1
+
+
+class _DPTrainer:
+    """A co-process online trainer (the reference's ``AbstractCoProcessFunction`` home of
+    training) run as P worker-process subtasks of one job: full micro-batches only, so every
+    subtask takes the same number of steps (each step is collective: dense all-reduce, the
+    owner sparse exchange); at the end of input it emits a digest of its replica."""
+
+    @staticmethod
+    def make(batch):
+        from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, WideDeepTrainer
+        from flink_tensorflow_amd.runtime.model_functions import ModelCoProcessFunction
+
+        class Fn(ModelCoProcessFunction):
+            def __init__(self):
+                super().__init__(WideDeepTrainer(WideDeepConfig.tiny(), device="cpu", seed=3))
+                self.buf, self.steps = [], 0
+
+            def process_element1(self, rec, ctx, out):
+                if self.steps == 0 and not self.buf:
+                    ctx.timer_service().register_event_time_timer(float("inf"))
+                self.buf.append(rec)
+                if len(self.buf) == batch:
+                    self.model.train_step(self.buf)
+                    self.buf, self.steps = [], self.steps + 1
+
+            def process_element2(self, tick, ctx, out):
+                pass
+
+            def on_timer(self, ts, ctx, out):
+                import hashlib
+
+                from flink_tensorflow_amd.parallel import comm
+
+                m, ex = self.model.model, self.model._exchange
+                parts = [p.detach().reshape(-1) for p in m.dense_parameters()]
+                for e in (m.emb, m.wide):
+                    parts.append((ex.merge_owner_shards(e.table.data) if ex is not None else e.table.data).reshape(-1))
+                digest = hashlib.sha256(torch.cat(parts).numpy().tobytes()).hexdigest()[:16]
+                out.collect((comm.rank_size(), self.steps, digest))
+
+        return Fn()
+
+
+def test_online_training_dp_inside_one_job(tmp_path):
+    """Wide&Deep online training in a ``ModelCoProcessFunction`` with parallelism 2 in
+    worker processes: the subtasks form the job communicator (loopback here, RCCL on a
+    node), start from rank 0's weights, all-reduce dense gradients and exchange sparse rows
+    by owner — both replicas end bit-identical after training on different records."""
+    from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, synthetic_click_records
+    from flink_tensorflow_amd.parallel.fake import FakeCommunicator
+    from flink_tensorflow_amd.runtime.sources import CollectionSource
+
+    recs = synthetic_click_records(2 * 4 * 64, WideDeepConfig.tiny(), seed=11)
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    env.enable_job_communicator(True, communicator=FakeCommunicator)
+    clicks = env.add_source(CollectionSource(recs), "clicks", parallelism=1).rebalance()
+    ticks = env.add_source(CollectionSource([]), "control", parallelism=1)
+    out = clicks.connect(ticks).process(_DPTrainer.make(64)).name("trainer").run_in_processes().execute_and_collect()
+    assert sorted(o[0] for o in out) == [(0, 2), (1, 2)]
+    assert [o[1] for o in out] == [4, 4]
+    assert out[0][2] == out[1][2]
