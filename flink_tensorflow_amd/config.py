@@ -41,10 +41,6 @@ class EngineConfig:
     conv_impl: str = "lite"            # implicit-GEMM convs: lite (4-wave LDS-DMA conv_lite) | incumbent
     #                                    (register-staged igemm) | auto (probe conv_pp) | pp
     conv_lite_pointwise: bool = False  # deep-K 1x1 reduces (K >= 1024) on conv_lite instead of gemm_pp
-    # conv_lite tile of the KxK convs: 2 = 128x128 on 2 LDS stages, 4 / 5 = 256x128 (waves of
-    # 128 x 64) on 2 / 3 stages, 6 = 128x128 on 3 stages; "auto" = 256x128 where it still gives
-    # every CU two workgroups' worth of tiles, else 128x128 (kernels/conv_pp.hip)
-    conv_lite_tile: str = "2"
     sibling_conv_fusion: bool = True   # fp8: an Inception module's sibling 1x1 convs as one multi-output GEMM
     fuse_block_tails: bool = True      # ResNet block boundary: expand + next reduce in one kernel
     fuse_wide_tails: bool = False      # ... also for stage 2 (weights streamed; measured no gain)
@@ -141,8 +137,6 @@ class EngineConfig:
             raise ValueError("precision must be bf16 or fp8")
         if self.conv_impl not in ("lite", "incumbent", "auto", "pp"):
             raise ValueError("conv_impl must be lite, incumbent, auto or pp")
-        if str(self.conv_lite_tile) not in ("2", "4", "5", "6", "auto"):
-            raise ValueError("conv_lite_tile must be 2, 4, 5, 6 or auto")
         if not 0 < self.arena_fraction <= 1:
             raise ValueError("arena_fraction must be in (0, 1]")
         if self.batch_buckets and sorted(self.batch_buckets) != list(self.batch_buckets):

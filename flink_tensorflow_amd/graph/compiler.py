@@ -67,16 +67,6 @@ _BINARY = {"Add": "add", "AddV2": "add", "Sub": "sub", "Mul": "mul", "RealDiv": 
 _CONV_TUNE: dict = {}  # layer signature -> ("pp", tile, splits) | ("incumbent", None, None)
 
 
-def _lite_tile(M: int, N: int, num_cu: int = 256) -> int:
-    """conv_lite tile code for an M x N implicit GEMM (``EngineConfig.conv_lite_tile``; the
-    32-deep K-tile, code 3, measured slower: profiles/r03_conv)."""
-    t = str(_cfg().conv_lite_tile)
-    if t != "auto":
-        return int(t)
-    tiles256 = -(-M // 256) * -(-N // 128)
-    return 5 if tiles256 >= 2 * num_cu else 2
-
-
 def _time_concurrent(f1, f2, dev, reps: int = 5) -> float:
     """µs per pair of launches issued on two streams that run concurrently."""
     s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
@@ -870,7 +860,8 @@ class CompiledFunction(TransformerLowering):
             # (kernels/conv_pp.hip conv_lite): 6-24 % faster than the register-staged igemm
             # per layer and 64 KiB of LDS, so it shares a CU with the sibling lane
             cl = K.ConvPP([(tuple(xin.shape), (KHe, KWe), (sh, sw), (pt, pl), (dh, dw))], Cout, tuple(out.shape[1:3]),
-                          self.device, tile=_lite_tile(xin.shape[0] * out.shape[1] * out.shape[2], Cout))
+                          self.device, tile=2)  # tiles 3 (32-deep K) and 256x128 / 3-stage variants measured
+            # slower: profiles/r03_conv, profiles/r04_a
 
             def run(xin=xin, out=out, res_val=res_val, cl=cl, w2=w_dev.reshape(Cout, -1), b_dev=b_dev):  # noqa: F811
                 cl([xin.buf], w2, b_dev, res_val.buf if res_val is not None else None, act, out=_target(out),

@@ -150,7 +150,7 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         from ...config import current
 
         use_fused = self.fused if self.fused is not None else current().wd_fused_step
-        if comm.is_dist() and current().wd_sparse_exchange == "owner":
+        if comm.is_dist() and comm.get().size > 1 and current().wd_sparse_exchange == "owner":
             from ...parallel.sparse_exchange import OwnerSparseExchange
 
             self._exchange = OwnerSparseExchange(comm.get())

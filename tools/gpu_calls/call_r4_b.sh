@@ -1,9 +1,9 @@
-# round 4 B: per-layer ResNet-50 table (default tile vs auto), the other BASELINE models,
-# the coordinator -> 8 workers transport (relocated source vs coordinator-produced), and
-# an Inception-v3 fp8 kernel trace analysed per replay (copyBuffer origin)
+# round 4 B: the GPU suite again (after the ws=1 W&D capture fix), the per-layer ResNet-50
+# table, the other BASELINE models, the coordinator -> 8 workers transport (relocated source
+# vs coordinator-produced), and an Inception-v3 fp8 kernel trace analysed per replay
 source tools/gpu_calls/gpu_steps.sh
+step pytest_gpu 900 python -u -m pytest tests/ -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread
 step layers_rn 400 python -u tools/layer_table.py --reps 5 --out "$OUT/layers_rn.md"
-step layers_rn_auto 400 env FT_CONV_LITE_TILE=auto python -u tools/layer_table.py --reps 5 --out "$OUT/layers_rn_auto.md"
 step bench_inc 300 python -u bench.py --model inception_v3 --steps 30 --warmup 5
 step bench_inc_dyn 300 python -u bench.py --model inception_v3 --steps 30 --warmup 5 --dynamic
 step bench_bert_graph 300 python -u bench.py --model bert_graph --steps 30 --warmup 5
