@@ -22,6 +22,8 @@ LAYERS = {  # name: (H, W, Cin, Cout, k, stride)
     "s3_3x3s2": (28, 28, 256, 256, 3, 2),
     "s3_reduce": (14, 14, 1024, 256, 1, 1),
     "s2_reduce": (28, 28, 512, 128, 1, 1),
+    "s4_expand": (7, 7, 512, 2048, 1, 1, True),  # + identity residual (units 2 / 3)
+    "s1_reduce": (56, 56, 64, 64, 1, 1),
 }
 
 
@@ -36,25 +38,26 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     B = a.batch
     for name in a.layers.split(","):
-        H, W, Cin, Cout, k, s = LAYERS[name]
+        H, W, Cin, Cout, k, s, *opt = LAYERS[name]
         pad = k // 2 if s == 1 else (0 if k == 1 else 1)
         OH, OW = (H + 2 * pad - k) // s + 1, (W + 2 * pad - k) // s + 1
         x = torch.randn((B, H, W, Cin), device=dev, generator=g).to(torch.bfloat16)
         w = (torch.randn((Cout, k, k, Cin), device=dev, generator=g) * 0.05).to(torch.bfloat16)
         b = torch.zeros(Cout, device=dev)
         y = torch.empty((B, OH, OW, Cout), dtype=torch.bfloat16, device=dev)
+        res = torch.randn((B, OH, OW, Cout), device=dev, generator=g).to(torch.bfloat16) if opt and opt[0] else None
         flops = 2.0 * B * OH * OW * Cout * k * k * Cin
         for impl in a.impls.split(","):
             if impl == "igemm":
                 def fn():
-                    K.conv2d_nhwc(x, w, b, None, (s, s), (pad, pad, pad, pad), (1, 1), K.ACT_RELU, out=y)
+                    K.conv2d_nhwc(x, w, b, res, (s, s), (pad, pad, pad, pad), (1, 1), K.ACT_RELU, out=y)
             else:  # pp: the 8-wave ping-pong tiles; lite: the 4-wave 128x128 LDS-DMA tile
                 cp = K.ConvPP([((B, H, W, Cin), (k, k), (s, s), (pad, pad), (1, 1))], Cout, (OH, OW), dev,
-                              tile={"lite": 2, "lite32": 3}.get(impl, 0 if Cout >= 256 else 1))
+                              tile={"lite": 2, "lite32": 3, "lite256": 4, "lite256s3": 5, "lites3": 6, "lite8s3": 7, "lite8": 8}.get(impl, 0 if Cout >= 256 else 1))
                 w2 = w.reshape(Cout, -1)
 
                 def fn(cp=cp, w2=w2):
-                    cp([x], w2, b, None, K.ACT_RELU, out=y)
+                    cp([x], w2, b, res, K.ACT_RELU, out=y)
             fn()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -41,6 +41,7 @@ class EngineConfig:
     conv_impl: str = "lite"            # implicit-GEMM convs: lite (4-wave LDS-DMA conv_lite) | incumbent
     #                                    (register-staged igemm) | auto (probe conv_pp) | pp
     conv_lite_pointwise: bool = False  # deep-K 1x1 reduces (K >= 1024) on conv_lite instead of gemm_pp
+    conv_lite_expand: bool = False     # identity-residual 1x1 expands outside pw_res (stage 4) on conv_lite
     sibling_conv_fusion: bool = True   # fp8: an Inception module's sibling 1x1 convs as one multi-output GEMM
     fuse_block_tails: bool = True      # ResNet block boundary: expand + next reduce in one kernel
     fuse_wide_tails: bool = False      # ... also for stage 2 (weights streamed; measured no gain)
@@ -48,6 +49,13 @@ class EngineConfig:
     pw_res_kernel: bool = True         # identity-residual expand convs on the persistent kernel
     pw_dual_kernel: bool = False       # stage-2 projection+expand on the persistent dual kernel
     conv3x3c64_kernel: bool = True     # 64-channel 3x3 convs with the filter bank in LDS
+    # cache-resident batch slices: the plan's leading run of large-activation layers (every
+    # tensor >= chain_min_hw pixels per image: ResNet-50's 56x56 stage 1) runs once per slice
+    # of chain_batch images, its intermediates in slice-sized buffers that stay in the
+    # 256 MiB Infinity Cache; 0 = off
+    chain_batch: int = 0
+    chain_min_hw: int = 3136
+    chain_edge: bool = False           # ... plus the layers leaving that resolution (stride-2 readers)
     wd_fused_step: bool = True         # Wide&Deep: hand-fused GPU step instead of autograd
     # Wide&Deep under DP: "owner" = deduplicated rows to their owner rank (row % world),
     # owner-side Adagrad, updated rows back (parallel/sparse_exchange.py); "allgather" = the

@@ -357,12 +357,16 @@ class CompiledFunction(TransformerLowering):
         for k, v in (feeds or self.synthetic_feeds()).items():
             self.input_buffer(k).copy_(v)
         by_id: dict[int, float] = {}
-        for s in self.steps:
+
+        def each(s):  # a batch-slice chain step runs once per slice: max over the slices
             s.fn()
             for o in s.outputs:
                 t = _view(o)
                 if t.is_floating_point() and t.numel():
-                    by_id[id(_root(o))] = float(t.float().abs().max())
+                    k = id(_root(o))
+                    by_id[k] = max(by_id.get(k, 0.0), float(t.float().abs().max()))
+
+        self._run_range(0, len(self.steps), each)
         for v in self.vals.values():  # concat targets: max over their stride-written children
             kids = getattr(v, "_concat_children", None)
             if kids:
@@ -851,12 +855,14 @@ class CompiledFunction(TransformerLowering):
         lite = (self.device.type == "cuda" and _cfg().conv_impl == "lite" and out.qscale is None
                 and xin_shape_override is None and (xin.phys_c or Cin) == Cin and Cin % 64 == 0 and Cout % 8 == 0
                 and _coff(out) % 8 == 0 and out.dtype == torch.bfloat16 and xin.dtype == torch.bfloat16
-                and not pointwise and act in (K.ACT_NONE, K.ACT_RELU)
+                and (not pointwise or (res_val is not None and _cfg().conv_lite_expand))
+                and act in (K.ACT_NONE, K.ACT_RELU)
                 and (res_val is None or (res_val.concat_slot is None and res_val.qscale is None
                                          and tuple(res_val.shape) == tuple(out.shape) and res_val.alias_of is None))
                 and max(pt, pb) < 1024 and max(pl, pr) < 1024)
         if lite:
-            # KxK convs (stage 2-4 3x3): 4-wave 128x128 implicit GEMM on two LDS-DMA stages
+            # KxK convs (stage 2-4 3x3), and with conv_lite_expand the identity-residual 1x1
+            # expands pw_res does not take (stage 4: K = 512): 4-wave 128x128 implicit GEMM on two LDS-DMA stages
             # (kernels/conv_pp.hip conv_lite): 6-24 % faster than the register-staged igemm
             # per layer and 64 KiB of LDS, so it shares a CU with the sibling lane
             cl = K.ConvPP([(tuple(xin.shape), (KHe, KWe), (sh, sw), (pt, pl), (dh, dw))], Cout, tuple(out.shape[1:3]),
@@ -1832,6 +1838,8 @@ class CompiledFunction(TransformerLowering):
             for v in s.inputs:
                 _root(v).last_use = max(_root(v).last_use, i)
         keep = {id(_root(v)) for v in fetch_vals}
+        chain = self._find_chain(keep)
+        internal = chain["internal"] if chain else {}
         owners: dict[int, Val] = {}   # buffer-owning values in order of first production
         born: dict[int, int] = {}
         for i, s in enumerate(self.steps):
@@ -1847,6 +1855,8 @@ class CompiledFunction(TransformerLowering):
             t.last_use = max([t.last_use] + [c.last_use for c in getattr(t, "_concat_children", [])])
         transient = []
         for k, t in owners.items():
+            if k in internal:
+                continue  # slice-sized buffer in the chain's own slab (below)
             if k in keep:
                 t.buf = self._persistent(_buf_shape(t), t.dtype)
             else:
@@ -1854,6 +1864,16 @@ class CompiledFunction(TransformerLowering):
         sizes = [_nbytes(_buf_shape(t), t.dtype) for t in transient]
         first = [born[id(t)] for t in transient]
         last = [max(born[id(t)], t.last_use) for t in transient]
+        if chain:
+            # a tensor the chain writes is written by its first slice pass and one it reads is
+            # read by its last: both live across the whole chain
+            i0, i1 = chain["range"]
+            for j, t in enumerate(transient):
+                if id(t) in chain["touched"]:
+                    if i0 <= first[j] < i1:
+                        first[j] = i0
+                    if last[j] >= i0:
+                        last[j] = max(last[j], i1 - 1)
         offs, total = plan_offsets(sizes, first, last)
         self.activation_bytes = total
         slab = self.arena.shared_slab(total) if self.arena is not None else \
@@ -1861,17 +1881,151 @@ class CompiledFunction(TransformerLowering):
         for t, off, nb, lu in zip(transient, offs, sizes, last):
             t.buf = slab[off:off + nb].view(t.dtype).view(tuple(_buf_shape(t)))
             self._poison_after.setdefault(lu, []).append(t.buf)
+        if chain:
+            self._bind_chain(chain, born)
         for v in self.vals.values():
             if v.alias_of is not None:
                 r = _root(v)
                 if r.buf is not None:
-                    v.buf = r.buf.view(v.shape) if r.buf.is_contiguous() else r.buf.reshape(v.shape)
+                    shape = v.shape if id(r) not in internal else (chain["batch"], *v.shape[1:])
+                    v.buf = r.buf.view(shape) if r.buf.is_contiguous() else r.buf.reshape(shape)
+        if chain:
+            self._chain = (chain["range"][0], chain["range"][1], chain["parts"], chain["batch"],
+                           [v for v in chain["vals"] if id(_root(v)) not in internal])
         self._outputs = []
         for fv in fetch_vals:
             if fv.is_const:
                 self._outputs.append(fv.const)
             else:
                 self._outputs.append(fv)
+
+    # ================================================================== batch-slice chain
+    _CHAIN_KINDS = ("conv", "gemm", "pool", "elementwise", "conv_fp8", "pool_fp8")
+
+    def _find_chain(self, keep: set) -> dict | None:
+        """The leading run of memory-bound layers that executes once per slice of
+        ``EngineConfig.chain_batch`` images instead of once over the batch (None when off
+        or nothing qualifies).
+
+        Every step of the run is per-image (convs, pools, element-wise) and every tensor it
+        touches is NHWC with at least ``chain_min_hw`` pixels per image — ResNet-50's stem
+        and 56x56 stage 1, where each tensor is 100-400 MB per 256-image batch and every
+        layer streams it from HBM.  Per slice those tensors are 13-51 MB: the values made
+        and consumed inside the run ("internal") get slice-sized buffers reused by every
+        slice, so a layer reads what the previous one just wrote from the Infinity Cache
+        (256 MiB) and a dead intermediate is overwritten there before it is written back.
+        Values entering or leaving the run keep their full buffers and are sliced."""
+        cfg = _cfg()
+        bs = int(getattr(cfg, "chain_batch", 0) or 0)
+        if bs <= 0 or self._pack is not None or not self.steps or not self.feed_names:
+            return None
+        tn = TensorName.parse(self.feed_names[0])
+        N = self.vals[(tn.name, tn.index)].shape[0] if self.vals[(tn.name, tn.index)].shape else 0
+        if not N or N % bs or N // bs < 2:
+            return None
+        min_hw = int(getattr(cfg, "chain_min_hw", 3136))
+
+        edge = bool(getattr(cfg, "chain_edge", False))
+
+        def val_ok(v):
+            if v is None or v.is_const:
+                return True
+            r = _root(v)
+            if v.rows is not None or v.concat_slot is not None or r.concat_slot is not None or r.is_const:
+                return False
+            if len(v.shape) != 4 or v.shape[0] != N:
+                return False
+            return _buf_shape(r)[0] == N
+
+        def step_ok(st):
+            vs = [v for v in list(st.inputs) + list(st.outputs) if v is not None and not v.is_const]
+            if st.kind not in self._CHAIN_KINDS or not vs or not all(val_ok(v) for v in vs):
+                return False
+            big = [v.shape[1] * v.shape[2] >= min_hw for v in vs]
+            # chain_edge: a layer reading the large resolution into a smaller one (the next
+            # stage's stride-2 conv / projection) joins too, so its large input stays internal
+            return any(big) if edge else all(big)
+
+        start = 1 if self.steps[0].kind == "preprocess" else 0  # the head runs per H2D piece
+        best, i = None, start
+        while i < len(self.steps):
+            if not step_ok(self.steps[i]):
+                i += 1
+                continue
+            j = i
+            while j < len(self.steps) and step_ok(self.steps[j]):
+                j += 1
+            if j - i >= 2 and (best is None or j - i > best[1] - best[0]):
+                best = (i, j)
+            i = j
+        if best is None:
+            return None
+        i0, i1 = best
+        vals, touched = [], set()
+        for st in self.steps[i0:i1]:
+            for v in list(st.inputs) + list(st.outputs):
+                while v is not None and not v.is_const:
+                    if all(v is not u for u in vals):
+                        vals.append(v)
+                    touched.add(id(_root(v)))
+                    v = v.alias_of
+        produced = {id(_root(o)) for st in self.steps[i0:i1] for o in st.outputs}
+        used_outside = {id(_root(v)) for k, st in enumerate(self.steps) if not i0 <= k < i1
+                        for v in list(st.inputs) + list(st.outputs) if v is not None and not v.is_const}
+        feeds = {id(_root(self.vals[(TensorName.parse(f).name, TensorName.parse(f).index)])) for f in self.feed_names}
+        internal = {}
+        for v in vals:
+            r = _root(v)
+            k = id(r)
+            if k in produced and k not in used_outside and k not in keep and k not in feeds and r.buf is None:
+                internal[k] = r
+        return {"range": (i0, i1), "batch": bs, "parts": N // bs, "vals": vals, "touched": touched,
+                "internal": internal}
+
+    def _bind_chain(self, chain: dict, born: dict):
+        """Slice-sized buffers for the chain's internal values, planned by the same liveness
+        planner over the chain's own step range (one slice's lifetime)."""
+        from ..batching.arena import plan_offsets
+
+        i0, i1 = chain["range"]
+        bs, parts = chain["batch"], chain["parts"]
+        ts = list(chain["internal"].values())
+        shapes = [(bs, *_buf_shape(t)[1:]) for t in ts]
+        sizes = [_nbytes(s, t.dtype) for s, t in zip(shapes, ts)]
+        first = [born[id(t)] - i0 for t in ts]
+        last = [max(born[id(t)], min(t.last_use, i1 - 1)) - i0 for t in ts]
+        offs, total = plan_offsets(sizes, first, last)
+        slab = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
+        for t, s, off, nb in zip(ts, shapes, offs, sizes):
+            t.buf = slab[off:off + nb].view(t.dtype).view(s)
+        self.chain_bytes = total
+        self.chain_layers = i1 - i0
+        LOG.info("batch-slice chain: steps %d-%d (%s .. %s) x %d slices of %d, %d internal values in %.1f MB",
+                 i0, i1 - 1, self.steps[i0].name, self.steps[i1 - 1].name, parts, bs, len(ts), total / 1e6)
+
+    def _run_range(self, lo: int, hi: int, each=None):
+        """Launches steps[lo:hi] (``each(step)`` instead of ``step.fn()`` if given), the
+        batch-slice chain once per slice."""
+        each = each or (lambda st: st.fn())
+        ch = getattr(self, "_chain", None)
+        i = lo
+        while i < hi:
+            if ch is not None and i == ch[0] and ch[1] <= hi:
+                i0, i1, parts, bs, ext = ch
+                full = [(v, v.buf) for v in ext if v.buf is not None]
+                try:
+                    for p in range(parts):
+                        for v, b in full:
+                            v.buf = b[p * bs:(p + 1) * bs]
+                        for st in self.steps[i0:i1]:
+                            each(st)
+                finally:
+                    for v, b in full:
+                        v.buf = b
+                i = i1
+                continue
+            each(self.steps[i])
+            i += 1
 
     def _persistent(self, shape, dtype) -> torch.Tensor:
         """A buffer outside the shared slab (plan inputs, fetched outputs)."""
@@ -1890,20 +2044,25 @@ class CompiledFunction(TransformerLowering):
     # ================================================================== execution
     def _run_steps(self):
         if not (self._debug_sync or self._poison_after and tracing.debug_poison()):
-            for s in self.steps:
-                s.fn()
+            self._run_range(0, len(self.steps))
             return
         poison = tracing.debug_poison()
-        for i, s in enumerate(self.steps):
+        index = {id(s): i for i, s in enumerate(self.steps)}
+        ch = getattr(self, "_chain", None)
+
+        def each(s):
+            i = index[id(s)]
             s.fn()
             if self._debug_sync and self.device.type == "cuda":
                 try:
                     torch.cuda.synchronize(self.device)
                 except RuntimeError as e:
                     raise RuntimeError(f"step {i} ({s.kind} {s.name}) failed: {e}") from e
-            if poison:
+            if poison and not (ch is not None and ch[0] <= i < ch[1]):  # chain buffers: live per slice
                 for b in self._poison_after.get(i, ()):
                     b.view(-1).view(torch.uint8).fill_(0xFF)  # NaN in bf16/fp32, 0xFF in e4m3 = NaN
+
+        self._run_range(0, len(self.steps), each)
 
     def profile(self, feeds: dict | None = None):
         """One eager run with a HIP event pair around every launch: a ``RunMetadata``
@@ -1914,22 +2073,31 @@ class CompiledFunction(TransformerLowering):
         for k, v in (feeds or {}).items():
             self.input_buffer(k).copy_(v)
         stats = []
+        index = {id(s): i for i, s in enumerate(self.steps)}
         if self.device.type == "cuda":
-            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in self.steps]
-            for s, (e0, e1) in zip(self.steps, evs):
+            evs = [[] for _ in self.steps]  # a chain step launches once per batch slice
+
+            def each(s):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 s.fn()
                 e1.record()
+                evs[index[id(s)]].append((e0, e1))
+
+            self._run_range(0, len(self.steps), each)
             torch.cuda.synchronize(self.device)
-            times = [e0.elapsed_time(e1) * 1e3 for e0, e1 in evs]
+            times = [sum(e0.elapsed_time(e1) * 1e3 for e0, e1 in ev) for ev in evs]
         else:
             import time
 
-            times = []
-            for s in self.steps:
+            times = [0.0] * len(self.steps)
+
+            def each(s):
                 t0 = time.perf_counter()
                 s.fn()
-                times.append((time.perf_counter() - t0) * 1e6)
+                times[index[id(s)]] += (time.perf_counter() - t0) * 1e6
+
+            self._run_range(0, len(self.steps), each)
         t = 0
         for s, us in zip(self.steps, times):
             stats.append(NodeExecStats(node_name=s.name, all_start_micros=int(t), op_end_rel_micros=int(us),
@@ -1957,8 +2125,7 @@ class CompiledFunction(TransformerLowering):
                 # the tail graph shares the full graph's private memory pool
                 gt = torch.cuda.CUDAGraph()
                 with tracing.graph_capture(gt, pool=g.pool()):
-                    for st in self.steps[1:]:
-                        st.fn()
+                    self._run_range(1, len(self.steps))
                 self._graph_tail = gt
 
     def _head_feed_step(self):

@@ -14,6 +14,7 @@ stream, so the ops are hipGraph-capturable.
 """
 from __future__ import annotations
 
+import copy
 import os
 
 import torch
@@ -587,21 +588,39 @@ class ConvPP:
         self.tile = conv_pp_tile(Cout) if tile is None else tile
         if self.tile == 3 and len(self.srcs) != 1:
             raise ValueError("conv_pp: the 32-deep 4-wave tile takes one source")
-        if self.tile == 2 and len(self.srcs) == 2:
+        if self.tile in (2, 4, 5, 6, 7, 8) and len(self.srcs) == 2:
             (xs1, k1, st1, pd1, dl1) = self.srcs[1]
             if tuple(k1) != (1, 1) or tuple(pd1) != (0, 0) or (self.OH - 1) * st1[0] >= xs1[1] \
                     or (self.OW - 1) * st1[1] >= xs1[2]:
                 raise ValueError("conv_pp: the 4-wave tile's second source must be 1x1, unpadded, in range")
-        self.splits = (1 if self.tile in (2, 3) else conv_pp_splits(self.M, Cout, self.K, self.tile)) if splits is None \
+        self.splits = (1 if self.tile in (2, 3, 4, 5, 6, 7, 8) else conv_pp_splits(self.M, Cout, self.K, self.tile)) if splits is None \
             else splits
         self.ktab = conv_pp_ktab([(xs[1], xs[2], xs[3], k[0], k[1], dl[0], dl[1])
                                   for xs, k, _, _, dl in self.srcs]).to(device)
         self.ws = (torch.empty(self.splits * self.M * Cout, dtype=torch.float32, device=device)
                    if self.splits > 1 else None)
 
+    def for_batch(self, n: int) -> "ConvPP":
+        """The same convolution planned for ``n`` images (a batch slice: the compiler's
+        batch-slice chain); shares the K-tile table and the split-K workspace."""
+        if n == self.N:
+            return self
+        subs = self.__dict__.setdefault("_subs", {})
+        sub = subs.get(n)
+        if sub is None:
+            sub = copy.copy(self)
+            sub.srcs = [((n, *xs[1:]), k, st, pd, dl) for xs, k, st, pd, dl in self.srcs]
+            sub.N, sub.M, sub._subs = n, n * self.OH * self.OW, {}
+            if n > self.N:
+                raise ValueError("conv_pp: a batch slice larger than the planned batch")
+            subs[n] = sub
+        return sub
+
     def __call__(self, xs, w, bias=None, residual=None, act=None, out=None, out_channel_offset: int = 0):
         if len(xs) != len(self.srcs):
             raise ValueError("conv_pp: source count")
+        if xs and xs[0].dim() == 4 and xs[0].shape[0] != self.N:
+            return self.for_batch(int(xs[0].shape[0]))(xs, w, bias, residual, act, out, out_channel_offset)
         for x, (shape, *_r) in zip(xs, self.srcs):
             if tuple(x.shape) != shape:
                 raise ValueError(f"conv_pp: input shape {tuple(x.shape)} != planned {shape}")
