@@ -41,7 +41,6 @@ class EngineConfig:
     conv_impl: str = "lite"            # implicit-GEMM convs: lite (4-wave LDS-DMA conv_lite) | incumbent
     #                                    (register-staged igemm) | auto (probe conv_pp) | pp
     conv_lite_pointwise: bool = False  # deep-K 1x1 reduces (K >= 1024) on conv_lite instead of gemm_pp
-    conv_lite_expand: bool = False     # identity-residual 1x1 expands outside pw_res (stage 4) on conv_lite
     sibling_conv_fusion: bool = True   # fp8: an Inception module's sibling 1x1 convs as one multi-output GEMM
     fp8_lite_wide: int = 0             # fp8 convs with >= this many 256-pixel workgroups on the 8-wave tile; 0 = off
     fuse_block_tails: bool = True      # ResNet block boundary: expand + next reduce in one kernel

@@ -855,19 +855,17 @@ class CompiledFunction(TransformerLowering):
         lite = (self.device.type == "cuda" and _cfg().conv_impl == "lite" and out.qscale is None
                 and xin_shape_override is None and (xin.phys_c or Cin) == Cin and Cin % 64 == 0 and Cout % 8 == 0
                 and _coff(out) % 8 == 0 and out.dtype == torch.bfloat16 and xin.dtype == torch.bfloat16
-                and (not pointwise or (res_val is not None and _cfg().conv_lite_expand))
-                and act in (K.ACT_NONE, K.ACT_RELU)
+                and not pointwise and act in (K.ACT_NONE, K.ACT_RELU)
                 and (res_val is None or (res_val.concat_slot is None and res_val.qscale is None
                                          and tuple(res_val.shape) == tuple(out.shape) and res_val.alias_of is None))
                 and max(pt, pb) < 1024 and max(pl, pr) < 1024)
         if lite:
-            # KxK convs (stage 2-4 3x3), and with conv_lite_expand the identity-residual 1x1
-            # expands pw_res does not take (stage 4: K = 512): 4-wave 128x128 implicit GEMM on two LDS-DMA stages
+            # KxK convs (stage 2-4 3x3): 4-wave 128x128 implicit GEMM on two LDS-DMA stages
             # (kernels/conv_pp.hip conv_lite): 6-24 % faster than the register-staged igemm
             # per layer and 64 KiB of LDS, so it shares a CU with the sibling lane
             cl = K.ConvPP([(tuple(xin.shape), (KHe, KWe), (sh, sw), (pt, pl), (dh, dw))], Cout, tuple(out.shape[1:3]),
-                          self.device, tile=2)  # tiles 3 (32-deep K) and 256x128 / 3-stage variants measured
-            # slower: profiles/r03_conv, profiles/r04_a
+                          self.device, tile=2)  # tiles 3 (32-deep K), 256x128 (4 or 8 waves) and 3-stage
+            # variants (raw-barrier, counted vmcnt) measured slower: profiles/r03_conv, r04_a, r04_c
 
             def run(xin=xin, out=out, res_val=res_val, cl=cl, w2=w_dev.reshape(Cout, -1), b_dev=b_dev):  # noqa: F811
                 cl([xin.buf], w2, b_dev, res_val.buf if res_val is not None else None, act, out=_target(out),

@@ -399,36 +399,20 @@ FTM_DEVICE int lite_slot(int row, int chunk) {
 // DUAL: a second, pointwise and unpadded source (the strided projection input of a ResNet
 // block's first expand: y = x W_e + x2[::s] W_p in one K loop); its K-tiles follow source
 // 0's, the weight rows are [W_e | W_p].
-// WM: output pixels per wave.  64: the 128x128 tile (2 x 2 waves of 64 x 64, 2 x 32 KiB
-// stages, two workgroups per CU).  128: a 256x128 tile (2 x 2 waves of 128 x 64, 2 x 48 KiB
-// stages, one workgroup per CU) — each wave reads 12 fragments per 32 MFMAs from LDS instead
-// of 8 per 16, so the LDS array (reads + DMA fills) carries 25 % less per MFMA.
-// NST: LDS stages.  2: one K-tile in flight behind the one being consumed; 3: two (the
-// DMA of tile t+2 is issued while tile t is consumed; each wave waits only for its own
-// pieces of tile t: a counted vmcnt).
-// WGM: waves along the pixel dimension (2: four waves; 4: eight waves, a 256x128 tile of
-// 64 x 64 wave tiles at one workgroup per CU with two waves per SIMD).
-template <int ACT, bool HAS_RES, int BK, bool DUAL = false, int WM = 64, int NST = 2, int WGM = 2>
-__global__ __launch_bounds__(WGM * 128, (WM == 64 && NST == 2 && WGM == 2 ? 2 : 1)) void conv_lite_kernel(CPParams p) {
-  // BK = 64: 128-B LDS rows, 2 MFMA steps per K-tile.
+template <int ACT, bool HAS_RES, int BK, bool DUAL = false>
+__global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
+  // BK = 64: 128-B LDS rows, 2 x 32 KiB stages, 2 MFMA steps per K-tile.
   // BK = 32: 64-B rows, 2 x 16 KiB stages (the igemm's footprint: four workgroups per CU),
   //          1 MFMA step per K-tile; 16-B chunk slot = chunk ^ ((row >> 2) & 3) keeps the
   //          16-lane ds_read_b128 groups on distinct banks.
-  constexpr int NT = WGM * 128;            // threads (2 * WGM waves)
-  constexpr int NW = 2 * WGM;
-  constexpr int BM = WGM * WM, BN = 128;
-  constexpr int NJ = WM / 16;              // pixel fragments per wave
+  constexpr int BM = 128, BN = 128;
   constexpr int ROWB = BK * 2;             // LDS row bytes
   constexpr int CPR = ROWB / 16;           // 16-B chunks per row
   constexpr int RPI = 1024 / ROWB;         // rows per DMA wave-instruction
-  constexpr int QX = BM / RPI / NW;        // DMA instructions per wave for the X (pixel) image
-  constexpr int QW = BN / RPI / NW;        // ... for the W (channel) image
-  static_assert(QX <= 8 && QW <= 4 && QW <= QX && QW >= 1, "DMA role arrays");
+  constexpr int QX = BM / RPI / 4;         // DMA instructions per wave per operand
   constexpr int XB = BM * ROWB, WB = BN * ROWB, STG = XB + WB;
   constexpr int OPITCH = BN * 2 + 16;
-  constexpr int LDS = NST * STG > BM * OPITCH ? NST * STG : BM * OPITCH;
-  static_assert(LDS <= 160 * 1024, "LDS budget");
-  constexpr int PER_TILE = QX + QW;  // DMA wave-instructions per K-tile (vmcnt accounting)
+  constexpr int LDS = 2 * STG > BM * OPITCH ? 2 * STG : BM * OPITCH;
   __shared__ __attribute__((aligned(1024))) uint8_t smem[LDS];
 
   const int nwg = p.tiles_m * p.tiles_n;
@@ -439,8 +423,8 @@ __global__ __launch_bounds__(WGM * 128, (WM == 64 && NST == 2 && WGM == 2 ? 2 : 
   const int n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave % WGM;  // pixel slice of the tile
-  const int wn = wave / WGM;  // channel half
+  const int wm = wave & 1;   // pixel half of the tile
+  const int wn = wave >> 1;  // channel half
 
   // DMA roles: wave w stages image rows RPI * (QX w + q) + lane / CPR of both the X (pixel)
   // and W (channel) images; the lane's 16-B chunk is pre-swizzled on the source
@@ -452,9 +436,9 @@ __global__ __launch_bounds__(WGM * 128, (WM == 64 && NST == 2 && WGM == 2 ? 2 : 
       (void*)S.x, 0, (int)(nimg * (unsigned)(S.H * S.W) * (unsigned)S.C * 2u), 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)p.w, 0, (int)((unsigned)p.N * (unsigned)p.ldw * 2u), 0x00020000);
-  // fixed-size (QX <= 8, QW <= 4): arrays sized by the template-dependent QX made hipcc's
-  // host pass drop the kernel by SFINAE (an undefined device stub at load time)
-  int pb[8], hw[8], pb1[8];
+  // fixed-size (QX <= 4): arrays sized by the template-dependent QX made hipcc's host pass
+  // drop the kernel by SFINAE (an undefined device stub at load time)
+  int pb[4], hw[4], pb1[4];
   unsigned offw[4];
   const CSrc& S1 = p.s[1];
   __amdgpu_buffer_rsrc_t rx1 = rx;
@@ -476,10 +460,7 @@ __global__ __launch_bounds__(WGM * 128, (WM == 64 && NST == 2 && WGM == 2 ? 2 : 
     pb[q] = ((n * S.H + ih0) * S.W + iw0) * S.C * 2 + dchunk * 16;
     hw[q] = (ih0 << 16) | (iw0 & 0xFFFF);
     if constexpr (DUAL) pb1[q] = live ? ((n * S1.H + oh * S1.sh) * S1.W + ow * S1.sw) * S1.C * 2 + dchunk * 16 : -1;
-  }
-#pragma unroll
-  for (int q = 0; q < QW; ++q) {
-    const unsigned co = n0 + RPI * (QW * wave + q) + drow;
+    const unsigned co = n0 + r;
     offw[q] = co < (unsigned)p.N ? (co * p.ldw + dchunk * 8) * 2u : 0x80000000u;
   }
   // The K walk (channel chunk, filter column, filter row) advances incrementally in scalar
@@ -494,15 +475,14 @@ __global__ __launch_bounds__(WGM * 128, (WM == 64 && NST == 2 && WGM == 2 ? 2 : 
         const int delta1 = (kt_dma - p.nk0) * BK * 2;
         ++kt_dma;
         uint8_t* bx = smem + stage * STG + QX * wave * RPI * ROWB;
-        uint8_t* bw = smem + stage * STG + XB + QW * wave * RPI * ROWB;
+        uint8_t* bw = bx + XB;
 #pragma unroll
-        for (int q = 0; q < QX; ++q)
+        for (int q = 0; q < QX; ++q) {
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rx1, (__attribute__((address_space(3))) void*)(bx + q * 1024), 16,
                                                    pb1[q] >= 0 ? (unsigned)(pb1[q] + delta1) : 0x80000000u, 0, 0, 0);
-#pragma unroll
-        for (int q = 0; q < QW; ++q)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 1024), 16,
                                                    offw[q], woff, 0, 0);
+        }
         return;
       }
     }
@@ -517,7 +497,7 @@ __global__ __launch_bounds__(WGM * 128, (WM == 64 && NST == 2 && WGM == 2 ? 2 : 
       }
     }
     uint8_t* bx = smem + stage * STG + QX * wave * RPI * ROWB;
-    uint8_t* bw = smem + stage * STG + XB + QW * wave * RPI * ROWB;
+    uint8_t* bw = bx + XB;
 #pragma unroll
     for (int q = 0; q < QX; ++q) {
       const int ih = (hw[q] >> 16) + dih;
@@ -525,60 +505,43 @@ __global__ __launch_bounds__(WGM * 128, (WM == 64 && NST == 2 && WGM == 2 ? 2 : 
       const bool ok = (unsigned)ih < (unsigned)S.H && (unsigned)iw < (unsigned)S.W;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(bx + q * 1024), 16,
                                                ok ? (unsigned)(pb[q] + delta) : 0x80000000u, 0, 0, 0);
-      if (q < QW)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 1024), 16,
-                                                 offw[q], woff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 1024), 16,
+                                               offw[q], woff, 0, 0);
     }
   };
 
   const int frow = lane & 15;
   const int fq = lane >> 4;
-  f32x4 acc[4][NJ];  // [channel fragment i][pixel fragment j]
+  f32x4 acc[4][4];  // [channel fragment i][pixel fragment j]
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = p.K / BK;
   dma(0);
-  if constexpr (NST == 3) {
-    if (nk > 1) dma(1);
-  }
-  int st = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    if constexpr (NST == 3) {
-      // this wave's pieces of tile kt have landed once at most the next tile's are pending
-      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // every wave's pieces of tile kt; every wave is past tile kt-1's reads.  A raw
-      // s_barrier: __syncthreads()'s fence would wait vmcnt(0) and drain tile kt+1's DMA
-      // (an LDS-DMA is a pending LDS write on the VM counter), undoing the third stage
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      CP_BARRIER();
-      if (kt + 2 < nk) dma(st == 0 ? 2 : st - 1);
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (kt + 1 < nk) dma(st ^ 1);
-    }
+    const int st = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) dma(st ^ 1);
     const uint8_t* xs = smem + st * STG;
     const uint8_t* ws = xs + XB;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       const int sl = lite_slot<CPR>(frow, ks * 4 + fq) << 4;
-      bf16x8 a[4], b[NJ];
+      bf16x8 a[4], b[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ws + (wn * 64 + i * 16 + frow) * ROWB + sl);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(xs + (wm * WM + j * 16 + frow) * ROWB + sl);
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(xs + (wm * 64 + j * 16 + frow) * ROWB + sl);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_s_setprio(0);
-    st = NST == 3 ? (st == 2 ? 0 : st + 1) : (st ^ 1);
   }
   __syncthreads();  // every wave is done with the stage images: the epilogue tile reuses them
 
@@ -588,8 +551,8 @@ __global__ __launch_bounds__(WGM * 128, (WM == 64 && NST == 2 && WGM == 2 ? 2 : 
     f32x4 bv = {0.f, 0.f, 0.f, 0.f};
     if (p.bias && n0 + cl < p.N) bv = *reinterpret_cast<const f32x4*>(p.bias + n0 + cl);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int pl = wm * WM + j * 16 + frow;
+    for (int j = 0; j < 4; ++j) {
+      const int pl = wm * 64 + j * 16 + frow;
       bf16x4 o;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -604,7 +567,7 @@ __global__ __launch_bounds__(WGM * 128, (WM == 64 && NST == 2 && WGM == 2 ? 2 : 
   bf16* y = reinterpret_cast<bf16*>(p.y);
   constexpr int SEGS = BN / 8;
 #pragma unroll 4
-  for (int q = threadIdx.x; q < BM * SEGS; q += NT) {
+  for (int q = threadIdx.x; q < BM * SEGS; q += 256) {
     const int ml = q / SEGS;
     const int ccol = q - ml * SEGS;
     const int m = m0 + ml;
@@ -622,19 +585,19 @@ __global__ __launch_bounds__(WGM * 128, (WM == 64 && NST == 2 && WGM == 2 ? 2 : 
   }
 }
 
-// lite_bk: 64 (tile 2 / 4) or 32 (tile 3); WM 64 (128x128 tile) or 128 (256x128, tile 4)
-template <int ACT, int BK, int WM = 64, int NST = 2, int WGM = 2>
+// lite_bk: 64 (tile 2) or 32 (tile 3)
+template <int ACT, int BK>
 void launch_lite(const CPParams& p, hipStream_t s, bool dual = false) {
-  const dim3 grid(p.tiles_m * p.tiles_n), block(WGM * 128);
+  const dim3 grid(p.tiles_m * p.tiles_n), block(256);
   if constexpr (BK == 64) {
     if (dual) {
-      if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, BK, true, WM, NST, WGM>), grid, block, 0, s, p);
-      else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, BK, true, WM, NST, WGM>), grid, block, 0, s, p);
+      if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, BK, true>), grid, block, 0, s, p);
+      else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, BK, true>), grid, block, 0, s, p);
       return;
     }
   }
-  if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, BK, false, WM, NST, WGM>), grid, block, 0, s, p);
-  else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, BK, false, WM, NST, WGM>), grid, block, 0, s, p);
+  if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, BK>), grid, block, 0, s, p);
+  else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, BK>), grid, block, 0, s, p);
 }
 
 template <int ACT, bool HAS_RES>
@@ -748,7 +711,7 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
       p.dh = dh;
       p.dw = dw;
       p.nk0 = (int)(K / 64);
-    } else if (tile == 2 || tile >= 4) {  // conv_lite's second source: pointwise, unpadded, in range
+    } else if (tile == 2) {  // conv_lite's second source: pointwise, unpadded, in range
       need(KH == 1 && KW == 1 && S.ph == 0 && S.pw == 0, "the 4-wave tile's second source must be 1x1 unpadded");
       need((OH - 1) * S.sh < S.H && (OW - 1) * S.sw < S.W, "second source smaller than the output grid");
     }
@@ -768,14 +731,11 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   p.K = (int)K;
   p.OH = OH; p.OW = OW;
   p.ldw = (int)K; p.ldy = ldy; p.y_coff = y_coff; p.ldr = ldr;
-  need(tile >= 0 && tile <= 8,
-       "tile must be 0 (256x256), 1 (512x128), 2 / 3 (128x128, 4 waves, K-tile 64 / 32), 4 / 5 (256x128, 4 waves, "
-       "2 / 3 LDS stages), 6 (128x128, 3 stages), 7 / 8 (256x128, 8 waves, 3 / 2 stages)");
+  need(tile >= 0 && tile <= 3, "tile must be 0 (256x256), 1 (512x128), 2 / 3 (128x128, 4 waves, K-tile 64 / 32)");
   const bool lite = tile >= 2;
-  need(!lite || ((ns == 1 || tile != 3) && splits <= 1), "the 4-wave tiles take no split-K (two sources: tile 2 / 4)");
+  need(!lite || ((ns == 1 || tile == 2) && splits <= 1), "the 4-wave tile takes no split-K (two sources: tile 2)");
   need(tile != 3 || p.s[0].C % 32 == 0, "the 32-deep 4-wave tile needs Cin % 32 == 0");
-  const int BM = tile == 1 ? 512 : (tile == 4 || tile == 5 || tile >= 7) ? 256 : lite ? 128 : 256,
-            BN = tile == 1 ? 128 : lite ? 128 : 256;
+  const int BM = tile == 1 ? 512 : lite ? 128 : 256, BN = tile == 1 ? 128 : lite ? 128 : 256;
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (Cout + BN - 1) / BN;
   const int nk = p.K / 64;
@@ -789,25 +749,7 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   float* wsp = reinterpret_cast<float*>(ws);
-  if (tile >= 4) {
-    need(act == ACT_NONE || act == ACT_RELU, "unsupported activation");
-    if (tile == 4) {
-      if (act == ACT_NONE) launch_lite<ACT_NONE, 64, 128>(p, s, ns == 2);
-      else launch_lite<ACT_RELU, 64, 128>(p, s, ns == 2);
-    } else if (tile == 5) {
-      if (act == ACT_NONE) launch_lite<ACT_NONE, 64, 128, 3>(p, s, ns == 2);
-      else launch_lite<ACT_RELU, 64, 128, 3>(p, s, ns == 2);
-    } else if (tile == 6) {
-      if (act == ACT_NONE) launch_lite<ACT_NONE, 64, 64, 3>(p, s, ns == 2);
-      else launch_lite<ACT_RELU, 64, 64, 3>(p, s, ns == 2);
-    } else if (tile == 7) {
-      if (act == ACT_NONE) launch_lite<ACT_NONE, 64, 64, 3, 4>(p, s, ns == 2);
-      else launch_lite<ACT_RELU, 64, 64, 3, 4>(p, s, ns == 2);
-    } else {
-      if (act == ACT_NONE) launch_lite<ACT_NONE, 64, 64, 2, 4>(p, s, ns == 2);
-      else launch_lite<ACT_RELU, 64, 64, 2, 4>(p, s, ns == 2);
-    }
-  } else if (lite) {
+  if (lite) {
     switch (act * 2 + (tile == 3)) {
       case ACT_NONE * 2: launch_lite<ACT_NONE, 64>(p, s, ns == 2); break;
       case ACT_NONE * 2 + 1: launch_lite<ACT_NONE, 32>(p, s); break;

@@ -58,27 +58,6 @@ CASES = [
     ("lite32_3x3s2", [((3, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 3, None),
     ("lite32_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (7, 7), True, "relu", 3, None),
     ("lite32_1x1", [((2, 14, 14, 256), (1, 1), (1, 1), (0, 0), (1, 1))], 1024, (14, 14), True, None, 3, None),
-    # the 4-wave 256x128 tile (waves of 128 x 64): 3x3 s1 / s2, M / N tails, residual, dual
-    ("lite256_3x3", [((4, 28, 28, 128), (3, 3), (1, 1), (1, 1), (1, 1))], 128, (28, 28), False, "relu", 4, None),
-    ("lite256_3x3s2", [((3, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 4, None),
-    ("lite256_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (7, 7), True, "relu", 4, None),
-    ("lite256_dual", [((2, 14, 14, 128), (1, 1), (1, 1), (0, 0), (1, 1)),
-                      ((2, 28, 28, 256), (1, 1), (2, 2), (0, 0), (1, 1))], 512, (14, 14), False, "relu", 4, None),
-    # three LDS stages: 256x128 (tile 5) and 128x128 (tile 6); K of one tile only (1x1, C=64)
-    ("lite256s3_3x3", [((4, 28, 28, 128), (3, 3), (1, 1), (1, 1), (1, 1))], 128, (28, 28), True, "relu", 5, None),
-    ("lite256s3_k1", [((2, 14, 14, 64), (1, 1), (1, 1), (0, 0), (1, 1))], 136, (14, 14), False, None, 5, None),
-    ("lite256s3_dual", [((2, 14, 14, 128), (1, 1), (1, 1), (0, 0), (1, 1)),
-                        ((2, 28, 28, 256), (1, 1), (2, 2), (0, 0), (1, 1))], 512, (14, 14), False, "relu", 5, None),
-    ("lites3_3x3s2", [((3, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 6, None),
-    ("lites3_k2", [((2, 14, 14, 128), (1, 1), (1, 1), (0, 0), (1, 1))], 72, (14, 14), False, None, 6, None),
-    # eight waves (4 x 2 of 64 x 64) on a 256x128 tile: three (tile 7) / two (tile 8) stages
-    ("lite8s3_3x3", [((4, 28, 28, 128), (3, 3), (1, 1), (1, 1), (1, 1))], 128, (28, 28), True, "relu", 7, None),
-    ("lite8s3_3x3s2", [((3, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 7, None),
-    ("lite8s3_k1", [((2, 14, 14, 64), (1, 1), (1, 1), (0, 0), (1, 1))], 136, (14, 14), False, None, 7, None),
-    ("lite8s3_dual", [((2, 14, 14, 128), (1, 1), (1, 1), (0, 0), (1, 1)),
-                      ((2, 28, 28, 256), (1, 1), (2, 2), (0, 0), (1, 1))], 512, (14, 14), False, "relu", 7, None),
-    ("lite8_3x3", [((4, 28, 28, 128), (3, 3), (1, 1), (1, 1), (1, 1))], 128, (28, 28), False, "relu", 8, None),
-    ("lite8_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (7, 7), True, "relu", 8, None),
 ]
 
 
