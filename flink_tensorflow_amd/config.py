@@ -42,7 +42,6 @@ class EngineConfig:
     #                                    (register-staged igemm) | auto (probe conv_pp) | pp
     conv_lite_pointwise: bool = False  # deep-K 1x1 reduces (K >= 1024) on conv_lite instead of gemm_pp
     sibling_conv_fusion: bool = True   # fp8: an Inception module's sibling 1x1 convs as one multi-output GEMM
-    fp8_lite_wide: int = 0             # fp8 convs with >= this many 256-pixel workgroups on the 8-wave tile; 0 = off
     fuse_block_tails: bool = True      # ResNet block boundary: expand + next reduce in one kernel
     fuse_wide_tails: bool = False      # ... also for stage 2 (weights streamed; measured no gain)
     decimate_tails: bool = True        # stage-1 tail output stored at the stride-2 reader's pixels

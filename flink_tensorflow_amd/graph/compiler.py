@@ -1230,23 +1230,16 @@ class CompiledFunction(TransformerLowering):
         # fp8 input: the 4-wave LDS-DMA tile (kernels/fp8.hip conv_lite_fp8, cfg 8); a bf16
         # input (the layer after the stem) is quantised on load by the register-staged kernel
         cfg = 8 if (x.qscale is not None and _cfg().conv_impl == "lite") else -1
-        wide_min = int(_cfg().fp8_lite_wide)
-        if cfg == 8 and wide_min > 0 and KH * KW * Cin > 128:
-            # the eight-wave 256-pixel tile on three LDS stages (cfg 9) where it still fills
-            # the chip: at least fp8_lite_wide workgroups (one per CU)
-            bn = min((128, 96, 64), key=lambda b: (-(-Cout // b) * b, -b))
-            M = out_nhw[0] * out_nhw[1] * out_nhw[2]
-            if bn in (128, 64) and -(-M // 256) * -(-Cout // bn) >= wide_min:
-                cfg = 9
+        # (an eight-wave 256-pixel tile on three LDS stages measured 5-40 % slower per layer
+        # and -2 % in the bench: profiles/r04_d)
 
         def run(x=x, out=out, wq=wq_dev, ws=ws_dev, cs=cs_dev, b=b_dev, x_scale=x_scale, cfg=cfg):
             F8.conv2d_nhwc_fp8(_view(x), x_scale, wq, (KH, KW), ws, b, stride, pads, dil, act,
                                out_scale=_eff_scale(out), out=_target(out), out_channel_offset=_coff(out), chan_scale=cs,
                                cfg=cfg)
 
-        self._emit(node.name, "conv_fp8", run, [x], [out],
-                   {"impl": "conv_lite_fp8" if cfg == 8 else "conv_lite_fp8_w8"} if cfg in (8, 9) else None)
-        if cfg in (8, 9):
+        self._emit(node.name, "conv_fp8", run, [x], [out], {"impl": "conv_lite_fp8"} if cfg == 8 else None)
+        if cfg == 8:
             self.conv_lite_layers = getattr(self, "conv_lite_layers", 0) + 1
         self.vals[(last.name, 0)] = out
         self._alias_fused_outputs(absorbed, out)

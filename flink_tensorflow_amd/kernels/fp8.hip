@@ -359,19 +359,12 @@ void launch_tile(const Fp8Params& p, int act, int cfg, hipStream_t s) {
 // 80, 160, 288 on 96; 320, 448, <= 64 on 64); NSTG = 1 (a single LDS stage) when the whole K fits one
 // K-tile (K <= 128: no prefetch to overlap, and half the LDS lets more workgroups hide the
 // load latency of these streaming layers).
-// WGM = 4: eight waves on a 256 x BN tile (4 x 2 waves of 64 x BN/2), one workgroup per CU
-// with two waves per SIMD; with NSTG = 3 two K-tiles are in flight behind the one being
-// consumed (counted vmcnt + a raw s_barrier: __syncthreads()'s fence would wait vmcnt(0),
-// draining the DMA of the tile after next).
-template <bool OUT_FP8, int ACT, int BN_ = 128, int NSTG = 2, bool MULTI = false, int WGM = 2>
-__global__ __launch_bounds__(WGM * 128, WGM == 2 ? 2 : 1) void conv_lite_fp8_kernel(Fp8Params p, Fp8Segs sg) {
+template <bool OUT_FP8, int ACT, int BN_ = 128, int NSTG = 2, bool MULTI = false>
+__global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8Segs sg) {
   static_assert(BN_ == 128 || BN_ == 96 || BN_ == 64, "channel tile 128, 96 or 64");
-  static_assert(WGM == 2 || (WGM == 4 && BN_ % 64 == 0), "eight waves: channel tile 128 or 64");
-  constexpr int NT = WGM * 128, NW = 2 * WGM;
-  constexpr int BM = 64 * WGM, BN = BN_;
+  constexpr int BM = 128, BN = BN_;
   constexpr int NI = BN / 32;  // weight fragments per wave (a wave covers BN / 2 channels)
-  constexpr int WQ = BN / (8 * NW);  // weight DMA rows-of-8 per wave
-  constexpr int PER_TILE = 4 + WQ;   // DMA wave-instructions per K-tile (vmcnt accounting)
+  constexpr int WQ = BN / 32;  // weight DMA rows-of-8 per wave
   constexpr int XB = BM * BK, WB = BN * BK, STG = XB + WB;
   constexpr int OB = (OUT_FP8 && !MULTI) ? 1 : 2;  // MULTI stages bf16, quantises per segment at the store
   constexpr int OLD = BN * OB + 16;
@@ -386,7 +379,7 @@ __global__ __launch_bounds__(WGM * 128, WGM == 2 ? 2 : 1) void conv_lite_fp8_ker
   const int n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave % WGM, wn = wave / WGM;
+  const int wm = wave & 1, wn = wave >> 1;
 
   const int drow = lane >> 3;
   const int dchunk = (lane & 7) ^ drow;  // this lane's logical 16-B chunk of every K-tile
@@ -467,24 +460,11 @@ __global__ __launch_bounds__(WGM * 128, WGM == 2 ? 2 : 1) void conv_lite_fp8_ker
 
   const int nk = NSTG == 1 ? 1 : (p.K + BK - 1) / BK;  // NSTG 1: the host guarantees K <= BK
   dma(0);
-  if constexpr (NSTG == 3) {
-    if (nk > 1) dma(1);
-  }
-  int st = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    if constexpr (NSTG == 3) {
-      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      if (kt + 2 < nk) dma(st == 0 ? 2 : st - 1);
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (NSTG > 1 && kt + 1 < nk) dma(st ^ 1);
-    }
+    const int st = NSTG == 1 ? 0 : (kt & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (NSTG > 1 && kt + 1 < nk) dma(st ^ 1);
     const uint8_t* xs = smem + st * STG;
     const uint8_t* ws = xs + XB;
     i32x8 a[NI], b[4];
@@ -506,7 +486,6 @@ __global__ __launch_bounds__(WGM * 128, WGM == 2 ? 2 : 1) void conv_lite_fp8_ker
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, E8M0_ONE, 0,
                                                                      E8M0_ONE);
-    st = NSTG == 3 ? (st == 2 ? 0 : st + 1) : NSTG == 2 ? (st ^ 1) : 0;
   }
   __syncthreads();  // the epilogue tile reuses the stage images
 
@@ -543,7 +522,7 @@ __global__ __launch_bounds__(WGM * 128, WGM == 2 ? 2 : 1) void conv_lite_fp8_ker
   if constexpr (MULTI) {
     constexpr int CPR16 = BN / 16;  // 16-channel chunks (32 B of the bf16 tile) per row
 #pragma unroll 2
-    for (int q = threadIdx.x; q < BM * CPR16; q += NT) {
+    for (int q = threadIdx.x; q < BM * CPR16; q += 256) {
       const int pl = q / CPR16;
       const int cc = q % CPR16;
       const int m = m0 + pl;
@@ -569,7 +548,7 @@ __global__ __launch_bounds__(WGM * 128, WGM == 2 ? 2 : 1) void conv_lite_fp8_ker
   constexpr int EPC = 16 / OB;
   constexpr int CPR = BN / EPC;
 #pragma unroll 4
-  for (int q = threadIdx.x; q < BM * CPR; q += NT) {
+  for (int q = threadIdx.x; q < BM * CPR; q += 256) {
     const int pl = q / CPR;
     const int cc = q % CPR;
     const int m = m0 + pl;
@@ -580,23 +559,18 @@ __global__ __launch_bounds__(WGM * 128, WGM == 2 ? 2 : 1) void conv_lite_fp8_ker
   }
 }
 
-template <bool OUT_FP8, int BN_, int NSTG, bool MULTI = false, int WGM = 2>
+template <bool OUT_FP8, int BN_, int NSTG, bool MULTI = false>
 void launch_lite_fp8_t(Fp8Params p, int act, hipStream_t s, const Fp8Segs& sg) {
-  constexpr int BM = 64 * WGM;
-  p.tiles_m = (p.M + BM - 1) / BM;
+  p.tiles_m = (p.M + 127) / 128;
   p.tiles_n = (p.Cout + BN_ - 1) / BN_;
-  dim3 grid(p.tiles_m * p.tiles_n), block(WGM * 128);
+  dim3 grid(p.tiles_m * p.tiles_n), block(256);
   if constexpr (MULTI) {  // the per-channel clamp replaces the activation
-    hipLaunchKernelGGL((conv_lite_fp8_kernel<false, ACT_NONE, BN_, NSTG, true, WGM>), grid, block, 0, s, p, sg);
+    hipLaunchKernelGGL((conv_lite_fp8_kernel<false, ACT_NONE, BN_, NSTG, true>), grid, block, 0, s, p, sg);
     return;
   }
   switch (act) {
-    case ACT_NONE:
-      hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_NONE, BN_, NSTG, false, WGM>), grid, block, 0, s, p, sg);
-      break;
-    case ACT_RELU:
-      hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_RELU, BN_, NSTG, false, WGM>), grid, block, 0, s, p, sg);
-      break;
+    case ACT_NONE: hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_NONE, BN_, NSTG>), grid, block, 0, s, p, sg); break;
+    case ACT_RELU: hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_RELU, BN_, NSTG>), grid, block, 0, s, p, sg); break;
     default: throw std::invalid_argument("fp8 conv_lite: activation must be none/relu");
   }
 }
@@ -613,15 +587,9 @@ int lite_fp8_bn(int Cout) {
 }
 
 template <bool OUT_FP8, bool MULTI = false>
-void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, const Fp8Segs& sg = Fp8Segs{}, int bn = 0,
-                     bool wide = false) {
+void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, const Fp8Segs& sg = Fp8Segs{}, int bn = 0) {
   const int b = bn ? bn : lite_fp8_bn(p.Cout);
   const bool one = p.K <= BK;
-  if (wide && !one && (b == 128 || b == 64)) {  // eight waves, 256-pixel tile, three stages
-    if (b == 128) launch_lite_fp8_t<OUT_FP8, 128, 3, MULTI, 4>(p, act, s, sg);
-    else launch_lite_fp8_t<OUT_FP8, 64, 3, MULTI, 4>(p, act, s, sg);
-    return;
-  }
 #define FTM_LITE(BN_)                                                     \
   do {                                                                    \
     if (one) launch_lite_fp8_t<OUT_FP8, BN_, 1, MULTI>(p, act, s, sg);    \
@@ -633,10 +601,8 @@ void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, const Fp8Segs& 
 #undef FTM_LITE
 }
 
-// cfg value selecting conv_lite_fp8 (fp8 input only; any conv geometry with Cin % 16 == 0);
-// LITE8_CFG: its eight-wave 256-pixel tile on three LDS stages (K > 128, 128 / 64 channel tile)
+// cfg value selecting conv_lite_fp8 (fp8 input only; any conv geometry with Cin % 16 == 0)
 constexpr int LITE_CFG = 8;
-constexpr int LITE8_CFG = 9;
 
 template <bool CONV>
 void launch_io(const Fp8Params& p, bool in_bf16, bool out_fp8, int act, int cfg, hipStream_t s) {
@@ -922,13 +888,12 @@ void conv2d_nhwc_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, 
   p.ldx = Cin;
   p.ldy = ldy; p.y_coff = y_coff;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (cfg == LITE_CFG || cfg == LITE8_CFG) {
+  if (cfg == LITE_CFG) {
     if (in_bf16) throw std::invalid_argument("conv2d_nhwc_fp8: the conv_lite tile takes fp8 input");
     if (ph >= 1024 || pw >= 1024 || H >= 16384 || W >= 16384) throw std::invalid_argument("conv2d_nhwc_fp8: geometry");
     if ((long)Cout * p.K >= (1L << 31)) throw std::invalid_argument("conv2d_nhwc_fp8: weights larger than 2 GiB");
-    const bool wide = cfg == LITE8_CFG;
-    if (out_fp8) launch_lite_fp8<true>(p, act, s, Fp8Segs{}, 0, wide);
-    else launch_lite_fp8<false>(p, act, s, Fp8Segs{}, 0, wide);
+    if (out_fp8) launch_lite_fp8<true>(p, act, s);
+    else launch_lite_fp8<false>(p, act, s);
     FTM_CHECK_LAUNCH();
     return;
   }

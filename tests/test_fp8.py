@@ -129,18 +129,6 @@ def test_conv_fp8_lite_shapes_gpu():
 
 
 @pytest.mark.gpu
-def test_conv_fp8_lite_wide_gpu():
-    """cfg 9: conv_lite_fp8's eight-wave 256-pixel tile on three LDS stages (K > 128; 128 / 64
-    channel tiles; others fall back to cfg 8): K tails, M tails, strided, concat offset."""
-    _conv_case(288, 384, 3, 2, (0, 0, 0, 0), False, True, 9, N=2, H=17, W=17)     # BN 128, 3 tiles
-    _conv_case(192, 64, (7, 1), 1, (3, 3, 0, 0), False, False, 9, N=5, H=9, W=9)  # BN 64
-    _conv_case(768, 128, 1, 1, (0, 0, 0, 0), False, True, 9, N=7, H=9, W=9)       # M 567: 3 tiles
-    _conv_case(80, 192, 3, 1, (1, 1, 1, 1), False, True, 9, offset=64, extra=128)  # BN 64, 3 tiles
-    _conv_case(256, 256, 3, 1, (1, 1, 1, 1), False, False, 9, N=3, H=7, W=7)      # K 2304: 18 K-tiles
-    _conv_case(160, 96, 3, 1, (1, 1, 1, 1), False, True, 9)                        # BN 96: falls back to cfg 8
-
-
-@pytest.mark.gpu
 def test_conv_fp8_pointwise_and_bf16_input_gpu():
     _conv_case(160, 128, 1, 1, (0, 0, 0, 0), False, True, -1, N=3, H=17, W=17)
     _conv_case(32, 32, 3, 1, (0, 0, 0, 0), True, True, -1)  # stem output (bf16) quantised on load
