@@ -49,12 +49,13 @@ class EngineConfig:
     pw_dual_kernel: bool = False       # stage-2 projection+expand on the persistent dual kernel
     conv3x3c64_kernel: bool = True     # 64-channel 3x3 convs with the filter bank in LDS
     # cache-resident batch slices: the plan's leading run of large-activation layers (every
-    # tensor >= chain_min_hw pixels per image: ResNet-50's 56x56 stage 1) runs once per slice
-    # of chain_batch images, its intermediates in slice-sized buffers that stay in the
-    # 256 MiB Infinity Cache; 0 = off
-    chain_batch: int = 0
-    chain_min_hw: int = 3136
-    chain_edge: bool = False           # ... plus the layers leaving that resolution (stride-2 readers)
+    # tensor >= chain_min_hw pixels per image: Inception-v3's 149x149 .. 71x71 stem) runs once
+    # per slice of chain_batch images, its intermediates in slice-sized buffers that stay in
+    # the 256 MiB Infinity Cache.  -1 = auto (32-image slices, never over a persistent
+    # weight-resident kernel: ResNet-50's stage 1 measured slower sliced), 0 = off
+    chain_batch: int = -1
+    chain_min_hw: int = 5041
+    chain_edge: bool = True            # ... plus the layers leaving that resolution (stride-2 readers)
     wd_fused_step: bool = True         # Wide&Deep: hand-fused GPU step instead of autograd
     # Wide&Deep under DP: "owner" = deduplicated rows to their owner rank (row % world),
     # owner-side Adagrad, updated rows back (parallel/sparse_exchange.py); "allgather" = the

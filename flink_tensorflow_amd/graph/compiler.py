@@ -1901,6 +1901,8 @@ class CompiledFunction(TransformerLowering):
 
     # ================================================================== batch-slice chain
     _CHAIN_KINDS = ("conv", "gemm", "pool", "elementwise", "conv_fp8", "pool_fp8")
+    # persistent kernels that load a resident weight bank per launch
+    _PERSISTENT_IMPLS = ("conv3x3c64", "bottleneck_tail", "pw_res")
 
     def _find_chain(self, keep: set) -> dict | None:
         """The leading run of memory-bound layers that executes once per slice of
@@ -1917,7 +1919,10 @@ class CompiledFunction(TransformerLowering):
         Values entering or leaving the run keep their full buffers and are sliced."""
         cfg = _cfg()
         bs = int(getattr(cfg, "chain_batch", 0) or 0)
-        if bs <= 0 or self._pack is not None or not self.steps or not self.feed_names:
+        auto = bs < 0
+        if auto:
+            bs = 32
+        if bs == 0 or self._pack is not None or not self.steps or not self.feed_names:
             return None
         tn = TensorName.parse(self.feed_names[0])
         N = self.vals[(tn.name, tn.index)].shape[0] if self.vals[(tn.name, tn.index)].shape else 0
@@ -1941,6 +1946,8 @@ class CompiledFunction(TransformerLowering):
             vs = [v for v in list(st.inputs) + list(st.outputs) if v is not None and not v.is_const]
             if st.kind not in self._CHAIN_KINDS or not vs or not all(val_ok(v) for v in vs):
                 return False
+            if auto and st.meta.get("impl") in self._PERSISTENT_IMPLS:
+                return False  # its per-launch weight prologue outweighs the cache residency (r04_d)
             big = [v.shape[1] * v.shape[2] >= min_hw for v in vs]
             # chain_edge: a layer reading the large resolution into a smaller one (the next
             # stage's stride-2 conv / projection) joins too, so its large input stays internal

@@ -19,8 +19,9 @@ def small_resnet():
 def _plans(graph, device, B, bs, **kw):
     feeds = {"images:0": ((B, 72, 72, 3), "UINT8")}
     fetch = ["logits:0", "top_k:1"]
-    base = CompiledFunction(graph, feeds, fetch, device, strict=True, **kw)
-    with config.override(chain_batch=bs, chain_min_hw=3136):
+    with config.override(chain_batch=0):
+        base = CompiledFunction(graph, feeds, fetch, device, strict=True, **kw)
+    with config.override(chain_batch=bs, chain_min_hw=3136, chain_edge=False):
         ch = CompiledFunction(graph, feeds, fetch, device, strict=True, **kw)
     return base, ch
 
@@ -47,7 +48,8 @@ def test_chain_host_matches_unsliced(small_resnet):
 def test_chain_edge_takes_the_stride2_readers(small_resnet):
     imgs = torch.randint(0, 256, (4, 72, 72, 3), dtype=torch.uint8)
     feeds = {"images:0": ((4, 72, 72, 3), "UINT8")}
-    base = CompiledFunction(small_resnet, feeds, ["logits:0"], "cpu", strict=True)
+    with config.override(chain_batch=0):
+        base = CompiledFunction(small_resnet, feeds, ["logits:0"], "cpu", strict=True)
     with config.override(chain_batch=2, chain_min_hw=3136, chain_edge=True):
         ch = CompiledFunction(small_resnet, feeds, ["logits:0"], "cpu", strict=True)
     names = [s.name for s in ch.steps[ch._chain[0]:ch._chain[1]]]
@@ -56,6 +58,27 @@ def test_chain_edge_takes_the_stride2_readers(small_resnet):
     assert "block2/unit1/conv2/Conv2D" in names
     assert not any(n.startswith("block2/unit2") for n in names)
     torch.testing.assert_close(ch({"images:0": imgs})[0], base({"images:0": imgs})[0], rtol=0, atol=1e-5)
+
+
+def test_chain_auto_takes_the_inception_stem_not_resnet_stage1(small_resnet):
+    """Default (auto): 32-image slices over the layers whose tensors reach 71x71 pixels per
+    image, never across a persistent weight-resident kernel — Inception-v3's stem chains,
+    ResNet-50 (56x56 stage 1 on persistent kernels) does not."""
+    from flink_tensorflow_amd.models.zoo.inception_v3 import inception_v3_graph_def
+
+    with config.override(chain_batch=-1, chain_min_hw=5041, chain_edge=True):
+        rn = CompiledFunction(small_resnet, {"images:0": ((64, 72, 72, 3), "UINT8")}, ["logits:0"], "cpu",
+                              strict=True)
+        g = Graph.from_graph_def(inception_v3_graph_def(image_hw=(299, 299), top_k=5, seed=0))
+        inc = CompiledFunction(g, {"images:0": ((64, 299, 299, 3), "UINT8")}, ["top_k:0"], "cpu", strict=True)
+    # (the GPU plan fuses ResNet's stem conv and max pool into one launch, so nothing chains;
+    # the host plan may chain those two steps, never stage 1)
+    rc = getattr(rn, "_chain", None)
+    assert rc is None or {s.name for s in rn.steps[rc[0]:rc[1]]} <= {"conv1/Conv2D", "pool1"}
+    c = inc._chain
+    assert c is not None and c[2] == 2 and c[3] == 32
+    names = [s.name for s in inc.steps[c[0]:c[1]]]
+    assert names[0].endswith("Conv2d_1a_3x3/Conv2D") and names[-1].endswith("MaxPool_5a_3x3"), names
 
 
 def test_chain_off_when_batch_not_divisible(small_resnet):

@@ -1,0 +1,12 @@
+# round 4 F: the whole GPU suite on a fresh box after this round's changes (automatic
+# batch-slice chain for Inception-v3's stem, kernel reverts), smoke, and the BASELINE
+# benches in their default configuration, plus an Inception-v3 kernel trace per replay
+source tools/gpu_calls/gpu_steps.sh
+step pytest_gpu 900 python -u -m pytest tests/ -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+step bench_rn_a 300 python -u bench.py --steps 20 --warmup 5
+step bench_inc 300 python -u bench.py --model inception_v3 --steps 30 --warmup 5
+step bench_inc_dyn 300 python -u bench.py --model inception_v3 --steps 30 --warmup 5 --dynamic
+step bench_rn_b 300 python -u bench.py --steps 20 --warmup 5
+cd /tmp && export TMPDIR=/tmp
+step rocprof_inc 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_inc" -o run -- python "$REPO/bench.py" --model inception_v3 --steps 20 --warmup 3
