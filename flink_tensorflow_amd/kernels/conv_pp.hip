@@ -64,6 +64,7 @@ struct CPParams {
   int kt_per_split;
   long split_stride;
   int nk0;  // conv_lite with two sources: K-tiles of source 0 (source 1 follows, pointwise)
+  unsigned long long* stamp;  // conv_lite STAMP diagnostics: [64 workgroups][64 K-tiles][5] clocks
 };
 
 #define CP_FENCE() __builtin_amdgcn_sched_barrier(0)
@@ -399,7 +400,10 @@ FTM_DEVICE int lite_slot(int row, int chunk) {
 // DUAL: a second, pointwise and unpadded source (the strided projection input of a ResNet
 // block's first expand: y = x W_e + x2[::s] W_p in one K loop); its K-tiles follow source
 // 0's, the weight rows are [W_e | W_p].
-template <int ACT, bool HAS_RES, int BK, bool DUAL = false>
+// STAMP (diagnostics, bench/conv_stamp_probe.py): wave 0 of the first 64 workgroups records
+// s_memtime before the vmcnt wait, after it, after the barrier, after the DMA issue and after
+// the MFMA issue of each of the first 64 K-tiles (lane 0, vector stores).
+template <int ACT, bool HAS_RES, int BK, bool DUAL = false, bool STAMP = false>
 __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
   // BK = 64: 128-B LDS rows, 2 x 32 KiB stages, 2 MFMA steps per K-tile.
   // BK = 32: 64-B rows, 2 x 16 KiB stages (the igemm's footprint: four workgroups per CU),
@@ -519,12 +523,21 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = p.K / BK;
+  unsigned long long* sp = nullptr;
+  unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+  if constexpr (STAMP) {
+    if (threadIdx.x == 0 && blockIdx.x < 64) sp = p.stamp + (size_t)blockIdx.x * 64 * 5;
+  }
   dma(0);
   for (int kt = 0; kt < nk; ++kt) {
     const int st = kt & 1;
+    if constexpr (STAMP) t0 = __builtin_amdgcn_s_memtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (STAMP) t1 = __builtin_amdgcn_s_memtime();
     __syncthreads();
+    if constexpr (STAMP) t2 = __builtin_amdgcn_s_memtime();
     if (kt + 1 < nk) dma(st ^ 1);
+    if constexpr (STAMP) t3 = __builtin_amdgcn_s_memtime();
     const uint8_t* xs = smem + st * STG;
     const uint8_t* ws = xs + XB;
     __builtin_amdgcn_s_setprio(1);
@@ -542,6 +555,16 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_s_setprio(0);
+    if constexpr (STAMP) {
+      const unsigned long long t4 = __builtin_amdgcn_s_memtime();
+      if (sp && kt < 64) {
+        sp[kt * 5 + 0] = t0;
+        sp[kt * 5 + 1] = t1;
+        sp[kt * 5 + 2] = t2;
+        sp[kt * 5 + 3] = t3;
+        sp[kt * 5 + 4] = t4;
+      }
+    }
   }
   __syncthreads();  // every wave is done with the stage images: the epilogue tile reuses them
 
@@ -593,6 +616,12 @@ void launch_lite(const CPParams& p, hipStream_t s, bool dual = false) {
     if (dual) {
       if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, BK, true>), grid, block, 0, s, p);
       else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, BK, true>), grid, block, 0, s, p);
+      return;
+    }
+  }
+  if constexpr (BK == 64 && ACT == ACT_RELU) {
+    if (p.stamp && !p.res) {  // diagnostics only (conv_lite_stamp)
+      hipLaunchKernelGGL((conv_lite_kernel<ACT, false, BK, false, true>), grid, block, 0, s, p);
       return;
     }
   }
@@ -682,6 +711,11 @@ void need(bool ok, const char* what) {
 // output grid (N, OH, OW); w [Cout, K] bf16 with K = sum KH*KW*C in (src, kh, kw, c) order;
 // ktab: int32 [K/64, 2] built by the host (conv_pp_ktab); bias fp32 [Cout] or 0;
 // res bf16 [N*OH*OW, ldr] or 0; y bf16 [N*OH*OW, ldy] at channel offset y_coff.
+// conv_lite STAMP diagnostics target (0 = off): set by conv_lite_stamp, read by conv_pp
+unsigned long long* g_lite_stamp = nullptr;
+
+void conv_lite_stamp(uintptr_t buf) { g_lite_stamp = reinterpret_cast<unsigned long long*>(buf); }
+
 void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int N,
              int OH, int OW, int Cout, int ldy, int y_coff, int ldr, int act, int tile, int splits, uintptr_t ws,
              uintptr_t stream) {
@@ -731,6 +765,7 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   p.K = (int)K;
   p.OH = OH; p.OW = OW;
   p.ldw = (int)K; p.ldy = ldy; p.y_coff = y_coff; p.ldr = ldr;
+  p.stamp = tile == 2 ? g_lite_stamp : nullptr;
   need(tile >= 0 && tile <= 3, "tile must be 0 (256x256), 1 (512x128), 2 / 3 (128x128, 4 waves, K-tile 64 / 32)");
   const bool lite = tile >= 2;
   need(!lite || ((ns == 1 || tile == 2) && splits <= 1), "the 4-wave tile takes no split-K (two sources: tile 2)");
@@ -762,4 +797,7 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   FTM_CHECK_LAUNCH();
 }
 
-void register_conv_pp(pybind11::module_& m) { m.def("conv_pp", &conv_pp); }
+void register_conv_pp(pybind11::module_& m) {
+  m.def("conv_pp", &conv_pp);
+  m.def("conv_lite_stamp", &conv_lite_stamp);
+}
