@@ -727,6 +727,77 @@ __global__ __launch_bounds__(256) void pool_fp8_kernel(const uint8_t* __restrict
   }
 }
 
+// 3x3 fp8 max pool (Inception's stem / grid-reduction pools), 16 channels x 2 adjacent
+// outputs per thread with every window load issued before the first use: the generic
+// kernel's runtime-bounded loops load, wait and decode one window pixel at a time (9
+// dependent L2 round trips per output).  Out-of-range pixels read a clamped in-range
+// address and are replaced by -448 (e4m3's lowest finite value, neutral for the max:
+// quantisation saturates, so no stored value is below it).
+template <int SW>
+__global__ __launch_bounds__(256) void maxpool3_fp8_kernel(const uint8_t* __restrict__ x, uint8_t* __restrict__ y, int N,
+                                                           int H, int W, int C, int Ho, int Wo, int ph, int pw, int ldy,
+                                                           int y_coff, float rq) {
+  constexpr int PX = 2, NC = (PX - 1) * SW + 3;
+  const int cchunks = C / 16;
+  const int wgroups = (Wo + PX - 1) / PX;
+  const long total = (long)N * Ho * wgroups * cchunks;
+  const u32x4 lowest = {0xFEFEFEFEu, 0xFEFEFEFEu, 0xFEFEFEFEu, 0xFEFEFEFEu};
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int cc = idx % cchunks;
+    long t = idx / cchunks;
+    const int oxg = t % wgroups;
+    t /= wgroups;
+    const int oy = t % Ho;
+    const int n = t / Ho;
+    const int ox0 = oxg * PX;
+    const int iy0 = oy * 2 - ph, ixs = ox0 * SW - pw;  // (the row stride of these pools is 2 as well)
+    u32x4 v[3][NC];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const int iy = iy0 + dy;
+      const int iyc = min(max(iy, 0), H - 1);
+      const uint8_t* row = x + ((size_t)n * H + iyc) * W * C + cc * 16;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int ix = ixs + c;
+        const int ixc = min(max(ix, 0), W - 1);
+        v[dy][c] = *reinterpret_cast<const u32x4*>(row + (size_t)ixc * C);
+      }
+    }
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const bool yok = (unsigned)(iy0 + dy) < (unsigned)H;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const bool ok = yok && (unsigned)(ixs + c) < (unsigned)W;
+        if (!ok) v[dy][c] = lowest;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < PX; ++p) {
+      const int ox = ox0 + p;
+      if (ox >= Wo) break;
+      f32x2 acc[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = f32x2{-INFINITY, -INFINITY};
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          f32x2 d[8];
+          decode16(v[dy][p * SW + dx], d);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] = f32x2{fmaxf(acc[e][0], d[e][0]), fmaxf(acc[e][1], d[e][1])};
+        }
+      u32x4 o;
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        o[w] = pack4(acc[2 * w][0] * rq, acc[2 * w][1] * rq, acc[2 * w + 1][0] * rq, acc[2 * w + 1][1] * rq);
+      *reinterpret_cast<u32x4*>(y + (((size_t)n * Ho + oy) * Wo + ox) * ldy + y_coff + cc * 16) = o;
+    }
+  }
+}
+
 // Average pool (TF SAME: the sum divided by the in-bounds count) over a bf16 NHWC tensor,
 // then the bias + activation of the conv that PRODUCED it, written as fp8 (sat(y * out_q))
 // or bf16 into a (concat) buffer at a channel offset.  Inception's AvgPool(3x3/1) -> 1x1
@@ -815,6 +886,91 @@ __global__ __launch_bounds__(256) void avgpool_epi_kernel(const bf16* __restrict
   }
 }
 
+// avgpool_epi_kernel for 3x3 / stride-1 windows (Inception's commuted AvgPool branches):
+// 16 channels x 2 adjacent outputs per thread, all 12 window pixels (24 16-B loads) issued
+// before the first add — the generic kernel's runtime loops wait for each one in turn.
+// Out-of-range pixels read a clamped in-range address and are masked out of the sum.
+template <bool OUT_FP8, int ACT>
+__global__ __launch_bounds__(256) void avgpool3_epi_kernel(const bf16* __restrict__ x, const float* __restrict__ bias,
+                                                           uint8_t* __restrict__ y, int N, int H, int W, int C, int Ho,
+                                                           int Wo, int ph, int pw, int ldy, int y_coff, float out_q) {
+  constexpr int PX = 2, NC = PX + 2;
+  const int cchunks = C / 16;
+  const int wgroups = (Wo + PX - 1) / PX;
+  const long total = (long)N * Ho * wgroups * cchunks;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int cc = idx % cchunks;
+    long t = idx / cchunks;
+    const int oxg = t % wgroups;
+    t /= wgroups;
+    const int oy = t % Ho;
+    const int n = t / Ho;
+    const int ox0 = oxg * PX;
+    const int iy0 = oy - ph, ixs = ox0 - pw;
+    bf16x8 va[3][NC], vb[3][NC];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const int iyc = min(max(iy0 + dy, 0), H - 1);
+      const bf16* row = x + ((size_t)n * H + iyc) * W * C + cc * 16;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int ixc = min(max(ixs + c, 0), W - 1);
+        const bf16x8* src = reinterpret_cast<const bf16x8*>(row + (size_t)ixc * C);
+        va[dy][c] = src[0];
+        vb[dy][c] = src[1];
+      }
+    }
+    float bv[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) bv[e] = bias[cc * 16 + e];
+#pragma unroll
+    for (int p = 0; p < PX; ++p) {
+      const int ox = ox0 + p;
+      if (ox >= Wo) break;
+      float acc[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      int cnt = 0;
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+        const bool yok = (unsigned)(iy0 + dy) < (unsigned)H;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const bool ok = yok && (unsigned)(ixs + p + dx) < (unsigned)W;
+          cnt += ok ? 1 : 0;
+          const float m = ok ? 1.f : 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            acc[e] = __builtin_fmaf((float)va[dy][p + dx][e], m, acc[e]);
+            acc[8 + e] = __builtin_fmaf((float)vb[dy][p + dx][e], m, acc[8 + e]);
+          }
+        }
+      }
+      const float inv = 1.f / (float)max(cnt, 1);
+      float v[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = apply_act<ACT>(__builtin_fmaf(acc[e], inv, bv[e]));
+      const size_t o = (((size_t)n * Ho + oy) * Wo + ox) * ldy + y_coff + cc * 16;
+      if constexpr (OUT_FP8) {
+        u32x4 q;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) q[w] = pack4(v[4 * w] * out_q, v[4 * w + 1] * out_q, v[4 * w + 2] * out_q, v[4 * w + 3] * out_q);
+        *reinterpret_cast<u32x4*>(y + o) = q;
+      } else {
+        bf16x8 o0, o1;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          o0[e] = f2bf(v[e]);
+          o1[e] = f2bf(v[8 + e]);
+        }
+        bf16x8* dst = reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(y) + o);
+        dst[0] = o0;
+        dst[1] = o1;
+      }
+    }
+  }
+}
+
 // [N, HW, C] fp8 -> [N, C] bf16 mean * s.  One block per image, 16 channels per thread.
 __global__ __launch_bounds__(256) void gap_fp8_kernel(const uint8_t* __restrict__ x, bf16* __restrict__ y, int HW, int C,
                                                       float s) {
@@ -823,7 +979,8 @@ __global__ __launch_bounds__(256) void gap_fp8_kernel(const uint8_t* __restrict_
   for (int cc = threadIdx.x; cc < C / 16; cc += blockDim.x) {
     float acc[16] = {};
     const uint8_t* p = x + (size_t)n * HW * C + cc * 16;
-    for (int i = 0; i < HW; ++i) {
+#pragma unroll 8
+    for (int i = 0; i < HW; ++i) {  // unrolled: 8 independent row loads in flight per thread
       u32x4 v = *reinterpret_cast<const u32x4*>(p + (size_t)i * C);
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
@@ -1015,6 +1172,17 @@ void pool2d_nhwc_fp8(uintptr_t x, uintptr_t y, int N, int H, int W, int C, int H
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   auto X = reinterpret_cast<const uint8_t*>(x);
   auto Y = reinterpret_cast<uint8_t*>(y);
+  if (is_max && kh == 3 && kw == 3 && sh == 2 && (sw == 1 || sw == 2) && H > 0 && W > 0) {
+    const long work = (long)N * Ho * ((Wo + 1) / 2) * (C / 16);
+    if (sw == 2)
+      hipLaunchKernelGGL((maxpool3_fp8_kernel<2>), dim3(grid_for(work, 256)), dim3(256), 0, s, X, Y, N, H, W, C, Ho, Wo,
+                         ph, pw, ldy, y_coff, rq);
+    else
+      hipLaunchKernelGGL((maxpool3_fp8_kernel<1>), dim3(grid_for(work, 256)), dim3(256), 0, s, X, Y, N, H, W, C, Ho, Wo,
+                         ph, pw, ldy, y_coff, rq);
+    FTM_CHECK_LAUNCH();
+    return;
+  }
   // stride-1 windows: 2 outputs per thread share window columns; strided: 1
   if (sw == 1) {
     const long work = (long)N * Ho * ((Wo + 1) / 2) * (C / 16);
@@ -1039,6 +1207,12 @@ void pool2d_nhwc_fp8(uintptr_t x, uintptr_t y, int N, int H, int W, int C, int H
 template <bool OUT_FP8, int ACT>
 void launch_avgpool_epi(const bf16* X, const float* B, uint8_t* Y, int N, int H, int W, int C, int Ho, int Wo, int kh,
                         int kw, int sh, int sw, int ph, int pw, int ldy, int y_coff, float out_q, hipStream_t s) {
+  if (kh == 3 && kw == 3 && sh == 1 && sw == 1 && H > 0 && W > 0) {
+    const long work = (long)N * Ho * ((Wo + 1) / 2) * (C / 16);
+    hipLaunchKernelGGL((avgpool3_epi_kernel<OUT_FP8, ACT>), dim3(grid_for(work, 256)), dim3(256), 0, s, X, B, Y, N, H,
+                       W, C, Ho, Wo, ph, pw, ldy, y_coff, out_q);
+    return;
+  }
   if (sw == 1) {
     const long work = (long)N * Ho * ((Wo + 1) / 2) * (C / 16);
     hipLaunchKernelGGL((avgpool_epi_kernel<OUT_FP8, ACT, 2>), dim3(grid_for(work, 256)), dim3(256), 0, s, X, B, Y, N, H,

@@ -227,6 +227,9 @@ __global__ __launch_bounds__(256) void global_avgpool_kernel(const bf16* __restr
   for (int cc = threadIdx.x; cc < C / 8; cc += blockDim.x) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const bf16* p = x + (size_t)n * HW * C + cc * 8;
+    // unrolled: 8 independent row loads in flight per thread (the rolled loop waited for
+    // each of the HW loads in turn)
+#pragma unroll 8
     for (int i = 0; i < HW; ++i) {
       bf16x8 v = *reinterpret_cast<const bf16x8*>(p + (size_t)i * C);
 #pragma unroll

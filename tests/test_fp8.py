@@ -173,6 +173,34 @@ def test_pool_fp8_gpu(mode):
 
 
 @pytest.mark.gpu
+def test_maxpool3_fp8_unrolled_gpu():
+    """The unrolled 3x3 / row-stride-2 max pool (Inception's stem and grid-reduction pools):
+    odd widths (an odd output count leaves the thread's second output unused), SAME and
+    VALID padding, column stride 1 and 2, signed inputs (padding must not win the max),
+    16..192 channels, a requantising rq and a channel offset into a wider buffer."""
+    torch.manual_seed(3)
+    for (N, H, W, C), pad, st in (((2, 15, 15, 64), (0, 0, 0, 0), (2, 2)),
+                                  ((3, 9, 13, 192), (1, 1, 1, 1), (2, 2)),
+                                  ((1, 8, 10, 16), (0, 1, 0, 1), (2, 2)),
+                                  ((2, 11, 7, 48), (1, 1, 1, 1), (2, 1))):
+        x = Q.quantize(torch.randn(N, H, W, C) * 3 - 1, 0.05)  # mostly negative
+        ref = Q.pool2d_nhwc_fp8(x, (3, 3), st, pad, "max")
+        got = Q.pool2d_nhwc_fp8(x.to(DEV), (3, 3), st, pad, "max").cpu()
+        assert torch.equal(got, ref), (N, H, W, C, pad, st)  # rq 1: the max is one of the input bytes
+        ref = Q.pool2d_nhwc_fp8(x, (3, 3), st, pad, "max", rq=0.8)
+        got = Q.pool2d_nhwc_fp8(x.to(DEV), (3, 3), st, pad, "max", rq=0.8).cpu()
+        gd, rd = Q.from_fp8_bytes(got), Q.from_fp8_bytes(ref)
+        assert ((gd - rd).abs() <= 0.13 * rd.abs() + 1e-6).all() and (got == ref).float().mean() > 0.99
+    x = Q.quantize(torch.randn(2, 13, 13, 32).relu(), 0.02)
+    ref = Q.pool2d_nhwc_fp8(x, (3, 3), (2, 2), (0, 0, 0, 0), "max")
+    out = torch.zeros((2, 6, 6, 96), dtype=torch.uint8, device=DEV)
+    Q.pool2d_nhwc_fp8(x.to(DEV), (3, 3), (2, 2), (0, 0, 0, 0), "max", out=out, out_channel_offset=32)
+    torch.cuda.synchronize()
+    assert torch.equal(out[..., 32:64].cpu(), ref)
+    assert (out[..., :32] == 0).all() and (out[..., 64:] == 0).all()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("out_fp8", [True, False])
 def test_avgpool_bias_act_gpu(out_fp8):
     """The pool half of a commuted AvgPool -> 1x1 conv branch: bf16 in, TF SAME average,
@@ -181,7 +209,8 @@ def test_avgpool_bias_act_gpu(out_fp8):
     x = (torch.randn(3, 17, 17, 64) * 2).to(torch.bfloat16)
     b = torch.randn(64) * 0.5
     so = 0.02 if out_fp8 else None
-    for ks, st, pad in (((3, 3), (1, 1), (1, 1, 1, 1)), ((3, 3), (2, 2), (0, 0, 0, 0))):
+    for ks, st, pad in (((3, 3), (1, 1), (1, 1, 1, 1)), ((3, 3), (2, 2), (0, 0, 0, 0)),
+                        ((3, 3), (1, 1), (0, 0, 0, 0)), ((3, 3), (1, 1), (1, 0, 0, 1))):
         ref = Q.avgpool_bias_act(x.float(), ks, st, pad, b, "relu", out_scale=so)
         Ho, Wo = ref.shape[1:3]
         out = torch.zeros((3, Ho, Wo, 96), dtype=torch.uint8 if out_fp8 else torch.bfloat16, device=DEV)
