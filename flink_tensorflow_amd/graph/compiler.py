@@ -209,6 +209,9 @@ class CompiledFunction(TransformerLowering):
         self.fp8_layers = 0
         self._debug_sync = tracing.debug_sync()
         self._poison_after: dict[int, list] = {}
+        # batch-slice chain (``_find_chain``): (first step, end step, slices, slice size,
+        # values whose full buffers are sliced per slice) or None
+        self._chain: tuple | None = None
         if self._debug_sync or tracing.debug_poison():
             use_graph = False  # debug modes act between launches: run the plan eagerly
         import contextlib
@@ -2012,9 +2015,13 @@ class CompiledFunction(TransformerLowering):
 
     def _run_range(self, lo: int, hi: int, each=None):
         """Launches steps[lo:hi] (``each(step)`` instead of ``step.fn()`` if given), the
-        batch-slice chain once per slice."""
+        batch-slice chain once per slice: the chain's external values are rebound to the
+        slice's rows while its steps launch (eager, or into a capture) and restored after.
+        A plan is driven by one thread at a time (one lane = one stream)."""
         each = each or (lambda st: st.fn())
-        ch = getattr(self, "_chain", None)
+        ch = self._chain
+        if ch is not None and (ch[0] < lo < ch[1] or ch[0] < hi < ch[1]):
+            raise CompileError(f"steps [{lo}, {hi}) cut the batch-slice chain [{ch[0]}, {ch[1]})")
         i = lo
         while i < hi:
             if ch is not None and i == ch[0] and ch[1] <= hi:
@@ -2055,7 +2062,7 @@ class CompiledFunction(TransformerLowering):
             return
         poison = tracing.debug_poison()
         index = {id(s): i for i, s in enumerate(self.steps)}
-        ch = getattr(self, "_chain", None)
+        ch = self._chain
 
         def each(s):
             i = index[id(s)]
