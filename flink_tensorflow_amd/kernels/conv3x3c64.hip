@@ -80,19 +80,20 @@ __global__ __launch_bounds__(NT, 1) void conv3x3c64_kernel(const bf16* __restric
     for (int r = 0; r < 4; ++r) bv[i][r] = bias[i * 16 + (lane >> 4) * 4 + r];
 
   u32x4 stage[PITER];
+  // patch loads through a buffer descriptor: the zero padding and the chunks past the patch
+  // read as zeros from an out-of-range offset — no branch around each load
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(x), 0, N * H * W * C * 2, 0x00020000);
   auto load_patch = [&](const Tile& t) {
 #pragma unroll
     for (int it = 0; it < PITER; ++it) {
       const int q = tid + it * NT;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (q < PCHUNKS) {
-        const int pix = q >> 3, c = q & 7;
-        const int py = pix / PC, px = pix - py * PC;
-        const int gy = t.y0 - 1 + py, gx = t.x0 - 1 + px;
-        if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-          v = reinterpret_cast<const u32x4*>(x + (((size_t)t.n * H + gy) * W + gx) * C)[c];
-      }
-      stage[it] = v;
+      const int pix = q >> 3, c = q & 7;
+      const int py = pix / PC, px = pix - py * PC;
+      const int gy = t.y0 - 1 + py, gx = t.x0 - 1 + px;
+      const bool ok = q < PCHUNKS && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+      const unsigned off = ok ? (unsigned)((((t.n * H + gy) * W + gx) * C) * 2 + c * 16) : 0x80000000u;
+      stage[it] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     }
   };
   auto store_patch = [&]() {
@@ -180,7 +181,7 @@ void conv3x3c64_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int 
                      int act, int num_cu, uintptr_t stream) {
   if (H < TR || W < TC) throw std::invalid_argument("conv3x3c64: needs H >= 8 and W >= 32");
   if (ldy % 4 || y_coff % 4 || ldy < y_coff + C) throw std::invalid_argument("conv3x3c64: bad output stride/offset");
-  if ((long)N * H * W * C >= (1L << 31) || (long)N * H * W * ldy >= (1L << 31))
+  if ((long)N * H * W * C * 2 >= (1L << 31) || (long)N * H * W * ldy >= (1L << 31))
     throw std::invalid_argument("conv3x3c64: tensor too large for 32-bit indexing");
   if (x % 16 || w % 16 || y % 8 || !bias) throw std::invalid_argument("conv3x3c64: misaligned pointers / no bias");
   const int tiles = N * ((H + TR - 1) / TR) * ((W + TC - 1) / TC);

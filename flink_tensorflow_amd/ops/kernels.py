@@ -178,7 +178,7 @@ def conv3x3_c64_eligible(x_shape, w_shape, stride, pad, dilation, residual, act)
     Cout, KH, KW, _ = w_shape
     return (Cin == 64 and Cout == 64 and (KH, KW) == (3, 3) and tuple(stride) == (1, 1) and tuple(pad) == (1, 1, 1, 1)
             and tuple(dilation) == (1, 1) and residual is None and act_code(act) in (ACT_NONE, ACT_RELU)
-            and H >= 8 and W >= 32)
+            and H >= 8 and W >= 32 and N * H * W * Cin * 2 < 2 ** 31)
 
 
 _NUM_CU: dict = {}
