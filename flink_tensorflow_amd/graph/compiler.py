@@ -2025,21 +2025,27 @@ class CompiledFunction(TransformerLowering):
         i = lo
         while i < hi:
             if ch is not None and i == ch[0] and ch[1] <= hi:
-                i0, i1, parts, bs, ext = ch
-                full = [(v, v.buf) for v in ext if v.buf is not None]
-                try:
-                    for p in range(parts):
-                        for v, b in full:
-                            v.buf = b[p * bs:(p + 1) * bs]
-                        for st in self.steps[i0:i1]:
-                            each(st)
-                finally:
-                    for v, b in full:
-                        v.buf = b
-                i = i1
+                for p in range(ch[2]):
+                    self._run_chain_slice(p, each)
+                i = ch[1]
                 continue
             each(self.steps[i])
             i += 1
+
+    def _run_chain_slice(self, p: int, each=None):
+        """The chain's steps for slice ``p`` (images [p*bs, (p+1)*bs)), its external values
+        rebound to the slice's rows while they launch."""
+        each = each or (lambda st: st.fn())
+        i0, i1, parts, bs, ext = self._chain
+        full = [(v, v.buf) for v in ext if v.buf is not None]
+        try:
+            for v, b in full:
+                v.buf = b[p * bs:(p + 1) * bs]
+            for st in self.steps[i0:i1]:
+                each(st)
+        finally:
+            for v, b in full:
+                v.buf = b
 
     def _persistent(self, shape, dtype) -> torch.Tensor:
         """A buffer outside the shared slab (plan inputs, fetched outputs)."""
