@@ -1877,6 +1877,11 @@ class CompiledFunction(TransformerLowering):
                         first[j] = i0
                     if last[j] >= i0:
                         last[j] = max(last[j], i1 - 1)
+            # the slice-sized internals form one region of the same slab, live across the chain
+            chain_layout = self._plan_chain(chain, born)
+            sizes.append(max(chain_layout[1], 1))
+            first.append(i0)
+            last.append(i1 - 1)
         offs, total = plan_offsets(sizes, first, last)
         self.activation_bytes = total
         slab = self.arena.shared_slab(total) if self.arena is not None else \
@@ -1885,7 +1890,7 @@ class CompiledFunction(TransformerLowering):
             t.buf = slab[off:off + nb].view(t.dtype).view(tuple(_buf_shape(t)))
             self._poison_after.setdefault(lu, []).append(t.buf)
         if chain:
-            self._bind_chain(chain, born)
+            self._bind_chain(chain, chain_layout, slab, offs[-1])
         for v in self.vals.values():
             if v.alias_of is not None:
                 r = _root(v)
@@ -1992,22 +1997,32 @@ class CompiledFunction(TransformerLowering):
         return {"range": (i0, i1), "batch": bs, "parts": N // bs, "vals": vals, "touched": touched,
                 "internal": internal}
 
-    def _bind_chain(self, chain: dict, born: dict):
-        """Slice-sized buffers for the chain's internal values, planned by the same liveness
-        planner over the chain's own step range (one slice's lifetime)."""
+    def _plan_chain(self, chain: dict, born: dict) -> tuple:
+        """Layout of the chain's slice-sized internal values, planned by the same liveness
+        planner over the chain's own step range (one slice's lifetime): (offsets, total)."""
         from ..batching.arena import plan_offsets
 
         i0, i1 = chain["range"]
-        bs, parts = chain["batch"], chain["parts"]
+        bs = chain["batch"]
         ts = list(chain["internal"].values())
         shapes = [(bs, *_buf_shape(t)[1:]) for t in ts]
         sizes = [_nbytes(s, t.dtype) for s, t in zip(shapes, ts)]
         first = [born[id(t)] - i0 for t in ts]
         last = [max(born[id(t)], min(t.last_use, i1 - 1)) - i0 for t in ts]
         offs, total = plan_offsets(sizes, first, last)
-        slab = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
-        for t, s, off, nb in zip(ts, shapes, offs, sizes):
-            t.buf = slab[off:off + nb].view(t.dtype).view(s)
+        return offs, total
+
+    def _bind_chain(self, chain: dict, layout: tuple, slab: torch.Tensor, base: int):
+        """Binds the chain's internal values into their region ``[base, base + total)`` of
+        the activation slab (the subtask arena's shared slab when there is one)."""
+        i0, i1 = chain["range"]
+        bs, parts = chain["batch"], chain["parts"]
+        offs, total = layout
+        ts = list(chain["internal"].values())
+        for t, off in zip(ts, offs):
+            s = (bs, *_buf_shape(t)[1:])
+            nb = _nbytes(s, t.dtype)
+            t.buf = slab[base + off:base + off + nb].view(t.dtype).view(s)
         self.chain_bytes = total
         self.chain_layers = i1 - i0
         LOG.info("batch-slice chain: steps %d-%d (%s .. %s) x %d slices of %d, %d internal values in %.1f MB",
