@@ -94,13 +94,8 @@ class PipelinedGpuRunner:
         # framework-owned streams, not torch's pool (a pooled stream can be the one a sibling
         # subtask thread is capturing a hipGraph on: utils/streams.py)
         self.copy_stream = dedicated_stream(self.device, owner=self)
-        # EngineConfig.lane_priority: lane 0 on a high-priority stream, so its kernels are
-        # dispatched first and the other lanes fill the CUs it leaves free
-        from ..config import current as _current_cfg
-
-        prio0 = -1 if getattr(_current_cfg(), "lane_priority", False) and len(self.lanes) > 1 else 0
-        self.compute_streams = [dedicated_stream(self.device, priority=prio0 if i == 0 else 0, owner=self)
-                                for i in range(len(self.lanes))]
+        # (lane 0 on a high-priority stream measured -1 to -5 %: profiles/r04_o)
+        self.compute_streams = [dedicated_stream(self.device, owner=self) for _ in self.lanes]
         self.compute_stream = self.compute_streams[0]
         self.gather_threads = gather_threads
         self.stage_chunk = stage_chunk  # records per gather + H2D piece (0: whole batch at once)

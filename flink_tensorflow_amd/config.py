@@ -31,7 +31,6 @@ class EngineConfig:
     arena_fraction: float = 0.9        # share of HBM a subtask's plans may claim
     use_hip_graph: bool = True
     pipeline_depth: int = 3            # in-flight micro-batches per GPU (pinned ring slots)
-    lane_priority: bool = False        # compute lane 0 on a high-priority HIP stream
     checkpoint_interval_s: float | None = None
     checkpoint_dir: str | None = None
     restart_attempts: int = 0
