@@ -77,6 +77,7 @@ struct Fp8Params {
   int ldy, y_coff;  // output pixel stride / channel offset (elements)
   int tiles_m, tiles_n;
   int prio;  // s_setprio(1) around each K-tile's MFMA cluster (fp8_prio)
+  unsigned long long* stamp;  // conv_lite_fp8 STAMP diagnostics: [64 workgroups][64 K-tiles][5] clocks
 };
 
 // Multi-output epilogue of conv_lite_fp8 (horizontally fused sibling 1x1 convs of one
@@ -359,7 +360,9 @@ void launch_tile(const Fp8Params& p, int act, int cfg, hipStream_t s) {
 // 80, 160, 288 on 96; 320, 448, <= 64 on 64); NSTG = 1 (a single LDS stage) when the whole K fits one
 // K-tile (K <= 128: no prefetch to overlap, and half the LDS lets more workgroups hide the
 // load latency of these streaming layers).
-template <bool OUT_FP8, int ACT, int BN_ = 128, int NSTG = 2, bool MULTI = false>
+// STAMP (diagnostics, bench/conv_stamp_probe.py --fp8): as conv_pp.hip's conv_lite STAMP —
+// wave 0 of the first 64 workgroups records s_memtime around each K-tile's phases.
+template <bool OUT_FP8, int ACT, int BN_ = 128, int NSTG = 2, bool MULTI = false, bool STAMP = false>
 __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8Segs sg) {
   static_assert(BN_ == 128 || BN_ == 96 || BN_ == 64, "channel tile 128, 96 or 64");
   constexpr int BM = 128, BN = BN_;
@@ -459,12 +462,21 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8S
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = NSTG == 1 ? 1 : (p.K + BK - 1) / BK;  // NSTG 1: the host guarantees K <= BK
+  unsigned long long* sp = nullptr;
+  unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+  if constexpr (STAMP) {
+    if (threadIdx.x == 0 && blockIdx.x < 64) sp = p.stamp + (size_t)blockIdx.x * 64 * 5;
+  }
   dma(0);
   for (int kt = 0; kt < nk; ++kt) {
     const int st = NSTG == 1 ? 0 : (kt & 1);
+    if constexpr (STAMP) t0 = __builtin_amdgcn_s_memtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (STAMP) t1 = __builtin_amdgcn_s_memtime();
     __syncthreads();
+    if constexpr (STAMP) t2 = __builtin_amdgcn_s_memtime();
     if (NSTG > 1 && kt + 1 < nk) dma(st ^ 1);
+    if constexpr (STAMP) t3 = __builtin_amdgcn_s_memtime();
     const uint8_t* xs = smem + st * STG;
     const uint8_t* ws = xs + XB;
     i32x8 a[NI], b[4];
@@ -486,6 +498,16 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8S
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, E8M0_ONE, 0,
                                                                      E8M0_ONE);
+    if constexpr (STAMP) {
+      const unsigned long long t4 = __builtin_amdgcn_s_memtime();
+      if (sp && kt < 64) {
+        sp[kt * 5 + 0] = t0;
+        sp[kt * 5 + 1] = t1;
+        sp[kt * 5 + 2] = t2;
+        sp[kt * 5 + 3] = t3;
+        sp[kt * 5 + 4] = t4;
+      }
+    }
   }
   __syncthreads();  // the epilogue tile reuses the stage images
 
@@ -568,6 +590,12 @@ void launch_lite_fp8_t(Fp8Params p, int act, hipStream_t s, const Fp8Segs& sg) {
     hipLaunchKernelGGL((conv_lite_fp8_kernel<false, ACT_NONE, BN_, NSTG, true>), grid, block, 0, s, p, sg);
     return;
   }
+  if constexpr (OUT_FP8 && NSTG == 2) {
+    if (p.stamp && act == ACT_RELU) {  // diagnostics only (conv_lite_fp8_stamp)
+      hipLaunchKernelGGL((conv_lite_fp8_kernel<true, ACT_RELU, BN_, 2, false, true>), grid, block, 0, s, p, sg);
+      return;
+    }
+  }
   switch (act) {
     case ACT_NONE: hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_NONE, BN_, NSTG>), grid, block, 0, s, p, sg); break;
     case ACT_RELU: hipLaunchKernelGGL((conv_lite_fp8_kernel<OUT_FP8, ACT_RELU, BN_, NSTG>), grid, block, 0, s, p, sg); break;
@@ -600,6 +628,9 @@ void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, const Fp8Segs& 
   else FTM_LITE(128);
 #undef FTM_LITE
 }
+
+// conv_lite_fp8 STAMP diagnostics target (0 = off): set by conv_lite_fp8_stamp
+unsigned long long* g_lite_fp8_stamp = nullptr;
 
 // cfg value selecting conv_lite_fp8 (fp8 input only; any conv geometry with Cin % 16 == 0)
 constexpr int LITE_CFG = 8;
@@ -1046,6 +1077,7 @@ void conv2d_nhwc_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, 
   p.ldy = ldy; p.y_coff = y_coff;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (cfg == LITE_CFG) {
+    p.stamp = g_lite_fp8_stamp;
     if (in_bf16) throw std::invalid_argument("conv2d_nhwc_fp8: the conv_lite tile takes fp8 input");
     if (ph >= 1024 || pw >= 1024 || H >= 16384 || W >= 16384) throw std::invalid_argument("conv2d_nhwc_fp8: geometry");
     if ((long)Cout * p.K >= (1L << 31)) throw std::invalid_argument("conv2d_nhwc_fp8: weights larger than 2 GiB");
@@ -1262,6 +1294,7 @@ void global_avgpool_fp8(uintptr_t x, uintptr_t y, int N, int HW, int C, float s,
 
 void register_fp8(pybind11::module_& m) {
   m.def("conv2d_nhwc_fp8", &conv2d_nhwc_fp8);
+  m.def("conv_lite_fp8_stamp", [](uintptr_t b) { g_lite_fp8_stamp = reinterpret_cast<unsigned long long*>(b); });
   m.def("gemm_fp8", &gemm_fp8);
   m.def("quantize_bf16_fp8", &quantize_bf16_fp8);
   m.def("dequantize_fp8_bf16", &dequantize_fp8_bf16);
