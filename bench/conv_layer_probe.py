@@ -48,7 +48,10 @@ def main():
         res = torch.randn((B, OH, OW, Cout), device=dev, generator=g).to(torch.bfloat16) if opt and opt[0] else None
         flops = 2.0 * B * OH * OW * Cout * k * k * Cin
         for impl in a.impls.split(","):
-            if impl == "igemm":
+            if impl == "halo":  # kernels/conv3x3h.hip (stride-1 3x3 only)
+                def fn():
+                    K.conv3x3_halo(x, w, b, K.ACT_RELU, out=y)
+            elif impl == "igemm":
                 def fn():
                     K.conv2d_nhwc(x, w, b, res, (s, s), (pad, pad, pad, pad), (1, 1), K.ACT_RELU, out=y)
             else:  # pp: the 8-wave ping-pong tiles; lite: the 4-wave 128x128 LDS-DMA tile

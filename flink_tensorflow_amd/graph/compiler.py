@@ -862,6 +862,20 @@ class CompiledFunction(TransformerLowering):
                 and (res_val is None or (res_val.concat_slot is None and res_val.qscale is None
                                          and tuple(res_val.shape) == tuple(out.shape) and res_val.alias_of is None))
                 and max(pt, pb) < 1024 and max(pl, pr) < 1024)
+        halo = (lite and res_val is None and _cfg().conv3x3_halo and b_dev is not None
+                and K.conv3x3_halo_eligible(tuple(xin.shape), tuple(w_ohwi.shape), (sh, sw), (pt, pb, pl, pr),
+                                            (dh, dw), None, act))
+        if halo:
+            # stride-1 3x3 convs (ResNet stages 2-4): the input is filled into LDS once per 64
+            # channels as the tile's halo, not once per tap (kernels/conv3x3h.hip)
+            def run(xin=xin, out=out, w_dev=w_dev, b_dev=b_dev):  # noqa: F811
+                K.conv3x3_halo(xin.buf, w_dev, b_dev, act, out=_target(out), out_channel_offset=_coff(out))
+
+            self._emit(node.name, "conv", run, [xin], [out], {"impl": "conv3x3h"})
+            self.conv3x3h_layers = getattr(self, "conv3x3h_layers", 0) + 1
+            self.vals[(last.name, 0)] = out
+            self._alias_fused_outputs(absorbed, out)
+            return
         if lite:
             # KxK convs (stage 2-4 3x3): 4-wave 128x128 implicit GEMM on two LDS-DMA stages
             # (kernels/conv_pp.hip conv_lite): 6-24 % faster than the register-staged igemm
@@ -2271,6 +2285,7 @@ class CompiledFunction(TransformerLowering):
                 "fp8_layers": self.fp8_layers, "fused_shortcuts": getattr(self, "fused_shortcuts", 0),
                 "fused_tails": getattr(self, "fused_tails", 0), "decimated_tails": getattr(self, "decimated_tails", 0),
                 "fused_pools": getattr(self, "fused_pools", 0), "conv3x3c64": getattr(self, "conv3x3c64", 0),
+                "conv3x3h": getattr(self, "conv3x3h_layers", 0),
                 "conv_pp": getattr(self, "conv_pp_layers", 0), "pw_res": getattr(self, "pw_res_layers", 0),
                 "conv_lite": getattr(self, "conv_lite_layers", 0),
                 "commuted_pools": getattr(self, "commuted_pools", 0),

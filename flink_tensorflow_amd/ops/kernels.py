@@ -181,6 +181,68 @@ def conv3x3_c64_eligible(x_shape, w_shape, stride, pad, dilation, residual, act)
             and H >= 8 and W >= 32 and N * H * W * Cin * 2 < 2 ** 31)
 
 
+def conv3x3_halo_len(N: int, H: int, W: int) -> int:
+    """Halo pixels the widest 128-pixel tile of kernels/conv3x3h.hip needs (padded
+    flattened coordinates; mirrors ``halo_len`` there)."""
+    key = (N, H, W)
+    if key not in _HALO_LEN:
+        Wp, Hp, hw = W + 2, H + 2, H * W
+
+        def pb(m):
+            n, r = divmod(m, hw)
+            oh, ow = divmod(r, W)
+            return (n * Hp + oh) * Wp + ow
+
+        M = N * hw
+        worst = max(pb(min(m0 + 127, M - 1)) - pb(m0) for m0 in range(0, M, 128))
+        _HALO_LEN[key] = worst + 2 * Wp + 3
+    return _HALO_LEN[key]
+
+
+_HALO_LEN: dict = {}
+
+
+def conv3x3_halo_eligible(x_shape, w_shape, stride, pad, dilation, residual, act) -> bool:
+    """kernels/conv3x3h.hip: 3x3, stride 1, SAME padding, Cin % 64 == 0, Cout % 8 == 0, no
+    residual, bias (+ReLU) epilogue, and a 128-pixel tile's halo within 288 pixels (ResNet-50
+    stages 2-4 at any batch: 28x28 -> 260, 14x14 -> 214, 7x7 -> 240)."""
+    if len(x_shape) != 4:
+        return False
+    N, H, W, Cin = x_shape
+    Cout, KH, KW, _ = w_shape
+    return (Cin % 64 == 0 and Cout % 8 == 0 and (KH, KW) == (3, 3) and tuple(stride) == (1, 1)
+            and tuple(pad) == (1, 1, 1, 1) and tuple(dilation) == (1, 1) and residual is None
+            and act_code(act) in (ACT_NONE, ACT_RELU) and N * H * W * Cin * 2 < 2 ** 31
+            and N * (H + 2) * (W + 2) < 2 ** 31 and conv3x3_halo_len(N, H, W) <= 288)
+
+
+def conv3x3_halo(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor, act=None,
+                 out: torch.Tensor | None = None, out_channel_offset: int = 0) -> torch.Tensor:
+    """3x3 / s1 / SAME conv, ``act(conv + bias)``; GPU: the halo-staged implicit GEMM
+    (kernels/conv3x3h.hip: the input is filled into LDS once per 64 channels, not once per
+    tap); host: the fp32 reference conv."""
+    N, H, W, Cin = x.shape
+    Cout = w_ohwi.shape[0]
+    a = act_code(act)
+    if out is None:
+        out = torch.empty((N, H, W, Cout), dtype=x.dtype if x.is_cuda else torch.float32, device=x.device)
+        out_channel_offset = 0
+    if not conv3x3_halo_eligible(tuple(x.shape), tuple(w_ohwi.shape), (1, 1), (1, 1, 1, 1), (1, 1), None, a):
+        raise ValueError(f"conv3x3_halo: unsupported shapes x {tuple(x.shape)} w {tuple(w_ohwi.shape)}")
+    if tuple(out.shape[:3]) != (N, H, W) or out_channel_offset + Cout > out.shape[3]:
+        raise ValueError("conv3x3_halo: output buffer does not fit")
+    if x.is_cuda:
+        _check(x, "x", device=x.device)
+        _check(w_ohwi, "w", device=x.device)
+        _check(out, "out", device=x.device)
+        _check(bias, "bias", torch.float32, x.device)
+        _hip().conv3x3h_bf16(x.data_ptr(), w_ohwi.data_ptr(), bias.data_ptr(), out.data_ptr(), N, H, W, Cin, Cout,
+                             out.shape[3], out_channel_offset, a, _stream())
+        return out
+    return conv2d_nhwc(x, w_ohwi, bias, None, (1, 1), (1, 1, 1, 1), (1, 1), a, out=out,
+                       out_channel_offset=out_channel_offset)
+
+
 _NUM_CU: dict = {}
 
 

@@ -126,6 +126,9 @@ def test_conv_fp8_lite_shapes_gpu():
     _conv_case(128, 448, 1, 1, (0, 0, 0, 0), False, True, 8, N=2, H=9, W=9)      # K 128 exactly, BN 64
     _conv_case(96, 96, 3, 1, (1, 1, 1, 1), False, True, 8, offset=32, extra=64)   # BN 96
     _conv_case(48, 160, (1, 7), 1, (0, 0, 3, 3), False, False, 8, N=2, H=9, W=9)  # BN 96, 2 tiles
+    # K walk past the 64-K-tile LDS table (K > 8192): those entries are computed in place
+    _conv_case(1040, 64, 3, 1, (1, 1, 1, 1), False, True, 8, N=1, H=7, W=7)       # 74 K-tiles
+    _conv_case(8320, 96, 1, 1, (0, 0, 0, 0), False, False, 8, N=1, H=5, W=5)      # 65 K-tiles
 
 
 @pytest.mark.gpu
