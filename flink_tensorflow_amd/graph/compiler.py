@@ -804,7 +804,7 @@ class CompiledFunction(TransformerLowering):
                 # stage 3/4 reduces: the 4-wave LDS-DMA tile beats the 256x256 ping-pong GEMM
                 # (stage 3: 37.8 vs 43.5 µs, profiles/r03_conv) and leaves room on the CU
                 cl = K.ConvPP([(tuple(xin.shape), (1, 1), (1, 1), (0, 0), (1, 1))], Cout, tuple(out.shape[1:3]),
-                              self.device, tile=2)
+                              self.device, tile=4 if _cfg().conv_lite_ws else 2)
 
                 def run_cl(xin=xin, out=out, cl=cl, w_nk=w_nk, bz=bz, act=act):
                     cl([xin.buf], w_nk, bz, None, act, out=_target(out), out_channel_offset=_coff(out))
@@ -881,7 +881,7 @@ class CompiledFunction(TransformerLowering):
             # (kernels/conv_pp.hip conv_lite): 6-24 % faster than the register-staged igemm
             # per layer and 64 KiB of LDS, so it shares a CU with the sibling lane
             cl = K.ConvPP([(tuple(xin.shape), (KHe, KWe), (sh, sw), (pt, pl), (dh, dw))], Cout, tuple(out.shape[1:3]),
-                          self.device, tile=2)  # tiles 3 (32-deep K), 256x128 (4 or 8 waves) and 3-stage
+                          self.device, tile=4 if _cfg().conv_lite_ws else 2)  # tiles 3 (32-deep K), 256x128 (4 or 8 waves) and 3-stage
             # variants (raw-barrier, counted vmcnt) measured slower: profiles/r03_conv, r04_a, r04_c
 
             def run(xin=xin, out=out, res_val=res_val, cl=cl, w2=w_dev.reshape(Cout, -1), b_dev=b_dev):  # noqa: F811
@@ -1246,7 +1246,7 @@ class CompiledFunction(TransformerLowering):
 
         # fp8 input: the 4-wave LDS-DMA tile (kernels/fp8.hip conv_lite_fp8, cfg 8); a bf16
         # input (the layer after the stem) is quantised on load by the register-staged kernel
-        cfg = 8 if (x.qscale is not None and _cfg().conv_impl == "lite") else -1
+        cfg = (9 if _cfg().conv_lite_ws else 8) if (x.qscale is not None and _cfg().conv_impl == "lite") else -1
         # (an eight-wave 256-pixel tile on three LDS stages measured 5-40 % slower per layer
         # and -2 % in the bench: profiles/r04_d)
 
@@ -1255,8 +1255,8 @@ class CompiledFunction(TransformerLowering):
                                out_scale=_eff_scale(out), out=_target(out), out_channel_offset=_coff(out), chan_scale=cs,
                                cfg=cfg)
 
-        self._emit(node.name, "conv_fp8", run, [x], [out], {"impl": "conv_lite_fp8"} if cfg == 8 else None)
-        if cfg == 8:
+        self._emit(node.name, "conv_fp8", run, [x], [out], {"impl": "conv_lite_fp8"} if cfg in (8, 9) else None)
+        if cfg in (8, 9):
             self.conv_lite_layers = getattr(self, "conv_lite_layers", 0) + 1
         self.vals[(last.name, 0)] = out
         self._alias_fused_outputs(absorbed, out)
@@ -1574,10 +1574,10 @@ class CompiledFunction(TransformerLowering):
         self.params += [wq_dev, cs_dev, b_dev, lo_dev]
         self.fp8_layers += len(members)
 
-        def run(x=x, segs=segs, wq=wq_dev, ws=ws_dev, cs=cs_dev, b=b_dev, lo=lo_dev, xs=xs):
+        def run(x=x, segs=segs, wq=wq_dev, ws=ws_dev, cs=cs_dev, b=b_dev, lo=lo_dev, xs=xs, wsp=_cfg().conv_lite_ws):
             F8.conv2d_nhwc_fp8_multi(_view(x), xs, wq, (1, 1), ws, b, lo,
                                      [(_target(v), a, e, _coff(v), _eff_scale(v) if v.qscale is not None else None)
-                                      for v, a, e in segs], chan_scale=cs)
+                                      for v, a, e in segs], chan_scale=cs, ws=wsp)
 
         self._emit("+".join(m["conv"].name for m in members), "conv_fp8", run, [x], [v for v, _, _ in segs],
                    {"impl": "conv_lite_fp8_multi", "multi_out": True})
@@ -1646,7 +1646,8 @@ class CompiledFunction(TransformerLowering):
             wq_dev, ws_dev, cs_dev = self._dev(wq), self._dev(ws), self._dev(ws * x.qscale, torch.float32)
             self.params += [wq_dev, cs_dev, zero, b_dev]
             self.fp8_layers += 1
-            cfg = 8 if (self.device.type == "cuda" and _cfg().conv_impl == "lite") else -1
+            cfg = ((9 if _cfg().conv_lite_ws else 8) if (self.device.type == "cuda" and _cfg().conv_impl == "lite")
+                   else -1)
 
             def run_conv(x=x, y=y, wq=wq_dev, ws=ws_dev, cs=cs_dev, zero=zero, cfg=cfg, xs=x.qscale):
                 F8.conv2d_nhwc_fp8(_view(x), xs, wq, (1, 1), ws, zero, act=K.ACT_NONE, out=y.buf, chan_scale=cs,

@@ -610,6 +610,180 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
   }
 }
 
+// conv_lite_ws (tile 4): conv_lite's 128x128 tile and LDS images with the roles split over
+// EIGHT waves — waves 0-3 only run the MFMAs (2 x 2, 64 x 64 outputs each), waves 4-7 only
+// issue the LDS-DMA (wave 4 + w stages what wave w stages in conv_lite).  In conv_lite each
+// wave issues its eight 1 KiB DMA pieces (~50-100 cycles each) and then its 32 MFMAs, so a
+// K-tile costs issue + MFMA per wave (in-kernel clocks: profiles/r04_g, r04_q); split, the
+// DMA of K-tile t+1 is issued by other waves while the MFMA waves run K-tile t.  One
+// barrier per K-tile for all eight waves: the DMA waves wait for their pieces (vmcnt), the
+// barrier publishes the stage and retires every MFMA wave's reads of the other one.
+template <int ACT, bool HAS_RES>
+__global__ __launch_bounds__(512, 4) void conv_lite_ws_kernel(CPParams p) {  // 4 waves / SIMD: 2 workgroups per CU
+  constexpr int BK = 64;
+  constexpr int BM = 128, BN = 128;
+  constexpr int ROWB = BK * 2;
+  constexpr int CPR = ROWB / 16;
+  constexpr int RPI = 1024 / ROWB;
+  constexpr int QX = BM / RPI / 4;
+  constexpr int XB = BM * ROWB, WB = BN * ROWB, STG = XB + WB;
+  constexpr int OPITCH = BN * 2 + 16;
+  constexpr int LDS = 2 * STG > BM * OPITCH ? 2 * STG : BM * OPITCH;
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[LDS];
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int tm = tile / p.tiles_n;
+  const int tn = tile - tm * p.tiles_n;
+  const int m0 = tm * BM;
+  const int n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool mfma_wave = wave < 4;  // wave-uniform role
+  const int role = wave & 3;
+  const int nk = p.K / BK;
+
+  if (!mfma_wave) {
+    // ---------------- DMA waves
+    const int drow = lane / CPR;
+    const int dchunk = lite_slot<CPR>(drow, lane % CPR);
+    const unsigned nimg = (unsigned)p.M / (unsigned)(p.OH * p.OW);
+    const CSrc& S = p.s[0];
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)S.x, 0, (int)(nimg * (unsigned)(S.H * S.W) * (unsigned)S.C * 2u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.w, 0, (int)((unsigned)p.N * (unsigned)p.ldw * 2u), 0x00020000);
+    int pb[4], hw[4];
+    unsigned offw[4];
+    const int ohw = p.OH * p.OW;
+#pragma unroll
+    for (int q = 0; q < QX; ++q) {
+      const int r = RPI * (QX * role + q) + drow;
+      const int m = m0 + r;
+      const bool live = m < p.M;
+      const int n = live ? m / ohw : 0;
+      const int rem = live ? m - n * ohw : 0;
+      const int oh = rem / p.OW;
+      const int ow = rem - oh * p.OW;
+      const int ih0 = live ? oh * S.sh - S.ph : -16384;
+      const int iw0 = ow * S.sw - S.pw;
+      pb[q] = ((n * S.H + ih0) * S.W + iw0) * S.C * 2 + dchunk * 16;
+      hw[q] = (ih0 << 16) | (iw0 & 0xFFFF);
+      const unsigned co = n0 + r;
+      offw[q] = co < (unsigned)p.N ? (co * p.ldw + dchunk * 8) * 2u : 0x80000000u;
+    }
+    const int cpt = S.C / BK;
+    int cc = 0, kw = 0, kh = 0, kt_dma = 0;
+    auto dma = [&](int stage) {
+      const unsigned woff = (unsigned)kt_dma * (unsigned)ROWB;
+      const int dih = kh * p.dh, diw = kw * p.dw;
+      const int delta = ((dih * S.W + diw) * S.C + cc * BK) * 2;
+      ++kt_dma;
+      if (++cc == cpt) {
+        cc = 0;
+        if (++kw == p.KW) {
+          kw = 0;
+          ++kh;
+        }
+      }
+      uint8_t* bx = smem + stage * STG + QX * role * RPI * ROWB;
+      uint8_t* bw = bx + XB;
+#pragma unroll
+      for (int q = 0; q < QX; ++q) {
+        const int ih = (hw[q] >> 16) + dih;
+        const int iw = ((hw[q] << 16) >> 16) + diw;
+        const bool ok = (unsigned)ih < (unsigned)S.H && (unsigned)iw < (unsigned)S.W;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(bx + q * 1024), 16,
+                                                 ok ? (unsigned)(pb[q] + delta) : 0x80000000u, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 1024), 16,
+                                                 offw[q], woff, 0, 0);
+      }
+    };
+    dma(0);
+    for (int kt = 0; kt < nk; ++kt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kt + 1 < nk) dma((kt & 1) ^ 1);
+    }
+    __syncthreads();  // the MFMA waves' epilogue tile is written
+  } else {
+    // ---------------- MFMA waves
+    const int wm = role & 1, wn = role >> 1;
+    const int frow = lane & 15;
+    const int fq = lane >> 4;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      __syncthreads();
+      const uint8_t* xs = smem + (kt & 1) * STG;
+      const uint8_t* ws = xs + XB;
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        const int sl = lite_slot<CPR>(frow, ks * 4 + fq) << 4;
+        bf16x8 a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ws + (wn * 64 + i * 16 + frow) * ROWB + sl);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(xs + (wm * 64 + j * 16 + frow) * ROWB + sl);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // every wave is done with the stage images: the epilogue tile reuses them
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cl = wn * 64 + i * 16 + fq * 4;
+      f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+      if (p.bias && n0 + cl < p.N) bv = *reinterpret_cast<const f32x4*>(p.bias + n0 + cl);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int pl = wm * 64 + j * 16 + frow;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] + bv[r];
+          if constexpr (!HAS_RES) v = apply_act<ACT>(v);
+          o[r] = f2bf(v);
+        }
+        *reinterpret_cast<bf16x4*>(smem + pl * OPITCH + cl * 2) = o;
+      }
+    }
+  }
+  // (both branches pass the same number of barriers: nk + 1, and one more below)
+  __syncthreads();
+  bf16* y = reinterpret_cast<bf16*>(p.y);
+  constexpr int SEGS = BN / 8;
+#pragma unroll 4
+  for (int q = threadIdx.x; q < BM * SEGS; q += 512) {
+    const int ml = q / SEGS;
+    const int ccol = q - ml * SEGS;
+    const int m = m0 + ml;
+    const int n = n0 + ccol * 8;
+    if (m >= p.M || n >= p.N) continue;
+    u32x4 v = *reinterpret_cast<const u32x4*>(smem + ml * OPITCH + ccol * 16);
+    if constexpr (HAS_RES) {
+      bf16x8 o = __builtin_bit_cast(bf16x8, v);
+      const bf16x8 r = *reinterpret_cast<const bf16x8*>(p.res + (size_t)m * p.ldr + n);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(apply_act<ACT>((float)o[e] + (float)r[e]));
+      v = __builtin_bit_cast(u32x4, o);
+    }
+    *reinterpret_cast<u32x4*>(y + (size_t)m * p.ldy + p.y_coff + n) = v;
+  }
+}
+
+template <int ACT>
+void launch_lite_ws(const CPParams& p, hipStream_t s) {
+  const dim3 grid(p.tiles_m * p.tiles_n), block(512);
+  if (p.res) hipLaunchKernelGGL((conv_lite_ws_kernel<ACT, true>), grid, block, 0, s, p);
+  else hipLaunchKernelGGL((conv_lite_ws_kernel<ACT, false>), grid, block, 0, s, p);
+}
+
 // lite_bk: 64 (tile 2) or 32 (tile 3)
 template <int ACT, int BK>
 void launch_lite(const CPParams& p, hipStream_t s, bool dual = false) {
@@ -768,7 +942,9 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   p.OH = OH; p.OW = OW;
   p.ldw = (int)K; p.ldy = ldy; p.y_coff = y_coff; p.ldr = ldr;
   p.stamp = tile == 2 ? g_lite_stamp : nullptr;
-  need(tile >= 0 && tile <= 3, "tile must be 0 (256x256), 1 (512x128), 2 / 3 (128x128, 4 waves, K-tile 64 / 32)");
+  need(tile >= 0 && tile <= 4,
+       "tile must be 0 (256x256), 1 (512x128), 2 / 3 (128x128, 4 waves, K-tile 64 / 32), 4 (128x128, DMA / MFMA waves)");
+  need(tile != 4 || ns == 1, "the wave-specialised tile takes one source");
   const bool lite = tile >= 2;
   need(!lite || ((ns == 1 || tile == 2) && splits <= 1), "the 4-wave tile takes no split-K (two sources: tile 2)");
   need(tile != 3 || p.s[0].C % 32 == 0, "the 32-deep 4-wave tile needs Cin % 32 == 0");
@@ -786,7 +962,11 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   float* wsp = reinterpret_cast<float*>(ws);
-  if (lite) {
+  if (tile == 4) {
+    if (act == ACT_RELU) launch_lite_ws<ACT_RELU>(p, s);
+    else if (act == ACT_NONE) launch_lite_ws<ACT_NONE>(p, s);
+    else throw std::invalid_argument("conv_pp: unsupported activation");
+  } else if (lite) {
     switch (act * 2 + (tile == 3)) {
       case ACT_NONE * 2: launch_lite<ACT_NONE, 64>(p, s, ns == 2); break;
       case ACT_NONE * 2 + 1: launch_lite<ACT_NONE, 32>(p, s); break;

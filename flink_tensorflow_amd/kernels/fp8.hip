@@ -78,6 +78,7 @@ struct Fp8Params {
   int tiles_m, tiles_n;
   int prio;  // s_setprio(1) around each K-tile's MFMA cluster (fp8_prio)
   unsigned long long* stamp;  // conv_lite_fp8 STAMP diagnostics: [64 workgroups][64 K-tiles][5] clocks
+  int ws;                     // conv_lite_fp8 on DMA / MFMA waves (cfg 9, multi: ws argument)
 };
 
 // Multi-output epilogue of conv_lite_fp8 (horizontally fused sibling 1x1 convs of one
@@ -362,8 +363,10 @@ void launch_tile(const Fp8Params& p, int act, int cfg, hipStream_t s) {
 // load latency of these streaming layers).
 // STAMP (diagnostics, bench/conv_stamp_probe.py --fp8): as conv_pp.hip's conv_lite STAMP —
 // wave 0 of the first 64 workgroups records s_memtime around each K-tile's phases.
-template <bool OUT_FP8, int ACT, int BN_ = 128, int NSTG = 2, bool MULTI = false, bool STAMP = false>
-__global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8Segs sg) {
+// WS (cfg 9): eight waves, the roles split as conv_pp.hip's conv_lite_ws — waves 0-3 run
+// only the MFMAs, waves 4-7 only issue the LDS-DMA (wave 4 + w stages wave w's pieces).
+template <bool OUT_FP8, int ACT, int BN_, int NSTG, bool MULTI, bool STAMP, bool WS>
+__device__ __forceinline__ void conv_lite_fp8_body(const Fp8Params& p, const Fp8Segs& sg) {
   static_assert(BN_ == 128 || BN_ == 96 || BN_ == 64, "channel tile 128, 96 or 64");
   constexpr int BM = 128, BN = BN_;
   constexpr int NI = BN / 32;  // weight fragments per wave (a wave covers BN / 2 channels)
@@ -381,7 +384,11 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8S
   const int m0 = tm * BM;
   const int n0 = tn * BN;
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int NT = WS ? 512 : 256;
+  const int wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool dma_wave = !WS || wave_id >= 4;  // wave-uniform roles (both, without WS)
+  const bool mma_wave = !WS || wave_id < 4;
+  const int wave = wave_id & 3;  // the role's wave index
   const int wm = wave & 1, wn = wave >> 1;
 
   const int drow = lane >> 3;
@@ -467,16 +474,17 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8S
   if constexpr (STAMP) {
     if (threadIdx.x == 0 && blockIdx.x < 64) sp = p.stamp + (size_t)blockIdx.x * 64 * 5;
   }
-  dma(0);
+  if (dma_wave) dma(0);
   for (int kt = 0; kt < nk; ++kt) {
     const int st = NSTG == 1 ? 0 : (kt & 1);
     if constexpr (STAMP) t0 = __builtin_amdgcn_s_memtime();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (dma_wave) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (STAMP) t1 = __builtin_amdgcn_s_memtime();
     __syncthreads();
     if constexpr (STAMP) t2 = __builtin_amdgcn_s_memtime();
-    if (NSTG > 1 && kt + 1 < nk) dma(st ^ 1);
+    if (dma_wave && NSTG > 1 && kt + 1 < nk) dma(st ^ 1);
     if constexpr (STAMP) t3 = __builtin_amdgcn_s_memtime();
+    if (!mma_wave) continue;
     const uint8_t* xs = smem + st * STG;
     const uint8_t* ws = xs + XB;
     i32x8 a[NI], b[4];
@@ -486,18 +494,32 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8S
       const u32x4 lo = *reinterpret_cast<const u32x4*>(r + sl0), hi = *reinterpret_cast<const u32x4*>(r + sl1);
       a[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
+    if constexpr (WS) {
+      // 128 VGPRs (four waves per SIMD): one pixel fragment at a time, all NI weight fragments held
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint8_t* r = xs + (wm * 64 + j * 16 + frow) * BK;
-      const u32x4 lo = *reinterpret_cast<const u32x4*>(r + sl0), hi = *reinterpret_cast<const u32x4*>(r + sl1);
-      b[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      for (int j = 0; j < 4; ++j) {
+        const uint8_t* r = xs + (wm * 64 + j * 16 + frow) * BK;
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(r + sl0), hi = *reinterpret_cast<const u32x4*>(r + sl1);
+        const i32x8 bj = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], bj, acc[i][j], 0, 0, 0, E8M0_ONE, 0,
+                                                                       E8M0_ONE);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint8_t* r = xs + (wm * 64 + j * 16 + frow) * BK;
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(r + sl0), hi = *reinterpret_cast<const u32x4*>(r + sl1);
+        b[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, E8M0_ONE, 0,
+                                                                       E8M0_ONE);
     }
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, E8M0_ONE, 0,
-                                                                     E8M0_ONE);
     if constexpr (STAMP) {
       const unsigned long long t4 = __builtin_amdgcn_s_memtime();
       if (sp && kt < 64) {
@@ -512,31 +534,33 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8S
   __syncthreads();  // the epilogue tile reuses the stage images
 
   uint8_t* Os = smem;
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int cl = wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
-    f32x4 sv = {0.f, 0.f, 0.f, 0.f}, bv = {0.f, 0.f, 0.f, 0.f}, lv = {0.f, 0.f, 0.f, 0.f};
-    if (n0 + cl < p.Cout) {
-      sv = *reinterpret_cast<const f32x4*>(p.scale + n0 + cl);
-      bv = *reinterpret_cast<const f32x4*>(p.bias + n0 + cl);
-      if constexpr (MULTI) lv = *reinterpret_cast<const f32x4*>(sg.lo + n0 + cl);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int pl = wm * 64 + j * 16 + frow;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if constexpr (MULTI) v[r] = fmaxf(acc[i][j][r] * sv[r] + bv[r], lv[r]);
-        else v[r] = apply_act<ACT>(acc[i][j][r] * sv[r] + bv[r]);
+  if (mma_wave) {  // (the DMA waves hold no accumulators)
+  #pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int cl = wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, bv = {0.f, 0.f, 0.f, 0.f}, lv = {0.f, 0.f, 0.f, 0.f};
+      if (n0 + cl < p.Cout) {
+        sv = *reinterpret_cast<const f32x4*>(p.scale + n0 + cl);
+        bv = *reinterpret_cast<const f32x4*>(p.bias + n0 + cl);
+        if constexpr (MULTI) lv = *reinterpret_cast<const f32x4*>(sg.lo + n0 + cl);
       }
-      if constexpr (OUT_FP8 && !MULTI) {
-        *reinterpret_cast<uint32_t*>(Os + pl * OLD + cl) =
-            pack4(v[0] * p.out_q, v[1] * p.out_q, v[2] * p.out_q, v[3] * p.out_q);
-      } else {
-        bf16x4 o;
-        o[0] = f2bf(v[0]); o[1] = f2bf(v[1]); o[2] = f2bf(v[2]); o[3] = f2bf(v[3]);
-        *reinterpret_cast<bf16x4*>(Os + pl * OLD + cl * 2) = o;
+  #pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int pl = wm * 64 + j * 16 + frow;
+        float v[4];
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if constexpr (MULTI) v[r] = fmaxf(acc[i][j][r] * sv[r] + bv[r], lv[r]);
+          else v[r] = apply_act<ACT>(acc[i][j][r] * sv[r] + bv[r]);
+        }
+        if constexpr (OUT_FP8 && !MULTI) {
+          *reinterpret_cast<uint32_t*>(Os + pl * OLD + cl) =
+              pack4(v[0] * p.out_q, v[1] * p.out_q, v[2] * p.out_q, v[3] * p.out_q);
+        } else {
+          bf16x4 o;
+          o[0] = f2bf(v[0]); o[1] = f2bf(v[1]); o[2] = f2bf(v[2]); o[3] = f2bf(v[3]);
+          *reinterpret_cast<bf16x4*>(Os + pl * OLD + cl * 2) = o;
+        }
       }
     }
   }
@@ -544,7 +568,7 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8S
   if constexpr (MULTI) {
     constexpr int CPR16 = BN / 16;  // 16-channel chunks (32 B of the bf16 tile) per row
 #pragma unroll 2
-    for (int q = threadIdx.x; q < BM * CPR16; q += 256) {
+    for (int q = threadIdx.x; q < BM * CPR16; q += NT) {
       const int pl = q / CPR16;
       const int cc = q % CPR16;
       const int m = m0 + pl;
@@ -570,7 +594,7 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8S
   constexpr int EPC = 16 / OB;
   constexpr int CPR = BN / EPC;
 #pragma unroll 4
-  for (int q = threadIdx.x; q < BM * CPR; q += 256) {
+  for (int q = threadIdx.x; q < BM * CPR; q += NT) {
     const int pl = q / CPR;
     const int cc = q % CPR;
     const int m = m0 + pl;
@@ -581,11 +605,33 @@ __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8S
   }
 }
 
+template <bool OUT_FP8, int ACT, int BN_ = 128, int NSTG = 2, bool MULTI = false, bool STAMP = false>
+__global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8Segs sg) {
+  conv_lite_fp8_body<OUT_FP8, ACT, BN_, NSTG, MULTI, STAMP, false>(p, sg);
+}
+
+// eight waves, two workgroups per CU: four waves per SIMD (HIP's second launch bound is
+// the minimum waves per execution unit), so at most 128 VGPRs
+template <bool OUT_FP8, int ACT, int BN_, bool MULTI = false>
+__global__ __launch_bounds__(512, 4) void conv_lite_fp8_ws_kernel(Fp8Params p, Fp8Segs sg) {
+  conv_lite_fp8_body<OUT_FP8, ACT, BN_, 2, MULTI, false, true>(p, sg);
+}
+
 template <bool OUT_FP8, int BN_, int NSTG, bool MULTI = false>
 void launch_lite_fp8_t(Fp8Params p, int act, hipStream_t s, const Fp8Segs& sg) {
   p.tiles_m = (p.M + 127) / 128;
   p.tiles_n = (p.Cout + BN_ - 1) / BN_;
   dim3 grid(p.tiles_m * p.tiles_n), block(256);
+  // DMA / MFMA waves: two-stage tiles only (one stage has no DMA to overlap) and channel
+  // tiles <= 96 (the 128-wide tile's accumulators do not fit 128 VGPRs without spilling)
+  if constexpr (NSTG == 2 && BN_ <= 96) if (p.ws) {
+    const dim3 b8(512);
+    if constexpr (MULTI) hipLaunchKernelGGL((conv_lite_fp8_ws_kernel<false, ACT_NONE, BN_, true>), grid, b8, 0, s, p, sg);
+    else if (act == ACT_RELU) hipLaunchKernelGGL((conv_lite_fp8_ws_kernel<OUT_FP8, ACT_RELU, BN_>), grid, b8, 0, s, p, sg);
+    else if (act == ACT_NONE) hipLaunchKernelGGL((conv_lite_fp8_ws_kernel<OUT_FP8, ACT_NONE, BN_>), grid, b8, 0, s, p, sg);
+    else throw std::invalid_argument("fp8 conv_lite: activation must be none/relu");
+    return;
+  }
   if constexpr (MULTI) {  // the per-channel clamp replaces the activation
     hipLaunchKernelGGL((conv_lite_fp8_kernel<false, ACT_NONE, BN_, NSTG, true>), grid, block, 0, s, p, sg);
     return;
@@ -632,8 +678,10 @@ void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, const Fp8Segs& 
 // conv_lite_fp8 STAMP diagnostics target (0 = off): set by conv_lite_fp8_stamp
 unsigned long long* g_lite_fp8_stamp = nullptr;
 
-// cfg value selecting conv_lite_fp8 (fp8 input only; any conv geometry with Cin % 16 == 0)
+// cfg value selecting conv_lite_fp8 (fp8 input only; any conv geometry with Cin % 16 == 0);
+// LITE_WS_CFG: the same tile on eight DMA / MFMA waves
 constexpr int LITE_CFG = 8;
+constexpr int LITE_WS_CFG = 9;
 
 template <bool CONV>
 void launch_io(const Fp8Params& p, bool in_bf16, bool out_fp8, int act, int cfg, hipStream_t s) {
@@ -1076,8 +1124,9 @@ void conv2d_nhwc_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, 
   p.ldx = Cin;
   p.ldy = ldy; p.y_coff = y_coff;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (cfg == LITE_CFG) {
+  if (cfg == LITE_CFG || cfg == LITE_WS_CFG) {
     p.stamp = g_lite_fp8_stamp;
+    p.ws = cfg == LITE_WS_CFG;
     if (in_bf16) throw std::invalid_argument("conv2d_nhwc_fp8: the conv_lite tile takes fp8 input");
     if (ph >= 1024 || pw >= 1024 || H >= 16384 || W >= 16384) throw std::invalid_argument("conv2d_nhwc_fp8: geometry");
     if ((long)Cout * p.K >= (1L << 31)) throw std::invalid_argument("conv2d_nhwc_fp8: weights larger than 2 GiB");
@@ -1097,7 +1146,7 @@ void conv2d_nhwc_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, 
 // order, every bound a multiple of 16; lo: fp32 [Cout] lower clamp (0 ReLU / -inf none).
 void conv2d_nhwc_fp8_multi(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t lo, int N, int H,
                            int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw,
-                           int Ho, int Wo, pybind11::list segs, uintptr_t stream) {
+                           int Ho, int Wo, pybind11::list segs, uintptr_t stream, int ws) {
   const int ns = (int)pybind11::len(segs);
   if (ns < 1 || ns > MAX_SEGS) throw std::invalid_argument("conv2d_nhwc_fp8_multi: 1.." + std::to_string(MAX_SEGS) + " segments");
   if (Cin % 16 || Cout % 16) throw std::invalid_argument("conv2d_nhwc_fp8_multi: Cin / Cout % 16 != 0");
@@ -1145,6 +1194,7 @@ void conv2d_nhwc_fp8_multi(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t 
   p.K = KH * KW * Cin;
   p.ldx = Cin;
   if ((long)Cout * p.K >= (1L << 31)) throw std::invalid_argument("conv2d_nhwc_fp8_multi: weights larger than 2 GiB");
+  p.ws = ws;
   launch_lite_fp8<false, true>(p, ACT_NONE, reinterpret_cast<hipStream_t>(stream), sg);
   FTM_CHECK_LAUNCH();
 }

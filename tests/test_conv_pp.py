@@ -58,6 +58,11 @@ CASES = [
     ("lite32_3x3s2", [((3, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 3, None),
     ("lite32_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (7, 7), True, "relu", 3, None),
     ("lite32_1x1", [((2, 14, 14, 256), (1, 1), (1, 1), (0, 0), (1, 1))], 1024, (14, 14), True, None, 3, None),
+    # the same 128x128 tile on eight waves: four issue the LDS-DMA, four run the MFMAs
+    ("ws_3x3", [((4, 28, 28, 128), (3, 3), (1, 1), (1, 1), (1, 1))], 128, (28, 28), False, "relu", 4, None),
+    ("ws_3x3s2", [((3, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 4, None),
+    ("ws_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (7, 7), True, "relu", 4, None),
+    ("ws_1x1", [((2, 14, 14, 256), (1, 1), (1, 1), (0, 0), (1, 1))], 1024, (14, 14), True, None, 4, None),
 ]
 
 

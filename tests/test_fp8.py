@@ -110,25 +110,26 @@ def test_conv_fp8_configs_gpu(cfg):
 
 
 @pytest.mark.gpu
-def test_conv_fp8_lite_shapes_gpu():
-    """conv_lite_fp8 (cfg 8, the 4-wave LDS-DMA tile): Cin not a multiple of the 128-byte
-    K-tile (288, 192, 80), K tails, Cout tails, 1x1 / 7x1 / strided, fp8 and bf16 output at a
-    concat offset."""
-    _conv_case(288, 384, 3, 2, (0, 0, 0, 0), False, True, 8, N=2, H=17, W=17)
-    _conv_case(192, 80, (7, 1), 1, (3, 3, 0, 0), False, False, 8, N=3, H=9, W=9)
-    _conv_case(80, 192, 3, 1, (1, 1, 1, 1), False, True, 8, offset=64, extra=128)
-    _conv_case(768, 128, 1, 1, (0, 0, 0, 0), False, True, 8, N=4, H=9, W=9)
-    _conv_case(16, 32, 3, 1, (1, 1, 1, 1), False, False, 8)
+@pytest.mark.parametrize("c", [8, 9])
+def test_conv_fp8_lite_shapes_gpu(c):
+    """conv_lite_fp8 (cfg 8, the 4-wave LDS-DMA tile; cfg 9, the same tile on DMA / MFMA
+    waves where the channel tile is <= 96): Cin not a multiple of the 128-byte K-tile (288,
+    192, 80), K tails, Cout tails, 1x1 / 7x1 / strided, fp8 and bf16 output at a concat offset."""
+    _conv_case(288, 384, 3, 2, (0, 0, 0, 0), False, True, c, N=2, H=17, W=17)
+    _conv_case(192, 80, (7, 1), 1, (3, 3, 0, 0), False, False, c, N=3, H=9, W=9)
+    _conv_case(80, 192, 3, 1, (1, 1, 1, 1), False, True, c, offset=64, extra=128)
+    _conv_case(768, 128, 1, 1, (0, 0, 0, 0), False, True, c, N=4, H=9, W=9)
+    _conv_case(16, 32, 3, 1, (1, 1, 1, 1), False, False, c)
     # channel tile 64 (Cout % 128 in (0, 64]) and the single-stage K <= 128 variants
-    _conv_case(64, 80, 1, 1, (0, 0, 0, 0), False, True, 8, N=3, H=13, W=13)      # K 64: one stage, BN 128
-    _conv_case(64, 192, 1, 1, (0, 0, 0, 0), False, True, 8, offset=64, extra=128)  # one stage, BN 64
-    _conv_case(32, 320, 3, 1, (1, 1, 1, 1), False, False, 8)                     # BN 64, 5 tiles
-    _conv_case(128, 448, 1, 1, (0, 0, 0, 0), False, True, 8, N=2, H=9, W=9)      # K 128 exactly, BN 64
-    _conv_case(96, 96, 3, 1, (1, 1, 1, 1), False, True, 8, offset=32, extra=64)   # BN 96
-    _conv_case(48, 160, (1, 7), 1, (0, 0, 3, 3), False, False, 8, N=2, H=9, W=9)  # BN 96, 2 tiles
-    # K walk past the 64-K-tile LDS table (K > 8192): those entries are computed in place
-    _conv_case(1040, 64, 3, 1, (1, 1, 1, 1), False, True, 8, N=1, H=7, W=7)       # 74 K-tiles
-    _conv_case(8320, 96, 1, 1, (0, 0, 0, 0), False, False, 8, N=1, H=5, W=5)      # 65 K-tiles
+    _conv_case(64, 80, 1, 1, (0, 0, 0, 0), False, True, c, N=3, H=13, W=13)      # K 64: one stage, BN 128
+    _conv_case(64, 192, 1, 1, (0, 0, 0, 0), False, True, c, offset=64, extra=128)  # one stage, BN 64
+    _conv_case(32, 320, 3, 1, (1, 1, 1, 1), False, False, c)                     # BN 64, 5 tiles
+    _conv_case(128, 448, 1, 1, (0, 0, 0, 0), False, True, c, N=2, H=9, W=9)      # K 128 exactly, BN 64
+    _conv_case(96, 96, 3, 1, (1, 1, 1, 1), False, True, c, offset=32, extra=64)   # BN 96
+    _conv_case(48, 160, (1, 7), 1, (0, 0, 3, 3), False, False, c, N=2, H=9, W=9)  # BN 96, 2 tiles
+    # long K walks (the per-lane tap / channel walk over 65-74 K-tiles)
+    _conv_case(1040, 64, 3, 1, (1, 1, 1, 1), False, True, c, N=1, H=7, W=7)       # 74 K-tiles
+    _conv_case(8320, 96, 1, 1, (0, 0, 0, 0), False, False, c, N=1, H=5, W=5)      # 65 K-tiles
 
 
 @pytest.mark.gpu
@@ -228,12 +229,14 @@ def test_avgpool_bias_act_gpu(out_fp8):
 
 
 @pytest.mark.gpu
-def test_conv_fp8_multi_output_gpu():
+@pytest.mark.parametrize("C,wsp", [(96, False), (192, False), (192, True)])
+def test_conv_fp8_multi_output_gpu(C, wsp):
     """Sibling 1x1 convs as one GEMM with a multi-destination epilogue: fp8 segments of
     different scales (one at a concat offset), a bf16 segment, ReLU and no-act channels;
-    against the host reference of the same kernel."""
+    against the host reference of the same kernel.  C 192 takes the two-stage tile, ``wsp``
+    its DMA / MFMA-wave form."""
     torch.manual_seed(6)
-    N, H, W, C = 2, 13, 11, 96
+    N, H, W = 2, 13, 11
     x = torch.randn(N, H, W, C).relu()
     sx = Q.scale_for(x.abs().max())
     xq = Q.quantize(x, sx)
@@ -255,7 +258,7 @@ def test_conv_fp8_multi_output_gpu():
     ref = outs("cpu")
     Q.conv2d_nhwc_fp8_multi(xq, sx, wq, (1, 1), ws, b, lo, segs(ref))
     got = outs(DEV)
-    Q.conv2d_nhwc_fp8_multi(xq.to(DEV), sx, wq.to(DEV), (1, 1), ws.to(DEV), b.to(DEV), lo.to(DEV), segs(got))
+    Q.conv2d_nhwc_fp8_multi(xq.to(DEV), sx, wq.to(DEV), (1, 1), ws.to(DEV), b.to(DEV), lo.to(DEV), segs(got), ws=wsp)
     torch.cuda.synchronize()
     for i, (r, g) in enumerate(zip(ref, got)):
         g = g.cpu()
