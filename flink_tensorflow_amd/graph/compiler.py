@@ -1914,7 +1914,8 @@ class CompiledFunction(TransformerLowering):
                     v.buf = r.buf.view(shape) if r.buf.is_contiguous() else r.buf.reshape(shape)
         if chain:
             self._chain = (chain["range"][0], chain["range"][1], chain["parts"], chain["batch"],
-                           [v for v in chain["vals"] if id(_root(v)) not in internal])
+                           [v for v in chain["vals"] if id(_root(v)) not in internal], chain["n"],
+                           [v for v in chain["vals"] if id(_root(v)) in internal and v.buf is not None])
         self._outputs = []
         for fv in fetch_vals:
             if fv.is_const:
@@ -1949,7 +1950,7 @@ class CompiledFunction(TransformerLowering):
             return None
         tn = TensorName.parse(self.feed_names[0])
         N = self.vals[(tn.name, tn.index)].shape[0] if self.vals[(tn.name, tn.index)].shape else 0
-        if not N or N % bs or N // bs < 2:
+        if not N or -(-N // bs) < 2:
             return None
         min_hw = int(getattr(cfg, "chain_min_hw", 3136))
 
@@ -2009,7 +2010,9 @@ class CompiledFunction(TransformerLowering):
             k = id(r)
             if k in produced and k not in used_outside and k not in keep and k not in feeds and r.buf is None:
                 internal[k] = r
-        return {"range": (i0, i1), "batch": bs, "parts": N // bs, "vals": vals, "touched": touched,
+        # a batch that is not a multiple of the slice runs a shorter last slice (the dynamic
+        # batch buckets of 8-image steps): its external rows and slice buffers are narrowed
+        return {"range": (i0, i1), "batch": bs, "parts": -(-N // bs), "n": N, "vals": vals, "touched": touched,
                 "internal": internal}
 
     def _plan_chain(self, chain: dict, born: dict) -> tuple:
@@ -2066,15 +2069,18 @@ class CompiledFunction(TransformerLowering):
         """The chain's steps for slice ``p`` (images [p*bs, (p+1)*bs)), its external values
         rebound to the slice's rows while they launch."""
         each = each or (lambda st: st.fn())
-        i0, i1, parts, bs, ext = self._chain
-        full = [(v, v.buf) for v in ext if v.buf is not None]
+        i0, i1, parts, bs, ext, n, ints = self._chain
+        lo, hi = p * bs, min(n, (p + 1) * bs)
+        full = [(v, v.buf, True) for v in ext if v.buf is not None]
+        if hi - lo < bs:  # the short last slice: the slice-sized internals' leading rows
+            full += [(v, v.buf, False) for v in ints]
         try:
-            for v, b in full:
-                v.buf = b[p * bs:(p + 1) * bs]
+            for v, b, external in full:
+                v.buf = b[lo:hi] if external else b[:hi - lo]
             for st in self.steps[i0:i1]:
                 each(st)
         finally:
-            for v, b in full:
+            for v, b, _ in full:
                 v.buf = b
 
     def _persistent(self, shape, dtype) -> torch.Tensor:

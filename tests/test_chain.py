@@ -81,8 +81,15 @@ def test_chain_auto_takes_the_inception_stem_not_resnet_stage1(small_resnet):
     assert names[0].endswith("Conv2d_1a_3x3/Conv2D") and names[-1].endswith("MaxPool_5a_3x3"), names
 
 
-def test_chain_off_when_batch_not_divisible(small_resnet):
-    with config.override(chain_batch=3, chain_min_hw=3136):
+def test_chain_short_last_slice(small_resnet):
+    """A batch that is not a multiple of the slice (the dynamic batch buckets): 5 images in
+    slices of 2 run 2 + 2 + 1, the last slice on the leading rows of the slice buffers."""
+    imgs = torch.randint(0, 256, (5, 72, 72, 3), dtype=torch.uint8)
+    base, ch = _plans(small_resnet, "cpu", 5, 2)
+    c = ch._chain
+    assert c is not None and c[2] == 3 and c[3] == 2
+    torch.testing.assert_close(ch({"images:0": imgs})[0], base({"images:0": imgs})[0], rtol=0, atol=1e-5)
+    with config.override(chain_batch=8, chain_min_hw=3136):  # one slice: nothing to chain
         plan = CompiledFunction(small_resnet, {"images:0": ((4, 72, 72, 3), "UINT8")}, ["logits:0"], "cpu",
                                 strict=True)
     assert getattr(plan, "_chain", None) is None
@@ -91,8 +98,8 @@ def test_chain_off_when_batch_not_divisible(small_resnet):
 @pytest.mark.gpu
 def test_chain_gpu_matches_unsliced(small_resnet):
     dev = torch.device("cuda", 0)
-    imgs = torch.randint(0, 256, (8, 72, 72, 3), dtype=torch.uint8)
-    base, ch = _plans(small_resnet, dev, 8, 2)
+    imgs = torch.randint(0, 256, (7, 72, 72, 3), dtype=torch.uint8)
+    base, ch = _plans(small_resnet, dev, 7, 2)  # slices 2 + 2 + 2 + 1
     assert ch._chain is not None and ch.summary()["hip_graph"]
     a = base({"images:0": imgs.to(dev)})
     b = ch({"images:0": imgs.to(dev)})
@@ -101,7 +108,7 @@ def test_chain_gpu_matches_unsliced(small_resnet):
     assert (a[1][:, 0] == b[1][:, 0]).float().mean().item() >= 0.75
     # the head preprocess per H2D piece, then the tail graph (chain inside)
     src = imgs.to(dev)
-    pieces = [(0, 3), (3, 8)]
+    pieces = [(0, 3), (3, 7)]
     assert ch.replay_from_chunks("images:0", src, pieces, lambda i: None)
     torch.cuda.synchronize()
     assert torch.equal(ch.output_tensors()[0].float(), b[0])
