@@ -102,3 +102,27 @@ def test_conv_pp_concat_offset_gpu():
     got, ref, left = _run(CASES[0], "cuda", coff=64)
     assert (got - ref).abs().max().item() <= 2e-2 * ref.abs().max().item() + 2e-2
     assert (left == 0).all()  # channels before the slice untouched
+
+
+@pytest.mark.gpu
+def test_conv_lite_ws_in_resnet_plan_gpu():
+    """The opt-in DMA / MFMA-wave tile (``EngineConfig.conv_lite_ws``) in the compiled
+    ResNet-50 matches the fp32 interpreter as the default plan does."""
+    from flink_tensorflow_amd.config import override
+    from flink_tensorflow_amd.graph.compiler import CompiledFunction
+    from flink_tensorflow_amd.graph.graph import Graph
+    from flink_tensorflow_amd.graph.session import Session
+    from flink_tensorflow_amd.models.zoo.resnet import resnet50_graph_def
+
+    dev = torch.device("cuda", 0)
+    g = Graph.from_graph_def(resnet50_graph_def(image_hw=(112, 112)))
+    with override(conv_lite_ws=True):
+        plan = CompiledFunction(g, {"images:0": ((2, 112, 112, 3), "UINT8")}, ["logits:0"], dev, strict=True)
+    assert plan.summary()["conv_lite"] > 0
+    imgs = torch.randint(0, 255, (2, 112, 112, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(9))
+    (got,) = plan({"images:0": imgs.to(dev)})
+    torch.cuda.synchronize()
+    (ref,) = Session(g, device=torch.device("cpu")).run(["logits:0"], {"images:0": imgs})
+    got, ref = got.float().cpu(), ref.float()
+    err = (got - ref).abs().max().item() / max((ref.max(-1).values - ref.min(-1).values).max().item(), 1e-6)
+    assert err < 0.03, err

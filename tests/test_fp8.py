@@ -285,6 +285,13 @@ def test_inception_v3_fp8_plan_gpu():
     lh = host({"images:0": img})[0]
     ld = dev({"images:0": img.to(DEV)})[0].cpu()
     assert F.cosine_similarity(lh.flatten(), ld.flatten(), dim=0) > 0.99
+    # the opt-in DMA / MFMA-wave tile (cfg 9) in the same plan
+    from flink_tensorflow_amd.config import override
+
+    with override(conv_lite_ws=True):
+        ws = CompiledFunction(g, feeds, ["logits:0"], DEV, strict=True, precision="fp8", calibration=calib)
+    lw = ws({"images:0": img.to(DEV)})[0].cpu()
+    assert F.cosine_similarity(lh.flatten(), lw.flatten(), dim=0) > 0.99
 
 
 @pytest.mark.gpu
