@@ -246,6 +246,23 @@ def conv3x3_halo(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor, act=
 _NUM_CU: dict = {}
 
 
+class _PersistentCUs(dict):
+    """CU count the persistent kernels size their grid to: the device's, or fewer when
+    ``EngineConfig.persistent_cus`` caps it (room on the chip for the other compute lane's
+    kernels while a persistent kernel runs)."""
+
+    def __missing__(self, dev):
+        n = torch.cuda.get_device_properties(dev).multi_processor_count
+        from ..config import current
+
+        cap = int(getattr(current(), "persistent_cus", 0) or 0)
+        self[dev] = min(n, cap) if cap > 0 else n
+        return self[dev]
+
+
+_NUM_CU = _PersistentCUs()
+
+
 def conv3x3_c64(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor, act=None, out: torch.Tensor | None = None,
                 out_channel_offset: int = 0) -> torch.Tensor:
     """3x3 / s1 / SAME conv, 64 -> 64 channels, ``act(conv + bias)``; GPU: persistent
@@ -265,8 +282,6 @@ def conv3x3_c64(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor, act=N
         _check(out, "out", device=x.device)
         _check(bias, "bias", torch.float32, x.device)
         dev = x.device.index if x.device.index is not None else torch.cuda.current_device()
-        if dev not in _NUM_CU:
-            _NUM_CU[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
         _hip().conv3x3c64_bf16(x.data_ptr(), w_ohwi.data_ptr(), bias.data_ptr(), out.data_ptr(), N, H, W, out.shape[3],
                                out_channel_offset, a, _NUM_CU[dev], _stream())
         return out
@@ -326,8 +341,6 @@ def bottleneck_tail(x2: torch.Tensor, res: torch.Tensor | None, w3: torch.Tensor
         _check(b3, "b3", torch.float32, x2.device)
         _check(b1, "b1", torch.float32, x2.device)
         dev = x2.device.index if x2.device.index is not None else torch.cuda.current_device()
-        if dev not in _NUM_CU:
-            _NUM_CU[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
         if cx == 128:
             if y3_decimated:
                 raise ValueError("bottleneck_tail: decimated y3 is a CX = 64 variant")
@@ -1188,8 +1201,6 @@ def pw_res(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor, residual: to
             _check(t, n, device=x.device)
         _check(bias, "bias", torch.float32, x.device)
         dev = x.device.index if x.device.index is not None else torch.cuda.current_device()
-        if dev not in _NUM_CU:
-            _NUM_CU[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
         _hip().pw_res_bf16(x.data_ptr(), w_nk.data_ptr(), bias.data_ptr(), residual.data_ptr(), out.data_ptr(), M, N,
                            K_, out.shape[-1], out_channel_offset, residual.shape[-1], _NUM_CU[dev], _stream(), tp)
         return out
@@ -1227,8 +1238,6 @@ def pw_dual(x: torch.Tensor, x2: torch.Tensor, w_cat: torch.Tensor, bias: torch.
         _check(t, n, device=x.device)
     _check(bias, "bias", torch.float32, x.device)
     dev = x.device.index if x.device.index is not None else torch.cuda.current_device()
-    if dev not in _NUM_CU:
-        _NUM_CU[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
     _hip().pw_dual_bf16(x.data_ptr(), x2.data_ptr(), w_cat.data_ptr(), bias.data_ptr(), out.data_ptr(),
                         x.numel() // K1, N, K1, C2, out.shape[-1], out_channel_offset, _NUM_CU[dev], _stream())
     return out
