@@ -365,6 +365,7 @@ void launch_tile(const Fp8Params& p, int act, int cfg, hipStream_t s) {
 // wave 0 of the first 64 workgroups records s_memtime around each K-tile's phases.
 // WS (cfg 9): eight waves, the roles split as conv_pp.hip's conv_lite_ws — waves 0-3 run
 // only the MFMAs, waves 4-7 only issue the LDS-DMA (wave 4 + w stages wave w's pieces).
+// Inception-v3 measured 4.5 % slower with it (profiles/r04_w): opt-in (conv_lite_ws).
 template <bool OUT_FP8, int ACT, int BN_, int NSTG, bool MULTI, bool STAMP, bool WS>
 __device__ __forceinline__ void conv_lite_fp8_body(const Fp8Params& p, const Fp8Segs& sg) {
   static_assert(BN_ == 128 || BN_ == 96 || BN_ == 64, "channel tile 128, 96 or 64");
