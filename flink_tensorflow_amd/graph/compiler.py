@@ -111,6 +111,13 @@ def _cfg():
 
     return current()
 
+def _lite_fp8_cfg() -> int:
+    """kernels/fp8.hip cfg of the conv_lite_fp8 tile: 8, 9 (DMA / MFMA waves,
+    ``conv_lite_ws``) or 10 (the 192-wide channel tile allowed, ``fp8_lite_wide``)."""
+    c = _cfg()
+    return 9 if c.conv_lite_ws else (10 if c.fp8_lite_wide else 8)
+
+
 class CompileError(RuntimeError):
     pass
 
@@ -1246,7 +1253,7 @@ class CompiledFunction(TransformerLowering):
 
         # fp8 input: the 4-wave LDS-DMA tile (kernels/fp8.hip conv_lite_fp8, cfg 8); a bf16
         # input (the layer after the stem) is quantised on load by the register-staged kernel
-        cfg = (9 if _cfg().conv_lite_ws else 8) if (x.qscale is not None and _cfg().conv_impl == "lite") else -1
+        cfg = _lite_fp8_cfg() if (x.qscale is not None and _cfg().conv_impl == "lite") else -1
         # (an eight-wave 256-pixel tile on three LDS stages measured 5-40 % slower per layer
         # and -2 % in the bench: profiles/r04_d)
 
@@ -1255,8 +1262,8 @@ class CompiledFunction(TransformerLowering):
                                out_scale=_eff_scale(out), out=_target(out), out_channel_offset=_coff(out), chan_scale=cs,
                                cfg=cfg)
 
-        self._emit(node.name, "conv_fp8", run, [x], [out], {"impl": "conv_lite_fp8"} if cfg in (8, 9) else None)
-        if cfg in (8, 9):
+        self._emit(node.name, "conv_fp8", run, [x], [out], {"impl": "conv_lite_fp8"} if cfg in (8, 9, 10) else None)
+        if cfg in (8, 9, 10):
             self.conv_lite_layers = getattr(self, "conv_lite_layers", 0) + 1
         self.vals[(last.name, 0)] = out
         self._alias_fused_outputs(absorbed, out)
@@ -1574,10 +1581,11 @@ class CompiledFunction(TransformerLowering):
         self.params += [wq_dev, cs_dev, b_dev, lo_dev]
         self.fp8_layers += len(members)
 
-        def run(x=x, segs=segs, wq=wq_dev, ws=ws_dev, cs=cs_dev, b=b_dev, lo=lo_dev, xs=xs, wsp=_cfg().conv_lite_ws):
+        def run(x=x, segs=segs, wq=wq_dev, ws=ws_dev, cs=cs_dev, b=b_dev, lo=lo_dev, xs=xs, wsp=_cfg().conv_lite_ws,
+                wide=_cfg().fp8_lite_wide):
             F8.conv2d_nhwc_fp8_multi(_view(x), xs, wq, (1, 1), ws, b, lo,
                                      [(_target(v), a, e, _coff(v), _eff_scale(v) if v.qscale is not None else None)
-                                      for v, a, e in segs], chan_scale=cs, ws=wsp)
+                                      for v, a, e in segs], chan_scale=cs, ws=wsp, wide=wide)
 
         self._emit("+".join(m["conv"].name for m in members), "conv_fp8", run, [x], [v for v, _, _ in segs],
                    {"impl": "conv_lite_fp8_multi", "multi_out": True})
@@ -1646,8 +1654,7 @@ class CompiledFunction(TransformerLowering):
             wq_dev, ws_dev, cs_dev = self._dev(wq), self._dev(ws), self._dev(ws * x.qscale, torch.float32)
             self.params += [wq_dev, cs_dev, zero, b_dev]
             self.fp8_layers += 1
-            cfg = ((9 if _cfg().conv_lite_ws else 8) if (self.device.type == "cuda" and _cfg().conv_impl == "lite")
-                   else -1)
+            cfg = _lite_fp8_cfg() if (self.device.type == "cuda" and _cfg().conv_impl == "lite") else -1
 
             def run_conv(x=x, y=y, wq=wq_dev, ws=ws_dev, cs=cs_dev, zero=zero, cfg=cfg, xs=x.qscale):
                 F8.conv2d_nhwc_fp8(_view(x), xs, wq, (1, 1), ws, zero, act=K.ACT_NONE, out=y.buf, chan_scale=cs,

@@ -78,7 +78,8 @@ struct Fp8Params {
   int tiles_m, tiles_n;
   int prio;  // s_setprio(1) around each K-tile's MFMA cluster (fp8_prio)
   unsigned long long* stamp;  // conv_lite_fp8 STAMP diagnostics: [64 workgroups][64 K-tiles][5] clocks
-  int ws;                     // conv_lite_fp8 on DMA / MFMA waves (cfg 9, multi: ws argument)
+  int ws;                     // conv_lite_fp8 on DMA / MFMA waves (cfg 9, multi: mode bit 0)
+  int wide;                   // conv_lite_fp8 may pick the 192-wide channel tile (cfg 10, multi: mode bit 1)
 };
 
 // Multi-output epilogue of conv_lite_fp8 (horizontally fused sibling 1x1 convs of one
@@ -368,10 +369,11 @@ void launch_tile(const Fp8Params& p, int act, int cfg, hipStream_t s) {
 // Inception-v3 measured 4.5 % slower with it (profiles/r04_w): opt-in (conv_lite_ws).
 template <bool OUT_FP8, int ACT, int BN_, int NSTG, bool MULTI, bool STAMP, bool WS>
 __device__ __forceinline__ void conv_lite_fp8_body(const Fp8Params& p, const Fp8Segs& sg) {
-  static_assert(BN_ == 128 || BN_ == 96 || BN_ == 64, "channel tile 128, 96 or 64");
+  static_assert(BN_ == 192 || BN_ == 128 || BN_ == 96 || BN_ == 64, "channel tile 192, 128, 96 or 64");
   constexpr int BM = 128, BN = BN_;
   constexpr int NI = BN / 32;  // weight fragments per wave (a wave covers BN / 2 channels)
   constexpr int WQ = BN / 32;  // weight DMA rows-of-8 per wave
+  constexpr int QD = WQ > 4 ? WQ : 4;  // DMA pieces per wave and operand pair (X: 4)
   constexpr int XB = BM * BK, WB = BN * BK, STG = XB + WB;
   constexpr int OB = (OUT_FP8 && !MULTI) ? 1 : 2;  // MULTI stages bf16, quantises per segment at the store
   constexpr int OLD = BN * OB + 16;
@@ -399,10 +401,13 @@ __device__ __forceinline__ void conv_lite_fp8_body(const Fp8Params& p, const Fp8
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)p.w, 0, (int)((unsigned)p.Cout * (unsigned)p.K), 0x00020000);
   int pb[4], ihw[4];
-  unsigned wrow[4];
+  unsigned wrow[6];  // fixed size (WQ <= 6): see conv_pp.hip on template-sized arrays
   const int ohw = p.Ho * p.Wo;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < QD; ++q) {
+    const unsigned co = n0 + 8 * (WQ * wave + q) + drow;  // weight rows: WQ rows-of-8 per wave
+    wrow[q] = (q < WQ && co < (unsigned)p.Cout) ? co * (unsigned)p.K : 0x80000000u;
+    if (q >= 4) continue;
     const int r = 8 * (4 * wave + q) + drow;
     const int m = m0 + r;
     const bool live = m < p.M;
@@ -414,8 +419,6 @@ __device__ __forceinline__ void conv_lite_fp8_body(const Fp8Params& p, const Fp8
     const int iw0 = ow * p.sw - p.pw;
     pb[q] = ((n * p.H + ih0) * p.W + iw0) * p.Cin;
     ihw[q] = (ih0 << 16) | (iw0 & 0xFFFF);
-    const unsigned co = n0 + 8 * (WQ * wave + q) + drow;  // weight rows: WQ rows-of-8 per wave
-    wrow[q] = (q < WQ && co < (unsigned)p.Cout) ? co * (unsigned)p.K : 0x80000000u;
   }
   // K walk of this lane's chunk: k = kt * 128 + dchunk * 16 -> (tap, ci), tap -> (kh, kw)
   const int ntaps = p.KH * p.KW;
@@ -432,12 +435,14 @@ __device__ __forceinline__ void conv_lite_fp8_body(const Fp8Params& p, const Fp8
     uint8_t* bx = smem + stage * STG + 4 * wave * 8 * BK;
     uint8_t* bw = smem + stage * STG + XB + WQ * wave * 8 * BK;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int ih = (ihw[q] >> 16) + dih;
-      const int iw = ((ihw[q] << 16) >> 16) + diw;
-      const bool ok = kin && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(bx + q * 8 * BK), 16,
-                                               ok ? (unsigned)(pb[q] + toff) : 0x80000000u, 0, 0, 0);
+    for (int q = 0; q < QD; ++q) {
+      if (q < 4) {
+        const int ih = (ihw[q] >> 16) + dih;
+        const int iw = ((ihw[q] << 16) >> 16) + diw;
+        const bool ok = kin && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(bx + q * 8 * BK), 16,
+                                                 ok ? (unsigned)(pb[q] + toff) : 0x80000000u, 0, 0, 0);
+      }
       if (q < WQ) {
         const unsigned wo = (k < p.K && wrow[q] != 0x80000000u) ? wrow[q] + (unsigned)k : 0x80000000u;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 8 * BK), 16,
@@ -652,8 +657,9 @@ void launch_lite_fp8_t(Fp8Params p, int act, hipStream_t s, const Fp8Segs& sg) {
 
 // channel tile: the one of 128 / 96 / 64 that pads Cout least (ties go to the wider tile:
 // more reuse of each pixel row); one LDS stage when K fits one K-tile.  ``bn`` > 0 forces it.
-int lite_fp8_bn(int Cout) {
+int lite_fp8_bn(int Cout, bool wide = false) {
   int best = 128, pad = (Cout + 127) / 128 * 128;
+  if (wide && (Cout + 191) / 192 * 192 <= pad) best = 192, pad = (Cout + 191) / 192 * 192;
   for (int bn : {96, 64}) {
     const int pd = (Cout + bn - 1) / bn * bn;
     if (pd < pad) best = bn, pad = pd;
@@ -663,7 +669,7 @@ int lite_fp8_bn(int Cout) {
 
 template <bool OUT_FP8, bool MULTI = false>
 void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, const Fp8Segs& sg = Fp8Segs{}, int bn = 0) {
-  const int b = bn ? bn : lite_fp8_bn(p.Cout);
+  const int b = bn ? bn : lite_fp8_bn(p.Cout, p.wide && !p.ws);
   const bool one = p.K <= BK;
 #define FTM_LITE(BN_)                                                     \
   do {                                                                    \
@@ -672,6 +678,7 @@ void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, const Fp8Segs& 
   } while (0)
   if (b == 64) FTM_LITE(64);
   else if (b == 96) FTM_LITE(96);
+  else if (b == 192) FTM_LITE(192);
   else FTM_LITE(128);
 #undef FTM_LITE
 }
@@ -683,6 +690,7 @@ unsigned long long* g_lite_fp8_stamp = nullptr;
 // LITE_WS_CFG: the same tile on eight DMA / MFMA waves
 constexpr int LITE_CFG = 8;
 constexpr int LITE_WS_CFG = 9;
+constexpr int LITE_WIDE_CFG = 10;  // + the 192-wide channel tile (Cout 192 / 384 / 768 in one tile per 192)
 
 template <bool CONV>
 void launch_io(const Fp8Params& p, bool in_bf16, bool out_fp8, int act, int cfg, hipStream_t s) {
@@ -1125,9 +1133,10 @@ void conv2d_nhwc_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, 
   p.ldx = Cin;
   p.ldy = ldy; p.y_coff = y_coff;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (cfg == LITE_CFG || cfg == LITE_WS_CFG) {
+  if (cfg == LITE_CFG || cfg == LITE_WS_CFG || cfg == LITE_WIDE_CFG) {
     p.stamp = g_lite_fp8_stamp;
     p.ws = cfg == LITE_WS_CFG;
+    p.wide = cfg == LITE_WIDE_CFG;
     if (in_bf16) throw std::invalid_argument("conv2d_nhwc_fp8: the conv_lite tile takes fp8 input");
     if (ph >= 1024 || pw >= 1024 || H >= 16384 || W >= 16384) throw std::invalid_argument("conv2d_nhwc_fp8: geometry");
     if ((long)Cout * p.K >= (1L << 31)) throw std::invalid_argument("conv2d_nhwc_fp8: weights larger than 2 GiB");
@@ -1147,7 +1156,7 @@ void conv2d_nhwc_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, 
 // order, every bound a multiple of 16; lo: fp32 [Cout] lower clamp (0 ReLU / -inf none).
 void conv2d_nhwc_fp8_multi(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t lo, int N, int H,
                            int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw,
-                           int Ho, int Wo, pybind11::list segs, uintptr_t stream, int ws) {
+                           int Ho, int Wo, pybind11::list segs, uintptr_t stream, int mode) {
   const int ns = (int)pybind11::len(segs);
   if (ns < 1 || ns > MAX_SEGS) throw std::invalid_argument("conv2d_nhwc_fp8_multi: 1.." + std::to_string(MAX_SEGS) + " segments");
   if (Cin % 16 || Cout % 16) throw std::invalid_argument("conv2d_nhwc_fp8_multi: Cin / Cout % 16 != 0");
@@ -1195,7 +1204,8 @@ void conv2d_nhwc_fp8_multi(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t 
   p.K = KH * KW * Cin;
   p.ldx = Cin;
   if ((long)Cout * p.K >= (1L << 31)) throw std::invalid_argument("conv2d_nhwc_fp8_multi: weights larger than 2 GiB");
-  p.ws = ws;
+  p.ws = mode & 1;
+  p.wide = (mode >> 1) & 1;
   launch_lite_fp8<false, true>(p, ACT_NONE, reinterpret_cast<hipStream_t>(stream), sg);
   FTM_CHECK_LAUNCH();
 }

@@ -110,7 +110,7 @@ def test_conv_fp8_configs_gpu(cfg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("c", [8, 9])
+@pytest.mark.parametrize("c", [8, 9, 10])
 def test_conv_fp8_lite_shapes_gpu(c):
     """conv_lite_fp8 (cfg 8, the 4-wave LDS-DMA tile; cfg 9, the same tile on DMA / MFMA
     waves where the channel tile is <= 96): Cin not a multiple of the 128-byte K-tile (288,
@@ -127,6 +127,10 @@ def test_conv_fp8_lite_shapes_gpu(c):
     _conv_case(128, 448, 1, 1, (0, 0, 0, 0), False, True, c, N=2, H=9, W=9)      # K 128 exactly, BN 64
     _conv_case(96, 96, 3, 1, (1, 1, 1, 1), False, True, c, offset=32, extra=64)   # BN 96
     _conv_case(48, 160, (1, 7), 1, (0, 0, 3, 3), False, False, c, N=2, H=9, W=9)  # BN 96, 2 tiles
+    # cfg 10's 192-wide tile: Cout 192 / 384, a Cout tail (160) and a concat offset
+    _conv_case(160, 192, (7, 1), 1, (3, 3, 0, 0), False, True, c, N=2, H=17, W=17)
+    _conv_case(288, 384, 3, 1, (1, 1, 1, 1), False, False, c, N=1, H=9, W=9)
+    _conv_case(192, 160, (1, 7), 1, (0, 0, 3, 3), False, True, c, offset=32, extra=64, N=2, H=9, W=9)
     # long K walks (the per-lane tap / channel walk over 65-74 K-tiles)
     _conv_case(1040, 64, 3, 1, (1, 1, 1, 1), False, True, c, N=1, H=7, W=7)       # 74 K-tiles
     _conv_case(8320, 96, 1, 1, (0, 0, 0, 0), False, False, c, N=1, H=5, W=5)      # 65 K-tiles
@@ -229,8 +233,9 @@ def test_avgpool_bias_act_gpu(out_fp8):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("C,wsp", [(96, False), (192, False), (192, True)])
-def test_conv_fp8_multi_output_gpu(C, wsp):
+@pytest.mark.parametrize("C,wsp,wide", [(96, False, False), (192, False, False), (192, True, False),
+                                        (192, False, True)])
+def test_conv_fp8_multi_output_gpu(C, wsp, wide):
     """Sibling 1x1 convs as one GEMM with a multi-destination epilogue: fp8 segments of
     different scales (one at a concat offset), a bf16 segment, ReLU and no-act channels;
     against the host reference of the same kernel.  C 192 takes the two-stage tile, ``wsp``
@@ -258,7 +263,7 @@ def test_conv_fp8_multi_output_gpu(C, wsp):
     ref = outs("cpu")
     Q.conv2d_nhwc_fp8_multi(xq, sx, wq, (1, 1), ws, b, lo, segs(ref))
     got = outs(DEV)
-    Q.conv2d_nhwc_fp8_multi(xq.to(DEV), sx, wq.to(DEV), (1, 1), ws.to(DEV), b.to(DEV), lo.to(DEV), segs(got), ws=wsp)
+    Q.conv2d_nhwc_fp8_multi(xq.to(DEV), sx, wq.to(DEV), (1, 1), ws.to(DEV), b.to(DEV), lo.to(DEV), segs(got), ws=wsp, wide=wide)
     torch.cuda.synchronize()
     for i, (r, g) in enumerate(zip(ref, got)):
         g = g.cpu()
