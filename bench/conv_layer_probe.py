@@ -56,7 +56,7 @@ def main():
                     K.conv2d_nhwc(x, w, b, res, (s, s), (pad, pad, pad, pad), (1, 1), K.ACT_RELU, out=y)
             else:  # pp: the 8-wave ping-pong tiles; lite: the 4-wave 128x128 LDS-DMA tile
                 cp = K.ConvPP([((B, H, W, Cin), (k, k), (s, s), (pad, pad), (1, 1))], Cout, (OH, OW), dev,
-                              tile={"lite": 2, "lite32": 3, "ws": 4}.get(impl, 0 if Cout >= 256 else 1))
+                              tile={"lite": 2, "lite32": 3, "ws": 4, "wide": 5}.get(impl, 0 if Cout >= 256 else 1))
                 w2 = w.reshape(Cout, -1)
 
                 def fn(cp=cp, w2=w2):

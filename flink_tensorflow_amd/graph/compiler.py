@@ -111,11 +111,22 @@ def _cfg():
 
     return current()
 
+def _lite_tile(Cout: int, dual: bool = False) -> int:
+    """kernels/conv_pp.hip tile of a bf16 conv_lite layer: 2 (128x128), 4 (the same on DMA /
+    MFMA waves, ``conv_lite_ws``) or 5 (128x256 with a 32-deep K-tile for Cout >= 256,
+    ``conv_lite_wide``: the input tile staged once per 256 channels)."""
+    c = _cfg()
+    if c.conv_lite_wide and Cout >= 256:
+        return 5
+    return 4 if (c.conv_lite_ws and not dual) else 2
+
+
 def _lite_fp8_cfg() -> int:
     """kernels/fp8.hip cfg of the conv_lite_fp8 tile: 8, 9 (DMA / MFMA waves,
-    ``conv_lite_ws``) or 10 (the 192-wide channel tile allowed, ``fp8_lite_wide``)."""
+    ``conv_lite_ws``), 10 (the 192-wide channel tile allowed, ``fp8_lite_wide`` 1) or 11
+    (the tile staging the fewest rows, 160 and 192 included, ``fp8_lite_wide`` 2)."""
     c = _cfg()
-    return 9 if c.conv_lite_ws else (10 if c.fp8_lite_wide else 8)
+    return 9 if c.conv_lite_ws else {0: 8, 1: 10, 2: 11}[int(c.fp8_lite_wide)]
 
 
 class CompileError(RuntimeError):
@@ -811,7 +822,7 @@ class CompiledFunction(TransformerLowering):
                 # stage 3/4 reduces: the 4-wave LDS-DMA tile beats the 256x256 ping-pong GEMM
                 # (stage 3: 37.8 vs 43.5 µs, profiles/r03_conv) and leaves room on the CU
                 cl = K.ConvPP([(tuple(xin.shape), (1, 1), (1, 1), (0, 0), (1, 1))], Cout, tuple(out.shape[1:3]),
-                              self.device, tile=4 if _cfg().conv_lite_ws else 2)
+                              self.device, tile=_lite_tile(Cout))
 
                 def run_cl(xin=xin, out=out, cl=cl, w_nk=w_nk, bz=bz, act=act):
                     cl([xin.buf], w_nk, bz, None, act, out=_target(out), out_channel_offset=_coff(out))
@@ -888,7 +899,7 @@ class CompiledFunction(TransformerLowering):
             # (kernels/conv_pp.hip conv_lite): 6-24 % faster than the register-staged igemm
             # per layer and 64 KiB of LDS, so it shares a CU with the sibling lane
             cl = K.ConvPP([(tuple(xin.shape), (KHe, KWe), (sh, sw), (pt, pl), (dh, dw))], Cout, tuple(out.shape[1:3]),
-                          self.device, tile=4 if _cfg().conv_lite_ws else 2)  # tiles 3 (32-deep K), 256x128 (4 or 8 waves) and 3-stage
+                          self.device, tile=_lite_tile(Cout))  # tiles 3 (32-deep K), 256x128 (4 or 8 waves) and 3-stage
             # variants (raw-barrier, counted vmcnt) measured slower: profiles/r03_conv, r04_a, r04_c
 
             def run(xin=xin, out=out, res_val=res_val, cl=cl, w2=w_dev.reshape(Cout, -1), b_dev=b_dev):  # noqa: F811
@@ -978,11 +989,11 @@ class CompiledFunction(TransformerLowering):
             # stage 2's 200k-row GEMM stays on the igemm (141 vs 158 µs, profiles/r03_operating_points)
             xs0 = (tuple(xin.shape), (1, 1), (1, 1), (0, 0), (1, 1))
             lite = {s2: K.ConvPP([xs0, (tuple(x2.shape), (1, 1), (s2, s2), (0, 0), (1, 1))], Cout, (Ho, Wo),
-                                 self.device, tile=2)}
+                                 self.device, tile=_lite_tile(Cout, dual=True))}
             N2, H2, W2, _ = x2.shape
             if s2 == 2 and H2 % 2 == 0 and W2 % 2 == 0:
                 lite[1] = K.ConvPP([xs0, ((N2, H2 // 2, W2 // 2, C2), (1, 1), (1, 1), (0, 0), (1, 1))], Cout, (Ho, Wo),
-                                   self.device, tile=2)
+                                   self.device, tile=_lite_tile(Cout, dual=True))
 
             def run(xin=xin, x2=x2, out=out, w_dev=w_dev, b_dev=b_dev, s2cfg=s2cfg, lite=lite):  # noqa: F811
                 lite[s2cfg["s2"]]([xin.buf, x2.buf], w_dev, b_dev, None, act, out=_target(out),
@@ -1262,8 +1273,8 @@ class CompiledFunction(TransformerLowering):
                                out_scale=_eff_scale(out), out=_target(out), out_channel_offset=_coff(out), chan_scale=cs,
                                cfg=cfg)
 
-        self._emit(node.name, "conv_fp8", run, [x], [out], {"impl": "conv_lite_fp8"} if cfg in (8, 9, 10) else None)
-        if cfg in (8, 9, 10):
+        self._emit(node.name, "conv_fp8", run, [x], [out], {"impl": "conv_lite_fp8"} if cfg in (8, 9, 10, 11) else None)
+        if cfg in (8, 9, 10, 11):
             self.conv_lite_layers = getattr(self, "conv_lite_layers", 0) + 1
         self.vals[(last.name, 0)] = out
         self._alias_fused_outputs(absorbed, out)
@@ -1582,7 +1593,7 @@ class CompiledFunction(TransformerLowering):
         self.fp8_layers += len(members)
 
         def run(x=x, segs=segs, wq=wq_dev, ws=ws_dev, cs=cs_dev, b=b_dev, lo=lo_dev, xs=xs, wsp=_cfg().conv_lite_ws,
-                wide=_cfg().fp8_lite_wide):
+                wide=int(_cfg().fp8_lite_wide)):
             F8.conv2d_nhwc_fp8_multi(_view(x), xs, wq, (1, 1), ws, b, lo,
                                      [(_target(v), a, e, _coff(v), _eff_scale(v) if v.qscale is not None else None)
                                       for v, a, e in segs], chan_scale=cs, ws=wsp, wide=wide)

@@ -403,17 +403,25 @@ FTM_DEVICE int lite_slot(int row, int chunk) {
 // STAMP (diagnostics, bench/conv_stamp_probe.py): wave 0 of the first 64 workgroups records
 // s_memtime before the vmcnt wait, after it, after the barrier, after the DMA issue and after
 // the MFMA issue of each of the first 64 K-tiles (lane 0, vector stores).
-template <int ACT, bool HAS_RES, int BK, bool DUAL = false, bool STAMP = false>
+// BN_ = 256 (tile 5, with BK = 32): a 128 x 256 tile — each wave 64 pixels x 128 channels —
+// for Cout >= 256, so one workgroup stages the input tile once for 256 channels where two
+// 128-wide tiles stage it twice: 24 KiB per 32-deep K-tile for 128 x 256 outputs, 25 % fewer
+// bytes per MAC than the 128x128 / 64-deep tile (the fp8 192-wide tile's gain: r04_ac).
+template <int ACT, bool HAS_RES, int BK, bool DUAL = false, bool STAMP = false, int BN_ = 128>
 __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
   // BK = 64: 128-B LDS rows, 2 x 32 KiB stages, 2 MFMA steps per K-tile.
   // BK = 32: 64-B rows, 2 x 16 KiB stages (the igemm's footprint: four workgroups per CU),
   //          1 MFMA step per K-tile; 16-B chunk slot = chunk ^ ((row >> 2) & 3) keeps the
   //          16-lane ds_read_b128 groups on distinct banks.
-  constexpr int BM = 128, BN = 128;
+  constexpr int BM = 128, BN = BN_;
   constexpr int ROWB = BK * 2;             // LDS row bytes
   constexpr int CPR = ROWB / 16;           // 16-B chunks per row
   constexpr int RPI = 1024 / ROWB;         // rows per DMA wave-instruction
-  constexpr int QX = BM / RPI / 4;         // DMA instructions per wave per operand
+  constexpr int QX = BM / RPI / 4;         // DMA instructions per wave for the pixel image
+  constexpr int QW = BN / RPI / 4;         // ... for the weight image
+  constexpr int QM = QX > QW ? QX : QW;
+  constexpr int NI = BN / 32;              // channel fragments per wave (BN / 2 channels)
+  static_assert(QW <= 4 && (BN == 128 || BN == 256), "channel tile 128 or 256");
   constexpr int XB = BM * ROWB, WB = BN * ROWB, STG = XB + WB;
   constexpr int OPITCH = BN * 2 + 16;
   constexpr int LDS = 2 * STG > BM * OPITCH ? 2 * STG : BM * OPITCH;
@@ -451,7 +459,12 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
                                             0x00020000);
   const int ohw = p.OH * p.OW;
 #pragma unroll
-  for (int q = 0; q < QX; ++q) {
+  for (int q = 0; q < QM; ++q) {
+    if (q < QW) {
+      const unsigned co = n0 + RPI * (QW * wave + q) + drow;
+      offw[q] = co < (unsigned)p.N ? (co * p.ldw + dchunk * 8) * 2u : 0x80000000u;
+    }
+    if (q >= QX) continue;
     const int r = RPI * (QX * wave + q) + drow;
     const int m = m0 + r;
     const bool live = m < p.M;
@@ -464,8 +477,6 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
     pb[q] = ((n * S.H + ih0) * S.W + iw0) * S.C * 2 + dchunk * 16;
     hw[q] = (ih0 << 16) | (iw0 & 0xFFFF);
     if constexpr (DUAL) pb1[q] = live ? ((n * S1.H + oh * S1.sh) * S1.W + ow * S1.sw) * S1.C * 2 + dchunk * 16 : -1;
-    const unsigned co = n0 + r;
-    offw[q] = co < (unsigned)p.N ? (co * p.ldw + dchunk * 8) * 2u : 0x80000000u;
   }
   // The K walk (channel chunk, filter column, filter row) advances incrementally in scalar
   // registers: no table read inside the loop (a ktab load there is a vector load — the
@@ -479,13 +490,15 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
         const int delta1 = (kt_dma - p.nk0) * BK * 2;
         ++kt_dma;
         uint8_t* bx = smem + stage * STG + QX * wave * RPI * ROWB;
-        uint8_t* bw = bx + XB;
+        uint8_t* bw = smem + stage * STG + XB + QW * wave * RPI * ROWB;
 #pragma unroll
-        for (int q = 0; q < QX; ++q) {
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rx1, (__attribute__((address_space(3))) void*)(bx + q * 1024), 16,
-                                                   pb1[q] >= 0 ? (unsigned)(pb1[q] + delta1) : 0x80000000u, 0, 0, 0);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 1024), 16,
-                                                   offw[q], woff, 0, 0);
+        for (int q = 0; q < QM; ++q) {
+          if (q < QX)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rx1, (__attribute__((address_space(3))) void*)(bx + q * 1024), 16,
+                                                     pb1[q] >= 0 ? (unsigned)(pb1[q] + delta1) : 0x80000000u, 0, 0, 0);
+          if (q < QW)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 1024), 16,
+                                                     offw[q], woff, 0, 0);
         }
         return;
       }
@@ -501,24 +514,27 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
       }
     }
     uint8_t* bx = smem + stage * STG + QX * wave * RPI * ROWB;
-    uint8_t* bw = bx + XB;
+    uint8_t* bw = smem + stage * STG + XB + QW * wave * RPI * ROWB;
 #pragma unroll
-    for (int q = 0; q < QX; ++q) {
-      const int ih = (hw[q] >> 16) + dih;
-      const int iw = ((hw[q] << 16) >> 16) + diw;
-      const bool ok = (unsigned)ih < (unsigned)S.H && (unsigned)iw < (unsigned)S.W;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(bx + q * 1024), 16,
-                                               ok ? (unsigned)(pb[q] + delta) : 0x80000000u, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 1024), 16,
-                                               offw[q], woff, 0, 0);
+    for (int q = 0; q < QM; ++q) {
+      if (q < QX) {
+        const int ih = (hw[q] >> 16) + dih;
+        const int iw = ((hw[q] << 16) >> 16) + diw;
+        const bool ok = (unsigned)ih < (unsigned)S.H && (unsigned)iw < (unsigned)S.W;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(bx + q * 1024), 16,
+                                                 ok ? (unsigned)(pb[q] + delta) : 0x80000000u, 0, 0, 0);
+      }
+      if (q < QW)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(bw + q * 1024), 16,
+                                                 offw[q], woff, 0, 0);
     }
   };
 
   const int frow = lane & 15;
   const int fq = lane >> 4;
-  f32x4 acc[4][4];  // [channel fragment i][pixel fragment j]
+  f32x4 acc[NI][4];  // [channel fragment i][pixel fragment j]
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -546,13 +562,14 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       const int sl = lite_slot<CPR>(frow, ks * 4 + fq) << 4;
-      bf16x8 a[4], b[4];
+      bf16x8 a[NI], b[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ws + (wn * 64 + i * 16 + frow) * ROWB + sl);
+      for (int i = 0; i < NI; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(ws + (wn * (BN / 2) + i * 16 + frow) * ROWB + sl);
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(xs + (wm * 64 + j * 16 + frow) * ROWB + sl);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
@@ -571,8 +588,8 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
   __syncthreads();  // every wave is done with the stage images: the epilogue tile reuses them
 
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int cl = wn * 64 + i * 16 + fq * 4;
+  for (int i = 0; i < NI; ++i) {
+    const int cl = wn * (BN / 2) + i * 16 + fq * 4;
     f32x4 bv = {0.f, 0.f, 0.f, 0.f};
     if (p.bias && n0 + cl < p.N) bv = *reinterpret_cast<const f32x4*>(p.bias + n0 + cl);
 #pragma unroll
@@ -786,10 +803,20 @@ void launch_lite_ws(const CPParams& p, hipStream_t s) {
   else hipLaunchKernelGGL((conv_lite_ws_kernel<ACT, false>), grid, block, 0, s, p);
 }
 
-// lite_bk: 64 (tile 2) or 32 (tile 3)
-template <int ACT, int BK>
+// lite_bk: 64 (tile 2) or 32 (tile 3; tile 5 with BN 256)
+template <int ACT, int BK, int BN = 128>
 void launch_lite(const CPParams& p, hipStream_t s, bool dual = false) {
   const dim3 grid(p.tiles_m * p.tiles_n), block(256);
+  if constexpr (BN == 256) {
+    if (dual) {
+      if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, BK, true, false, BN>), grid, block, 0, s, p);
+      else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, BK, true, false, BN>), grid, block, 0, s, p);
+    } else {
+      if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, BK, false, false, BN>), grid, block, 0, s, p);
+      else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, BK, false, false, BN>), grid, block, 0, s, p);
+    }
+    return;
+  }
   if constexpr (BK == 64) {
     if (dual) {
       if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, BK, true>), grid, block, 0, s, p);
@@ -922,8 +949,8 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
       p.KW = KW;
       p.dh = dh;
       p.dw = dw;
-      p.nk0 = (int)(K / 64);
-    } else if (tile == 2) {  // conv_lite's second source: pointwise, unpadded, in range
+      p.nk0 = (int)(K / (tile == 5 ? 32 : 64));  // K-tiles of source 0 in the tile's K-tile depth
+    } else if (tile == 2 || tile == 5) {  // conv_lite's second source: pointwise, unpadded, in range
       need(KH == 1 && KW == 1 && S.ph == 0 && S.pw == 0, "the 4-wave tile's second source must be 1x1 unpadded");
       need((OH - 1) * S.sh < S.H && (OW - 1) * S.sw < S.W, "second source smaller than the output grid");
     }
@@ -944,13 +971,15 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   p.OH = OH; p.OW = OW;
   p.ldw = (int)K; p.ldy = ldy; p.y_coff = y_coff; p.ldr = ldr;
   p.stamp = tile == 2 ? g_lite_stamp : nullptr;
-  need(tile >= 0 && tile <= 4,
-       "tile must be 0 (256x256), 1 (512x128), 2 / 3 (128x128, 4 waves, K-tile 64 / 32), 4 (128x128, DMA / MFMA waves)");
+  need(tile >= 0 && tile <= 5,
+       "tile must be 0 (256x256), 1 (512x128), 2 / 3 (128x128, 4 waves, K-tile 64 / 32), 4 (128x128, DMA / MFMA "
+       "waves), 5 (128x256, 4 waves, K-tile 32)");
   need(tile != 4 || ns == 1, "the wave-specialised tile takes one source");
   const bool lite = tile >= 2;
-  need(!lite || ((ns == 1 || tile == 2) && splits <= 1), "the 4-wave tile takes no split-K (two sources: tile 2)");
+  need(!lite || ((ns == 1 || tile == 2 || tile == 5) && splits <= 1),
+       "the 4-wave tiles take no split-K (two sources: tiles 2 and 5)");
   need(tile != 3 || p.s[0].C % 32 == 0, "the 32-deep 4-wave tile needs Cin % 32 == 0");
-  const int BM = tile == 1 ? 512 : lite ? 128 : 256, BN = tile == 1 ? 128 : lite ? 128 : 256;
+  const int BM = tile == 1 ? 512 : lite ? 128 : 256, BN = tile == 1 ? 128 : tile == 5 ? 256 : lite ? 128 : 256;
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (Cout + BN - 1) / BN;
   const int nk = p.K / 64;
@@ -967,6 +996,10 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   if (tile == 4) {
     if (act == ACT_RELU) launch_lite_ws<ACT_RELU>(p, s);
     else if (act == ACT_NONE) launch_lite_ws<ACT_NONE>(p, s);
+    else throw std::invalid_argument("conv_pp: unsupported activation");
+  } else if (tile == 5) {
+    if (act == ACT_RELU) launch_lite<ACT_RELU, 32, 256>(p, s, ns == 2);
+    else if (act == ACT_NONE) launch_lite<ACT_NONE, 32, 256>(p, s, ns == 2);
     else throw std::invalid_argument("conv_pp: unsupported activation");
   } else if (lite) {
     switch (act * 2 + (tile == 3)) {

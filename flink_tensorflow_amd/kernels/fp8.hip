@@ -79,7 +79,8 @@ struct Fp8Params {
   int prio;  // s_setprio(1) around each K-tile's MFMA cluster (fp8_prio)
   unsigned long long* stamp;  // conv_lite_fp8 STAMP diagnostics: [64 workgroups][64 K-tiles][5] clocks
   int ws;                     // conv_lite_fp8 on DMA / MFMA waves (cfg 9, multi: mode bit 0)
-  int wide;                   // conv_lite_fp8 may pick the 192-wide channel tile (cfg 10, multi: mode bit 1)
+  int wide;                   // conv_lite_fp8 channel tiles: 1 = + 192 (cfg 10), 2 = fewest staged rows over
+                              // 192 / 160 / 128 / 96 / 64 (cfg 11); multi: mode >> 1
 };
 
 // Multi-output epilogue of conv_lite_fp8 (horizontally fused sibling 1x1 convs of one
@@ -369,7 +370,7 @@ void launch_tile(const Fp8Params& p, int act, int cfg, hipStream_t s) {
 // Inception-v3 measured 4.5 % slower with it (profiles/r04_w): opt-in (conv_lite_ws).
 template <bool OUT_FP8, int ACT, int BN_, int NSTG, bool MULTI, bool STAMP, bool WS>
 __device__ __forceinline__ void conv_lite_fp8_body(const Fp8Params& p, const Fp8Segs& sg) {
-  static_assert(BN_ == 192 || BN_ == 128 || BN_ == 96 || BN_ == 64, "channel tile 192, 128, 96 or 64");
+  static_assert(BN_ == 192 || BN_ == 160 || BN_ == 128 || BN_ == 96 || BN_ == 64, "channel tile 192 .. 64");
   constexpr int BM = 128, BN = BN_;
   constexpr int NI = BN / 32;  // weight fragments per wave (a wave covers BN / 2 channels)
   constexpr int WQ = BN / 32;  // weight DMA rows-of-8 per wave
@@ -657,19 +658,28 @@ void launch_lite_fp8_t(Fp8Params p, int act, hipStream_t s, const Fp8Segs& sg) {
 
 // channel tile: the one of 128 / 96 / 64 that pads Cout least (ties go to the wider tile:
 // more reuse of each pixel row); one LDS stage when K fits one K-tile.  ``bn`` > 0 forces it.
-int lite_fp8_bn(int Cout, bool wide = false) {
+int lite_fp8_bn(int Cout, int wide = 0) {
   int best = 128, pad = (Cout + 127) / 128 * 128;
-  if (wide && (Cout + 191) / 192 * 192 <= pad) best = 192, pad = (Cout + 191) / 192 * 192;
+  if (wide == 1 && (Cout + 191) / 192 * 192 <= pad) best = 192, pad = (Cout + 191) / 192 * 192;
   for (int bn : {96, 64}) {
     const int pd = (Cout + bn - 1) / bn * bn;
     if (pd < pad) best = bn, pad = pd;
+  }
+  if (wide != 2) return best;
+  // wide: the tile that stages the fewest rows per 128-pixel tile and K-tile — the channel
+  // tiles' count x (128 pixel rows + BN weight rows), as the K loop is bound by the bytes it
+  // fills (profiles/r04_ac); ties go to the wider tile
+  int cost = (Cout + best - 1) / best * (128 + best);
+  for (int bn : {192, 160, 128, 96, 64}) {
+    const int c = (Cout + bn - 1) / bn * (128 + bn);
+    if (c < cost || (c == cost && bn > best)) best = bn, cost = c;
   }
   return best;
 }
 
 template <bool OUT_FP8, bool MULTI = false>
 void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, const Fp8Segs& sg = Fp8Segs{}, int bn = 0) {
-  const int b = bn ? bn : lite_fp8_bn(p.Cout, p.wide && !p.ws);
+  const int b = bn ? bn : lite_fp8_bn(p.Cout, p.ws ? 0 : p.wide);
   const bool one = p.K <= BK;
 #define FTM_LITE(BN_)                                                     \
   do {                                                                    \
@@ -679,6 +689,7 @@ void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, const Fp8Segs& 
   if (b == 64) FTM_LITE(64);
   else if (b == 96) FTM_LITE(96);
   else if (b == 192) FTM_LITE(192);
+  else if (b == 160) FTM_LITE(160);
   else FTM_LITE(128);
 #undef FTM_LITE
 }
@@ -690,7 +701,8 @@ unsigned long long* g_lite_fp8_stamp = nullptr;
 // LITE_WS_CFG: the same tile on eight DMA / MFMA waves
 constexpr int LITE_CFG = 8;
 constexpr int LITE_WS_CFG = 9;
-constexpr int LITE_WIDE_CFG = 10;  // + the 192-wide channel tile (Cout 192 / 384 / 768 in one tile per 192)
+constexpr int LITE_WIDE_CFG = 10;   // + the 192-wide channel tile (Cout 192 / 384 / 768 in one tile per 192)
+constexpr int LITE_WIDE2_CFG = 11;  // the tile staging the fewest rows, 160 and 192 included
 
 template <bool CONV>
 void launch_io(const Fp8Params& p, bool in_bf16, bool out_fp8, int act, int cfg, hipStream_t s) {
@@ -1133,10 +1145,10 @@ void conv2d_nhwc_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, 
   p.ldx = Cin;
   p.ldy = ldy; p.y_coff = y_coff;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (cfg == LITE_CFG || cfg == LITE_WS_CFG || cfg == LITE_WIDE_CFG) {
+  if (cfg == LITE_CFG || cfg == LITE_WS_CFG || cfg == LITE_WIDE_CFG || cfg == LITE_WIDE2_CFG) {
     p.stamp = g_lite_fp8_stamp;
     p.ws = cfg == LITE_WS_CFG;
-    p.wide = cfg == LITE_WIDE_CFG;
+    p.wide = cfg == LITE_WIDE_CFG ? 1 : cfg == LITE_WIDE2_CFG ? 2 : 0;
     if (in_bf16) throw std::invalid_argument("conv2d_nhwc_fp8: the conv_lite tile takes fp8 input");
     if (ph >= 1024 || pw >= 1024 || H >= 16384 || W >= 16384) throw std::invalid_argument("conv2d_nhwc_fp8: geometry");
     if ((long)Cout * p.K >= (1L << 31)) throw std::invalid_argument("conv2d_nhwc_fp8: weights larger than 2 GiB");
@@ -1205,7 +1217,7 @@ void conv2d_nhwc_fp8_multi(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t 
   p.ldx = Cin;
   if ((long)Cout * p.K >= (1L << 31)) throw std::invalid_argument("conv2d_nhwc_fp8_multi: weights larger than 2 GiB");
   p.ws = mode & 1;
-  p.wide = (mode >> 1) & 1;
+  p.wide = (mode >> 1) & 3;
   launch_lite_fp8<false, true>(p, ACT_NONE, reinterpret_cast<hipStream_t>(stream), sg);
   FTM_CHECK_LAUNCH();
 }

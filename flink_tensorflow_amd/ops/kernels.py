@@ -663,12 +663,12 @@ class ConvPP:
         self.tile = conv_pp_tile(Cout) if tile is None else tile
         if self.tile in (3, 4) and len(self.srcs) != 1:
             raise ValueError("conv_pp: the 32-deep 4-wave tile and the wave-specialised tile take one source")
-        if self.tile == 2 and len(self.srcs) == 2:
+        if self.tile in (2, 5) and len(self.srcs) == 2:
             (xs1, k1, st1, pd1, dl1) = self.srcs[1]
             if tuple(k1) != (1, 1) or tuple(pd1) != (0, 0) or (self.OH - 1) * st1[0] >= xs1[1] \
                     or (self.OW - 1) * st1[1] >= xs1[2]:
                 raise ValueError("conv_pp: the 4-wave tile's second source must be 1x1, unpadded, in range")
-        self.splits = (1 if self.tile in (2, 3, 4) else conv_pp_splits(self.M, Cout, self.K, self.tile)) if splits is None \
+        self.splits = (1 if self.tile in (2, 3, 4, 5) else conv_pp_splits(self.M, Cout, self.K, self.tile)) if splits is None \
             else splits
         self.ktab = conv_pp_ktab([(xs[1], xs[2], xs[3], k[0], k[1], dl[0], dl[1])
                                   for xs, k, _, _, dl in self.srcs]).to(device)

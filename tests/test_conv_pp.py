@@ -63,6 +63,15 @@ CASES = [
     ("ws_3x3s2", [((3, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 4, None),
     ("ws_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (7, 7), True, "relu", 4, None),
     ("ws_1x1", [((2, 14, 14, 256), (1, 1), (1, 1), (0, 0), (1, 1))], 1024, (14, 14), True, None, 4, None),
+    # the 128x256 tile with a 32-deep K-tile: 3x3 s1 / s2, N tail (Cout 200 / 456), M tail,
+    # residual, 1x1, and two sources (expand + strided projection)
+    ("wide_3x3", [((3, 14, 14, 256), (3, 3), (1, 1), (1, 1), (1, 1))], 256, (14, 14), False, "relu", 5, None),
+    ("wide_3x3s2", [((3, 28, 28, 128), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 5, None),
+    ("wide_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 456, (7, 7), True, "relu", 5, None),
+    ("wide_n200", [((2, 9, 9, 64), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (9, 9), False, None, 5, None),
+    ("wide_1x1", [((2, 14, 14, 1024), (1, 1), (1, 1), (0, 0), (1, 1))], 512, (14, 14), False, "relu", 5, None),
+    ("wide_dual", [((2, 14, 14, 128), (1, 1), (1, 1), (0, 0), (1, 1)),
+                   ((2, 28, 28, 256), (1, 1), (2, 2), (0, 0), (1, 1))], 512, (14, 14), False, "relu", 5, None),
 ]
 
 

@@ -110,7 +110,7 @@ def test_conv_fp8_configs_gpu(cfg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("c", [8, 9, 10])
+@pytest.mark.parametrize("c", [8, 9, 10, 11])
 def test_conv_fp8_lite_shapes_gpu(c):
     """conv_lite_fp8 (cfg 8, the 4-wave LDS-DMA tile; cfg 9, the same tile on DMA / MFMA
     waves where the channel tile is <= 96): Cin not a multiple of the 128-byte K-tile (288,
@@ -131,6 +131,9 @@ def test_conv_fp8_lite_shapes_gpu(c):
     _conv_case(160, 192, (7, 1), 1, (3, 3, 0, 0), False, True, c, N=2, H=17, W=17)
     _conv_case(288, 384, 3, 1, (1, 1, 1, 1), False, False, c, N=1, H=9, W=9)
     _conv_case(192, 160, (1, 7), 1, (0, 0, 3, 3), False, True, c, offset=32, extra=64, N=2, H=9, W=9)
+    # ... and its 160-wide tile (cfg 10 picks the fewest staged rows: 320 = 2 x 160, 448 = 3 x 160)
+    _conv_case(1280, 320, 1, 1, (0, 0, 0, 0), False, True, c, N=2, H=8, W=8)
+    _conv_case(448, 448, (1, 3), 1, (0, 0, 1, 1), False, False, c, N=2, H=8, W=8)
     # long K walks (the per-lane tap / channel walk over 65-74 K-tiles)
     _conv_case(1040, 64, 3, 1, (1, 1, 1, 1), False, True, c, N=1, H=7, W=7)       # 74 K-tiles
     _conv_case(8320, 96, 1, 1, (0, 0, 0, 0), False, False, c, N=1, H=5, W=5)      # 65 K-tiles
@@ -233,8 +236,8 @@ def test_avgpool_bias_act_gpu(out_fp8):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("C,wsp,wide", [(96, False, False), (192, False, False), (192, True, False),
-                                        (192, False, True)])
+@pytest.mark.parametrize("C,wsp,wide", [(96, False, 0), (192, False, 0), (192, True, 0), (192, False, 1),
+                                        (192, False, 2)])
 def test_conv_fp8_multi_output_gpu(C, wsp, wide):
     """Sibling 1x1 convs as one GEMM with a multi-destination epilogue: fp8 segments of
     different scales (one at a concat offset), a bf16 segment, ReLU and no-act channels;
