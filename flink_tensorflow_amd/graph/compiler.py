@@ -124,9 +124,10 @@ def _lite_tile(Cout: int, dual: bool = False) -> int:
 def _lite_fp8_cfg() -> int:
     """kernels/fp8.hip cfg of the conv_lite_fp8 tile: 8, 9 (DMA / MFMA waves,
     ``conv_lite_ws``), 10 (the 192-wide channel tile allowed, ``fp8_lite_wide`` 1) or 11
-    (the tile staging the fewest rows, 160 and 192 included, ``fp8_lite_wide`` 2)."""
+    (the tile staging the fewest rows, 160 and 192 included, ``fp8_lite_wide`` 2) or 12 (the
+    same over whole waves of 512 workgroups, ``fp8_lite_wide`` 3)."""
     c = _cfg()
-    return 9 if c.conv_lite_ws else {0: 8, 1: 10, 2: 11}[int(c.fp8_lite_wide)]
+    return 9 if c.conv_lite_ws else {0: 8, 1: 10, 2: 11, 3: 12}[int(c.fp8_lite_wide)]
 
 
 class CompileError(RuntimeError):
@@ -1273,8 +1274,8 @@ class CompiledFunction(TransformerLowering):
                                out_scale=_eff_scale(out), out=_target(out), out_channel_offset=_coff(out), chan_scale=cs,
                                cfg=cfg)
 
-        self._emit(node.name, "conv_fp8", run, [x], [out], {"impl": "conv_lite_fp8"} if cfg in (8, 9, 10, 11) else None)
-        if cfg in (8, 9, 10, 11):
+        self._emit(node.name, "conv_fp8", run, [x], [out], {"impl": "conv_lite_fp8"} if cfg in (8, 9, 10, 11, 12) else None)
+        if cfg in (8, 9, 10, 11, 12):
             self.conv_lite_layers = getattr(self, "conv_lite_layers", 0) + 1
         self.vals[(last.name, 0)] = out
         self._alias_fused_outputs(absorbed, out)

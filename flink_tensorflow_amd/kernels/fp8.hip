@@ -658,20 +658,28 @@ void launch_lite_fp8_t(Fp8Params p, int act, hipStream_t s, const Fp8Segs& sg) {
 
 // channel tile: the one of 128 / 96 / 64 that pads Cout least (ties go to the wider tile:
 // more reuse of each pixel row); one LDS stage when K fits one K-tile.  ``bn`` > 0 forces it.
-int lite_fp8_bn(int Cout, int wide = 0) {
+int lite_fp8_bn(int Cout, int wide = 0, int M = 0) {
   int best = 128, pad = (Cout + 127) / 128 * 128;
   if (wide == 1 && (Cout + 191) / 192 * 192 <= pad) best = 192, pad = (Cout + 191) / 192 * 192;
   for (int bn : {96, 64}) {
     const int pd = (Cout + bn - 1) / bn * bn;
     if (pd < pad) best = bn, pad = pd;
   }
-  if (wide != 2) return best;
+  if (wide < 2) return best;
   // wide: the tile that stages the fewest rows per 128-pixel tile and K-tile — the channel
   // tiles' count x (128 pixel rows + BN weight rows), as the K loop is bound by the bytes it
   // fills (profiles/r04_ac); ties go to the wider tile
-  int cost = (Cout + best - 1) / best * (128 + best);
+  // wide 3: the same over whole waves of workgroups — a grid short of two workgroups per CU
+  // (8x8 layers) takes the narrower tile that still fits one wave of 512
+  const long tm = (M + 127) / 128;
+  auto rows = [&](int bn) -> long {
+    const long nt = (Cout + bn - 1) / bn;
+    if (wide == 3) return (tm * nt + 511) / 512 * (128 + bn);
+    return nt * (128 + bn);
+  };
+  long cost = rows(best);
   for (int bn : {192, 160, 128, 96, 64}) {
-    const int c = (Cout + bn - 1) / bn * (128 + bn);
+    const long c = rows(bn);
     if (c < cost || (c == cost && bn > best)) best = bn, cost = c;
   }
   return best;
@@ -679,7 +687,7 @@ int lite_fp8_bn(int Cout, int wide = 0) {
 
 template <bool OUT_FP8, bool MULTI = false>
 void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, const Fp8Segs& sg = Fp8Segs{}, int bn = 0) {
-  const int b = bn ? bn : lite_fp8_bn(p.Cout, p.ws ? 0 : p.wide);
+  const int b = bn ? bn : lite_fp8_bn(p.Cout, p.ws ? 0 : p.wide, p.M);
   const bool one = p.K <= BK;
 #define FTM_LITE(BN_)                                                     \
   do {                                                                    \
@@ -703,6 +711,7 @@ constexpr int LITE_CFG = 8;
 constexpr int LITE_WS_CFG = 9;
 constexpr int LITE_WIDE_CFG = 10;   // + the 192-wide channel tile (Cout 192 / 384 / 768 in one tile per 192)
 constexpr int LITE_WIDE2_CFG = 11;  // the tile staging the fewest rows, 160 and 192 included
+constexpr int LITE_WIDE3_CFG = 12;  // ... counted over whole waves of 512 workgroups
 
 template <bool CONV>
 void launch_io(const Fp8Params& p, bool in_bf16, bool out_fp8, int act, int cfg, hipStream_t s) {
@@ -1145,10 +1154,10 @@ void conv2d_nhwc_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, 
   p.ldx = Cin;
   p.ldy = ldy; p.y_coff = y_coff;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (cfg == LITE_CFG || cfg == LITE_WS_CFG || cfg == LITE_WIDE_CFG || cfg == LITE_WIDE2_CFG) {
+  if (cfg == LITE_CFG || cfg == LITE_WS_CFG || cfg == LITE_WIDE_CFG || cfg == LITE_WIDE2_CFG || cfg == LITE_WIDE3_CFG) {
     p.stamp = g_lite_fp8_stamp;
     p.ws = cfg == LITE_WS_CFG;
-    p.wide = cfg == LITE_WIDE_CFG ? 1 : cfg == LITE_WIDE2_CFG ? 2 : 0;
+    p.wide = cfg == LITE_WIDE_CFG ? 1 : cfg == LITE_WIDE2_CFG ? 2 : cfg == LITE_WIDE3_CFG ? 3 : 0;
     if (in_bf16) throw std::invalid_argument("conv2d_nhwc_fp8: the conv_lite tile takes fp8 input");
     if (ph >= 1024 || pw >= 1024 || H >= 16384 || W >= 16384) throw std::invalid_argument("conv2d_nhwc_fp8: geometry");
     if ((long)Cout * p.K >= (1L << 31)) throw std::invalid_argument("conv2d_nhwc_fp8: weights larger than 2 GiB");

@@ -110,7 +110,7 @@ def test_conv_fp8_configs_gpu(cfg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("c", [8, 9, 10, 11])
+@pytest.mark.parametrize("c", [8, 9, 10, 11, 12])
 def test_conv_fp8_lite_shapes_gpu(c):
     """conv_lite_fp8 (cfg 8, the 4-wave LDS-DMA tile; cfg 9, the same tile on DMA / MFMA
     waves where the channel tile is <= 96): Cin not a multiple of the 128-byte K-tile (288,
