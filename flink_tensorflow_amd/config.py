@@ -49,7 +49,7 @@ class EngineConfig:
     pw_dual_kernel: bool = False       # stage-2 projection+expand on the persistent dual kernel
     conv3x3c64_kernel: bool = True     # 64-channel 3x3 convs with the filter bank in LDS
     persistent_cus: int = 0            # grid cap of the persistent kernels (0: every CU)
-    conv_lite_wide: bool = False       # bf16 conv_lite layers with Cout >= 256 on the 128x256 tile (tile 5)
+    conv_lite_wide: int = 0            # bf16 conv_lite on the 128x256 tile (tile 5): 1 = Cout >= 256, 2 = where its grid stays >= 768
     fp8_lite_wide: int = 2             # conv_lite_fp8 channel tiles: 2 = fewest staged rows of 192 / 160 / 128 / 96 / 64 (profiles/r04_af), 1 = 192 added to the least-padding pick (r04_ac), 0 = <= 128
     conv_lite_ws: bool = False         # conv_lite tiles on 8 waves: 4 issue the LDS-DMA, 4 run the MFMAs
     conv3x3_halo: bool = False         # stride-1 3x3 convs (Cin % 64 == 0) on the halo-staged kernel (profiles/r04_s..)

@@ -111,12 +111,15 @@ def _cfg():
 
     return current()
 
-def _lite_tile(Cout: int, dual: bool = False) -> int:
+def _lite_tile(Cout: int, dual: bool = False, M: int = 0) -> int:
     """kernels/conv_pp.hip tile of a bf16 conv_lite layer: 2 (128x128), 4 (the same on DMA /
     MFMA waves, ``conv_lite_ws``) or 5 (128x256 with a 32-deep K-tile for Cout >= 256,
-    ``conv_lite_wide``: the input tile staged once per 256 channels)."""
+    ``conv_lite_wide``: the input tile staged once per 256 channels — 1: every such layer,
+    2: only where the 256-wide grid keeps >= 768 workgroups, 1.5 waves of two per CU; the
+    short stage 3/4 grids lost with it, profiles/r04_ad)."""
     c = _cfg()
-    if c.conv_lite_wide and Cout >= 256:
+    w = int(c.conv_lite_wide)
+    if w and Cout >= 256 and (w == 1 or -(-M // 128) * -(-Cout // 256) >= 768):
         return 5
     return 4 if (c.conv_lite_ws and not dual) else 2
 
@@ -823,7 +826,7 @@ class CompiledFunction(TransformerLowering):
                 # stage 3/4 reduces: the 4-wave LDS-DMA tile beats the 256x256 ping-pong GEMM
                 # (stage 3: 37.8 vs 43.5 µs, profiles/r03_conv) and leaves room on the CU
                 cl = K.ConvPP([(tuple(xin.shape), (1, 1), (1, 1), (0, 0), (1, 1))], Cout, tuple(out.shape[1:3]),
-                              self.device, tile=_lite_tile(Cout))
+                              self.device, tile=_lite_tile(Cout, M=int(np.prod(out.shape[:3]))))
 
                 def run_cl(xin=xin, out=out, cl=cl, w_nk=w_nk, bz=bz, act=act):
                     cl([xin.buf], w_nk, bz, None, act, out=_target(out), out_channel_offset=_coff(out))
@@ -900,7 +903,7 @@ class CompiledFunction(TransformerLowering):
             # (kernels/conv_pp.hip conv_lite): 6-24 % faster than the register-staged igemm
             # per layer and 64 KiB of LDS, so it shares a CU with the sibling lane
             cl = K.ConvPP([(tuple(xin.shape), (KHe, KWe), (sh, sw), (pt, pl), (dh, dw))], Cout, tuple(out.shape[1:3]),
-                          self.device, tile=_lite_tile(Cout))  # tiles 3 (32-deep K), 256x128 (4 or 8 waves) and 3-stage
+                          self.device, tile=_lite_tile(Cout, M=int(np.prod(out.shape[:3]))))  # tiles 3 (32-deep K), 256x128 (4 or 8 waves) and 3-stage
             # variants (raw-barrier, counted vmcnt) measured slower: profiles/r03_conv, r04_a, r04_c
 
             def run(xin=xin, out=out, res_val=res_val, cl=cl, w2=w_dev.reshape(Cout, -1), b_dev=b_dev):  # noqa: F811
@@ -990,11 +993,11 @@ class CompiledFunction(TransformerLowering):
             # stage 2's 200k-row GEMM stays on the igemm (141 vs 158 µs, profiles/r03_operating_points)
             xs0 = (tuple(xin.shape), (1, 1), (1, 1), (0, 0), (1, 1))
             lite = {s2: K.ConvPP([xs0, (tuple(x2.shape), (1, 1), (s2, s2), (0, 0), (1, 1))], Cout, (Ho, Wo),
-                                 self.device, tile=_lite_tile(Cout, dual=True))}
+                                 self.device, tile=_lite_tile(Cout, dual=True, M=N * Ho * Wo))}
             N2, H2, W2, _ = x2.shape
             if s2 == 2 and H2 % 2 == 0 and W2 % 2 == 0:
                 lite[1] = K.ConvPP([xs0, ((N2, H2 // 2, W2 // 2, C2), (1, 1), (1, 1), (0, 0), (1, 1))], Cout, (Ho, Wo),
-                                   self.device, tile=_lite_tile(Cout, dual=True))
+                                   self.device, tile=_lite_tile(Cout, dual=True, M=N * Ho * Wo))
 
             def run(xin=xin, x2=x2, out=out, w_dev=w_dev, b_dev=b_dev, s2cfg=s2cfg, lite=lite):  # noqa: F811
                 lite[s2cfg["s2"]]([xin.buf, x2.buf], w_dev, b_dev, None, act, out=_target(out),
