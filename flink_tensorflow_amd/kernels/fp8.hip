@@ -1384,5 +1384,7 @@ void register_fp8(pybind11::module_& m) {
   m.def("global_avgpool_fp8", &global_avgpool_fp8);
   m.def("avgpool_bias_act", &avgpool_bias_act);
   m.def("conv2d_nhwc_fp8_multi", &conv2d_nhwc_fp8_multi);
+  // the channel tile conv_lite_fp8 picks (host logic only; tests/test_fp8.py)
+  m.def("lite_fp8_tile", [](int Cout, int wide, int M) { return lite_fp8_bn(Cout, wide, M); });
   m.attr("fp8_igemm_num_configs") = NCFG;
 }

@@ -37,6 +37,21 @@ def test_conv_fp8_host_reference_tracks_fp32():
     assert (y - ref).abs().max() < 0.08 * ref.abs().max()
 
 
+def test_lite_fp8_tile_choice():
+    """conv_lite_fp8's channel tile (kernels/fp8.hip ``lite_fp8_bn``; host logic, no GPU):
+    mode 0 pads Cout least over 128 / 96 / 64; mode 1 adds 192; mode 2 (default) stages the
+    fewest rows per 128-pixel tile, (Cout / BN tiles) x (128 + BN)."""
+    from flink_tensorflow_amd import _ext
+
+    hip = _ext.hip(required=False)
+    if hip is None:
+        pytest.skip("HIP kernel library not built")
+    t = lambda c, w: hip.lite_fp8_tile(c, w, 65536)  # noqa: E731
+    assert [t(c, 0) for c in (64, 96, 192, 320, 384)] == [64, 96, 96, 64, 128]
+    assert [t(c, 1) for c in (192, 384, 768, 320)] == [192, 192, 192, 64]
+    assert [t(c, 2) for c in (80, 128, 160, 192, 288, 320, 448, 768)] == [96, 128, 160, 192, 160, 160, 160, 192]
+
+
 def _inception_plans(device, hw=75, batch=2, **kw):
     g = Graph.from_graph_def(inception_v3_graph_def(image_hw=(hw, hw), out_hw=(hw, hw)))
     feeds = {"images:0": ((batch, hw, hw, 3), "UINT8")}
