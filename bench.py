@@ -138,6 +138,9 @@ def main():
     ap.add_argument("--lanes", type=int, default=None,
                     help="compute lanes: independent plan instances on their own HIP streams, batches round-robin "
                          "(default: 3 for bert / bert_graph, 2 otherwise; measured in profiles/r01_lanes)")
+    ap.add_argument("--timeline", action="store_true",
+                    help="also print, per timed batch, its lane and the GPU times of its first H2D piece, first "
+                         "kernel and completion relative to the start of the timed window (diagnostics)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, rendezvous, exchange one object per rank and print the world the "
                          "communicator sees (no model; with --rehearse-fake-comm it runs on a CPU-only box)")
@@ -314,7 +317,8 @@ def main():
     records = [pool[i] for i in range(args.pool)]
     runner = PipelinedGpuRunner(lane_plans, feed, lambda p: p.output_tensors(), rec_shape, rec_dtype,
                                 depth=args.depth, device=dev, gather_threads=args.gather_threads,
-                                stagger=args.stagger_lanes, freeze_gc=not args.no_gc_freeze)
+                                stagger=args.stagger_lanes, freeze_gc=not args.no_gc_freeze,
+                                timeline=args.timeline)
 
     if args.offered_rate:
         return run_offered(args, runner, records, B, rank, ws, dev, comm, MetricGroup, model_name, data, lanes,
@@ -351,6 +355,7 @@ def main():
     comm.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
+    runner.mark()
     for _ in range(args.steps):
         step(True)
     for r in runner.drain():
@@ -406,6 +411,8 @@ def main():
             "host_ms_per_batch": {k: round(v * 1e3 / max(1, runner.batches), 3) for k, v in runner.host_s.items()},
         }
         print(json.dumps(out), flush=True)
+        if runner.timeline is not None:
+            print(json.dumps({"timeline": runner.timeline, "elapsed_ms": round(elapsed * 1e3, 3)}), flush=True)
     comm.destroy()
 
 

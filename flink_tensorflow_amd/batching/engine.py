@@ -46,14 +46,17 @@ class BatchResult:
 
 
 class _Slot:
-    def __init__(self, bucket: int, rec_shape, rec_dtype, out_shapes, device, pin=True):
+    def __init__(self, bucket: int, rec_shape, rec_dtype, out_shapes, device, pin=True, timing=False):
         self.bucket = bucket
         self.pinned_in = torch.empty((bucket, *rec_shape), dtype=rec_dtype, pin_memory=pin)
         self.dev_in = torch.empty((bucket, *rec_shape), dtype=rec_dtype, device=device)
         self.pinned_out = [torch.empty(s, dtype=d, pin_memory=pin) for s, d in out_shapes]
         self.h2d = torch.cuda.Event()
         self.h2d_parts: list[torch.cuda.Event] = []  # one per staged piece (chunked head launch)
-        self.done = torch.cuda.Event()
+        self.done = torch.cuda.Event(enable_timing=timing)
+        # timeline mode: GPU timestamps of the first H2D piece and of the plan's first kernel
+        self.t_h2d = torch.cuda.Event(enable_timing=True) if timing else None
+        self.t_start = torch.cuda.Event(enable_timing=True) if timing else None
         self.busy = False
         self.n = 0
         self.ts = None
@@ -78,7 +81,7 @@ class PipelinedGpuRunner:
 
     def __init__(self, plans, feed: str, fetch_bufs: Callable[[Any], Sequence[torch.Tensor]],
                  record_shape, record_dtype=torch.uint8, depth: int = 3, device=None, gather_threads: int = 8,
-                 stage_chunk: int = 64, stagger: bool = False, freeze_gc: bool = True):
+                 stage_chunk: int = 64, stagger: bool = False, freeze_gc: bool = True, timeline: bool = False):
         lanes = plans if isinstance(plans, (list, tuple)) else [plans]
         self.lanes = [dict(sorted(p.items())) for p in lanes]
         self.plans = self.lanes[0]
@@ -108,7 +111,12 @@ class PipelinedGpuRunner:
         self.slots: dict[int, list[_Slot]] = {}
         for b, plan in self.plans.items():
             outs = [(tuple(t.shape), t.dtype) for t in fetch_bufs(plan)]
-            self.slots[b] = [_Slot(b, self.record_shape, record_dtype, outs, self.device) for _ in range(depth)]
+            self.slots[b] = [_Slot(b, self.record_shape, record_dtype, outs, self.device, timing=timeline)
+                             for _ in range(depth)]
+        # timeline: per harvested batch (lane, host submit s, GPU ms of first H2D / first kernel /
+        # done relative to ``mark()``) — where a short timed window loses time to fill and drain
+        self.timeline = [] if timeline else None
+        self._mark = None
         self._next = {b: 0 for b in self.buckets}
         self._lane = 0
         self._inflight: list[_Slot] = []  # submission order
@@ -159,6 +167,9 @@ class PipelinedGpuRunner:
         pieces = [(lo, min(n, lo + step)) for lo in range(0, n, step)]
         while len(slot.h2d_parts) < len(pieces):
             slot.h2d_parts.append(torch.cuda.Event())
+        if slot.t_h2d is not None:
+            slot.t_h2d.record(self.copy_stream)
+            slot.t_submit = t1
         with trace_range(f"gather[{n}/{b}]"):
             for i, (lo, hi) in enumerate(pieces):
                 self._native.gather_into(base + lo * rb, cap - lo * rb, payloads[lo:hi], rb, self.gather_threads)
@@ -187,7 +198,10 @@ class PipelinedGpuRunner:
             self._started.add(lane)
         with torch.cuda.stream(self.copy_stream):
             slot.h2d.record(self.copy_stream)
+        slot.lane = lane
         with torch.cuda.stream(stream):
+            if slot.t_start is not None:  # after the lane's previous work, before this batch's h2d wait
+                slot.t_start.record(stream)
             with trace_range(f"forward[{b}]@lane{lane}"):
                 chunked = getattr(plan, "replay_from_chunks", None)
                 # head kernel per staged piece: the GPU starts on the first piece while the
@@ -232,6 +246,12 @@ class PipelinedGpuRunner:
             time.sleep(5e-5)
         slot.busy = False
         self._inflight.remove(slot)
+        if self.timeline is not None and self._mark is not None:
+            m = self._mark
+            self.timeline.append({"lane": slot.lane, "n": slot.n, "submit_ms": round((slot.t_submit - m[1]) * 1e3, 3),
+                                  "h2d_ms": round(m[0].elapsed_time(slot.t_h2d), 3),
+                                  "start_ms": round(m[0].elapsed_time(slot.t_start), 3),
+                                  "done_ms": round(m[0].elapsed_time(slot.done), 3)})
         return BatchResult([t.clone() for t in slot.pinned_out], slot.n, slot.ts, time.perf_counter(),
                            slot.tags or [])
 
@@ -244,6 +264,15 @@ class PipelinedGpuRunner:
             if head is slot:
                 break
         return out
+
+    def mark(self):
+        """Timeline origin: a GPU timestamp on the copy stream and the host clock, now."""
+        if self.timeline is None:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(self.copy_stream)
+        self._mark = (ev, time.perf_counter())
+        self.timeline.clear()
 
     def poll(self) -> list[BatchResult]:
         """Harvests completed batches without blocking, oldest first, stopping at the
