@@ -224,7 +224,13 @@ def run_dataflow(session, plan, feeds: dict, ctx, stats: list | None, lookup, va
                 return
             st.ndead += 1
             nb = len(back.get(dst, ()))
-            want = (len(node.inputs) - nb) if tag[1] == 0 else nb
+            # a loop Merge (NextIteration inputs) hears only its Enter inputs at iteration 0
+            # and only its back edges after; any other Merge — a cond's Merge inside a loop
+            # body included — waits for ALL its inputs to be dead, at every iteration
+            if nb == 0:
+                want = len(node.inputs)
+            else:
+                want = (len(node.inputs) - nb) if tag[1] == 0 else nb
             if st.ndead >= want:
                 st.fired = True
                 ready.append((dst, tag, DEAD))

@@ -134,17 +134,31 @@ class _Lowering:
         cret = [f"{prefix}/{v.split(':')[0]}" for v in f.control_ret.values()]
         return rets, cret
 
+    def _gate(self, n: Node, tensors: list) -> tuple[list, list[str]]:
+        """TF's inliner semantics for a call / If / While with control inputs: one
+        ``<name>/input_control`` NoOp carries them and every argument passes through an
+        Identity that depends on it, so each inlined node that reads an argument (not only
+        the input-less ones) waits for the caller's control dependencies, and pruning keeps
+        them.  Returns (gated arguments, anchor for input-less body nodes)."""
+        if not n.control_inputs:
+            return list(tensors), []
+        ic = self._add(f"{n.name}/input_control", "NoOp", [], list(n.control_inputs))
+        gated = [(self._add(f"{n.name}/arg_{i}", "Identity", [t], [ic]), 0) for i, t in enumerate(tensors)]
+        return gated, [ic]
+
     # ------------------------------------------------------------------ lowering
     def call(self, n: Node):
         fn, fa = _func(n, "f")
-        rets, cret = self.inline(n.name + "/body", fn, list(n.inputs), list(n.control_inputs), fa)
+        args, anchor = self._gate(n, list(n.inputs))
+        rets, cret = self.inline(n.name + "/body", fn, args, anchor, fa)
         for i, r in enumerate(rets):
             self.remap[(n.name, i)] = r
         self._add(n.name, "IdentityN", rets, cret)
 
     def if_(self, n: Node):
-        cond, args = n.inputs[0], list(n.inputs[1:])
-        sw = self._add(f"{n.name}/switch_pred", "Switch", [cond, cond], n.control_inputs)
+        gated, _ = self._gate(n, list(n.inputs))
+        cond, args = gated[0], gated[1:]
+        sw = self._add(f"{n.name}/switch_pred", "Switch", [cond, cond])
         pt = self._add(f"{n.name}/pivot_t", "Identity", [(sw, 1)])
         pf = self._add(f"{n.name}/pivot_f", "Identity", [(sw, 0)])
         sws = [self._add(f"{n.name}/switch_{i}", "Switch", [a, cond]) for i, a in enumerate(args)]
@@ -163,11 +177,11 @@ class _Lowering:
         self._add(n.name, "IdentityN", merges)
 
     def while_(self, n: Node):
-        vars_ = list(n.inputs)
+        vars_, _ = self._gate(n, list(n.inputs))
         if not vars_:
             raise ValueError(f"While {n.name} has no loop variables")
         frame = n.name
-        enters = [self._add(f"{n.name}/enter_{i}", "Enter", [v], n.control_inputs if i == 0 else [],
+        enters = [self._add(f"{n.name}/enter_{i}", "Enter", [v], [],
                             {"frame_name": _s_attr(frame), "is_constant": _b_attr(False),
                              "parallel_iterations": _i_attr(10)}) for i, v in enumerate(vars_)]
         merges = [self._add(f"{n.name}/merge_{i}", "Merge", [(e, 0), (e, 0)]) for i, e in enumerate(enters)]

@@ -129,6 +129,7 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
     ``(label, dense[13], cats[26], cross[C])`` records; ``predict(records)``."""
 
     _TRANSIENT = ("_model", "_opt", "_bucketer", "_graph", "_static", "_static_loss", "_fused", "_exchange")
+    uses_collectives = True  # under DP every step all-reduces / exchanges: the job forms a communicator
 
     def __init__(self, cfg: WideDeepConfig | None = None, device=None, seed: int = 0, fused: bool | None = None):
         self.cfg = cfg or WideDeepConfig()

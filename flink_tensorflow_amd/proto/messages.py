@@ -171,8 +171,10 @@ class OpDef(Message):
 
     FIELDS = [F(1, "name", "string"), F(2, "input_arg", "message", repeated=True, msg=ArgDef),
               F(3, "output_arg", "message", repeated=True, msg=ArgDef),
-              F(4, "attr", "message", repeated=True, msg=AttrDef), F(16, "is_stateful", "bool"),
-              F(20, "control_output", "string", repeated=True)]
+              F(4, "attr", "message", repeated=True, msg=AttrDef), F(5, "summary", "string"),
+              F(6, "description", "string"), F(16, "is_aggregate", "bool"), F(17, "is_stateful", "bool"),
+              F(18, "is_commutative", "bool"), F(19, "allows_uninitialized_input", "bool"),
+              F(20, "control_output", "string", repeated=True)]  # op_def.proto field numbers
 
 
 class FunctionDef(Message):

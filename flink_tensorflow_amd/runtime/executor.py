@@ -583,15 +583,16 @@ class LocalExecutor:
         coordinator, under an attempt-scoped prefix.  Each worker opens its communicator on
         it (subtask = rank) before ``op.open()``; rank 0 publishes the RCCL unique id.  None
         when the operator does not form one: SPMD jobs (each rank runs its own subtasks
-        and already has the global communicator), host operators, or fewer GPUs than
-        subtasks (RCCL needs one GPU per rank).  GPUs are counted from sysfs: the
+        and already has the global communicator), host operators, operators that run no
+        collectives under the default "auto" mode (pure inference without
+        ``distributed_weights``), or fewer GPUs than subtasks (RCCL needs one GPU per rank).  GPUs are counted from sysfs: the
         coordinator never initialises HIP for this."""
         mode = getattr(self.env, "job_communicator", "auto")
         test_cls = getattr(self.env, "test_communicator", None)
         if not mode or self.world_size > 1 or not node.uses_gpu:
             return None
-        if mode == "auto" and node.parallelism <= 1:
-            return None
+        if mode == "auto" and (node.parallelism <= 1 or not getattr(node, "wants_group", False)):
+            return None  # "auto": only operators that run collectives pay for an RCCL group
         if test_cls is None:
             from ..utils.gpus import sysfs_gpu_count
 

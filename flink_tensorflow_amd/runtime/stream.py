@@ -56,7 +56,7 @@ def register_types(config: ExecutionConfig) -> None:
 
 class _Node:
     def __init__(self, name: str, factory: Callable[[], Operator], parallelism: int, inputs=None,
-                 is_source: bool = False, uses_gpu: bool = False):
+                 is_source: bool = False, uses_gpu: bool = False, wants_group: bool = False):
         self.uid = f"{next(_uid)}-{name}"
         self.name = name
         self.factory = factory
@@ -64,6 +64,9 @@ class _Node:
         self.inputs: list[tuple[_Node, Partitioner, Any]] = inputs or []
         self.is_source = is_source
         self.uses_gpu = uses_gpu
+        # the operator's subtasks run collectives (distributed weights, a DP trainer): with
+        # the job communicator on "auto" only such operators form one (runtime/executor.py)
+        self.wants_group = wants_group
 
     def make_operator(self) -> Operator:
         return self.factory()
@@ -187,10 +190,11 @@ class DataStream:
 
     # ---- plumbing
     def _add(self, name: str, factory, parallelism=None, partitioner: Partitioner | None = None,
-             uses_gpu: bool = False, extra_inputs=()) -> "DataStream":
+             uses_gpu: bool = False, extra_inputs=(), wants_group: bool = False) -> "DataStream":
         part = partitioner or Partitioner("forward")
         inputs = [(self.node, part, None)] + list(extra_inputs)
-        node = _Node(name, factory, parallelism or self.env.parallelism, inputs, uses_gpu=uses_gpu)
+        node = _Node(name, factory, parallelism or self.env.parallelism, inputs, uses_gpu=uses_gpu,
+                     wants_group=wants_group)
         self.env.nodes.append(node)
         return DataStream(self.env, node)
 
@@ -266,12 +270,12 @@ class DataStream:
     def map(self, fn, name: str = "map", parallelism=None) -> "DataStream":
         proto = F.as_map(fn)
         return self._add(name, lambda: MapOperator(clone_function(proto), name), parallelism,
-                         self._edge_partitioner(), uses_gpu=_uses_gpu(proto))
+                         self._edge_partitioner(), uses_gpu=_uses_gpu(proto), wants_group=_wants_group(proto))
 
     def flat_map(self, fn, name: str = "flat-map", parallelism=None) -> "DataStream":
         proto = F.as_flat_map(fn)
         return self._add(name, lambda: FlatMapOperator(clone_function(proto), name), parallelism,
-                         self._edge_partitioner(), uses_gpu=_uses_gpu(proto))
+                         self._edge_partitioner(), uses_gpu=_uses_gpu(proto), wants_group=_wants_group(proto))
 
     flatMap = flat_map
 
@@ -282,7 +286,7 @@ class DataStream:
     def process(self, fn: F.ProcessFunction, name: str = "process", parallelism=None) -> "DataStream":
         proto = fn
         return self._add(name, lambda: ProcessOperator(clone_function(proto), None, name), parallelism,
-                         self._edge_partitioner(), uses_gpu=_uses_gpu(proto))
+                         self._edge_partitioner(), uses_gpu=_uses_gpu(proto), wants_group=_wants_group(proto))
 
     def assign_timestamps_and_watermarks(self, extractor: Callable, max_out_of_orderness_s: float = 0.0):
         return self._add("timestamps", lambda: TimestampAssignerOperator(extractor, max_out_of_orderness_s))
@@ -334,7 +338,8 @@ class DataStream:
         return self._add(name, lambda: BatchedModelOperator(clone_function(proto_model),
                                                             clone_function(proto_fn) if proto_fn else None,
                                                             max_batch, max_delay_ms, name, emit_batches),
-                         parallelism, self._edge_partitioner(), uses_gpu=True)
+                         parallelism, self._edge_partitioner(), uses_gpu=True,
+                         wants_group=_wants_group(proto_model) or _wants_group(proto_fn))
 
     # ---- sinks
     def add_sink(self, fn, name: str = "sink", parallelism=None) -> "DataStream":
@@ -375,7 +380,7 @@ class KeyedStream(DataStream):
     def process(self, fn: F.ProcessFunction, name: str = "keyed-process", parallelism=None) -> DataStream:
         proto, ks = fn, self.key_selector
         return self._add(name, lambda: ProcessOperator(clone_function(proto), ks, name), parallelism,
-                         self._edge_partitioner(), uses_gpu=_uses_gpu(proto))
+                         self._edge_partitioner(), uses_gpu=_uses_gpu(proto), wants_group=_wants_group(proto))
 
     def window(self, assigner: WindowAssigner) -> "WindowedStream":
         return WindowedStream(self, assigner)
@@ -408,7 +413,8 @@ class ConnectedStreams:
         if k2 is None:
             p2 = Partitioner("broadcast")
         return self.a._add(name, lambda: CoProcessOperator(clone_function(proto), k1, k2, name), parallelism, p1,
-                           uses_gpu=_uses_gpu(proto), extra_inputs=[(self.b.node, p2, None)])
+                           uses_gpu=_uses_gpu(proto), wants_group=_wants_group(proto),
+                           extra_inputs=[(self.b.node, p2, None)])
 
 
 class WindowedStream:
@@ -418,7 +424,8 @@ class WindowedStream:
     def apply(self, fn: F.WindowFunction, name: str = "window", parallelism=None) -> DataStream:
         proto, ks, asg = fn, self.keyed.key_selector, self.assigner
         return self.keyed._add(name, lambda: WindowOperator(clone_function(proto), asg, ks, False, name), parallelism,
-                               self.keyed._edge_partitioner(), uses_gpu=_uses_gpu(proto))
+                               self.keyed._edge_partitioner(), uses_gpu=_uses_gpu(proto),
+                               wants_group=_wants_group(proto))
 
     def reduce(self, fn: Callable, name="window-reduce") -> DataStream:
         return self.apply(_ReduceWindow(fn), name)
@@ -431,7 +438,7 @@ class AllWindowedStream:
     def apply(self, fn: F.AllWindowFunction, name: str = "all-window") -> DataStream:
         proto, asg = fn, self.assigner
         return self.stream._add(name, lambda: WindowOperator(clone_function(proto), asg, None, True, name), 1,
-                                Partitioner("global"), uses_gpu=_uses_gpu(proto))
+                                Partitioner("global"), uses_gpu=_uses_gpu(proto), wants_group=_wants_group(proto))
 
 
 # ------------------------------------------------------------------ helpers
@@ -439,6 +446,16 @@ def _uses_gpu(fn) -> bool:
     from .model_functions import ModelAwareFunction
 
     return isinstance(fn, ModelAwareFunction)
+
+
+def _wants_group(obj) -> bool:
+    """Does an operator's function (or its model) run collectives across its subtasks:
+    ``distributed_weights`` (rank-0 read + broadcast at open) or ``uses_collectives`` (a
+    data-parallel trainer: gradient all-reduce, sparse exchange)?"""
+    for o in (obj, getattr(obj, "model", None), getattr(obj, "_model", None)):
+        if o is not None and (getattr(o, "distributed_weights", False) or getattr(o, "uses_collectives", False)):
+            return True
+    return False
 
 
 class _ReduceProcess(F.ProcessFunction):

@@ -174,3 +174,39 @@ def test_cond_gated_cnn_compiles_glue_free_gpu():
     got = pc({"images:0": imgs.to(dev)})[0].float().cpu()
     ref = Session(g_twin).run("logits:0", {"images:0": imgs})
     assert (got - ref).abs().max() <= 0.03 * ref.abs().max() + 1e-3
+
+
+def _cond_in_loop_graph():
+    """i = i0, acc = 1; while i < n: acc = cond(i % 2 == 0, acc + 1, acc * 2); i += 1 — a
+    cond's Merge inside a loop body, taking a different branch on alternate iterations."""
+    gb = GraphBuilder()
+    n = gb.placeholder("n", "INT32", [])
+    i0 = gb.placeholder("i0", "INT32", [])
+    a0 = gb.constant("a0", np.float32(1.0))
+
+    def body(i, acc, n_):
+        even = gb.op("Equal", [gb.op("FloorMod", [i, gb.constant("two_i", np.int32(2))]),
+                               gb.constant("zero_i", np.int32(0))], name="even")
+        acc2 = gb.cond(even, lambda a: gb.add(a, gb.constant("one_f", np.float32(1.0)), name="plus1"),
+                       lambda a: gb.mul(a, gb.constant("two_f", np.float32(2.0)), name="times2"),
+                       inputs=[acc], name="pick")
+        return [gb.add(i, gb.constant("one_i", np.int32(1)), name="inc"), acc2]
+
+    i_out, acc_out = gb.while_loop(lambda i, acc, n_: gb.op("Less", [i, n_], name="less"), body, [i0, a0],
+                                   invariants=[n])
+    gb.identity(acc_out, name="acc")
+    gb.identity(i_out, name="iters")
+    return gb.build()
+
+
+@pytest.mark.parametrize("i0,n", [(0, 5), (1, 6), (0, 1), (3, 3), (1, 9)])
+def test_cond_inside_while_body_every_iteration(i0, n):
+    """Regression: a non-loop Merge fired DEAD on its first dead input at
+    iterations >= 1, before the live branch arrived."""
+    s = Session(_cond_in_loop_graph())
+    acc, it = s.run(["acc:0", "iters:0"], {"n:0": torch.tensor(n, dtype=torch.int32),
+                                           "i0:0": torch.tensor(i0, dtype=torch.int32)})
+    want = 1.0
+    for i in range(i0, n):
+        want = want + 1 if i % 2 == 0 else want * 2
+    assert int(it) == max(i0, n) and float(acc) == want

@@ -133,3 +133,81 @@ def test_compiled_plan_through_a_call():
     got = plan({"a:0": a, "b:0": b})[0].float()
     assert (got - (2 * a + b)).abs().max() < 0.05
     assert np.isfinite(got.numpy()).all()
+
+
+def test_stateless_if_inside_stateless_while():
+    """A functional If in a While body (lowered to a cond inside a loop frame): the branch
+    alternates per iteration — regression for the Merge dead-token rule."""
+    then2 = _fn("inc_fn", [("x", F32)], [("out", F32)],
+                [_const("k", 1.0), NodeDef(name="a", op="AddV2", input=["x", "k:output:0"])], {"out": "a:z:0"})
+    else2 = _fn("dbl_fn", [("x", F32)], [("out", F32)],
+                [_const("k", 2.0), NodeDef(name="m", op="Mul", input=["x", "k:output:0"])], {"out": "m:z:0"})
+    body2 = _fn("body2_fn", [("i", I32), ("acc", F32), ("n", I32)], [("i1", I32), ("acc1", F32), ("n1", I32)],
+                [_const("one", 1, torch.int32), _const("two", 2, torch.int32), _const("zero", 0, torch.int32),
+                 NodeDef(name="mod", op="FloorMod", input=["i", "two:output:0"]),
+                 NodeDef(name="even", op="Equal", input=["mod:z:0", "zero:output:0"]),
+                 NodeDef(name="pick", op="StatelessIf", input=["even:z:0", "acc"],
+                         attr={"then_branch": _f("inc_fn"), "else_branch": _f("dbl_fn")}),
+                 NodeDef(name="inc", op="AddV2", input=["i", "one:output:0"]),
+                 NodeDef(name="n_id", op="Identity", input=["n"])],
+                {"i1": "inc:z:0", "acc1": "pick:output:0", "n1": "n_id:output:0"})
+    lib = FunctionDefLibrary(function=[COND, then2, else2, body2])
+    g = Graph.from_graph_def(GraphDef(node=[
+        _ph("n", I32), _ph("i0", I32), _const("acc0", 1.0),
+        NodeDef(name="loop", op="StatelessWhile", input=["i0", "acc0", "n"],
+                attr={"cond": _f("cond_fn"), "body": _f("body2_fn")}),
+        NodeDef(name="acc", op="Identity", input=["loop:1"])], library=lib).encode())
+    s = Session(g)
+    for i0, n in ((0, 5), (1, 6), (2, 9)):
+        acc = s.run("acc:0", {"n:0": torch.tensor(n, dtype=torch.int32), "i0:0": torch.tensor(i0, dtype=torch.int32)})
+        want = 1.0
+        for i in range(i0, n):
+            want = want + 1 if i % 2 == 0 else want * 2
+        assert float(acc) == want, (i0, n, float(acc), want)
+
+
+def test_call_control_inputs_gate_the_inlined_body():
+    """``StatefulPartitionedCall ^assign`` whose body reads the variable through an argument:
+    the read waits for (and pruning keeps) the assign (inlining dropped the
+    call's control inputs for every body node fed by an argument)."""
+    g = _graph([NodeDef(name="v", op="VarHandleOp", attr={"dtype": AttrValue(type=F32), "shape": AttrValue(
+        shape=TensorShapeProto.of([2])), "shared_name": AttrValue(s=b"v")}),
+                _const("v_init", [3.0, 4.0]),
+                NodeDef(name="assign", op="AssignVariableOp", input=["v", "v_init"], attr={"dtype": AttrValue(type=F32)}),
+                _ph("x", F32),
+                NodeDef(name="call", op="StatefulPartitionedCall", input=["v", "x", "^assign"],
+                        attr={"f": _f("read_fn")})])
+    s = Session(g)  # no separate init run: the call's control input must bring the assign
+    assert torch.equal(s.run("call:0", {"x:0": torch.tensor([1.0, 1.0])}), torch.tensor([4.0, 5.0]))
+
+
+def test_if_and_while_control_inputs_gate_their_arguments():
+    nodes = [NodeDef(name="v", op="VarHandleOp", attr={"dtype": AttrValue(type=F32), "shape": AttrValue(
+        shape=TensorShapeProto.of([2])), "shared_name": AttrValue(s=b"w")}),
+             _const("v_init", [3.0, 4.0]),
+             NodeDef(name="assign", op="AssignVariableOp", input=["v", "v_init"], attr={"dtype": AttrValue(type=F32)}),
+             _ph("p", BOOL),
+             NodeDef(name="rd", op="ReadVariableOp", input=["v"], attr={"dtype": AttrValue(type=F32)}),
+             NodeDef(name="if", op="StatelessIf", input=["p", "rd", "^assign"],
+                     attr={"then_branch": _f("then_fn"), "else_branch": _f("else_fn")})]
+    from flink_tensorflow_amd.graph.functions import lower_functional_ops
+
+    low = lower_functional_ops(_graph(nodes))
+    assert "if/input_control" in low.nodes and low.nodes["if/input_control"].control_inputs == ["assign"]
+    assert all(low.nodes[f"if/arg_{i}"].control_inputs == ["if/input_control"] for i in range(2))
+
+
+def test_opdef_flags_round_trip_with_tf_field_numbers():
+    """op_def.proto: is_aggregate = 16, is_stateful = 17 (is_stateful was
+    written as tag 16 and came back as is_aggregate in TF)."""
+    from flink_tensorflow_amd.proto.wire import scan
+
+    sig = OpDef(name="f", is_stateful=True)
+    raw = sig.encode()
+    tags = {num for num, _, _ in scan(raw)}
+    assert 17 in tags and 16 not in tags
+    back = OpDef.decode(raw)
+    assert back.is_stateful and not back.is_aggregate
+    fd = FunctionDef(signature=OpDef(name="g", is_stateful=True, is_aggregate=True))
+    again = FunctionDef.decode(fd.encode())
+    assert again.signature.is_stateful and again.signature.is_aggregate

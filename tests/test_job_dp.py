@@ -30,8 +30,8 @@ class _RecordingLoader(DefaultSavedModelLoader):
 
 
 class _HalfPlusTwo(TensorFlowModel):
-    def __init__(self, path, marks):
-        super().__init__(None, distributed_weights=True)
+    def __init__(self, path, marks, distributed=True):
+        super().__init__(None, distributed_weights=distributed)
         self._loader = _RecordingLoader(path, marks)
 
     @property
@@ -78,6 +78,24 @@ def test_no_group_without_enough_gpus_or_for_host_operators(tmp_path, half_plus_
         .run_in_processes().execute_and_collect()
     if torch.cuda.device_count() < 2:
         assert {o[1] for o in out} == {(0, 1)} and len(os.listdir(marks)) == 2
+
+
+def test_auto_mode_forms_a_group_only_for_collective_operators(tmp_path, half_plus_two):
+    """The default "auto" job communicator: a P=2 inference operator without
+    ``distributed_weights`` opens no communicator (each subtask reads its model); the same
+    operator with ``distributed_weights=True`` forms one group of 2."""
+    from flink_tensorflow_amd.parallel.fake import FakeCommunicator
+
+    for distributed, want_ranks, want_reads in ((False, {(0, 1)}, 2), (True, {(0, 2), (1, 2)}, 1)):
+        marks = tmp_path / f"marks{int(distributed)}"
+        marks.mkdir()
+        env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+        env.enable_job_communicator("auto", communicator=FakeCommunicator)
+        model = _HalfPlusTwo(half_plus_two, str(marks), distributed=distributed)
+        out = env.from_collection(list(range(12))).rebalance().map_with_model(model, _variables_of) \
+            .run_in_processes().execute_and_collect()
+        assert {o[1] for o in out} == want_ranks, distributed
+        assert len(os.listdir(marks)) == want_reads, distributed
 
 
 def _rccl_probe(value, model):
