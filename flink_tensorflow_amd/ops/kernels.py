@@ -15,6 +15,7 @@ stream, so the ops are hipGraph-capturable.
 from __future__ import annotations
 
 import copy
+import functools
 import os
 
 import torch
@@ -179,6 +180,114 @@ def conv3x3_c64_eligible(x_shape, w_shape, stride, pad, dilation, residual, act)
     return (Cin == 64 and Cout == 64 and (KH, KW) == (3, 3) and tuple(stride) == (1, 1) and tuple(pad) == (1, 1, 1, 1)
             and tuple(dilation) == (1, 1) and residual is None and act_code(act) in (ACT_NONE, ACT_RELU)
             and H >= 8 and W >= 32 and N * H * W * Cin * 2 < 2 ** 31)
+
+
+# ------------------------------------------------------------------------------ Winograd
+# F(2x2, 3x3) (kernels/wino3x3.hip): Y = A^T [(G g G^T) .* (B^T d B)] A per 2x2 output tile
+_WG = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
+_WBT = ((1, 0, -1, 0), (0, 1, 1, 0), (0, -1, 1, 0), (0, 1, 0, -1))
+_WAT = ((1, 1, 1, 0), (0, 1, -1, -1))
+WINO_TB = 64        # tiles per workgroup (kernels/wino3x3.hip TB)
+WINO_MAX_CHUNKS = 12 * 256
+
+
+@functools.lru_cache(maxsize=None)
+def wino_f23_max_rows(N: int, H: int, W: int) -> int:
+    """Padded input rows the worst 64-tile block of a layer stages (mirror of
+    ``wino_f23_max_rows`` in kernels/wino3x3.hip; memoised: eager launches call it)."""
+    TH, TW = (H + 1) // 2, (W + 1) // 2
+    per, Hp = TH * TW, 2 * TH + 2
+    T = N * per
+    worst = 0
+    for t0 in range(0, T, WINO_TB):
+        ta, tb = t0, min(t0 + WINO_TB - 1, T - 1)
+        na, tya = ta // per, (ta % per) // TW
+        nb, tyb = tb // per, (tb % per) // TW
+        worst = max(worst, nb * Hp + 2 * tyb + 4 - (na * Hp + 2 * tya))
+    return worst
+
+
+def wino_f23_eligible(x_shape, w_shape, stride, pad, dilation, residual, act) -> bool:
+    """3x3 / stride 1 / SAME, Cin % 32 == 0, Cout % 64 == 0, no residual, bias (+ReLU), and a
+    64-tile block whose staged input rows fit the kernel's per-thread staging (<= 12 x 256
+    16-byte chunks per K-step): every stride-1 3x3 of ResNet-50 at any batch."""
+    if len(x_shape) != 4:
+        return False
+    N, H, W, Cin = x_shape
+    Cout, KH, KW, Ci = w_shape
+    if not (Cin == Ci and Cin % 32 == 0 and Cout % 64 == 0 and (KH, KW) == (3, 3) and tuple(stride) == (1, 1)
+            and tuple(pad) == (1, 1, 1, 1) and tuple(dilation) == (1, 1) and residual is None
+            and act_code(act) in (ACT_NONE, ACT_RELU) and N * H * W * Cin * 2 < 2 ** 31 - 4096):
+        return False
+    return wino_f23_max_rows(N, H, W) * 8 * ((W + 1) // 2 + 1) <= WINO_MAX_CHUNKS
+
+
+def wino_f23_weights(w_hwio: torch.Tensor) -> torch.Tensor:
+    """fp16 U = G g G^T of a [3, 3, Cin, Cout] filter (BN folded), laid out as the kernel's
+    MFMA A fragments: ``[Cout/32][Cin/16][16 xi][64 lanes][8]`` with lane ``r + 32 h``
+    holding ``U[xi][16 ks + 8 h + j][32 cbg + r]``, j = 0..7 (computed in fp64, one
+    rounding)."""
+    KH, KW, C, K = w_hwio.shape
+    if (KH, KW) != (3, 3) or C % 16 or K % 32:
+        raise ValueError(f"wino_f23_weights: bad filter shape {tuple(w_hwio.shape)}")
+    G = torch.tensor(_WG, dtype=torch.float64)
+    U = torch.einsum("ia,abck,jb->ijck", G, w_hwio.detach().to("cpu", torch.float64), G).reshape(16, C, K)
+    U = U.reshape(16, C // 16, 2, 8, K // 32, 32).permute(4, 1, 0, 2, 5, 3)
+    return U.contiguous().reshape(-1).to(torch.float16)
+
+
+def wino_f23_reference(x: torch.Tensor, u_frag: torch.Tensor, Cout: int, bias: torch.Tensor | None, act=None,
+                       fp16_domain: bool = True) -> torch.Tensor:
+    """Host model of the kernel's arithmetic from its own weight fragments: NHWC input ->
+    padded 4x4 patches per 2x2 tile -> V = B^T d B (fp16 when ``fp16_domain``, as staged and
+    transformed on the GPU) -> M_xi = V_xi . U_xi (fp32) -> Y = A^T M A + bias -> act."""
+    N, H, W, C = x.shape
+    TH, TW = (H + 1) // 2, (W + 1) // 2
+    U = u_frag.reshape(Cout // 32, C // 16, 16, 2, 32, 8).permute(2, 1, 3, 5, 0, 4).reshape(16, C, Cout).float()
+    xp = torch.zeros((N, 2 * TH + 2, 2 * TW + 2, C), dtype=torch.float32)
+    xp[:, 1:H + 1, 1:W + 1] = x.detach().to("cpu", torch.float32)
+    if fp16_domain:
+        xp = xp.half().float()
+    d = xp.unfold(1, 4, 2).unfold(2, 4, 2)  # [N, TH, TW, C, 4, 4]
+    BT = torch.tensor(_WBT, dtype=torch.float32)
+    V = torch.einsum("ia,ntwcab,jb->ntwijc", BT, d, BT).reshape(N, TH, TW, 16, C)
+    if fp16_domain:
+        V = V.half().float()
+    M = torch.einsum("ntwxc,xck->ntwxk", V, U).reshape(N, TH, TW, 4, 4, Cout)
+    AT = torch.tensor(_WAT, dtype=torch.float32)
+    Y = torch.einsum("ri,ntwijk,cj->ntrwck", AT, M, AT).reshape(N, 2 * TH, 2 * TW, Cout)[:, :H, :W]
+    if bias is not None:
+        Y = Y + bias.detach().to("cpu", torch.float32)
+    if act_code(act) == ACT_RELU:
+        Y = torch.relu(Y)
+    return Y
+
+
+def wino_f23(x: torch.Tensor, u_frag: torch.Tensor, Cout: int, bias: torch.Tensor, act=None,
+             out: torch.Tensor | None = None, out_channel_offset: int = 0) -> torch.Tensor:
+    """3x3 / s1 / SAME conv by Winograd F(2x2, 3x3): ``act(conv + bias)`` with the fp16 U
+    fragments of :func:`wino_f23_weights`.  GPU: kernels/wino3x3.hip; host: the same
+    arithmetic in torch (:func:`wino_f23_reference`)."""
+    N, H, W, C = x.shape
+    a = act_code(act)
+    if out is None:
+        out = torch.empty((N, H, W, Cout), dtype=torch.bfloat16 if x.is_cuda else torch.float32, device=x.device)
+        out_channel_offset = 0
+    if not wino_f23_eligible(tuple(x.shape), (Cout, 3, 3, C), (1, 1), (1, 1, 1, 1), (1, 1), None, a):
+        raise ValueError(f"wino_f23: unsupported shapes x {tuple(x.shape)} -> {Cout} channels")
+    if out.shape[:3] != (N, H, W) or out_channel_offset + Cout > out.shape[3] or u_frag.numel() != 16 * C * Cout:
+        raise ValueError("wino_f23: output buffer or weight fragments do not fit")
+    if x.is_cuda:
+        _check(x, "x", device=x.device)
+        _check(u_frag, "u", torch.float16, x.device)
+        _check(out, "out", device=x.device)
+        _check(bias, "bias", torch.float32, x.device)
+        _hip().wino_f23_bf16(x.data_ptr(), u_frag.data_ptr(), bias.data_ptr(), out.data_ptr(), N, H, W, C, Cout,
+                             out.shape[3], out_channel_offset, a, _stream())
+        return out
+    y = wino_f23_reference(x, u_frag, Cout, bias, a, fp16_domain=False)
+    out[..., out_channel_offset:out_channel_offset + Cout] = y.to(out.dtype)
+    return out
 
 
 def conv3x3_halo_len(N: int, H: int, W: int) -> int:
