@@ -27,6 +27,13 @@ CSRC = PKG / "csrc"
 CSRC_RCCL = PKG / "csrc_rccl"
 KERNELS = PKG / "kernels"
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+# what the last build_* call did per library: "compiled" (from source) or "reused" (the
+# stamped library matched the sources and flags); FTM_FORCE_BUILD=1 forces "compiled"
+STATUS: dict[str, str] = {}
+
+
+def _forced(force: bool) -> bool:
+    return force or os.environ.get("FTM_FORCE_BUILD", "") == "1"
 HIP_ARCH = os.environ.get("FTM_HIP_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -76,8 +83,10 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
     extra = os.environ.get("FTM_NATIVE_CFLAGS", "").split()  # e.g. sanitizer builds
     lib = native_lib_path()
     dig = _digest(srcs + hdrs, flags + extra)
-    if not force and _up_to_date(lib, dig):
+    if not _forced(force) and _up_to_date(lib, dig):
+        STATUS["_native"] = "reused"
         return lib
+    STATUS["_native"] = "compiled"
     cxx = os.environ.get("CXX", "g++")
     tmp = lib.with_name(lib.name + ".tmp")
     cmd = [cxx, *flags, *extra, *_pybind_includes(), *map(str, srcs), "-lrt", "-o", str(tmp)]
@@ -133,8 +142,10 @@ def build_hip(force: bool = False, verbose: bool = False, jobs: int | None = Non
     flags = hip_flags()
     lib = hip_lib_path()
     dig = _digest(srcs + hdrs, flags)
-    if not force and _up_to_date(lib, dig):
+    if not _forced(force) and _up_to_date(lib, dig):
+        STATUS["_hip"] = "reused"
         return lib
+    STATUS["_hip"] = "compiled"
     hipcc = os.environ.get("HIPCC", f"{ROCM}/bin/hipcc")
     objdir = PKG / "build" / "hip_obj"
     objdir.mkdir(parents=True, exist_ok=True)
@@ -168,8 +179,10 @@ def build_rccl(force: bool = False, verbose: bool = False) -> Path:
              f"-I{ROCM}/include", f"-L{ROCM}/lib", "-lrccl", "-lamdhip64"]
     lib = rccl_lib_path()
     dig = _digest(srcs, flags)
-    if not force and _up_to_date(lib, dig):
+    if not _forced(force) and _up_to_date(lib, dig):
+        STATUS["_rccl"] = "reused"
         return lib
+    STATUS["_rccl"] = "compiled"
     hipcc = os.environ.get("HIPCC", f"{ROCM}/bin/hipcc")
     tmp = lib.with_name(lib.name + ".tmp")
     # -x c++ : host-only translation unit (no device code, no offload bundle)
@@ -197,8 +210,8 @@ if __name__ == "__main__":
     ap.add_argument("what", nargs="?", default="all", choices=["all", "native", "hip", "rccl"])
     a = ap.parse_args()
     if a.what in ("all", "native"):
-        print(build_native(a.force, a.verbose))
+        print(build_native(a.force, a.verbose), STATUS.get("_native"))
     if a.what in ("all", "hip"):
-        print(build_hip(a.force, a.verbose))
+        print(build_hip(a.force, a.verbose), STATUS.get("_hip"))
     if a.what in ("all", "rccl"):
-        print(build_rccl(a.force, a.verbose))
+        print(build_rccl(a.force, a.verbose), STATUS.get("_rccl"))

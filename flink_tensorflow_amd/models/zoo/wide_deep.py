@@ -402,10 +402,20 @@ def synthetic_click_records(n: int, cfg: WideDeepConfig, seed: int = 0, n_cross:
     return [(labels[i], dense[i], cats[i].astype(np.int32), cross[i]) for i in range(n)]
 
 
-def smoke_train_step(device) -> torch.Tensor:
-    t = WideDeepTrainer(WideDeepConfig.tiny(), device=device)
+def smoke_train_step(device, steps: int = 2) -> tuple[list[float], dict]:
+    """Losses of ``steps`` training steps of the tiny Wide&Deep on fixed records and the
+    parameter updates they made (``state - initial state`` per tensor, optimizer state
+    excluded): the GPU runs the fused step, the host the autograd trainer in fp32, and the
+    smoke test compares the two (as ``tests/test_widedeep.py::
+    test_fused_step_tracks_fp32_host_trainer_gpu`` does over 8 steps)."""
+    t = WideDeepTrainer(WideDeepConfig.tiny(), device=device, seed=0)
     t.open()
-    recs = synthetic_click_records(64, t.cfg)
-    loss = t.train_step(recs)
+    p0 = {k: v.detach().float().cpu().clone() for k, v in t.model.state_dict().items()}
+    recs = synthetic_click_records(256, t.cfg, seed=5)
+    out = [float(t.train_step(recs[i * 128:(i + 1) * 128])) for i in range(steps)]
+    if t.model.device.type == "cuda":
+        torch.cuda.synchronize(t.model.device)
+    deltas = {k: (v.detach().float().cpu() - p0[k]).reshape(-1) for k, v in t.model.state_dict().items()
+              if not (k.endswith("accum") or k.endswith("anchor"))}
     t.close()
-    return loss
+    return out, deltas

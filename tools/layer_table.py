@@ -2,8 +2,10 @@
 default, as bench.py builds it): one eager pass with a HIP event pair around every launch
 (``CompiledFunction.profile``), repeated ``--reps`` times, median per step.  Prints one JSON
 line per step (name, kind, kernel, output shape, µs, TF/s) and a markdown table; a step
-named after a Conv2D gets its FLOPs from the graph (2 * B*Ho*Wo*Cout * KH*KW*Cin); steps
-that fuse several convs into one launch (stage-1 tails) report time only.
+named after a Conv2D gets its FLOPs from the graph (2 * B*Ho*Wo*Cout * KH*KW*Cin) on the
+grid the kernel computes: a stem conv with a fused max pool is counted on its full-resolution
+(pre-pool) output (the step's ``conv_out``), not on the pooled tensor it stores; steps that
+fuse several convs into one launch (stage-1 tails) report time only.
 
     python tools/layer_table.py [--model resnet50|inception_v3] [--batch 256] [--reps 5]
 """
@@ -61,6 +63,7 @@ def main():
         total += us
         # a stage-1 tail launch also runs the next block's reduce: time only
         out = st.outputs[0].shape if st.outputs and hasattr(st.outputs[0], "shape") else None
+        grid = st.meta.get("conv_out") or out  # the computed grid (pre-pool for a pool-fused stem)
         flops = 0.0
         node = graph.nodes.get(st.name)
         if node is not None and node.op == "Conv2D" and out is not None and st.meta.get("impl") != "bottleneck_tail":
@@ -69,16 +72,18 @@ def main():
             wn = graph.nodes.get(node.inputs[1][0])
             if wn is not None and wn.op == "Const":
                 KH, KW, Cin, Cout = tensor_from_proto(wn.tensor_attr("value")).shape
-                flops = 2.0 * out[0] * out[1] * out[2] * Cout * KH * KW * Cin
+                flops = 2.0 * grid[0] * grid[1] * grid[2] * Cout * KH * KW * Cin
         rows.append({"i": i, "name": st.name, "kind": st.kind, "impl": st.meta.get("impl", ""),
-                     "out": list(out) if out is not None else None, "us": round(us, 1),
+                     "out": list(out) if out is not None else None,
+                     "grid": list(grid) if grid is not None and grid is not out else None, "us": round(us, 1),
                      "tflops": round(flops / us / 1e6, 1) if flops and us else None})
     for r in rows:
         print(json.dumps(r))
     print(json.dumps({"total_us": round(total, 1), "steps": len(rows), "batch": B, "model": a.model}))
-    lines = ["| # | step | kind / kernel | output | µs | TF/s |", "|---|---|---|---|---|---|"]
+    lines = ["| # | step | kind / kernel | output (computed grid) | µs | TF/s |", "|---|---|---|---|---|---|"]
     for r in rows:
-        lines.append(f"| {r['i']} | {r['name']} | {r['kind']} {r['impl']} | {r['out']} | {r['us']} | "
+        shown = f"{r['out']} (grid {r['grid']})" if r["grid"] else f"{r['out']}"
+        lines.append(f"| {r['i']} | {r['name']} | {r['kind']} {r['impl']} | {shown} | {r['us']} | "
                      f"{r['tflops'] if r['tflops'] is not None else ''} |")
     lines.append(f"| | **total** | | | **{round(total, 1)}** | |")
     md = "\n".join(lines)
