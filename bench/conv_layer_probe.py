@@ -30,7 +30,7 @@ LAYERS = {  # name: (H, W, Cin, Cout, k, stride)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layers", default="s2_3x3,s3_3x3,s4_3x3")
-    ap.add_argument("--impls", default="igemm,pp")
+    ap.add_argument("--impls", default="igemm,lite")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256)
     a = ap.parse_args()
@@ -48,15 +48,11 @@ def main():
         res = torch.randn((B, OH, OW, Cout), device=dev, generator=g).to(torch.bfloat16) if opt and opt[0] else None
         flops = 2.0 * B * OH * OW * Cout * k * k * Cin
         for impl in a.impls.split(","):
-            if impl == "halo":  # kernels/conv3x3h.hip (stride-1 3x3 only)
-                def fn():
-                    K.conv3x3_halo(x, w, b, K.ACT_RELU, out=y)
-            elif impl == "igemm":
+            if impl == "igemm":
                 def fn():
                     K.conv2d_nhwc(x, w, b, res, (s, s), (pad, pad, pad, pad), (1, 1), K.ACT_RELU, out=y)
-            else:  # pp: the 8-wave ping-pong tiles; lite: the 4-wave 128x128 LDS-DMA tile
-                cp = K.ConvPP([((B, H, W, Cin), (k, k), (s, s), (pad, pad), (1, 1))], Cout, (OH, OW), dev,
-                              tile={"lite": 2, "lite32": 3, "ws": 4, "wide": 5}.get(impl, 0 if Cout >= 256 else 1))
+            else:  # lite: the 4-wave 128x128 LDS-DMA tile
+                cp = K.ConvPP([((B, H, W, Cin), (k, k), (s, s), (pad, pad), (1, 1))], Cout, (OH, OW), dev)
                 w2 = w.reshape(Cout, -1)
 
                 def fn(cp=cp, w2=w2):

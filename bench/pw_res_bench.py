@@ -48,23 +48,7 @@ def main():
         print(json.dumps({"layer": name, "igemm_us": [round(t_ig, 1), round(t_ig2, 1)],
                           "pw_res_us": [round(t_pw, 1), round(t_pw2, 1)],
                           "pw_res_TBps": round(nbytes / min(t_pw, t_pw2) / 1e6, 2), "max_rel_diff": round(err, 4)}))
-    # dual form: stage-2 entry expand (28x28, 128 -> 512) + decimated projection (256 ch)
-    x = torch.randn(256, 28, 28, 128, device=dev, generator=g).bfloat16()
-    x2 = torch.randn(256, 28, 28, 256, device=dev, generator=g).bfloat16()
-    w = (torch.randn(512, 384, device=dev, generator=g) / 20).bfloat16()
-    b = torch.randn(512, device=dev, generator=g)
-    o1 = torch.empty(256, 28, 28, 512, device=dev, dtype=torch.bfloat16)
-    o2 = torch.empty_like(o1)
-    f_ig = lambda: K.conv1x1_dual(x, x2, w, b, 1, "relu", out=o1)  # noqa: E731
-    f_pw = lambda: K.pw_dual(x, x2, w, b, out=o2)  # noqa: E731
-    f_ig(), f_pw()
-    torch.cuda.synchronize()
-    err = ((o1.float() - o2.float()).abs().max() / o1.float().abs().max()).item()
-    t = [time_us(f_ig), time_us(f_pw), time_us(f_ig), time_us(f_pw)]
-    nbytes = (x.numel() + x2.numel() + o1.numel()) * 2
-    print(json.dumps({"layer": "s2_entry_dual", "igemm_us": [round(t[0], 1), round(t[2], 1)],
-                      "pw_res_us": [round(t[1], 1), round(t[3], 1)],
-                      "pw_res_TBps": round(nbytes / min(t[1], t[3]) / 1e6, 2), "max_rel_diff": round(err, 4)}))
+
 
 
 if __name__ == "__main__":

@@ -37,22 +37,14 @@ class EngineConfig:
     restart_delay_s: float = 0.0
     channel_capacity: int = 1024
     log_level: str = "INFO"
-    # ---- compiler / kernel selection (measured choices; FT_<NAME> env vars or YAML)
-    conv_impl: str = "lite"            # implicit-GEMM convs: lite (4-wave LDS-DMA conv_lite) | incumbent
-    #                                    (register-staged igemm) | auto (probe conv_pp) | pp
-    conv_lite_pointwise: bool = False  # deep-K 1x1 reduces (K >= 1024) on conv_lite instead of gemm_pp
+    # ---- compiler / kernel selection (FT_<NAME> env vars or YAML): every default is the
+    # measured-fastest choice; these switch a fusion OFF for A/B runs.  Variants measured
+    # slower were removed with their kernels (graph/compiler.py LITE_TILE comment)
     sibling_conv_fusion: bool = True   # fp8: an Inception module's sibling 1x1 convs as one multi-output GEMM
     fuse_block_tails: bool = True      # ResNet block boundary: expand + next reduce in one kernel
-    fuse_wide_tails: bool = False      # ... also for stage 2 (weights streamed; measured no gain)
     decimate_tails: bool = True        # stage-1 tail output stored at the stride-2 reader's pixels
     pw_res_kernel: bool = True         # identity-residual expand convs on the persistent kernel
-    pw_dual_kernel: bool = False       # stage-2 projection+expand on the persistent dual kernel
     conv3x3c64_kernel: bool = True     # 64-channel 3x3 convs with the filter bank in LDS
-    persistent_cus: int = 0            # grid cap of the persistent kernels (0: every CU)
-    conv_lite_wide: int = 0            # bf16 conv_lite on the 128x256 tile (tile 5): 1 = Cout >= 256, 2 = where its grid stays >= 768
-    fp8_lite_wide: int = 2             # conv_lite_fp8 channel tiles: 2 = fewest staged rows of 192 / 160 / 128 / 96 / 64 (profiles/r04_af), 1 = 192 added to the least-padding pick (r04_ac), 0 = <= 128
-    conv_lite_ws: bool = False         # conv_lite tiles on 8 waves: 4 issue the LDS-DMA, 4 run the MFMAs
-    conv3x3_halo: bool = False         # stride-1 3x3 convs (Cin % 64 == 0) on the halo-staged kernel (profiles/r04_s..)
     # cache-resident batch slices: the plan's leading run of large-activation layers (every
     # tensor >= chain_min_hw pixels per image: Inception-v3's 149x149 .. 71x71 stem) runs once
     # per slice of chain_batch images, its intermediates in slice-sized buffers that stay in
@@ -148,8 +140,6 @@ class EngineConfig:
             raise ValueError("max_batch >= 1 and max_delay_ms >= 0 required")
         if self.precision not in ("bf16", "fp8"):
             raise ValueError("precision must be bf16 or fp8")
-        if self.conv_impl not in ("lite", "incumbent", "auto", "pp"):
-            raise ValueError("conv_impl must be lite, incumbent, auto or pp")
         if not 0 < self.arena_fraction <= 1:
             raise ValueError("arena_fraction must be in (0, 1]")
         if self.batch_buckets and sorted(self.batch_buckets) != list(self.batch_buckets):

@@ -64,73 +64,21 @@ _BINARY = {"Add": "add", "AddV2": "add", "Sub": "sub", "Mul": "mul", "RealDiv": 
            "Maximum": "max", "Minimum": "min"}
 
 
-_CONV_TUNE: dict = {}  # layer signature -> ("pp", tile, splits) | ("incumbent", None, None)
-
-
-def _time_concurrent(f1, f2, dev, reps: int = 5) -> float:
-    """µs per pair of launches issued on two streams that run concurrently."""
-    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    cur = torch.cuda.current_stream(dev)
-    for s, f in ((s1, f1), (s2, f2)):
-        s.wait_stream(cur)
-        with torch.cuda.stream(s):
-            f()
-    torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(cur)
-    for s in (s1, s2):
-        s.wait_stream(cur)
-    for _ in range(reps):
-        with torch.cuda.stream(s1):
-            f1()
-        with torch.cuda.stream(s2):
-            f2()
-    cur.wait_stream(s1)
-    cur.wait_stream(s2)
-    e1.record(cur)
-    torch.cuda.synchronize(dev)
-    return e0.elapsed_time(e1) * 1e3 / reps
-
-
-def _time_launch(fn, dev, reps: int = 5) -> float:
-    """Median-free quick timing of a launch sequence (µs per call) on the current stream."""
-    fn()
-    torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        fn()
-    e1.record()
-    torch.cuda.synchronize(dev)
-    return e0.elapsed_time(e1) * 1e3 / reps
-
-
-
 def _cfg():
     from ..config import current
 
     return current()
 
-def _lite_tile(Cout: int, dual: bool = False, M: int = 0) -> int:
-    """kernels/conv_pp.hip tile of a bf16 conv_lite layer: 2 (128x128), 4 (the same on DMA /
-    MFMA waves, ``conv_lite_ws``) or 5 (128x256 with a 32-deep K-tile for Cout >= 256,
-    ``conv_lite_wide``: the input tile staged once per 256 channels — 1: every such layer,
-    2: only where the 256-wide grid keeps >= 768 workgroups, 1.5 waves of two per CU; the
-    short stage 3/4 grids lost with it, profiles/r04_ad)."""
-    c = _cfg()
-    w = int(c.conv_lite_wide)
-    if w and Cout >= 256 and (w == 1 or -(-M // 128) * -(-Cout // 256) >= 768):
-        return 5
-    return 4 if (c.conv_lite_ws and not dual) else 2
-
-
-def _lite_fp8_cfg() -> int:
-    """kernels/fp8.hip cfg of the conv_lite_fp8 tile: 8, 9 (DMA / MFMA waves,
-    ``conv_lite_ws``), 10 (the 192-wide channel tile allowed, ``fp8_lite_wide`` 1) or 11
-    (the tile staging the fewest rows, 160 and 192 included, ``fp8_lite_wide`` 2) or 12 (the
-    same over whole waves of 512 workgroups, ``fp8_lite_wide`` 3)."""
-    c = _cfg()
-    return 9 if c.conv_lite_ws else {0: 8, 1: 10, 2: 11, 3: 12}[int(c.fp8_lite_wide)]
+# conv_lite tiles (kernels/conv_pp.hip): bf16 tile 2 = 128 pixels x 128 channels on 4 waves,
+# two LDS-DMA stages; fp8 cfg 11 = the channel tile (192 / 160 / 128 / 96 / 64) staging the
+# fewest rows per layer (profiles/r04_af).  Measured slower and removed (numbers in the
+# profile READMEs): the 128x256 bf16 tile (r04_ad), the 8-wave DMA / MFMA-split tiles (r04_u,
+# r04_w), the halo-staged 3x3 kernel (r04_s-u), the 32-deep tile, the fp8 tile choosers
+# 0 / 1 / 3 (r04_ac, r04_ah), conv_lite for the deep-K 1x1 reduces (r03_conv), the streamed
+# stage-2 block tail (r01_tail), the persistent dual projection kernel (r02_pw_res2) and the
+# probe-selected ping-pong conv_pp tiles (r02_conv_pp).
+LITE_TILE = 2
+LITE_FP8_CFG = 11
 
 
 class CompileError(RuntimeError):
@@ -822,20 +770,6 @@ class CompiledFunction(TransformerLowering):
             w_nk = w_dev.reshape(Cout, Cin)
             bz = b_dev if b_dev is not None else self._dev(torch.zeros(Cout), torch.float32)
             M = int(np.prod(xin.shape[:-1]))
-            if _cfg().conv_impl == "lite" and _cfg().conv_lite_pointwise and Cin >= 1024 and len(xin.shape) == 4:
-                # stage 3/4 reduces: the 4-wave LDS-DMA tile beats the 256x256 ping-pong GEMM
-                # (stage 3: 37.8 vs 43.5 µs, profiles/r03_conv) and leaves room on the CU
-                cl = K.ConvPP([(tuple(xin.shape), (1, 1), (1, 1), (0, 0), (1, 1))], Cout, tuple(out.shape[1:3]),
-                              self.device, tile=_lite_tile(Cout, M=int(np.prod(out.shape[:3]))))
-
-                def run_cl(xin=xin, out=out, cl=cl, w_nk=w_nk, bz=bz, act=act):
-                    cl([xin.buf], w_nk, bz, None, act, out=_target(out), out_channel_offset=_coff(out))
-
-                self._emit(node.name, "conv", run_cl, [xin], [out], {"impl": "conv_lite"})
-                self.conv_lite_layers = getattr(self, "conv_lite_layers", 0) + 1
-                self.vals[(last.name, 0)] = out
-                self._alias_fused_outputs(absorbed, out)
-                return
             splits = K.gemm_pp_splits(M, Cout, Cin)
             ws = torch.empty(splits * M * Cout, dtype=torch.float32, device=self.device) if splits > 1 else None
 
@@ -877,33 +811,19 @@ class CompiledFunction(TransformerLowering):
                           (pt, pb, pl, pr), (dh, dw), act, out=_target(out), out_channel_offset=_coff(out),
                           out_scale=_eff_scale(out) if out.qscale is not None else None)
 
-        lite = (self.device.type == "cuda" and _cfg().conv_impl == "lite" and out.qscale is None
+        lite = (self.device.type == "cuda" and out.qscale is None
                 and xin_shape_override is None and (xin.phys_c or Cin) == Cin and Cin % 64 == 0 and Cout % 8 == 0
                 and _coff(out) % 8 == 0 and out.dtype == torch.bfloat16 and xin.dtype == torch.bfloat16
                 and not pointwise and act in (K.ACT_NONE, K.ACT_RELU)
                 and (res_val is None or (res_val.concat_slot is None and res_val.qscale is None
                                          and tuple(res_val.shape) == tuple(out.shape) and res_val.alias_of is None))
                 and max(pt, pb) < 1024 and max(pl, pr) < 1024)
-        halo = (lite and res_val is None and _cfg().conv3x3_halo and b_dev is not None
-                and K.conv3x3_halo_eligible(tuple(xin.shape), tuple(w_ohwi.shape), (sh, sw), (pt, pb, pl, pr),
-                                            (dh, dw), None, act))
-        if halo:
-            # stride-1 3x3 convs (ResNet stages 2-4): the input is filled into LDS once per 64
-            # channels as the tile's halo, not once per tap (kernels/conv3x3h.hip)
-            def run(xin=xin, out=out, w_dev=w_dev, b_dev=b_dev):  # noqa: F811
-                K.conv3x3_halo(xin.buf, w_dev, b_dev, act, out=_target(out), out_channel_offset=_coff(out))
-
-            self._emit(node.name, "conv", run, [xin], [out], {"impl": "conv3x3h"})
-            self.conv3x3h_layers = getattr(self, "conv3x3h_layers", 0) + 1
-            self.vals[(last.name, 0)] = out
-            self._alias_fused_outputs(absorbed, out)
-            return
         if lite:
             # KxK convs (stage 2-4 3x3): 4-wave 128x128 implicit GEMM on two LDS-DMA stages
             # (kernels/conv_pp.hip conv_lite): 6-24 % faster than the register-staged igemm
             # per layer and 64 KiB of LDS, so it shares a CU with the sibling lane
             cl = K.ConvPP([(tuple(xin.shape), (KHe, KWe), (sh, sw), (pt, pl), (dh, dw))], Cout, tuple(out.shape[1:3]),
-                          self.device, tile=_lite_tile(Cout, M=int(np.prod(out.shape[:3]))))  # tiles 3 (32-deep K), 256x128 (4 or 8 waves) and 3-stage
+                          self.device, tile=LITE_TILE)  # tiles 3 (32-deep K), 256x128 (4 or 8 waves) and 3-stage
             # variants (raw-barrier, counted vmcnt) measured slower: profiles/r03_conv, r04_a, r04_c
 
             def run(xin=xin, out=out, res_val=res_val, cl=cl, w2=w_dev.reshape(Cout, -1), b_dev=b_dev):  # noqa: F811
@@ -911,15 +831,6 @@ class CompiledFunction(TransformerLowering):
                    out_channel_offset=_coff(out))
 
             self.conv_lite_layers = getattr(self, "conv_lite_layers", 0) + 1
-        elif out.qscale is None and xin_shape_override is None and (xin.phys_c or Cin) == Cin:
-            pp = self._conv_pp_choice(node.name, [(tuple(xin.shape), (KHe, KWe), (sh, sw), (pt, pl), (dh, dw))],
-                                      Cout, out, res_val, act, w_dev, b_dev,
-                                      lambda xs, o, r: K.conv2d_nhwc(xs[0], w_dev, b_dev, r, (sh, sw),
-                                                                     (pt, pb, pl, pr), (dh, dw), act, out=o))
-            if pp is not None:
-                def run(xin=xin, out=out, res_val=res_val, pp=pp, w2=w_dev.reshape(Cout, -1), b_dev=b_dev):  # noqa: F811
-                    pp([xin.buf], w2, b_dev, res_val.buf if res_val is not None else None, act, out=_target(out),
-                       out_channel_offset=_coff(out))
 
         shortcut_ok = (KHe == KWe == 1 and sh == sw and (pt, pb, pl, pr) == (0, 0, 0, 0) and (dh, dw) == (1, 1)
                        and res_val is None and act == K.ACT_NONE and out.qscale is None
@@ -968,21 +879,12 @@ class CompiledFunction(TransformerLowering):
             return True
 
         s2cfg = {"s2": s2}  # _decimate_tails: x2 stored already decimated -> stride 1
-        # stride 1 over a same-size x2 (the decimated stage-1 -> 2 hand-over): opt-in
-        # (EngineConfig.pw_dual_kernel) persistent prefetching kernel (kernels/pw_res.hip, dual form) — 10 %
-        # faster alone (124 vs 139 µs) but 0.2-0.4 % slower end to end next to the sibling
-        # lane (profiles/r02_pw_res2)
-        use_pw = (act == K.ACT_RELU and K.pw_dual_ok(K1, C2, Cout) and (xin.phys_c or K1) == K1
-                  and (x2.phys_c or C2) == C2 and _cfg().pw_dual_kernel)
 
-        def run(xin=xin, x2=x2, out=out, w_dev=w_dev, b_dev=b_dev, s2cfg=s2cfg, use_pw=use_pw):
-            if use_pw and s2cfg["s2"] == 1 and tuple(x2.buf.shape[:3]) == tuple(xin.buf.shape[:3]):
-                K.pw_dual(xin.buf, x2.buf, w_dev, b_dev, out=_target(out), out_channel_offset=_coff(out))
-                return
+        def run(xin=xin, x2=x2, out=out, w_dev=w_dev, b_dev=b_dev, s2cfg=s2cfg):
             K.conv1x1_dual(xin.buf, x2.buf, w_dev, b_dev, s2cfg["s2"], act, out=_target(out),
                            out_channel_offset=_coff(out))
 
-        if (self.device.type == "cuda" and _cfg().conv_impl == "lite" and not use_pw and K1 % 64 == 0
+        if (self.device.type == "cuda" and K1 % 64 == 0
                 and C2 % 64 == 0 and (xin.phys_c or K1) == K1 and (x2.phys_c or C2) == C2
                 and act in (K.ACT_NONE, K.ACT_RELU) and out.dtype == torch.bfloat16 and out.qscale is None
                 and _coff(out) % 8 == 0 and len(xin.shape) == 4 and N * Ho * Wo <= 65536):
@@ -993,11 +895,11 @@ class CompiledFunction(TransformerLowering):
             # stage 2's 200k-row GEMM stays on the igemm (141 vs 158 µs, profiles/r03_operating_points)
             xs0 = (tuple(xin.shape), (1, 1), (1, 1), (0, 0), (1, 1))
             lite = {s2: K.ConvPP([xs0, (tuple(x2.shape), (1, 1), (s2, s2), (0, 0), (1, 1))], Cout, (Ho, Wo),
-                                 self.device, tile=_lite_tile(Cout, dual=True, M=N * Ho * Wo))}
+                                 self.device, tile=LITE_TILE)}
             N2, H2, W2, _ = x2.shape
             if s2 == 2 and H2 % 2 == 0 and W2 % 2 == 0:
                 lite[1] = K.ConvPP([xs0, ((N2, H2 // 2, W2 // 2, C2), (1, 1), (1, 1), (0, 0), (1, 1))], Cout, (Ho, Wo),
-                                   self.device, tile=_lite_tile(Cout, dual=True, M=N * Ho * Wo))
+                                   self.device, tile=LITE_TILE)
 
             def run(xin=xin, x2=x2, out=out, w_dev=w_dev, b_dev=b_dev, s2cfg=s2cfg, lite=lite):  # noqa: F811
                 lite[s2cfg["s2"]]([xin.buf, x2.buf], w_dev, b_dev, None, act, out=_target(out),
@@ -1010,17 +912,7 @@ class CompiledFunction(TransformerLowering):
             self.fused_shortcuts = getattr(self, "fused_shortcuts", 0) + 1
             return True
 
-        pp = None
-        if (xin.phys_c or K1) == K1 and (x2.phys_c or C2) == C2:
-            pp = self._conv_pp_choice(node.name, [(tuple(xin.shape), (1, 1), (1, 1), (0, 0), (1, 1)),
-                                                  (tuple(x2.shape), (1, 1), (s2, s2), (0, 0), (1, 1))],
-                                      Cout, out, None, act, w_dev, b_dev,
-                                      lambda xs, o, r: K.conv1x1_dual(xs[0], xs[1], w_dev, b_dev, s2, act, out=o))
-            if pp is not None:
-                def run(xin=xin, x2=x2, out=out, pp=pp, w_dev=w_dev, b_dev=b_dev):  # noqa: F811
-                    pp([xin.buf, x2.buf], w_dev, b_dev, None, act, out=_target(out), out_channel_offset=_coff(out))
-
-        self._emit(node.name, "conv", run, [xin, x2], [out], {"s2cfg": s2cfg} if pp is None else None)
+        self._emit(node.name, "conv", run, [xin, x2], [out], {"s2cfg": s2cfg})
         self.vals[(last.name, 0)] = out
         self._alias_fused_outputs(absorbed, out)
         self.fused_shortcuts = getattr(self, "fused_shortcuts", 0) + 1
@@ -1038,11 +930,9 @@ class CompiledFunction(TransformerLowering):
             return False
         cx = xin.shape[-1]
         co = 4 * cx
-        # stage 2 (weights streamed through LDS) measured no faster than the two convs it
-        # replaces (profiles/r01_tail): opt-in only
-        wide = _cfg().fuse_wide_tails
-        widths = {64: (64, 128), 128: (128,) if wide else ()}.get(cx, ()) if xs_val is None \
-            else ((64,) if cx == 64 else ())
+        # (stage 2, its weights streamed through LDS, measured no faster than the two convs
+        # it would replace: profiles/r01_tail — stage 1 only)
+        widths = {64: (64, 128)}.get(cx, ()) if xs_val is None else ((64,) if cx == 64 else ())
 
         def plain(v):
             return v.shape[-1] == cx and (v.phys_c or cx) == cx and v.concat_slot is None and v.qscale is None \
@@ -1105,65 +995,6 @@ class CompiledFunction(TransformerLowering):
         self._alias_fused_outputs(absorbed2, out2)
         self.fused_tails = getattr(self, "fused_tails", 0) + 1
         return True
-
-    def _conv_pp_choice(self, name, srcs, Cout, out: Val, res_val, act, w_dev, b_dev, incumbent):
-        """A ``ConvPP`` launch for this convolution when the ping-pong implicit GEMM
-        (kernels/conv_pp.hip) beats the incumbent kernel on this exact layer, else None.
-
-        The choice is measured, not guessed: both candidates (and both conv_pp tile shapes)
-        run a few times on scratch tensors of the layer's shapes on this device, and the
-        result is cached per layer signature for the process (every bucket plan and lane of
-        a model reuses it).  Default off (``EngineConfig.conv_impl = "incumbent"``): with two compute
-        lanes the probe-selected layers measured ~1 % slower end to end
-        (profiles/r02_conv_pp); ``conv_impl = "auto"`` enables the probe, ``"pp"`` forces
-        conv_pp wherever eligible."""
-        force = _cfg().conv_impl
-        if self.device.type != "cuda" or force in ("incumbent", "lite") or self.precision == "fp8":
-            return None
-        if any(s[0][3] % 64 for s in srcs) or Cout % 8 or _coff(out) % 8 or out.dtype != torch.bfloat16:
-            return None
-        if res_val is not None and (res_val.concat_slot is not None or res_val.qscale is not None
-                                    or tuple(res_val.shape) != tuple(out.shape) or res_val.alias_of is not None):
-            return None
-        N, OH, OW, _ = out.shape
-        key = (tuple(srcs), Cout, (OH, OW), res_val is not None, int(K.act_code(act)), out.shape[-1] != Cout)
-        hit = _CONV_TUNE.get(key)
-        if hit is None:
-            hit = self._tune_conv(srcs, Cout, (OH, OW), res_val is not None, act, w_dev, b_dev, incumbent, force)
-            _CONV_TUNE[key] = hit
-            LOG.info("conv %s %s -> %s", name, key[:3], hit)
-        if hit[0] == "incumbent":
-            return None
-        self.conv_pp_layers = getattr(self, "conv_pp_layers", 0) + 1
-        return K.ConvPP(srcs, Cout, (OH, OW), self.device, tile=hit[1], splits=hit[2])
-
-    def _tune_conv(self, srcs, Cout, ohw, with_res, act, w_dev, b_dev, incumbent, force):
-        dev = self.device
-        g = torch.Generator(device=dev).manual_seed(0)
-        xs = [torch.randn(s[0], device=dev, generator=g).to(torch.bfloat16) for s in srcs]
-        N = srcs[0][0][0]
-        o = torch.empty((N, *ohw, Cout), dtype=torch.bfloat16, device=dev)
-        r = torch.randn((N, *ohw, Cout), device=dev, generator=g).to(torch.bfloat16) if with_res else None
-        o2 = torch.empty_like(o)
-        w2 = w_dev.reshape(Cout, -1)
-        cands = {}
-        for tile in (0, 1):
-            cp = K.ConvPP(srcs, Cout, ohw, dev, tile=tile)
-            cp2 = K.ConvPP(srcs, Cout, ohw, dev, tile=tile)  # own split-K workspace
-            cands[("pp", tile, cp.splits)] = (lambda cp=cp: cp(xs, w2, b_dev, r, act, out=o),
-                                             lambda cp2=cp2: cp2(xs, w2, b_dev, r, act, out=o2))
-        if force != "pp":
-            cands[("incumbent", None, None)] = (lambda: incumbent(xs, o, r), lambda: incumbent(xs, o2, r))
-        # timed as TWO concurrent instances on two streams: plans run in compute lanes, and a
-        # kernel that monopolises the CUs (one 160 KiB-LDS workgroup per CU) can win alone
-        # and lose next to the sibling lane's kernels (measured: profiles/r02_conv_pp)
-        best, best_t = None, float("inf")
-        for k, (f1, f2) in cands.items():
-            t = _time_concurrent(f1, f2, dev)
-            if t < best_t:
-                best, best_t = k, t
-        del xs, o, o2, r
-        return best
 
     def _fusable_maxpool(self, last: Node, act, out: Val, fp8: bool = False):
         """The single consumer of a ReLU conv chain when it is a 3x3 / stride-2 NHWC
@@ -1268,7 +1099,7 @@ class CompiledFunction(TransformerLowering):
 
         # fp8 input: the 4-wave LDS-DMA tile (kernels/fp8.hip conv_lite_fp8, cfg 8); a bf16
         # input (the layer after the stem) is quantised on load by the register-staged kernel
-        cfg = _lite_fp8_cfg() if (x.qscale is not None and _cfg().conv_impl == "lite") else -1
+        cfg = LITE_FP8_CFG if x.qscale is not None else -1
         # (an eight-wave 256-pixel tile on three LDS stages measured 5-40 % slower per layer
         # and -2 % in the bench: profiles/r04_d)
 
@@ -1596,11 +1427,10 @@ class CompiledFunction(TransformerLowering):
         self.params += [wq_dev, cs_dev, b_dev, lo_dev]
         self.fp8_layers += len(members)
 
-        def run(x=x, segs=segs, wq=wq_dev, ws=ws_dev, cs=cs_dev, b=b_dev, lo=lo_dev, xs=xs, wsp=_cfg().conv_lite_ws,
-                wide=int(_cfg().fp8_lite_wide)):
+        def run(x=x, segs=segs, wq=wq_dev, ws=ws_dev, cs=cs_dev, b=b_dev, lo=lo_dev, xs=xs):
             F8.conv2d_nhwc_fp8_multi(_view(x), xs, wq, (1, 1), ws, b, lo,
                                      [(_target(v), a, e, _coff(v), _eff_scale(v) if v.qscale is not None else None)
-                                      for v, a, e in segs], chan_scale=cs, ws=wsp, wide=wide)
+                                      for v, a, e in segs], chan_scale=cs)
 
         self._emit("+".join(m["conv"].name for m in members), "conv_fp8", run, [x], [v for v, _, _ in segs],
                    {"impl": "conv_lite_fp8_multi", "multi_out": True})
@@ -1669,7 +1499,7 @@ class CompiledFunction(TransformerLowering):
             wq_dev, ws_dev, cs_dev = self._dev(wq), self._dev(ws), self._dev(ws * x.qscale, torch.float32)
             self.params += [wq_dev, cs_dev, zero, b_dev]
             self.fp8_layers += 1
-            cfg = _lite_fp8_cfg() if (self.device.type == "cuda" and _cfg().conv_impl == "lite") else -1
+            cfg = LITE_FP8_CFG if self.device.type == "cuda" else -1
 
             def run_conv(x=x, y=y, wq=wq_dev, ws=ws_dev, cs=cs_dev, zero=zero, cfg=cfg, xs=x.qscale):
                 F8.conv2d_nhwc_fp8(_view(x), xs, wq, (1, 1), ws, zero, act=K.ACT_NONE, out=y.buf, chan_scale=cs,
@@ -2314,8 +2144,7 @@ class CompiledFunction(TransformerLowering):
                 "fp8_layers": self.fp8_layers, "fused_shortcuts": getattr(self, "fused_shortcuts", 0),
                 "fused_tails": getattr(self, "fused_tails", 0), "decimated_tails": getattr(self, "decimated_tails", 0),
                 "fused_pools": getattr(self, "fused_pools", 0), "conv3x3c64": getattr(self, "conv3x3c64", 0),
-                "conv3x3h": getattr(self, "conv3x3h_layers", 0),
-                "conv_pp": getattr(self, "conv_pp_layers", 0), "pw_res": getattr(self, "pw_res_layers", 0),
+                "pw_res": getattr(self, "pw_res_layers", 0),
                 "conv_lite": getattr(self, "conv_lite_layers", 0),
                 "commuted_pools": getattr(self, "commuted_pools", 0),
                 "sibling_groups": getattr(self, "sibling_groups", 0),

@@ -257,218 +257,6 @@ void launch_tail(const bf16* x2, const bf16* xs, const bf16* res, const bf16* w3
 }
 
 
-// ------------------------------------------------------------------------------------
-// Stage 2 (128 / 512 channels): y3 = relu(x2 . W3^T + b3 + r) (128 -> 512) and
-// y1 = relu(y3 . W1^T + b1) (512 -> 128).  The two weight matrices (2 x 128 KB) do not fit
-// next to the tiles, so they stream through a double-buffered LDS stage in 8 chunks of
-// [128 rows][128 k] per 64-pixel tile (W3 rows 128j.. for j < 4, W1's k-slice 128(j-4).. for
-// j >= 4; the same chunk sequence every tile, so it stays L2-resident), prefetched two
-// chunks ahead in registers.  LDS: X tile (x2, then the y1 staging tile) 16 KB | Y tile
-// [64][512] 64 KB | 2 x 32 KB weight stage = 144 KB.  Waves: 2 (32-pixel halves) x 4
-// (32-channel quarters of the chunk's 128 outputs); the next tile's residual and x2 loads
-// are issued during phase 2.  Measured 166 µs per boundary at micro-batch 256 — no faster
-// than the expand + reduce convs it replaces (the weight stream's L2 latency is exposed
-// with only two chunks in flight), so the compiler uses it only with EngineConfig.fuse_wide_tails.
-constexpr int WX = 128, WO = 512, WTP = 64;
-constexpr int WCHUNK = 128 * 128 / 8;  // 16-B pieces of one weight chunk
-constexpr int WIT = WCHUNK / NT;       // 4 per thread
-
-__global__ __launch_bounds__(NT, 1) void bottleneck_tail_wide_kernel(
-    const bf16* __restrict__ x2, const bf16* __restrict__ res, const bf16* __restrict__ w3,
-    const float* __restrict__ b3, const bf16* __restrict__ w1, const float* __restrict__ b1, bf16* __restrict__ y3,
-    bf16* __restrict__ y1, int M) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  u32x4* Xs = reinterpret_cast<u32x4*>(smem);                     // [64][128]
-  u32x4* Ys = reinterpret_cast<u32x4*>(smem + WTP * WX * 2);      // [64][512]
-  u32x4* Wb = reinterpret_cast<u32x4*>(smem + WTP * WX * 2 + WTP * WO * 2);  // 2 x [128][128]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int prow = lane & 15, kg = lane >> 4;
-  const int wp = wave & 1, wc = wave >> 1;
-  const int ntiles = (M + WTP - 1) / WTP;
-  if ((int)blockIdx.x >= ntiles) return;  // block-uniform, before any barrier
-
-  u32x4 wr[2][WIT];
-  auto load_w = [&](int g, u32x4(&dst)[WIT]) {
-    const bf16* base = g < 4 ? w3 + (size_t)g * 128 * WX : w1 + 128 * (g - 4);
-    const int pitch = g < 4 ? WX : WO;
-    asm volatile("" : "+s"(base));  // opaque per call: no hoisted per-chunk address registers
-#pragma unroll
-    for (int it = 0; it < WIT; ++it) {
-      const int q = tid + it * NT, r = q >> 4, c = q & 15;
-      dst[it] = *reinterpret_cast<const u32x4*>(base + r * pitch + c * 8);
-    }
-  };
-  auto store_w = [&](int buf, const u32x4(&src)[WIT]) {
-#pragma unroll
-    for (int it = 0; it < WIT; ++it) {
-      const int q = tid + it * NT;
-      Wb[buf * WCHUNK + swz<16>(q >> 4, q & 15)] = src[it];
-    }
-  };
-  constexpr int XIT = WTP * WX / 8 / NT;  // 2
-  constexpr int YIT = WTP * WO / 8 / NT;  // 8
-  u32x4 xr[XIT], rv[YIT];
-  auto load_x = [&](int t) {
-#pragma unroll
-    for (int it = 0; it < XIT; ++it) {
-      const int q = tid + it * NT, px = t * WTP + (q >> 4);
-      xr[it] = px < M ? reinterpret_cast<const u32x4*>(x2 + (size_t)px * WX)[q & 15] : u32x4{0u, 0u, 0u, 0u};
-    }
-  };
-  auto store_x = [&]() {
-#pragma unroll
-    for (int it = 0; it < XIT; ++it) {
-      const int q = tid + it * NT;
-      Xs[swz<16>(q >> 4, q & 15)] = xr[it];
-    }
-  };
-  auto load_r = [&](int t) {
-#pragma unroll
-    for (int it = 0; it < YIT; ++it) {
-      const int q = tid + it * NT, px = t * WTP + (q >> 6);
-      rv[it] = px < M ? reinterpret_cast<const u32x4*>(res + (size_t)px * WO)[q & 63] : u32x4{0u, 0u, 0u, 0u};
-    }
-  };
-
-  int t = blockIdx.x;
-  load_w(0, wr[0]);
-  load_w(1, wr[1]);
-  load_r(t);
-  load_x(t);
-  store_w(0, wr[0]);
-  load_w(2, wr[0]);
-  store_x();
-  __syncthreads();
-  while (true) {
-    const int p0 = t * WTP;
-    const int tn = t + gridDim.x;
-    const bool more = tn < ntiles;
-    f32x4 acc2[2][2];
-    // one weight chunk; J is a template constant so the register-slot indices stay static
-    auto chunk_step = [&](auto Jc) {
-      constexpr int j = decltype(Jc)::value;
-      const u32x4* W = Wb + (j & 1) * WCHUNK;
-      if constexpr (j < 4) {
-        // ---- phase 1, chunk j: y3 channels 128j + (32 wc ..) for pixels 32 wp ..
-        f32x4 acc[2][2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < WX / 32; ++ks) {
-          const int c = ks * 4 + kg;
-          bf16x8 a[2], b[2];
-#pragma unroll
-          for (int i = 0; i < 2; ++i) a[i] = __builtin_bit_cast(bf16x8, W[swz<16>(wc * 32 + i * 16 + prow, c)]);
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj) b[jj] = __builtin_bit_cast(bf16x8, Xs[swz<16>(wp * 32 + jj * 16 + prow, c)]);
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj)
-              acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[jj], acc[i][jj], 0, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int co = 128 * j + wc * 32 + i * 16 + kg * 4;
-          const f32x4 bv = *reinterpret_cast<const f32x4*>(b3 + co);
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj) {
-            bf16x4 o;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[i][jj][r] + bv[r]);
-            bf16* chunk = reinterpret_cast<bf16*>(Ys + swz<64>(wp * 32 + jj * 16 + prow, co >> 3));
-            *reinterpret_cast<bf16x4*>(chunk + (co & 7)) = o;
-          }
-        }
-      } else {
-        // ---- phase 2, chunk j: y1 += Y[:, 128(j-4) ..] . W1[:, 128(j-4) ..]^T
-        if constexpr (j == 4) {
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj) acc2[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const int c = ks * 4 + kg;
-          bf16x8 a[2], b[2];
-#pragma unroll
-          for (int i = 0; i < 2; ++i) a[i] = __builtin_bit_cast(bf16x8, W[swz<16>(wc * 32 + i * 16 + prow, c)]);
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
-            b[jj] = __builtin_bit_cast(bf16x8, Ys[swz<64>(wp * 32 + jj * 16 + prow, (j - 4) * 16 + c)]);
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj)
-              acc2[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[jj], acc2[i][jj], 0, 0, 0);
-        }
-        if constexpr (j == 7) {  // y1 tile -> X region (x2 is no longer read)
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int co = wc * 32 + i * 16 + kg * 4;
-            const f32x4 bv = *reinterpret_cast<const f32x4*>(b1 + co);
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj) {
-              bf16x4 o;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) o[r] = f2bf(fmaxf(acc2[i][jj][r] + bv[r], 0.f));
-              bf16* chunk = reinterpret_cast<bf16*>(Xs + swz<16>(wp * 32 + jj * 16 + prow, co >> 3));
-              *reinterpret_cast<bf16x4*>(chunk + (co & 7)) = o;
-            }
-          }
-        }
-      }
-      // weight pipeline: chunk j+1 into the other LDS buffer, chunk j+3 into its registers
-      store_w((j + 1) & 1, wr[(j + 1) & 1]);
-      if (more || j + 3 < 8) load_w((j + 3) & 7, wr[(j + 1) & 1]);
-      __syncthreads();
-      if constexpr (j == 3) {
-        // ---- + residual, relu -> y3 (global) and back into Y
-#pragma unroll
-        for (int it = 0; it < YIT; ++it) {
-          const int q = tid + it * NT;
-          const int pl = q >> 6, c = q & 63;
-          const int si = swz<64>(pl, c);
-          bf16x8 v = __builtin_bit_cast(bf16x8, Ys[si]);
-          const bf16x8 r = __builtin_bit_cast(bf16x8, rv[it]);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = f2bf(fmaxf((float)v[e] + (float)r[e], 0.f));
-          Ys[si] = __builtin_bit_cast(u32x4, v);
-          if (p0 + pl < M) reinterpret_cast<u32x4*>(y3 + (size_t)(p0 + pl) * WO)[c] = __builtin_bit_cast(u32x4, v);
-        }
-        if (more) {  // next tile's activations in flight during phase 2
-          load_r(tn);
-          load_x(tn);
-        }
-        __syncthreads();
-      }
-    };
-    chunk_step(std::integral_constant<int, 0>{});
-    chunk_step(std::integral_constant<int, 1>{});
-    chunk_step(std::integral_constant<int, 2>{});
-    chunk_step(std::integral_constant<int, 3>{});
-    chunk_step(std::integral_constant<int, 4>{});
-    chunk_step(std::integral_constant<int, 5>{});
-    chunk_step(std::integral_constant<int, 6>{});
-    chunk_step(std::integral_constant<int, 7>{});
-    // ---- coalesced y1 stores
-#pragma unroll
-    for (int it = 0; it < XIT; ++it) {
-      const int q = tid + it * NT;
-      const int pl = q >> 4, c = q & 15;
-      if (p0 + pl < M) reinterpret_cast<u32x4*>(y1 + (size_t)(p0 + pl) * WX)[c] = Xs[swz<16>(pl, c)];
-    }
-    if (!more) break;
-    __syncthreads();  // staging read before the next x2 overwrites it
-    store_x();
-    __syncthreads();
-    t = tn;
-  }
-}
-
 }  // namespace
 
 // x2 [M, 64], res [M, 256] (or, dual: xs [M, 64] and no residual), w3 [256, 64] (dual:
@@ -503,28 +291,6 @@ void bottleneck_tail_bf16(uintptr_t x2, uintptr_t xs, uintptr_t res, uintptr_t w
   FTM_CHECK_LAUNCH();
 }
 
-// x2 [M, 128], res [M, 512], w3 [512, 128], b3 [512], w1 [128, 512], b1 [128] -> y3 [M, 512],
-// y1 [M, 128].
-void bottleneck_tail_wide_bf16(uintptr_t x2, uintptr_t res, uintptr_t w3, uintptr_t b3, uintptr_t w1, uintptr_t b1,
-                               uintptr_t y3, uintptr_t y1, int M, int num_cu, uintptr_t stream) {
-  if (M <= 0) throw std::invalid_argument("bottleneck_tail_wide: empty problem");
-  if ((long)M * WO >= (1L << 31)) throw std::invalid_argument("bottleneck_tail_wide: tensor too large");
-  for (uintptr_t p : {x2, res, w3, w1, y3, y1, b3, b1})
-    if (!p || p % 16) throw std::invalid_argument("bottleneck_tail_wide: null or non-16-byte-aligned pointer");
-  const int tiles = (M + WTP - 1) / WTP;
-  const int grid = tiles < num_cu ? tiles : num_cu;
-  constexpr size_t lds = WTP * WX * 2 + WTP * WO * 2 + 2 * WCHUNK * 16;
-  static_assert(lds <= 160 * 1024, "LDS");
-  hipFuncSetAttribute((const void*)bottleneck_tail_wide_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL(bottleneck_tail_wide_kernel, dim3(grid), dim3(NT), lds, reinterpret_cast<hipStream_t>(stream),
-                     reinterpret_cast<const bf16*>(x2), reinterpret_cast<const bf16*>(res),
-                     reinterpret_cast<const bf16*>(w3), reinterpret_cast<const float*>(b3),
-                     reinterpret_cast<const bf16*>(w1), reinterpret_cast<const float*>(b1), reinterpret_cast<bf16*>(y3),
-                     reinterpret_cast<bf16*>(y1), M);
-  FTM_CHECK_LAUNCH();
-}
-
 void register_bottleneck(pybind11::module_& m) {
   m.def("bottleneck_tail_bf16", &bottleneck_tail_bf16);
-  m.def("bottleneck_tail_wide_bf16", &bottleneck_tail_wide_bf16);
 }

@@ -78,9 +78,6 @@ struct Fp8Params {
   int tiles_m, tiles_n;
   int prio;  // s_setprio(1) around each K-tile's MFMA cluster (fp8_prio)
   unsigned long long* stamp;  // conv_lite_fp8 STAMP diagnostics: [64 workgroups][64 K-tiles][5] clocks
-  int ws;                     // conv_lite_fp8 on DMA / MFMA waves (cfg 9, multi: mode bit 0)
-  int wide;                   // conv_lite_fp8 channel tiles: 1 = + 192 (cfg 10), 2 = fewest staged rows over
-                              // 192 / 160 / 128 / 96 / 64 (cfg 11); multi: mode >> 1
 };
 
 // Multi-output epilogue of conv_lite_fp8 (horizontally fused sibling 1x1 convs of one
@@ -365,10 +362,9 @@ void launch_tile(const Fp8Params& p, int act, int cfg, hipStream_t s) {
 // load latency of these streaming layers).
 // STAMP (diagnostics, bench/conv_stamp_probe.py --fp8): as conv_pp.hip's conv_lite STAMP —
 // wave 0 of the first 64 workgroups records s_memtime around each K-tile's phases.
-// WS (cfg 9): eight waves, the roles split as conv_pp.hip's conv_lite_ws — waves 0-3 run
-// only the MFMAs, waves 4-7 only issue the LDS-DMA (wave 4 + w stages wave w's pieces).
-// Inception-v3 measured 4.5 % slower with it (profiles/r04_w): opt-in (conv_lite_ws).
-template <bool OUT_FP8, int ACT, int BN_, int NSTG, bool MULTI, bool STAMP, bool WS>
+// (An eight-wave form with the DMA and MFMA roles split measured 4.5 % slower on
+// Inception-v3, profiles/r04_w, and was removed.)
+template <bool OUT_FP8, int ACT, int BN_, int NSTG, bool MULTI, bool STAMP>
 __device__ __forceinline__ void conv_lite_fp8_body(const Fp8Params& p, const Fp8Segs& sg) {
   static_assert(BN_ == 192 || BN_ == 160 || BN_ == 128 || BN_ == 96 || BN_ == 64, "channel tile 192 .. 64");
   constexpr int BM = 128, BN = BN_;
@@ -388,11 +384,8 @@ __device__ __forceinline__ void conv_lite_fp8_body(const Fp8Params& p, const Fp8
   const int m0 = tm * BM;
   const int n0 = tn * BN;
   const int lane = threadIdx.x & 63;
-  constexpr int NT = WS ? 512 : 256;
-  const int wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool dma_wave = !WS || wave_id >= 4;  // wave-uniform roles (both, without WS)
-  const bool mma_wave = !WS || wave_id < 4;
-  const int wave = wave_id & 3;  // the role's wave index
+  constexpr int NT = 256;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave & 1, wn = wave >> 1;
 
   const int drow = lane >> 3;
@@ -481,17 +474,16 @@ __device__ __forceinline__ void conv_lite_fp8_body(const Fp8Params& p, const Fp8
   if constexpr (STAMP) {
     if (threadIdx.x == 0 && blockIdx.x < 64) sp = p.stamp + (size_t)blockIdx.x * 64 * 5;
   }
-  if (dma_wave) dma(0);
+  dma(0);
   for (int kt = 0; kt < nk; ++kt) {
     const int st = NSTG == 1 ? 0 : (kt & 1);
     if constexpr (STAMP) t0 = __builtin_amdgcn_s_memtime();
-    if (dma_wave) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (STAMP) t1 = __builtin_amdgcn_s_memtime();
     __syncthreads();
     if constexpr (STAMP) t2 = __builtin_amdgcn_s_memtime();
-    if (dma_wave && NSTG > 1 && kt + 1 < nk) dma(st ^ 1);
+    if (NSTG > 1 && kt + 1 < nk) dma(st ^ 1);
     if constexpr (STAMP) t3 = __builtin_amdgcn_s_memtime();
-    if (!mma_wave) continue;
     const uint8_t* xs = smem + st * STG;
     const uint8_t* ws = xs + XB;
     i32x8 a[NI], b[4];
@@ -501,19 +493,7 @@ __device__ __forceinline__ void conv_lite_fp8_body(const Fp8Params& p, const Fp8
       const u32x4 lo = *reinterpret_cast<const u32x4*>(r + sl0), hi = *reinterpret_cast<const u32x4*>(r + sl1);
       a[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
-    if constexpr (WS) {
-      // 128 VGPRs (four waves per SIMD): one pixel fragment at a time, all NI weight fragments held
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint8_t* r = xs + (wm * 64 + j * 16 + frow) * BK;
-        const u32x4 lo = *reinterpret_cast<const u32x4*>(r + sl0), hi = *reinterpret_cast<const u32x4*>(r + sl1);
-        const i32x8 bj = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], bj, acc[i][j], 0, 0, 0, E8M0_ONE, 0,
-                                                                       E8M0_ONE);
-      }
-    } else {
+    {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint8_t* r = xs + (wm * 64 + j * 16 + frow) * BK;
@@ -541,7 +521,7 @@ __device__ __forceinline__ void conv_lite_fp8_body(const Fp8Params& p, const Fp8
   __syncthreads();  // the epilogue tile reuses the stage images
 
   uint8_t* Os = smem;
-  if (mma_wave) {  // (the DMA waves hold no accumulators)
+  {
   #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int cl = wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
@@ -614,14 +594,7 @@ __device__ __forceinline__ void conv_lite_fp8_body(const Fp8Params& p, const Fp8
 
 template <bool OUT_FP8, int ACT, int BN_ = 128, int NSTG = 2, bool MULTI = false, bool STAMP = false>
 __global__ __launch_bounds__(256, 2) void conv_lite_fp8_kernel(Fp8Params p, Fp8Segs sg) {
-  conv_lite_fp8_body<OUT_FP8, ACT, BN_, NSTG, MULTI, STAMP, false>(p, sg);
-}
-
-// eight waves, two workgroups per CU: four waves per SIMD (HIP's second launch bound is
-// the minimum waves per execution unit), so at most 128 VGPRs
-template <bool OUT_FP8, int ACT, int BN_, bool MULTI = false>
-__global__ __launch_bounds__(512, 4) void conv_lite_fp8_ws_kernel(Fp8Params p, Fp8Segs sg) {
-  conv_lite_fp8_body<OUT_FP8, ACT, BN_, 2, MULTI, false, true>(p, sg);
+  conv_lite_fp8_body<OUT_FP8, ACT, BN_, NSTG, MULTI, STAMP>(p, sg);
 }
 
 template <bool OUT_FP8, int BN_, int NSTG, bool MULTI = false>
@@ -629,16 +602,6 @@ void launch_lite_fp8_t(Fp8Params p, int act, hipStream_t s, const Fp8Segs& sg) {
   p.tiles_m = (p.M + 127) / 128;
   p.tiles_n = (p.Cout + BN_ - 1) / BN_;
   dim3 grid(p.tiles_m * p.tiles_n), block(256);
-  // DMA / MFMA waves: two-stage tiles only (one stage has no DMA to overlap) and channel
-  // tiles <= 96 (the 128-wide tile's accumulators do not fit 128 VGPRs without spilling)
-  if constexpr (NSTG == 2 && BN_ <= 96) if (p.ws) {
-    const dim3 b8(512);
-    if constexpr (MULTI) hipLaunchKernelGGL((conv_lite_fp8_ws_kernel<false, ACT_NONE, BN_, true>), grid, b8, 0, s, p, sg);
-    else if (act == ACT_RELU) hipLaunchKernelGGL((conv_lite_fp8_ws_kernel<OUT_FP8, ACT_RELU, BN_>), grid, b8, 0, s, p, sg);
-    else if (act == ACT_NONE) hipLaunchKernelGGL((conv_lite_fp8_ws_kernel<OUT_FP8, ACT_NONE, BN_>), grid, b8, 0, s, p, sg);
-    else throw std::invalid_argument("fp8 conv_lite: activation must be none/relu");
-    return;
-  }
   if constexpr (MULTI) {  // the per-channel clamp replaces the activation
     hipLaunchKernelGGL((conv_lite_fp8_kernel<false, ACT_NONE, BN_, NSTG, true>), grid, block, 0, s, p, sg);
     return;
@@ -656,38 +619,25 @@ void launch_lite_fp8_t(Fp8Params p, int act, hipStream_t s, const Fp8Segs& sg) {
   }
 }
 
-// channel tile: the one of 128 / 96 / 64 that pads Cout least (ties go to the wider tile:
-// more reuse of each pixel row); one LDS stage when K fits one K-tile.  ``bn`` > 0 forces it.
-int lite_fp8_bn(int Cout, int wide = 0, int M = 0) {
-  int best = 128, pad = (Cout + 127) / 128 * 128;
-  if (wide == 1 && (Cout + 191) / 192 * 192 <= pad) best = 192, pad = (Cout + 191) / 192 * 192;
-  for (int bn : {96, 64}) {
-    const int pd = (Cout + bn - 1) / bn * bn;
-    if (pd < pad) best = bn, pad = pd;
-  }
-  if (wide < 2) return best;
-  // wide: the tile that stages the fewest rows per 128-pixel tile and K-tile — the channel
-  // tiles' count x (128 pixel rows + BN weight rows), as the K loop is bound by the bytes it
-  // fills (profiles/r04_ac); ties go to the wider tile
-  // wide 3: the same over whole waves of workgroups — a grid short of two workgroups per CU
-  // (8x8 layers) takes the narrower tile that still fits one wave of 512
-  const long tm = (M + 127) / 128;
-  auto rows = [&](int bn) -> long {
-    const long nt = (Cout + bn - 1) / bn;
-    if (wide == 3) return (tm * nt + 511) / 512 * (128 + bn);
-    return nt * (128 + bn);
-  };
-  long cost = rows(best);
+// channel tile: the one of 192 / 160 / 128 / 96 / 64 that stages the fewest rows per
+// 128-pixel tile and K-tile — the channel tiles' count x (128 pixel rows + BN weight rows),
+// as the K loop is bound by the bytes it fills (profiles/r04_ac, r04_af); ties go to the
+// wider tile.  (Least padding among 128 / 96 / 64, with or without 192, and the same count
+// over whole waves of 512 workgroups measured slower: r04_ac, r04_ah.)  One LDS stage when
+// K fits one K-tile.
+int lite_fp8_bn(int Cout) {
+  int best = 128;
+  long cost = 1L << 62;
   for (int bn : {192, 160, 128, 96, 64}) {
-    const long c = rows(bn);
-    if (c < cost || (c == cost && bn > best)) best = bn, cost = c;
+    const long c = (long)((Cout + bn - 1) / bn) * (128 + bn);
+    if (c < cost) best = bn, cost = c;
   }
   return best;
 }
 
 template <bool OUT_FP8, bool MULTI = false>
 void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, const Fp8Segs& sg = Fp8Segs{}, int bn = 0) {
-  const int b = bn ? bn : lite_fp8_bn(p.Cout, p.ws ? 0 : p.wide, p.M);
+  const int b = bn ? bn : lite_fp8_bn(p.Cout);
   const bool one = p.K <= BK;
 #define FTM_LITE(BN_)                                                     \
   do {                                                                    \
@@ -705,13 +655,8 @@ void launch_lite_fp8(const Fp8Params& p, int act, hipStream_t s, const Fp8Segs& 
 // conv_lite_fp8 STAMP diagnostics target (0 = off): set by conv_lite_fp8_stamp
 unsigned long long* g_lite_fp8_stamp = nullptr;
 
-// cfg value selecting conv_lite_fp8 (fp8 input only; any conv geometry with Cin % 16 == 0);
-// LITE_WS_CFG: the same tile on eight DMA / MFMA waves
-constexpr int LITE_CFG = 8;
-constexpr int LITE_WS_CFG = 9;
-constexpr int LITE_WIDE_CFG = 10;   // + the 192-wide channel tile (Cout 192 / 384 / 768 in one tile per 192)
-constexpr int LITE_WIDE2_CFG = 11;  // the tile staging the fewest rows, 160 and 192 included
-constexpr int LITE_WIDE3_CFG = 12;  // ... counted over whole waves of 512 workgroups
+// cfg value selecting conv_lite_fp8 (fp8 input only; any conv geometry with Cin % 16 == 0)
+constexpr int LITE_CFG = 11;
 
 template <bool CONV>
 void launch_io(const Fp8Params& p, bool in_bf16, bool out_fp8, int act, int cfg, hipStream_t s) {
@@ -1154,10 +1099,8 @@ void conv2d_nhwc_fp8(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, 
   p.ldx = Cin;
   p.ldy = ldy; p.y_coff = y_coff;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (cfg == LITE_CFG || cfg == LITE_WS_CFG || cfg == LITE_WIDE_CFG || cfg == LITE_WIDE2_CFG || cfg == LITE_WIDE3_CFG) {
+  if (cfg == LITE_CFG) {
     p.stamp = g_lite_fp8_stamp;
-    p.ws = cfg == LITE_WS_CFG;
-    p.wide = cfg == LITE_WIDE_CFG ? 1 : cfg == LITE_WIDE2_CFG ? 2 : cfg == LITE_WIDE3_CFG ? 3 : 0;
     if (in_bf16) throw std::invalid_argument("conv2d_nhwc_fp8: the conv_lite tile takes fp8 input");
     if (ph >= 1024 || pw >= 1024 || H >= 16384 || W >= 16384) throw std::invalid_argument("conv2d_nhwc_fp8: geometry");
     if ((long)Cout * p.K >= (1L << 31)) throw std::invalid_argument("conv2d_nhwc_fp8: weights larger than 2 GiB");
@@ -1225,8 +1168,7 @@ void conv2d_nhwc_fp8_multi(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t 
   p.K = KH * KW * Cin;
   p.ldx = Cin;
   if ((long)Cout * p.K >= (1L << 31)) throw std::invalid_argument("conv2d_nhwc_fp8_multi: weights larger than 2 GiB");
-  p.ws = mode & 1;
-  p.wide = (mode >> 1) & 3;
+  (void)mode;
   launch_lite_fp8<false, true>(p, ACT_NONE, reinterpret_cast<hipStream_t>(stream), sg);
   FTM_CHECK_LAUNCH();
 }
@@ -1385,6 +1327,6 @@ void register_fp8(pybind11::module_& m) {
   m.def("avgpool_bias_act", &avgpool_bias_act);
   m.def("conv2d_nhwc_fp8_multi", &conv2d_nhwc_fp8_multi);
   // the channel tile conv_lite_fp8 picks (host logic only; tests/test_fp8.py)
-  m.def("lite_fp8_tile", [](int Cout, int wide, int M) { return lite_fp8_bn(Cout, wide, M); });
+  m.def("lite_fp8_tile", [](int Cout) { return lite_fp8_bn(Cout); });
   m.attr("fp8_igemm_num_configs") = NCFG;
 }

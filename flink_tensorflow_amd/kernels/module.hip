@@ -19,7 +19,6 @@ void register_igemm_v2(pybind11::module_& m);
 void register_dconv(pybind11::module_& m);
 void register_elementwise(pybind11::module_& m);
 void register_conv3x3c64(pybind11::module_& m);
-void register_conv3x3h(pybind11::module_& m);
 void register_bottleneck(pybind11::module_& m);
 void register_gemm_pp(pybind11::module_& m);
 void register_conv_pp(pybind11::module_& m);
@@ -42,7 +41,6 @@ PYBIND11_MODULE(_hip, m) {
   register_dconv(m);
   register_elementwise(m);
   register_conv3x3c64(m);
-  register_conv3x3h(m);
   register_bottleneck(m);
   register_gemm_pp(m);
   register_conv_pp(m);

@@ -33,7 +33,8 @@ template <int CPR>
 FTM_DEVICE int swz(int row, int c) { return row * CPR + (c ^ (row & (CPR >= 16 ? 15 : CPR - 1))); }
 
 // K = K1 + K2 input channels (K2 > 0: DUAL, a second [M, K2] source x2 — a 1x1 conv with its
-// stride-1 projection shortcut, no residual), TP pixels per tile, BN output channels per
+// stride-1 projection shortcut, no residual; its host entry was removed: 0.2-0.4 % slower end
+// to end, profiles/r02_pw_res2 — only K2 = 0 is instantiated), TP pixels per tile, BN output channels per
 // workgroup (resident slice)
 template <int K1, int K2, int TP, int BN>
 __global__ __launch_bounds__(NT, 2) void pw_res_kernel(const bf16* __restrict__ x, const bf16* __restrict__ x2,
@@ -224,21 +225,6 @@ void pw_res_bf16(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintpt
 // ResNet's stage-2 entry expand conv with its projection shortcut, whose input the stage-1
 // tail stored already decimated (compiler._decimate_tails), so both sources are plain
 // pixel matrices.  N % 128 == 0.
-void pw_dual_bf16(uintptr_t x, uintptr_t x2, uintptr_t w, uintptr_t bias, uintptr_t y, int M, int N, int K1, int K2,
-                  int ldy, int y_coff, int num_cu, uintptr_t stream) {
-  if (K1 != 128 || K2 != 256) throw std::invalid_argument("pw_dual: sources must have 128 and 256 channels");
-  if (M <= 0 || N <= 0) throw std::invalid_argument("pw_dual: empty problem");
-  if (ldy % 8 || y_coff % 8 || ldy < y_coff + N) throw std::invalid_argument("pw_dual: output stride");
-  if ((long)M * (ldy > K2 ? ldy : K2) >= (1L << 31)) throw std::invalid_argument("pw_dual: tensor too large");
-  for (uintptr_t p : {x, x2, w, bias, y})
-    if (!p || p % 16) throw std::invalid_argument("pw_dual: null or non-16-byte-aligned pointer");
-  auto bp = [](uintptr_t p) { return reinterpret_cast<bf16*>(p); };
-  launch<128, 256, 64, 128>(bp(x), bp(x2), bp(w), reinterpret_cast<const float*>(bias), nullptr, bp(y), M, N, ldy,
-                            y_coff, N, num_cu, reinterpret_cast<hipStream_t>(stream));
-  FTM_CHECK_LAUNCH();
-}
-
 void register_pw_res(pybind11::module_& m) {
   m.def("pw_res_bf16", &pw_res_bf16);
-  m.def("pw_dual_bf16", &pw_dual_bf16);
 }

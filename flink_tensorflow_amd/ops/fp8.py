@@ -144,7 +144,7 @@ def conv2d_nhwc_fp8(x: torch.Tensor, x_scale: float, wq: torch.Tensor, kshape, w
 
 def conv2d_nhwc_fp8_multi(x: torch.Tensor, x_scale: float, wq: torch.Tensor, kshape, w_scale: torch.Tensor,
                           bias: torch.Tensor, lo: torch.Tensor, segs, stride=(1, 1), pad=(0, 0, 0, 0), dilation=(1, 1),
-                          chan_scale: torch.Tensor | None = None, ws: bool = False, wide: int = 0) -> None:
+                          chan_scale: torch.Tensor | None = None) -> None:
     """Horizontally fused sibling convs (``kernels/fp8.hip`` conv_lite_fp8, multi-output
     epilogue): one implicit GEMM over the concatenated filters ``wq`` [Cout_total, K]; output
     channels are clamped below by ``lo`` (0 = ReLU, -inf = none) and split into ``segs``:
@@ -176,7 +176,7 @@ def conv2d_nhwc_fp8_multi(x: torch.Tensor, x_scale: float, wq: torch.Tensor, ksh
             x.data_ptr(), wq.data_ptr(), chan_scale.data_ptr(), bias.data_ptr(), lo.data_ptr(), N, H, W, Cin, Cout, KH,
             KW, sh, sw, pt, pl, dh, dw, Ho, Wo,
             [(o.data_ptr(), c0, c1, o.shape[-1], off, int(osc is None), 1.0 / osc if osc is not None else 1.0)
-             for o, c0, c1, off, osc in segs], _stream(), int(ws) | (int(wide) << 1))
+             for o, c0, c1, off, osc in segs], _stream(), 0)
         return
     y = conv2d_nhwc_fp8(x, x_scale, wq, kshape, w_scale, bias, stride, pad, dilation, None)  # fp32, no act
     y = torch.maximum(y, lo.float()).to(torch.bfloat16).float()  # the kernel stages the tile in bf16

@@ -290,82 +290,15 @@ def wino_f23(x: torch.Tensor, u_frag: torch.Tensor, Cout: int, bias: torch.Tenso
     return out
 
 
-def conv3x3_halo_len(N: int, H: int, W: int) -> int:
-    """Halo pixels the widest 128-pixel tile of kernels/conv3x3h.hip needs (padded
-    flattened coordinates; mirrors ``halo_len`` there)."""
-    key = (N, H, W)
-    if key not in _HALO_LEN:
-        Wp, Hp, hw = W + 2, H + 2, H * W
-
-        def pb(m):
-            n, r = divmod(m, hw)
-            oh, ow = divmod(r, W)
-            return (n * Hp + oh) * Wp + ow
-
-        M = N * hw
-        worst = max(pb(min(m0 + 127, M - 1)) - pb(m0) for m0 in range(0, M, 128))
-        _HALO_LEN[key] = worst + 2 * Wp + 3
-    return _HALO_LEN[key]
-
-
-_HALO_LEN: dict = {}
-
-
-def conv3x3_halo_eligible(x_shape, w_shape, stride, pad, dilation, residual, act) -> bool:
-    """kernels/conv3x3h.hip: 3x3, stride 1, SAME padding, Cin % 64 == 0, Cout % 8 == 0, no
-    residual, bias (+ReLU) epilogue, and a 128-pixel tile's halo within 288 pixels (ResNet-50
-    stages 2-4 at any batch: 28x28 -> 260, 14x14 -> 214, 7x7 -> 240)."""
-    if len(x_shape) != 4:
-        return False
-    N, H, W, Cin = x_shape
-    Cout, KH, KW, _ = w_shape
-    return (Cin % 64 == 0 and Cout % 8 == 0 and (KH, KW) == (3, 3) and tuple(stride) == (1, 1)
-            and tuple(pad) == (1, 1, 1, 1) and tuple(dilation) == (1, 1) and residual is None
-            and act_code(act) in (ACT_NONE, ACT_RELU) and N * H * W * Cin * 2 < 2 ** 31
-            and N * (H + 2) * (W + 2) < 2 ** 31 and conv3x3_halo_len(N, H, W) <= 288)
-
-
-def conv3x3_halo(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor, act=None,
-                 out: torch.Tensor | None = None, out_channel_offset: int = 0) -> torch.Tensor:
-    """3x3 / s1 / SAME conv, ``act(conv + bias)``; GPU: the halo-staged implicit GEMM
-    (kernels/conv3x3h.hip: the input is filled into LDS once per 64 channels, not once per
-    tap); host: the fp32 reference conv."""
-    N, H, W, Cin = x.shape
-    Cout = w_ohwi.shape[0]
-    a = act_code(act)
-    if out is None:
-        out = torch.empty((N, H, W, Cout), dtype=x.dtype if x.is_cuda else torch.float32, device=x.device)
-        out_channel_offset = 0
-    if not conv3x3_halo_eligible(tuple(x.shape), tuple(w_ohwi.shape), (1, 1), (1, 1, 1, 1), (1, 1), None, a):
-        raise ValueError(f"conv3x3_halo: unsupported shapes x {tuple(x.shape)} w {tuple(w_ohwi.shape)}")
-    if tuple(out.shape[:3]) != (N, H, W) or out_channel_offset + Cout > out.shape[3]:
-        raise ValueError("conv3x3_halo: output buffer does not fit")
-    if x.is_cuda:
-        _check(x, "x", device=x.device)
-        _check(w_ohwi, "w", device=x.device)
-        _check(out, "out", device=x.device)
-        _check(bias, "bias", torch.float32, x.device)
-        _hip().conv3x3h_bf16(x.data_ptr(), w_ohwi.data_ptr(), bias.data_ptr(), out.data_ptr(), N, H, W, Cin, Cout,
-                             out.shape[3], out_channel_offset, a, _stream())
-        return out
-    return conv2d_nhwc(x, w_ohwi, bias, None, (1, 1), (1, 1, 1, 1), (1, 1), a, out=out,
-                       out_channel_offset=out_channel_offset)
-
-
 _NUM_CU: dict = {}
 
 
 class _PersistentCUs(dict):
-    """CU count the persistent kernels size their grid to: the device's, or fewer when
-    ``EngineConfig.persistent_cus`` caps it (room on the chip for the other compute lane's
-    kernels while a persistent kernel runs)."""
+    """CU count the persistent kernels size their grid to: the device's (caps of 224 / 192 /
+    160 CUs, room for the sibling lane, measured -0.6 to -5 %: profiles/r04_ab)."""
 
     def __missing__(self, dev):
-        n = torch.cuda.get_device_properties(dev).multi_processor_count
-        from ..config import current
-
-        cap = int(getattr(current(), "persistent_cus", 0) or 0)
-        self[dev] = min(n, cap) if cap > 0 else n
+        self[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
         return self[dev]
 
 
@@ -404,8 +337,9 @@ def bottleneck_tail(x2: torch.Tensor, res: torch.Tensor | None, w3: torch.Tensor
     """Fused ResNet bottleneck block boundary (kernels/bottleneck.hip):
     ``y3 = relu(x2 @ w3^T + b3 + res)`` (1x1 expand CX -> 4 CX with residual) and
     ``y1 = relu(y3 @ w1^T + b1)`` (the next block's 1x1 reduce 4 CX -> CN); returns
-    ``(y3, y1)``.  Variants: CX = 64 (stage 1) with CN = 64 or 128; CX = 128 (stage 2) with
-    CN = 128 (weights streamed through LDS).  Dual form (stage 1's first block, stride-1
+    ``(y3, y1)``.  Variants: CX = 64 (stage 1) with CN = 64 or 128 (a stage-2 form with the
+    weights streamed through LDS measured no faster than the two convs and was removed:
+    profiles/r01_tail).  Dual form (stage 1's first block, stride-1
     projection shortcut): ``xs [..., 64]`` instead of ``res`` and ``w3 [256, 128]`` =
     [expand | projection] — ``y3 = relu([x2 | xs] @ w3^T + b3)`` (CN = 64).  Weights are 1x1
     OHWI squeezed ([out, in]), biases fp32.  GPU: one persistent kernel, y3 reused from LDS;
@@ -426,7 +360,7 @@ def bottleneck_tail(x2: torch.Tensor, res: torch.Tensor | None, w3: torch.Tensor
     cn = w1.shape[0]
     if (res is None) != dual:
         raise ValueError("bottleneck_tail: pass exactly one of res and xs")
-    if (cx, dual, cn) not in ((64, True, 64), (64, False, 64), (64, False, 128), (128, False, 128)):
+    if (cx, dual, cn) not in ((64, True, 64), (64, False, 64), (64, False, 128)):
         raise ValueError(f"bottleneck_tail: unsupported variant x2 [..., {cx}], dual {dual}, reduce width {cn}")
     k3 = 2 * cx if dual else cx
     if (dual and tuple(xs.shape) != (*lead, cx)) or (not dual and tuple(res.shape) != (*lead, co)):
@@ -450,16 +384,9 @@ def bottleneck_tail(x2: torch.Tensor, res: torch.Tensor | None, w3: torch.Tensor
         _check(b3, "b3", torch.float32, x2.device)
         _check(b1, "b1", torch.float32, x2.device)
         dev = x2.device.index if x2.device.index is not None else torch.cuda.current_device()
-        if cx == 128:
-            if y3_decimated:
-                raise ValueError("bottleneck_tail: decimated y3 is a CX = 64 variant")
-            _hip().bottleneck_tail_wide_bf16(x2.data_ptr(), res.data_ptr(), w3.data_ptr(), b3.data_ptr(),
-                                             w1.data_ptr(), b1.data_ptr(), y3.data_ptr(), y1.data_ptr(), M,
-                                             _NUM_CU[dev], _stream())
-        else:
-            _hip().bottleneck_tail_bf16(x2.data_ptr(), _ptr(xs), _ptr(res), w3.data_ptr(), b3.data_ptr(),
-                                        w1.data_ptr(), b1.data_ptr(), y3.data_ptr(), y1.data_ptr(), M, cn,
-                                        _NUM_CU[dev], _stream(), dec_hw[0], dec_hw[1])
+        _hip().bottleneck_tail_bf16(x2.data_ptr(), _ptr(xs), _ptr(res), w3.data_ptr(), b3.data_ptr(),
+                                    w1.data_ptr(), b1.data_ptr(), y3.data_ptr(), y1.data_ptr(), M, cn,
+                                    _NUM_CU[dev], _stream(), dec_hw[0], dec_hw[1])
         return y3, y1
     xin = torch.cat([x2.reshape(M, cx), xs.reshape(M, cx)], 1) if dual else x2.reshape(M, cx)
     a = xin.float() @ w3.reshape(co, k3).float().t() + b3.float()
@@ -726,36 +653,16 @@ def conv_pp_ktab(srcs) -> torch.Tensor:
     return torch.tensor(rows, dtype=torch.int32)
 
 
-def conv_pp_tile(Cout: int) -> int:
-    """0 = 256x256 tiles, 1 = 512x128 tiles (channel counts that would waste half of a
-    256-wide tile); 2 / 3 (never chosen here) = the 4-wave 128x128 ``conv_lite`` tile with a
-    64- / 32-deep K-tile (64 / 32 KiB of LDS).  (A 256x128 tile of 128 x 64 waves and
-    3-stage LDS pipelines measured 25-45 % slower per layer: profiles/r04_a.)"""
-    return 1 if Cout <= 128 or (Cout % 256 and Cout % 128 == 0) else 0
-
-
-def conv_pp_splits(M: int, N: int, K: int, tile: int, num_cu: int = 256) -> int:
-    """Split-K factor for ``conv_pp`` (same cost model as ``gemm_pp_splits``)."""
-    bm, bn = (512, 128) if tile == 1 else (256, 256)
-    tiles = -(-M // bm) * -(-N // bn)
-    nk = K // 64
-    best_s, best_t = 1, -(-tiles // num_cu) * nk * _PP_KTILE_US
-    for s in range(2, min(16, nk) + 1):
-        per = -(-nk // s)
-        se = -(-nk // per)
-        t = -(-tiles * se // num_cu) * per * _PP_KTILE_US + 2.0 * se * M * N * 4 / _PP_SPLIT_BW + 2.0
-        if t < 0.9 * best_t:
-            best_s, best_t = se, t
-    return best_s
-
-
 class ConvPP:
-    """A planned ``conv_pp`` launch (kernels/conv_pp.hip): implicit-GEMM NHWC convolution
-    of one or two sources into one accumulator on the ping-pong MFMA pipeline.
+    """A planned ``conv_lite`` launch (kernels/conv_pp.hip): implicit-GEMM NHWC convolution
+    of one or two sources into one accumulator on the 4-wave 128x128 LDS-DMA tile
+    (``tile`` 2, the only one left: the ping-pong / wide / 32-deep / wave-split tiles
+    measured slower and were removed).
 
     ``srcs``: [(x_shape NHWC, (KH, KW), (sh, sw), (pt, pl), (dh, dw))]; the weight is the
-    concatenation of the sources' OHWI filters, [Cout, sum KH*KW*C] bf16.  The K-tile
-    table and the split-K workspace are built once (device tensors kept on the object)."""
+    concatenation of the sources' OHWI filters, [Cout, sum KH*KW*C] bf16; a second source
+    must be 1x1, unpadded and in range (a projection shortcut).  The K-tile table is built
+    once (a device tensor kept on the object)."""
 
     def __init__(self, srcs, Cout: int, out_hw, device, tile: int | None = None, splits: int | None = None):
         self.srcs = [(tuple(xs), tuple(k), tuple(st), tuple(pd), tuple(dl)) for xs, k, st, pd, dl in srcs]
@@ -769,16 +676,15 @@ class ConvPP:
         if Cout % 8:
             raise ValueError("conv_pp: Cout % 8")
         self.M = self.N * self.OH * self.OW
-        self.tile = conv_pp_tile(Cout) if tile is None else tile
-        if self.tile in (3, 4) and len(self.srcs) != 1:
-            raise ValueError("conv_pp: the 32-deep 4-wave tile and the wave-specialised tile take one source")
-        if self.tile in (2, 5) and len(self.srcs) == 2:
+        self.tile = 2 if tile is None else tile
+        if self.tile != 2 or (splits or 1) != 1:
+            raise ValueError("conv_pp: only the conv_lite tile (2) without split-K remains")
+        if len(self.srcs) == 2:
             (xs1, k1, st1, pd1, dl1) = self.srcs[1]
             if tuple(k1) != (1, 1) or tuple(pd1) != (0, 0) or (self.OH - 1) * st1[0] >= xs1[1] \
                     or (self.OW - 1) * st1[1] >= xs1[2]:
                 raise ValueError("conv_pp: the 4-wave tile's second source must be 1x1, unpadded, in range")
-        self.splits = (1 if self.tile in (2, 3, 4, 5) else conv_pp_splits(self.M, Cout, self.K, self.tile)) if splits is None \
-            else splits
+        self.splits = 1
         self.ktab = conv_pp_ktab([(xs[1], xs[2], xs[3], k[0], k[1], dl[0], dl[1])
                                   for xs, k, _, _, dl in self.srcs]).to(device)
         self.ws = (torch.empty(self.splits * self.M * Cout, dtype=torch.float32, device=device)
@@ -1316,39 +1222,6 @@ def pw_res(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor, residual: to
     y = x.reshape(M, K_).float() @ w_nk.reshape(N, K_).float().t() + bias.float()
     y = torch.relu(y.to(out.dtype).float() + residual.reshape(M, N).float())
     out[..., out_channel_offset:out_channel_offset + N] = y.reshape(*lead, N).to(out.dtype)
-    return out
-
-
-def pw_dual_ok(K1: int, C2: int, N: int, num_cu: int = 256) -> bool:
-    """Shapes ``pw_dual`` takes (ResNet's stage-2 entry expand + projection)."""
-    return K1 == 128 and C2 == 256 and N % 128 == 0 and 8 * (N // 128) <= num_cu
-
-
-def pw_dual(x: torch.Tensor, x2: torch.Tensor, w_cat: torch.Tensor, bias: torch.Tensor,
-            out: torch.Tensor | None = None, out_channel_offset: int = 0) -> torch.Tensor:
-    """``relu([x | x2] @ w_cat^T + bias)`` with ``x`` ``[..., 128]`` and ``x2`` ``[..., 256]`` on
-    the same pixels (a 1x1 expand conv with its stride-1 — or already decimated — projection
-    shortcut, no residual).  GPU: the persistent ``pw_res`` kernel in its dual-source form
-    (kernels/pw_res.hip); host: ``conv1x1_dual``."""
-    K1, C2 = x.shape[-1], x2.shape[-1]
-    N = w_cat.shape[0]
-    lead = tuple(x.shape[:-1])
-    if not pw_dual_ok(K1, C2, N) or tuple(x2.shape[:-1]) != lead or tuple(w_cat.shape) != (N, K1 + C2):
-        raise ValueError(f"pw_dual: unsupported shapes x {tuple(x.shape)}, x2 {tuple(x2.shape)}, "
-                         f"w {tuple(w_cat.shape)}")
-    if not x.is_cuda:
-        return conv1x1_dual(x, x2, w_cat, bias, 1, "relu", out=out, out_channel_offset=out_channel_offset)
-    if out is None:
-        out = torch.empty((*lead, N), dtype=x.dtype, device=x.device)
-        out_channel_offset = 0
-    if tuple(out.shape[:-1]) != lead or out_channel_offset + N > out.shape[-1]:
-        raise ValueError(f"pw_dual: out {tuple(out.shape)} cannot hold [..., {N}] at offset {out_channel_offset}")
-    for t, n in ((x, "x"), (x2, "x2"), (w_cat, "w"), (out, "out")):
-        _check(t, n, device=x.device)
-    _check(bias, "bias", torch.float32, x.device)
-    dev = x.device.index if x.device.index is not None else torch.cuda.current_device()
-    _hip().pw_dual_bf16(x.data_ptr(), x2.data_ptr(), w_cat.data_ptr(), bias.data_ptr(), out.data_ptr(),
-                        x.numel() // K1, N, K1, C2, out.shape[-1], out_channel_offset, _NUM_CU[dev], _stream())
     return out
 
 

@@ -1,8 +1,8 @@
 """Fused ResNet stage-1 block boundary (``ops.kernels.bottleneck_tail``): the host
 reference, and the compiler's fusion of a 1x1 expand conv with the next block's 1x1
-reduce conv (five boundaries in ResNet-50: the two inside stage 1 — the first one with the
-projection shortcut folded in —, stage 1 -> stage 2, and, opt-in, two inside stage 2), and
-the library-GEMM lowering of the deep-K 1x1 convs (GPU)."""
+reduce conv (three boundaries in ResNet-50: the two inside stage 1 — the first one with the
+projection shortcut folded in — and stage 1 -> stage 2), and the GEMM lowering of the
+deep-K 1x1 convs (GPU)."""
 import os
 
 import pytest
@@ -34,23 +34,16 @@ def test_host_reference_matches_two_convs():
     e1 = K.conv2d_nhwc(e3, w1.reshape(64, 1, 1, 256), b1[:64], act="relu")
     torch.testing.assert_close(y3, e3, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(y1, e1, rtol=1e-4, atol=1e-3)
-    # stage-2 form: 128 -> 512 (+ residual) -> 128
-    x2, res = torch.randn(3, 4, 128, generator=g), torch.randn(3, 4, 512, generator=g)
-    w3, w1 = torch.randn(512, 128, generator=g), torch.randn(128, 512, generator=g)
-    b3, b1 = torch.randn(512, generator=g), torch.randn(128, generator=g)
-    y3, y1 = K.bottleneck_tail(x2, res, w3, b3, w1, b1)
-    e3 = K.conv2d_nhwc(x2[None], w3.reshape(512, 1, 1, 128), b3, res[None], act="relu")[0]
-    e1 = K.conv2d_nhwc(e3[None], w1.reshape(128, 1, 1, 512), b1, act="relu")[0]
-    torch.testing.assert_close(y3, e3, rtol=1e-4, atol=1e-3)
-    torch.testing.assert_close(y1, e1, rtol=1e-4, atol=1e-3)
+    # the stage-2 form (128 -> 512 -> 128, weights streamed through LDS) was removed
     with pytest.raises(ValueError):
-        K.bottleneck_tail(x2, res, w3, b3, w1[:64], b1[:64])  # stage 2 reduces to 128 only
+        K.bottleneck_tail(torch.randn(3, 4, 128), torch.randn(3, 4, 512), torch.randn(512, 128), torch.randn(512),
+                          torch.randn(128, 512), torch.randn(128))
 
 
-def _compile(g, dev, fuse, wide="0"):
+def _compile(g, dev, fuse):
     from flink_tensorflow_amd.config import override
 
-    with override(fuse_block_tails=fuse, fuse_wide_tails=wide == "1"):
+    with override(fuse_block_tails=fuse):
         return CompiledFunction(g, {"images:0": ((2, 64, 64, 3), "UINT8")}, ["logits:0"], dev, strict=True)
 
 
@@ -59,11 +52,10 @@ def r50():
     return Graph.from_graph_def(resnet50_graph_def(depth=50, image_hw=(64, 64), num_classes=16))
 
 
-def _check(r50, dev, wide="0"):
-    fused, plain = _compile(r50, dev, True, wide=wide), _compile(r50, dev, False)
-    # stage 1: block 1 (dual: projection shortcut) -> 2 -> 3 -> stage 2 block 1; opt-in
-    # (fuse_wide_tails), stage 2: block 2 -> 3 -> 4 (weights streamed through LDS)
-    n = 5 if wide == "1" else 3
+def _check(r50, dev):
+    fused, plain = _compile(r50, dev, True), _compile(r50, dev, False)
+    # stage 1: block 1 (dual: projection shortcut) -> 2 -> 3 -> stage 2 block 1
+    n = 3
     assert fused.summary()["fused_tails"] == n and plain.summary()["fused_tails"] == 0
     assert fused.summary()["fused_shortcuts"] == plain.summary()["fused_shortcuts"] == 4
     # stage 1 -> stage 2: the tail's 256-channel output is stored decimated (only the
@@ -83,15 +75,13 @@ def _check(r50, dev, wide="0"):
     torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2 * b.abs().max().item())
 
 
-@pytest.mark.parametrize("wide", ["0", "1"])
-def test_compiled_resnet50_fuses_block_boundaries_cpu(r50, wide):
-    _check(r50, torch.device("cpu"), wide)
+def test_compiled_resnet50_fuses_block_boundaries_cpu(r50):
+    _check(r50, torch.device("cpu"))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wide", ["0", "1"])
-def test_compiled_resnet50_fuses_block_boundaries_gpu(r50, wide):
-    _check(r50, torch.device("cuda", 0), wide)
+def test_compiled_resnet50_fuses_block_boundaries_gpu(r50):
+    _check(r50, torch.device("cuda", 0))
 
 
 def _decimated_case(dev):

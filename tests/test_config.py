@@ -53,12 +53,12 @@ def test_kernel_selection_lives_in_engine_config(monkeypatch):
     YAML, CLI, or ``override``), not ad-hoc environment variables."""
     from flink_tensorflow_amd import config
 
-    monkeypatch.setenv("FT_CONV_IMPL", "auto")
+    monkeypatch.setenv("FT_CHAIN_BATCH", "16")
     monkeypatch.setenv("FT_FUSE_BLOCK_TAILS", "0")
     config.set_current(None)
     try:
         cfg = config.current()
-        assert cfg.conv_impl == "auto" and cfg.fuse_block_tails is False
+        assert cfg.chain_batch == 16 and cfg.fuse_block_tails is False
         with config.override(fuse_block_tails=True, pw_res_kernel=False):
             assert config.current().fuse_block_tails and not config.current().pw_res_kernel
         assert config.current() is cfg

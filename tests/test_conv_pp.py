@@ -29,54 +29,27 @@ def _ref(srcs, xs, w, bias, res, act, OH, OW):
 
 
 CASES = [
-    # name, [(N,H,W,C), (KH,KW), stride, (pt,pl), dil], Cout, (OH, OW), residual, act, tile, splits
-    ("3x3_c128", [((4, 28, 28, 128), (3, 3), (1, 1), (1, 1), (1, 1))], 128, (28, 28), False, "relu", None, None),
-    ("3x3s2_c256", [((4, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", None, None),
-    ("1x1_res", [((2, 14, 14, 256), (1, 1), (1, 1), (0, 0), (1, 1))], 1024, (14, 14), True, "relu", None, None),
-    ("tail_m", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 512, (7, 7), False, None, None, None),
-    ("split3", [((2, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 512, (7, 7), True, "relu", 0, 3),
-    ("dil2_5x5", [((2, 17, 17, 64), (5, 5), (1, 1), (4, 4), (2, 2))], 192, (17, 17), False, "relu", None, None),
-    ("1x7", [((2, 17, 17, 128), (1, 7), (1, 1), (0, 3), (1, 1))], 192, (17, 17), False, "relu", 1, None),
-    ("7x1", [((2, 17, 17, 192), (7, 1), (1, 1), (3, 0), (1, 1))], 136, (17, 17), False, None, 0, None),
-    ("dual", [((2, 14, 14, 128), (1, 1), (1, 1), (0, 0), (1, 1)),
-              ((2, 28, 28, 256), (1, 1), (2, 2), (0, 0), (1, 1))], 512, (14, 14), False, "relu", None, None),
-    ("dual_t1", [((2, 14, 14, 64), (1, 1), (1, 1), (0, 0), (1, 1)),
-                 ((2, 28, 28, 64), (1, 1), (2, 2), (0, 0), (1, 1))], 128, (14, 14), False, "relu", 1, None),
-    # the 4-wave 128x128 LDS-DMA tile (conv_lite): 3x3 s1 / s2, N tail, M tail, residual, dilation
-    ("lite_3x3", [((4, 28, 28, 128), (3, 3), (1, 1), (1, 1), (1, 1))], 128, (28, 28), False, "relu", 2, None),
-    ("lite_3x3s2", [((3, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 2, None),
-    ("lite_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (7, 7), True, "relu", 2, None),
-    ("lite_1x1", [((2, 14, 14, 256), (1, 1), (1, 1), (0, 0), (1, 1))], 1024, (14, 14), True, None, 2, None),
-    ("lite_dil", [((2, 17, 17, 64), (5, 5), (1, 1), (4, 4), (2, 2))], 192, (17, 17), False, "relu", 2, None),
+    # name, [(N,H,W,C), (KH,KW), stride, (pt,pl), dil], Cout, (OH, OW), residual, act
+    # the 4-wave 128x128 LDS-DMA tile (conv_lite): 3x3 s1 / s2, N tail, M tail, residual,
+    # dilation, 1xK / Kx1
+    ("lite_3x3", [((4, 28, 28, 128), (3, 3), (1, 1), (1, 1), (1, 1))], 128, (28, 28), False, "relu"),
+    ("lite_3x3s2", [((3, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu"),
+    ("lite_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (7, 7), True, "relu"),
+    ("lite_tail_m", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 512, (7, 7), False, None),
+    ("lite_1x1", [((2, 14, 14, 256), (1, 1), (1, 1), (0, 0), (1, 1))], 1024, (14, 14), True, None),
+    ("lite_dil", [((2, 17, 17, 64), (5, 5), (1, 1), (4, 4), (2, 2))], 192, (17, 17), False, "relu"),
+    ("lite_1x7", [((2, 17, 17, 128), (1, 7), (1, 1), (0, 3), (1, 1))], 192, (17, 17), False, "relu"),
+    ("lite_7x1", [((2, 17, 17, 192), (7, 1), (1, 1), (3, 0), (1, 1))], 136, (17, 17), False, None),
     # two sources on the 4-wave tile (expand + strided projection shortcut), M tail, N tail
     ("lite_dual", [((2, 14, 14, 128), (1, 1), (1, 1), (0, 0), (1, 1)),
-                   ((2, 28, 28, 256), (1, 1), (2, 2), (0, 0), (1, 1))], 512, (14, 14), False, "relu", 2, None),
+                   ((2, 28, 28, 256), (1, 1), (2, 2), (0, 0), (1, 1))], 512, (14, 14), False, "relu"),
     ("lite_dual_s1", [((3, 7, 7, 64), (1, 1), (1, 1), (0, 0), (1, 1)),
-                      ((3, 7, 7, 128), (1, 1), (1, 1), (0, 0), (1, 1))], 200, (7, 7), False, None, 2, None),
-    # the same tile with a 32-deep K-tile (32 KiB of LDS)
-    ("lite32_3x3", [((4, 28, 28, 128), (3, 3), (1, 1), (1, 1), (1, 1))], 128, (28, 28), False, "relu", 3, None),
-    ("lite32_3x3s2", [((3, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 3, None),
-    ("lite32_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (7, 7), True, "relu", 3, None),
-    ("lite32_1x1", [((2, 14, 14, 256), (1, 1), (1, 1), (0, 0), (1, 1))], 1024, (14, 14), True, None, 3, None),
-    # the same 128x128 tile on eight waves: four issue the LDS-DMA, four run the MFMAs
-    ("ws_3x3", [((4, 28, 28, 128), (3, 3), (1, 1), (1, 1), (1, 1))], 128, (28, 28), False, "relu", 4, None),
-    ("ws_3x3s2", [((3, 28, 28, 256), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 4, None),
-    ("ws_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (7, 7), True, "relu", 4, None),
-    ("ws_1x1", [((2, 14, 14, 256), (1, 1), (1, 1), (0, 0), (1, 1))], 1024, (14, 14), True, None, 4, None),
-    # the 128x256 tile with a 32-deep K-tile: 3x3 s1 / s2, N tail (Cout 200 / 456), M tail,
-    # residual, 1x1, and two sources (expand + strided projection)
-    ("wide_3x3", [((3, 14, 14, 256), (3, 3), (1, 1), (1, 1), (1, 1))], 256, (14, 14), False, "relu", 5, None),
-    ("wide_3x3s2", [((3, 28, 28, 128), (3, 3), (2, 2), (0, 0), (1, 1))], 256, (14, 14), False, "relu", 5, None),
-    ("wide_tail", [((3, 7, 7, 512), (3, 3), (1, 1), (1, 1), (1, 1))], 456, (7, 7), True, "relu", 5, None),
-    ("wide_n200", [((2, 9, 9, 64), (3, 3), (1, 1), (1, 1), (1, 1))], 200, (9, 9), False, None, 5, None),
-    ("wide_1x1", [((2, 14, 14, 1024), (1, 1), (1, 1), (0, 0), (1, 1))], 512, (14, 14), False, "relu", 5, None),
-    ("wide_dual", [((2, 14, 14, 128), (1, 1), (1, 1), (0, 0), (1, 1)),
-                   ((2, 28, 28, 256), (1, 1), (2, 2), (0, 0), (1, 1))], 512, (14, 14), False, "relu", 5, None),
+                      ((3, 7, 7, 128), (1, 1), (1, 1), (0, 0), (1, 1))], 200, (7, 7), False, None),
 ]
 
 
 def _run(case, dev, coff=0):
-    name, srcs, Cout, (OH, OW), with_res, act, tile, splits = case
+    name, srcs, Cout, (OH, OW), with_res, act = case
     torch.manual_seed(0)
     xs = [torch.randn(s[0], device=dev).to(torch.bfloat16) for s in srcs]
     Ktot = sum(s[1][0] * s[1][1] * s[0][3] for s in srcs)
@@ -84,7 +57,7 @@ def _run(case, dev, coff=0):
     bias = torch.randn(Cout, device=dev)
     N = srcs[0][0][0]
     res = torch.randn(N, OH, OW, Cout, device=dev).to(torch.bfloat16) if with_res else None
-    cp = K.ConvPP(srcs, Cout, (OH, OW), dev, tile=tile, splits=splits)
+    cp = K.ConvPP(srcs, Cout, (OH, OW), dev)
     out = torch.zeros(N, OH, OW, Cout + coff, dtype=torch.bfloat16, device=dev)
     cp(xs, w, bias, res, act, out=out, out_channel_offset=coff)
     ref = _ref(srcs, xs, w, bias, res, act, OH, OW)
@@ -113,25 +86,6 @@ def test_conv_pp_concat_offset_gpu():
     assert (left == 0).all()  # channels before the slice untouched
 
 
-@pytest.mark.gpu
-def test_conv_lite_ws_in_resnet_plan_gpu():
-    """The opt-in DMA / MFMA-wave tile (``EngineConfig.conv_lite_ws``) in the compiled
-    ResNet-50 matches the fp32 interpreter as the default plan does."""
-    from flink_tensorflow_amd.config import override
-    from flink_tensorflow_amd.graph.compiler import CompiledFunction
-    from flink_tensorflow_amd.graph.graph import Graph
-    from flink_tensorflow_amd.graph.session import Session
-    from flink_tensorflow_amd.models.zoo.resnet import resnet50_graph_def
-
-    dev = torch.device("cuda", 0)
-    g = Graph.from_graph_def(resnet50_graph_def(image_hw=(112, 112)))
-    with override(conv_lite_ws=True):
-        plan = CompiledFunction(g, {"images:0": ((2, 112, 112, 3), "UINT8")}, ["logits:0"], dev, strict=True)
-    assert plan.summary()["conv_lite"] > 0
-    imgs = torch.randint(0, 255, (2, 112, 112, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(9))
-    (got,) = plan({"images:0": imgs.to(dev)})
-    torch.cuda.synchronize()
-    (ref,) = Session(g, device=torch.device("cpu")).run(["logits:0"], {"images:0": imgs})
-    got, ref = got.float().cpu(), ref.float()
-    err = (got - ref).abs().max().item() / max((ref.max(-1).values - ref.min(-1).values).max().item(), 1e-6)
-    assert err < 0.03, err
+def test_removed_tiles_are_refused():
+    with pytest.raises(ValueError):
+        K.ConvPP([((2, 14, 14, 64), (3, 3), (1, 1), (1, 1), (1, 1))], 64, (14, 14), "cpu", tile=0)

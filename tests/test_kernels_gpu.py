@@ -308,24 +308,6 @@ def test_bottleneck_tail_dual_kernel(M):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M", [2 * 28 * 28, 1000 + 37, 40])
-def test_bottleneck_tail_wide_kernel(M):
-    """Stage-2 form, weights streamed through LDS: 128 -> 512 (+residual, ReLU) -> 128."""
-    g = torch.Generator().manual_seed(M + 1)
-    x2 = torch.randn(M, 128, generator=g).to(torch.bfloat16)
-    res = torch.randn(M, 512, generator=g).to(torch.bfloat16)
-    w3 = (torch.randn(512, 128, generator=g) * 0.08).to(torch.bfloat16)
-    w1 = (torch.randn(128, 512, generator=g) * 0.04).to(torch.bfloat16)
-    b3, b1 = torch.randn(512, generator=g), torch.randn(128, generator=g)
-    y3_ref = torch.relu(x2.float() @ w3.float().t() + b3 + res.float())
-    y1_ref = torch.relu(y3_ref.to(torch.bfloat16).float() @ w1.float().t() + b1)
-    y3, y1 = K.bottleneck_tail(x2.to(DEV), res.to(DEV), w3.to(DEV), b3.to(DEV), w1.to(DEV), b1.to(DEV))
-    torch.cuda.synchronize()
-    _close(y3, y3_ref)
-    _close(y1, y1_ref)
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("D,dtype", [(768, torch.bfloat16), (64, torch.float32)])
 def test_gather_rows_kernel(D, dtype):
     """First-token (CLS) row gather of the packed encoder: == torch indexing; an index

@@ -54,31 +54,6 @@ def test_pw_res_gpu_channel_offset():
     assert (got[:, :128] == 0).all() and (got[:, 384:] == 0).all()
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("M,N", [(200704 // 8, 512), (1000 + 7, 256)])
-def test_pw_dual_gpu(M, N):
-    """Dual-source form: relu([x | x2] @ w^T + b) (expand conv + decimated projection)."""
-    g = torch.Generator().manual_seed(M)
-    x = torch.randn(M, 128, generator=g).bfloat16()
-    x2 = torch.randn(M, 256, generator=g).bfloat16()
-    w = (torch.randn(N, 384, generator=g) / 20).bfloat16()
-    b = torch.randn(N, generator=g)
-    ref = torch.relu(torch.cat([x, x2], 1).float() @ w.float().t() + b)
-    dev = torch.device("cuda", 0)
-    got = K.pw_dual(x.to(dev), x2.to(dev), w.to(dev), b.to(dev)).float().cpu()
-    torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
-
-
-def test_pw_dual_host():
-    g = torch.Generator().manual_seed(1)
-    x, x2 = torch.randn(2, 3, 5, 128, generator=g), torch.randn(2, 3, 5, 256, generator=g)
-    w, b = torch.randn(256, 384, generator=g) / 20, torch.randn(256, generator=g)
-    ref = torch.relu(torch.cat([x, x2], -1) @ w.t() + b)
-    torch.testing.assert_close(K.pw_dual(x, x2, w, b), ref, rtol=1e-4, atol=1e-4)
-    with pytest.raises(ValueError):
-        K.pw_dual(x[..., :64], x2, w[:, :320], b)
-
-
 def test_resnet50_plan_routes_expands_to_pw_res():
     from flink_tensorflow_amd.graph.compiler import CompiledFunction
     from flink_tensorflow_amd.graph.graph import Graph
