@@ -22,6 +22,27 @@ def label_is(name, threshold=0.5):
     return lambda v: any(lbl == name and p >= threshold for p, lbl in v[1])
 
 
+def build_job(env, model, images_dir: str, polls=None, interval_s: float = 1.0, image_hw=(224, 224),
+              workers: bool = False):
+    """The Johnny pipeline: monitor ``images_dir`` continuously → label each new image with
+    ``model`` (``label([img]) -> [[(p, label), ...]]``) → CEP.  The readers run at the
+    environment's parallelism and, with ``workers``, are chained with the model operator in
+    its worker processes.  Returns the CEP result stream."""
+    images = env.read_file(ImageInputFormat(resize_to=image_hw), images_dir, PROCESS_CONTINUOUSLY, interval_s,
+                           max_polls=polls)
+    labels = images.map_with_model(model, lambda rec, m: (rec[0], m.label([rec[1]])[0]))
+    if workers:
+        labels = labels.run_in_processes()
+    # CEP needs the labels in arrival order on one subtask
+    labels = labels.global_() if env.parallelism > 1 else labels
+    pattern = (Pattern.begin("first").where(label_is("cheeseburger"))
+               .followed_by("second").where(label_is("ladybug"))
+               .followed_by("third").where(label_is("llama")).within(60))
+    return CEP.pattern(labels, pattern).select(
+        lambda m: ("AccessGranted", [m[k][0] for k in ("first", "second", "third")]),
+        lambda partial, ts: ("AccessDenied", sorted(partial)))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("model_dir")
@@ -29,15 +50,7 @@ def main():
     ap.add_argument("--polls", type=int, default=None, help="stop after N directory polls (default: run forever)")
     a = ap.parse_args()
     env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(1)
-    images = env.read_file(ImageInputFormat(resize_to=(224, 224)), a.images_dir, PROCESS_CONTINUOUSLY, 1.0,
-                           max_polls=a.polls)
-    labels = images.map_with_model(InceptionModel(a.model_dir, image_hw=(224, 224)),
-                                   lambda rec, m: (rec[0], m.label([rec[1]])[0]))
-    pattern = (Pattern.begin("first").where(label_is("cheeseburger"))
-               .followed_by("second").where(label_is("ladybug"))
-               .followed_by("third").where(label_is("llama")).within(60))
-    CEP.pattern(labels, pattern).select(lambda m: ("AccessGranted", [m[k][0] for k in ("first", "second", "third")]),
-                                        lambda partial, ts: ("AccessDenied", sorted(partial))).print()
+    build_job(env, InceptionModel(a.model_dir, image_hw=(224, 224)), a.images_dir, a.polls).print()
     env.execute("Johnny")
 
 

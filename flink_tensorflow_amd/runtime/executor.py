@@ -683,7 +683,7 @@ class LocalExecutor:
     # ---- build + run
     def _build(self, restore_states: dict | None):
         self._groups = {}  # a restarted attempt rendezvouses afresh (new store, new prefix)
-        nodes = self.env._topo_nodes()
+        nodes = self._chain_into_workers(self.env._topo_nodes())
         self.relocated = self._relocate_sources(nodes)
         cap = self.config.channel_capacity
         ops = {(n.uid, i): n.make_operator() for n in nodes if not n.is_source and not getattr(n, "remote", False)
@@ -755,6 +755,39 @@ class LocalExecutor:
         from .remote import RemoteOperatorProxy
 
         return RemoteOperatorProxy(node, subtask, self)
+
+    def _chain_into_workers(self, nodes) -> list:
+        """Chains a host operator marked ``chain_into_worker`` (``read_file``'s readers) into
+        the worker process of the worker-process operator it feeds — same parallelism,
+        forward or rebalance edge, that operator's only input: the worker then runs
+        ``ChainOperator([reader, op])``, so files are read and decoded where their records
+        are consumed and the coordinator sends only the monitor's paths (Flink chains the
+        ``ContinuousFileReaderOperator`` with its successor in one task slot).  Idempotent
+        across restart attempts.  Returns the nodes left to schedule."""
+        from .operators import ChainOperator
+
+        if not getattr(self.env, "chaining", True):
+            return list(nodes)
+        consumers: dict[str, list] = {}
+        for n in nodes:
+            for up, part, side_tag in n.inputs:
+                consumers.setdefault(up.uid, []).append((n, part, side_tag))
+        for r in nodes:
+            if not getattr(r, "chain_into_worker", False) or getattr(r, "merged_into", None) is not None:
+                continue
+            cs = consumers.get(r.uid, [])
+            if len(cs) != 1:
+                continue
+            d, part, side_tag = cs[0]
+            if (not getattr(d, "remote", False) or d.is_source or side_tag is not None or len(d.inputs) != 1
+                    or d.parallelism != r.parallelism or part.kind not in ("forward", "rebalance")
+                    or not getattr(d, "chaining", True)):
+                continue
+            head, tail, name = r.factory, d.factory, d.name
+            d.factory = lambda head=head, tail=tail, name=name: ChainOperator([head(), tail()], name)
+            d.inputs = list(r.inputs)
+            r.merged_into = d
+        return [n for n in nodes if getattr(n, "merged_into", None) is None]
 
     def _relocate_sources(self, nodes) -> list[str]:
         """Moves relocatable sources into the worker processes of their consumer: a source

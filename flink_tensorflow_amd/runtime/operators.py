@@ -439,3 +439,115 @@ class UnionOperator(Operator):
 
     def process(self, rec, input_index=0):
         self.out._emit(rec)
+
+
+# ------------------------------------------------------------------ file readers
+class FileReaderOperator(Operator):
+    """Flink's ``ContinuousFileReaderOperator``: receives file paths from the file monitor
+    (``FileMonitorFunction``) and emits one record per file — ``fmt.read_record(path, bytes)`` (decode,
+    normalise, the format's source-owned model) runs here, in the reader subtask, which the
+    executor chains into the worker process of a GPU operator it feeds
+    (``LocalExecutor._chain_into_workers``).  State: the splits received but not yet read
+    (re-read after a restore), as Flink's reader keeps its pending splits."""
+
+    def __init__(self, fmt, name: str = "file-reader"):
+        super().__init__(None, name)
+        self.fmt = fmt
+        self.pending: list = []
+
+    def open(self):
+        self.fmt.open_input_format()
+        self._drain(None)  # splits restored from a checkpoint
+
+    def close(self):
+        self.fmt.close_input_format()
+
+    def process(self, rec: Record, input_index: int = 0):
+        self.pending.append(rec.value)
+        self._drain(rec.ts)
+
+    def _drain(self, ts):
+        from ..utils import fs
+
+        while self.pending:
+            path = self.pending[0]
+            out = self.fmt.read_record(path, fs.read_bytes(path))
+            self.pending.pop(0)
+            if out is not None:
+                self.out.emit(out, ts)
+
+    def snapshot_extra(self):
+        return {"pending": list(self.pending)}
+
+    def restore_extra(self, extra):
+        self.pending = list((extra or {}).get("pending", []))
+
+
+class ChainOperator(Operator):
+    """Operators run back to back in one subtask (Flink's operator chain) when the head
+    must live where the tail runs: a file reader chained in front of the GPU operator in
+    its worker process.  Elements and watermarks flow through direct calls; checkpoint
+    hooks visit the members head first (so the head's flushed output reaches the next one
+    before it snapshots); the state is the list of the members' states."""
+
+    def __init__(self, ops: list, name: str = "chain"):
+        super().__init__(None, name)
+        self.ops = list(ops)
+
+    @property
+    def chainable(self):
+        return all(getattr(o, "chainable", True) for o in self.ops)
+
+    def setup(self, ctx, out: Output):
+        super().setup(ctx, out)
+        for a, b in zip(self.ops, self.ops[1:]):
+            def fwd(elem, b=b):
+                if isinstance(elem, Watermark):
+                    b.process_watermark(elem, 0)
+                else:
+                    b.process(elem, 0)
+
+            a.setup(ctx, Output(fwd, out._side))
+        self.ops[-1].setup(ctx, out)
+
+    def initialize(self, snapshot, checkpoint_dir):
+        states = (snapshot or {}).get("chain") if snapshot is not None else None
+        for i, op in enumerate(self.ops):
+            op.initialize(states[i] if states is not None else None, checkpoint_dir)
+
+    def open(self):
+        for op in self.ops:
+            op.open()
+
+    def close(self):
+        for op in self.ops:
+            op.close()
+
+    def process(self, rec: Record, input_index: int = 0):
+        self.ops[0].process(rec, input_index)
+
+    def process_watermark(self, wm: Watermark, input_index: int = 0):
+        self.ops[0].process_watermark(wm, input_index)
+
+    def on_idle(self, now: float):
+        for op in self.ops:
+            op.on_idle(now)
+
+    def next_deadline(self):
+        ds = [d for d in (op.next_deadline() for op in self.ops) if d is not None]
+        return min(ds) if ds else None
+
+    def end_input(self):
+        for op in self.ops:
+            op.end_input()
+
+    def prepare_snapshot(self):
+        for op in self.ops:
+            op.prepare_snapshot()
+
+    def snapshot_state(self, checkpoint_id: int, checkpoint_dir):
+        return {"chain": [op.snapshot_state(checkpoint_id, checkpoint_dir) for op in self.ops]}
+
+    def notify_checkpoint_complete(self, checkpoint_id: int):
+        for op in self.ops:
+            op.notify_checkpoint_complete(checkpoint_id)

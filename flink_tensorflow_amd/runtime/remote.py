@@ -310,7 +310,7 @@ class ShmChannel:
         self.name = name
         self.owner = create
 
-    def send(self, msg, timeout_s: float = -1.0, alive=None):
+    def send(self, msg, timeout_s: float = -1.0, alive=None) -> int:
         data = cloudpickle.dumps(msg, protocol=5)
         step = self.ring.max_message - 1
         parts = [data[i:i + step] for i in range(0, len(data), step)] or [b""]
@@ -321,6 +321,7 @@ class ShmChannel:
                     raise RemoteTaskError(f"peer of {self.name} died")
                 if timeout_s >= 0:
                     raise TimeoutError(f"{self.name}: ring full")
+        return len(data)
 
     def recv(self, timeout_s: float):
         """A message, or None on timeout (or when the producer closed the ring)."""
@@ -702,6 +703,10 @@ def _job_group(job, node):
     return f(node) if f is not None and getattr(node, "uses_gpu", False) else None
 
 
+# (operator name, subtask) -> the last attempt's coordinator -> worker record traffic
+TRANSPORT_STATS: dict = {}
+
+
 class RemoteOperatorProxy:
     """Stands in for the operator inside the coordinator's task loop."""
 
@@ -724,6 +729,9 @@ class RemoteOperatorProxy:
         self._error: tuple | None = None
         self._drainer: threading.Thread | None = None
         self.worker_metrics: dict | None = None
+        # coordinator -> worker record traffic: records, bytes of the "recs" messages on the
+        # ring (pickled values or slab descriptors) and payload bytes through the slab
+        self.stats = {"records": 0, "ring_bytes": 0, "slab_bytes": 0}
 
     # ---- lifecycle (called by the task thread)
     def setup(self, ctx, out: Output):
@@ -777,6 +785,7 @@ class RemoteOperatorProxy:
             self._shutdown(graceful)
 
     def _shutdown(self, graceful: bool = False):
+        TRANSPORT_STATS[(self.node.name, self.subtask)] = dict(self.stats)
         if self.proc is not None:
             if not graceful and self.proc.is_alive():
                 self.proc.terminate()  # failed / cancelled attempt: its state is discarded anyway
@@ -839,17 +848,20 @@ class RemoteOperatorProxy:
     def _alive(self) -> bool:
         return self.proc is not None and self.proc.is_alive()
 
-    def _send(self, msg):
+    def _send(self, msg) -> int:
         self._check()
         with self._send_lock:  # task thread + checkpoint-complete notifications: one producer at a time
-            self.to_worker.send(msg, alive=self._alive)
+            return self.to_worker.send(msg, alive=self._alive)
 
     def _flush(self):
         if self._buf:
             batch, self._buf = self._buf, []
             if self.slab is not None:
+                b0 = self.slab.bytes
                 batch = self.slab.put_batch(batch)
-            self._send(("recs", batch))
+                self.stats["slab_bytes"] += self.slab.bytes - b0
+            self.stats["records"] += len(batch)
+            self.stats["ring_bytes"] += self._send(("recs", batch))
 
     def _check(self):
         if self._error is not None:

@@ -2,11 +2,17 @@
 
 * ``CollectionSource`` — ``env.from_collection`` (checkpoints its offset; partitioned across
   subtasks and across ranks in distributed mode).
-* ``FileMonitoringSource`` + ``WholeFileInputFormat`` — ``env.read_file(format, path,
-  PROCESS_ONCE | PROCESS_CONTINUOUSLY, interval)`` with exactly one record per file
-  (``LIB/io/WholeFileInputFormat.scala:14-80``).  End detection is an explicit
-  "emitted" flag, so zero-length files do not re-emit forever (B5); include/exclude glob
-  filters are merged rather than overwritten (B8).
+* ``env.read_file(format, path, PROCESS_ONCE | PROCESS_CONTINUOUSLY, interval)`` as Flink
+  builds it: ``FileMonitorFunction`` (parallelism 1) lists the directory and forwards only
+  the new files' PATHS, round-robin to the parallel
+  ``FileReaderOperator`` subtasks, which read each file and run the format's
+  ``read_record`` (decode, normalise) — chained into the worker process of the GPU
+  operator they feed, so the coordinator ships a path per record, not the decoded tensor.
+  Exactly one record per file (``LIB/io/WholeFileInputFormat.scala:14-80``); end
+  detection is an explicit "emitted" flag, so zero-length files do not re-emit forever
+  (B5); include/exclude glob filters are merged rather than overwritten (B8).
+* ``FileMonitoringSource`` — the single-operator form (each subtask lists, reads and
+  decodes the files hashed to it), for jobs that add it as a plain source.
 * ``GeneratorSource`` — records from a Python generator factory (synthetic load).
 * ``PrintSink``, ``MemorySink`` (``TST/.../util/MemorySinkFunction.java``), ``CollectSink``.
 """
@@ -191,6 +197,62 @@ class FileMonitoringSource(SourceFunction, CheckpointedFunction):
 
     def cancel(self):
         self._running = False
+
+
+class FileMonitorFunction(SourceFunction, CheckpointedFunction):
+    """Flink's ``ContinuousFileMonitoringFunction``: lists ``path`` through the format's
+    filters and emits each file not seen before as its path (a plain ``str``: a whole file
+    is one split, and the path is all a reader needs) — nothing read or decoded here; PROCESS_CONTINUOUSLY re-lists every ``interval_s``.  Runs with
+    parallelism 1; its checkpoint state is the set of paths already forwarded (a path
+    forwarded before a barrier is read by its reader before the reader snapshots, so every
+    file is read exactly once across restarts).  The format is never opened here (a
+    source-owned model, ``ImageInputFormat``'s normaliser, loads in the readers)."""
+
+    def __init__(self, fmt: WholeFileInputFormat, path: str, mode: FileProcessingMode = PROCESS_ONCE,
+                 interval_s: float = 1.0, max_polls: int | None = None):
+        super().__init__()
+        self.fmt = fmt
+        self.path = path
+        self.mode = mode
+        self.interval = interval_s
+        self.max_polls = max_polls
+        self.seen: set[str] = set()
+        self._running = True
+
+    def initialize_state(self, ctx):
+        self._state = ctx.operator_state.get_list_state(ListStateDescriptor("seen"))
+        if ctx.is_restored():
+            self.seen = set(self._state.get())
+
+    def snapshot_state(self, ctx):
+        self._state.update(sorted(self.seen))
+
+    def run(self, ctx):
+        polls = 0
+        while self._running:
+            # oldest first, as Flink forwards splits by modification time
+            for f in sorted((f for f in self.fmt.files(self.path) if f not in self.seen), key=_mtime_then_name):
+                with ctx.checkpoint_lock:
+                    ctx.collect(str(f))
+                    self.seen.add(f)
+            polls += 1
+            if self.mode == PROCESS_ONCE or (self.max_polls is not None and polls >= self.max_polls):
+                break
+            t_end = time.time() + self.interval
+            while self._running and time.time() < t_end:
+                time.sleep(min(0.05, self.interval))
+
+    def cancel(self):
+        self._running = False
+
+
+def _mtime_then_name(path: str):
+    import os
+
+    try:
+        return (os.path.getmtime(path), path)
+    except OSError:
+        return (0.0, path)
 
 
 def hash_str(s: str) -> int:

@@ -169,9 +169,22 @@ class StreamExecutionEnvironment:
         return self.add_source(GeneratorSource(factory, limit), "generator", parallelism)
 
     def read_file(self, fmt: WholeFileInputFormat, path: str, mode=PROCESS_ONCE, interval_s: float = 1.0,
-                  parallelism: int = 1, max_polls: int | None = None) -> "DataStream":
-        return self.add_source(FileMonitoringSource(fmt, path, mode, interval_s, max_polls), "file-source",
-                               parallelism)
+                  parallelism: int | None = None, max_polls: int | None = None) -> "DataStream":
+        """``StreamExecutionEnvironment.readFile`` (``EX/inception/inception.scala:33-34``)
+        as Flink builds it: one monitor (parallelism 1, in the coordinator) forwarding the
+        new files' paths round-robin to ``parallelism`` readers (default: the
+        environment's) that read and decode them.  A reader feeding a worker-process GPU
+        operator of its parallelism is chained into that worker, so decoding happens where
+        the records are consumed and only paths cross the coordinator."""
+        from .operators import FileReaderOperator
+        from .sources import FileMonitorFunction
+
+        mon = self.add_source(FileMonitorFunction(fmt, path, mode, interval_s, max_polls), "file-monitor", 1)
+        proto = fmt
+        readers = mon._add("file-reader", lambda: FileReaderOperator(clone_function(proto), "file-reader"),
+                           parallelism or self.parallelism, Partitioner("rebalance"))
+        readers.node.chain_into_worker = True
+        return readers
 
     readFile = read_file
 
