@@ -39,6 +39,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from flink_tensorflow_amd.models.zoo.wide_deep import (WideDeepConfig, WideDeepTrainer,  # noqa: E402
                                                        synthetic_click_records)
 from flink_tensorflow_amd.runtime import StreamExecutionEnvironment  # noqa: E402
+from flink_tensorflow_amd.runtime.lockstep import LockstepTrainer  # noqa: E402
 from flink_tensorflow_amd.runtime.model_functions import ModelCoProcessFunction  # noqa: E402
 from flink_tensorflow_amd.runtime.sources import CollectionSource  # noqa: E402
 
@@ -100,6 +101,9 @@ def main():
     ap.add_argument("--eval-every", type=float, default=0.5, help="seconds between eval ticks")
     ap.add_argument("--checkpoint-dir", default=None)
     ap.add_argument("--cpu", action="store_true", help="tiny model on the host (plumbing check)")
+    ap.add_argument("--parallelism", type=int, default=1,
+                    help="P > 1: P worker-process ranks (one per GPU) of ONE data-parallel trainer, kept in "
+                         "lockstep over the uneven rebalanced stream (runtime/lockstep.py)")
     a = ap.parse_args()
 
     import torch
@@ -112,21 +116,32 @@ def main():
     heldout, recs = recs[:batch], recs[batch:]
     n_ticks = max(1, int(math.ceil(3.0 / max(1e-3, a.eval_every))))
 
-    env = StreamExecutionEnvironment.get_execution_environment()
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(a.parallelism)
     if a.checkpoint_dir:
         env.enable_checkpointing(1.0, a.checkpoint_dir)
-    clicks = env.add_source(CollectionSource(recs), "clicks")
-    ticks = env.add_source(CollectionSource(["eval"] * n_ticks, delay_s=a.eval_every), "control")
-    trainer = WideDeepTrainer(cfg, device="cuda" if gpu else "cpu", seed=0)
-    fn = OnlineTrainer(trainer, batch, a.max_delay_ms, heldout)
-    sink = clicks.connect(ticks).process(fn).name("widedeep-online").collect_into()
+    clicks = env.add_source(CollectionSource(recs), "clicks", parallelism=1)
+    ticks = env.add_source(CollectionSource(["eval"] * n_ticks, delay_s=a.eval_every), "control", parallelism=1)
+    if a.parallelism > 1:  # the subtasks form the job communicator (RCCL, one GPU each)
+        env.enable_job_communicator(True)
+        trainer = WideDeepTrainer(cfg, device=None if gpu else "cpu", seed=0)  # None: the subtask's GPU
+        fn = LockstepTrainer(trainer, batch, a.max_delay_ms, heldout)
+        sink = clicks.rebalance().connect(ticks).process(fn).name("widedeep-online").run_in_processes().collect_into()
+    else:
+        trainer = WideDeepTrainer(cfg, device="cuda" if gpu else "cpu", seed=0)
+        fn = OnlineTrainer(trainer, batch, a.max_delay_ms, heldout)
+        sink = clicks.connect(ticks).process(fn).name("widedeep-online").collect_into()
     t0 = time.perf_counter()
     res = env.execute("widedeep-online")
     wall = time.perf_counter() - t0
     out = sink.results()
     train = [o for o in out if o[0] == "train"]
     evals = [o for o in out if o[0] == "eval"]
-    trained = sum(o[2] for o in train)
+    if a.parallelism > 1:  # ("train", step, rank, n, total, loss): one line per rank and step
+        trained = sum(o[3] for o in train)
+        train = sorted((o for o in train if o[2] == 0), key=lambda o: o[1])
+        train = [(o[0], o[1], o[4], o[5]) for o in train]
+    else:
+        trained = sum(o[2] for o in train)
     print(json.dumps({
         "job": "widedeep-online", "device": "gpu" if gpu else "cpu", "records_trained": trained,
         "steps": len(train), "records_per_s_wall": round(trained / wall, 1), "wall_s": round(wall, 2),

@@ -81,9 +81,9 @@ __global__ __launch_bounds__(256) void wd_gather_kernel(const int* __restrict__ 
 __global__ __launch_bounds__(256) void wd_loss_kernel(const bf16* __restrict__ head, int ldh,
                                                       const float* __restrict__ wsum, const float* __restrict__ wbias,
                                                       const float* __restrict__ labels, int ldl, int B,
-                                                      float* __restrict__ dlogit, bf16* __restrict__ dlogit16,
-                                                      float* __restrict__ part, float* __restrict__ wgrad, int C,
-                                                      int WD) {
+                                                      float norm, float* __restrict__ dlogit,
+                                                      bf16* __restrict__ dlogit16, float* __restrict__ part,
+                                                      float* __restrict__ wgrad, int C, int WD) {
   __shared__ float red[2][4];
   const int b = blockIdx.x * 256 + threadIdx.x;
   float lo = 0.f, d = 0.f;
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void wd_loss_kernel(const bf16* __restrict__ h
     const float l = (float)head[(size_t)b * ldh] + wsum[b] + wbias[0];
     const float y = labels[(size_t)b * ldl];
     lo = fmaxf(l, 0.f) - l * y + log1pf(__expf(-fabsf(l)));
-    d = (__builtin_amdgcn_rcpf(1.f + __expf(-l)) - y) / (float)B;
+    d = (__builtin_amdgcn_rcpf(1.f + __expf(-l)) - y) / norm;
     dlogit[b] = d;
     dlogit16[b] = f2bf(d);
     for (int c = 0; c < C; ++c) {  // the wide part: every lookup's row gets d in column 0
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void wd_loss_kernel(const bf16* __restrict__ h
   }
 }
 
-__global__ __launch_bounds__(64) void wd_loss_final_kernel(const float* __restrict__ part, int nb, int B,
+__global__ __launch_bounds__(64) void wd_loss_final_kernel(const float* __restrict__ part, int nb, float norm,
                                                            float* __restrict__ loss, float* __restrict__ g_wbias,
                                                            float* __restrict__ g_hb0) {
   float a = 0.f, s = 0.f;
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(64) void wd_loss_final_kernel(const float* __restri
   a = wave_reduce_sum(a);
   s = wave_reduce_sum(s);
   if (threadIdx.x == 0) {
-    loss[0] = a / (float)B;
+    loss[0] = a / norm;
     g_wbias[0] = s;
     g_hb0[0] = s;
   }
@@ -287,20 +287,23 @@ void wd_gather(uintptr_t cats, int ldc, uintptr_t dense, int ldd, uintptr_t cros
   FTM_CHECK_LAUNCH();
 }
 
-// part: >= 2 * ceil(B / 256) floats of workspace
-void wd_loss(uintptr_t head, int ldh, uintptr_t wsum, uintptr_t wbias, uintptr_t labels, int ldl, int B, uintptr_t dlogit,
-             uintptr_t dlogit16, uintptr_t loss, uintptr_t g_wbias, uintptr_t g_hb0, uintptr_t wgrad, int C, int WD,
-             uintptr_t part, uintptr_t stream) {
+// part: >= 2 * ceil(B / 256) floats of workspace.  norm: the loss is sum / norm — B for the
+// batch mean; the global record count of an agreed data-parallel step over uneven pieces
+// (parallel/step_agreement.py), so the summed gradients are those of the union's mean.
+void wd_loss(uintptr_t head, int ldh, uintptr_t wsum, uintptr_t wbias, uintptr_t labels, int ldl, int B, float norm,
+             uintptr_t dlogit, uintptr_t dlogit16, uintptr_t loss, uintptr_t g_wbias, uintptr_t g_hb0, uintptr_t wgrad,
+             int C, int WD, uintptr_t part, uintptr_t stream) {
   if (B <= 0) throw std::invalid_argument("wd_loss: empty batch");
+  if (!(norm > 0.f)) throw std::invalid_argument("wd_loss: norm must be positive");
   if (wgrad % 16) throw std::invalid_argument("wd_loss: wgrad must be 16-byte aligned");
   auto s = reinterpret_cast<hipStream_t>(stream);
   const int nb = (B + 255) / 256;
   hipLaunchKernelGGL(wd_loss_kernel, dim3(nb), dim3(256), 0, s, reinterpret_cast<const bf16*>(head), ldh,
                      reinterpret_cast<const float*>(wsum), reinterpret_cast<const float*>(wbias),
-                     reinterpret_cast<const float*>(labels), ldl, B, reinterpret_cast<float*>(dlogit),
+                     reinterpret_cast<const float*>(labels), ldl, B, norm, reinterpret_cast<float*>(dlogit),
                      reinterpret_cast<bf16*>(dlogit16), reinterpret_cast<float*>(part), reinterpret_cast<float*>(wgrad),
                      C, WD);
-  hipLaunchKernelGGL(wd_loss_final_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<const float*>(part), nb, B,
+  hipLaunchKernelGGL(wd_loss_final_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<const float*>(part), nb, norm,
                      reinterpret_cast<float*>(loss), reinterpret_cast<float*>(g_wbias), reinterpret_cast<float*>(g_hb0));
   FTM_CHECK_LAUNCH();
 }

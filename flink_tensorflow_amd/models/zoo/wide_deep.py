@@ -32,7 +32,7 @@ from ...ops.autograd import Linear
 from ...utils.tracing import capture_lock, graph_capture
 from ...ops.embedding import SparseEmbedding
 from ...parallel import comm
-from ...runtime.model_functions import CheckpointedModel, model_state_dir
+from ...runtime.model_functions import CheckpointedModel
 from ..core import RichModel, default_device
 
 
@@ -124,6 +124,24 @@ def _sparse_sync(uids: torch.Tensor, rows: torch.Tensor):
     return gu, gr  # -1 ids are dropped by the merge
 
 
+def _sparse_sync_var(uids: torch.Tensor, rows: torch.Tensor):
+    """``_sparse_sync`` for pieces of different sizes (an agreed step over uneven inputs,
+    ``parallel/step_agreement.py``): the slot counts are all-gathered first and every rank
+    pads its slots (uid -1, zero rows) to the largest."""
+    if not comm.is_dist():
+        return uids, rows
+    c = comm.get()
+    n = torch.tensor([uids.numel()], dtype=torch.int64, device=c.device)
+    sizes = torch.empty(c.size, dtype=torch.int64, device=c.device)
+    c.all_gather(sizes, n)
+    cap = int(sizes.max().item())
+    if cap > uids.numel():
+        pad = cap - uids.numel()
+        uids = torch.cat([uids.reshape(-1), torch.full((pad,), -1, dtype=uids.dtype, device=uids.device)])
+        rows = torch.cat([rows, torch.zeros((pad, rows.shape[1]), dtype=rows.dtype, device=rows.device)])
+    return _sparse_sync(uids, rows)
+
+
 class WideDeepTrainer(RichModel, CheckpointedModel):
     """Online trainer: ``train_step(records)`` on micro-batches of
     ``(label, dense[13], cats[26], cross[C])`` records; ``predict(records)``."""
@@ -195,7 +213,19 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         return (labels.to(d, non_blocking=nb), dense.to(d, non_blocking=nb), cats.to(d, non_blocking=nb),
                 cross.to(d, non_blocking=nb))
 
-    def train_step(self, records=None, batch=None) -> float:
+    def train_step(self, records=None, batch=None, counts=None) -> float:
+        """One training step on a micro-batch (``records`` or a collated ``batch``).
+
+        ``counts``: the per-rank record counts of an AGREED step (``parallel/step_agreement.py``,
+        driven by ``runtime/lockstep.py``): this rank's piece may be empty or smaller than
+        its peers'; the loss is the piece's sum over ``sum(counts)`` and the dense gradients
+        are summed across ranks, so the update is the gradient of the mean over the union
+        of the pieces, and every rank issues the same collectives in the same order."""
+        if counts is not None:
+            n = int(batch[0].shape[0]) if batch is not None else len(records or ())
+            if n:
+                batch = batch if batch is not None else self.collate(records)
+            return self._step(batch if n else None, norm=int(sum(counts)))
         batch = batch if batch is not None else self.collate(records)
         if self._graph is not None and all(a.shape == b.shape for a, b in zip(batch, self._static)):
             sp, bp = getattr(self._static, "packed", None), getattr(batch, "packed", None)
@@ -239,27 +269,83 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
                 self._static_loss = self._step(self._static)
             self._graph = g
 
-    def _step(self, batch):
+    def _step(self, batch, norm: int | None = None):
+        """``norm`` None: a plain step (batch mean, gradients averaged over ranks).  Else an
+        agreed step: ``batch`` None when this rank brings no records."""
         m = self._model
-        labels, dense, cats, cross = batch
+        agreed = norm is not None
         if self._fused is not None:
-            loss = self._fused.step(labels, dense, cats, cross)
+            loss = self._fused.step(*batch, norm=norm) if batch is not None else self._fused.empty_step()
             self.steps += 1
             return loss
+        if batch is None:
+            batch = self._empty_batch()
+        labels, dense, cats, cross = batch
         if self._exchange is not None:
             self._exchange.begin_step()
             self.pull_rows(cats, cross)
-        logits = m(dense, cats, cross)
-        loss = F.binary_cross_entropy_with_logits(logits, labels)
         self._opt.zero_grad(set_to_none=True)
-        loss.backward()
-        self._bucketer.synchronize()  # dense grads: bucketed all-reduce launched during backward
+        # agreed steps launch the buckets in index order at synchronize(): a rank without
+        # records has no backward to launch them from, and the order must match its peers'
+        self._bucketer.deferred = agreed
+        self._bucketer.average = not agreed
+        if labels.numel():
+            logits = m(dense, cats, cross)
+            if agreed:
+                loss = F.binary_cross_entropy_with_logits(logits, labels, reduction="sum") / norm
+            else:
+                loss = F.binary_cross_entropy_with_logits(logits, labels)
+            loss.backward()
+        else:  # no rows to send, but the sparse exchange is collective: take part with none
+            loss = torch.zeros((), device=m.device)
+            for e in (m.emb, m.wide):
+                e.sparse_grads.append((torch.empty(0, dtype=torch.int32, device=m.device),
+                                       torch.empty((0, e.table.shape[1]), dtype=torch.float32, device=m.device)))
+        self._bucketer.synchronize()  # dense grads: bucketed all-reduce (launched during backward unless deferred)
         self._opt.step()
-        sync = _sparse_sync if comm.is_dist() else None
+        sync = (_sparse_sync_var if agreed else _sparse_sync) if comm.is_dist() else None
         m.emb.apply_updates(self.cfg.lr_sparse, sync, self._exchange)
         m.wide.apply_updates(self.cfg.lr_sparse, sync, self._exchange)
         self.steps += 1
         return loss.detach()
+
+    def _empty_batch(self):
+        cfg, dev = self.cfg, self._model.device
+        return (torch.empty(0, device=dev), torch.empty((0, cfg.num_dense), device=dev),
+                torch.empty((0, cfg.num_fields), dtype=torch.int32, device=dev),
+                torch.empty((0, 1), dtype=torch.int32, device=dev))
+
+    def train_pieces(self, pieces) -> torch.Tensor:
+        """The 1-rank reference of an agreed data-parallel step: the pieces ``P`` ranks
+        bring to one round (rank order, empty ones included), trained in ONE process with
+        the arithmetic of the P-rank step — each piece's gradients of its loss sum over the
+        round's record count, summed in rank order starting from rank 0's (zeros for an
+        empty piece), as the loopback / 2-rank all-reduce sums them; the sparse rows merged
+        in (id, piece) order, as the owner exchange and the padded all-gather merge them.
+        Host autograd path only (tests pin DP replicas to it bit for bit)."""
+        if comm.is_dist() or self._fused is not None:
+            raise RuntimeError("train_pieces is the single-process host reference")
+        m = self._model
+        norm = sum(len(p) for p in pieces)
+        params = [p for p in self._opt.param_groups[0]["params"]]
+        acc = None
+        total = torch.zeros(())
+        for recs in pieces:
+            self._opt.zero_grad(set_to_none=True)
+            if recs:
+                labels, dense, cats, cross = self.collate(recs)
+                loss = F.binary_cross_entropy_with_logits(m(dense, cats, cross), labels, reduction="sum") / norm
+                loss.backward()
+                total = total + loss.detach()
+            g = [p.grad.detach().clone() if p.grad is not None else torch.zeros_like(p) for p in params]
+            acc = g if acc is None else [a + b for a, b in zip(acc, g)]
+        for p, a in zip(params, acc):
+            p.grad = a
+        self._opt.step()
+        m.emb.apply_updates(self.cfg.lr_sparse, merge=True)
+        m.wide.apply_updates(self.cfg.lr_sparse, merge=True)
+        self.steps += 1
+        return total
 
     def pull_rows(self, cats, cross) -> None:
         """Owner exchange: refreshes the embedding / wide rows this batch looks up from their
@@ -270,35 +356,76 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         self._exchange.pull_lookups(m.wide.table.data, cross)
 
     @torch.no_grad()
+    def refresh_rows(self, records) -> None:
+        """Under the owner exchange: refreshes the rows ``records`` look up from their owners
+        (COLLECTIVE — every rank calls it at the same point, with its own records or none;
+        ``runtime/lockstep.py`` does so in an agreed round).  No-op otherwise."""
+        if self._exchange is None:
+            return
+        if records:
+            _, _, cats, cross = self.collate(records)
+        else:
+            _, _, cats, cross = self._empty_batch()
+        self.pull_rows(cats, cross)
+
+    @torch.no_grad()
     def predict(self, records) -> list[float]:
+        """Scores ``records`` with this replica's tables — collective-free, so it is safe
+        anywhere in a stream.  Under the owner exchange the rows this rank does not own are
+        its cache, current as of the last step or ``refresh_rows`` that read them: call
+        ``refresh_rows`` in an agreed round first for owner-fresh rows."""
         _, dense, cats, cross = self.collate(records)
-        if self._exchange is not None:
-            self.pull_rows(cats, cross)
         return torch.sigmoid(self._model(dense, cats, cross)).tolist()
 
     # ---- CheckpointedModel
+    _SHARDED = ("emb.table", "emb.accum", "wide.table", "wide.accum")
+
     def snapshot_state(self, ctx):
-        d = model_state_dir(ctx, "widedeep")
-        st = {f"model/{k}": v for k, v in self._model.state().items()}
-        if self._exchange is not None:  # owner-authoritative rows and Adagrad state: merge the shards
-            for name, e in (("emb", self._model.emb), ("wide", self._model.wide)):
-                st[f"model/{name}.table"] = self._exchange.merge_owner_shards(e.table.data)
-                st[f"model/{name}.accum"] = self._exchange.merge_owner_shards(e.accum)
-        if self._fused is not None:
-            st.update(self._fused.state())
-        else:
-            for i, s in enumerate(self._opt.state_dict()["state"].values()):
-                for k, v in s.items():
-                    if torch.is_tensor(v):
-                        st[f"adam/{i}/{k}"] = v.detach().reshape(v.shape)
-        if d is not None and comm.rank_size()[0] == 0:
-            bundle.save_tensors(os.path.join(d, "variables"), st)
+        """Collective-free (a barrier reaches the ranks at different points of
+        their step sequences, so a collective here could pair with a peer's step).  The
+        dense weights and optimizer state are identical on every replica: rank 0 writes
+        them.  Under the owner exchange only the owner's copy of a row (and its Adagrad
+        state) is authoritative: every rank writes the rows it owns (``row % world ==
+        rank``) as its own shard file, and a restore assembles the tables from all shards.
+        With ``runtime/lockstep.py`` the ranks snapshot after the same agreed step."""
+        rank, ws = comm.rank_size()
+        sharded = self._exchange is not None
+        st, shard = {}, {}
+        for k, v in self._model.state().items():
+            if sharded and k in self._SHARDED:
+                shard[f"shard/{k}"] = v[rank::ws].contiguous()
+            elif rank == 0:
+                st[f"model/{k}"] = v
+        if rank == 0:
+            if self._fused is not None:
+                st.update(self._fused.state())
+            else:
+                for i, s in enumerate(self._opt.state_dict()["state"].values()):
+                    for k, v in s.items():
+                        if torch.is_tensor(v):
+                            st[f"adam/{i}/{k}"] = v.detach().reshape(v.shape)
+        d = self._state_dir(ctx)
+        if d is not None:
+            if st:
+                bundle.save_tensors(os.path.join(d, "variables"), st)
+            if shard:
+                bundle.save_tensors(os.path.join(d, f"shard-{rank}-of-{ws}"), shard)
         ctx.operator_state.blobs["widedeep_steps"] = self.steps
+
+    @staticmethod
+    def _state_dir(ctx) -> str | None:
+        """One directory for the whole group (rank 0's dense state + every rank's shard)."""
+        if ctx.checkpoint_dir is None:
+            return None
+        d = os.path.join(ctx.checkpoint_dir, "models", "widedeep-0")
+        os.makedirs(d, exist_ok=True)
+        return d
 
     def initialize_state(self, ctx):
         if not ctx.is_restored() or ctx.checkpoint_dir is None:
             return
-        prefix = os.path.join(ctx.checkpoint_dir, "models", "widedeep-0", "variables")
+        d = os.path.join(ctx.checkpoint_dir, "models", "widedeep-0")
+        prefix = os.path.join(d, "variables")
         if not os.path.exists(prefix + ".index"):
             return
         if self._model is None:
@@ -306,13 +433,42 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         with bundle.BundleReader(prefix) as r:
             sd = {k[len("model/"):]: r.read(k) for k in r.keys() if k.startswith("model/")}
             adam = {k: r.read(k) for k in r.keys() if k.startswith("adam/")}
+        shards = sorted(f[:-len(".index")] for f in os.listdir(d) if f.startswith("shard-") and f.endswith(".index"))
+        if shards:  # owner shards: rows r::world of every sharded tensor come from rank r's file
+            world = int(shards[0].rsplit("-of-", 1)[1])
+            if len(shards) != world:
+                raise RuntimeError(f"checkpoint {d} holds {len(shards)} of {world} owner shards")
+            cur = self._model.state()
+            for k in self._SHARDED:
+                sd[k] = torch.empty_like(cur[k], device="cpu")
+            for f in shards:
+                rank = int(f.split("-")[1])
+                with bundle.BundleReader(os.path.join(d, f)) as r:
+                    for k in self._SHARDED:
+                        sd[k][rank::world] = r.read(f"shard/{k}").reshape(sd[k][rank::world].shape)
         with torch.no_grad():  # in place: the fused step's parameters are views of its flat buffer
             for k, v in self._model.state_dict().items():
                 if k in sd:
                     v.copy_(sd[k].to(v.device).reshape(v.shape))
         if self._fused is not None:
             self._fused.load_state(adam)
+        else:
+            self._load_adam(adam)
         self.steps = ctx.operator_state.blobs.get("widedeep_steps", 0)
+
+    def _load_adam(self, adam: dict) -> None:
+        """Restores torch Adam's per-parameter state (``adam/<i>/<key>``) of the autograd path."""
+        if not adam:
+            return
+        sd = self._opt.state_dict()
+        ids = list(sd["state"].keys()) or [i for g in sd["param_groups"] for i in g["params"]]
+        state = {}
+        for i, pid in enumerate(ids):
+            ent = {k.split("/", 2)[2]: v for k, v in adam.items() if k.startswith(f"adam/{i}/")}
+            if ent:
+                state[pid] = ent
+        sd["state"] = state
+        self._opt.load_state_dict(sd)
 
 
 def click_record_layout(cfg: WideDeepConfig, n_cross: int = 8) -> np.dtype:

@@ -147,7 +147,10 @@ class FusedWideDeepStep:
         H = a.h[-1].shape[1]
         a.head_part = torch.empty(self.head_blocks, 2 * H, dtype=torch.float32, device=dev)
 
-    def step(self, labels, dense, cats, cross) -> torch.Tensor:
+    def step(self, labels, dense, cats, cross, norm: int | None = None) -> torch.Tensor:
+        """One step.  ``norm``: an agreed data-parallel step over uneven pieces
+        (``parallel/step_agreement.py``) — the loss is this piece's sum over the round's
+        global record count and the all-reduced gradients are summed, not averaged."""
         H, m, cfg = self._H, self.m, self.cfg
         B = labels.shape[0]
         a = self._acts.get(B)
@@ -183,7 +186,8 @@ class FusedWideDeepStep:
             h = K.gemm_train(h, self.w16[i], bias=l.bias, act="relu", out=a.h[i])
         K.gemm_train(h, self.w16[-1], bias=m.head.bias, out=a.hd)
         H.wd_loss(a.hd.data_ptr(), a.hd.shape[1], a.wsum.data_ptr(), m.wide_bias.data_ptr(),
-                  labels.data_ptr(), labels.stride(0), B, a.dlogit.data_ptr(), a.dlogit16.data_ptr(), a.loss.data_ptr(),
+                  labels.data_ptr(), labels.stride(0), B, float(norm if norm is not None else B), a.dlogit.data_ptr(),
+                  a.dlogit16.data_ptr(), a.loss.data_ptr(),
                   self.g["wide_bias"].data_ptr(), self.g["head.bias"].data_ptr(), a.wgrad.data_ptr(), C, WD, a.part.data_ptr(), s)
         # backward: head (only logit column 0 is used) -> dh, top bias and head weight gradients
         last = a.h[-1]
@@ -225,22 +229,65 @@ class FusedWideDeepStep:
             self.exchange.apply(m.emb.table.data, m.emb.accum, u, re, self.lr_sparse)
             self.exchange.apply(m.wide.table.data, m.wide.accum, u, rw, self.lr_sparse, offset=FV)
         elif dist:
-            from .wide_deep import _sparse_sync
+            from .wide_deep import _sparse_sync, _sparse_sync_var
 
-            ue, re = segment_sum(*_sparse_sync(u, re), FV + WV, static=True)
-            uw, rw = segment_sum(*_sparse_sync(u, rw), FV + WV, static=True)
+            sync = _sparse_sync if norm is None else _sparse_sync_var  # uneven pieces: pad to the largest
+            ue, re = segment_sum(*sync(u, re), FV + WV, static=True)
+            uw, rw = segment_sum(*sync(u, rw), FV + WV, static=True)
             ws = comm.get().size
         if not (dist and self.exchange is not None):
             sparse_adagrad(m.emb.table.data, m.emb.accum, ue, re, self.lr_sparse)
             sparse_adagrad(m.wide.table.data, m.wide.accum, uw, rw, self.lr_sparse, offset=FV)
         for w in works:  # dense gradients reduced (overlapped with the GEMMs + sparse pipeline)
             w.wait()
-        # dense Adam over the flat buffer + the bf16 operands of the next step
-        self.t.add_(1.0)
-        H.wd_adam(self.flat.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
-                  self.flat.numel(), self.t.data_ptr(), self.lr, self.b1, self.b2, self.eps, 1.0 / ws,
-                  self.seg.data_ptr(), self.seg.shape[1], s)
+        self._adam(1.0 / ws if norm is None else 1.0, s)
         return a.loss
+
+    def _adam(self, scale: float, s) -> None:
+        """Dense Adam over the flat buffer + the bf16 operands of the next step."""
+        self.t.add_(1.0)
+        self._H.wd_adam(self.flat.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                        self.flat.numel(), self.t.data_ptr(), self.lr, self.b1, self.b2, self.eps, scale,
+                        self.seg.data_ptr(), self.seg.shape[1], s)
+
+    def empty_step(self) -> torch.Tensor:
+        """This rank's part of an agreed step it brings no records to: zero gradients into
+        the same all-reduces, no rows into the same sparse exchange, the same Adam update —
+        the collectives are issued in ``step``'s order, so the ranks stay paired."""
+        m = self.m
+        dev = self.dev
+        s = _stream()
+        FV, WV = m.emb.table.shape[0], m.wide.table.shape[0]
+        none = torch.empty(0, dtype=torch.int64, device=dev)
+        dist = comm.is_dist()
+        if dist and self.exchange is not None:
+            self.exchange.begin_step()
+            self.exchange.pull_lookups(m.emb.table.data, none)
+            self.exchange.pull_lookups(m.wide.table.data, none)
+        self.grad.zero_()
+        if dist:
+            c = comm.get()
+            if len(self.layers) > 1 and self._chunk < self.grad.numel():
+                works = [c.all_reduce_async(self.grad[self._chunk:]), c.all_reduce_async(self.grad[:self._chunk])]
+            else:
+                works = [c.all_reduce_async(self.grad)]
+            u = torch.empty(0, dtype=torch.int32, device=dev)
+            re = torch.empty(0, self.D, dtype=torch.float32, device=dev)
+            rw = torch.empty(0, m.wide.table.shape[1], dtype=torch.float32, device=dev)
+            if self.exchange is not None:
+                self.exchange.apply(m.emb.table.data, m.emb.accum, u, re, self.lr_sparse)
+                self.exchange.apply(m.wide.table.data, m.wide.accum, u, rw, self.lr_sparse, offset=FV)
+            else:
+                from .wide_deep import _sparse_sync_var
+
+                ue, re = segment_sum(*_sparse_sync_var(u, re), FV + WV, static=True)
+                uw, rw = segment_sum(*_sparse_sync_var(u, rw), FV + WV, static=True)
+                sparse_adagrad(m.emb.table.data, m.emb.accum, ue, re, self.lr_sparse)
+                sparse_adagrad(m.wide.table.data, m.wide.accum, uw, rw, self.lr_sparse, offset=FV)
+            for w in works:
+                w.wait()
+        self._adam(1.0, s)
+        return torch.zeros((), dtype=torch.float32, device=dev)
 
     # ------------------------------------------------------------------ checkpoints
     def state(self) -> dict[str, torch.Tensor]:

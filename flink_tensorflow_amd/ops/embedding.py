@@ -196,10 +196,12 @@ class SparseEmbedding(torch.nn.Module):
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
         return EmbeddingBagFunction.apply(ids, self.table, self.anchor, self)
 
-    def apply_updates(self, lr: float, sync=None, exchange=None):
+    def apply_updates(self, lr: float, sync=None, exchange=None, merge: bool = False):
         """Applies the step's sparse gradients (optionally synchronised across ranks:
         ``sync`` all-gathers them for every replica to apply; ``exchange`` — an
-        ``parallel.sparse_exchange.OwnerSparseExchange`` — sends them to the rows' owners)."""
+        ``parallel.sparse_exchange.OwnerSparseExchange`` — sends them to the rows' owners).
+        ``merge``: always pass the rows through the segment sum, as the synchronised paths
+        do (bitwise the same rows, signed zeros included, for single-process references)."""
         if not self.sparse_grads:
             return 0
         several = len(self.sparse_grads) > 1
@@ -216,7 +218,7 @@ class SparseEmbedding(torch.nn.Module):
         # merge duplicate rows (several lookups, several ranks) with the deterministic
         # segment sum so every replica applies bit-identical updates (one lookup on one
         # rank is already unique); static shapes keep the step free of host syncs
-        if several or sync is not None:
+        if several or sync is not None or merge:
             uids, rows = segment_sum(uids, rows, self.table.shape[0], static=True)
         sparse_adagrad(self.table.data, self.accum, uids.to(torch.int32).contiguous(), rows.contiguous(), lr)
         return int(uids.numel())

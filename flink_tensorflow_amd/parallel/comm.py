@@ -462,6 +462,9 @@ class GradBucketer:
                  comm: Communicator | None = None):
         self.params = [p for p in params if p.requires_grad]
         self.average = average
+        # deferred: hooks only count; synchronize() launches every bucket in index order (an
+        # agreed step where a rank without records has no backward, runtime/lockstep.py)
+        self.deferred = False
         self.comm = comm or _COMM
         self.buckets: list[list[torch.nn.Parameter]] = []
         cur, cur_bytes = [], 0
@@ -490,7 +493,7 @@ class GradBucketer:
     def _on_grad(self, p):
         i = self._bucket_of[id(p)]
         self._ready[i] += 1
-        if self._ready[i] == len(self.buckets[i]):
+        if self._ready[i] == len(self.buckets[i]) and not self.deferred:
             self._launch(i)
 
     def _launch(self, i):

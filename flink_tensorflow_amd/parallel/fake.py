@@ -120,7 +120,8 @@ class FakeCommunicator(Communicator):
         parts = []
         for r, b in enumerate(got):
             o = np.frombuffer(b[:nmeta], np.int64)
-            flat = torch.from_numpy(np.frombuffer(b[nmeta:], np.uint8).copy()).view(host.dtype)
+            raw = np.frombuffer(b[nmeta:], np.uint8).copy()
+            flat = torch.from_numpy(raw).view(host.dtype) if raw.size else torch.empty(0, dtype=host.dtype)
             part = flat[o[self.rank] * row:o[self.rank + 1] * row]
             if part.numel() != out_splits[r] * row:
                 raise ValueError(f"all_to_all_v: rank {r} sends {part.numel() // max(row, 1)} rows, expected "

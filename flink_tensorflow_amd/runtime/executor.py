@@ -75,6 +75,12 @@ class Partitioner:
             import random
 
             return [random.randrange(n)]
+        if k == "custom":  # key_selector = (partition(key, n) -> channel, key selector)
+            fn, ks = self.key_selector
+            c = int(fn(ks(rec.value), n))
+            if not 0 <= c < n:
+                raise ValueError(f"custom partitioner returned {c} for {n} channels")
+            return [c]
         raise ValueError(k)
 
     def clone(self):

@@ -133,6 +133,17 @@ class ProcessFunction(RichFunction):
     def on_timer(self, timestamp: float, ctx: ProcessContext, out: Collector) -> None:  # noqa: B027
         pass
 
+    # lifecycle hooks (extensions: an operator whose subtasks must act together — the
+    # collective trainer of runtime/lockstep.py — needs to act at these points too)
+    def on_start(self, ctx: ProcessContext, out: Collector) -> None:  # noqa: B027
+        """After ``open``, before the first element (timers may be registered here)."""
+
+    def on_barrier(self, ctx: ProcessContext, out: Collector) -> None:  # noqa: B027
+        """A checkpoint barrier is aligned: called right before the snapshot."""
+
+    def on_end_of_input(self, ctx: ProcessContext, out: Collector) -> None:  # noqa: B027
+        """Every input is exhausted (after the final event-time timers fired)."""
+
 
 KeyedProcessFunction = ProcessFunction
 
@@ -148,6 +159,17 @@ class CoProcessFunction(RichFunction):
 
     def on_timer(self, timestamp: float, ctx: ProcessContext, out: Collector) -> None:  # noqa: B027
         pass
+
+    # lifecycle hooks (extensions: an operator whose subtasks must act together — the
+    # collective trainer of runtime/lockstep.py — needs to act at these points too)
+    def on_start(self, ctx: ProcessContext, out: Collector) -> None:  # noqa: B027
+        """After ``open``, before the first element (timers may be registered here)."""
+
+    def on_barrier(self, ctx: ProcessContext, out: Collector) -> None:  # noqa: B027
+        """A checkpoint barrier is aligned: called right before the snapshot."""
+
+    def on_end_of_input(self, ctx: ProcessContext, out: Collector) -> None:  # noqa: B027
+        """Every input is exhausted (after the final event-time timers fired)."""
 
 
 @dataclass(frozen=True)

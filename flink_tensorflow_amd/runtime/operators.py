@@ -280,8 +280,21 @@ class ProcessOperator(Operator):
     def next_deadline(self):
         return self.timer_service.proc[0][0] if self.timer_service.proc else None
 
+    def _hook(self, name):
+        f = getattr(self.fn, name, None)
+        if f is not None:
+            f(self._pctx, self._col)
+
+    def open(self):
+        super().open()
+        self._hook("on_start")
+
+    def prepare_snapshot(self):
+        self._hook("on_barrier")
+
     def end_input(self):
         self._fire(self.timer_service.event, float("inf"))
+        self._hook("on_end_of_input")
 
     def snapshot_extra(self):
         return {"timers": self.timer_service.snapshot()}

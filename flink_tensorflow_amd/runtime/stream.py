@@ -253,8 +253,8 @@ class DataStream:
         return self
 
     # ---- partitioning
-    def _repartition(self, kind: str) -> "DataStream":
-        ds = self._add(kind, lambda: UnionOperator(None, kind), partitioner=Partitioner(kind))
+    def _repartition(self, kind: str, arg=None) -> "DataStream":
+        ds = self._add(kind, lambda: UnionOperator(None, kind), partitioner=Partitioner(kind, arg))
         ds.node.passthrough = kind  # a pass-through node that only repartitions
         return ds
 
@@ -266,6 +266,13 @@ class DataStream:
 
     def shuffle(self):
         return self._repartition("shuffle")
+
+    def partition_custom(self, partitioner: Callable[[Any, int], int], key_selector: Callable) -> "DataStream":
+        """``DataStream.partitionCustom(partitioner, keySelector)``: each record goes to
+        channel ``partitioner(key_selector(record), num_channels)``."""
+        return self._repartition("custom", (partitioner, key_selector))
+
+    partitionCustom = partition_custom
 
     def global_(self):
         return self._repartition("global")

@@ -1,0 +1,215 @@
+"""Collective online training over uneven streams (``parallel/step_agreement.py``,
+``runtime/lockstep.py``): P = 2 worker-process ranks of one Wide&Deep trainer fed 5 : 3,
+with a rebalance remainder, across checkpoints and a restart — no hang, and both replicas
+bit-identical to a 1-rank reference trained on the same pieces in the same step order
+(``WideDeepTrainer.train_pieces``)."""
+import hashlib
+
+import pytest
+import torch
+
+from flink_tensorflow_amd.parallel.step_agreement import RoundPlan, StepAgreement
+from flink_tensorflow_amd.runtime import RestartStrategy, StreamExecutionEnvironment
+from flink_tensorflow_amd.runtime.lockstep import LockstepTrainer
+from flink_tensorflow_amd.runtime.sources import CollectionSource
+
+BATCH = 64
+
+
+def _digest(model, exchange=None) -> str:
+    parts = [p.detach().reshape(-1).float() for p in model.dense_parameters()]
+    for e in (model.emb, model.wide):
+        for t in (e.table.data, e.accum):
+            parts.append((exchange.merge_owner_shards(t) if exchange is not None else t).reshape(-1).float())
+    return hashlib.sha256(torch.cat([p.cpu() for p in parts]).numpy().tobytes()).hexdigest()[:16]
+
+
+class _Logged(LockstepTrainer):
+    """Emits every step's piece (record ids) and, once all ranks finished, a digest of the
+    replica (a collective: safe in ``on_finished``)."""
+
+    def __init__(self, batch=BATCH, max_delay_ms=15.0, device="cpu"):
+        from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, WideDeepTrainer
+
+        super().__init__(WideDeepTrainer(WideDeepConfig.tiny(), device=device, seed=3), batch, max_delay_ms)
+
+    def on_step(self, plan, piece, loss, out):
+        out.collect(("piece", self.get_runtime_context().attempt, self.steps, self.rank, [r[4] for r in piece],
+                     plan.counts))
+
+    def on_finished(self, out):
+        out.collect(("digest", self.rank, self.steps, _digest(self.model.model, self.model._exchange)))
+
+
+def _records(n, seed=11):
+    from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, synthetic_click_records
+
+    recs = synthetic_click_records(n, WideDeepConfig.tiny(), seed=seed)
+    return [tuple(r) + (i,) for i, r in enumerate(recs)]
+
+
+def _reference(recs, pieces_by_step) -> str:
+    """1-rank reference: the same pieces, same step order, one process, no communicator."""
+    from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, WideDeepTrainer
+
+    t = WideDeepTrainer(WideDeepConfig.tiny(), device="cpu", seed=3)
+    t.open()
+    for s in sorted(pieces_by_step):
+        ranks = pieces_by_step[s]
+        t.train_pieces([[recs[i] for i in ranks.get(r, [])] for r in range(2)])
+    return _digest(t.model)
+
+
+def _run(recs, partition, checkpoint_dir=None, fail_after=None, device="cpu"):
+    from flink_tensorflow_amd.parallel.fake import FakeCommunicator
+
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    env.enable_job_communicator(True, communicator=FakeCommunicator)
+    if checkpoint_dir is not None:
+        env.enable_checkpointing(0.05, checkpoint_dir)
+        env.set_restart_strategy(RestartStrategy.fixed_delay(2, 0.0))
+    clicks = env.add_source(CollectionSource(recs, delay_s=0.0005), "clicks", parallelism=1)
+    if fail_after is not None:
+        from flink_tensorflow_amd.utils.fault import FailAfter
+
+        clicks = clicks.map(FailAfter(fail_after, attempts=(0,))).name("fault").set_parallelism(1)
+    clicks = partition(clicks)
+    ticks = env.add_source(CollectionSource([]), "control", parallelism=1)
+    sink = clicks.connect(ticks).process(_Logged(device=device)).name("trainer").run_in_processes().collect_into()
+    res = env.execute("lockstep")
+    return res, sink.results()
+
+
+def _check(recs, out, final_attempt=0):
+    digests = [o for o in out if o[0] == "digest"]
+    assert sorted(d[1] for d in digests) == [0, 1], digests
+    assert digests[0][2] == digests[1][2] and digests[0][3] == digests[1][3]  # replicas bit-identical
+    pieces = [o for o in out if o[0] == "piece"]
+    final = [p for p in pieces if p[1] == final_attempt]
+    first_final = min(p[2] for p in final)
+    by_step: dict = {}
+    for _, att, step, rank, ids, counts in pieces:
+        if (att == final_attempt and step >= first_final) or (att < final_attempt and step < first_final):
+            by_step.setdefault(step, {})[rank] = ids
+    assert sorted(by_step) == list(range(1, digests[0][2] + 1))  # every step accounted for, once
+    trained = sorted(i for s in by_step.values() for ids in s.values() for i in ids)
+    assert trained == list(range(len(recs)))  # every record trained exactly once
+    assert _reference(recs, by_step) == digests[0][3]
+    return by_step
+
+
+def test_step_agreement_plan_local():
+    a = StepAgreement()
+    p = a.round(5, ended=False, barrier=-1)
+    assert p == RoundPlan((5,), (False,), (-1,), (0,), 0) and p.step and not p.finished
+    assert a.round(0, ended=True).finished
+    assert RoundPlan((0, 0), (True, False), (3, 3), (0, 0)).snapshot_barrier == 3
+    assert RoundPlan((0, 0), (False, False), (3, -1), (0, 0)).snapshot_barrier is None
+
+
+def test_uneven_5_to_3_split_matches_one_rank_reference():
+    """Rank 0 gets 5 micro-batches' worth of records, rank 1 gets 3 (custom partitioner):
+    the ranks agree on every step (rank 1 joins the last ones with empty pieces), the job
+    ends without a hang, both replicas are bit-identical to each other and to the 1-rank
+    reference trained on the same pieces in the same order."""
+    recs = _records(8 * BATCH)
+    res, out = _run(recs, lambda s: s.partition_custom(lambda k, n: k, lambda r: 0 if r[4] % 8 < 5 else 1))
+    by_step = _check(recs, out)
+    per_rank = [sum(len(s.get(r, [])) for s in by_step.values()) for r in range(2)]
+    assert per_rank == [5 * BATCH, 3 * BATCH]
+    assert any(len(s.get(1, [])) == 0 for s in by_step.values())  # rank 1 stepped with an empty piece
+
+
+def test_rebalance_remainder_matches_one_rank_reference():
+    """A record count that is not a multiple of P x batch: the remainders are trained in
+    agreed partial steps at end of input."""
+    recs = _records(4 * BATCH + 37)
+    res, out = _run(recs, lambda s: s.rebalance())
+    by_step = _check(recs, out)
+    assert any(sum(len(v) for v in s.values()) < 2 * BATCH for s in by_step.values())
+
+
+def test_checkpoint_and_restart_stay_in_lockstep(tmp_path):
+    """Checkpoints every 50 ms snapshot both ranks after the same agreed step (collective-
+    free, owner shards); a failure restarts the job from the last one and the result is
+    still bit-identical to the reference over (pre-checkpoint pieces + replayed pieces)."""
+    import os
+
+    recs = _records(6 * BATCH + 11)
+    res, out = _run(recs, lambda s: s.partition_custom(lambda k, n: k, lambda r: 0 if r[4] % 8 < 5 else 1),
+                    str(tmp_path / "chk"), fail_after=4 * BATCH)
+    assert res.attempts == 1 and res.checkpoints, res
+    _check(recs, out, final_attempt=1)
+    # the trainer's checkpoints: rank 0's dense state + one owner shard per rank
+    dirs = [os.path.join(str(tmp_path / "chk"), f"chk-{c}", "models", "widedeep-0") for c in res.checkpoints]
+    dirs = [d for d in dirs if os.path.isdir(d)]
+    assert dirs
+    for d in dirs:
+        files = sorted(os.listdir(d))
+        assert "variables.index" in files and "shard-0-of-2.index" in files and "shard-1-of-2.index" in files
+
+
+class _Eval(_Logged):
+    def __init__(self, heldout):
+        super().__init__()
+        self.eval_records = heldout
+
+    def on_eval(self, probs, out):
+        out.collect(("eval", self.steps, self.rank, list(probs)))
+
+
+def test_eval_requests_are_served_in_agreed_rounds():
+    """``predict`` is collective-free; an eval command reaching one rank refreshes its
+    rows from their owners in an agreed round (the peers take part with none).  Every eval
+    scores exactly what the 1-rank reference predicts after the same number of steps."""
+    from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, WideDeepTrainer
+    from flink_tensorflow_amd.parallel.fake import FakeCommunicator
+
+    recs = _records(6 * BATCH)
+    heldout = _records(32, seed=99)
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    env.enable_job_communicator(True, communicator=FakeCommunicator)
+    clicks = env.add_source(CollectionSource(recs, delay_s=0.002), "clicks", parallelism=1).rebalance()
+    ticks = env.add_source(CollectionSource(["eval"] * 4, delay_s=0.1), "control", parallelism=1)
+    sink = clicks.connect(ticks).process(_Eval(heldout)).name("trainer").run_in_processes().collect_into()
+    env.execute("lockstep-eval")
+    out = sink.results()
+    evals = [o for o in out if o[0] == "eval"]
+    assert len(evals) >= 4  # (the control stream may reach both ranks)
+    by_step = _check(recs, out)
+    t = WideDeepTrainer(WideDeepConfig.tiny(), device="cpu", seed=3)
+    t.open()
+    done = 0
+    for _, steps, rank, probs in sorted(evals, key=lambda e: e[1]):
+        while done < steps:
+            done += 1
+            t.train_pieces([[recs[i] for i in by_step[done].get(r, [])] for r in range(2)])
+        assert t.predict(heldout) == probs, (steps, rank)
+
+
+@pytest.mark.gpu
+def test_fused_agreed_step_gpu():
+    """The fused GPU step under the agreement: ``counts=[B]`` is bitwise the plain step
+    (the loss normaliser is the batch), and two ranks sharing the GPU (loopback
+    communicator) fed 5 : 3 — one of them stepping with empty pieces (``empty_step``) —
+    finish without a hang with bit-identical replicas."""
+    from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, WideDeepTrainer
+
+    recs = _records(8 * BATCH)
+    a = WideDeepTrainer(WideDeepConfig.tiny(), device="cuda", seed=3)
+    b = WideDeepTrainer(WideDeepConfig.tiny(), device="cuda", seed=3)
+    a.open()
+    b.open()
+    assert a._fused is not None
+    for i in range(3):
+        piece = recs[i * BATCH:(i + 1) * BATCH]
+        la, lb = a.train_step(piece), b.train_step(piece, counts=[BATCH])
+        assert float(la) == float(lb)
+    assert _digest(a.model) == _digest(b.model)
+    res, out = _run(recs, lambda s: s.partition_custom(lambda k, n: k, lambda r: 0 if r[4] % 8 < 5 else 1),
+                    device=None)
+    digests = [o for o in out if o[0] == "digest"]
+    assert sorted(d[1] for d in digests) == [0, 1] and digests[0][2:] == digests[1][2:], digests
+    pieces = [o for o in out if o[0] == "piece"]
+    assert any(len(p[4]) == 0 for p in pieces if p[3] == 1)  # rank 1 ran empty steps
+    assert sorted(i for p in pieces for i in p[4]) == list(range(len(recs)))
