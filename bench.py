@@ -141,11 +141,19 @@ def main():
     ap.add_argument("--timeline", action="store_true",
                     help="also print, per timed batch, its lane and the GPU times of its first H2D piece, first "
                          "kernel and completion relative to the start of the timed window (diagnostics)")
+    ap.add_argument("--job", action="store_true",
+                    help="JOB MODE (resnet50): ONE DataStream job with --gpus worker-process subtasks, one GPU "
+                         "each — a source chained into each subtask's worker, the ResNet-50 operator with "
+                         "distributed_weights (rank 0 compiles, weights broadcast over the operator's RCCL "
+                         "group) — timed on the operator (batching/timed.py).  Run as ONE process (not under "
+                         "torch.distributed.run): the job starts its own workers")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, rendezvous, exchange one object per rank and print the world the "
                          "communicator sees (no model; with --rehearse-fake-comm it runs on a CPU-only box)")
     args = ap.parse_args()
 
+    if args.job:
+        return run_job(args)
     rc = self_launch(args)
     if rc is not None:
         raise SystemExit(rc)
@@ -414,6 +422,83 @@ def main():
         if runner.timeline is not None:
             print(json.dumps({"timeline": runner.timeline, "elapsed_ms": round(elapsed * 1e3, 3)}), flush=True)
     comm.destroy()
+
+
+def run_job(args):
+    """``--job``: the headline config as the framework's own job model.
+    This process is the coordinator: it never touches HIP; each subtask's worker process
+    binds its GPU, joins the operator's communicator (RCCL), compiles (rank 0's weights
+    are broadcast), generates its synthetic records in place (source chained into the
+    worker: no record crosses a process boundary) and runs W + K micro-batches; the
+    operator times the K (barrier + synchronize on both sides) and the JSON line reports
+    the max elapsed over subtasks."""
+    import shutil
+    import tempfile
+
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1:
+        raise SystemExit("[bench] --job runs one coordinator process; do not launch it under torch.distributed.run")
+    if args.model != "resnet50":
+        raise SystemExit("[bench] --job: resnet50 only")
+    from flink_tensorflow_amd.utils.gpus import sysfs_gpu_count
+
+    if sysfs_gpu_count() < args.gpus:
+        raise SystemExit(f"[bench] --job --gpus {args.gpus} but {sysfs_gpu_count()} GPU(s) visible")
+    from flink_tensorflow_amd.batching.timed import TimedWindow
+    from flink_tensorflow_amd.models.zoo.image_classifier import ResNet50Model
+    from flink_tensorflow_amd.models.zoo.resnet import resnet50_flops_per_image
+    from flink_tensorflow_amd.runtime import StreamExecutionEnvironment
+    from flink_tensorflow_amd.runtime.sources import DiscardingSink
+
+    class JobResNet50(TimedWindow, ResNet50Model):
+        pass
+
+    B, W, K, P = args.batch, args.warmup, args.steps, args.gpus
+    HW = args.image_hw or 256
+    lanes = args.lanes or 2
+    pool_n = args.pool
+    out_dir = tempfile.mkdtemp(prefix="ftm-bench-job-")
+    t0 = time.perf_counter()
+    try:
+        env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(P)
+        env.enable_job_communicator(True)  # one RCCL group for the operator, P = 1 included
+
+        def images(idx, par, start):  # runs in the subtask's worker process
+            pool = np.random.default_rng(1234 + idx).integers(0, 256, size=(pool_n, HW, HW, 3), dtype=np.uint8)
+            for i in range(start, (W + K) * B):
+                yield pool[i % pool_n]
+
+        model = JobResNet50(image_hw=(HW, HW), buckets=(B,), distributed_weights=True, lanes=lanes,
+                            depth=args.depth).timed_window(W, K, out_dir)
+        src = env.generate(images).run_in_processes()
+        src.map_with_model_batched(model, None, max_batch=B, max_delay_ms=60_000.0, name="resnet50") \
+            .run_in_processes().add_sink(DiscardingSink()).run_in_processes()  # results stay in the worker
+        res = env.execute("bench-job")
+        wall = time.perf_counter() - t0
+        ranks = []
+        for r in range(P):
+            with open(os.path.join(out_dir, f"rank{r}.json")) as f:
+                ranks.append(json.load(f))
+    finally:
+        shutil.rmtree(out_dir, ignore_errors=True)
+    elapsed = max(r["elapsed_s"] for r in ranks)
+    n_rec = sum(r["records"] for r in ranks)
+    lat = np.concatenate([np.asarray(r["latencies_s"]) for r in ranks]) if ranks else np.zeros(1)
+    total = n_rec / elapsed
+    print(json.dumps({
+        "metric": METRIC, "value": round(total, 1), "unit": "records/s", "n_gpus": P, "steps": K, "warmup": W,
+        "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16",
+        "data": f"synthetic decoded uint8 {HW}x{HW}x3 images generated in each worker, random-init weights",
+        "config": {"model": "ResNet-50 v1.5", "global_batch": B * P, "seq_len": None, "parallelism": f"dp{P}",
+                   "micro_batch_per_gpu": B, "input_hw": 224, "batch_buckets": [B], "compute_lanes": lanes,
+                   "mode": "job: one DataStream job, P worker-process GPU subtasks, chained sources, "
+                           "distributed_weights over the operator's communicator"},
+        "p50_latency_ms": round(float(np.percentile(lat, 50)) * 1e3, 3) if lat.size else None,
+        "p99_latency_ms": round(float(np.percentile(lat, 99)) * 1e3, 3) if lat.size else None,
+        "per_rank_records_per_s": [round(r["records"] / r["elapsed_s"], 1) for r in ranks],
+        "communicator": ranks[0]["communicator"], "comm_world_size": ranks[0]["world"],
+        "model_tflops_per_s": round(resnet50_flops_per_image(224) * total / 1e12, 1),
+        "job_wall_s": round(wall, 2), "job_attempts": res.attempts}), flush=True)
 
 
 def run_offered(args, runner, records, B, rank, ws, dev, comm, MetricGroup, model_name, data, lanes, buckets):

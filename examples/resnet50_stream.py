@@ -1,12 +1,17 @@
 #!/usr/bin/env python3
 """ResNet-50 bf16 image-classification stream on the full DataStream runtime.
 
-    python examples/resnet50_stream.py [--records N] [--batch 256] [--delay-ms 5]
+    python examples/resnet50_stream.py [--records N] [--batch 256] [--delay-ms 5] [--parallelism P]
 
 synthetic decoded-image source → map_with_model_batched(ResNet50Model) → sink.  On a GPU
 the model is compiled per batch bucket and run by the pipelined pinned-H2D / hipGraph
 runner; prints throughput and the per-record latency histogram of the model operator.
 (``bench.py`` times the same engine step-by-step for the headline number.)
+
+``--parallelism P``: the reference's data parallelism (``env.setParallelism``,
+``inception.scala:22-23``) the MI355X way — P worker-process subtasks, one GPU each, every
+subtask's source chained into its worker, the model operator with ``distributed_weights``
+(subtask 0 compiles, its weights are broadcast over the operator's RCCL group).
 """
 import argparse
 import json
@@ -40,6 +45,9 @@ def main():
     ap.add_argument("--worker-source", action="store_true",
                     help="run the source inside the model's worker process too (a chained source: records are "
                          "produced where the GPU operator consumes them; implies --processes)")
+    ap.add_argument("--parallelism", type=int, default=1,
+                    help="P GPU subtasks in worker processes (implies --worker-source), one RCCL group, "
+                         "rank 0's weights broadcast")
     ap.add_argument("--no-chain", action="store_true",
                     help="disable operator chaining: the in-process source runs in its own thread and hands "
                          "records to the model thread through a queue")
@@ -53,7 +61,11 @@ def main():
             if k >= start:
                 yield pool[i % len(pool)]
 
-    env = StreamExecutionEnvironment.get_execution_environment()
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(a.parallelism)
+    dist = a.parallelism > 1
+    if dist:
+        a.worker_source = True
+        env.enable_job_communicator(True)
     if a.no_chain:
         env.disable_operator_chaining()
     if a.savedmodel:
@@ -64,9 +76,11 @@ def main():
 
         d = export_resnet50_saved_model(os.path.join(tempfile.mkdtemp(), "rn50"), image_hw=(a.hw, a.hw),
                                         depth=a.depth_layers)
-        model = SignatureBatchedModel(d, buckets=(a.batch,), output_keys=["classes", "scores"])
+        model = SignatureBatchedModel(d, buckets=(a.batch,), output_keys=["classes", "scores"],
+                                      distributed_weights=dist)
     else:
-        model = ResNet50Model(image_hw=(a.hw, a.hw), buckets=(a.batch,), depth_layers=a.depth_layers)
+        model = ResNet50Model(image_hw=(a.hw, a.hw), buckets=(a.batch,), depth_layers=a.depth_layers,
+                              distributed_weights=dist)
     src = env.generate(images)
     if a.worker_source:
         src = src.run_in_processes()
@@ -79,7 +93,7 @@ def main():
     el = time.time() - t0
     m = [v for k, v in res.metrics.items() if k.startswith("resnet50")][0]
     steady = sink.rate(0.2)  # steady state: skip the first fifth (compile, capture, pipeline fill)
-    print(json.dumps({"records": a.records, "savedmodel": a.savedmodel, "worker_process": a.processes or a.worker_source,
+    print(json.dumps({"records": a.records, "parallelism": a.parallelism, "savedmodel": a.savedmodel, "worker_process": a.processes or a.worker_source,
                       "worker_source": a.worker_source, "chained": not a.no_chain, "seconds": round(el, 3), "records_per_s": round(a.records / el, 1),
                       "steady_records_per_s": round(steady, 1) if steady else None,
                       "latency_s": m["histograms"].get("latency_s"), "batch": m["histograms"].get("batch_size")}))

@@ -1,0 +1,83 @@
+"""A timed window inside a streaming job: the benchmark contract (W untimed warm-up
+micro-batches, then exactly K timed ones bracketed by a barrier + device synchronize on
+both sides, elapsed = max over ranks) measured on the operator itself, so ``bench.py
+--job`` can time the real job shape — one DataStream job whose P worker-process subtasks
+each own a GPU, the source chained into them, the weights read once and broadcast over the
+operator's communicator — instead of P independent SPMD pipelines.
+
+``TimedWindow`` is a mixin for a ``BatchedGpuModel`` (``submit`` / ``poll`` / ``drain``):
+it counts ``submit`` calls (one per micro-batch), fences before the first timed batch and
+after the last one (drain the pipeline, synchronize, barrier on the operator's
+communicator, synchronize), keeps the per-record latencies of the timed batches and writes
+``{rank, elapsed_s, records, latencies}`` to ``<out_dir>/rank<r>.json`` at the second fence.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+
+import numpy as np
+
+
+class TimedWindow:
+    def timed_window(self, warmup: int, steps: int, out_dir: str):
+        self._tw = {"w": int(warmup), "k": int(steps), "dir": out_dir, "n": 0, "t0": None, "lat": [],
+                    "records": 0}
+        return self
+
+    def _fence(self) -> list:
+        import torch
+
+        from ..parallel import comm
+
+        done = super().drain()
+        dev = torch.cuda.current_device() if torch.cuda.is_available() else None
+        if dev is not None:
+            torch.cuda.synchronize(dev)
+        comm.barrier()
+        if dev is not None:
+            torch.cuda.synchronize(dev)
+        return done
+
+    def _keep(self, results: list) -> list:
+        tw = self._tw
+        if tw["t0"] is not None:
+            for _, _, lat in results:
+                tw["lat"].append(np.asarray(lat, np.float64).reshape(-1))
+        return results
+
+    def submit(self, records, ingest_ts, tags):
+        tw = self._tw
+        i = tw["n"]
+        tw["n"] += 1
+        out = []
+        if i == tw["w"]:
+            out += self._fence()  # warm-up results: not timed
+            tw["t0"] = time.perf_counter()
+        if tw["w"] <= i < tw["w"] + tw["k"]:
+            tw["records"] += len(records)
+        out += self._keep(super().submit(records, ingest_ts, tags))
+        if i == tw["w"] + tw["k"] - 1:
+            out += self._keep(self._fence())
+            elapsed = time.perf_counter() - tw["t0"]
+            self._write(elapsed)
+            tw["t0"] = None
+        return out
+
+    def poll(self):
+        return self._keep(super().poll())
+
+    def _write(self, elapsed: float) -> None:
+        from ..parallel import comm
+
+        tw = self._tw
+        rank = comm.rank_size()[0]
+        lat = np.concatenate(tw["lat"]) if tw["lat"] else np.zeros(0)
+        os.makedirs(tw["dir"], exist_ok=True)
+        tmp = os.path.join(tw["dir"], f".rank{rank}.json")
+        with open(tmp, "w") as f:
+            json.dump({"rank": rank, "world": comm.rank_size()[1], "elapsed_s": elapsed, "records": tw["records"],
+                       "latencies_s": lat.tolist(), "pid": os.getpid(),
+                       "communicator": type(comm.get()).__name__ if comm.is_dist() else None}, f)
+        os.replace(tmp, os.path.join(tw["dir"], f"rank{rank}.json"))

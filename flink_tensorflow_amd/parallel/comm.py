@@ -34,6 +34,8 @@ product path never selects it.
 from __future__ import annotations
 
 import abc
+import contextlib
+import contextvars
 import datetime
 import os
 import pickle
@@ -314,6 +316,27 @@ class RcclCommunicator(Communicator):
 
 
 _COMM: Communicator | None = None
+# one communicator per OPERATOR: a worker process running several grouped GPU operators
+# (a chain) binds each operator's group around that operator's calls (``bound``); the
+# process-wide ``_COMM`` (SPMD launch) is the fallback
+_BOUND: contextvars.ContextVar = contextvars.ContextVar("ftm_bound_comm", default=None)
+
+
+def _cur() -> "Communicator | None":
+    b = _BOUND.get()
+    return b if b is not None else _COMM
+
+
+@contextlib.contextmanager
+def bound(c: "Communicator | None"):
+    """Within the block (this thread), ``get()`` / ``is_dist()`` / the helpers below use
+    ``c``: the communicator of the operator whose calls the block runs
+    (``runtime/remote.py``: ``_GroupBound``)."""
+    tok = _BOUND.set(c)
+    try:
+        yield c
+    finally:
+        _BOUND.reset(tok)
 
 
 def init_distributed(communicator: type | None = None, timeout_s: int = 600, device=None) -> bool:
@@ -343,9 +366,10 @@ def set_communicator(c: Communicator | None) -> None:
 
 
 def get() -> Communicator:
-    if _COMM is None:
+    c = _cur()
+    if c is None:
         raise RuntimeError("no communicator: call init_distributed() under a launcher")
-    return _COMM
+    return c
 
 
 def destroy(abort: bool = False) -> None:
@@ -360,16 +384,18 @@ def destroy(abort: bool = False) -> None:
 def is_dist() -> bool:
     """True when a communicator is installed (a world-size-1 RCCL communicator counts: its
     collectives still run through RCCL, e.g. in the GPU tests)."""
-    return _COMM is not None
+    return _cur() is not None
 
 
 def rank_size() -> tuple[int, int]:
-    return (_COMM.rank, _COMM.size) if _COMM is not None else (0, 1)
+    c = _cur()
+    return (c.rank, c.size) if c is not None else (0, 1)
 
 
 def barrier():
-    if _COMM is not None:
-        _COMM.barrier()
+    c = _cur()
+    if c is not None:
+        c.barrier()
 
 
 def _bucket_plan(ts: Sequence[torch.Tensor], cap_elems: int):
@@ -393,7 +419,7 @@ def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0, comm: Commu
     Tensors of at least a quarter bucket that are contiguous are broadcast where they live
     (zero extra memory); the rest are packed into one reusable staging bucket per dtype of
     ``bucket_bytes``.  Each round's calls are issued in one RCCL group."""
-    c = comm or _COMM
+    c = comm or _cur()
     if c is None:
         return 0
     seen, by_dtype = set(), {}
@@ -433,15 +459,16 @@ def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0, comm: Commu
 def all_reduce_scalar(x: float, op: str = "sum", device=None) -> float:
     if not is_dist():
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=_COMM.device)
-    _COMM.all_reduce(t, op)
+    c = _cur()
+    t = torch.tensor([x], dtype=torch.float64, device=c.device)
+    c.all_reduce(t, op)
     return float(t.item())
 
 
 def all_gather_object(obj):
     if not is_dist():
         return [obj]
-    return _COMM.all_gather_object(obj)
+    return _cur().all_gather_object(obj)
 
 
 def all_gather_into_tensor(out: torch.Tensor, inp: torch.Tensor) -> None:
@@ -465,7 +492,7 @@ class GradBucketer:
         # deferred: hooks only count; synchronize() launches every bucket in index order (an
         # agreed step where a rank without records has no backward, runtime/lockstep.py)
         self.deferred = False
-        self.comm = comm or _COMM
+        self.comm = comm or _cur()
         self.buckets: list[list[torch.nn.Parameter]] = []
         cur, cur_bytes = [], 0
         for p in reversed(self.params):
@@ -562,10 +589,11 @@ def allgather_metrics(group) -> dict:
             o = len(cnames) + j * BucketHistogram.N
             vec[o:o + BucketHistogram.N] = histogram_buckets(group.histograms[n]).counts
     if is_dist():
-        t = torch.from_numpy(vec).to(_COMM.device)
-        _COMM.all_reduce(t)
+        c = _cur()
+        t = torch.from_numpy(vec).to(c.device)
+        c.all_reduce(t)
         vec = t.cpu().numpy()
-    out = {"world_size": _COMM.size if is_dist() else 1,
+    out = {"world_size": _cur().size if is_dist() else 1,
            "counters": {n: int(vec[i]) for i, n in enumerate(cnames)}, "histograms": {}}
     for j, n in enumerate(hnames):
         o = len(cnames) + j * BucketHistogram.N

@@ -347,9 +347,10 @@ class ShmChannel:
 
 # ------------------------------------------------------------------ worker side
 def _open_group(spec, device):
-    """Joins the operator's communicator (``LocalExecutor.operator_group``) and installs it
-    as this process's ``parallel.comm`` communicator: RCCL on the subtask's GPU, or the
-    test implementation the job injected."""
+    """Joins the operator's communicator (``LocalExecutor.operator_group``): RCCL on the
+    subtask's GPU, or the test implementation the job injected.  It is bound to THIS
+    operator's calls (``_GroupBound``), not installed process-wide: two grouped operators
+    chained in one worker each keep their own group."""
     g = spec.get("group")
     if not g:
         return None
@@ -367,20 +368,43 @@ def _open_group(spec, device):
         c = cloudpickle.loads(g["cls"])(spec["subtask"], g["size"], device or "cpu", store)
     else:
         c = comm.RcclCommunicator(spec["subtask"], g["size"], device, store)
-    comm.set_communicator(c)
     return c
 
 
 def _close_group(c, abort: bool) -> None:
     if c is None:
         return
-    from ..parallel import comm
-
     try:
-        comm.set_communicator(None)
         c.destroy(abort=abort)  # a failed subtask aborts: the restarted attempt builds a new group
     except Exception:  # noqa: BLE001
         pass
+
+
+class _GroupBound:
+    """An operator whose every call runs with its communicator bound
+    (``parallel.comm.bound``): ``comm.get()`` / ``is_dist()`` inside the operator — model
+    open, broadcasts, collective training steps, snapshots — see this operator's group,
+    whichever thread makes the call (task loop, chain timer)."""
+
+    _CALLS = ("setup", "initialize", "open", "close", "process", "process_watermark", "on_idle", "next_deadline",
+              "end_input", "prepare_snapshot", "snapshot_state", "notify_checkpoint_complete")
+
+    def __init__(self, op, group):
+        self.__dict__["_op"], self.__dict__["_group"] = op, group
+
+    def __getattr__(self, name):
+        a = getattr(self._op, name)
+        if name not in self._CALLS or self._group is None:
+            return a
+        from ..parallel import comm
+
+        def call(*args, **kw):
+            with comm.bound(self._group):
+                return a(*args, **kw)
+        return call
+
+    def __setattr__(self, name, value):
+        setattr(self._op, name, value)
 
 
 def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
@@ -437,7 +461,7 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
         ctx.global_index, ctx.global_parallelism = spec["global_index"], spec["global_parallelism"]
         ctx.worker_pid = os.getpid()
         group = _open_group(spec, device)
-        op = cloudpickle.loads(factory)()
+        op = _GroupBound(cloudpickle.loads(factory)(), group)
         op.setup(ctx, Output(emit, lambda tag, v: (flush(), out.send(("side", [(tag, v)]), alive=parent_alive))))
         op.initialize(restore, restore_dir)
         op.open()
@@ -555,7 +579,9 @@ def _run_source_chain(msg, inp, out, emit, flush, parent_alive):
                 raise TypeError(f"operators emit records and watermarks, not {type(elem).__name__}")
         return e
 
-    group = _open_group(gpu_spec, device) if gpu_spec is not None else None
+    # one communicator per grouped member, bound to that member's calls
+    groups = [_open_group(sp, device) if sp["gpu"] else None for sp in specs]
+    ops = [_GroupBound(o, g) for o, g in zip(ops, groups)]
     for i, (op, sp) in enumerate(zip(ops, specs)):
         mg = MetricGroup(f"{sp['name']}[{sp['subtask']}]")
         metrics.append(mg)
@@ -683,8 +709,9 @@ def _run_source_chain(msg, inp, out, emit, flush, parent_alive):
         for o in ops:
             o.close()
         ops = []
-        _close_group(group, abort=False)
-        group = None
+        for g in groups:
+            _close_group(g, abort=False)
+        groups = []
         metrics[0].inc("records_out", recs_out[0])
         out.send(("closed", [mg.snapshot() for mg in metrics]), alive=parent_alive)
     except _ChainCancelled:
@@ -695,7 +722,8 @@ def _run_source_chain(msg, inp, out, emit, flush, parent_alive):
                 o.close()
             except Exception:  # noqa: BLE001
                 pass
-        _close_group(group, abort=True)
+        for g in groups:
+            _close_group(g, abort=True)
 
 # ------------------------------------------------------------------ coordinator side
 def _job_group(job, node):

@@ -311,6 +311,14 @@ class CollectSink(MemorySink):
     """A MemorySink whose results are returned by ``DataStream.execute_and_collect``."""
 
 
+class DiscardingSink(SinkFunction):
+    """Flink's ``DiscardingSink``: drops every record (benchmarks; chained into a worker
+    process, results never leave it)."""
+
+    def invoke(self, value):
+        pass
+
+
 class ThroughputSink(SinkFunction):
     """Counts records and timestamps every ``every``-th one (process-wide registry keyed
     like ``MemorySink``): ``rate(skip_fraction)`` is the steady-state records/s after the

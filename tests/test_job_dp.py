@@ -184,3 +184,165 @@ def test_online_training_dp_inside_one_job(tmp_path):
     assert sorted(o[0] for o in out) == [(0, 2), (1, 2)]
     assert [o[1] for o in out] == [4, 4]
     assert out[0][2] == out[1][2]
+
+
+def _group_of(value, model):
+    from flink_tensorflow_amd.parallel import comm
+
+    return tuple(value) + ((os.getpid(), id(comm.get()), comm.rank_size()),)
+
+
+def test_two_grouped_operators_chained_in_one_worker_keep_their_own_groups(tmp_path, half_plus_two):
+    """A worker-process source chained with TWO ``distributed_weights`` model operators:
+    one worker process per subtask runs all three, and each model operator sees its own
+    communicator (one group per operator, bound around that operator's calls), both of
+    world size 2."""
+    from flink_tensorflow_amd.parallel.fake import FakeCommunicator
+
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    env.enable_job_communicator(True, communicator=FakeCommunicator)
+    marks = [tmp_path / "m1", tmp_path / "m2"]
+    for m in marks:
+        m.mkdir()
+    src = env.generate(lambda idx, par, start: ((idx, i) for i in range(start, 6))).run_in_processes()
+    a = src.map_with_model(_HalfPlusTwo(half_plus_two, str(marks[0])), _group_of, name="first").run_in_processes()
+    b = a.map_with_model(_HalfPlusTwo(half_plus_two, str(marks[1])), _group_of, name="second").run_in_processes()
+    out = b.execute_and_collect()
+    assert len(out) == 12
+    for rec in out:
+        (pid1, g1, rs1), (pid2, g2, rs2) = rec[-2], rec[-1]
+        assert pid1 == pid2 != os.getpid()  # chained into one worker process
+        assert g1 != g2  # two communicators in that process
+        assert rs1 == rs2 and rs1[1] == 2
+    assert {rec[-1][2][0] for rec in out} == {0, 1}
+    assert [len(os.listdir(m)) for m in marks] == [1, 1]  # each operator: one rank-0 bundle read
+
+
+class _RecordingCNN:
+    """A ``SignatureBatchedModel`` over a ResNet SavedModel whose loader marks the process
+    that reads the variables bundle."""
+
+    @staticmethod
+    def make(path, marks, distributed=True):
+        from flink_tensorflow_amd.models import SignatureBatchedModel
+
+        class M(SignatureBatchedModel):
+            @property
+            def loader(self):
+                return _RecordingLoader(path, marks)
+
+        return M(path, buckets=(8,), output_keys=["classes", "scores"], distributed_weights=distributed)
+
+
+def _cnn_batch(m, vals):
+    import hashlib
+
+    import numpy as np
+
+    from flink_tensorflow_amd.parallel import comm
+
+    vs = m.session().variables
+    h = hashlib.sha256()
+    for k in sorted(vs):
+        h.update(k.encode())
+        h.update(vs[k].detach().cpu().contiguous().numpy().tobytes())
+    rows = m.submit(vals, np.zeros(len(vals)), list(range(len(vals))))[0][0]
+    return [(os.getpid(), comm.rank_size(), h.hexdigest()[:16], int(r["classes"].reshape(-1)[0])) for r in rows]
+
+
+def test_p4_distributed_weights_cnn_operator_rehearsal(tmp_path):
+    """P = 4 rehearsal of the headline job shape on the host (loopback communicator): a
+    ResNet SavedModel served by ``SignatureBatchedModel(distributed_weights=True)`` in 4
+    worker processes, fed by a worker-process source chained into them.  Only rank 0 reads
+    the variables bundle; all four end with bit-identical weights and classify every
+    record the same way the 1-process model does."""
+    import numpy as np
+
+    from flink_tensorflow_amd.models import SignatureBatchedModel
+    from flink_tensorflow_amd.models.zoo.resnet import export_resnet50_saved_model
+    from flink_tensorflow_amd.parallel.fake import FakeCommunicator
+
+    d = export_resnet50_saved_model(str(tmp_path / "rn"), image_hw=(32, 32), depth=26, num_classes=16, seed=4)
+    marks = tmp_path / "marks"
+    marks.mkdir()
+    pool = np.random.default_rng(0).integers(0, 256, (16, 32, 32, 3), dtype=np.uint8)
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(4)
+    env.enable_job_communicator(True, communicator=FakeCommunicator)
+    src = env.generate(lambda idx, par, start: (pool[(idx + i * par) % 16] for i in range(start, 8))).run_in_processes()
+    out = src.map_with_model_batched(_RecordingCNN.make(d, str(marks)), _cnn_batch, max_batch=8, max_delay_ms=50,
+                                     name="resnet").run_in_processes().execute_and_collect()
+    assert len(out) == 32
+    assert {o[1] for o in out} == {(r, 4) for r in range(4)}
+    assert len({o[0] for o in out}) == 4 and os.getpid() not in {o[0] for o in out}
+    assert len({o[2] for o in out}) == 1  # bit-identical weights on every rank
+    assert len(os.listdir(marks)) == 1  # one bundle read (rank 0)
+    ref = SignatureBatchedModel(d, buckets=(8,), output_keys=["classes", "scores"], device="cpu")
+    ref.open()
+    cls = [int(r["classes"].reshape(-1)[0]) for r in ref.submit(list(pool), np.zeros(16), list(range(16)))[0][0]]
+    ref.close()
+    assert sorted(o[3] for o in out) == sorted(cls[(idx + i * 4) % 16] for idx in range(4) for i in range(8))
+
+
+def _timed_job(tmp_path, P, communicator=None, device_note=""):
+    import json
+
+    import numpy as np
+
+    from flink_tensorflow_amd.batching.timed import TimedWindow
+    from flink_tensorflow_amd.models.zoo.image_classifier import ResNet50Model
+    from flink_tensorflow_amd.runtime.sources import DiscardingSink
+
+    class TimedResNet(TimedWindow, ResNet50Model):
+        pass
+
+    W, K, B, HW = 1, 2, 4, 32
+    out_dir = str(tmp_path / "timed")
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(P)
+    env.enable_job_communicator(True, communicator=communicator)
+
+    def images(idx, par, start):
+        pool = np.random.default_rng(idx).integers(0, 256, (8, HW, HW, 3), dtype=np.uint8)
+        for i in range(start, (W + K) * B):
+            yield pool[i % 8]
+
+    model = TimedResNet(image_hw=(HW, HW), buckets=(B,), distributed_weights=True, depth_layers=26, lanes=1) \
+        .timed_window(W, K, out_dir)
+    env.generate(images).run_in_processes() \
+        .map_with_model_batched(model, None, max_batch=B, max_delay_ms=60_000.0, name="resnet").run_in_processes() \
+        .add_sink(DiscardingSink()).run_in_processes()
+    env.execute("timed-job")
+    ranks = []
+    for r in range(P):
+        with open(os.path.join(out_dir, f"rank{r}.json")) as f:
+            ranks.append(json.load(f))
+    return ranks, K * B
+
+
+def test_bench_job_shape_rehearsal_p2(tmp_path):
+    """The ``bench.py --job`` job shape on the host: 2 worker-process subtasks, each a
+    chained source + a ``distributed_weights`` ResNet operator timing its own window
+    (``batching/timed.py``): every rank writes its K-batch window, inside a 2-rank group."""
+    from flink_tensorflow_amd.parallel.fake import FakeCommunicator
+
+    ranks, per_rank = _timed_job(tmp_path, 2, FakeCommunicator)
+    assert [r["rank"] for r in ranks] == [0, 1] and {r["world"] for r in ranks} == {2}
+    assert all(r["records"] == per_rank and r["elapsed_s"] > 0 for r in ranks)
+    assert all(len(r["latencies_s"]) == per_rank for r in ranks)
+    assert len({r["pid"] for r in ranks}) == 2 and os.getpid() not in {r["pid"] for r in ranks}
+
+
+@pytest.mark.gpu
+def test_bench_job_mode_p1_through_rccl_gpu(tmp_path):
+    """``bench.py --job`` at P = 1: the operator's communicator is RCCL (world 1) and the
+    timed window covers exactly K micro-batches."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--job", "--steps", "4", "--warmup", "2",
+                        "--batch", "64"], capture_output=True, text=True, timeout=600, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["communicator"] == "RcclCommunicator" and out["comm_world_size"] == 1
+    assert out["n_gpus"] == 1 and out["steps"] == 4 and out["value"] > 0
