@@ -627,6 +627,9 @@ def run_widedeep(args, dev, rank, ws):
     elapsed = time.perf_counter() - t_start
     elapsed_max = comm.all_reduce_scalar(elapsed, "max", device=dev)
     total = ws * B * args.steps / elapsed_max
+    ex = tr._exchange
+    if ex is not None and hasattr(ex, "check"):
+        ex.check()  # no bucket of the fixed-capacity exchange overflowed in the timed steps
     if rank == 0:
         print(json.dumps({
             "metric": "records/sec (whole node), Wide&Deep online training (DP all-reduce)",
@@ -638,7 +641,9 @@ def run_widedeep(args, dev, rank, ws):
             "config": {"model": "Wide&Deep (26x100k x32 embeddings, MLP 1024-512-256)", "global_batch": B * ws,
                        "seq_len": None, "parallelism": f"dp{ws}", "micro_batch_per_gpu": B},
             "final_loss": round(float(loss), 4), "setup_s": round(compile_s, 2),
-            "hip_graph": tr._graph is not None}), flush=True)
+            "hip_graph": tr._graph is not None,
+            "sparse_exchange": type(ex).__name__ if ex is not None else ("allgather" if ws > 1 else None),
+            "bucket_capacities": {str(k): v for k, v in getattr(ex, "_caps", {}).items()} or None}), flush=True)
     tr.close()
     comm.destroy()
 

@@ -54,10 +54,13 @@ class EngineConfig:
     chain_min_hw: int = 5041
     chain_edge: bool = True            # ... plus the layers leaving that resolution (stride-2 readers)
     wd_fused_step: bool = True         # Wide&Deep: hand-fused GPU step instead of autograd
-    # Wide&Deep under DP: "owner" = deduplicated rows to their owner rank (row % world),
-    # owner-side Adagrad, updated rows back (parallel/sparse_exchange.py); "allgather" = the
-    # padded all-gather of one row per lookup (sync-free: the DP step stays capturable)
-    wd_sparse_exchange: str = "owner"
+    # Wide&Deep under DP (parallel/sparse_exchange.py): "bucketed" = deduplicated rows to
+    # their owner rank (row % world) in fixed-capacity per-peer buckets, owner-side Adagrad,
+    # updated rows back — static shapes, no host sync: the DP step is captured in a hipGraph;
+    # "owner" = the same with exact per-step sizes (host-synced counts, not capturable);
+    # "allgather" = the padded all-gather of one row per lookup (capturable, most bytes)
+    wd_sparse_exchange: str = "bucketed"
+    wd_bucket_slack: float = 2.0       # bucket capacity = slack x (slots / world) + 64
     extra: dict = field(default_factory=dict)
 
     # ------------------------------------------------------------------ sources
@@ -142,6 +145,10 @@ class EngineConfig:
             raise ValueError("precision must be bf16 or fp8")
         if not 0 < self.arena_fraction <= 1:
             raise ValueError("arena_fraction must be in (0, 1]")
+        if self.wd_sparse_exchange not in ("bucketed", "owner", "allgather"):
+            raise ValueError("wd_sparse_exchange must be bucketed, owner or allgather")
+        if self.wd_bucket_slack <= 0:
+            raise ValueError("wd_bucket_slack must be positive")
         if self.batch_buckets and sorted(self.batch_buckets) != list(self.batch_buckets):
             self.batch_buckets = tuple(sorted(self.batch_buckets))
 

@@ -339,6 +339,34 @@ __global__ __launch_bounds__(256) void sparse_adagrad_kernel(float* __restrict__
   *reinterpret_cast<f32x4*>(table + row + c) = tv;
 }
 
+// Row moves of the bucketed owner exchange (parallel/sparse_exchange.py): slot k carries
+// table row ids[k] (ids outside [0, V) are padding).  gather: out[k] = table[ids[k]] (zeros
+// for padding); scatter: table[ids[k]] = rows[k] (padding skipped; ids are unique).  One
+// thread per 4 floats of a row.
+__global__ __launch_bounds__(256) void rows_gather_kernel(const float* __restrict__ table, const int* __restrict__ ids,
+                                                          float* __restrict__ out, long n, int D, int V, int gs) {
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  const long k = t >> gs;
+  if (k >= n) return;
+  const int c = (int)(t & ((1 << gs) - 1)) * 4;
+  const int id = ids[k];
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (id >= 0 && id < V) v = *reinterpret_cast<const f32x4*>(table + (size_t)id * D + c);
+  *reinterpret_cast<f32x4*>(out + k * D + c) = v;
+}
+
+__global__ __launch_bounds__(256) void rows_scatter_kernel(float* __restrict__ table, const int* __restrict__ ids,
+                                                           const float* __restrict__ rows, long n, int D, int V,
+                                                           int gs) {
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  const long k = t >> gs;
+  if (k >= n) return;
+  const int id = ids[k];
+  if (id < 0 || id >= V) return;
+  const int c = (int)(t & ((1 << gs) - 1)) * 4;
+  *reinterpret_cast<f32x4*>(table + (size_t)id * D + c) = *reinterpret_cast<const f32x4*>(rows + k * D + c);
+}
+
 }  // namespace
 
 // log2 of a power of two in [1, 64], or -1
@@ -472,7 +500,36 @@ void segment_starts(uintptr_t sorted, uintptr_t seg_id, uintptr_t seg, uintptr_t
   FTM_CHECK_LAUNCH();
 }
 
+static void rows_move(bool gather, uintptr_t table, uintptr_t ids, uintptr_t rows, long long n, int D, int V,
+                      uintptr_t stream) {
+  if (D % 4) throw std::invalid_argument("rows_gather/scatter: D % 4 != 0");
+  const int gs = pow2_shift(D / 4);
+  if (gs < 0) throw std::invalid_argument("rows_gather/scatter: D / 4 must be a power of two <= 64");
+  if (table % 16 || rows % 16) throw std::invalid_argument("rows_gather/scatter: 16-byte alignment required");
+  if (n <= 0) return;
+  const long long threads = n << gs;
+  auto s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  if (gather)
+    hipLaunchKernelGGL(rows_gather_kernel, grid, dim3(256), 0, s, reinterpret_cast<const float*>(table),
+                       reinterpret_cast<const int*>(ids), reinterpret_cast<float*>(rows), (long)n, D, V, gs);
+  else
+    hipLaunchKernelGGL(rows_scatter_kernel, grid, dim3(256), 0, s, reinterpret_cast<float*>(table),
+                       reinterpret_cast<const int*>(ids), reinterpret_cast<const float*>(rows), (long)n, D, V, gs);
+  FTM_CHECK_LAUNCH();
+}
+
+void rows_gather(uintptr_t table, uintptr_t ids, uintptr_t out, long long n, int D, int V, uintptr_t stream) {
+  rows_move(true, table, ids, out, n, D, V, stream);
+}
+
+void rows_scatter(uintptr_t table, uintptr_t ids, uintptr_t rows, long long n, int D, int V, uintptr_t stream) {
+  rows_move(false, table, ids, rows, n, D, V, stream);
+}
+
 void register_embedding(pybind11::module_& m) {
+  m.def("rows_gather", &rows_gather);
+  m.def("rows_scatter", &rows_scatter);
   m.def("segment_starts", &segment_starts);
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
   m.def("segment_sum_rows", &segment_sum_rows);

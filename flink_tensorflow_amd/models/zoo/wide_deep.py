@@ -169,10 +169,12 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         from ...config import current
 
         use_fused = self.fused if self.fused is not None else current().wd_fused_step
-        if comm.is_dist() and comm.get().size > 1 and current().wd_sparse_exchange == "owner":
-            from ...parallel.sparse_exchange import OwnerSparseExchange
+        mode = current().wd_sparse_exchange
+        if comm.is_dist() and comm.get().size > 1 and mode in ("owner", "bucketed"):
+            from ...parallel.sparse_exchange import BucketedOwnerExchange, OwnerSparseExchange
 
-            self._exchange = OwnerSparseExchange(comm.get())
+            self._exchange = (BucketedOwnerExchange(comm.get(), current().wd_bucket_slack) if mode == "bucketed"
+                              else OwnerSparseExchange(comm.get()))
         from .wide_deep_fused import FusedWideDeepStep
 
         if dev.type == "cuda" and use_fused and FusedWideDeepStep.supports(self.cfg):
@@ -225,7 +227,14 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
             n = int(batch[0].shape[0]) if batch is not None else len(records or ())
             if n:
                 batch = batch if batch is not None else self.collate(records)
-            return self._step(batch if n else None, norm=int(sum(counts)))
+            ex = self._exchange
+            if ex is not None and hasattr(ex, "exact"):
+                ex.exact = True  # pieces differ in size across ranks: exact, host-sized exchange
+            try:
+                return self._step(batch if n else None, norm=int(sum(counts)))
+            finally:
+                if ex is not None and hasattr(ex, "exact"):
+                    ex.exact = False
         batch = batch if batch is not None else self.collate(records)
         if self._graph is not None and all(a.shape == b.shape for a, b in zip(batch, self._static)):
             sp, bp = getattr(self._static, "packed", None), getattr(batch, "packed", None)
@@ -236,8 +245,15 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
                     dst.copy_(src, non_blocking=True)
             self._graph.replay()
             self.steps += 1
+            self._after_step()
             return self._static_loss
-        return self._step(batch)
+        loss = self._step(batch)
+        self._after_step()
+        return loss
+
+    def _after_step(self) -> None:
+        if self._exchange is not None and hasattr(self._exchange, "step_done"):
+            self._exchange.step_done()  # bucket overflow check, one step late and sync-free
 
     def capture(self, batch) -> None:
         """Captures one whole training step (forward, backward, fused Adam, sparse Adagrad
@@ -246,11 +262,12 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         sparse pipeline is static-shape and sync-free, which is what makes this possible.
         Under data parallelism the RCCL collectives are captured too: the bucketed dense
         all-reduce forks onto the communicator's stream and joins back through events, and
-        the row-sparse all-gathers run on the capturing stream, so one replay is one whole
-        DP step."""
+        the row-sparse exchange — the fixed-capacity owner buckets (``wd_sparse_exchange =
+        "bucketed"``, calibrated on the warm-up steps) or the padded all-gathers — runs on
+        the capturing stream, so one replay is one whole DP step."""
         dev = self._model.device
-        if self._exchange is not None:
-            return  # the owner exchange sizes its messages on the host: steps run uncaptured
+        if self._exchange is not None and not getattr(self._exchange, "capturable", False):
+            return  # the exact owner exchange sizes its messages on the host: steps run uncaptured
         packed = getattr(batch, "packed", None)
         if packed is not None:  # static copy of the packed buffer + the same views into it
             sp = packed.to(dev).clone()
@@ -263,6 +280,9 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
             with torch.cuda.stream(s):
                 for _ in range(2):  # warm-up (real steps): allocator pools, optimizer state
                     self._step(self._static)
+                if self._exchange is not None and hasattr(self._exchange, "calibrate"):
+                    self._exchange.calibrate()  # bucket capacities from the warm-up demand (one sync)
+                    self._step(self._static)    # ... and one step on the calibrated buckets
             torch.cuda.current_stream(dev).wait_stream(s)
             g = torch.cuda.CUDAGraph()
             with graph_capture(g):
@@ -388,6 +408,8 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         state) is authoritative: every rank writes the rows it owns (``row % world ==
         rank``) as its own shard file, and a restore assembles the tables from all shards.
         With ``runtime/lockstep.py`` the ranks snapshot after the same agreed step."""
+        if self._exchange is not None and hasattr(self._exchange, "check"):
+            self._exchange.check()  # a dropped bucket slot must never reach a checkpoint
         rank, ws = comm.rank_size()
         sharded = self._exchange is not None
         st, shard = {}, {}

@@ -135,6 +135,47 @@ def segment_sum(keys: torch.Tensor, rows: torch.Tensor, num_rows: int, L: int = 
     return uids.to(torch.int32), out
 
 
+def unique_static(keys: torch.Tensor, num_rows: int) -> torch.Tensor:
+    """The distinct keys in [0, num_rows) of ``keys``, one int32 slot per key (ascending,
+    -1 past the last): static shape and, on the GPU, the in-tree radix sort — no host
+    sync (a capturable replacement of ``torch.unique``)."""
+    flat = keys.reshape(-1)
+    if flat.is_cuda and flat.numel():
+        return group_keys(flat, num_rows)[3]
+    f = flat.long()
+    u = torch.unique(f[(f >= 0) & (f < num_rows)])
+    out = torch.full((flat.numel(),), -1, dtype=torch.int32, device=flat.device)
+    out[: u.numel()] = u.to(torch.int32)
+    return out
+
+
+def rows_gather(table: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    """fp32 [n, D]: ``table[ids[k]]`` per slot, zeros where ``ids[k]`` is outside the table."""
+    n, (V, D) = ids.numel(), table.shape
+    out = torch.empty((n, D), dtype=torch.float32, device=table.device)
+    if table.is_cuda:
+        ids = ids.reshape(-1).to(torch.int32).contiguous()
+        _hip().rows_gather(table.data_ptr(), ids.data_ptr(), out.data_ptr(), n, D, V, _stream())
+        return out
+    i = ids.reshape(-1).long()
+    ok = (i >= 0) & (i < V)
+    out.copy_(table[i.clamp(0, V - 1)] * ok.unsqueeze(-1))
+    return out
+
+
+def rows_scatter(table: torch.Tensor, ids: torch.Tensor, rows: torch.Tensor) -> None:
+    """``table[ids[k]] = rows[k]`` for the slots whose id lies in the table (ids unique)."""
+    n, (V, D) = ids.numel(), table.shape
+    if table.is_cuda:
+        ids = ids.reshape(-1).to(torch.int32).contiguous()
+        rows = rows.contiguous()
+        _hip().rows_scatter(table.data_ptr(), ids.data_ptr(), rows.data_ptr(), n, D, V, _stream())
+        return
+    i = ids.reshape(-1).long()
+    ok = (i >= 0) & (i < V)
+    table[i[ok]] = rows[ok].to(table.dtype)
+
+
 def embedding_bag_backward(ids: torch.Tensor, grad_out: torch.Tensor, num_rows: int, static: bool = False):
     """Row-sparse gradient of ``embedding_bag``: returns ``(uids int32 [U], rows fp32 [U, D])``."""
     return segment_sum(ids, grad_out, num_rows, ids.shape[1], static=static)

@@ -33,7 +33,7 @@ from dataclasses import dataclass
 
 import torch
 
-from ..ops.embedding import segment_sum, sparse_adagrad
+from ..ops.embedding import segment_sum, sparse_adagrad, unique_static
 
 
 @dataclass
@@ -153,3 +153,202 @@ class OwnerSparseExchange:
         bits = full.view(ity)
         self.comm.all_reduce(bits)
         return bits.view(full.dtype)
+
+
+class CapacityExceeded(RuntimeError):
+    """A bucketed exchange dropped rows: some owner's bucket needed more slots than its
+    capacity.  Raised at the next check, BEFORE the state is checkpointed, so the job
+    restarts from a checkpoint that never saw a dropped update."""
+
+
+class BucketedOwnerExchange(OwnerSparseExchange):
+    """The owner exchange with FIXED-CAPACITY per-peer buckets: static shapes end to end,
+    no host synchronisation, so a data-parallel step using it is captured in a hipGraph.
+
+    Every exchange sends each peer a bucket of ``cap`` slots (ids, -1 padding; rows for the
+    gradient direction) with one equal-split ``all_to_all`` — RCCL's grouped send/recv with
+    sizes fixed at capture time.  Ids are deduplicated with the in-tree radix sort
+    (``ops.embedding.unique_static`` / ``segment_sum``), a slot's position in its owner's
+    bucket is a prefix count over a one-hot of the owners (a [n, world] cumsum: stable, in
+    id order), rows move with the ``rows_gather`` / ``rows_scatter`` kernels.  Nothing calls
+    ``torch.unique`` / ``sort`` / ``bincount``; the owner-side merge is the same (id, source
+    rank) association as the exact exchange.
+
+    Capacity: before ``calibrate`` ``min(n, ceil(slack * n / world) + 64)`` for n candidate
+    slots (ids spread over owners by ``id % world``: a bucket holds about U / world ≤ n /
+    world distinct ids); ``calibrate`` (once, after the warm-up steps, before the capture)
+    sizes every call site at ``slack x`` the largest demand its steps showed, agreed across
+    ranks — Zipf click ids have far fewer distinct ids than lookups.
+    Slots beyond a bucket's capacity cannot travel: they are counted on the device
+    (``over``, the largest demand beyond capacity) and ``check()`` raises
+    ``CapacityExceeded`` — the trainer checks before every snapshot and every
+    ``check_every`` steps (one step late, from a pinned copy: no sync in the step), so a
+    dropped update never reaches a checkpoint and the restart replays it.
+
+    ``exact = True`` switches to the parent's exact, host-synced exchange (the agreed steps
+    of ``runtime/lockstep.py``, whose pieces differ in size across ranks)."""
+
+    capturable = True
+
+    def __init__(self, comm, slack: float = 2.0, check_every: int = 64):
+        super().__init__(comm)
+        self.slack = float(slack)
+        self.check_every = int(check_every)
+        self.exact = False
+        dev = comm.device
+        self.need = torch.zeros(1, dtype=torch.int64, device=dev)   # largest bucket demand seen (any site)
+        self.over = torch.zeros(1, dtype=torch.int64, device=dev)   # largest demand beyond capacity
+        self._site_need: dict = {}   # (rows, slots) -> device max demand of that call site
+        self._caps: dict = {}        # (rows, slots) -> calibrated per-peer capacity
+        self._pinned = None
+        self._pending = None
+        self._steps = 0
+
+    def capacity(self, n: int, rows: int | None = None) -> int:
+        """Per-peer slots for an exchange of ``n`` candidate ids of a ``rows``-row table:
+        calibrated (``calibrate``) or the a-priori ``slack x n / world + 64``."""
+        c = self._caps.get((rows, n))
+        if c is not None:
+            return c
+        ws = self.comm.size
+        return max(1, min(n, -(-int(self.slack * n) // ws) + 64))
+
+    def calibrate(self) -> dict:
+        """Sizes every call site's buckets from the demand its steps so far showed
+        (``slack x`` the largest, + 64, at most the slot count), agreed across ranks (max).
+        One host sync: the trainer calls it once, after its warm-up steps and before it
+        captures the step (``WideDeepTrainer.capture``)."""
+        keys = sorted(self._site_need, key=str)
+        if not keys:
+            return {}
+        d = torch.cat([self._site_need[k] for k in keys]).to(self.comm.device)
+        self.comm.all_reduce(d, "max")
+        ws = self.comm.size
+        for k, v in zip(keys, d.cpu().tolist()):
+            n = k[1]
+            self._caps[k] = max(1, min(n, int(self.slack * v) + 64, -(-int(self.slack * n) // ws) + 64))
+        return dict(self._caps)
+
+    # ---- overflow accounting
+    def check(self) -> None:
+        """Raises ``CapacityExceeded`` if any bucket overflowed so far (host sync)."""
+        over = int(self.over.item())
+        if over:
+            raise CapacityExceeded(f"owner bucket overflow: a bucket needed {over} slots beyond its capacity "
+                                   f"(slack {self.slack}); raise EngineConfig.wd_bucket_slack")
+
+    def step_done(self) -> None:
+        """Once per training step: every ``check_every`` steps the overflow counter is copied
+        to pinned memory without a sync, and the previous copy (long landed) is checked."""
+        self._steps += 1
+        if self.check_every <= 0 or self._steps % self.check_every:
+            return
+        if self._pending is not None:
+            ev, host = self._pending
+            ev.synchronize()
+            if int(host[0]):
+                raise CapacityExceeded(f"owner bucket overflow by {int(host[0])} slots (slack {self.slack})")
+        if self.over.is_cuda:
+            if self._pinned is None:
+                self._pinned = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+            self._pinned.copy_(self.over, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._pending = (ev, self._pinned)
+        else:
+            self._pending = (_Done(), self.over.clone())
+
+    # ---- buckets
+    def _bucket(self, ids: torch.Tensor, cap: int, site=None):
+        """``ids`` int32 [n] (distinct; -1 = none) -> (slot int64 [n]: position in the flat
+        [world * cap] send buffer, world * cap = not sent)."""
+        ws = self.comm.size
+        n = ids.numel()
+        dev = ids.device
+        valid = ids >= 0
+        owner = torch.where(valid, ids.remainder(ws), torch.full_like(ids, ws)).long()
+        onehot = (owner.unsqueeze(1) == torch.arange(ws, device=dev).unsqueeze(0)).to(torch.int32)
+        pos = onehot.cumsum(0).gather(1, owner.clamp(max=ws - 1).unsqueeze(1)).squeeze(1).long() - 1
+        fits = valid & (pos < cap)
+        demand = torch.where(valid, pos + 1, torch.zeros_like(pos))
+        if n:
+            top = demand.max().reshape(1)
+            torch.maximum(self.need, top, out=self.need)
+            if site is not None:
+                sn = self._site_need.get(site)
+                if sn is None:
+                    sn = self._site_need[site] = torch.zeros(1, dtype=torch.int64, device=dev)
+                torch.maximum(sn, top, out=sn)
+            torch.maximum(self.over, torch.where(fits, torch.zeros_like(demand), demand - cap).max().reshape(1),
+                          out=self.over)
+        return torch.where(fits, owner * cap + pos, torch.full_like(pos, ws * cap))
+
+    def _send_ids(self, ids, slot, cap):
+        ws = self.comm.size
+        buf = torch.full((ws * cap + 1,), -1, dtype=torch.int32, device=ids.device)
+        buf.scatter_(0, slot, ids.to(torch.int32))
+        buf[ws * cap] = -1
+        return buf[: ws * cap]
+
+    def _a2a(self, out, inp, cap):
+        ws = self.comm.size
+        self.comm.all_to_all_v(out, [cap] * ws, inp, [cap] * ws)
+
+    def pull_lookups(self, table: torch.Tensor, ids: torch.Tensor, offset: int = 0) -> ExchangeStats:
+        if self.exact:
+            return super().pull_lookups(table, ids, offset)
+        V = table.shape[0]
+        flat = ids.reshape(-1)
+        loc = torch.where((flat >= offset) & (flat < offset + V), flat - offset, torch.full_like(flat, -1))
+        return self.pull(table, unique_static(loc, V), 0)
+
+    def pull(self, table: torch.Tensor, uids: torch.Tensor, offset: int = 0) -> ExchangeStats:
+        if self.exact:
+            return super().pull(table, uids, offset)
+        from ..ops.embedding import rows_gather, rows_scatter
+
+        ws, me = self.comm.size, self.comm.rank
+        V, D = table.shape
+        u = uids.reshape(-1).to(torch.int64) - offset
+        ids = torch.where((uids.reshape(-1) >= 0) & (u >= 0) & (u < V), u, torch.full_like(u, -1)).to(torch.int32)
+        cap = self.capacity(ids.numel(), V)
+        slot = self._bucket(ids, cap, (V, ids.numel()))
+        ask = self._send_ids(ids, slot, cap)
+        asked = torch.empty_like(ask)
+        self._a2a(asked, ask, cap)            # ids each rank asks of me (rank-major buckets)
+        ans = rows_gather(table, asked)       # my authoritative rows (zeros for padding)
+        got = torch.empty_like(ans)
+        self._a2a(got, ans, cap)              # answers, aligned with my buckets
+        rows_scatter(table, ask, got)
+        row_b = D * table.element_size()
+        return self._add(ExchangeStats(sent=(ws - 1) * cap * (4 + row_b), received=(ws - 1) * cap * (4 + row_b)))
+
+    def apply(self, table: torch.Tensor, accum: torch.Tensor, uids: torch.Tensor, rows: torch.Tensor, lr: float,
+              eps: float = 1e-8, offset: int = 0) -> ExchangeStats:
+        if self.exact:
+            return super().apply(table, accum, uids, rows, lr, eps, offset)
+        ws = self.comm.size
+        V, D = table.shape
+        u = uids.reshape(-1).to(torch.int64) - offset
+        ids = torch.where((uids.reshape(-1) >= 0) & (u >= 0) & (u < V), u, torch.full_like(u, -1)).to(torch.int32)
+        cap = self.capacity(ids.numel(), V)
+        slot = self._bucket(ids, cap, (V, ids.numel()))
+        send_ids = self._send_ids(ids, slot, cap)
+        send_rows = torch.zeros((ws * cap + 1, D), dtype=torch.float32, device=rows.device)
+        send_rows.index_copy_(0, slot, rows.reshape(-1, D).float())
+        send_rows = send_rows[: ws * cap]
+        r_ids = torch.empty_like(send_ids)
+        r_g = torch.empty_like(send_rows)
+        with self.comm.group():
+            self._a2a(r_ids, send_ids, cap)
+            self._a2a(r_g, send_rows, cap)
+        # the owner's merged update: static segment sum in (id, source rank) order
+        own_u, own_g = segment_sum(r_ids, r_g, V, static=True)
+        sparse_adagrad(table, accum, own_u.to(torch.int32).contiguous(), own_g.contiguous(), lr, eps)
+        row_b = 4 + 4 * D
+        return self._add(ExchangeStats(sent=(ws - 1) * cap * row_b, received=(ws - 1) * cap * row_b))
+
+
+class _Done:
+    def synchronize(self):
+        pass

@@ -147,3 +147,43 @@ def test_widedeep_dp_step_captured_with_rccl(rccl_comm):
         torch.testing.assert_close(vb, va, rtol=1e-4, atol=1e-5, msg=k)
     a.close()
     b.close()
+
+
+def test_widedeep_bucketed_owner_step_captured_with_rccl(rccl_comm):
+    """The fused Wide&Deep DP step with the fixed-capacity owner exchange
+    (``BucketedOwnerExchange``: static unique ids from the in-tree radix sort, per-peer
+    buckets, equal-split RCCL all-to-alls, row gather / scatter kernels) is host-sync free:
+    it captures as ONE hipGraph (capacities calibrated on the warm-up steps), and replays
+    track the eager step with the same exchange.  World size 1: every row is owned here,
+    the all-to-alls run through RCCL with the values unchanged."""
+    from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, WideDeepTrainer, synthetic_click_records
+    from flink_tensorflow_amd.parallel.sparse_exchange import BucketedOwnerExchange
+
+    dev = rccl_comm.device
+    cfg = WideDeepConfig.tiny()
+    recs = synthetic_click_records(64 * 8, cfg, seed=6)
+    tr = []
+    for _ in range(2):
+        t = WideDeepTrainer(cfg, device=dev, seed=2)
+        t.open()
+        assert t._fused is not None
+        ex = BucketedOwnerExchange(rccl_comm)
+        t._exchange = t._fused.exchange = ex
+        tr.append(t)
+    a, b = tr
+    batches = [a.collate(recs[i * 64:(i + 1) * 64]) for i in range(8)]
+    for _ in range(3):  # b's capture runs 3 real steps (2 warm-up + 1 calibrated)
+        a.train_step(batch=batches[0])
+    a._exchange.calibrate()
+    b.capture(batches[0])
+    assert b._graph is not None  # a host sync inside the step would have failed the capture
+    la = [float(a.train_step(batch=bt)) for bt in batches[2:]]
+    lb = [float(b.train_step(batch=bt)) for bt in batches[2:]]
+    torch.testing.assert_close(torch.tensor(lb), torch.tensor(la), rtol=1e-4, atol=1e-5)
+    for (k, va), vb in zip(a.model.state_dict().items(), b.model.state_dict().values()):
+        torch.testing.assert_close(vb, va, rtol=1e-4, atol=1e-5, msg=k)
+    a._exchange.check()
+    b._exchange.check()
+    assert b._exchange.capacity(64 * cfg.num_fields, cfg.num_fields * cfg.vocab_per_field) <= 64 * cfg.num_fields
+    a.close()
+    b.close()

@@ -5,7 +5,10 @@
   dense parameters bit-identical to the padded all-gather exchange it replaces — and
   identical on every rank;
 * at the benchmark's shapes the bytes a rank receives per step fall from ~95 MB to the
-  deduplicated rows (printed; the verdict's bound is 15 MB)."""
+  deduplicated rows (printed; the verdict's bound is 15 MB);
+* the fixed-capacity bucketed exchange (static shapes, capturable) trains bit-identically
+  too, never overflows its buckets at the benchmark's ids, and still receives well under
+  the all-gather's bytes."""
 from _helpers import torchrun_smoke
 
 
@@ -15,7 +18,7 @@ def test_owner_exchange_matches_allgather_bit_for_bit_ws8():
     ref = out[0]["allgather"]
     for o in out:
         for k in ("emb", "wide", "emb_accum", "wide_accum", "dense"):
-            assert o["owner"][k] == o["allgather"][k] == ref[k], (o["rank"], k)
+            assert o["owner"][k] == o["bucketed"][k] == o["allgather"][k] == ref[k], (o["rank"], k)
         assert len(o["owner"]["received"]) == 3 and all(b > 0 for b in o["owner"]["received"])
 
 
@@ -28,7 +31,23 @@ def test_owner_exchange_bytes_at_benchmark_shapes_ws8():
         allg = b["emb"]["allgather_received"] + b["wide"]["allgather_received"]
         per_rank.append((owner, allg))
     worst = max(o for o, _ in per_rank)
+    bucketed = max(o["bytes"]["emb"]["bucketed_received"] + o["bytes"]["wide"]["bucketed_received"] for o in out)
+    for o in out:  # fixed-capacity buckets: no overflow at the benchmark's Zipf ids
+        for t in ("emb", "wide"):
+            assert o["bytes"][t]["bucket_demand"] <= o["bytes"][t]["bucket_capacity"]
+    print(f"[sparse exchange] bucketed (fixed capacity, capturable): {bucketed / 1e6:.2f} MB per rank per step")
+    assert bucketed * 2 < per_rank[0][1]
     print(f"\n[sparse exchange] DP=8, B=4096/rank: received per rank per step: owner {worst / 1e6:.2f} MB "
           f"(max over ranks; pull + push) vs padded all-gather {per_rank[0][1] / 1e6:.1f} MB")
     assert worst <= 15e6, per_rank
     assert all(o * 5 < a for o, a in per_rank)
+
+
+def test_bucket_overflow_is_reported_ws2():
+    """Buckets too small for the ids (all owned by rank 0, slack 0.5): the device-side
+    counter reports it through ``check`` and the sync-free periodic check — a dropped slot
+    raises before the trainer could checkpoint the state."""
+    out = torchrun_smoke(2, "--mode", "overflow", script="wd_exchange_check.py", timeout=300)
+    for o in out:
+        ov = o["overflow"]
+        assert ov["demand"] > ov["capacity"] and len(ov["raised"]) == 2, ov

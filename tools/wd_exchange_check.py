@@ -6,6 +6,9 @@ the padded all-gather it replaces — and prints checksums of both tables, the m
 Adagrad state and the dense parameters for both runs: they must agree bit for bit, on
 every rank.
 
+``--mode overflow``: a bucketed exchange whose buckets are too small reports it
+(``CapacityExceeded`` from ``check`` and from the delayed ``step_done`` check).
+
 ``--mode bytes``: the exchange alone at the benchmark's shapes (26 fields x 100k rows x 32,
 wide 1,000,003 x 8, micro-batch 4096 per rank, Zipf ids of ``synthetic_click_records``):
 prints the bytes this rank received in one step with each scheme.
@@ -25,7 +28,7 @@ def _digest(t) -> str:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["train", "bytes"], default="train")
+    ap.add_argument("--mode", choices=["train", "bytes", "overflow"], default="train")
     ap.add_argument("--steps", type=int, default=3)
     a = ap.parse_args()
     import torch
@@ -42,7 +45,7 @@ def main():
     if a.mode == "train":
         cfg = WideDeepConfig.tiny(hidden=(32, 16), embed_dim=8, vocab_per_field=64, wide_buckets=257)
         recs = synthetic_click_records(128 * a.steps, cfg, seed=100 + rank)
-        for mode in ("owner", "allgather"):
+        for mode in ("owner", "bucketed", "allgather"):
             C.set_current(C.EngineConfig(wd_sparse_exchange=mode))
             tr = WideDeepTrainer(cfg, device="cpu", seed=7 + rank, fused=False)
             tr.open()
@@ -62,18 +65,38 @@ def main():
                          "dense": _digest(torch.cat([p.detach().reshape(-1) for p in m.dense_parameters()])),
                          "received": recv}
             tr.close()
+    elif a.mode == "overflow":
+        # every id owned by rank 0 and a small slack: rank 0's bucket cannot hold them
+        from flink_tensorflow_amd.parallel.sparse_exchange import BucketedOwnerExchange, CapacityExceeded
+
+        bx = BucketedOwnerExchange(comm.get(), slack=0.5, check_every=1)
+        ids = torch.arange(0, 2000, 2, dtype=torch.int32)
+        table = torch.zeros(4000, 8)
+        accum = torch.full((4000, 8), 0.1)
+        bx.pull(table, ids)
+        bx.apply(table, accum, ids, torch.ones(ids.numel(), 8), 0.05)
+        bx.step_done()  # schedules the sync-free copy of the counter
+        raised = []
+        for fn in (bx.check, bx.step_done):
+            try:
+                fn()
+            except CapacityExceeded as e:
+                raised.append(str(e)[:60])
+        out["overflow"] = {"capacity": bx.capacity(ids.numel(), 4000), "demand": int(bx.need.item()),
+                           "raised": raised}
     else:
         cfg = WideDeepConfig()
         B = 4096
         recs = synthetic_click_records(B, cfg, seed=100 + rank)
         from flink_tensorflow_amd.ops.embedding import segment_sum
-        from flink_tensorflow_amd.parallel.sparse_exchange import OwnerSparseExchange
+        from flink_tensorflow_amd.parallel.sparse_exchange import BucketedOwnerExchange, OwnerSparseExchange
 
         cats = torch.tensor([r[2] for r in recs], dtype=torch.int64)
         cross = torch.tensor([r[3] for r in recs], dtype=torch.int64)
         ids = (cats + torch.arange(cfg.num_fields) * cfg.vocab_per_field).reshape(-1)
         FV = cfg.num_fields * cfg.vocab_per_field
         ex = OwnerSparseExchange(comm.get())
+        bx = BucketedOwnerExchange(comm.get())
         res = {}
         for name, V, D, keys in (("emb", FV, cfg.embed_dim, ids), ("wide", cfg.wide_buckets, 8, cross.reshape(-1))):
             g = torch.randn(keys.numel(), D)
@@ -84,8 +107,20 @@ def main():
             ex.pull(table, u)
             ex.apply(table, accum, u, r, 0.05)
             st = ex.stats
+            bx.begin_step()  # warm-up step: measures every site's demand
+            bx.pull(table, u)
+            bx.apply(table, accum, u, r, 0.05)
+            bx.calibrate()  # buckets sized from it (what the trainer does before capturing)
+            g2 = torch.randn(keys.numel(), D)
+            u2, r2 = segment_sum(keys.flip(0), g2, V, static=True)  # another step, same ids
+            bx.begin_step()
+            bx.pull(table, u2)
+            bx.apply(table, accum, u2, r2, 0.05)
+            bx.check()
             # the padded all-gather receives (ws - 1) x (one id + one row) per lookup
             res[name] = {"owner_received": st.received, "rows_out": st.rows_out, "lookups": int(keys.numel()),
+                         "bucketed_received": bx.stats.received, "bucket_capacity": bx.capacity(int(keys.numel()), V),
+                         "bucket_demand": int(bx._site_need[(V, int(keys.numel()))].item()),
                          "allgather_received": (ws - 1) * int(keys.numel()) * (4 + 4 * D)}
             _sparse_sync  # noqa: B018 - the scheme priced above
         out["bytes"] = res
