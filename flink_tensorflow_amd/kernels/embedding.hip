@@ -367,6 +367,59 @@ __global__ __launch_bounds__(256) void rows_scatter_kernel(float* __restrict__ t
   *reinterpret_cast<f32x4*>(table + (size_t)id * D + c) = *reinterpret_cast<const f32x4*>(rows + k * D + c);
 }
 
+// Fixed-capacity owner buckets of the bucketed exchange (parallel/sparse_exchange.py).
+// ids [n]: keys of a shared key space (-1 / outside [off, off + V) = none), distinct.  Block
+// o collects, in input order, the ids whose table-local id (id - off) is owned by rank o
+// (local % ws == o): slot o * cap + k gets the k-th one (send_ids: the local id, src: its
+// input position); slots past the count get -1.  A 1024-thread block scans the ids in
+// chunks: wave ballots + a 16-entry LDS prefix give each id its position.  need / over:
+// running maxima (global atomics) of the demand and of the demand beyond capacity.
+__global__ __launch_bounds__(1024) void owner_buckets_kernel(const int* __restrict__ ids, int n, int off, int V, int ws,
+                                                             int cap, int* __restrict__ send_ids,
+                                                             int* __restrict__ src, int* __restrict__ need,
+                                                             int* __restrict__ over) {
+  __shared__ int cnt[16];
+  const int o = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int run = 0;
+  for (int b0 = 0; b0 < n; b0 += 1024) {
+    const int i = b0 + t;
+    int loc = -1;
+    bool f = false;
+    if (i < n) {
+      const int id = ids[i];
+      loc = id - off;
+      f = id >= 0 && loc >= 0 && loc < V && (loc % ws) == o;
+    }
+    const unsigned long long m = __ballot(f);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) cnt[w] = __popcll(m);
+    __syncthreads();
+    int wbase = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int c = cnt[k];
+      wbase += k < w ? c : 0;
+      tot += c;
+    }
+    const int pos = run + wbase + before;
+    if (f && pos < cap) {
+      send_ids[(size_t)o * cap + pos] = loc;
+      src[(size_t)o * cap + pos] = i;
+    }
+    run += tot;
+    __syncthreads();
+  }
+  for (int p = (run < cap ? run : cap) + t; p < cap; p += 1024) {
+    send_ids[(size_t)o * cap + p] = -1;
+    src[(size_t)o * cap + p] = -1;
+  }
+  if (t == 0) {
+    atomicMax(need, run);
+    if (run > cap) atomicMax(over, run - cap);
+  }
+}
+
 }  // namespace
 
 // log2 of a power of two in [1, 64], or -1
@@ -527,7 +580,17 @@ void rows_scatter(uintptr_t table, uintptr_t ids, uintptr_t rows, long long n, i
   rows_move(false, table, ids, rows, n, D, V, stream);
 }
 
+void owner_buckets(uintptr_t ids, int n, int off, int V, int ws, int cap, uintptr_t send_ids, uintptr_t src,
+                   uintptr_t need, uintptr_t over, uintptr_t stream) {
+  if (ws < 1 || ws > 1024 || cap < 1) throw std::invalid_argument("owner_buckets: 1 <= ws <= 1024, cap >= 1");
+  hipLaunchKernelGGL(owner_buckets_kernel, dim3(ws), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const int*>(ids), n, off, V, ws, cap, reinterpret_cast<int*>(send_ids),
+                     reinterpret_cast<int*>(src), reinterpret_cast<int*>(need), reinterpret_cast<int*>(over));
+  FTM_CHECK_LAUNCH();
+}
+
 void register_embedding(pybind11::module_& m) {
+  m.def("owner_buckets", &owner_buckets);
   m.def("rows_gather", &rows_gather);
   m.def("rows_scatter", &rows_scatter);
   m.def("segment_starts", &segment_starts);

@@ -26,6 +26,27 @@ namespace {
 // packed record buffer.  keys [B*F + B*C]: the sparse-gradient grouping keys of BOTH
 // tables in one key space — embedding rows as is, wide rows offset by F*V, invalid ids of
 // either table -> F*V + WV (one dropped bucket) — so one radix sort groups both.
+// The lookup keys of a micro-batch in the shared key space (embedding rows, then the wide
+// table offset by F*V; F*V + WV = invalid) — exactly the keys wd_gather writes, but
+// available BEFORE the gather: the data-parallel owner exchange refreshes those rows first.
+__global__ __launch_bounds__(256) void wd_keys_kernel(const int* __restrict__ cats, int ldc, const int* __restrict__ cross,
+                                                      int ldx, int* __restrict__ keys, int B, int F, int V, int C,
+                                                      int WV) {
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  const long nemb = (long)B * F;
+  const int FV = F * V, BAD = FV + WV;
+  if (t < nemb) {
+    const int b = (int)(t / F), f = (int)(t - (long)b * F);
+    const int gid = cats[(size_t)b * ldc + f] + f * V;
+    keys[t] = (gid >= 0 && gid < FV) ? gid : BAD;
+  } else if (t < nemb + (long)B * C) {
+    const long r = t - nemb;
+    const int b = (int)(r / C), c = (int)(r - (long)b * C);
+    const int id = cross[(size_t)b * ldx + c];
+    keys[t] = (id >= 0 && id < WV) ? FV + id : BAD;
+  }
+}
+
 __global__ __launch_bounds__(256) void wd_gather_kernel(const int* __restrict__ cats, int ldc,
                                                         const float* __restrict__ dense, int ldd,
                                                         const int* __restrict__ cross, int ldx,
@@ -120,7 +141,7 @@ __global__ __launch_bounds__(256) void wd_loss_kernel(const bf16* __restrict__ h
 
 __global__ __launch_bounds__(64) void wd_loss_final_kernel(const float* __restrict__ part, int nb, float norm,
                                                            float* __restrict__ loss, float* __restrict__ g_wbias,
-                                                           float* __restrict__ g_hb0) {
+                                                           float* __restrict__ g_hb0, float* __restrict__ step) {
   float a = 0.f, s = 0.f;
   for (int i = threadIdx.x; i < nb; i += 64) {
     a += part[2 * i];
@@ -132,6 +153,7 @@ __global__ __launch_bounds__(64) void wd_loss_final_kernel(const float* __restri
     loss[0] = a / norm;
     g_wbias[0] = s;
     g_hb0[0] = s;
+    if (step) step[0] += 1.f;  // Adam's step count (read by wd_adam later on the stream)
   }
 }
 
@@ -287,12 +309,24 @@ void wd_gather(uintptr_t cats, int ldc, uintptr_t dense, int ldd, uintptr_t cros
   FTM_CHECK_LAUNCH();
 }
 
+void wd_keys(uintptr_t cats, int ldc, uintptr_t cross, int ldx, uintptr_t keys, int B, int F, int V, int C, int WV,
+             uintptr_t stream) {
+  const long n = (long)B * (F + C);
+  if (n <= 0) return;
+  hipLaunchKernelGGL(wd_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const int*>(cats), ldc,
+                     reinterpret_cast<const int*>(cross), ldx, reinterpret_cast<int*>(keys), B, F, V, C, WV);
+  FTM_CHECK_LAUNCH();
+}
+
 // part: >= 2 * ceil(B / 256) floats of workspace.  norm: the loss is sum / norm — B for the
 // batch mean; the global record count of an agreed data-parallel step over uneven pieces
 // (parallel/step_agreement.py), so the summed gradients are those of the union's mean.
+// step (optional, 0 = none): Adam's step counter, incremented here so the captured step has
+// no separate increment launch.
 void wd_loss(uintptr_t head, int ldh, uintptr_t wsum, uintptr_t wbias, uintptr_t labels, int ldl, int B, float norm,
              uintptr_t dlogit, uintptr_t dlogit16, uintptr_t loss, uintptr_t g_wbias, uintptr_t g_hb0, uintptr_t wgrad,
-             int C, int WD, uintptr_t part, uintptr_t stream) {
+             int C, int WD, uintptr_t part, uintptr_t step, uintptr_t stream) {
   if (B <= 0) throw std::invalid_argument("wd_loss: empty batch");
   if (!(norm > 0.f)) throw std::invalid_argument("wd_loss: norm must be positive");
   if (wgrad % 16) throw std::invalid_argument("wd_loss: wgrad must be 16-byte aligned");
@@ -304,7 +338,8 @@ void wd_loss(uintptr_t head, int ldh, uintptr_t wsum, uintptr_t wbias, uintptr_t
                      reinterpret_cast<bf16*>(dlogit16), reinterpret_cast<float*>(part), reinterpret_cast<float*>(wgrad),
                      C, WD);
   hipLaunchKernelGGL(wd_loss_final_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<const float*>(part), nb, norm,
-                     reinterpret_cast<float*>(loss), reinterpret_cast<float*>(g_wbias), reinterpret_cast<float*>(g_hb0));
+                     reinterpret_cast<float*>(loss), reinterpret_cast<float*>(g_wbias), reinterpret_cast<float*>(g_hb0),
+                     reinterpret_cast<float*>(step));
   FTM_CHECK_LAUNCH();
 }
 
@@ -354,6 +389,7 @@ void wd_mask_colsum(uintptr_t x, uintptr_t h, uintptr_t db, int B, int n, uintpt
 void register_widedeep(pybind11::module_& m) {
   m.def("wd_gather", &wd_gather);
   m.def("wd_loss", &wd_loss);
+  m.def("wd_keys", &wd_keys);
   m.def("wd_head_bwd", &wd_head_bwd);
   m.def("wd_head_bwd2", &wd_head_bwd2);
   m.def("wd_adam", &wd_adam);

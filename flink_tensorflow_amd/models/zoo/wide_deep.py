@@ -386,7 +386,15 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
             _, _, cats, cross = self.collate(records)
         else:
             _, _, cats, cross = self._empty_batch()
-        self.pull_rows(cats, cross)
+        ex = self._exchange
+        exact = getattr(ex, "exact", None)
+        if exact is not None:
+            ex.exact = True  # one rank asks, the others ask nothing: exact, host-sized exchange
+        try:
+            self.pull_rows(cats, cross)
+        finally:
+            if exact is not None:
+                ex.exact = exact
 
     @torch.no_grad()
     def predict(self, records) -> list[float]:

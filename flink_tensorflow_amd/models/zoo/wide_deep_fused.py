@@ -173,10 +173,14 @@ class FusedWideDeepStep:
             labels = labels.reshape(-1)
         dist = comm.is_dist()
         if dist and self.exchange is not None:  # fresh copies of the rows this batch reads
+            # the batch's keys in the shared key space (wd_keys: the ones wd_gather will
+            # read), deduplicated by the radix sort, refreshed from their owners per table
             self.exchange.begin_step()
-            offs = torch.arange(self.F, device=cats.device, dtype=torch.int64) * cfg.vocab_per_field
-            self.exchange.pull_lookups(m.emb.table.data, cats.to(torch.int64) + offs)
-            self.exchange.pull_lookups(m.wide.table.data, cross)
+            H.wd_keys(cats.data_ptr(), cats.stride(0), cross.data_ptr(), cross.stride(0), a.keys.data_ptr(), B, self.F,
+                      cfg.vocab_per_field, C, WV, s)
+            pu = group_keys(a.keys, m.emb.table.shape[0] + WV)[3]
+            self.exchange.pull(m.emb.table.data, pu, 0)
+            self.exchange.pull(m.wide.table.data, pu, m.emb.table.shape[0])
         # forward
         H.wd_gather(cats.data_ptr(), cats.stride(0), dense.data_ptr(), dense.stride(0), cross.data_ptr(),
                     cross.stride(0), m.emb.table.data_ptr(), m.wide.table.data_ptr(), a.x.data_ptr(), a.wsum.data_ptr(),
@@ -188,7 +192,8 @@ class FusedWideDeepStep:
         H.wd_loss(a.hd.data_ptr(), a.hd.shape[1], a.wsum.data_ptr(), m.wide_bias.data_ptr(),
                   labels.data_ptr(), labels.stride(0), B, float(norm if norm is not None else B), a.dlogit.data_ptr(),
                   a.dlogit16.data_ptr(), a.loss.data_ptr(),
-                  self.g["wide_bias"].data_ptr(), self.g["head.bias"].data_ptr(), a.wgrad.data_ptr(), C, WD, a.part.data_ptr(), s)
+                  self.g["wide_bias"].data_ptr(), self.g["head.bias"].data_ptr(), a.wgrad.data_ptr(), C, WD, a.part.data_ptr(),
+                  self.t.data_ptr(), s)  # also counts Adam's step
         # backward: head (only logit column 0 is used) -> dh, top bias and head weight gradients
         last = a.h[-1]
         Hl = last.shape[1]
@@ -244,8 +249,8 @@ class FusedWideDeepStep:
         return a.loss
 
     def _adam(self, scale: float, s) -> None:
-        """Dense Adam over the flat buffer + the bf16 operands of the next step."""
-        self.t.add_(1.0)
+        """Dense Adam over the flat buffer + the bf16 operands of the next step (the step
+        count ``t`` was advanced by ``wd_loss``, or by ``empty_step``)."""
         self._H.wd_adam(self.flat.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
                         self.flat.numel(), self.t.data_ptr(), self.lr, self.b1, self.b2, self.eps, scale,
                         self.seg.data_ptr(), self.seg.shape[1], s)
@@ -286,6 +291,7 @@ class FusedWideDeepStep:
                 sparse_adagrad(m.wide.table.data, m.wide.accum, uw, rw, self.lr_sparse, offset=FV)
             for w in works:
                 w.wait()
+        self.t.add_(1.0)
         self._adam(1.0, s)
         return torch.zeros((), dtype=torch.float32, device=dev)
 

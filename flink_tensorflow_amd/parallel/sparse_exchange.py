@@ -165,25 +165,26 @@ class BucketedOwnerExchange(OwnerSparseExchange):
     """The owner exchange with FIXED-CAPACITY per-peer buckets: static shapes end to end,
     no host synchronisation, so a data-parallel step using it is captured in a hipGraph.
 
-    Every exchange sends each peer a bucket of ``cap`` slots (ids, -1 padding; rows for the
-    gradient direction) with one equal-split ``all_to_all`` — RCCL's grouped send/recv with
-    sizes fixed at capture time.  Ids are deduplicated with the in-tree radix sort
-    (``ops.embedding.unique_static`` / ``segment_sum``), a slot's position in its owner's
-    bucket is a prefix count over a one-hot of the owners (a [n, world] cumsum: stable, in
-    id order), rows move with the ``rows_gather`` / ``rows_scatter`` kernels.  Nothing calls
-    ``torch.unique`` / ``sort`` / ``bincount``; the owner-side merge is the same (id, source
-    rank) association as the exact exchange.
+    Every exchange sends each peer a bucket of ``cap`` slots (table-local ids, -1 padding;
+    rows for the gradient direction) with one equal-split ``all_to_all`` — RCCL's grouped
+    send/recv with sizes fixed at capture time.  On the GPU every data movement is an
+    in-tree kernel: ids are deduplicated by the radix sort (``kernels/sort_segments.hip``),
+    ``owner_buckets`` (``kernels/embedding.hip``) places each id in its owner's bucket (one
+    1024-thread block per owner: wave ballots + an LDS prefix, input order kept), rows move
+    with ``rows_gather`` / ``rows_scatter`` and the owner merges with the static segment sum
+    in (id, source rank) order — no ``torch.unique`` / ``sort`` / ``bincount``, no fancy
+    indexing, and the merge association of the exact exchange.
 
     Capacity: before ``calibrate`` ``min(n, ceil(slack * n / world) + 64)`` for n candidate
     slots (ids spread over owners by ``id % world``: a bucket holds about U / world ≤ n /
     world distinct ids); ``calibrate`` (once, after the warm-up steps, before the capture)
     sizes every call site at ``slack x`` the largest demand its steps showed, agreed across
-    ranks — Zipf click ids have far fewer distinct ids than lookups.
-    Slots beyond a bucket's capacity cannot travel: they are counted on the device
-    (``over``, the largest demand beyond capacity) and ``check()`` raises
-    ``CapacityExceeded`` — the trainer checks before every snapshot and every
-    ``check_every`` steps (one step late, from a pinned copy: no sync in the step), so a
-    dropped update never reaches a checkpoint and the restart replays it.
+    ranks — Zipf click ids have far fewer distinct ids than lookups.  Slots beyond a
+    bucket's capacity cannot travel: the kernel keeps the largest excess in a device
+    counter (``over``) and ``check()`` raises ``CapacityExceeded`` — the trainer checks
+    before every snapshot and every ``check_every`` steps (one step late, from a pinned
+    copy: no sync in the step), so a dropped update never reaches a checkpoint and the
+    restart replays it.
 
     ``exact = True`` switches to the parent's exact, host-synced exchange (the agreed steps
     of ``runtime/lockstep.py``, whose pieces differ in size across ranks)."""
@@ -195,14 +196,19 @@ class BucketedOwnerExchange(OwnerSparseExchange):
         self.slack = float(slack)
         self.check_every = int(check_every)
         self.exact = False
-        dev = comm.device
-        self.need = torch.zeros(1, dtype=torch.int64, device=dev)   # largest bucket demand seen (any site)
-        self.over = torch.zeros(1, dtype=torch.int64, device=dev)   # largest demand beyond capacity
+        self.over = torch.zeros(1, dtype=torch.int32, device=comm.device)  # largest demand beyond capacity
         self._site_need: dict = {}   # (rows, slots) -> device max demand of that call site
         self._caps: dict = {}        # (rows, slots) -> calibrated per-peer capacity
         self._pinned = None
         self._pending = None
         self._steps = 0
+
+    @property
+    def need(self) -> torch.Tensor:
+        """The largest bucket demand any call site showed (device scalar)."""
+        if not self._site_need:
+            return torch.zeros(1, dtype=torch.int32, device=self.over.device)
+        return torch.stack([v.reshape(()) for v in self._site_need.values()]).max().reshape(1)
 
     def capacity(self, n: int, rows: int | None = None) -> int:
         """Per-peer slots for an exchange of ``n`` candidate ids of a ``rows``-row table:
@@ -221,7 +227,7 @@ class BucketedOwnerExchange(OwnerSparseExchange):
         keys = sorted(self._site_need, key=str)
         if not keys:
             return {}
-        d = torch.cat([self._site_need[k] for k in keys]).to(self.comm.device)
+        d = torch.cat([self._site_need[k].reshape(1) for k in keys]).to(self.comm.device)
         self.comm.all_reduce(d, "max")
         ws = self.comm.size
         for k, v in zip(keys, d.cpu().tolist()):
@@ -250,7 +256,7 @@ class BucketedOwnerExchange(OwnerSparseExchange):
                 raise CapacityExceeded(f"owner bucket overflow by {int(host[0])} slots (slack {self.slack})")
         if self.over.is_cuda:
             if self._pinned is None:
-                self._pinned = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+                self._pinned = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             self._pinned.copy_(self.over, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
@@ -259,36 +265,44 @@ class BucketedOwnerExchange(OwnerSparseExchange):
             self._pending = (_Done(), self.over.clone())
 
     # ---- buckets
-    def _bucket(self, ids: torch.Tensor, cap: int, site=None):
-        """``ids`` int32 [n] (distinct; -1 = none) -> (slot int64 [n]: position in the flat
-        [world * cap] send buffer, world * cap = not sent)."""
+    def _bucket(self, uids: torch.Tensor, off: int, V: int):
+        """``uids`` int32 [n] (distinct keys; -1 / outside [off, off + V) = none) ->
+        (send_ids int32 [world * cap]: table-local ids by owner bucket, -1 padding;
+        src int32 [world * cap]: each slot's position in ``uids``, -1 padding; cap)."""
         ws = self.comm.size
+        ids = uids.reshape(-1)
         n = ids.numel()
         dev = ids.device
-        valid = ids >= 0
-        owner = torch.where(valid, ids.remainder(ws), torch.full_like(ids, ws)).long()
-        onehot = (owner.unsqueeze(1) == torch.arange(ws, device=dev).unsqueeze(0)).to(torch.int32)
-        pos = onehot.cumsum(0).gather(1, owner.clamp(max=ws - 1).unsqueeze(1)).squeeze(1).long() - 1
-        fits = valid & (pos < cap)
-        demand = torch.where(valid, pos + 1, torch.zeros_like(pos))
-        if n:
-            top = demand.max().reshape(1)
-            torch.maximum(self.need, top, out=self.need)
-            if site is not None:
-                sn = self._site_need.get(site)
-                if sn is None:
-                    sn = self._site_need[site] = torch.zeros(1, dtype=torch.int64, device=dev)
-                torch.maximum(sn, top, out=sn)
-            torch.maximum(self.over, torch.where(fits, torch.zeros_like(demand), demand - cap).max().reshape(1),
-                          out=self.over)
-        return torch.where(fits, owner * cap + pos, torch.full_like(pos, ws * cap))
+        site = (V, n)
+        cap = self.capacity(n, V)
+        need = self._site_need.get(site)
+        if need is None:
+            need = self._site_need[site] = torch.zeros(1, dtype=torch.int32, device=dev)
+        send = torch.empty(ws * cap, dtype=torch.int32, device=dev)
+        src = torch.empty(ws * cap, dtype=torch.int32, device=dev)
+        if ids.is_cuda:
+            from .. import _ext
 
-    def _send_ids(self, ids, slot, cap):
-        ws = self.comm.size
-        buf = torch.full((ws * cap + 1,), -1, dtype=torch.int32, device=ids.device)
-        buf.scatter_(0, slot, ids.to(torch.int32))
-        buf[ws * cap] = -1
-        return buf[: ws * cap]
+            ids = ids if ids.dtype == torch.int32 else ids.to(torch.int32)
+            _ext.hip().owner_buckets(ids.contiguous().data_ptr(), n, off, V, ws, cap, send.data_ptr(),
+                                     src.data_ptr(), need.data_ptr(), self.over.data_ptr(),
+                                     torch.cuda.current_stream().cuda_stream)
+            return send, src, cap
+        # host: the same placement with torch ops (tests; the loopback communicator)
+        loc = ids.long() - off
+        valid = (ids >= 0) & (loc >= 0) & (loc < V)
+        owner = torch.where(valid, loc.remainder(ws), torch.full_like(loc, ws))
+        send.fill_(-1)
+        src.fill_(-1)
+        for o in range(ws):
+            idx = torch.nonzero(owner == o).reshape(-1)
+            k = min(idx.numel(), cap)
+            send[o * cap:o * cap + k] = loc[idx[:k]].to(torch.int32)
+            src[o * cap:o * cap + k] = idx[:k].to(torch.int32)
+            need.copy_(torch.maximum(need, torch.tensor([idx.numel()], dtype=torch.int32)))
+            if idx.numel() > cap:
+                self.over.copy_(torch.maximum(self.over, torch.tensor([idx.numel() - cap], dtype=torch.int32)))
+        return send, src, cap
 
     def _a2a(self, out, inp, cap):
         ws = self.comm.size
@@ -307,13 +321,9 @@ class BucketedOwnerExchange(OwnerSparseExchange):
             return super().pull(table, uids, offset)
         from ..ops.embedding import rows_gather, rows_scatter
 
-        ws, me = self.comm.size, self.comm.rank
+        ws = self.comm.size
         V, D = table.shape
-        u = uids.reshape(-1).to(torch.int64) - offset
-        ids = torch.where((uids.reshape(-1) >= 0) & (u >= 0) & (u < V), u, torch.full_like(u, -1)).to(torch.int32)
-        cap = self.capacity(ids.numel(), V)
-        slot = self._bucket(ids, cap, (V, ids.numel()))
-        ask = self._send_ids(ids, slot, cap)
+        ask, _, cap = self._bucket(uids, offset, V)
         asked = torch.empty_like(ask)
         self._a2a(asked, ask, cap)            # ids each rank asks of me (rank-major buckets)
         ans = rows_gather(table, asked)       # my authoritative rows (zeros for padding)
@@ -327,16 +337,12 @@ class BucketedOwnerExchange(OwnerSparseExchange):
               eps: float = 1e-8, offset: int = 0) -> ExchangeStats:
         if self.exact:
             return super().apply(table, accum, uids, rows, lr, eps, offset)
+        from ..ops.embedding import rows_gather
+
         ws = self.comm.size
         V, D = table.shape
-        u = uids.reshape(-1).to(torch.int64) - offset
-        ids = torch.where((uids.reshape(-1) >= 0) & (u >= 0) & (u < V), u, torch.full_like(u, -1)).to(torch.int32)
-        cap = self.capacity(ids.numel(), V)
-        slot = self._bucket(ids, cap, (V, ids.numel()))
-        send_ids = self._send_ids(ids, slot, cap)
-        send_rows = torch.zeros((ws * cap + 1, D), dtype=torch.float32, device=rows.device)
-        send_rows.index_copy_(0, slot, rows.reshape(-1, D).float())
-        send_rows = send_rows[: ws * cap]
+        send_ids, src, cap = self._bucket(uids, offset, V)
+        send_rows = rows_gather(rows.reshape(-1, D).float().contiguous(), src)  # zeros for padding
         r_ids = torch.empty_like(send_ids)
         r_g = torch.empty_like(send_rows)
         with self.comm.group():
@@ -344,7 +350,7 @@ class BucketedOwnerExchange(OwnerSparseExchange):
             self._a2a(r_g, send_rows, cap)
         # the owner's merged update: static segment sum in (id, source rank) order
         own_u, own_g = segment_sum(r_ids, r_g, V, static=True)
-        sparse_adagrad(table, accum, own_u.to(torch.int32).contiguous(), own_g.contiguous(), lr, eps)
+        sparse_adagrad(table, accum, own_u, own_g, lr, eps)
         row_b = 4 + 4 * D
         return self._add(ExchangeStats(sent=(ws - 1) * cap * row_b, received=(ws - 1) * cap * row_b))
 

@@ -116,7 +116,7 @@ def _conv_case(cin, cout, k, stride, pads, in_bf16, out_fp8, cfg, offset=0, extr
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [0, 1, 2, 8, 16, 17])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 11, 16, 17])
 def test_conv_fp8_configs_gpu(cfg):
     _conv_case(32, 64, 3, 1, (1, 1, 1, 1), False, True, cfg)
     _conv_case(64, 192, 3, 2, (0, 0, 0, 0), False, False, cfg)
@@ -124,10 +124,10 @@ def test_conv_fp8_configs_gpu(cfg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("c", [8, 9, 10, 11, 12])
+@pytest.mark.parametrize("c", [11])
 def test_conv_fp8_lite_shapes_gpu(c):
-    """conv_lite_fp8 (cfg 8, the 4-wave LDS-DMA tile; cfg 9, the same tile on DMA / MFMA
-    waves where the channel tile is <= 96): Cin not a multiple of the 128-byte K-tile (288,
+    """conv_lite_fp8 (cfg 11, the LDS-DMA tile the compiler uses; the other tiles were
+    measured slower and removed): Cin not a multiple of the 128-byte K-tile (288,
     192, 80), K tails, Cout tails, 1x1 / 7x1 / strided, fp8 and bf16 output at a concat offset."""
     _conv_case(288, 384, 3, 2, (0, 0, 0, 0), False, True, c, N=2, H=17, W=17)
     _conv_case(192, 80, (7, 1), 1, (3, 3, 0, 0), False, False, c, N=3, H=9, W=9)

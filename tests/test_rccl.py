@@ -177,7 +177,12 @@ def test_widedeep_bucketed_owner_step_captured_with_rccl(rccl_comm):
     a._exchange.calibrate()
     b.capture(batches[0])
     assert b._graph is not None  # a host sync inside the step would have failed the capture
-    la = [float(a.train_step(batch=bt)) for bt in batches[2:]]
+    torch.cuda.set_sync_debug_mode("error")  # the eager bucketed DP step never syncs with the host
+    try:
+        la = [a.train_step(batch=bt).clone() for bt in batches[2:]]
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    la = [float(x) for x in la]
     lb = [float(b.train_step(batch=bt)) for bt in batches[2:]]
     torch.testing.assert_close(torch.tensor(lb), torch.tensor(la), rtol=1e-4, atol=1e-5)
     for (k, va), vb in zip(a.model.state_dict().items(), b.model.state_dict().values()):
