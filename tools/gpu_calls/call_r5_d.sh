@@ -1,8 +1,24 @@
-# round 5 D: Winograd with the conflict-aware LDS layout: numerics, per-layer A/B, kernel trace
-source tools/gpu_calls/gpu_steps.sh
-step test_wino 300 python -u -m pytest tests/test_wino.py -x -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread
-step wino_bench 300 python -u bench/wino_bench.py
-cd /tmp && export TMPDIR=/tmp && cd "$REPO"
-step wino_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/wino_prof_d" -o wino -- python3 -u bench/wino_bench.py --reps 20
-python3 tools/rocpd_stats.py "$OUT"/wino_prof_d/wino_results.db "$OUT/wino_stats_d.csv"
-python3 -c "import sys; sys.path.insert(0,'.'); from flink_tensorflow_amd import _ext; h=_ext.hip(required=True); print([ (H, h.wino_f23_layout(256,H,H)) for H in (56,28,14,7)])"
+#!/bin/bash
+# round 5 D: new kernels first (pool+1x1 fp8, bucketed exchange capture, lockstep fused
+# step, bench --job P=1), then the whole GPU suite, smoke, and the benches (ResNet-50 SPMD
+# and job mode, Inception-v3 fp8 static).  Every GPU step has its own time limit; a crash,
+# abort or time-out ends the call (no later GPU step runs).
+OUT=gpurun_out/r05_d
+mkdir -p "$OUT"
+step() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "[step] $name" >&2
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" >> "$OUT/rc.txt"
+  if [ $rc -gt 1 ]; then echo "[step] $name ended with $rc: stopping" >&2; exit $rc; fi
+  return 0
+}
+PYT="python -u -m pytest -q --timeout 120 --timeout-method thread -p no:cacheprovider"
+step new_tests 400 $PYT -m gpu tests/test_fp8.py::test_pool_conv1x1_fp8_gpu tests/test_fp8.py::test_inception_v3_fp8_plan_gpu tests/test_rccl.py tests/test_lockstep.py tests/test_job_dp.py
+step gpu_suite 780 $PYT -m gpu tests --maxfail 10
+step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+step bench_rn 150 python bench.py
+step bench_job 200 python bench.py --job
+step bench_inc 200 python bench.py --model inception_v3 --steps 30 --warmup 5
+echo done >&2
