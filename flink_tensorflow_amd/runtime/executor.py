@@ -785,6 +785,15 @@ class LocalExecutor:
             if len(cs) != 1:
                 continue
             d, part, side_tag = cs[0]
+            skipped = []
+            # a rebalance / shuffle right after the readers (``read_file(...).rebalance()``) only
+            # spreads records the readers already spread: chained, the records are produced
+            # in the consumer's worker and the repartition has nothing to move
+            while (getattr(d, "passthrough", None) in ("rebalance", "shuffle") and side_tag is None
+                   and len(consumers.get(d.uid, [])) == 1):
+                skipped.append(d)
+                d, part, side_tag = consumers[d.uid][0]
+                part = Partitioner("rebalance") if part.kind == "forward" else part
             if (not getattr(d, "remote", False) or d.is_source or side_tag is not None or len(d.inputs) != 1
                     or d.parallelism != r.parallelism or part.kind not in ("forward", "rebalance")
                     or not getattr(d, "chaining", True)):
@@ -793,6 +802,8 @@ class LocalExecutor:
             d.factory = lambda head=head, tail=tail, name=name: ChainOperator([head(), tail()], name)
             d.inputs = list(r.inputs)
             r.merged_into = d
+            for n in skipped:
+                n.merged_into = d
         return [n for n in nodes if getattr(n, "merged_into", None) is None]
 
     def _relocate_sources(self, nodes) -> list[str]:

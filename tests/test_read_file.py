@@ -176,3 +176,28 @@ def test_inception_process_continuously_picks_up_new_files(tmp_path):
     out = sink.results()
     assert sorted(n for n, _ in out) == ["a0.jpg", "a1.jpg", "a2.jpg", "b0.jpg", "b1.jpg", "b2.jpg"]
     assert all(0.0 <= p <= 1.0 and lbl.startswith("class_") for _, (p, lbl) in out)
+
+
+def test_read_file_rebalance_then_workers_still_chains(tmp_path):
+    """``read_file(...).rebalance().map_with_model(...)`` (the reference's shape with an
+    explicit repartition): the repartition has nothing to move once the readers run in the
+    model workers, so the readers still chain into them and only paths cross."""
+    from flink_tensorflow_amd.runtime.remote import TRANSPORT_STATS
+
+    imgs = tmp_path / "imgs"
+    imgs.mkdir()
+    for i in range(6):
+        (imgs / f"img{i}.jpg").write_bytes(_jpeg(seed=i))
+    TRANSPORT_STATS.clear()
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    sink = (env.read_file(ImageInputFormat(), str(imgs), PROCESS_ONCE).rebalance()
+            .map_with_model(_ColorModel(), lambda rec, m: (rec[0], os.getpid(), m.label([rec[1]])[0][0][1]))
+            .run_in_processes().collect_into())
+    env.execute("read-file-rebalance")
+    out = sink.results()
+    assert sorted(n for n, _, _ in out) == [f"img{i}.jpg" for i in range(6)]
+    assert os.getpid() not in {p for _, p, _ in out}
+    stats = [v for k, v in TRANSPORT_STATS.items() if k[0] == "map-with-model"]
+    recs = sum(v["records"] for v in stats)
+    longest = max(len(str(p)) for p in imgs.iterdir())
+    assert recs == 6 and sum(v["ring_bytes"] for v in stats) / recs <= longest + 32
