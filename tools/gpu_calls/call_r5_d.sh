@@ -21,4 +21,8 @@ step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_rn 150 python bench.py
 step bench_job 200 python bench.py --job
 step bench_inc 200 python bench.py --model inception_v3 --steps 30 --warmup 5
+export TMPDIR=/tmp
+R=$(pwd)
+step layers_inc 300 python -u tools/layer_table.py --model inception_v3 --reps 3 --out "$OUT/layers_inc.md"
+step wd_trace 300 bash -c "cd /tmp && rocprofv3 --kernel-trace --stats -d $R/$OUT/wd_prof -o wd -- python3 $R/tools/wd_bucketed_trace.py"
 echo done >&2
