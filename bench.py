@@ -138,6 +138,9 @@ def main():
     ap.add_argument("--lanes", type=int, default=None,
                     help="compute lanes: independent plan instances on their own HIP streams, batches round-robin "
                          "(default: 3 for bert / bert_graph, 2 otherwise; measured in profiles/r01_lanes)")
+    ap.add_argument("--no-interleave", action="store_true",
+                    help="A/B: launch a batch's per-piece head kernels after the whole host gather instead of "
+                         "interleaved with it")
     ap.add_argument("--timeline", action="store_true",
                     help="also print, per timed batch, its lane and the GPU times of its first H2D piece, first "
                          "kernel and completion relative to the start of the timed window (diagnostics)")
@@ -326,7 +329,7 @@ def main():
     runner = PipelinedGpuRunner(lane_plans, feed, lambda p: p.output_tensors(), rec_shape, rec_dtype,
                                 depth=args.depth, device=dev, gather_threads=args.gather_threads,
                                 stagger=args.stagger_lanes, freeze_gc=not args.no_gc_freeze,
-                                timeline=args.timeline)
+                                timeline=args.timeline, interleave_head=not args.no_interleave)
 
     if args.offered_rate:
         return run_offered(args, runner, records, B, rank, ws, dev, comm, MetricGroup, model_name, data, lanes,

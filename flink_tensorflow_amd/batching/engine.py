@@ -81,7 +81,8 @@ class PipelinedGpuRunner:
 
     def __init__(self, plans, feed: str, fetch_bufs: Callable[[Any], Sequence[torch.Tensor]],
                  record_shape, record_dtype=torch.uint8, depth: int = 3, device=None, gather_threads: int = 8,
-                 stage_chunk: int = 64, stagger: bool = False, freeze_gc: bool = True, timeline: bool = False):
+                 stage_chunk: int = 64, stagger: bool = False, freeze_gc: bool = True, timeline: bool = False,
+                 interleave_head: bool = True):
         lanes = plans if isinstance(plans, (list, tuple)) else [plans]
         self.lanes = [dict(sorted(p.items())) for p in lanes]
         self.plans = self.lanes[0]
@@ -102,6 +103,7 @@ class PipelinedGpuRunner:
         self.compute_stream = self.compute_streams[0]
         self.gather_threads = gather_threads
         self.stage_chunk = stage_chunk  # records per gather + H2D piece (0: whole batch at once)
+        self.interleave_head = interleave_head  # launch each piece's head kernel inside the gather loop
         self._native = _ext.native()
         depth = max(depth, len(self.lanes) + 1)  # every lane busy + one batch being staged
         # batches in flight over ALL buckets (each bucket has its own ``depth`` slots): with
@@ -170,6 +172,18 @@ class PipelinedGpuRunner:
         if slot.t_h2d is not None:
             slot.t_h2d.record(self.copy_stream)
             slot.t_submit = t1
+        lane = self._lane
+        plan = self.lanes[lane][b]
+        stream = self.compute_streams[lane]
+        # a plan whose head kernel runs per staged piece and that needs no host look at the
+        # batch (``select``): each piece's head is launched right after its H2D, WHILE the
+        # host gathers the next piece — the GPU starts one piece after the first records are
+        # gathered instead of after the whole batch (the pipeline fill of a timed window)
+        interleave = (self.interleave_head and len(pieces) > 1 and getattr(plan, "select", None) is None
+                      and getattr(plan, "head_pieces_ok", None) is not None
+                      and plan.head_pieces_ok(self.feed, slot.dev_in))
+        if interleave:
+            self._begin_lane(slot, lane, stream)
         with trace_range(f"gather[{n}/{b}]"):
             for i, (lo, hi) in enumerate(pieces):
                 self._native.gather_into(base + lo * rb, cap - lo * rb, payloads[lo:hi], rb, self.gather_threads)
@@ -180,41 +194,38 @@ class PipelinedGpuRunner:
                 with torch.cuda.stream(self.copy_stream):
                     slot.dev_in[lo:hi].copy_(slot.pinned_in[lo:hi], non_blocking=True)
                     slot.h2d_parts[i].record(self.copy_stream)
+                if interleave:
+                    with torch.cuda.stream(stream):
+                        stream.wait_event(slot.h2d_parts[i])
+                        plan.launch_head_piece(slot.dev_in, lo, hi)
         t2 = time.perf_counter()
-        lane = self._lane
         self._lane = (self._lane + 1) % len(self.lanes)
-        plan = self.lanes[lane][b]
         select = getattr(plan, "select", None)
         if select is not None:  # e.g. the padding-free BERT encoder: pick a token-capacity plan
             plan = select(slot.pinned_in, n)
         t3 = time.perf_counter()
-        stream = self.compute_streams[lane]
-        if self.stagger:
-            if not self._inflight:  # the pipeline restarts from empty
-                self._started.clear()
-                self._stagger_evt = None
-            if lane not in self._started and lane != 0 and self._stagger_evt is not None:
-                stream.wait_event(self._stagger_evt)
-            self._started.add(lane)
+        if not interleave:
+            self._begin_lane(slot, lane, stream)
         with torch.cuda.stream(self.copy_stream):
             slot.h2d.record(self.copy_stream)
         slot.lane = lane
         with torch.cuda.stream(stream):
-            if slot.t_start is not None:  # after the lane's previous work, before this batch's h2d wait
-                slot.t_start.record(stream)
             with trace_range(f"forward[{b}]@lane{lane}"):
-                chunked = getattr(plan, "replay_from_chunks", None)
-                # head kernel per staged piece: the GPU starts on the first piece while the
-                # later ones are still in flight (shortens the pipeline fill)
-                if not (len(pieces) > 1 and chunked is not None and chunked(
-                        self.feed, slot.dev_in, pieces, lambda i: stream.wait_event(slot.h2d_parts[i]))):
-                    stream.wait_event(slot.h2d)
-                    replay_from = getattr(plan, "replay_from", None)
-                    if replay_from is not None:  # head kernel reads the staging slot: no D2D copy
-                        replay_from(self.feed, slot.dev_in)
-                    else:
-                        plan.input_buffer(self.feed).copy_(slot.dev_in, non_blocking=True)
-                        plan.replay()
+                if interleave:
+                    plan.replay_tail()
+                else:
+                    chunked = getattr(plan, "replay_from_chunks", None)
+                    # head kernel per staged piece: the GPU starts on the first piece while
+                    # the later ones are still in flight (shortens the pipeline fill)
+                    if not (len(pieces) > 1 and chunked is not None and chunked(
+                            self.feed, slot.dev_in, pieces, lambda i: stream.wait_event(slot.h2d_parts[i]))):
+                        stream.wait_event(slot.h2d)
+                        replay_from = getattr(plan, "replay_from", None)
+                        if replay_from is not None:  # head kernel reads the staging slot: no D2D copy
+                            replay_from(self.feed, slot.dev_in)
+                        else:
+                            plan.input_buffer(self.feed).copy_(slot.dev_in, non_blocking=True)
+                            plan.replay()
             with trace_range("d2h"):
                 for dst, src in zip(slot.pinned_out, self.fetch_bufs(plan)):
                     dst.copy_(src, non_blocking=True)
@@ -234,6 +245,20 @@ class PipelinedGpuRunner:
         hs["launch"] += t4 - t3
         self.batches += 1
         return finished
+
+    def _begin_lane(self, slot: _Slot, lane: int, stream) -> None:
+        """The lane's stream work that precedes a batch: the stagger wait of a restarting
+        pipeline and the batch's start stamp (timeline)."""
+        if self.stagger:
+            if not self._inflight:  # the pipeline restarts from empty
+                self._started.clear()
+                self._stagger_evt = None
+            if lane not in self._started and lane != 0 and self._stagger_evt is not None:
+                stream.wait_event(self._stagger_evt)
+            self._started.add(lane)
+        if slot.t_start is not None:  # after the lane's previous work, before this batch's h2d wait
+            with torch.cuda.stream(stream):
+                slot.t_start.record(stream)
 
     def _harvest(self, slot: _Slot) -> BatchResult:
         # event waits / queries are rejected while a sibling subtask thread captures a

@@ -2131,19 +2131,32 @@ class CompiledFunction(TransformerLowering):
         (the current stream waits for that piece's H2D), so the GPU starts on the first
         records while the rest are still being gathered / copied; then the graph of the
         remaining steps.  False (nothing launched) when the plan has no such head."""
-        h = self._head
-        buf = self.input_buffer(feed)
-        if (h is None or self._graph_tail is None or h[0] != str(TensorName.parse(feed))
-                or src.shape != buf.shape or src.dtype != buf.dtype or src.device != buf.device
-                or not src.is_contiguous() or len(h[1].outputs) != 1):
+        if not self.head_pieces_ok(feed, src):
             return False
-        st = h[1]
-        out = _root(st.outputs[0]).buf
         for i, (lo, hi) in enumerate(chunks):
             wait(i)
-            st.fn(x=types.SimpleNamespace(buf=src[lo:hi]), out=types.SimpleNamespace(buf=out[lo:hi]))
-        self._graph_tail.replay()
+            self.launch_head_piece(src, lo, hi)
+        self.replay_tail()
         return True
+
+    def head_pieces_ok(self, feed: str, src: torch.Tensor) -> bool:
+        """The plan starts with a head kernel on ``feed`` that can run per piece of ``src``
+        (``launch_head_piece``), the rest of the plan being one captured graph
+        (``replay_tail``): the pipelined runner launches each piece's head right after that
+        piece's H2D, interleaved with the host gather of the next piece."""
+        h = self._head
+        buf = self.input_buffer(feed)
+        return not (h is None or self._graph_tail is None or h[0] != str(TensorName.parse(feed))
+                    or src.shape != buf.shape or src.dtype != buf.dtype or src.device != buf.device
+                    or not src.is_contiguous() or len(h[1].outputs) != 1)
+
+    def launch_head_piece(self, src: torch.Tensor, lo: int, hi: int) -> None:
+        st = self._head[1]
+        out = _root(st.outputs[0]).buf
+        st.fn(x=types.SimpleNamespace(buf=src[lo:hi]), out=types.SimpleNamespace(buf=out[lo:hi]))
+
+    def replay_tail(self) -> None:
+        self._graph_tail.replay()
 
     def replay(self):
         """Runs the plan on the current input buffers (no host synchronisation)."""
