@@ -163,3 +163,41 @@ def test_gc_freeze_moves_setup_objects_out_of_collection():
     finally:
         unfreeze_setup_objects()
     assert gc.get_freeze_count() == 0
+
+
+@pytest.mark.gpu
+def test_interleaved_head_pieces_match_whole_batch_gpu(small_graph):
+    """Per-piece head kernels launched inside the host gather loop (``interleave_head``)
+    give the same results as the head launched after the whole gather, full and short
+    (padded) batches included, over two lanes."""
+    import numpy as np
+
+    from flink_tensorflow_amd.batching.engine import PipelinedGpuRunner
+
+    dev = torch.device("cuda", 0)
+    feeds = {"images:0": ((8, 48, 48, 3), "UINT8")}
+
+    def lane():
+        return {8: CompiledFunction(small_graph, feeds, ["top_k:0", "top_k:1"], dev, strict=True,
+                                    arena=DeviceArena(dev, 4 << 30))}
+
+    rng = np.random.default_rng(1)
+    batches = [[rng.integers(0, 256, (48, 48, 3), dtype=np.uint8) for _ in range(8 if i % 3 else 6)]
+               for i in range(7)]
+
+    def run(interleave):
+        lanes = [lane(), lane()]
+        assert lanes[0][8].head_pieces_ok("images:0", torch.empty((8, 48, 48, 3), dtype=torch.uint8, device=dev))
+        r = PipelinedGpuRunner(lanes, "images:0", lambda p: p.output_tensors(), (48, 48, 3), depth=3, device=dev,
+                               stage_chunk=3, interleave_head=interleave)
+        out = []
+        for i, b in enumerate(batches):
+            out += r.submit(b, np.full(len(b), float(i)), [i] * len(b))
+        out += r.drain()
+        return out
+
+    a, b = run(True), run(False)
+    assert [r.tags[0] for r in a] == list(range(7)) and [r.n for r in a] == [len(x) for x in batches]
+    for x, y in zip(a, b):
+        torch.testing.assert_close(x.outputs[0][: x.n], y.outputs[0][: y.n])
+        assert torch.equal(x.outputs[1][: x.n], y.outputs[1][: y.n])
