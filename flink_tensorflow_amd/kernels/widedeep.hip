@@ -102,13 +102,20 @@ __global__ __launch_bounds__(256) void wd_gather_kernel(const int* __restrict__ 
 __global__ __launch_bounds__(256) void wd_loss_kernel(const bf16* __restrict__ head, int ldh,
                                                       const float* __restrict__ wsum, const float* __restrict__ wbias,
                                                       const float* __restrict__ labels, int ldl, int B,
-                                                      float norm, float* __restrict__ dlogit,
+                                                      int nvalid, float norm, float* __restrict__ dlogit,
                                                       bf16* __restrict__ dlogit16, float* __restrict__ part,
                                                       float* __restrict__ wgrad, int C, int WD) {
   __shared__ float red[2][4];
   const int b = blockIdx.x * 256 + threadIdx.x;
   float lo = 0.f, d = 0.f;
-  if (b < B) {
+  if (b >= nvalid && b < B) {  // padding rows of a batch rounded up to the GEMM granule: no loss, no gradient
+    dlogit[b] = 0.f;
+    dlogit16[b] = f2bf(0.f);
+    for (int c = 0; c < C; ++c) {
+      float* row = wgrad + ((size_t)b * C + c) * WD;
+      for (int k = 0; k < WD; ++k) row[k] = 0.f;
+    }
+  } else if (b < B) {
     const float l = (float)head[(size_t)b * ldh] + wsum[b] + wbias[0];
     const float y = labels[(size_t)b * ldl];
     lo = fmaxf(l, 0.f) - l * y + log1pf(__expf(-fabsf(l)));
@@ -324,17 +331,19 @@ void wd_keys(uintptr_t cats, int ldc, uintptr_t cross, int ldx, uintptr_t keys, 
 // (parallel/step_agreement.py), so the summed gradients are those of the union's mean.
 // step (optional, 0 = none): Adam's step counter, incremented here so the captured step has
 // no separate increment launch.
-void wd_loss(uintptr_t head, int ldh, uintptr_t wsum, uintptr_t wbias, uintptr_t labels, int ldl, int B, float norm,
-             uintptr_t dlogit, uintptr_t dlogit16, uintptr_t loss, uintptr_t g_wbias, uintptr_t g_hb0, uintptr_t wgrad,
-             int C, int WD, uintptr_t part, uintptr_t step, uintptr_t stream) {
-  if (B <= 0) throw std::invalid_argument("wd_loss: empty batch");
+// nvalid <= B: rows [nvalid, B) are padding (a batch rounded up to the training GEMM's
+// 8-row granule) and get zero loss and gradient.
+void wd_loss(uintptr_t head, int ldh, uintptr_t wsum, uintptr_t wbias, uintptr_t labels, int ldl, int B, int nvalid,
+             float norm, uintptr_t dlogit, uintptr_t dlogit16, uintptr_t loss, uintptr_t g_wbias, uintptr_t g_hb0,
+             uintptr_t wgrad, int C, int WD, uintptr_t part, uintptr_t step, uintptr_t stream) {
+  if (B <= 0 || nvalid <= 0 || nvalid > B) throw std::invalid_argument("wd_loss: empty batch or bad nvalid");
   if (!(norm > 0.f)) throw std::invalid_argument("wd_loss: norm must be positive");
   if (wgrad % 16) throw std::invalid_argument("wd_loss: wgrad must be 16-byte aligned");
   auto s = reinterpret_cast<hipStream_t>(stream);
   const int nb = (B + 255) / 256;
   hipLaunchKernelGGL(wd_loss_kernel, dim3(nb), dim3(256), 0, s, reinterpret_cast<const bf16*>(head), ldh,
                      reinterpret_cast<const float*>(wsum), reinterpret_cast<const float*>(wbias),
-                     reinterpret_cast<const float*>(labels), ldl, B, norm, reinterpret_cast<float*>(dlogit),
+                     reinterpret_cast<const float*>(labels), ldl, B, nvalid, norm, reinterpret_cast<float*>(dlogit),
                      reinterpret_cast<bf16*>(dlogit16), reinterpret_cast<float*>(part), reinterpret_cast<float*>(wgrad),
                      C, WD);
   hipLaunchKernelGGL(wd_loss_final_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<const float*>(part), nb, norm,

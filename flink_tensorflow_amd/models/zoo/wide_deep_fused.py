@@ -152,6 +152,17 @@ class FusedWideDeepStep:
         (``parallel/step_agreement.py``) — the loss is this piece's sum over the round's
         global record count and the all-reduced gradients are summed, not averaged."""
         H, m, cfg = self._H, self.m, self.cfg
+        nvalid = labels.shape[0]
+        if nvalid % 8:  # the training GEMMs take 8-row granules: pad with rows that look up
+            # nothing (ids < 0) and get zero loss and gradient (wd_loss nvalid)
+            pad = 8 - nvalid % 8
+            dev = labels.device
+            labels = torch.cat([labels.reshape(-1).float(), torch.zeros(pad, device=dev)])
+            dense = torch.cat([dense.float(), torch.zeros((pad, dense.shape[1]), device=dev)])
+            cats = torch.cat([cats.to(torch.int32), torch.full((pad, cats.shape[1]), -(1 << 30), dtype=torch.int32,
+                                                                  device=dev)])
+            cross = torch.cat([cross.to(torch.int32), torch.full((pad, cross.shape[1]), -1, dtype=torch.int32,
+                                                                    device=dev)])
         B = labels.shape[0]
         a = self._acts.get(B)
         if a is None:
@@ -190,7 +201,8 @@ class FusedWideDeepStep:
             h = K.gemm_train(h, self.w16[i], bias=l.bias, act="relu", out=a.h[i])
         K.gemm_train(h, self.w16[-1], bias=m.head.bias, out=a.hd)
         H.wd_loss(a.hd.data_ptr(), a.hd.shape[1], a.wsum.data_ptr(), m.wide_bias.data_ptr(),
-                  labels.data_ptr(), labels.stride(0), B, float(norm if norm is not None else B), a.dlogit.data_ptr(),
+                  labels.data_ptr(), labels.stride(0), B, nvalid, float(norm if norm is not None else nvalid),
+                  a.dlogit.data_ptr(),
                   a.dlogit16.data_ptr(), a.loss.data_ptr(),
                   self.g["wide_bias"].data_ptr(), self.g["head.bias"].data_ptr(), a.wgrad.data_ptr(), C, WD, a.part.data_ptr(),
                   self.t.data_ptr(), s)  # also counts Adam's step

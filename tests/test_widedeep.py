@@ -394,3 +394,24 @@ def test_group_keys_three_pass_radix_gpu():
     starts = torch.cat([torch.zeros(1, dtype=torch.long), counts.cumsum(0)])
     assert torch.equal(seg[:nr + 1].cpu().long(), starts) and (seg[nr:] == n).all()
     assert torch.equal(seg_id.cpu().long(), torch.repeat_interleave(torch.arange(nr), counts))
+
+
+@pytest.mark.gpu
+def test_fused_step_partial_batch_gpu():
+    """A micro-batch that is not a multiple of the training GEMM's 8-row granule (a
+    deadline-flushed or agreed partial piece): the fused step pads it with rows that look
+    up nothing and get zero loss / gradient; the loss matches the host trainer."""
+    from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, WideDeepTrainer, synthetic_click_records
+
+    cfg = WideDeepConfig.tiny()
+    recs = synthetic_click_records(37, cfg, seed=9)
+    g = WideDeepTrainer(cfg, device="cuda", seed=4)
+    h = WideDeepTrainer(cfg, device="cpu", seed=4, fused=False)
+    g.open()
+    h.open()
+    assert g._fused is not None
+    lg, lh = float(g.train_step(recs)), float(h.train_step(recs))
+    assert abs(lg - lh) <= 2e-2 * abs(lh) + 2e-3, (lg, lh)
+    lg2 = float(g.train_step(recs, counts=[37]))  # the agreed form of the same piece
+    lh2 = float(h.train_step(recs))
+    assert abs(lg2 - lh2) <= 3e-2 * abs(lh2) + 3e-3, (lg2, lh2)
