@@ -13,8 +13,10 @@
 //      per 16x16 fragment: 4 waves x 4 pixel fragments x (Cout / 16) channel fragments,
 //      the [Cout][Cin] filter bank in LDS;
 //   3. dequantise (w_scale * x_scale per channel) + bias + activation, requantise to e4m3
-//      with the consumer's scale, stage through LDS and store 16-B row segments
-//      (concat-offset capable).
+//      with the consumer's scale and store each lane's 4 channels straight from the
+//      accumulators (16 contiguous bytes per pixel per fragment; concat-offset capable).
+// Load items are groups of 4 adjacent pooled pixels x one 16-B chunk: inside a pooled row
+// they share window columns (27 loads for 4 outputs instead of 36).
 // The pooled tensor never exists in memory: one read of the pre-pool tensor (L2 serves
 // the window overlap) and one write of the conv output.
 #include <pybind11/pybind11.h>
@@ -60,19 +62,29 @@ FTM_DEVICE i32x8 ld32(const uint8_t* p) {
   return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
 }
 
+// one pooled pixel's 16-B channel chunk: the max of its 3x3 window (keys, order-preserving)
+FTM_DEVICE u8x16 pool_chunk(const uint8_t* base, int W, int cin) {
+  u8x16 v[9];
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) v[dy * 3 + dx] = *reinterpret_cast<const u8x16*>(base + ((size_t)dy * W + dx) * cin);
+  u8x16 k = fp8_key(v[0]);
+#pragma unroll
+  for (int i = 1; i < 9; ++i) k = __builtin_elementwise_max(k, fp8_key(v[i]));
+  return fp8_unkey(k);
+}
+
 template <int CIN, int I, int ACT>
 __global__ __launch_bounds__(256) void pool_conv1x1_fp8_kernel(PoolConvParams p) {
   static_assert(CIN == 64, "one 128-byte MFMA K-step with half of it zero");
   constexpr int XP = CIN + 16;      // pooled-row pitch in LDS (bytes; +16 spreads banks)
-  constexpr int OC = I * 16;        // output channels handled (Cout == OC)
-  constexpr int OP = OC + 16;       // output staging pitch
+  constexpr int OC = I * 16;        // output channels (Cout == OC)
   constexpr int CH = CIN / 16;      // 16-B chunks per pooled row
-  // pooled rows + filter bank, then (after the fragments are in registers) the output tile
-  constexpr int IN_B = PX * XP + OC * XP, OUT_B = PX * OP;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[IN_B > OUT_B ? IN_B : OUT_B];
-  uint8_t* Xs = smem;
-  uint8_t* Ws = smem + PX * XP;
-  uint8_t* Os = smem;
+  constexpr int G = 4;              // pooled pixels per load item (adjacent along the row)
+  static_assert(PX / G * CH == 256, "one load item per thread");
+  __shared__ __attribute__((aligned(16))) uint8_t Xs[PX * XP];
+  __shared__ __attribute__((aligned(16))) uint8_t Ws[OC * XP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long m0 = (long)blockIdx.x * PX;
 
@@ -81,69 +93,78 @@ __global__ __launch_bounds__(256) void pool_conv1x1_fp8_kernel(PoolConvParams p)
     const int r = q / CH, c = q - r * CH;
     *reinterpret_cast<u32x4*>(Ws + r * XP + c * 16) = *reinterpret_cast<const u32x4*>(p.w + (size_t)r * CIN + c * 16);
   }
-  for (int q = tid; q < PX * CH; q += 256) {
-    const int pl = q / CH, c = q - pl * CH;
-    const long m = m0 + pl;
-    u8x16 key = {};
-    if (m < p.M) {
-      const long t = m / p.Wp;
-      const int pw = (int)(m - t * p.Wp), ph = (int)(t % p.Hp), n = (int)(t / p.Hp);
+  {
+    // thread = (group of G adjacent pooled pixels, 16-B chunk): a group inside one pooled
+    // row shares window columns — 3 rows x (2G + 1) loads for G outputs instead of 9 G
+    const int c = tid % CH, g = tid / CH;
+    const long mg = m0 + (long)g * G;
+    const long t = mg / p.Wp;
+    const int pw = (int)(mg - t * p.Wp), ph = (int)(t % p.Hp), n = (int)(t / p.Hp);
+    u8x16 out[G];
+    if (mg + G <= p.M && pw + G <= p.Wp) {
       const uint8_t* base = p.x + (((size_t)n * p.H + 2 * ph) * p.W + 2 * pw) * CIN + c * 16;
-      u8x16 v[9];
+      u8x16 k[G];
 #pragma unroll
-      for (int dy = 0; dy < 3; ++dy)
+      for (int dy = 0; dy < 3; ++dy) {
+        u8x16 v[2 * G + 1];
 #pragma unroll
-        for (int dx = 0; dx < 3; ++dx)
-          v[dy * 3 + dx] = *reinterpret_cast<const u8x16*>(base + ((size_t)dy * p.W + dx) * CIN);
-      key = fp8_key(v[0]);
+        for (int x = 0; x < 2 * G + 1; ++x)
+          v[x] = fp8_key(*reinterpret_cast<const u8x16*>(base + ((size_t)dy * p.W + x) * CIN));
 #pragma unroll
-      for (int k = 1; k < 9; ++k) key = __builtin_elementwise_max(key, fp8_key(v[k]));
-      key = fp8_unkey(key);
+        for (int o = 0; o < G; ++o) {
+          const u8x16 r = __builtin_elementwise_max(__builtin_elementwise_max(v[2 * o], v[2 * o + 1]), v[2 * o + 2]);
+          k[o] = dy == 0 ? r : __builtin_elementwise_max(k[o], r);
+        }
+      }
+#pragma unroll
+      for (int o = 0; o < G; ++o) out[o] = fp8_unkey(k[o]);
+    } else {  // the group crosses a pooled row or the end: pixel by pixel
+#pragma unroll
+      for (int o = 0; o < G; ++o) {
+        const long m = mg + o;
+        out[o] = u8x16{};
+        if (m < p.M) {
+          const long tt = m / p.Wp;
+          const int pwo = (int)(m - tt * p.Wp), pho = (int)(tt % p.Hp), no = (int)(tt / p.Hp);
+          out[o] = pool_chunk(p.x + (((size_t)no * p.H + 2 * pho) * p.W + 2 * pwo) * CIN + c * 16, p.W, CIN);
+        }
+      }
     }
-    *reinterpret_cast<u8x16*>(Xs + pl * XP + c * 16) = key;
+#pragma unroll
+    for (int o = 0; o < G; ++o) *reinterpret_cast<u8x16*>(Xs + (g * G + o) * XP + c * 16) = out[o];
   }
   __syncthreads();
 
-  // ---- 2. one MFMA K-step: lane groups fq = 0, 1 carry the 64 channel bytes, 2, 3 zeros
+  // ---- 2./3. per pixel fragment: one MFMA K-step (lane groups fq = 0, 1 carry the 64
+  // channel bytes, 2, 3 zeros), then dequantise + bias + act + requantise and store each
+  // lane's 4 channels of its pixel (16 contiguous bytes per pixel per 16-channel fragment)
   const int frow = lane & 15, fq = lane >> 4;
   const bool kval = fq * 32 < CIN;
   const i32x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
-  i32x8 a[I], b[4];
+  i32x8 a[I];
 #pragma unroll
   for (int i = 0; i < I; ++i) a[i] = kval ? ld32(Ws + (i * 16 + frow) * XP + fq * 32) : zero;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) b[j] = kval ? ld32(Xs + ((wave * 4 + j) * 16 + frow) * XP + fq * 32) : zero;
-  f32x4 acc[I][4];
-#pragma unroll
-  for (int i = 0; i < I; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0,
-                                                                    127, 0, 127);
-  __syncthreads();  // every wave holds its fragments: the LDS becomes the output tile
-
-  // ---- 3. epilogue: rows = channels (4 fq + r), columns = pixels (frow)
+  f32x4 sv[I], bv[I];
 #pragma unroll
   for (int i = 0; i < I; ++i) {
-    const int cl = i * 16 + fq * 4;
-    const f32x4 sv = *reinterpret_cast<const f32x4*>(p.cs + cl);
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bias + cl);
+    sv[i] = *reinterpret_cast<const f32x4*>(p.cs + i * 16 + fq * 4);
+    bv[i] = *reinterpret_cast<const f32x4*>(p.bias + i * 16 + fq * 4);
+  }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int pl = (wave * 4 + j) * 16 + frow;
+  for (int j = 0; j < 4; ++j) {
+    const int pl = (wave * 4 + j) * 16 + frow;
+    const i32x8 b = kval ? ld32(Xs + pl * XP + fq * 32) : zero;
+    const long m = m0 + pl;
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      const f32x4 acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0,
+                                                                         127, 0, 127);
       float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = apply_act<ACT>(acc[i][j][r] * sv[r] + bv[r]) * p.out_q;
-      *reinterpret_cast<uint32_t*>(Os + pl * OP + cl) = pack4_e4m3(v[0], v[1], v[2], v[3]);
+      for (int r = 0; r < 4; ++r) v[r] = apply_act<ACT>(acc[r] * sv[i][r] + bv[i][r]) * p.out_q;
+      if (m < p.M)
+        *reinterpret_cast<uint32_t*>(p.y + m * p.ldy + p.y_coff + i * 16 + fq * 4) = pack4_e4m3(v[0], v[1], v[2], v[3]);
     }
-  }
-  __syncthreads();
-  constexpr int SEG = OC / 16;
-  for (int q = tid; q < PX * SEG; q += 256) {
-    const int pl = q / SEG, c = q - pl * SEG;
-    const long m = m0 + pl;
-    if (m < p.M)
-      *reinterpret_cast<u32x4*>(p.y + m * p.ldy + p.y_coff + c * 16) = *reinterpret_cast<const u32x4*>(Os + pl * OP + c * 16);
   }
 }
 
