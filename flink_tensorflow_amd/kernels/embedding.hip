@@ -368,29 +368,60 @@ __global__ __launch_bounds__(256) void rows_scatter_kernel(float* __restrict__ t
 }
 
 // Fixed-capacity owner buckets of the bucketed exchange (parallel/sparse_exchange.py).
-// ids [n]: keys of a shared key space (-1 / outside [off, off + V) = none), distinct.  Block
-// o collects, in input order, the ids whose table-local id (id - off) is owned by rank o
-// (local % ws == o): slot o * cap + k gets the k-th one (send_ids: the local id, src: its
-// input position); slots past the count get -1.  A 1024-thread block scans the ids in
-// chunks: wave ballots + a 16-entry LDS prefix give each id its position.  need / over:
-// running maxima (global atomics) of the demand and of the demand beyond capacity.
-__global__ __launch_bounds__(1024) void owner_buckets_kernel(const int* __restrict__ ids, int n, int off, int V, int ws,
-                                                             int cap, int* __restrict__ send_ids,
-                                                             int* __restrict__ src, int* __restrict__ need,
-                                                             int* __restrict__ over) {
+// ids [n]: keys of a shared key space (-1 / outside [off, off + V) = none), distinct.  The
+// ids whose table-local id (id - off) is owned by rank o (local % ws == o) go, in input
+// order, to slots o * cap + k (send_ids: the local id, src: its input position); slots past
+// the count get -1.  Two passes over SEG-id segments, grid (segments, owners): count, then
+// place at the segment's offset (the sum of the earlier segments' counts, read by every
+// placing block: the segment count is small).  Inside a segment, 1024 threads scan it in
+// chunks: wave ballots + a 16-entry LDS prefix.  need / over: running maxima (global
+// atomics) of the demand and of the demand beyond capacity.
+constexpr int OB_SEG = 4096;
+
+FTM_DEVICE bool owned_by(int id, int off, int V, int ws, int o, int& loc) {
+  loc = id - off;
+  return id >= 0 && loc >= 0 && loc < V && (loc % ws) == o;
+}
+
+__global__ __launch_bounds__(1024) void owner_count_kernel(const int* __restrict__ ids, int n, int off, int V, int ws,
+                                                           int* __restrict__ counts) {
   __shared__ int cnt[16];
-  const int o = blockIdx.x;
+  const int s = blockIdx.x, o = blockIdx.y, nseg = gridDim.x;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  int run = 0;
-  for (int b0 = 0; b0 < n; b0 += 1024) {
+  int total = 0;
+  for (int b0 = s * OB_SEG; b0 < n && b0 < (s + 1) * OB_SEG; b0 += 1024) {
+    const int i = b0 + t;
+    int loc;
+    const bool f = i < n && owned_by(ids[i], off, V, ws, o, loc);
+    const unsigned long long m = __ballot(f);
+    if (lane == 0) cnt[w] = __popcll(m);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) total += cnt[k];
+    __syncthreads();
+  }
+  if (t == 0) counts[o * nseg + s] = total;
+}
+
+__global__ __launch_bounds__(1024) void owner_place_kernel(const int* __restrict__ ids, int n, int off, int V, int ws,
+                                                           int cap, const int* __restrict__ counts,
+                                                           int* __restrict__ send_ids, int* __restrict__ src,
+                                                           int* __restrict__ need, int* __restrict__ over) {
+  __shared__ int cnt[16];
+  __shared__ int base_s;
+  const int s = blockIdx.x, o = blockIdx.y, nseg = gridDim.x;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) {
+    int b = 0;
+    for (int k = 0; k < s; ++k) b += counts[o * nseg + k];
+    base_s = b;
+  }
+  __syncthreads();
+  int run = base_s;
+  for (int b0 = s * OB_SEG; b0 < n && b0 < (s + 1) * OB_SEG; b0 += 1024) {
     const int i = b0 + t;
     int loc = -1;
-    bool f = false;
-    if (i < n) {
-      const int id = ids[i];
-      loc = id - off;
-      f = id >= 0 && loc >= 0 && loc < V && (loc % ws) == o;
-    }
+    const bool f = i < n && owned_by(ids[i], off, V, ws, o, loc);
     const unsigned long long m = __ballot(f);
     const int before = __popcll(m & ((1ull << lane) - 1ull));
     if (lane == 0) cnt[w] = __popcll(m);
@@ -410,13 +441,15 @@ __global__ __launch_bounds__(1024) void owner_buckets_kernel(const int* __restri
     run += tot;
     __syncthreads();
   }
-  for (int p = (run < cap ? run : cap) + t; p < cap; p += 1024) {
-    send_ids[(size_t)o * cap + p] = -1;
-    src[(size_t)o * cap + p] = -1;
-  }
-  if (t == 0) {
-    atomicMax(need, run);
-    if (run > cap) atomicMax(over, run - cap);
+  if (s == nseg - 1) {  // the last segment knows the owner's total: pad the bucket, record demand
+    for (int p = (run < cap ? run : cap) + t; p < cap; p += 1024) {
+      send_ids[(size_t)o * cap + p] = -1;
+      src[(size_t)o * cap + p] = -1;
+    }
+    if (t == 0) {
+      atomicMax(need, run);
+      if (run > cap) atomicMax(over, run - cap);
+    }
   }
 }
 
@@ -580,17 +613,25 @@ void rows_scatter(uintptr_t table, uintptr_t ids, uintptr_t rows, long long n, i
   rows_move(false, table, ids, rows, n, D, V, stream);
 }
 
+// counts: int32 workspace of ws * owner_buckets_segments(n) entries
+int owner_buckets_segments(int n) { return n > 0 ? (n + OB_SEG - 1) / OB_SEG : 1; }
+
 void owner_buckets(uintptr_t ids, int n, int off, int V, int ws, int cap, uintptr_t send_ids, uintptr_t src,
-                   uintptr_t need, uintptr_t over, uintptr_t stream) {
+                   uintptr_t need, uintptr_t over, uintptr_t counts, uintptr_t stream) {
   if (ws < 1 || ws > 1024 || cap < 1) throw std::invalid_argument("owner_buckets: 1 <= ws <= 1024, cap >= 1");
-  hipLaunchKernelGGL(owner_buckets_kernel, dim3(ws), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream),
-                     reinterpret_cast<const int*>(ids), n, off, V, ws, cap, reinterpret_cast<int*>(send_ids),
-                     reinterpret_cast<int*>(src), reinterpret_cast<int*>(need), reinterpret_cast<int*>(over));
+  auto s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid(owner_buckets_segments(n), ws), block(1024);
+  hipLaunchKernelGGL(owner_count_kernel, grid, block, 0, s, reinterpret_cast<const int*>(ids), n, off, V, ws,
+                     reinterpret_cast<int*>(counts));
+  hipLaunchKernelGGL(owner_place_kernel, grid, block, 0, s, reinterpret_cast<const int*>(ids), n, off, V, ws, cap,
+                     reinterpret_cast<const int*>(counts), reinterpret_cast<int*>(send_ids), reinterpret_cast<int*>(src),
+                     reinterpret_cast<int*>(need), reinterpret_cast<int*>(over));
   FTM_CHECK_LAUNCH();
 }
 
 void register_embedding(pybind11::module_& m) {
   m.def("owner_buckets", &owner_buckets);
+  m.def("owner_buckets_segments", &owner_buckets_segments);
   m.def("rows_gather", &rows_gather);
   m.def("rows_scatter", &rows_scatter);
   m.def("segment_starts", &segment_starts);

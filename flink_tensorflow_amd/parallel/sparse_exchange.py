@@ -169,8 +169,9 @@ class BucketedOwnerExchange(OwnerSparseExchange):
     rows for the gradient direction) with one equal-split ``all_to_all`` — RCCL's grouped
     send/recv with sizes fixed at capture time.  On the GPU every data movement is an
     in-tree kernel: ids are deduplicated by the radix sort (``kernels/sort_segments.hip``),
-    ``owner_buckets`` (``kernels/embedding.hip``) places each id in its owner's bucket (one
-    1024-thread block per owner: wave ballots + an LDS prefix, input order kept), rows move
+    ``owner_buckets`` (``kernels/embedding.hip``) places each id in its owner's bucket (a
+    count pass and a place pass over 4096-id segments x owners: wave ballots + an LDS
+    prefix, input order kept), rows move
     with ``rows_gather`` / ``rows_scatter`` and the owner merges with the static segment sum
     in (id, source rank) order — no ``torch.unique`` / ``sort`` / ``bincount``, no fancy
     indexing, and the merge association of the exact exchange.
@@ -283,10 +284,12 @@ class BucketedOwnerExchange(OwnerSparseExchange):
         if ids.is_cuda:
             from .. import _ext
 
+            H = _ext.hip()
             ids = ids if ids.dtype == torch.int32 else ids.to(torch.int32)
-            _ext.hip().owner_buckets(ids.contiguous().data_ptr(), n, off, V, ws, cap, send.data_ptr(),
-                                     src.data_ptr(), need.data_ptr(), self.over.data_ptr(),
-                                     torch.cuda.current_stream().cuda_stream)
+            counts = torch.empty(ws * H.owner_buckets_segments(n), dtype=torch.int32, device=dev)
+            H.owner_buckets(ids.contiguous().data_ptr(), n, off, V, ws, cap, send.data_ptr(), src.data_ptr(),
+                            need.data_ptr(), self.over.data_ptr(), counts.data_ptr(),
+                            torch.cuda.current_stream().cuda_stream)
             return send, src, cap
         # host: the same placement with torch ops (tests; the loopback communicator)
         loc = ids.long() - off
