@@ -728,6 +728,29 @@ class CompiledFunction(TransformerLowering):
             else:
                 mpad = None
 
+            pp = getattr(x, "pre_params", None)
+            if (mpad is None and xin_shape_override is not None and pp is not None and not pp["resize"]
+                    and _cfg().fuse_preprocess_stem and len(self.steps) == 1 and self.steps[0].kind == "preprocess"
+                    and self.steps[0].outputs[0] is x and _root(out) is out and _coff(out) == 0):
+                # the plan's head preprocess kernel folds into this stem: the conv builds its s2d
+                # patches from the raw uint8 batch (Inception-v3's Conv2d_1a: no resize)
+                self.steps.pop()
+                xu = pp["x"]
+                osc = _eff_scale(out) if out.qscale is not None else None
+
+                def run_u(x=xu, out=out, w_arr=w_arr, b_dev=b_dev, bn=bn, osc=osc, mean=pp["mean"], std=pp["std"],
+                          pads=(pt, pb, pl, pr)):
+                    K.conv2d_direct_u8s2d(x.buf, w_arr, (KHe, KWe), Cout, b_dev, pads, act, mean, std, out=out.buf,
+                                          bn=bn, out_scale=osc)
+
+                # kind "preprocess": still the plan's head, launched per H2D piece by the runner
+                self._emit(node.name, "preprocess", run_u, [xu], [out],
+                           {"impl": "dconv_u8s2d", "conv_out": (N, Ho, Wo, Cout)})
+                self.fused_preprocess = 1
+                self.vals[(last.name, 0)] = out
+                self._alias_fused_outputs(absorbed, out)
+                return
+
             def run_d(xin=xin, out=out, w_arr=w_arr, b_dev=b_dev, bn=bn, mpad=mpad):
                 K.conv2d_direct(xin.buf, w_arr, (KHe, KWe), Cout, b_dev, (sh, sw), (pt, pb, pl, pr), act,
                                 out=_target(out), out_channel_offset=_coff(out), bn=bn,
@@ -1273,6 +1296,9 @@ class CompiledFunction(TransformerLowering):
         out.buf_shape = out_buf_shape
         out.pre_cfg = {"s2d": False}
         out.pre_chain = {n.name for n in chain}
+        # what a stem conv needs to absorb this kernel (dconv_u8s2d): no resize, the affine only
+        out.pre_params = {"x": x, "mean": tuple(mean.tolist()), "std": tuple(std.tolist()),
+                          "resize": size != (x.shape[1], x.shape[2])}
         for n in chain[1:]:
             self._fused.add(n.name)
         mean_t, std_t = tuple(mean.tolist()), tuple(std.tolist())
@@ -2208,6 +2234,7 @@ class CompiledFunction(TransformerLowering):
                 "commuted_pools": getattr(self, "commuted_pools", 0),
                 "sibling_groups": getattr(self, "sibling_groups", 0),
                 "pool_convs": getattr(self, "pool_convs", 0),
+                "fused_preprocess": getattr(self, "fused_preprocess", 0),
                 "activation_bytes": self.activation_bytes,
                 "param_bytes": self.param_bytes(),
                 **({"token_capacity": self.token_cap, "first_token_only_nodes": len(self._cls_nodes)}

@@ -55,6 +55,13 @@ struct DconvParams {
   // 14t - ppt.., cols 16t - ppl..); out-of-range conv positions enter the max as 0
   // (exact after a ReLU).
   int Hp, Wp, ppt, ppl;
+  // U8: the input is the raw uint8 RGB batch [N, Hi, Wi, 3] and the patch is built as the
+  // 2x2 space-to-depth bf16 rows the preprocess kernel would write ((v - mean) * istd at
+  // channel (2a + b) * 3 + c of block (y, x) <- pixel (2y + a, 2x + b); 12..15 and pixels
+  // past the image zero): the preprocess pass and its HBM round trip disappear
+  const uint8_t* xu8;
+  int Hi, Wi;
+  float mean[3], istd[3];
   // byte offset into the patch of each (K-step, lane group) relative to the lane's pixel:
   // (dy * PW + dx) * RB + channel byte of the K segment's tap; host-built so the K loop has
   // no integer divisions (two runtime divides per step used to cost more than its MFMAs)
@@ -109,7 +116,7 @@ FTM_DEVICE u8x16 pool3x3_max_u8(const uint8_t* base, int row_bytes, int px_bytes
   return m;
 }
 
-template <int ES, int BN, int ACT, bool OUT_FP8, bool POOL = false, int WAVES = 4>
+template <int ES, int BN, int ACT, bool OUT_FP8, bool POOL = false, int WAVES = 4, bool U8 = false>
 __global__ __launch_bounds__(WAVES * 64) void dconv_kernel(DconvParams p) {
   static_assert(WAVES == 4 || WAVES == 8, "4 or 8 waves");
   constexpr int NTH = WAVES * 64;
@@ -138,9 +145,41 @@ __global__ __launch_bounds__(WAVES * 64) void dconv_kernel(DconvParams p) {
   uint8_t* Wsm = smem + ((patch_bytes + 1023) & ~1023);   // weights [BN][WP]
 
   // ---- 1. DMA the patch and the filter bank (lane-linear 16-B chunks)
+  if constexpr (U8) {
+    static_assert(ES == 2 && !POOL, "uint8 RGB input: bf16 s2d patch, no pool");
+    const int iy0 = oy0 * p.S - p.ph, ix0 = ox0 * p.S - p.pw;
+    const uint8_t* xb = p.xu8 + (size_t)n * p.Hi * p.Wi * 3;
+    for (int q = tid; q < p.PH * p.PW; q += NTH) {
+      const int py = q / p.PW, px = q - py * p.PW;
+      const int by = iy0 + py, bx = ix0 + px;
+      float v[12];
+#pragma unroll
+      for (int e = 0; e < 12; ++e) v[e] = 0.f;
+      if ((unsigned)by < (unsigned)p.H && (unsigned)bx < (unsigned)p.W) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b2 = 0; b2 < 2; ++b2) {
+            const int r = 2 * by + a, c = 2 * bx + b2;
+            if (r < p.Hi && c < p.Wi) {
+              const uint8_t* src = xb + ((size_t)r * p.Wi + c) * 3;
+#pragma unroll
+              for (int ch = 0; ch < 3; ++ch) v[(a * 2 + b2) * 3 + ch] = ((float)src[ch] - p.mean[ch]) * p.istd[ch];
+            }
+          }
+      }
+      bf16x8 lo, hi;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) lo[e] = f2bf(v[e]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) hi[e] = f2bf(e < 4 ? v[8 + e] : 0.f);
+      *reinterpret_cast<bf16x8*>(Ps + q * 32) = lo;
+      *reinterpret_cast<bf16x8*>(Ps + q * 32 + 16) = hi;
+    }
+  }
   {
     const int cpr = p.RB >> 4;  // 16-B chunks per patch row
-    const int nchunks = p.PH * p.PW * cpr;
+    const int nchunks = U8 ? 0 : p.PH * p.PW * cpr;
     const int iy0 = oy0 * p.S - p.ph, ix0 = ox0 * p.S - p.pw;
     const uint8_t* xb = p.x + (size_t)n * p.H * p.W * p.RB;
     for (int q0 = wave * 64; q0 < nchunks; q0 += NTH) {
@@ -305,6 +344,21 @@ void launch_act(const DconvParams& p, int act, size_t lds, hipStream_t s) {
   }
 }
 
+template <int BN, bool OUT_FP8, int WAVES>
+void launch_u8(const DconvParams& p, int act, size_t lds, hipStream_t s) {
+  dim3 grid(p.N * p.tiles_h * p.tiles_w * p.tiles_n), block(WAVES * 64);
+  static bool done = false;
+  if (!done) {
+    for (auto f : {(const void*)dconv_kernel<2, BN, ACT_NONE, OUT_FP8, false, WAVES, true>,
+                   (const void*)dconv_kernel<2, BN, ACT_RELU, OUT_FP8, false, WAVES, true>})
+      hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    done = true;
+  }
+  if (act == ACT_RELU) hipLaunchKernelGGL((dconv_kernel<2, BN, ACT_RELU, OUT_FP8, false, WAVES, true>), grid, block, lds, s, p);
+  else if (act == ACT_NONE) hipLaunchKernelGGL((dconv_kernel<2, BN, ACT_NONE, OUT_FP8, false, WAVES, true>), grid, block, lds, s, p);
+  else throw std::invalid_argument("dconv: activation must be none/relu");
+}
+
 template <int ES, int BN, bool OUT_FP8, int WAVES>
 void set_lds_limit() {
   static bool done = false;
@@ -417,7 +471,74 @@ void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t 
   FTM_CHECK_LAUNCH();
 }
 
+// The RGB stem straight from the raw uint8 batch (the preprocess kernel fused away): a
+// stride-2 conv already rewritten as a stride-1 conv over the 2x2 space-to-depth input
+// (s2d_stem_weights: [Cout][KH][KW][16] bf16 rows), the patch built from uint8 pixels with
+// the preprocess normalisation.  x: [N, Hi, Wi, 3] uint8; the conv input is [N, ceil(Hi/2),
+// ceil(Wi/2), 16].
+void dconv_u8s2d(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int N, int Hi, int Wi, int Cout, int KH, int KW,
+                 int ph, int pw, int Ho, int Wo, int wp, int ldy, int y_coff, int out_fp8, float out_q, int act, int bn,
+                 float m0, float m1, float m2, float s0, float s1, float s2, uintptr_t stream, int waves) {
+  const int Cin = 16, es = 2, KL = 16;
+  if (bn != 32 && bn != 64) throw std::invalid_argument("dconv_u8s2d: bn must be 32 or 64");
+  const int kb = KH * KW * Cin * es;
+  const int kpad = (kb + 4 * KL - 1) / (4 * KL) * (4 * KL);
+  if (wp != kpad + 16) throw std::invalid_argument("dconv_u8s2d: weight pitch must be round_up(K bytes, 64) + 16");
+  const int oe = out_fp8 ? 16 : 8;
+  if (Cout % oe || ldy % oe || y_coff % oe) throw std::invalid_argument("dconv_u8s2d: Cout/ldy/y_coff alignment");
+  if (!bias || w % 16 || y % 16 || bias % 16) throw std::invalid_argument("dconv_u8s2d: bias / alignment");
+  if (waves != 4 && waves != 8) throw std::invalid_argument("dconv_u8s2d: waves must be 4 or 8");
+  if (waves == 8 && lds_bytes(es, bn, KH, KW, 1, Cin, wp, false, 512) > 160 * 1024) waves = 4;
+  const int npx = waves * 64;
+  const int lds = lds_bytes(es, bn, KH, KW, 1, Cin, wp, false, npx);
+  if (lds > 160 * 1024) throw std::invalid_argument("dconv_u8s2d: tile does not fit LDS");
+  DconvParams p{};
+  p.x = nullptr;
+  p.xu8 = reinterpret_cast<const uint8_t*>(x);
+  p.Hi = Hi; p.Wi = Wi;
+  p.mean[0] = m0; p.mean[1] = m1; p.mean[2] = m2;
+  p.istd[0] = s0; p.istd[1] = s1; p.istd[2] = s2;
+  p.w = reinterpret_cast<const uint8_t*>(w);
+  p.scale = nullptr;
+  p.bias = reinterpret_cast<const float*>(bias);
+  p.y = reinterpret_cast<uint8_t*>(y);
+  p.out_q = out_q;
+  p.N = N; p.H = (Hi + 1) / 2; p.W = (Wi + 1) / 2; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout;
+  p.KH = KH; p.KW = KW; p.S = 1; p.ph = ph; p.pw = pw;
+  p.RB = Cin * es;
+  p.WP = wp;
+  p.ksteps = kpad / (4 * KL);
+  if (p.ksteps > 64) throw std::invalid_argument("dconv_u8s2d: more than 64 K-steps");
+  p.PH = patch_rows(KH, 1, false, npx);
+  p.PW = (TW - 1) + KW;
+  p.ldy = ldy; p.y_coff = y_coff;
+  p.prio = ftm_mfma_prio();
+  for (int st = 0; st < p.ksteps; ++st)
+    for (int fq = 0; fq < 4; ++fq) {
+      const int kb2 = st * 4 * KL + fq * KL;
+      int tap = kb2 / p.RB;
+      const int cb = kb2 - tap * p.RB;
+      if (tap >= KH * KW) tap = 0;
+      const int dy = tap / KW, dx = tap - dy * KW;
+      p.koff[st * 4 + fq] = (dy * p.PW + dx) * p.RB + cb;
+    }
+  p.tiles_h = (Ho + npx / TW - 1) / (npx / TW);
+  p.tiles_w = (Wo + TW - 1) / TW;
+  p.tiles_n = (Cout + bn - 1) / bn;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+#define FTM_U8(BN_, OF_)                                              \
+  do {                                                                \
+    if (waves == 8) launch_u8<BN_, OF_, 8>(p, act, lds, s);            \
+    else launch_u8<BN_, OF_, 4>(p, act, lds, s);                       \
+  } while (0)
+  if (bn == 32) { if (out_fp8) FTM_U8(32, true); else FTM_U8(32, false); }
+  else { if (out_fp8) FTM_U8(64, true); else FTM_U8(64, false); }
+#undef FTM_U8
+  FTM_CHECK_LAUNCH();
+}
+
 void register_dconv(pybind11::module_& m) {
   m.def("dconv", &dconv);
+  m.def("dconv_u8s2d", &dconv_u8s2d);
   m.def("dconv_lds_bytes", &dconv_lds_bytes);
 }

@@ -303,6 +303,7 @@ def test_inception_v3_fp8_plan_gpu():
     # Conv2d_2b + MaxPool_3a stay apart: the pooled tiling would waste > 15 % of the conv work;
     # MaxPool_3a + Conv2d_3b_1x1 run as one kernel (kernels/poolconv.hip)
     assert dev.summary()["fused_pools"] == 0 and dev.summary()["pool_convs"] == 1
+    assert dev.summary()["fused_preprocess"] == 1  # Conv2d_1a reads the raw uint8 batch
     lh = host({"images:0": img})[0]
     ld = dev({"images:0": img.to(DEV)})[0].cpu()
     assert F.cosine_similarity(lh.flatten(), ld.flatten(), dim=0) > 0.99
@@ -351,3 +352,25 @@ def test_pool_conv1x1_fp8_gpu(cout, act):
     pooled = Q.pool2d_nhwc_fp8(x.to(DEV), (3, 3), (2, 2), (0, 0, 0, 0), "max")
     assert torch.equal(pooled.cpu(), Q.to_fp8_bytes(F.max_pool2d(Q.from_fp8_bytes(x).permute(0, 3, 1, 2), 3, 2)
                                                    .permute(0, 2, 3, 1)))
+
+
+@pytest.mark.gpu
+def test_stem_from_raw_uint8_equals_preprocess_then_conv_gpu():
+    """The s2d RGB stem built straight from the raw uint8 batch (``dconv_u8s2d``, the
+    resize-free preprocess folded in) equals the preprocess kernel's s2d output fed to the
+    same direct conv, bit for bit (odd image size: the last block row / column is zero)."""
+    from flink_tensorflow_amd.ops import kernels as K
+
+    torch.manual_seed(2)
+    N, Hi, Wi, Cout = 3, 37, 35, 32
+    x = torch.randint(0, 256, (N, Hi, Wi, 3), dtype=torch.uint8)
+    w = torch.randn(3, 3, 3, Cout) / 4
+    b = torch.randn(Cout) * 0.1
+    w2, bp = K.s2d_stem_weights(w, Hi, Wi, (0, 0, 0, 0))
+    w_arr = K.dconv_bf16_weight_bytes(w2, 32).to(DEV)
+    mean, std = (128.0, 120.0, 110.0), (64.0, 60.0, 70.0)
+    xs = K.preprocess_images(x.to(DEV), (Hi, Wi), mean, std, s2d=True)
+    ref = K.conv2d_direct(xs, w_arr, (2, 2), Cout, b.to(DEV), (1, 1), bp, "relu", bn=32, out_scale=0.05)
+    got = K.conv2d_direct_u8s2d(x.to(DEV), w_arr, (2, 2), Cout, b.to(DEV), bp, "relu", mean, std, bn=32,
+                                out_scale=0.05)
+    assert torch.equal(got, ref)
