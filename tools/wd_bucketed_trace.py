@@ -64,7 +64,9 @@ def main():
                       "replay_ms_per_step": round((t2 - t1) * 1e3 / max(1, a.replays), 3),
                       "captured": t._graph is not None, "bucket_capacities": {str(k): v for k, v in ex._caps.items()},
                       "overflow": int(ex.over.item())}), flush=True)
+    del g  # the captured graph (RCCL kernels inside) goes before the communicator
     t.close()
+    torch.cuda.synchronize(dev)
     comm.destroy()
 
 
