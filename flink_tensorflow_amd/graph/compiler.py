@@ -1333,9 +1333,6 @@ class CompiledFunction(TransformerLowering):
             return
         if mode == "avg" and (sh, sw) == (1, 1) and self._commute_avgpool(node, x, (kh, kw), (pt, pb, pl, pr)):
             return
-        if (x.qscale is not None and mode == "max" and (kh, kw, sh, sw) == (3, 3, 2, 2)
-                and (pt, pb, pl, pr) == (0, 0, 0, 0) and self._lower_pool_conv(node, x, Ho, Wo)):
-            return
         if x.qscale is not None and C % 16 == 0:
             # pooled values stay within the input range: keep the input scale, requantise
             # only when written into a concat buffer of another scale
@@ -1358,49 +1355,6 @@ class CompiledFunction(TransformerLowering):
 
         self._emit(node.name, "pool", run, [xin], [out])
         self.vals[(node.name, 0)] = out
-
-    def _lower_pool_conv(self, node: Node, x: Val, Hp: int, Wp: int) -> bool:
-        """An fp8 3x3 / stride-2 VALID MaxPool whose only consumer is a 1x1 fp8 conv
-        (Inception-v3's MaxPool_3a -> Conv2d_3b_1x1) as ONE kernel
-        (``kernels/poolconv.hip``): the pooled tensor is never written."""
-        if not _cfg().pool_conv_fusion or self.device.type != "cuda" or x.phys_c or x.rows is not None:
-            return False
-        if any(TensorName.parse(f).name == node.name for f in self.fetch_names):
-            return False
-        cons = [c for c in dict.fromkeys(self.cons.get(node.name, [])) if c not in self._fused]
-        if len(cons) != 1:
-            return False
-        c = self.graph[cons[0]]
-        m = self._pw_member(c, x, (node.name, 0), max_cout=128)
-        N, H, W, Cin = x.shape
-        if m is None or not F8.pool_conv1x1_fp8_supported(Cin, m["Cout"]):
-            return False
-        last, Cout = m["last"], m["Cout"]
-        o_scale = self._qscale(last.name) if self._fp8_consumers_ok(last.name) else None
-        if o_scale is None:
-            return False
-        wq, wsc = F8.quantize_weight(m["w"])
-        wq_dev = self._dev(wq)
-        cs_dev = self._dev(wsc * x.qscale, torch.float32)
-        b_dev = self._dev(m["bias"] if m["bias"] is not None else torch.zeros(Cout), torch.float32)
-        self.params += [wq_dev, cs_dev, b_dev]
-        out = self._new((N, Hp, Wp, Cout), torch.uint8)
-        out.qscale = o_scale
-        act = m["act"]
-
-        def run(x=x, out=out, wq=wq_dev, cs=cs_dev, b=b_dev, act=act):
-            F8.pool_conv1x1_fp8(_view(x), wq, cs, b, act, out_scale=_eff_scale(out), out=_target(out),
-                                out_channel_offset=_coff(out))
-
-        self._emit(node.name + "+" + c.name, "conv_fp8", run, [x], [out], {"impl": "pool_conv1x1_fp8"})
-        self._fused.add(c.name)
-        for a in m["absorbed"]:
-            self._fused.add(a.name)
-        self.vals[(last.name, 0)] = out
-        self._alias_fused_outputs(m["absorbed"], out)
-        self.fp8_layers += 1
-        self.pool_convs = getattr(self, "pool_convs", 0) + 1
-        return True
 
     # ---- horizontal fusion of sibling pointwise convs (Inception module heads)
     def _pw_member(self, c: Node, x: Val, src, max_cout: int | None = None):
@@ -2233,7 +2187,6 @@ class CompiledFunction(TransformerLowering):
                 "conv_lite": getattr(self, "conv_lite_layers", 0),
                 "commuted_pools": getattr(self, "commuted_pools", 0),
                 "sibling_groups": getattr(self, "sibling_groups", 0),
-                "pool_convs": getattr(self, "pool_convs", 0),
                 "fused_preprocess": getattr(self, "fused_preprocess", 0),
                 "activation_bytes": self.activation_bytes,
                 "param_bytes": self.param_bytes(),

@@ -27,7 +27,6 @@ void register_sort_segments(pybind11::module_& m);
 void register_pw_res(pybind11::module_& m);
 void register_gemm_train(pybind11::module_& m);
 void register_wino3x3(pybind11::module_& m);
-void register_poolconv(pybind11::module_& m);
 
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "flink_tensorflow_amd CDNA4 (gfx950) kernels";
@@ -50,7 +49,6 @@ PYBIND11_MODULE(_hip, m) {
   register_pw_res(m);
   register_gemm_train(m);
   register_wino3x3(m);
-  register_poolconv(m);
   // Streams owned by the framework (not torch's round-robin pool of 32 per device): a pooled
   // stream handed to a runner can be the very stream another thread is capturing a hipGraph
   // on, and then that thread's launches land in the capture (or are rejected).

@@ -279,42 +279,3 @@ def global_avgpool_fp8(x: torch.Tensor, scale: float, out=None) -> torch.Tensor:
         return out
     return y
 
-
-def pool_conv1x1_fp8_supported(cin: int, cout: int) -> bool:
-    return cin == 64 and cout in (64, 80, 96, 128)
-
-
-def pool_conv1x1_fp8(x: torch.Tensor, wq: torch.Tensor, chan_scale: torch.Tensor, bias: torch.Tensor, act=None,
-                     out_scale: float = 1.0, out: torch.Tensor | None = None,
-                     out_channel_offset: int = 0) -> torch.Tensor:
-    """3x3 / stride-2 VALID max pool of the e4m3 ``x`` [N, H, W, 64] and the 1x1 conv that
-    consumes it, in one kernel (``kernels/poolconv.hip``): ``wq`` [Cout, 64] e4m3,
-    ``chan_scale`` = w_scale * x_scale, e4m3 output with ``out_scale``.  The pooled tensor
-    never reaches memory."""
-    N, H, W, Cin = x.shape
-    Cout = wq.shape[0]
-    Hp, Wp = (H - 3) // 2 + 1, (W - 3) // 2 + 1
-    if out is None:
-        out = torch.empty((N, Hp, Wp, Cout), dtype=torch.uint8, device=x.device)
-        out_channel_offset = 0
-    a = act_code(act)
-    if x.is_cuda:
-        if not pool_conv1x1_fp8_supported(Cin, Cout):
-            raise ValueError(f"pool_conv1x1_fp8: Cin 64 and Cout in (64, 80, 96, 128), got {Cin}, {Cout}")
-        _check(x, "x", torch.uint8, x.device)
-        _check(wq, "wq", torch.uint8, x.device)
-        _check(chan_scale, "chan_scale", torch.float32, x.device)
-        _check(bias, "bias", torch.float32, x.device)
-        _check(out, "out", torch.uint8, x.device)
-        if tuple(out.shape[:3]) != (N, Hp, Wp) or wq.shape[1] != Cin:
-            raise ValueError(f"pool_conv1x1_fp8: out {tuple(out.shape)} / wq {tuple(wq.shape)} for x {tuple(x.shape)}")
-        _hip().pool_conv1x1_fp8(x.data_ptr(), wq.data_ptr(), chan_scale.data_ptr(), bias.data_ptr(), out.data_ptr(), N,
-                                H, W, Cin, Cout, out.shape[-1], out_channel_offset, 1.0 / out_scale, a, _stream())
-        return out
-    # host reference: the unfused pair on dequantised values
-    xf = from_fp8_bytes(x).permute(0, 3, 1, 2)
-    pooled = F.max_pool2d(xf, 3, 2).permute(0, 2, 3, 1)
-    y = pooled.reshape(-1, Cin) @ from_fp8_bytes(wq).t() * chan_scale.cpu().float() + bias.cpu().float()
-    y = _apply_act_ref(y, a).reshape(N, Hp, Wp, Cout)
-    out[..., out_channel_offset:out_channel_offset + Cout] = to_fp8_bytes(y / out_scale)
-    return out
