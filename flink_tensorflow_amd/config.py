@@ -41,7 +41,7 @@ class EngineConfig:
     # measured-fastest choice; these switch a fusion OFF for A/B runs.  Variants measured
     # slower were removed with their kernels (graph/compiler.py LITE_TILE comment)
     sibling_conv_fusion: bool = True   # fp8: an Inception module's sibling 1x1 convs as one multi-output GEMM
-    fuse_preprocess_stem: bool = True  # preprocess (resize + normalise) folded into the s2d RGB stem conv
+    fuse_preprocess_stem: bool = True  # resize-free preprocess folded into the s2d RGB stem conv
     fuse_block_tails: bool = True      # ResNet block boundary: expand + next reduce in one kernel
     decimate_tails: bool = True        # stage-1 tail output stored at the stride-2 reader's pixels
     pw_res_kernel: bool = True         # identity-residual expand convs on the persistent kernel

@@ -729,30 +729,24 @@ class CompiledFunction(TransformerLowering):
                 mpad = None
 
             pp = getattr(x, "pre_params", None)
-            if (xin_shape_override is not None and pp is not None and _cfg().fuse_preprocess_stem
-                    and len(self.steps) == 1 and self.steps[0].kind == "preprocess"
+            if (mpad is None and xin_shape_override is not None and pp is not None and not pp["resize"]
+                    and _cfg().fuse_preprocess_stem and len(self.steps) == 1 and self.steps[0].kind == "preprocess"
                     and self.steps[0].outputs[0] is x and _root(out) is out and _coff(out) == 0):
                 # the plan's head preprocess kernel folds into this stem: the conv builds its s2d
-                # patches from the raw uint8 batch, resize + normalisation included (Inception-v3's
-                # Conv2d_1a; ResNet-50's conv1 with its fused max pool)
+                # patches from the raw uint8 batch (Inception-v3's Conv2d_1a: no resize)
                 self.steps.pop()
                 xu = pp["x"]
                 osc = _eff_scale(out) if out.qscale is not None else None
 
-                def run_u(x=xu, out=out, w_arr=w_arr, b_dev=b_dev, bn=bn, osc=osc, pp=pp, pads=(pt, pb, pl, pr),
-                          mpad=mpad):
-                    K.conv2d_direct_u8s2d(x.buf, w_arr, (KHe, KWe), Cout, b_dev, pads, act, pp["mean"], pp["std"],
-                                          out=out.buf, bn=bn, out_scale=osc, resize_to=pp["size"],
-                                          align_corners=pp["align"], half_pixel_centers=pp["half"], maxpool_pad=mpad)
+                def run_u(x=xu, out=out, w_arr=w_arr, b_dev=b_dev, bn=bn, osc=osc, mean=pp["mean"], std=pp["std"],
+                          pads=(pt, pb, pl, pr)):
+                    K.conv2d_direct_u8s2d(x.buf, w_arr, (KHe, KWe), Cout, b_dev, pads, act, mean, std, out=out.buf,
+                                          bn=bn, out_scale=osc)
 
                 # kind "preprocess": still the plan's head, launched per H2D piece by the runner
                 self._emit(node.name, "preprocess", run_u, [xu], [out],
                            {"impl": "dconv_u8s2d", "conv_out": (N, Ho, Wo, Cout)})
                 self.fused_preprocess = 1
-                if pool is not None:
-                    self.vals[(pool[0].name, 0)] = out
-                    self.fused_pools = getattr(self, "fused_pools", 0) + 1
-                    return
                 self.vals[(last.name, 0)] = out
                 self._alias_fused_outputs(absorbed, out)
                 return
@@ -1303,8 +1297,8 @@ class CompiledFunction(TransformerLowering):
         out.pre_cfg = {"s2d": False}
         out.pre_chain = {n.name for n in chain}
         # what a stem conv needs to absorb this kernel (dconv_u8s2d): no resize, the affine only
-        out.pre_params = {"x": x, "mean": tuple(mean.tolist()), "std": tuple(std.tolist()), "size": size,
-                          "align": align, "half": half}
+        out.pre_params = {"x": x, "mean": tuple(mean.tolist()), "std": tuple(std.tolist()),
+                          "resize": size != (x.shape[1], x.shape[2])}
         for n in chain[1:]:
             self._fused.add(n.name)
         mean_t, std_t = tuple(mean.tolist()), tuple(std.tolist())

@@ -62,10 +62,6 @@ struct DconvParams {
   const uint8_t* xu8;
   int Hi, Wi;
   float mean[3], istd[3];
-  // ... optionally through the TF ResizeBilinear the preprocess kernel applies (resized
-  // image Hr x Wr; nn_misc.hip resize_pixel's arithmetic, bit for bit)
-  int resize, half_pixel, Hr, Wr;
-  float sy, sx;
   // byte offset into the patch of each (K-step, lane group) relative to the lane's pixel:
   // (dy * PW + dx) * RB + channel byte of the K segment's tap; host-built so the K loop has
   // no integer divisions (two runtime divides per step used to cost more than its MFMAs)
@@ -120,28 +116,6 @@ FTM_DEVICE u8x16 pool3x3_max_u8(const uint8_t* base, int row_bytes, int px_bytes
   return m;
 }
 
-// One resized + normalised RGB pixel of the uint8 image (nn_misc.hip resize_pixel, same
-// arithmetic, so the fused stem sees exactly the preprocess kernel's values).
-FTM_DEVICE void resize_px(const uint8_t* img, const DconvParams& q, int oy, int ox, float* out) {
-  float fy = q.half_pixel ? (oy + 0.5f) * q.sy - 0.5f : oy * q.sy;
-  float fx = q.half_pixel ? (ox + 0.5f) * q.sx - 0.5f : ox * q.sx;
-  float fy0 = floorf(fy), fx0 = floorf(fx);
-  int y0 = max((int)fy0, 0), x0 = max((int)fx0, 0);
-  int y1 = min(y0 + 1, q.Hi - 1), x1 = min(x0 + 1, q.Wi - 1);
-  float wy = fminf(fmaxf(fy - (q.half_pixel ? (float)y0 : fy0), 0.f), 1.f);
-  float wx = fminf(fmaxf(fx - (q.half_pixel ? (float)x0 : fx0), 0.f), 1.f);
-  const uint8_t* p00 = img + ((size_t)y0 * q.Wi + x0) * 3;
-  const uint8_t* p01 = img + ((size_t)y0 * q.Wi + x1) * 3;
-  const uint8_t* p10 = img + ((size_t)y1 * q.Wi + x0) * 3;
-  const uint8_t* p11 = img + ((size_t)y1 * q.Wi + x1) * 3;
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    float top = (float)p00[c] + ((float)p01[c] - (float)p00[c]) * wx;
-    float bot = (float)p10[c] + ((float)p11[c] - (float)p10[c]) * wx;
-    out[c] = (top + (bot - top) * wy - q.mean[c]) * q.istd[c];
-  }
-}
-
 template <int ES, int BN, int ACT, bool OUT_FP8, bool POOL = false, int WAVES = 4, bool U8 = false>
 __global__ __launch_bounds__(WAVES * 64) void dconv_kernel(DconvParams p) {
   static_assert(WAVES == 4 || WAVES == 8, "4 or 8 waves");
@@ -172,7 +146,7 @@ __global__ __launch_bounds__(WAVES * 64) void dconv_kernel(DconvParams p) {
 
   // ---- 1. DMA the patch and the filter bank (lane-linear 16-B chunks)
   if constexpr (U8) {
-    static_assert(ES == 2, "uint8 RGB input: bf16 s2d patch");
+    static_assert(ES == 2 && !POOL, "uint8 RGB input: bf16 s2d patch, no pool");
     const int iy0 = oy0 * p.S - p.ph, ix0 = ox0 * p.S - p.pw;
     const uint8_t* xb = p.xu8 + (size_t)n * p.Hi * p.Wi * 3;
     for (int q = tid; q < p.PH * p.PW; q += NTH) {
@@ -187,14 +161,10 @@ __global__ __launch_bounds__(WAVES * 64) void dconv_kernel(DconvParams p) {
 #pragma unroll
           for (int b2 = 0; b2 < 2; ++b2) {
             const int r = 2 * by + a, c = 2 * bx + b2;
-            if (r < p.Hr && c < p.Wr) {
-              if (p.resize) {
-                resize_px(xb, p, r, c, v + (a * 2 + b2) * 3);
-              } else {
-                const uint8_t* src = xb + ((size_t)r * p.Wi + c) * 3;
+            if (r < p.Hi && c < p.Wi) {
+              const uint8_t* src = xb + ((size_t)r * p.Wi + c) * 3;
 #pragma unroll
-                for (int ch = 0; ch < 3; ++ch) v[(a * 2 + b2) * 3 + ch] = ((float)src[ch] - p.mean[ch]) * p.istd[ch];
-              }
+              for (int ch = 0; ch < 3; ++ch) v[(a * 2 + b2) * 3 + ch] = ((float)src[ch] - p.mean[ch]) * p.istd[ch];
             }
           }
       }
@@ -380,21 +350,13 @@ void launch_u8(const DconvParams& p, int act, size_t lds, hipStream_t s) {
   static bool done = false;
   if (!done) {
     for (auto f : {(const void*)dconv_kernel<2, BN, ACT_NONE, OUT_FP8, false, WAVES, true>,
-                   (const void*)dconv_kernel<2, BN, ACT_RELU, OUT_FP8, false, WAVES, true>,
-                   (const void*)dconv_kernel<2, BN, ACT_RELU, OUT_FP8, true, WAVES, true>})
+                   (const void*)dconv_kernel<2, BN, ACT_RELU, OUT_FP8, false, WAVES, true>})
       hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     done = true;
   }
-  if (p.Hp > 0) {  // fused max pool (the ResNet stem)
-    if (act != ACT_RELU) throw std::invalid_argument("dconv_u8s2d: fused pool needs a ReLU conv");
-    hipLaunchKernelGGL((dconv_kernel<2, BN, ACT_RELU, OUT_FP8, true, WAVES, true>), grid, block, lds, s, p);
-  } else if (act == ACT_RELU) {
-    hipLaunchKernelGGL((dconv_kernel<2, BN, ACT_RELU, OUT_FP8, false, WAVES, true>), grid, block, lds, s, p);
-  } else if (act == ACT_NONE) {
-    hipLaunchKernelGGL((dconv_kernel<2, BN, ACT_NONE, OUT_FP8, false, WAVES, true>), grid, block, lds, s, p);
-  } else {
-    throw std::invalid_argument("dconv: activation must be none/relu");
-  }
+  if (act == ACT_RELU) hipLaunchKernelGGL((dconv_kernel<2, BN, ACT_RELU, OUT_FP8, false, WAVES, true>), grid, block, lds, s, p);
+  else if (act == ACT_NONE) hipLaunchKernelGGL((dconv_kernel<2, BN, ACT_NONE, OUT_FP8, false, WAVES, true>), grid, block, lds, s, p);
+  else throw std::invalid_argument("dconv: activation must be none/relu");
 }
 
 template <int ES, int BN, bool OUT_FP8, int WAVES>
@@ -514,12 +476,9 @@ void dconv(uintptr_t x, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t 
 // (s2d_stem_weights: [Cout][KH][KW][16] bf16 rows), the patch built from uint8 pixels with
 // the preprocess normalisation.  x: [N, Hi, Wi, 3] uint8; the conv input is [N, ceil(Hi/2),
 // ceil(Wi/2), 16].
-// Hr, Wr: the resized image (== Hi, Wi: no resize); Hp > 0: fused 3x3 / stride-2 max pool
-// as in dconv (pool pads ppt, ppl).
-void dconv_u8s2d(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int N, int Hi, int Wi, int Hr, int Wr,
-                 int align_corners, int half_pixel, int Cout, int KH, int KW, int ph, int pw, int Ho, int Wo, int wp,
-                 int ldy, int y_coff, int out_fp8, float out_q, int act, int bn, float m0, float m1, float m2, float s0,
-                 float s1, float s2, uintptr_t stream, int Hp, int Wp, int ppt, int ppl, int waves) {
+void dconv_u8s2d(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int N, int Hi, int Wi, int Cout, int KH, int KW,
+                 int ph, int pw, int Ho, int Wo, int wp, int ldy, int y_coff, int out_fp8, float out_q, int act, int bn,
+                 float m0, float m1, float m2, float s0, float s1, float s2, uintptr_t stream, int waves) {
   const int Cin = 16, es = 2, KL = 16;
   if (bn != 32 && bn != 64) throw std::invalid_argument("dconv_u8s2d: bn must be 32 or 64");
   const int kb = KH * KW * Cin * es;
@@ -529,20 +488,14 @@ void dconv_u8s2d(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int N, i
   if (Cout % oe || ldy % oe || y_coff % oe) throw std::invalid_argument("dconv_u8s2d: Cout/ldy/y_coff alignment");
   if (!bias || w % 16 || y % 16 || bias % 16) throw std::invalid_argument("dconv_u8s2d: bias / alignment");
   if (waves != 4 && waves != 8) throw std::invalid_argument("dconv_u8s2d: waves must be 4 or 8");
-  const bool pool = Hp > 0;
-  if (waves == 8 && lds_bytes(es, bn, KH, KW, 1, Cin, wp, pool, 512) > 160 * 1024) waves = 4;
+  if (waves == 8 && lds_bytes(es, bn, KH, KW, 1, Cin, wp, false, 512) > 160 * 1024) waves = 4;
   const int npx = waves * 64;
-  const int pool_rows = waves == 8 ? 14 : 7;
-  const int lds = lds_bytes(es, bn, KH, KW, 1, Cin, wp, pool, npx);
+  const int lds = lds_bytes(es, bn, KH, KW, 1, Cin, wp, false, npx);
   if (lds > 160 * 1024) throw std::invalid_argument("dconv_u8s2d: tile does not fit LDS");
   DconvParams p{};
   p.x = nullptr;
   p.xu8 = reinterpret_cast<const uint8_t*>(x);
-  p.Hi = Hi; p.Wi = Wi; p.Hr = Hr; p.Wr = Wr;
-  p.resize = Hr != Hi || Wr != Wi;
-  p.half_pixel = half_pixel;
-  p.sy = (align_corners && Hr > 1) ? (float)(Hi - 1) / (Hr - 1) : (float)Hi / Hr;
-  p.sx = (align_corners && Wr > 1) ? (float)(Wi - 1) / (Wr - 1) : (float)Wi / Wr;
+  p.Hi = Hi; p.Wi = Wi;
   p.mean[0] = m0; p.mean[1] = m1; p.mean[2] = m2;
   p.istd[0] = s0; p.istd[1] = s1; p.istd[2] = s2;
   p.w = reinterpret_cast<const uint8_t*>(w);
@@ -550,17 +503,16 @@ void dconv_u8s2d(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int N, i
   p.bias = reinterpret_cast<const float*>(bias);
   p.y = reinterpret_cast<uint8_t*>(y);
   p.out_q = out_q;
-  p.N = N; p.H = (Hr + 1) / 2; p.W = (Wr + 1) / 2; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout;
+  p.N = N; p.H = (Hi + 1) / 2; p.W = (Wi + 1) / 2; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout;
   p.KH = KH; p.KW = KW; p.S = 1; p.ph = ph; p.pw = pw;
   p.RB = Cin * es;
   p.WP = wp;
   p.ksteps = kpad / (4 * KL);
   if (p.ksteps > 64) throw std::invalid_argument("dconv_u8s2d: more than 64 K-steps");
-  p.PH = patch_rows(KH, 1, pool, npx);
-  p.PW = (pool ? TW : TW - 1) + KW;
+  p.PH = patch_rows(KH, 1, false, npx);
+  p.PW = (TW - 1) + KW;
   p.ldy = ldy; p.y_coff = y_coff;
   p.prio = ftm_mfma_prio();
-  p.Hp = Hp; p.Wp = Wp; p.ppt = ppt; p.ppl = ppl;
   for (int st = 0; st < p.ksteps; ++st)
     for (int fq = 0; fq < 4; ++fq) {
       const int kb2 = st * 4 * KL + fq * KL;
@@ -570,14 +522,8 @@ void dconv_u8s2d(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int N, i
       const int dy = tap / KW, dx = tap - dy * KW;
       p.koff[st * 4 + fq] = (dy * p.PW + dx) * p.RB + cb;
     }
-  if (pool) {
-    if (ppt < 0 || ppt > 1 || ppl < 0 || ppl > 1) throw std::invalid_argument("dconv_u8s2d: pool padding must be 0/1");
-    p.tiles_h = (Hp + pool_rows - 1) / pool_rows;
-    p.tiles_w = (Wp + 7) / 8;
-  } else {
-    p.tiles_h = (Ho + npx / TW - 1) / (npx / TW);
-    p.tiles_w = (Wo + TW - 1) / TW;
-  }
+  p.tiles_h = (Ho + npx / TW - 1) / (npx / TW);
+  p.tiles_w = (Wo + TW - 1) / TW;
   p.tiles_n = (Cout + bn - 1) / bn;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 #define FTM_U8(BN_, OF_)                                              \

@@ -1159,41 +1159,29 @@ def conv2d_direct(x: torch.Tensor, w_arr: torch.Tensor, kshape, Cout: int, bias:
 
 def conv2d_direct_u8s2d(x_u8: torch.Tensor, w_arr: torch.Tensor, kshape, Cout: int, bias: torch.Tensor, pad, act,
                         mean, std, out: torch.Tensor | None = None, bn: int = 64, out_scale: float | None = None,
-                        waves: int | None = None, resize_to=None, align_corners: bool = False,
-                        half_pixel_centers: bool = False, maxpool_pad: tuple | None = None,
-                        pool_rows: int | None = None) -> torch.Tensor:
+                        waves: int | None = None) -> torch.Tensor:
     """The s2d RGB stem (``s2d_stem_weights``) straight from the raw uint8 batch ``x_u8``
-    [N, Hi, Wi, 3]: the kernel builds each patch as the space-to-depth rows the preprocess
-    kernel would write — TF ResizeBilinear to ``resize_to`` (same arithmetic), then
-    (v - mean) / std — so the preprocess pass and its bf16 tensor disappear.  ``pad``: the
-    block-space pads; ``maxpool_pad``: a fused 3x3 / stride-2 max pool as in
-    ``conv2d_direct`` (the ResNet stem).  Device-only."""
+    [N, Hi, Wi, 3]: the kernel builds each patch as the normalised space-to-depth rows the
+    preprocess kernel would write ((v - mean) / std, no resize), so the preprocess pass and
+    its bf16 tensor disappear.  ``pad``: the block-space pads; device-only."""
     N, Hi, Wi, _ = x_u8.shape
-    Hr, Wr = tuple(resize_to) if resize_to is not None else (Hi, Wi)
     KH, KW = kshape
     pt, pb, pl, pr = pad
-    Hb, Wb = (Hr + 1) // 2, (Wr + 1) // 2
+    Hb, Wb = (Hi + 1) // 2, (Wi + 1) // 2
     Ho, Wo = conv_out_hw(Hb, Wb, KH, KW, 1, 1, pt, pl, 1, 1, pb, pr)
-    Hp = Wp = ppt = ppl = 0
-    oh, ow = Ho, Wo
-    if maxpool_pad is not None:
-        ppt, ppb, ppl, ppr = maxpool_pad
-        Hp, Wp = (Ho + ppt + ppb - 3) // 2 + 1, (Wo + ppl + ppr - 3) // 2 + 1
-        oh, ow = Hp, Wp
     out_fp8 = out_scale is not None
     if out is None:
-        out = torch.empty((N, oh, ow, Cout), dtype=torch.uint8 if out_fp8 else torch.bfloat16, device=x_u8.device)
-    if tuple(out.shape[:3]) != (N, oh, ow) or out.shape[3] < Cout:
-        raise ValueError(f"conv2d_direct_u8s2d: out {tuple(out.shape)} cannot hold [{N},{oh},{ow},{Cout}]")
+        out = torch.empty((N, Ho, Wo, Cout), dtype=torch.uint8 if out_fp8 else torch.bfloat16, device=x_u8.device)
+    if tuple(out.shape[:3]) != (N, Ho, Wo) or out.shape[3] < Cout:
+        raise ValueError(f"conv2d_direct_u8s2d: out {tuple(out.shape)} cannot hold [{N},{Ho},{Wo},{Cout}]")
     _check(x_u8, "x", torch.uint8, x_u8.device)
     _check(w_arr, "w", torch.uint8, x_u8.device)
     _check(bias, "bias", torch.float32, x_u8.device)
     _check(out, "out", torch.uint8 if out_fp8 else torch.bfloat16, x_u8.device)
-    _hip().dconv_u8s2d(x_u8.data_ptr(), w_arr.data_ptr(), bias.data_ptr(), out.data_ptr(), N, Hi, Wi, Hr, Wr,
-                       int(align_corners), int(half_pixel_centers), Cout, KH, KW, pt, pl, Ho, Wo, w_arr.shape[1],
-                       out.shape[3], 0, int(out_fp8), 1.0 / out_scale if out_fp8 else 1.0, act_code(act), bn,
-                       float(mean[0]), float(mean[1]), float(mean[2]), 1.0 / std[0], 1.0 / std[1], 1.0 / std[2],
-                       _stream(), Hp, Wp, ppt, ppl, _dconv_waves(waves, pool_rows, bn))
+    _hip().dconv_u8s2d(x_u8.data_ptr(), w_arr.data_ptr(), bias.data_ptr(), out.data_ptr(), N, Hi, Wi, Cout, KH, KW, pt,
+                       pl, Ho, Wo, w_arr.shape[1], out.shape[3], 0, int(out_fp8), 1.0 / out_scale if out_fp8 else 1.0,
+                       act_code(act), bn, float(mean[0]), float(mean[1]), float(mean[2]), 1.0 / std[0], 1.0 / std[1],
+                       1.0 / std[2], _stream(), _dconv_waves(waves, None, bn))
     return out
 
 

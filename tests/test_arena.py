@@ -202,25 +202,3 @@ def test_interleaved_head_pieces_match_whole_batch_gpu(small_graph):
         torch.testing.assert_close(x.outputs[0][: x.n], y.outputs[0][: y.n])
         assert torch.equal(x.outputs[1][: x.n], y.outputs[1][: y.n])
 
-
-@pytest.mark.gpu
-def test_resnet_stem_reads_raw_uint8_gpu():
-    """ResNet's plan head: the bilinear-resize preprocess folded into the pool-fused s2d stem
-    (``fuse_preprocess_stem``) gives the same logits as the separate preprocess kernel."""
-    from flink_tensorflow_amd import config as C
-    from flink_tensorflow_amd.models.zoo.resnet import resnet50_graph_def
-
-    dev = torch.device("cuda", 0)
-    g = Graph.from_graph_def(resnet50_graph_def(depth=26, image_hw=(48, 48), num_classes=32))
-    feeds = {"images:0": ((4, 64, 64, 3), "UINT8")}
-    imgs = torch.randint(0, 256, (4, 64, 64, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(3))
-    outs = []
-    for on in (True, False):
-        C.set_current(C.EngineConfig(fuse_preprocess_stem=on))
-        try:
-            p = CompiledFunction(g, feeds, ["logits:0"], dev, strict=True)
-            assert p.summary()["fused_preprocess"] == int(on)
-            outs.append(p({"images:0": imgs.to(dev)})[0].float().cpu())
-        finally:
-            C.set_current(C.EngineConfig())
-    assert torch.equal(outs[0], outs[1])
