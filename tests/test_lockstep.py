@@ -213,3 +213,41 @@ def test_fused_agreed_step_gpu():
     pieces = [o for o in out if o[0] == "piece"]
     assert any(len(p[4]) == 0 for p in pieces if p[3] == 1)  # rank 1 ran empty steps
     assert sorted(i for p in pieces for i in p[4]) == list(range(len(recs)))
+
+
+def _reference_p(recs, pieces_by_step, P) -> str:
+    from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, WideDeepTrainer
+
+    t = WideDeepTrainer(WideDeepConfig.tiny(), device="cpu", seed=3)
+    t.open()
+    for s in sorted(pieces_by_step):
+        t.train_pieces([[recs[i] for i in pieces_by_step[s].get(r, [])] for r in range(P)])
+    return _digest(t.model)
+
+
+def test_idle_rank_and_three_ranks_match_reference():
+    """P = 3 with a keyed skew that starves rank 2 completely (it never receives a record:
+    it only heartbeats and joins every step with an empty piece) and gives rank 0 twice
+    rank 1's share: no hang, all three replicas bit-identical to the 1-rank reference."""
+    from flink_tensorflow_amd.parallel.fake import FakeCommunicator
+
+    P = 3
+    recs = _records(6 * BATCH + 5)
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(P)
+    env.enable_job_communicator(True, communicator=FakeCommunicator)
+    clicks = env.add_source(CollectionSource(recs, delay_s=0.0005), "clicks", parallelism=1) \
+        .partition_custom(lambda k, n: k, lambda r: 0 if r[4] % 3 else 1)
+    ticks = env.add_source(CollectionSource([]), "control", parallelism=1)
+    sink = clicks.connect(ticks).process(_Logged()).name("trainer").run_in_processes().collect_into()
+    env.execute("lockstep-p3")
+    out = sink.results()
+    digests = [o for o in out if o[0] == "digest"]
+    assert sorted(d[1] for d in digests) == [0, 1, 2]
+    assert len({(d[2], d[3]) for d in digests}) == 1  # three bit-identical replicas, same step count
+    by_step: dict = {}
+    for _, att, step, rank, ids, counts in (o for o in out if o[0] == "piece"):
+        by_step.setdefault(step, {})[rank] = ids
+    assert sorted(by_step) == list(range(1, digests[0][2] + 1))
+    assert all(len(s.get(2, [])) == 0 for s in by_step.values())  # rank 2 never had data
+    assert sorted(i for s in by_step.values() for ids in s.values() for i in ids) == list(range(len(recs)))
+    assert _reference_p(recs, by_step, P) == digests[0][3]
