@@ -43,7 +43,6 @@ class EngineConfig:
     sibling_conv_fusion: bool = True   # fp8: an Inception module's sibling 1x1 convs as one multi-output GEMM
     fuse_preprocess_stem: bool = True  # resize-free preprocess folded into the s2d RGB stem conv
     fuse_block_tails: bool = True      # ResNet block boundary: expand + next reduce in one kernel
-    fuse_conv3_tails: bool = True      # ... plus the block's 3x3 in front of it (stage 1: bottleneck3)
     decimate_tails: bool = True        # stage-1 tail output stored at the stride-2 reader's pixels
     pw_res_kernel: bool = True         # identity-residual expand convs on the persistent kernel
     conv3x3c64_kernel: bool = True     # 64-channel 3x3 convs with the filter bank in LDS

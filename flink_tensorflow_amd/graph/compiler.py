@@ -272,51 +272,6 @@ class CompiledFunction(TransformerLowering):
             if self.vals[(tn.name, tn.index)].rows is not None:
                 raise CompileError(f"fetch {f} is a token-packed tensor (fetch a per-sequence output)")
         self._decimate_tails()
-        self._fuse_conv3_tails()
-
-    def _fuse_conv3_tails(self):
-        """A stage-1 bottleneck's 3x3 conv (``conv3x3c64``) whose only reader is the fused
-        block tail right after it (as the tail's x2) joins that tail: one persistent kernel
-        (``bottleneck3``) computes x2 per tile in LDS from the 3x3's input, so the 64-channel
-        x2 (103 MB per 256 images) is neither written nor read back, and the 3x3's MFMA work
-        overlaps the tail's HBM streams instead of running as its own launch."""
-        self.fused_conv3_tails = 0
-        if not _cfg().fuse_conv3_tails or self.device.type != "cuda":
-            return
-        fetched = {id(_root(self.vals[(TensorName.parse(f).name, TensorName.parse(f).index)]))
-                   for f in self.fetch_names}
-        i = 0
-        while i < len(self.steps):
-            st = self.steps[i]
-            c3 = st.meta.get("c3")
-            if c3 is None:
-                i += 1
-                continue
-            w2, b2, act = c3
-            x2, y1 = st.outputs[0], st.inputs[0]
-            readers = [k for k, r in enumerate(self.steps) if r is not st and any(_root(v) is _root(x2) for v in r.inputs)]
-            r = self.steps[readers[0]] if len(readers) == 1 else None
-            ok = (r is not None and "tail" in r.meta and r.inputs[0] is x2 and K.act_code(act) == K.ACT_RELU
-                  and id(_root(x2)) not in fetched and _root(x2) is x2 and x2.concat_slot is None and _coff(x2) == 0
-                  and not any(v is not x2 and _root(v) is x2 for v in self.vals.values())
-                  and _root(y1) is y1 and y1.concat_slot is None and (y1.phys_c or 64) == 64
-                  and y1.dtype == torch.bfloat16 and len(y1.shape) == 4)
-            if not ok:
-                i += 1
-                continue
-            w3, b3, w1, b1, dual, dec = r.meta["tail"]
-            second = r.inputs[1]
-            y3, y1o = r.outputs
-
-            def run(y1=y1, second=second, y3=y3, y1o=y1o, w2=w2, b2=b2, w3=w3, b3=b3, w1=w1, b1=b1, dual=dual, dec=dec):
-                K.bottleneck3(y1.buf, w2, b2, None if dual else second.buf, w3, b3, w1, b1, y3=y3.buf, y1_out=y1o.buf,
-                              xs=second.buf if dual else None, y3_decimated=dec["on"])
-
-            k = readers[0]
-            self.steps[k] = Step(f"{st.name}+{r.name}", r.kind, run, [y1, second], [y3, y1o],
-                                 {"impl": "bottleneck3", "dec": r.meta.get("dec"), "conv_out": tuple(x2.shape)})
-            del self.steps[i]
-            self.fused_conv3_tails += 1
 
     def _decimate_tails(self):
         """A fused block tail's wide output y3 whose only other reader is the next stage's
@@ -821,7 +776,7 @@ class CompiledFunction(TransformerLowering):
             def run_c(xin=xin, out=out, w_dev=w_dev, bz=bz):
                 K.conv3x3_c64(xin.buf, w_dev, bz, act, out=_target(out), out_channel_offset=_coff(out))
 
-            self._emit(node.name, "conv", run_c, [xin], [out], {"impl": "conv3x3c64", "c3": (w_dev, bz, act)})
+            self._emit(node.name, "conv", run_c, [xin], [out], {"impl": "conv3x3c64"})
             self.conv3x3c64 = getattr(self, "conv3x3c64", 0) + 1
             self.vals[(last.name, 0)] = out
             self._alias_fused_outputs(absorbed, out)
@@ -1056,8 +1011,7 @@ class CompiledFunction(TransformerLowering):
                               y1=out2.buf, xs=second.buf if dual else None, y3_decimated=dec["on"])
 
         self._emit(name, "conv", run, [xin, second], [out, out2],
-                   {"impl": "bottleneck_tail", "dec": dec if xs_val is None and cx == 64 else None,
-                    "tail": (w3_dev, b3_dev, w1_dev, b1_dev, xs_val is not None, dec)})
+                   {"impl": "bottleneck_tail", "dec": dec if xs_val is None and cx == 64 else None})
         self.vals[(last.name, 0)] = out
         self._alias_fused_outputs(absorbed, out)
         self.vals[(last2.name, 0)] = out2
@@ -1850,7 +1804,7 @@ class CompiledFunction(TransformerLowering):
     # ================================================================== batch-slice chain
     _CHAIN_KINDS = ("conv", "gemm", "pool", "elementwise", "conv_fp8", "pool_fp8")
     # persistent kernels that load a resident weight bank per launch
-    _PERSISTENT_IMPLS = ("conv3x3c64", "bottleneck_tail", "bottleneck3", "pw_res")
+    _PERSISTENT_IMPLS = ("conv3x3c64", "bottleneck_tail", "pw_res")
 
     def _find_chain(self, keep: set) -> dict | None:
         """The leading run of memory-bound layers that executes once per slice of
@@ -2228,7 +2182,6 @@ class CompiledFunction(TransformerLowering):
                 "hip_graph": self._graph_obj is not None, "precision": self.precision,
                 "fp8_layers": self.fp8_layers, "fused_shortcuts": getattr(self, "fused_shortcuts", 0),
                 "fused_tails": getattr(self, "fused_tails", 0), "decimated_tails": getattr(self, "decimated_tails", 0),
-                "fused_conv3_tails": getattr(self, "fused_conv3_tails", 0),
                 "fused_pools": getattr(self, "fused_pools", 0), "conv3x3c64": getattr(self, "conv3x3c64", 0),
                 "pw_res": getattr(self, "pw_res_layers", 0),
                 "conv_lite": getattr(self, "conv_lite_layers", 0),

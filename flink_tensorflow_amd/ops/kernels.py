@@ -398,55 +398,6 @@ def bottleneck_tail(x2: torch.Tensor, res: torch.Tensor | None, w3: torch.Tensor
     return y3, y1
 
 
-def bottleneck3(y1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor, res: torch.Tensor | None, w3: torch.Tensor,
-                b3: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, y3: torch.Tensor | None = None,
-                y1_out: torch.Tensor | None = None, xs: torch.Tensor | None = None, y3_decimated: bool = False):
-    """A stage-1 ResNet bottleneck's 3x3 conv and its block tail as one kernel
-    (kernels/bottleneck.hip ``bottleneck3_kernel``): ``x2 = relu(conv3x3(y1, w2) + b2)``
-    (SAME, 64 -> 64, ``w2`` OHWI [64, 3, 3, 64]) computed per tile in LDS, then exactly
-    :func:`bottleneck_tail` of ``x2`` — x2 never reaches HBM.  ``y1`` [N, H, W, 64];
-    returns ``(y3, y1_out)``.  Host: the fp32 reference conv with x2 rounded to the output
-    dtype, then the tail's host path."""
-    if y1.dim() != 4 or y1.shape[-1] != 64 or tuple(w2.shape) != (64, 3, 3, 64) or b2.numel() != 64:
-        raise ValueError(f"bottleneck3: y1 [N, H, W, 64] and w2 [64, 3, 3, 64] expected, got {tuple(y1.shape)} "
-                         f"{tuple(w2.shape)}")
-    N, H, W, _ = y1.shape
-    if not y1.is_cuda:
-        x2 = conv2d_nhwc(y1.float(), w2.float(), b2.float(), None, (1, 1), (1, 1, 1, 1), (1, 1), ACT_RELU)
-        return bottleneck_tail(x2.to(y1.dtype).float() if y1.dtype != torch.float32 else x2, res, w3, b3, w1, b1,
-                               y3=y3, y1=y1_out, xs=xs, y3_decimated=y3_decimated)
-    dual = xs is not None
-    cn = w1.shape[0]
-    if (res is None) != dual or (64, dual, cn) not in ((64, True, 64), (64, False, 64), (64, False, 128)):
-        raise ValueError(f"bottleneck3: unsupported variant (dual {dual}, reduce width {cn})")
-    if (dual and tuple(xs.shape) != (N, H, W, 64)) or (not dual and tuple(res.shape) != (N, H, W, 256)):
-        raise ValueError("bottleneck3: the second input must be [N, H, W, 64 (xs) / 256 (res)]")
-    if tuple(w3.reshape(256, -1).shape) != (256, 128 if dual else 64) or tuple(w1.reshape(cn, -1).shape) != (cn, 256):
-        raise ValueError("bottleneck3: expand / reduce weight shapes")
-    if b3.numel() != 256 or b1.numel() != cn:
-        raise ValueError("bottleneck3: bias sizes must match the output channels")
-    if y3_decimated and (H % 2 or W % 2):
-        raise ValueError("bottleneck3: decimated y3 needs even H, W")
-    lead3 = (N, H // 2, W // 2) if y3_decimated else (N, H, W)
-    y3 = torch.empty((*lead3, 256), dtype=y1.dtype, device=y1.device) if y3 is None else y3
-    y1_out = torch.empty((N, H, W, cn), dtype=y1.dtype, device=y1.device) if y1_out is None else y1_out
-    if tuple(y3.shape) != (*lead3, 256) or tuple(y1_out.shape) != (N, H, W, cn):
-        raise ValueError("bottleneck3: output buffers do not fit")
-    second = xs if dual else res
-    for t, n in ((y1, "y1"), (w2, "w2"), (second, "xs" if dual else "res"), (w3, "w3"), (w1, "w1"), (y3, "y3"),
-                 (y1_out, "y1_out")):
-        _check(t, n, device=y1.device)
-        if not t.is_contiguous():
-            raise ValueError(f"bottleneck3: {n} must be contiguous")
-    for t, n in ((b2, "b2"), (b3, "b3"), (b1, "b1")):
-        _check(t, n, torch.float32, y1.device)
-    dev = y1.device.index if y1.device.index is not None else torch.cuda.current_device()
-    _hip().bottleneck3_bf16(y1.data_ptr(), _ptr(xs), _ptr(res), w2.data_ptr(), b2.data_ptr(), w3.data_ptr(),
-                            b3.data_ptr(), w1.data_ptr(), b1.data_ptr(), y3.data_ptr(), y1_out.data_ptr(), N, H, W, cn,
-                            _NUM_CU[dev], _stream(), int(y3_decimated))
-    return y3, y1_out
-
-
 def gemm(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = None, residual: torch.Tensor | None = None,
          act=None, out: torch.Tensor | None = None, cfg: int = -1) -> torch.Tensor:
     """``act(x[M,K] @ w[N,K]^T + bias + residual)``; leading dims of x are flattened."""

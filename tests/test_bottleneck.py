@@ -61,10 +61,7 @@ def _check(r50, dev):
     # stage 1 -> stage 2: the tail's 256-channel output is stored decimated (only the
     # stride-2 projection reads it besides the fused reduce conv)
     assert fused.summary()["decimated_tails"] == 1 and plain.summary()["decimated_tails"] == 0
-    # on the GPU the three stage-1 3x3 convs also join their tails (bottleneck3)
-    c3 = fused.summary()["fused_conv3_tails"]
-    assert c3 == (3 if dev.type == "cuda" else 0) and plain.summary()["fused_conv3_tails"] == 0
-    assert len(fused.steps) == len(plain.steps) - n - c3
+    assert len(fused.steps) == len(plain.steps) - n
     # deep-K 1x1 reduce convs (stages 3/4) run on the ping-pong GEMM on the GPU; the FC head
     # too; no library GEMM anywhere
     for plan in (fused, plain):
@@ -115,102 +112,3 @@ def test_decimated_tail_reference():
 @pytest.mark.gpu
 def test_decimated_tail_gpu():
     _decimated_case(torch.device("cuda", 0))
-
-
-def _b3_case(g, N, H, W, dual, cn):
-    y1 = torch.randn(N, H, W, 64, generator=g).relu()
-    w2 = torch.randn(64, 3, 3, 64, generator=g) / 24
-    b2 = torch.randn(64, generator=g) * 0.1
-    w3 = torch.randn(256, 128 if dual else 64, generator=g) / 8
-    b3 = torch.randn(256, generator=g) * 0.1
-    w1 = torch.randn(cn, 256, generator=g) / 16
-    b1 = torch.randn(cn, generator=g) * 0.1
-    second = torch.randn(N, H, W, 64 if dual else 256, generator=g)
-    return y1, w2, b2, w3, b3, w1, b1, second
-
-
-def test_bottleneck3_host_reference():
-    """bottleneck3 = the 3x3 conv (+ bias, ReLU) then the block tail, on the host path."""
-    g = torch.Generator().manual_seed(3)
-    for dual, cn in ((True, 64), (False, 64), (False, 128)):
-        y1, w2, b2, w3, b3, w1, b1, second = _b3_case(g, 2, 5, 7, dual, cn)
-        y3, y1o = K.bottleneck3(y1, w2, b2, None if dual else second, w3, b3, w1, b1, xs=second if dual else None)
-        x2 = K.conv2d_nhwc(y1, w2, b2, None, (1, 1), (1, 1, 1, 1), (1, 1), "relu")
-        e3, e1 = K.bottleneck_tail(x2, None if dual else second, w3, b3, w1, b1, xs=second if dual else None)
-        torch.testing.assert_close(y3, e3)
-        torch.testing.assert_close(y1o, e1)
-    with pytest.raises(ValueError):
-        K.bottleneck3(y1, w2[:32], b2, second, w3, b3, w1, b1)
-
-
-B3_CASES = [  # N, H, W, dual, cn, decimated
-    (3, 56, 56, True, 64, False),    # stage 1's first block (projection shortcut)
-    (3, 56, 56, False, 64, False),
-    (3, 56, 56, False, 128, True),   # stage 1 -> stage 2: y3 stored decimated
-    (2, 10, 40, False, 64, False),   # partial tiles: a 12-column last tile
-    (2, 12, 34, False, 128, False),
-]
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("case", B3_CASES)
-def test_bottleneck3_matches_unfused_gpu(case):
-    """The fused kernel equals conv3x3c64 followed by bottleneck_tail up to bf16 rounding
-    flips (its 3x3 sums two K halves in fp32; everything after x2 is the tail's arithmetic)."""
-    N, H, W, dual, cn, dec = case
-    dev = torch.device("cuda", 0)
-    g = torch.Generator().manual_seed(N * H + W + cn)
-    y1, w2, b2, w3, b3, w1, b1, second = (t.to(dev) for t in _b3_case(g, N, H, W, dual, cn))
-    bf = lambda t: t.to(torch.bfloat16).contiguous()  # noqa: E731
-    y1, w2, w3, w1, second = bf(y1), bf(w2), bf(w3), bf(w1), bf(second)
-    x2 = K.conv3x3_c64(y1, w2, b2, "relu")
-    e3, e1 = K.bottleneck_tail(x2, None if dual else second, w3, b3, w1, b1, xs=second if dual else None,
-                               y3_decimated=dec)
-    y3, y1o = K.bottleneck3(y1, w2, b2, None if dual else second, w3, b3, w1, b1, xs=second if dual else None,
-                            y3_decimated=dec)
-    torch.cuda.synchronize()
-    for got, ref in ((y3, e3), (y1o, e1)):
-        g32, r32 = got.float(), ref.float()
-        torch.testing.assert_close(g32, r32, rtol=2e-2, atol=2e-2 * r32.abs().max().item())
-        assert (g32 == r32).float().mean() > 0.9
-    # and against the fp32 host reference
-    r3, r1 = K.bottleneck3(y1.float().cpu(), w2.float().cpu(), b2.cpu(), None if dual else second.float().cpu(),
-                           w3.float().cpu(), b3.cpu(), w1.float().cpu(), b1.cpu(),
-                           xs=second.float().cpu() if dual else None, y3_decimated=dec)
-    torch.testing.assert_close(y3.float().cpu(), r3, rtol=3e-2, atol=3e-2 * r3.abs().max().item())
-    torch.testing.assert_close(y1o.float().cpu(), r1, rtol=3e-2, atol=3e-2 * r1.abs().max().item())
-
-
-@pytest.mark.gpu
-def test_bottleneck3_odd_shape_gpu():
-    """Shapes conv3x3c64 does not take (H < 8, W < 32, odd): against the fp32 reference."""
-    dev = torch.device("cuda", 0)
-    g = torch.Generator().manual_seed(11)
-    y1, w2, b2, w3, b3, w1, b1, res = _b3_case(g, 2, 7, 30, False, 64)
-    bf = lambda t: t.to(dev, torch.bfloat16).contiguous()  # noqa: E731
-    y3, y1o = K.bottleneck3(bf(y1), bf(w2), b2.to(dev), bf(res), bf(w3), b3.to(dev), bf(w1), b1.to(dev))
-    r3, r1 = K.bottleneck3(*(bf(t).float().cpu() for t in (y1, w2)), b2, bf(res).float().cpu(),
-                           bf(w3).float().cpu(), b3, bf(w1).float().cpu(), b1)
-    torch.testing.assert_close(y3.float().cpu(), r3, rtol=3e-2, atol=3e-2 * r3.abs().max().item())
-    torch.testing.assert_close(y1o.float().cpu(), r1, rtol=3e-2, atol=3e-2 * r1.abs().max().item())
-
-
-@pytest.mark.gpu
-def test_compiled_resnet50_fuses_conv3_tails_gpu():
-    """At 128x128 input (stage 1 at 32x32, where conv3x3c64 applies) the three stage-1
-    3x3 convs join their block tails; logits match the unfused plan."""
-    from flink_tensorflow_amd.config import override
-
-    dev = torch.device("cuda", 0)
-    r = Graph.from_graph_def(resnet50_graph_def(depth=50, image_hw=(128, 128), num_classes=16))
-    plans = {}
-    for on in (True, False):
-        with override(fuse_conv3_tails=on):
-            plans[on] = CompiledFunction(r, {"images:0": ((4, 128, 128, 3), "UINT8")}, ["logits:0"], dev, strict=True)
-    assert plans[True].summary()["fused_conv3_tails"] == 3 and plans[False].summary()["fused_conv3_tails"] == 0
-    assert len(plans[True].steps) == len(plans[False].steps) - 3
-    assert sum(st.meta.get("impl") == "bottleneck3" for st in plans[True].steps) == 3
-    imgs = torch.randint(0, 256, (4, 128, 128, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(2))
-    a = plans[True]({"images:0": imgs.to(dev)})[0].float().cpu()
-    b = plans[False]({"images:0": imgs.to(dev)})[0].float().cpu()
-    torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2 * b.abs().max().item())
