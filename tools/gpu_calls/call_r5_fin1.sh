@@ -1,0 +1,17 @@
+#!/bin/bash
+# round 5 final, part 1: the whole GPU suite and smoke on the final tree.
+REPO="${GRAFT_REPO_ROOT:-$(pwd)}"
+OUT="$REPO/gpurun_out/r05_final"
+mkdir -p "$OUT"
+step() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "[step] $name" >&2
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" >> "$OUT/rc.txt"
+  if [ $rc -gt 1 ]; then echo "[step] $name ended with $rc: stopping" >&2; exit $rc; fi
+  return 0
+}
+step gpu_suite 1000 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
+step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
+echo done >&2
