@@ -137,7 +137,9 @@ def main():
                          "of this script where there is one GPU; numbers from such runs are not results")
     ap.add_argument("--lanes", type=int, default=None,
                     help="compute lanes: independent plan instances on their own HIP streams, batches round-robin "
-                         "(default: 3 for bert / bert_graph, 2 otherwise; measured in profiles/r01_lanes)")
+                         "(default: 3 for bert / bert_graph and inception_v3, 2 otherwise; measured in "
+                         "profiles/r01_lanes, r05_m: Inception-v3 fp8 +3.7 %% static / +7.6 %% dynamic at 3, "
+                         "ResNet-50 no better)")
     ap.add_argument("--no-interleave", action="store_true",
                     help="A/B: launch a batch's per-piece head kernels after the whole host gather instead of "
                          "interleaved with it")
@@ -203,7 +205,7 @@ def main():
     from flink_tensorflow_amd.batching.arena import DeviceArena
     from flink_tensorflow_amd.config import EngineConfig
 
-    lanes = args.lanes or (3 if args.model in ("bert", "bert_graph") else 2)
+    lanes = args.lanes or (3 if args.model in ("bert", "bert_graph", "inception_v3") else 2)
     budget = EngineConfig().arena_bytes(dev) // lanes  # this subtask's HBM share, split over its lanes
     lane_plans, params = [], []
     if args.model == "inception_v3":
