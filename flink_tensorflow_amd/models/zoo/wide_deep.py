@@ -146,6 +146,8 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
     """Online trainer: ``train_step(records)`` on micro-batches of
     ``(label, dense[13], cats[26], cross[C])`` records; ``predict(records)``."""
 
+    restart_attempt = 0  # the job attempt this replica was opened in (set by the operator)
+
     _TRANSIENT = ("_model", "_opt", "_bucketer", "_graph", "_static", "_static_loss", "_fused", "_exchange")
     uses_collectives = True  # under DP every step all-reduces / exchanges: the job forms a communicator
 
@@ -173,7 +175,11 @@ class WideDeepTrainer(RichModel, CheckpointedModel):
         if comm.is_dist() and comm.get().size > 1 and mode in ("owner", "bucketed"):
             from ...parallel.sparse_exchange import BucketedOwnerExchange, OwnerSparseExchange
 
-            self._exchange = (BucketedOwnerExchange(comm.get(), current().wd_bucket_slack) if mode == "bucketed"
+            # each restart doubles the bucket slack (up to 16x): a job that failed on a bucket
+            # overflow (CapacityExceeded, raised before any checkpoint saw a dropped row)
+            # replays its input with larger buckets instead of overflowing again
+            slack = current().wd_bucket_slack * 2.0 ** min(int(self.restart_attempt), 4)
+            self._exchange = (BucketedOwnerExchange(comm.get(), slack) if mode == "bucketed"
                               else OwnerSparseExchange(comm.get()))
         from .wide_deep_fused import FusedWideDeepStep
 

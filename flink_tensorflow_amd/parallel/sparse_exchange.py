@@ -158,7 +158,9 @@ class OwnerSparseExchange:
 class CapacityExceeded(RuntimeError):
     """A bucketed exchange dropped rows: some owner's bucket needed more slots than its
     capacity.  Raised at the next check, BEFORE the state is checkpointed, so the job
-    restarts from a checkpoint that never saw a dropped update."""
+    restarts from a checkpoint that never saw a dropped update — and the restarted
+    trainer opens its exchange with the slack doubled per attempt (``WideDeepTrainer``),
+    so the replay does not overflow the same way again."""
 
 
 class BucketedOwnerExchange(OwnerSparseExchange):

@@ -54,6 +54,8 @@ class ModelAwareFunction(F.RichFunction):
 
     def open(self, config=None):
         ctx = getattr(self, "_runtime_context", None)
+        if ctx is not None and hasattr(self.model, "restart_attempt"):
+            self.model.restart_attempt = ctx.attempt  # models that adapt after a failure
         open_model(self.model, ctx.device if ctx is not None else None)
 
     def close(self):

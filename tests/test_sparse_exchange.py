@@ -51,3 +51,5 @@ def test_bucket_overflow_is_reported_ws2():
     for o in out:
         ov = o["overflow"]
         assert ov["demand"] > ov["capacity"] and len(ov["raised"]) == 2, ov
+        # the restarted attempt replays with larger buckets (slack x 2^attempt)
+        assert ov["restart_slack"] == 1.5 * 4, ov

@@ -82,8 +82,14 @@ def main():
                 fn()
             except CapacityExceeded as e:
                 raised.append(str(e)[:60])
+        # a restarted job (attempt 2) opens its trainer with 4x the configured slack
+        C.set_current(C.EngineConfig(wd_sparse_exchange="bucketed", wd_bucket_slack=1.5))
+        tr = WideDeepTrainer(WideDeepConfig.tiny(), device="cpu", seed=7, fused=False)
+        tr.restart_attempt = 2
+        tr.open()
         out["overflow"] = {"capacity": bx.capacity(ids.numel(), 4000), "demand": int(bx.need.item()),
-                           "raised": raised}
+                           "raised": raised, "restart_slack": tr._exchange.slack}
+        tr.close()
     else:
         cfg = WideDeepConfig()
         B = 4096
