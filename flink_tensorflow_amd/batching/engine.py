@@ -81,7 +81,7 @@ class PipelinedGpuRunner:
 
     def __init__(self, plans, feed: str, fetch_bufs: Callable[[Any], Sequence[torch.Tensor]],
                  record_shape, record_dtype=torch.uint8, depth: int = 3, device=None, gather_threads: int = 8,
-                 stage_chunk: int = 64, stagger: bool = False, freeze_gc: bool = True, timeline: bool = False,
+                 stage_chunk: int = 64, lane_offset_us: float = 0.0, freeze_gc: bool = True, timeline: bool = False,
                  interleave_head: bool = True):
         lanes = plans if isinstance(plans, (list, tuple)) else [plans]
         self.lanes = [dict(sorted(p.items())) for p in lanes]
@@ -126,13 +126,12 @@ class PipelinedGpuRunner:
         # thread's time goes when the GPU is not saturated
         self.host_s = {"gather": 0.0, "select": 0.0, "launch": 0.0, "wait": 0.0}
         self.batches = 0
-        # stagger: when the pipeline starts from empty, lane k >= 1 starts its first batch
-        # only when lane 0's first batch is done, so the lanes run half a period apart (one
-        # lane's memory-bound layers against the other's compute-bound ones) instead of
-        # in step
-        self.stagger = stagger and len(self.lanes) > 1
-        self._stagger_evt = None
-        self._started: set[int] = set()
+        # lane phase: when the pipeline starts from empty, the k-th lane to receive a batch
+        # starts it k x lane_offset_us after the first (a stream-ordered delay kernel), so
+        # the lanes begin in the staggered phase of the steady state (one lane's
+        # memory-bound layers against another's compute-bound ones) instead of in step
+        self.lane_offset_us = float(lane_offset_us) if len(self.lanes) > 1 else 0.0
+        self._started: list[int] = []
         if freeze_gc:  # the plans are compiled: keep the GC's full passes off them
             from ..utils.gcfreeze import freeze_setup_objects
 
@@ -230,8 +229,6 @@ class PipelinedGpuRunner:
                 for dst, src in zip(slot.pinned_out, self.fetch_bufs(plan)):
                     dst.copy_(src, non_blocking=True)
             slot.done.record(stream)
-        if self.stagger and lane == 0 and self._stagger_evt is None:
-            self._stagger_evt = slot.done
         slot.busy = True
         slot.n = n
         slot.ts = ingest_ts
@@ -247,15 +244,16 @@ class PipelinedGpuRunner:
         return finished
 
     def _begin_lane(self, slot: _Slot, lane: int, stream) -> None:
-        """The lane's stream work that precedes a batch: the stagger wait of a restarting
+        """The lane's stream work that precedes a batch: the phase delay of a restarting
         pipeline and the batch's start stamp (timeline)."""
-        if self.stagger:
+        if self.lane_offset_us > 0:
             if not self._inflight:  # the pipeline restarts from empty
                 self._started.clear()
-                self._stagger_evt = None
-            if lane not in self._started and lane != 0 and self._stagger_evt is not None:
-                stream.wait_event(self._stagger_evt)
-            self._started.add(lane)
+            if lane not in self._started:
+                k = len(self._started)
+                self._started.append(lane)
+                if k:
+                    _ext.hip().stream_delay(k * self.lane_offset_us, stream.cuda_stream)
         if slot.t_start is not None:  # after the lane's previous work, before this batch's h2d wait
             with torch.cuda.stream(stream):
                 slot.t_start.record(stream)

@@ -183,7 +183,30 @@ void gather_rows(uintptr_t x, uintptr_t idx, uintptr_t y, int n_out, int n_src, 
   FTM_CHECK_LAUNCH();
 }
 
+namespace {
+
+// One wave that holds its stream for ``ticks`` of the 100 MHz constant real-time counter
+// (s_memrealtime: a counter read, sleeping between reads) — a stream-ordered delay that
+// occupies one wave slot of one CU.  Used to start a restarting pipeline's second lane a
+// fraction of a batch after the first (batching/engine.py, lane phase).
+__global__ __launch_bounds__(64) void stream_delay_kernel(long long ticks) {
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+}  // namespace
+
+// delays ``stream`` by ``us`` microseconds (GPU-side; returns immediately)
+void stream_delay(double us, uintptr_t stream) {
+  if (us <= 0) return;
+  if (us > 1e6) throw std::invalid_argument("stream_delay: at most one second");
+  hipLaunchKernelGGL(stream_delay_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                     (long long)(us * 100.0));
+  FTM_CHECK_LAUNCH();
+}
+
 void register_elementwise(pybind11::module_& m) {
+  m.def("stream_delay", &stream_delay);
   m.def("gather_rows", &gather_rows);
   m.def("binary_bf16", &binary_bf16);
   m.def("lrn_bf16", &lrn_bf16);

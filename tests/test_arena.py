@@ -202,3 +202,58 @@ def test_interleaved_head_pieces_match_whole_batch_gpu(small_graph):
         torch.testing.assert_close(x.outputs[0][: x.n], y.outputs[0][: y.n])
         assert torch.equal(x.outputs[1][: x.n], y.outputs[1][: y.n])
 
+
+
+@pytest.mark.gpu
+def test_stream_delay_and_lane_phase_gpu(small_graph):
+    """``stream_delay`` holds a stream for the requested time (the lane-phase offset of a
+    restarting pipeline); a runner with ``lane_offset_us`` gives the same results as one
+    without, and delays only the second lane's first batch after each restart."""
+    import numpy as np
+
+    from flink_tensorflow_amd import _ext
+    from flink_tensorflow_amd.batching.engine import PipelinedGpuRunner
+
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(s):
+        e0.record(s)
+        _ext.hip().stream_delay(3000.0, s.cuda_stream)
+        e1.record(s)
+    e1.synchronize()
+    assert 2.9 <= e0.elapsed_time(e1) < 20.0
+    with pytest.raises(ValueError):
+        _ext.hip().stream_delay(2e6, s.cuda_stream)
+
+    feeds = {"images:0": ((8, 48, 48, 3), "UINT8")}
+
+    def lane():
+        return {8: CompiledFunction(small_graph, feeds, ["top_k:0", "top_k:1"], dev, strict=True,
+                                    arena=DeviceArena(dev, 4 << 30))}
+
+    rng = np.random.default_rng(2)
+    batches = [[rng.integers(0, 256, (48, 48, 3), dtype=np.uint8) for _ in range(8)] for _ in range(6)]
+
+    def run(offset):
+        r = PipelinedGpuRunner([lane(), lane()], "images:0", lambda p: p.output_tensors(), (48, 48, 3), depth=3,
+                               device=dev, lane_offset_us=offset, timeline=True)
+        r.mark()
+        out = []
+        for i, b in enumerate(batches):
+            out += r.submit(b, np.full(len(b), float(i)), [i] * len(b))
+            if i == 2:  # drain: the pipeline restarts from empty at batch 3
+                out += r.drain()
+        out += r.drain()
+        return out, r.timeline
+
+    (a, _), (b, tl) = run(0.0), run(2000.0)
+    for x, y in zip(a, b):
+        assert torch.equal(x.outputs[1][: x.n], y.outputs[1][: y.n])
+    # after each (re)start the second lane's first batch begins ~2 ms after the first batch
+    # (its start stamp follows the delay kernel); the first lane is never delayed
+    tl = sorted(tl, key=lambda t: t["submit_ms"])
+    starts = [t["start_ms"] for t in tl]
+    assert len(starts) == 6
+    for i in (0, 3):
+        assert starts[i + 1] - starts[i] >= 1.8, starts
