@@ -2,7 +2,7 @@
 # round 5 final, part 2: the headline (driver window and 300 steps), the job mode, Inception
 # fp8 static / dynamic, per-layer tables, and the headline's kernel stats under rocprofv3.
 REPO="${GRAFT_REPO_ROOT:-$(pwd)}"
-OUT="$REPO/gpurun_out/r05_final"
+OUT="$REPO/gpurun_out/r05_final2"
 mkdir -p "$OUT"
 step() {  # name seconds cmd...
   local name=$1 secs=$2; shift 2
@@ -20,6 +20,7 @@ step bench_job 200 python bench.py --job
 step bench_inc 200 python bench.py --model inception_v3 --steps 30 --warmup 5
 step bench_inc2 200 python bench.py --model inception_v3 --steps 30 --warmup 5
 step bench_inc_dyn 200 python bench.py --model inception_v3 --steps 30 --warmup 5 --dynamic
+step bench_inc_l2 200 python bench.py --model inception_v3 --steps 30 --warmup 5 --lanes 2
 step bench_wd 200 python bench.py --model widedeep --steps 50 --warmup 10
 step layers_rn 300 python -u tools/layer_table.py --model resnet50 --reps 3 --out "$OUT/layers_rn.md"
 step layers_inc 300 python -u tools/layer_table.py --model inception_v3 --reps 3 --out "$OUT/layers_inc.md"

@@ -1,7 +1,7 @@
 #!/bin/bash
-# round 5 final, part 1: the whole GPU suite and smoke on the final tree.
-REPO="${GRAFT_REPO_ROOT:-$(pwd)}"
-OUT="$REPO/gpurun_out/r05_final2"
+# round 5 V: the lane-phase test and the arena / engine GPU tests; the headline bench with
+# the new default lane offset.
+OUT=gpurun_out/r05_v
 mkdir -p "$OUT"
 step() {  # name seconds cmd...
   local name=$1 secs=$2; shift 2
@@ -12,6 +12,7 @@ step() {  # name seconds cmd...
   if [ $rc -gt 1 ]; then echo "[step] $name ended with $rc: stopping" >&2; exit $rc; fi
   return 0
 }
-step gpu_suite 1000 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
-step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
+step tests 300 python -u -m pytest -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_arena.py
+step bench 150 python bench.py
+step bench2 150 python bench.py
 echo done >&2
