@@ -476,7 +476,7 @@ def run_job(args):
                 yield pool[i % pool_n]
 
         model = JobResNet50(image_hw=(HW, HW), buckets=(B,), distributed_weights=True, lanes=lanes,
-                            depth=args.depth).timed_window(W, K, out_dir)
+                            depth=args.depth, lane_offset_us=args.lane_offset_us).timed_window(W, K, out_dir)
         src = env.generate(images).run_in_processes()
         src.map_with_model_batched(model, None, max_batch=B, max_delay_ms=60_000.0, name="resnet50") \
             .run_in_processes().add_sink(DiscardingSink()).run_in_processes()  # results stay in the worker

@@ -32,9 +32,12 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
                  buckets: Sequence[int] = (64, 256), top_k: int = 5, labels: Sequence[str] | None = None,
                  feed: str = "images:0", fetches: Sequence[str] = ("top_k:0", "top_k:1"), depth: int = 3,
                  device=None, use_graph: bool = True, precision: str = "bf16", calibration_images=None,
-                 distributed_weights: bool = False, lanes: int = 2):
+                 distributed_weights: bool = False, lanes: int = 2, lane_offset_us: float = 0.0):
         super().__init__(device)
         self.lanes = max(1, int(lanes))  # concurrent plan instances on their own HIP streams
+        # lane phase at a pipeline restart (PipelinedGpuRunner): off by default — under light
+        # load every batch that overlaps a running one would wait; throughput runs set it
+        self.lane_offset_us = float(lane_offset_us)
         self.distributed_weights = distributed_weights  # DP: broadcast rank 0's compiled weights at open
         self.precision = precision
         self.calibration_images = calibration_images  # uint8 [n, H, W, 3] for fp8 scales (synthetic if None)
@@ -82,7 +85,8 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
                 # in place, so the captured hipGraphs keep reading the same buffers
                 comm.broadcast_tensors([t for ln in lanes for p in ln.values() for t in p.params], src=0)
             self._runner = PipelinedGpuRunner(lanes, self.feed, lambda p: p.output_tensors(), (H, W, 3),
-                                              torch.uint8, depth=self.depth, device=dev)
+                                              torch.uint8, depth=self.depth, device=dev,
+                                              lane_offset_us=getattr(self, "lane_offset_us", 0.0))
 
     def _calibration(self, b: int):
         if self.precision != "fp8" or self.calibration_images is None:
