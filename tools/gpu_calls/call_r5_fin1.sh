@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5 final, part 1: the whole GPU suite and smoke on the final tree.
 REPO="${GRAFT_REPO_ROOT:-$(pwd)}"
-OUT="$REPO/gpurun_out/r05_final2"
+OUT="$REPO/gpurun_out/r05_final3"
 mkdir -p "$OUT"
 step() {  # name seconds cmd...
   local name=$1 secs=$2; shift 2
