@@ -121,3 +121,20 @@ def test_sysfs_gpu_count_reads_kfd_topology(tmp_path, monkeypatch):
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
     assert sysfs_gpu_count(str(tmp_path)) == 1
     assert sysfs_gpu_count(str(tmp_path / "missing")) == 0
+
+
+def test_window_timeline_splits_fill_from_steady_state():
+    """tools/window_timeline.py: a two-lane window whose batches complete every 3 ms after a
+    7 ms first batch reports the 3 ms period and the fill as a constant overhead."""
+    import importlib.util
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "window_timeline.py")
+    spec = importlib.util.spec_from_file_location("window_timeline", path)
+    wt = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(wt)
+    tl = [{"lane": i % 2, "n": 256, "submit_ms": 0.1 * i, "h2d_ms": 0.2, "start_ms": 0.1 + 3.0 * max(0, i - 1),
+           "done_ms": 7.0 + 3.0 * i} for i in range(20)]
+    r = wt.analyse(tl, elapsed=7.0 + 3.0 * 19 + 0.1)
+    assert abs(r["period_ms"] - 3.0) < 1e-9 and r["batches"] == 20
+    assert abs(r["overhead_ms"] - (r["elapsed_ms"] - 60.0)) < 1e-9 and 3.9 < r["overhead_ms"] < 4.2
