@@ -411,7 +411,7 @@ def main():
                        "parallelism": f"dp{ws}", "micro_batch_per_gpu": B,
                        "input_hw": (299 if args.model == "inception_v3" else 224) if seq is None else None,
                        "batch_buckets": sorted(lane_plans[0]), "dynamic_batching": args.dynamic,
-                       "compute_lanes": lanes},
+                       "compute_lanes": lanes, "lane_offset_us": args.lane_offset_us},
             "p50_latency_ms": round(node_lat["p50"] * 1e3, 3),
             "p99_latency_ms": round(node_lat["p99"] * 1e3, 3),
             "per_gpu_records_per_s": round(per_gpu, 1),
@@ -499,6 +499,7 @@ def run_job(args):
         "data": f"synthetic decoded uint8 {HW}x{HW}x3 images generated in each worker, random-init weights",
         "config": {"model": "ResNet-50 v1.5", "global_batch": B * P, "seq_len": None, "parallelism": f"dp{P}",
                    "micro_batch_per_gpu": B, "input_hw": 224, "batch_buckets": [B], "compute_lanes": lanes,
+                   "lane_offset_us": args.lane_offset_us,
                    "mode": "job: one DataStream job, P worker-process GPU subtasks, chained sources, "
                            "distributed_weights over the operator's communicator"},
         "p50_latency_ms": round(float(np.percentile(lat, 50)) * 1e3, 3) if lat.size else None,
