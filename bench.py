@@ -150,11 +150,14 @@ def main():
                     help="also print, per timed batch, its lane and the GPU times of its first H2D piece, first "
                          "kernel and completion relative to the start of the timed window (diagnostics)")
     ap.add_argument("--job", action="store_true",
-                    help="JOB MODE (resnet50): ONE DataStream job with --gpus worker-process subtasks, one GPU "
+                    help="JOB MODE (resnet50, widedeep): ONE DataStream job with --gpus worker-process subtasks, one GPU "
                          "each — a source chained into each subtask's worker, the ResNet-50 operator with "
                          "distributed_weights (rank 0 compiles, weights broadcast over the operator's RCCL "
                          "group) — timed on the operator (batching/timed.py).  Run as ONE process (not under "
                          "torch.distributed.run): the job starts its own workers")
+    ap.add_argument("--wd-steps-per-round", type=int, default=8,
+                    help="widedeep --job: full micro-batches a trainer subtask gathers before it calls an agreement "
+                         "round (each round runs all of them as agreed steps)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, rendezvous, exchange one object per rank and print the world the "
                          "communicator sees (no model; with --rehearse-fake-comm it runs on a CPU-only box)")
@@ -445,12 +448,14 @@ def run_job(args):
 
     if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1:
         raise SystemExit("[bench] --job runs one coordinator process; do not launch it under torch.distributed.run")
-    if args.model != "resnet50":
-        raise SystemExit("[bench] --job: resnet50 only")
     from flink_tensorflow_amd.utils.gpus import sysfs_gpu_count
 
     if sysfs_gpu_count() < args.gpus:
         raise SystemExit(f"[bench] --job --gpus {args.gpus} but {sysfs_gpu_count()} GPU(s) visible")
+    if args.model == "widedeep":
+        return run_job_widedeep(args)
+    if args.model != "resnet50":
+        raise SystemExit("[bench] --job: resnet50 or widedeep")
     from flink_tensorflow_amd.batching.timed import TimedWindow
     from flink_tensorflow_amd.models.zoo.image_classifier import ResNet50Model
     from flink_tensorflow_amd.models.zoo.resnet import resnet50_flops_per_image
@@ -508,6 +513,85 @@ def run_job(args):
         "communicator": ranks[0]["communicator"], "comm_world_size": ranks[0]["world"],
         "model_tflops_per_s": round(resnet50_flops_per_image(224) * total / 1e12, 1),
         "job_wall_s": round(wall, 2), "job_attempts": res.attempts}), flush=True)
+
+
+def run_job_widedeep(args):
+    """``--job --model widedeep``: Wide&Deep online training as ONE DataStream job
+    (VERDICT r5 #2): P worker-process subtasks of a ``LockstepTrainer`` (the agreed-step
+    co-process trainer, one GPU each), each fed by a generator source chained into its
+    worker that hands over blocks of packed 192-B click rows.  Every agreed step is the
+    captured fused step (pieces padded to the micro-batch, ``{nvalid, norm}`` in device
+    memory); rounds carry up to ``--wd-steps-per-round`` full batches and agree over the
+    host control channel.  The trainer times W + K agreed steps (``batching/timed.py``
+    ``TimedSteps``); the JSON line reports the max elapsed over subtasks."""
+    import shutil
+    import tempfile
+
+    from flink_tensorflow_amd.batching.timed import TimedSteps
+    from flink_tensorflow_amd.models.zoo.wide_deep import (WideDeepConfig, WideDeepTrainer, pack_click_records,
+                                                           synthetic_click_records)
+    from flink_tensorflow_amd.runtime import RestartStrategy, StreamExecutionEnvironment
+    from flink_tensorflow_amd.runtime.lockstep import LockstepTrainer
+    from flink_tensorflow_amd.runtime.sources import DiscardingSink
+
+    class JobTrainer(TimedSteps, LockstepTrainer):
+        pass
+
+    B = args.batch if args.batch != 256 else 4096
+    W, K, P = args.warmup, args.steps, args.gpus
+    spr = args.wd_steps_per_round
+    blk = B  # rows per source block
+    cfg = WideDeepConfig()
+    out_dir = tempfile.mkdtemp(prefix="ftm-bench-wdjob-")
+    if P > 1:  # the capturable fixed-capacity exchange; its overflow recovery is a job restart
+        os.environ["FT_WD_SPARSE_EXCHANGE"] = "bucketed"
+    t0 = time.perf_counter()
+    try:
+        env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(P)
+        env.enable_job_communicator(P > 1)
+        if P > 1:
+            env.set_restart_strategy(RestartStrategy.fixed_delay(1, 0.0))
+        total = (W + K) * B
+
+        def clicks(idx, par, start):  # runs in the subtask's worker process
+            pool = pack_click_records(synthetic_click_records(16 * B, cfg, seed=idx), cfg)
+            i = start
+            while i < total:
+                o = i % len(pool)
+                n = min(blk, total - i, len(pool) - o)
+                yield pool[o:o + n]
+                i += n
+
+        trainer = JobTrainer(WideDeepTrainer(cfg, seed=0), B, max_delay_ms=20.0, steps_per_round=spr,
+                             max_steps_per_round=max(spr, 64)).timed_window(W, K, out_dir)
+        env.generate(clicks).run_in_processes().process(trainer, "widedeep-trainer").run_in_processes() \
+            .add_sink(DiscardingSink()).run_in_processes()
+        res = env.execute("bench-widedeep-job")
+        wall = time.perf_counter() - t0
+        ranks = []
+        for r in range(P):
+            with open(os.path.join(out_dir, f"rank{r}.json")) as f:
+                ranks.append(json.load(f))
+    finally:
+        shutil.rmtree(out_dir, ignore_errors=True)
+    elapsed = max(r["elapsed_s"] for r in ranks)
+    n_rec = sum(r["records"] for r in ranks)
+    value = n_rec / elapsed
+    print(json.dumps({
+        "metric": "records/sec (whole node), Wide&Deep online training (DP all-reduce)",
+        "value": round(value, 1), "unit": "records/s", "n_gpus": P, "steps": K, "warmup": W,
+        "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16 compute / fp32 master weights",
+        "data": "synthetic Criteo-shaped click records as 192-B packed rows generated in each worker "
+                "(source chained into the trainer), random init",
+        "config": {"model": "Wide&Deep (26x100k x32 embeddings, MLP 1024-512-256)", "global_batch": B * P,
+                   "seq_len": None, "parallelism": f"dp{P}", "micro_batch_per_gpu": B,
+                   "mode": "job: one DataStream job, P worker-process LockstepTrainer subtasks, agreed steps "
+                           "(host control channel), captured padded step",
+                   "steps_per_round": spr},
+        "per_rank_records_per_s": [round(r["records"] / r["elapsed_s"], 1) for r in ranks],
+        "rounds": [r.get("rounds") for r in ranks], "job_wall_s": round(wall, 2),
+        "job_attempts": res.attempts}), flush=True)
 
 
 def run_offered(args, runner, records, B, rank, ws, dev, comm, MetricGroup, model_name, data, lanes, buckets):
@@ -594,6 +678,14 @@ def run_widedeep(args, dev, rank, ws):
     B = args.batch if args.batch != 256 else 4096
     cfg = WideDeepConfig()
     t0 = time.perf_counter()
+    if ws > 1 and "FT_WD_SPARSE_EXCHANGE" not in os.environ:
+        import dataclasses
+
+        from flink_tensorflow_amd import config as C
+
+        # the capturable fixed-capacity exchange: a bounded run that checks for overflow at
+        # its end (ex.check() below) and fails loudly, never a silent drop
+        C.set_current(dataclasses.replace(C.current(), wd_sparse_exchange="bucketed"))
     tr = WideDeepTrainer(cfg, device=dev, seed=0)
     tr.open()
     pool_n = 16 * B

@@ -81,3 +81,53 @@ class TimedWindow:
                        "latencies_s": lat.tolist(), "pid": os.getpid(),
                        "communicator": type(comm.get()).__name__ if comm.is_dist() else None}, f)
         os.replace(tmp, os.path.join(tw["dir"], f"rank{rank}.json"))
+
+
+class TimedSteps:
+    """The same contract for a step-driven operator (``runtime/lockstep.py``
+    ``LockstepTrainer``: agreed training steps, so every rank reaches step ``W`` and step
+    ``W + K`` in the same round): fence after the ``W``-th step, count the records of the
+    next ``K`` steps, fence after step ``W + K`` and write ``rank<r>.json``."""
+
+    def timed_window(self, warmup: int, steps: int, out_dir: str):
+        self._tw = {"w": int(warmup), "k": int(steps), "dir": out_dir, "t0": None, "records": 0}
+        return self
+
+    def _fence(self) -> None:
+        import torch
+
+        from ..parallel import comm
+
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if comm.is_dist():
+            comm.barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    def on_step(self, plan, piece, loss, out, counts=None):
+        from ..runtime.lockstep import piece_len
+
+        tw = self._tw
+        i = self.steps  # steps done, this one included
+        if tw["t0"] is not None:
+            tw["records"] += piece_len(piece)
+        if i == tw["w"]:
+            self._fence()
+            tw["t0"] = time.perf_counter()
+        elif i == tw["w"] + tw["k"] and tw["t0"] is not None:
+            self._fence()
+            self._write_steps(time.perf_counter() - tw["t0"])
+            tw["t0"] = None
+
+    def _write_steps(self, elapsed: float) -> None:
+        from ..parallel import comm
+
+        tw = self._tw
+        rank, world = comm.rank_size()
+        os.makedirs(tw["dir"], exist_ok=True)
+        tmp = os.path.join(tw["dir"], f".rank{rank}.json")
+        with open(tmp, "w") as f:
+            json.dump({"rank": rank, "world": world, "elapsed_s": elapsed, "records": tw["records"],
+                       "steps": tw["k"], "rounds": getattr(self, "rounds", None)}, f)
+        os.replace(tmp, os.path.join(tw["dir"], f"rank{rank}.json"))

@@ -55,12 +55,14 @@ class EngineConfig:
     chain_min_hw: int = 5041
     chain_edge: bool = True            # ... plus the layers leaving that resolution (stride-2 readers)
     wd_fused_step: bool = True         # Wide&Deep: hand-fused GPU step instead of autograd
-    # Wide&Deep under DP (parallel/sparse_exchange.py): "bucketed" = deduplicated rows to
-    # their owner rank (row % world) in fixed-capacity per-peer buckets, owner-side Adagrad,
-    # updated rows back — static shapes, no host sync: the DP step is captured in a hipGraph;
-    # "owner" = the same with exact per-step sizes (host-synced counts, not capturable);
+    # Wide&Deep under DP (parallel/sparse_exchange.py): "owner" (default) = deduplicated rows
+    # to their owner rank (row % world), owner-side Adagrad, updated rows back, with exact
+    # per-step sizes (host-synced counts, not capturable); "bucketed" = the same in
+    # fixed-capacity per-peer buckets — static shapes, no host sync, the DP step captured in
+    # a hipGraph — whose overflow (CapacityExceeded) is recovered by a job restart with
+    # doubled slack, so a job operator refuses it without a restart strategy;
     # "allgather" = the padded all-gather of one row per lookup (capturable, most bytes)
-    wd_sparse_exchange: str = "bucketed"
+    wd_sparse_exchange: str = "owner"
     wd_bucket_slack: float = 2.0       # bucket capacity = slack x (slots / world) + 64
     extra: dict = field(default_factory=dict)
 

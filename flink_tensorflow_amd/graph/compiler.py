@@ -699,9 +699,12 @@ class CompiledFunction(TransformerLowering):
         b_dev = self._dev(bias, torch.float32) if bias is not None else None
         self.params += [w_dev] + ([b_dev] if b_dev is not None else [])
         out = self._new((N, Ho, Wo, Cout))
+        KHe, KWe = w_ohwi.shape[1], w_ohwi.shape[2]
         if (self.precision == "fp8" and residual is None and act in (K.ACT_NONE, K.ACT_RELU) and Cout % 16 == 0
-                and self._fp8_consumers_ok(last.name) and self._qscale(last.name) is not None):
-            # bf16 layer (e.g. the RGB stem) feeding fp8 consumers: emit e4m3 directly
+                and self._fp8_consumers_ok(last.name) and self._qscale(last.name) is not None
+                and self._use_dconv(cin_pad, KHe, KWe, (sh, sw), (dh, dw), 2, residual, act)):
+            # bf16 direct-conv layer (the RGB stem) feeding fp8 consumers: emit e4m3 directly
+            # (a wider bf16 layer hands bf16 on; its fp8 successor quantises on load)
             out = self._new((N, Ho, Wo, Cout), torch.uint8)
             out.qscale = self._qscale(last.name)
         res_val = None
@@ -711,7 +714,6 @@ class CompiledFunction(TransformerLowering):
         xin = x if xin_shape_override is not None else self._ensure_padded(x, cin_pad, node.name)
         for a in absorbed:
             self._fused.add(a.name)
-        KHe, KWe = w_ohwi.shape[1], w_ohwi.shape[2]
         if self._use_dconv(cin_pad, KHe, KWe, (sh, sw), (dh, dw), 2, residual, act):
             bn = 64 if Cout >= 64 else 32
             w_arr = self._dev(K.dconv_bf16_weight_bytes(w_ohwi, bn))

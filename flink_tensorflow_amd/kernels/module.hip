@@ -15,7 +15,6 @@ void register_transformer(pybind11::module_& m);
 void register_embedding(pybind11::module_& m);
 void register_fp8(pybind11::module_& m);
 void register_attention(pybind11::module_& m);
-void register_igemm_v2(pybind11::module_& m);
 void register_dconv(pybind11::module_& m);
 void register_elementwise(pybind11::module_& m);
 void register_conv3x3c64(pybind11::module_& m);
@@ -26,7 +25,6 @@ void register_widedeep(pybind11::module_& m);
 void register_sort_segments(pybind11::module_& m);
 void register_pw_res(pybind11::module_& m);
 void register_gemm_train(pybind11::module_& m);
-void register_wino3x3(pybind11::module_& m);
 
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "flink_tensorflow_amd CDNA4 (gfx950) kernels";
@@ -37,7 +35,6 @@ PYBIND11_MODULE(_hip, m) {
   register_embedding(m);
   register_fp8(m);
   register_attention(m);
-  register_igemm_v2(m);
   register_dconv(m);
   register_elementwise(m);
   register_conv3x3c64(m);
@@ -48,7 +45,6 @@ PYBIND11_MODULE(_hip, m) {
   register_sort_segments(m);
   register_pw_res(m);
   register_gemm_train(m);
-  register_wino3x3(m);
   // Streams owned by the framework (not torch's round-robin pool of 32 per device): a pooled
   // stream handed to a runner can be the very stream another thread is capturing a hipGraph
   // on, and then that thread's launches land in the capture (or are rejected).

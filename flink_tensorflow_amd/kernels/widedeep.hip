@@ -104,8 +104,13 @@ __global__ __launch_bounds__(256) void wd_loss_kernel(const bf16* __restrict__ h
                                                       const float* __restrict__ labels, int ldl, int B,
                                                       int nvalid, float norm, float* __restrict__ dlogit,
                                                       bf16* __restrict__ dlogit16, float* __restrict__ part,
-                                                      float* __restrict__ wgrad, int C, int WD) {
+                                                      float* __restrict__ wgrad, int C, int WD,
+                                                      const int* __restrict__ args) {
   __shared__ float red[2][4];
+  if (args) {  // device-resident {nvalid, norm bits}: one captured step serves every piece size
+    nvalid = args[0];
+    norm = __int_as_float(args[1]);
+  }
   const int b = blockIdx.x * 256 + threadIdx.x;
   float lo = 0.f, d = 0.f;
   if (b >= nvalid && b < B) {  // padding rows of a batch rounded up to the GEMM granule: no loss, no gradient
@@ -148,7 +153,9 @@ __global__ __launch_bounds__(256) void wd_loss_kernel(const bf16* __restrict__ h
 
 __global__ __launch_bounds__(64) void wd_loss_final_kernel(const float* __restrict__ part, int nb, float norm,
                                                            float* __restrict__ loss, float* __restrict__ g_wbias,
-                                                           float* __restrict__ g_hb0, float* __restrict__ step) {
+                                                           float* __restrict__ g_hb0, float* __restrict__ step,
+                                                           const int* __restrict__ args) {
+  if (args) norm = __int_as_float(args[1]);
   float a = 0.f, s = 0.f;
   for (int i = threadIdx.x; i < nb; i += 64) {
     a += part[2 * i];
@@ -332,12 +339,16 @@ void wd_keys(uintptr_t cats, int ldc, uintptr_t cross, int ldx, uintptr_t keys, 
 // step (optional, 0 = none): Adam's step counter, incremented here so the captured step has
 // no separate increment launch.
 // nvalid <= B: rows [nvalid, B) are padding (a batch rounded up to the training GEMM's
-// 8-row granule) and get zero loss and gradient.
+// 8-row granule, or an agreed step's piece padded to the fixed micro-batch) and get zero
+// loss and gradient.  args (0 = none): device int32 {nvalid, bits of float norm} read by the
+// kernels instead of the host values — the agreed step of runtime/lockstep.py is captured
+// once and replayed for every piece size (0 <= nvalid <= B, norm > 0 when the step runs).
 void wd_loss(uintptr_t head, int ldh, uintptr_t wsum, uintptr_t wbias, uintptr_t labels, int ldl, int B, int nvalid,
              float norm, uintptr_t dlogit, uintptr_t dlogit16, uintptr_t loss, uintptr_t g_wbias, uintptr_t g_hb0,
-             uintptr_t wgrad, int C, int WD, uintptr_t part, uintptr_t step, uintptr_t stream) {
-  if (B <= 0 || nvalid <= 0 || nvalid > B) throw std::invalid_argument("wd_loss: empty batch or bad nvalid");
-  if (!(norm > 0.f)) throw std::invalid_argument("wd_loss: norm must be positive");
+             uintptr_t wgrad, int C, int WD, uintptr_t part, uintptr_t step, uintptr_t args, uintptr_t stream) {
+  if (B <= 0 || (!args && (nvalid <= 0 || nvalid > B))) throw std::invalid_argument("wd_loss: empty batch or bad nvalid");
+  if (!args && !(norm > 0.f)) throw std::invalid_argument("wd_loss: norm must be positive");
+  if (args % 8) throw std::invalid_argument("wd_loss: args must be 8-byte aligned");
   if (wgrad % 16) throw std::invalid_argument("wd_loss: wgrad must be 16-byte aligned");
   auto s = reinterpret_cast<hipStream_t>(stream);
   const int nb = (B + 255) / 256;
@@ -345,10 +356,10 @@ void wd_loss(uintptr_t head, int ldh, uintptr_t wsum, uintptr_t wbias, uintptr_t
                      reinterpret_cast<const float*>(wsum), reinterpret_cast<const float*>(wbias),
                      reinterpret_cast<const float*>(labels), ldl, B, nvalid, norm, reinterpret_cast<float*>(dlogit),
                      reinterpret_cast<bf16*>(dlogit16), reinterpret_cast<float*>(part), reinterpret_cast<float*>(wgrad),
-                     C, WD);
+                     C, WD, reinterpret_cast<const int*>(args));
   hipLaunchKernelGGL(wd_loss_final_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<const float*>(part), nb, norm,
                      reinterpret_cast<float*>(loss), reinterpret_cast<float*>(g_wbias), reinterpret_cast<float*>(g_hb0),
-                     reinterpret_cast<float*>(step));
+                     reinterpret_cast<float*>(step), reinterpret_cast<const int*>(args));
   FTM_CHECK_LAUNCH();
 }
 

@@ -147,12 +147,19 @@ class FusedWideDeepStep:
         H = a.h[-1].shape[1]
         a.head_part = torch.empty(self.head_blocks, 2 * H, dtype=torch.float32, device=dev)
 
-    def step(self, labels, dense, cats, cross, norm: int | None = None) -> torch.Tensor:
+    def step(self, labels, dense, cats, cross, norm: int | None = None, args: torch.Tensor | None = None
+             ) -> torch.Tensor:
         """One step.  ``norm``: an agreed data-parallel step over uneven pieces
         (``parallel/step_agreement.py``) — the loss is this piece's sum over the round's
-        global record count and the all-reduced gradients are summed, not averaged."""
+        global record count and the all-reduced gradients are summed, not averaged.
+        ``args``: the same, with the piece's valid-row count and the global count in device
+        memory (int32 ``{nvalid, bits of float norm}``, ``PackedBatchStager`` header): the
+        batch is a fixed-size piece padded with look-up-nothing rows, so one captured step
+        replays for every piece size (``WideDeepTrainer`` agreed steps)."""
         H, m, cfg = self._H, self.m, self.cfg
         nvalid = labels.shape[0]
+        if args is not None and nvalid % 8:
+            raise ValueError("fused step: a device-argument batch must be a multiple of 8 rows")
         if nvalid % 8:  # the training GEMMs take 8-row granules: pad with rows that look up
             # nothing (ids < 0) and get zero loss and gradient (wd_loss nvalid)
             pad = 8 - nvalid % 8
@@ -205,7 +212,7 @@ class FusedWideDeepStep:
                   a.dlogit.data_ptr(),
                   a.dlogit16.data_ptr(), a.loss.data_ptr(),
                   self.g["wide_bias"].data_ptr(), self.g["head.bias"].data_ptr(), a.wgrad.data_ptr(), C, WD, a.part.data_ptr(),
-                  self.t.data_ptr(), s)  # also counts Adam's step
+                  self.t.data_ptr(), args.data_ptr() if args is not None else 0, s)  # also counts Adam's step
         # backward: head (only logit column 0 is used) -> dh, top bias and head weight gradients
         last = a.h[-1]
         Hl = last.shape[1]
@@ -257,7 +264,7 @@ class FusedWideDeepStep:
             sparse_adagrad(m.wide.table.data, m.wide.accum, uw, rw, self.lr_sparse, offset=FV)
         for w in works:  # dense gradients reduced (overlapped with the GEMMs + sparse pipeline)
             w.wait()
-        self._adam(1.0 / ws if norm is None else 1.0, s)
+        self._adam(1.0 / ws if norm is None and args is None else 1.0, s)
         return a.loss
 
     def _adam(self, scale: float, s) -> None:
@@ -306,6 +313,14 @@ class FusedWideDeepStep:
         self.t.add_(1.0)
         self._adam(1.0, s)
         return torch.zeros((), dtype=torch.float32, device=dev)
+
+    def mutable_tensors(self) -> list[torch.Tensor]:
+        """Every device tensor a step writes that outlives it (dense masters, Adam state,
+        step count, the tables and their Adagrad accumulators): what a capture's warm-up
+        steps must hand back unchanged (``WideDeepTrainer._capture_agreed``)."""
+        m = self.m
+        return [self.flat, self.exp_avg, self.exp_avg_sq, self.t, m.emb.table.data, m.emb.accum, m.wide.table.data,
+                m.wide.accum]
 
     # ------------------------------------------------------------------ checkpoints
     def state(self) -> dict[str, torch.Tensor]:

@@ -12,7 +12,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from .kernels import V2_CONFIGS, _apply_act_ref, _check, _hip, _stream, act_code, conv_out_hw
+from .kernels import _apply_act_ref, _check, _hip, _stream, act_code, conv_out_hw
 
 FP8_MAX = 448.0
 E4M3 = torch.float8_e4m3fn
@@ -116,11 +116,6 @@ def conv2d_nhwc_fp8(x: torch.Tensor, x_scale: float, wq: torch.Tensor, kshape, w
         _check(chan_scale, "chan_scale", torch.float32, x.device)
         _check(bias, "bias", torch.float32, x.device)
         _check(out, "out", odt, x.device)
-        if cfg in V2_CONFIGS and not in_bf16:  # pipelined LDS-DMA kernel (igemm_v2.hip)
-            _hip().igemm_v2(x.data_ptr(), wq.data_ptr(), chan_scale.data_ptr(), bias.data_ptr(), 0, out.data_ptr(), 1,
-                            N, H, W, Cin, Cout, KH, KW, sh, sw, pt, pl, dh, dw, Ho, Wo, ldy, out_channel_offset, 0,
-                            int(out_fp8), 1.0 / out_scale if out_fp8 else 1.0, a, V2_CONFIGS[cfg], _stream())
-            return out
         _hip().conv2d_nhwc_fp8(x.data_ptr(), wq.data_ptr(), chan_scale.data_ptr(), bias.data_ptr(), out.data_ptr(), N,
                                H, W, Cin, Cout, KH, KW, sh, sw, pt, pl, dh, dw, Ho, Wo, ldy, out_channel_offset,
                                int(in_bf16), 1.0 / x_scale, int(out_fp8), 1.0 / out_scale if out_fp8 else 1.0, a,

@@ -85,9 +85,8 @@ def _zeros_bias(n: int, device) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------------------ conv
-# tile configs >= 16 select the pipelined 256-pixel LDS-DMA kernel (igemm_v2.hip) with
-# 128 or 64 output channels per tile; 0..4 are the register-staged igemm_bf16 tiles
-V2_CONFIGS = {16: 128, 17: 64, 18: 256}  # 18: GEMM mode only
+# tile configs 0..4 are the register-staged igemm_bf16 tiles (-1: chosen by shape); the
+# pipelined 256-pixel LDS-DMA kernel (igemm_v2) was in no default plan and was removed (r06)
 def conv_out_hw(H, W, KH, KW, sh, sw, ph, pw, dh=1, dw=1, ph_hi=None, pw_hi=None):
     ph_hi = ph if ph_hi is None else ph_hi
     pw_hi = pw if pw_hi is None else pw_hi
@@ -104,8 +103,8 @@ def conv2d_nhwc(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor | None
 
     Fused epilogue ``act(conv + bias + residual)``.  With ``out`` given, the result is
     written at channel offset ``out_channel_offset`` of ``out`` (concat-by-stride-write).
-    ``out_scale`` stores the result as OCP e4m3 bytes (``y / out_scale``, uint8) — the bf16
-    stem of an fp8 network hands its successor fp8 directly (pipelined kernel only).
+    ``out_scale`` stores the result as OCP e4m3 bytes (``y / out_scale``, uint8): host
+    reference only (the reference of ``conv2d_direct``'s fp8 epilogue).
     """
     a = act_code(act)
     N, H, W, Cin = x.shape
@@ -119,8 +118,9 @@ def conv2d_nhwc(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor | None
     if out_scale is not None:
         if residual is not None:
             raise ValueError("conv2d_nhwc: fp8 output does not take a residual")
-        if cfg not in V2_CONFIGS:
-            cfg = 17 if Cout <= 64 else 16
+        if x.is_cuda:
+            raise ValueError("conv2d_nhwc: e4m3 output is host-reference only on the implicit GEMM; "
+                             "fp8 stems run on conv2d_direct")
     if out is None:
         odt = torch.uint8 if out_scale is not None else (x.dtype if x.is_cuda else torch.float32)
         out = torch.empty((N, Ho, Wo, Cout), dtype=odt, device=x.device)
@@ -143,12 +143,6 @@ def conv2d_nhwc(x: torch.Tensor, w_ohwi: torch.Tensor, bias: torch.Tensor | None
         else:
             bias = _zeros_bias(Cout, x.device)
         # bottom/right padding is implied by the kernel's bounds check (Ho/Wo carry it)
-        if cfg in V2_CONFIGS:  # pipelined LDS-DMA kernel (igemm_v2.hip)
-            _hip().igemm_v2(x.data_ptr(), w_ohwi.data_ptr(), 0, bias.data_ptr(), _ptr(residual), out.data_ptr(), 2,
-                            N, H, W, Cin, Cout, KH, KW, sh, sw, pt, pl, dh, dw, Ho, Wo, out.shape[3], out_channel_offset,
-                            Cout if residual is None else residual.shape[3], int(out_scale is not None),
-                            1.0 / out_scale if out_scale is not None else 1.0, a, V2_CONFIGS[cfg], _stream())
-            return out
         _hip().conv2d_nhwc_bf16(x.data_ptr(), w_ohwi.data_ptr(), bias.data_ptr(), _ptr(residual), out.data_ptr(),
                                 N, H, W, Cin, Cout, KH, KW, sh, sw, pt, pl, dh, dw, Ho, Wo, out.shape[3],
                                 out_channel_offset, Cout if residual is None else residual.shape[3], a, _stream(), cfg)
@@ -180,114 +174,6 @@ def conv3x3_c64_eligible(x_shape, w_shape, stride, pad, dilation, residual, act)
     return (Cin == 64 and Cout == 64 and (KH, KW) == (3, 3) and tuple(stride) == (1, 1) and tuple(pad) == (1, 1, 1, 1)
             and tuple(dilation) == (1, 1) and residual is None and act_code(act) in (ACT_NONE, ACT_RELU)
             and H >= 8 and W >= 32 and N * H * W * Cin * 2 < 2 ** 31)
-
-
-# ------------------------------------------------------------------------------ Winograd
-# F(2x2, 3x3) (kernels/wino3x3.hip): Y = A^T [(G g G^T) .* (B^T d B)] A per 2x2 output tile
-_WG = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
-_WBT = ((1, 0, -1, 0), (0, 1, 1, 0), (0, -1, 1, 0), (0, 1, 0, -1))
-_WAT = ((1, 1, 1, 0), (0, 1, -1, -1))
-WINO_TB = 64        # tiles per workgroup (kernels/wino3x3.hip TB)
-WINO_MAX_CHUNKS = 12 * 256
-
-
-@functools.lru_cache(maxsize=None)
-def wino_f23_max_rows(N: int, H: int, W: int) -> int:
-    """Padded input rows the worst 64-tile block of a layer stages (mirror of
-    ``wino_f23_max_rows`` in kernels/wino3x3.hip; memoised: eager launches call it)."""
-    TH, TW = (H + 1) // 2, (W + 1) // 2
-    per, Hp = TH * TW, 2 * TH + 2
-    T = N * per
-    worst = 0
-    for t0 in range(0, T, WINO_TB):
-        ta, tb = t0, min(t0 + WINO_TB - 1, T - 1)
-        na, tya = ta // per, (ta % per) // TW
-        nb, tyb = tb // per, (tb % per) // TW
-        worst = max(worst, nb * Hp + 2 * tyb + 4 - (na * Hp + 2 * tya))
-    return worst
-
-
-def wino_f23_eligible(x_shape, w_shape, stride, pad, dilation, residual, act) -> bool:
-    """3x3 / stride 1 / SAME, Cin % 32 == 0, Cout % 64 == 0, no residual, bias (+ReLU), and a
-    64-tile block whose staged input rows fit the kernel's per-thread staging (<= 12 x 256
-    16-byte chunks per K-step): every stride-1 3x3 of ResNet-50 at any batch."""
-    if len(x_shape) != 4:
-        return False
-    N, H, W, Cin = x_shape
-    Cout, KH, KW, Ci = w_shape
-    if not (Cin == Ci and Cin % 32 == 0 and Cout % 64 == 0 and (KH, KW) == (3, 3) and tuple(stride) == (1, 1)
-            and tuple(pad) == (1, 1, 1, 1) and tuple(dilation) == (1, 1) and residual is None
-            and act_code(act) in (ACT_NONE, ACT_RELU) and N * H * W * Cin * 2 < 2 ** 31 - 4096):
-        return False
-    return wino_f23_max_rows(N, H, W) * 8 * ((W + 1) // 2 + 1) <= WINO_MAX_CHUNKS
-
-
-def wino_f23_weights(w_hwio: torch.Tensor) -> torch.Tensor:
-    """fp16 U = G g G^T of a [3, 3, Cin, Cout] filter (BN folded), laid out as the kernel's
-    MFMA A fragments: ``[Cout/32][Cin/16][16 xi][64 lanes][8]`` with lane ``r + 32 h``
-    holding ``U[xi][16 ks + 8 h + j][32 cbg + r]``, j = 0..7 (computed in fp64, one
-    rounding)."""
-    KH, KW, C, K = w_hwio.shape
-    if (KH, KW) != (3, 3) or C % 16 or K % 32:
-        raise ValueError(f"wino_f23_weights: bad filter shape {tuple(w_hwio.shape)}")
-    G = torch.tensor(_WG, dtype=torch.float64)
-    U = torch.einsum("ia,abck,jb->ijck", G, w_hwio.detach().to("cpu", torch.float64), G).reshape(16, C, K)
-    U = U.reshape(16, C // 16, 2, 8, K // 32, 32).permute(4, 1, 0, 2, 5, 3)
-    return U.contiguous().reshape(-1).to(torch.float16)
-
-
-def wino_f23_reference(x: torch.Tensor, u_frag: torch.Tensor, Cout: int, bias: torch.Tensor | None, act=None,
-                       fp16_domain: bool = True) -> torch.Tensor:
-    """Host model of the kernel's arithmetic from its own weight fragments: NHWC input ->
-    padded 4x4 patches per 2x2 tile -> V = B^T d B (fp16 when ``fp16_domain``, as staged and
-    transformed on the GPU) -> M_xi = V_xi . U_xi (fp32) -> Y = A^T M A + bias -> act."""
-    N, H, W, C = x.shape
-    TH, TW = (H + 1) // 2, (W + 1) // 2
-    U = u_frag.reshape(Cout // 32, C // 16, 16, 2, 32, 8).permute(2, 1, 3, 5, 0, 4).reshape(16, C, Cout).float()
-    xp = torch.zeros((N, 2 * TH + 2, 2 * TW + 2, C), dtype=torch.float32)
-    xp[:, 1:H + 1, 1:W + 1] = x.detach().to("cpu", torch.float32)
-    if fp16_domain:
-        xp = xp.half().float()
-    d = xp.unfold(1, 4, 2).unfold(2, 4, 2)  # [N, TH, TW, C, 4, 4]
-    BT = torch.tensor(_WBT, dtype=torch.float32)
-    V = torch.einsum("ia,ntwcab,jb->ntwijc", BT, d, BT).reshape(N, TH, TW, 16, C)
-    if fp16_domain:
-        V = V.half().float()
-    M = torch.einsum("ntwxc,xck->ntwxk", V, U).reshape(N, TH, TW, 4, 4, Cout)
-    AT = torch.tensor(_WAT, dtype=torch.float32)
-    Y = torch.einsum("ri,ntwijk,cj->ntrwck", AT, M, AT).reshape(N, 2 * TH, 2 * TW, Cout)[:, :H, :W]
-    if bias is not None:
-        Y = Y + bias.detach().to("cpu", torch.float32)
-    if act_code(act) == ACT_RELU:
-        Y = torch.relu(Y)
-    return Y
-
-
-def wino_f23(x: torch.Tensor, u_frag: torch.Tensor, Cout: int, bias: torch.Tensor, act=None,
-             out: torch.Tensor | None = None, out_channel_offset: int = 0) -> torch.Tensor:
-    """3x3 / s1 / SAME conv by Winograd F(2x2, 3x3): ``act(conv + bias)`` with the fp16 U
-    fragments of :func:`wino_f23_weights`.  GPU: kernels/wino3x3.hip; host: the same
-    arithmetic in torch (:func:`wino_f23_reference`)."""
-    N, H, W, C = x.shape
-    a = act_code(act)
-    if out is None:
-        out = torch.empty((N, H, W, Cout), dtype=torch.bfloat16 if x.is_cuda else torch.float32, device=x.device)
-        out_channel_offset = 0
-    if not wino_f23_eligible(tuple(x.shape), (Cout, 3, 3, C), (1, 1), (1, 1, 1, 1), (1, 1), None, a):
-        raise ValueError(f"wino_f23: unsupported shapes x {tuple(x.shape)} -> {Cout} channels")
-    if out.shape[:3] != (N, H, W) or out_channel_offset + Cout > out.shape[3] or u_frag.numel() != 16 * C * Cout:
-        raise ValueError("wino_f23: output buffer or weight fragments do not fit")
-    if x.is_cuda:
-        _check(x, "x", device=x.device)
-        _check(u_frag, "u", torch.float16, x.device)
-        _check(out, "out", device=x.device)
-        _check(bias, "bias", torch.float32, x.device)
-        _hip().wino_f23_bf16(x.data_ptr(), u_frag.data_ptr(), bias.data_ptr(), out.data_ptr(), N, H, W, C, Cout,
-                             out.shape[3], out_channel_offset, a, _stream())
-        return out
-    y = wino_f23_reference(x, u_frag, Cout, bias, a, fp16_domain=False)
-    out[..., out_channel_offset:out_channel_offset + Cout] = y.to(out.dtype)
-    return out
 
 
 _NUM_CU: dict = {}
@@ -424,10 +310,6 @@ def gemm(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = None, 
             bias = _zeros_bias(N, x.device)
         if residual is not None:
             _check(residual, "residual", device=x.device)
-        if cfg in V2_CONFIGS:  # pipelined LDS-DMA kernel, GEMM mode (1x1 "conv" over M rows)
-            _hip().igemm_v2(x2.data_ptr(), w_nk.data_ptr(), 0, bias.data_ptr(), _ptr(residual), out2.data_ptr(), 2, 1,
-                            M, 1, K, N, 1, 1, 1, 1, 0, 0, 1, 1, M, 1, N, 0, N, 0, 1.0, a, V2_CONFIGS[cfg], _stream())
-            return out
         _hip().gemm_bf16(x2.data_ptr(), w_nk.data_ptr(), bias.data_ptr(), _ptr(residual), out2.data_ptr(), M, N, K, K,
                          N, N, a, _stream(), cfg)
         return out

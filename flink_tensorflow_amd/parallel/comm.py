@@ -221,6 +221,7 @@ class RcclCommunicator(Communicator):
 
         self._lib = _ext.rccl()
         self.rank, self.size = rank, size
+        self.store = store  # the rendezvous store: also the host control channel (step agreement)
         self.device = torch.device(device)
         if unique_id is None:
             if rank == 0:

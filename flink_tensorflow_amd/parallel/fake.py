@@ -17,12 +17,15 @@ from .comm import Communicator
 
 
 class FakeCommunicator(Communicator):
+    capturable = False  # host round trips: never inside a hipGraph capture
+
     def __init__(self, rank: int, size: int, device="cpu", store=None):
         if store is None:
             raise ValueError("FakeCommunicator needs the rendezvous store")
         self.rank, self.size = rank, size
         self.device = torch.device(device)
         self._store = store
+        self.store = store  # host control channel (parallel/step_agreement.py HostChannel)
         self._seq = 0
 
     _CHUNK = 4 << 20  # the TCP store rejects values above 8 MiB

@@ -226,6 +226,7 @@ class _Task:
                              self.job.config, self.job)
         ctx.global_index = self.job.rank * self.node.parallelism + self.subtask
         ctx.global_parallelism = self.job.world_size * self.node.parallelism
+        ctx.restart_attempts = self.job.env.restart_strategy.attempts
         return ctx
 
     def start(self):

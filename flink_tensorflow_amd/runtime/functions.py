@@ -20,6 +20,7 @@ class RuntimeContext:
         self.parallelism = parallelism
         self.device = device
         self.attempt = attempt
+        self.restart_attempts: int | None = None  # the job's restart budget (None: not in a job)
         self.metrics = metrics
         self.config = config
         self._job = job

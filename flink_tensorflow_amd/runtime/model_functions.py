@@ -56,6 +56,7 @@ class ModelAwareFunction(F.RichFunction):
         ctx = getattr(self, "_runtime_context", None)
         if ctx is not None and hasattr(self.model, "restart_attempt"):
             self.model.restart_attempt = ctx.attempt  # models that adapt after a failure
+            self.model.restart_budget = getattr(ctx, "restart_attempts", None)
         open_model(self.model, ctx.device if ctx is not None else None)
 
     def close(self):

@@ -459,6 +459,7 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
         ctx = RuntimeContext(spec["name"], spec["subtask"], spec["parallelism"], device, spec["attempt"], metrics,
                              spec["config"], None)
         ctx.global_index, ctx.global_parallelism = spec["global_index"], spec["global_parallelism"]
+        ctx.restart_attempts = spec.get("restarts")
         ctx.worker_pid = os.getpid()
         group = _open_group(spec, device)
         op = _GroupBound(cloudpickle.loads(factory)(), group)
@@ -588,6 +589,7 @@ def _run_source_chain(msg, inp, out, emit, flush, parent_alive):
         ctx = RuntimeContext(sp["name"], sp["subtask"], sp["parallelism"], device if sp["gpu"] else None,
                              sp["attempt"], mg, sp["config"], None)
         ctx.global_index, ctx.global_parallelism = sp["global_index"], sp["global_parallelism"]
+        ctx.restart_attempts = sp.get("restarts")
         ctx.worker_pid = os.getpid()
         op.setup(ctx, Output(into(ops[i + 1]) if i + 1 < len(ops) else emit, side))
         op.initialize(restores[i], restore_dir)
@@ -794,6 +796,7 @@ class RemoteOperatorProxy:
             self.slab.unlink()
         spec = {"name": self.node.name, "subtask": self.subtask, "parallelism": self.node.parallelism,
                 "gpu": bool(self.node.uses_gpu), "attempt": self.job.attempt, "config": self.job.config,
+                "restarts": self.job.env.restart_strategy.attempts,
                 "global_index": self.ctx.global_index, "global_parallelism": self.ctx.global_parallelism,
                 "group": _job_group(self.job, self.node)}
         self._send(("init", cloudpickle.dumps(self.node.factory), spec, snapshot, checkpoint_dir))
@@ -990,6 +993,7 @@ class RemoteChainProxy(RemoteOperatorProxy):
         self.from_worker.unlink()
         specs = [{"name": n.name, "subtask": self.subtask, "parallelism": n.parallelism, "gpu": bool(n.uses_gpu),
                   "attempt": self.job.attempt, "config": self.job.config, "global_index": c.global_index,
+                  "restarts": self.job.env.restart_strategy.attempts,
                   "global_parallelism": c.global_parallelism, "group": _job_group(self.job, n)}
                  for n, c in zip(self.nodes, contexts)]
         self._send(("init_chain", [cloudpickle.dumps(n.factory) for n in self.nodes], specs, list(restores),

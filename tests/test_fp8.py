@@ -116,7 +116,7 @@ def _conv_case(cin, cout, k, stride, pads, in_bf16, out_fp8, cfg, offset=0, extr
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [0, 1, 2, 11, 16, 17])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 11])
 def test_conv_fp8_configs_gpu(cfg):
     _conv_case(32, 64, 3, 1, (1, 1, 1, 1), False, True, cfg)
     _conv_case(64, 192, 3, 2, (0, 0, 0, 0), False, False, cfg)
@@ -306,22 +306,6 @@ def test_inception_v3_fp8_plan_gpu():
     lh = host({"images:0": img})[0]
     ld = dev({"images:0": img.to(DEV)})[0].cpu()
     assert F.cosine_similarity(lh.flatten(), ld.flatten(), dim=0) > 0.99
-
-
-@pytest.mark.gpu
-def test_bf16_conv_fp8_output_gpu():
-    """bf16 stem conv writing e4m3 for its fp8 successor (pipelined kernel)."""
-    from flink_tensorflow_amd.ops import kernels as K
-
-    torch.manual_seed(3)
-    x = torch.randn(2, 31, 31, 8).to(torch.bfloat16)
-    w = (torch.randn(32, 3, 3, 8) / 5).to(torch.bfloat16)
-    b = torch.randn(32) * 0.1
-    ref = K.conv2d_nhwc(x, w, b, None, (2, 2), (0, 0, 0, 0), (1, 1), "relu", out_scale=0.01)
-    got = K.conv2d_nhwc(x.to(DEV), w.to(DEV), b.to(DEV), None, (2, 2), (0, 0, 0, 0), (1, 1), "relu",
-                        out_scale=0.01).cpu()
-    gd, rd = Q.from_fp8_bytes(got), Q.from_fp8_bytes(ref)
-    assert ((gd - rd).abs() <= 0.13 * rd.abs() + 1e-3).all()
 
 
 @pytest.mark.gpu

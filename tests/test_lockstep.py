@@ -33,9 +33,9 @@ class _Logged(LockstepTrainer):
 
         super().__init__(WideDeepTrainer(WideDeepConfig.tiny(), device=device, seed=3), batch, max_delay_ms)
 
-    def on_step(self, plan, piece, loss, out):
+    def on_step(self, plan, piece, loss, out, counts=None):
         out.collect(("piece", self.get_runtime_context().attempt, self.steps, self.rank, [r[4] for r in piece],
-                     plan.counts))
+                     counts))
 
     def on_finished(self, out):
         out.collect(("digest", self.rank, self.steps, _digest(self.model.model, self.model._exchange)))
@@ -101,10 +101,15 @@ def _check(recs, out, final_attempt=0):
 def test_step_agreement_plan_local():
     a = StepAgreement()
     p = a.round(5, ended=False, barrier=-1)
-    assert p == RoundPlan((5,), (False,), (-1,), (0,), 0) and p.step and not p.finished
+    assert p == RoundPlan(((5,),), (False,), (-1,), (0,), 0) and p.step and not p.finished
     assert a.round(0, ended=True).finished
-    assert RoundPlan((0, 0), (True, False), (3, 3), (0, 0)).snapshot_barrier == 3
-    assert RoundPlan((0, 0), (False, False), (3, -1), (0, 0)).snapshot_barrier is None
+    assert RoundPlan(((), ()), (True, False), (3, 3), (0, 0)).snapshot_barrier == 3
+    assert RoundPlan(((), ()), (False, False), (3, -1), (0, 0)).snapshot_barrier is None
+    # k steps per round: the busiest rank sets k, the others bring empty pieces
+    q = a.round(7, full=3, batch=64)
+    assert q.pieces == ((64, 64, 64, 7),) and q.k == 4 and q.total == 199
+    r = RoundPlan(((64, 64, 64), (), (64, 10)), (False,) * 3, (-1,) * 3, (0,) * 3)
+    assert r.k == 3 and [r.counts_at(j) for j in range(3)] == [(64, 0, 64), (64, 0, 10), (64, 0, 0)]
 
 
 def test_uneven_5_to_3_split_matches_one_rank_reference():
@@ -250,4 +255,186 @@ def test_idle_rank_and_three_ranks_match_reference():
     assert sorted(by_step) == list(range(1, digests[0][2] + 1))
     assert all(len(s.get(2, [])) == 0 for s in by_step.values())  # rank 2 never had data
     assert sorted(i for s in by_step.values() for ids in s.values() for i in ids) == list(range(len(recs)))
+    assert _reference_p(recs, by_step, P) == digests[0][3]
+
+
+class _SleepStep:
+    """A stand-in trainer whose step is one small collective plus 4 ms of "GPU" work: the
+    skew test measures the agreement protocol, not a model."""
+
+    def train_step(self, piece, counts=None):
+        import time
+
+        import torch
+
+        from flink_tensorflow_amd.parallel import comm
+
+        if comm.is_dist():
+            comm.get().all_reduce(torch.ones(1))
+        time.sleep(0.004)
+        return 0.0
+
+
+class _Timed(LockstepTrainer):
+    """Records each step's wall time and piece size."""
+
+    def __init__(self, **kw):
+        super().__init__(_SleepStep(), BATCH, **kw)
+
+    def on_step(self, plan, piece, loss, out, counts=None):
+        import time
+
+        from flink_tensorflow_amd.runtime.lockstep import piece_len
+
+        out.collect(("step", self.rank, time.perf_counter(), piece_len(piece)))
+
+
+def _busy_rank_rate(skew: bool, **kw) -> tuple[float, int]:
+    """P = 2; rank 0's generator yields 40 micro-batches of packed rows in blocks of 3
+    batches; rank 1's the same (unskewed), or nothing for 3 s (skewed: its source is alive
+    but idle, so it only heartbeats): rank 0's steps per second between its first and last
+    step, and the records it trained."""
+    import time
+
+    import numpy as np
+
+    from flink_tensorflow_amd.parallel.fake import FakeCommunicator
+
+    rows = np.zeros((40 * BATCH, 64), np.uint8)
+
+    def gen(idx, par, start):
+        if skew and idx == 1:
+            t_end = time.time() + 3.0
+            while time.time() < t_end:
+                time.sleep(0.01)
+            return
+        for b in range(0, len(rows), 3 * BATCH):
+            yield rows[b:b + 3 * BATCH]
+
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(2)
+    env.enable_job_communicator(True, communicator=FakeCommunicator)
+    sink = env.generate(gen).run_in_processes().process(_Timed(**kw)).name("trainer").run_in_processes() \
+        .collect_into()
+    env.execute("lockstep-skew")
+    st = sorted((t, n) for kind, r, t, n in (o for o in sink.results() if o[0] == "step") if r == 0)
+    busy = [t for t, n in st if n]
+    return (len(busy) - 1) / (busy[-1] - busy[0]), sum(n for _, n in st)
+
+
+def test_idle_rank_does_not_gate_the_busy_rank():
+    """with one rank starved (its source alive but idle) the busy rank
+    must keep stepping at >= 80 % of its unskewed rate — the idle rank follows the busy
+    one round after round (``busy_poll_ms``) instead of joining once per ``max_delay_ms``
+    heartbeat (which capped it at 1000 / max_delay_ms = 20 steps/s here), and each round
+    carries every full batch the busy rank holds.  Both sources are chained into their
+    trainer in the worker and hand over packed-row blocks (the bench job's record form)."""
+    kw = dict(max_delay_ms=50.0, steps_per_round=2)
+    even, n_even = _busy_rank_rate(False, **kw)
+    skew, n_skew = _busy_rank_rate(True, **kw)
+    assert n_even == n_skew == 40 * BATCH  # every record of rank 0 trained exactly once
+    print(f"[lockstep] busy-rank step rate: unskewed {even:.1f}/s, skewed {skew:.1f}/s ({skew / even:.2f})")
+    assert skew >= 0.8 * even, (skew, even)
+    assert skew > 2 * 1000 / 50.0  # far above the one-step-per-heartbeat bound
+
+
+@pytest.mark.gpu
+def test_agreed_step_captured_tracks_exact_step_gpu():
+    """The captured agreed step (pieces padded to the fixed micro-batch with look-up-nothing
+    rows, ``{nvalid, norm}`` in the staged header, ONE hipGraph for every piece size) tracks
+    the exact uneven-piece step, capturing trains nothing (the first step equals the exact
+    first step), and the replays never synchronise with the host."""
+    import numpy as np
+
+    from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, WideDeepTrainer, pack_click_records
+
+    cfg = WideDeepConfig.tiny()
+    recs = [r[:4] for r in _records(6 * BATCH)]
+    a = WideDeepTrainer(cfg, device="cuda", seed=3)
+    b = WideDeepTrainer(cfg, device="cuda", seed=3)
+    a.micro_batch = BATCH
+    a.open()
+    b.open()
+    sizes = [BATCH, 40, BATCH, 17, BATCH, 3]
+    pieces, o = [], 0
+    for n in sizes:
+        pieces.append(recs[o:o + n])
+        o += n
+    # packed-row blocks for a (the job's record form), tuples for b
+    blocks = [[np.ascontiguousarray(pack_click_records(p, cfg, 3))] for p in pieces]
+    la = [a.train_step(blocks[0], counts=[sizes[0]]).clone()]
+    assert a._ag is not None and a._ag.graph is not None  # captured on the first piece
+    lb = [b.train_step(pieces[0], counts=[sizes[0]]).clone()]
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        for p, n in zip(blocks[1:], sizes[1:]):
+            la.append(a.train_step(p, counts=[n]).clone())
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    for p, n in zip(pieces[1:], sizes[1:]):
+        lb.append(b.train_step(p, counts=[n]).clone())
+    torch.testing.assert_close(torch.stack(la), torch.stack(lb), rtol=2e-3, atol=2e-4)
+    for (k, va), vb in zip(b.model.state_dict().items(), a.model.state_dict().values()):
+        torch.testing.assert_close(vb.float(), va.float(), rtol=2e-2, atol=2e-3, msg=k)
+    assert a.steps == b.steps == len(sizes)
+    a.close()
+    b.close()
+
+
+class _BlockLogged(LockstepTrainer):
+    """Packed-row blocks in, the ids (dense[0]) of every step's piece out, a digest at the end."""
+
+    def __init__(self, **kw):
+        from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, WideDeepTrainer
+
+        super().__init__(WideDeepTrainer(WideDeepConfig.tiny(), device="cpu", seed=3), BATCH, **kw)
+
+    def on_step(self, plan, piece, loss, out, counts=None):
+        from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, unpack_click_rows
+
+        ids = []
+        for blk in piece:
+            ids += [int(v) for v in unpack_click_rows(blk, WideDeepConfig.tiny())[1][:, 0].tolist()]
+        out.collect(("piece", self.steps, self.rank, ids, counts))
+
+    def on_finished(self, out):
+        out.collect(("digest", self.rank, self.steps, _digest(self.model.model, self.model._exchange)))
+
+
+def test_packed_blocks_k_steps_per_round_p3_match_reference():
+    """The bench job's shape on the CPU: P = 3 generator sources chained into their
+    trainers hand over packed-row BLOCKS (uneven: 7, 3 and 0 micro-batches' worth plus
+    remainders; block cuts fall inside micro-batches), rounds carry up to 4 full batches
+    each (``steps_per_round=2``), rank 2 only heartbeats — all three replicas end
+    bit-identical to the 1-rank reference trained on the same pieces in the same order."""
+    import numpy as np
+
+    from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, pack_click_records
+    from flink_tensorflow_amd.parallel.fake import FakeCommunicator
+
+    P = 3
+    cfg = WideDeepConfig.tiny()
+    recs = [(r[0], np.concatenate([[float(r[4])], r[1][1:]]).astype(np.float32), r[2], r[3])
+            for r in _records(10 * BATCH + 29)]
+    per = {0: recs[:7 * BATCH + 20], 1: recs[7 * BATCH + 20:], 2: []}
+
+    def gen(idx, par, start):
+        rows = pack_click_records(per[idx], cfg, 3) if per[idx] else None
+        for b in range(0, len(per[idx]), 45):
+            yield np.ascontiguousarray(rows[b:b + 45])
+
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(P)
+    env.enable_job_communicator(True, communicator=FakeCommunicator)
+    sink = env.generate(gen).run_in_processes().process(_BlockLogged(max_delay_ms=15.0, steps_per_round=2,
+                                                                     max_steps_per_round=4)) \
+        .name("trainer").run_in_processes().collect_into()
+    env.execute("lockstep-blocks")
+    out = sink.results()
+    digests = [o for o in out if o[0] == "digest"]
+    assert sorted(d[1] for d in digests) == [0, 1, 2] and len({d[2:] for d in digests}) == 1
+    by_step: dict = {}
+    for _, step, rank, ids, counts in (o for o in out if o[0] == "piece"):
+        by_step.setdefault(step, {})[rank] = ids
+    assert sorted(by_step) == list(range(1, digests[0][2] + 1))
+    assert sorted(i for s in by_step.values() for ids in s.values() for i in ids) == list(range(len(recs)))
+    assert all(len(s.get(2, [])) == 0 for s in by_step.values())
     assert _reference_p(recs, by_step, P) == digests[0][3]

@@ -53,3 +53,82 @@ def test_bucket_overflow_is_reported_ws2():
         assert ov["demand"] > ov["capacity"] and len(ov["raised"]) == 2, ov
         # the restarted attempt replays with larger buckets (slack x 2^attempt)
         assert ov["restart_slack"] == 1.5 * 4, ov
+
+
+def _stub_comm():
+    """Two ranks as seen from rank 0, collectives no-ops (single-process unit tests of the
+    trainer's exchange bookkeeping)."""
+    import torch
+
+    from flink_tensorflow_amd.parallel.comm import Communicator
+
+    class _Stub(Communicator):
+        rank, size = 0, 2
+
+        def __init__(self):
+            self.device = torch.device("cpu")
+
+        def broadcast(self, t, root=0):
+            pass
+
+        def all_reduce(self, t, op="sum"):
+            pass
+
+        def all_gather(self, out, inp):
+            out.copy_(inp.repeat(self.size).view(out.shape))
+
+        def reduce_scatter(self, out, inp, op="sum"):
+            pass
+
+    return _Stub()
+
+
+def test_overflow_in_the_last_steps_is_raised_at_end_of_training():
+    """a bucket overflow in the final steps of a bounded stream (after
+    the last every-64-steps window check, with no checkpoint after it) must not end
+    silently — ``finish_training`` (the lockstep trainer's agreed end of input) and
+    ``close`` raise ``CapacityExceeded``."""
+    import pytest
+    import torch
+
+    from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, WideDeepTrainer
+    from flink_tensorflow_amd.parallel import comm
+    from flink_tensorflow_amd.parallel.sparse_exchange import BucketedOwnerExchange, CapacityExceeded
+
+    with comm.bound(_stub_comm()):
+        t = WideDeepTrainer(WideDeepConfig.tiny(), device="cpu", seed=0, fused=False)
+        t.open()
+        ex = BucketedOwnerExchange(comm.get(), slack=0.01)
+        t._exchange = ex
+        ids = torch.arange(0, 400, dtype=torch.int32)
+        ex._bucket(ids, 0, 1000)  # 200 ids per owner into buckets of 66 slots: dropped rows
+        assert int(ex.over) > 0
+        ex.step_done()  # a step that is not a window boundary: nothing checked yet
+        with pytest.raises(CapacityExceeded):
+            t.finish_training()
+        with pytest.raises(CapacityExceeded):
+            t.close()
+        assert t._model is None  # resources released all the same
+
+
+def test_bucketed_exchange_refused_in_a_job_without_restarts():
+    """the bucketed exchange recovers from overflow by a job restart with
+    doubled slack; a job operator without a restart strategy refuses it at open instead of
+    failing later, and the default exchange is the exact one."""
+    import pytest
+
+    from flink_tensorflow_amd import config as C
+    from flink_tensorflow_amd.models.zoo.wide_deep import WideDeepConfig, WideDeepTrainer
+    from flink_tensorflow_amd.parallel import comm
+
+    assert C.EngineConfig().wd_sparse_exchange == "owner"
+    with comm.bound(_stub_comm()), C.override(wd_sparse_exchange="bucketed"):
+        t = WideDeepTrainer(WideDeepConfig.tiny(), device="cpu", seed=0, fused=False)
+        t.restart_budget = 0
+        with pytest.raises(ValueError, match="restart"):
+            t.open()
+        t = WideDeepTrainer(WideDeepConfig.tiny(), device="cpu", seed=0, fused=False)
+        t.restart_budget = 2
+        t.open()
+        assert type(t._exchange).__name__ == "BucketedOwnerExchange"
+        t.close()
