@@ -150,7 +150,8 @@ def main():
                     help="also print, per timed batch, its lane and the GPU times of its first H2D piece, first "
                          "kernel and completion relative to the start of the timed window (diagnostics)")
     ap.add_argument("--job", action="store_true",
-                    help="JOB MODE (resnet50, widedeep): ONE DataStream job with --gpus worker-process subtasks, one GPU "
+                    help="JOB MODE (resnet50, inception_v3, bert_graph, widedeep): ONE DataStream job with --gpus "
+                         "worker-process subtasks, one GPU "
                          "each — a source chained into each subtask's worker, the ResNet-50 operator with "
                          "distributed_weights (rank 0 compiles, weights broadcast over the operator's RCCL "
                          "group) — timed on the operator (batching/timed.py).  Run as ONE process (not under "
@@ -454,42 +455,94 @@ def run_job(args):
         raise SystemExit(f"[bench] --job --gpus {args.gpus} but {sysfs_gpu_count()} GPU(s) visible")
     if args.model == "widedeep":
         return run_job_widedeep(args)
-    if args.model != "resnet50":
-        raise SystemExit("[bench] --job: resnet50 or widedeep")
+    if args.model not in ("resnet50", "inception_v3", "bert_graph"):
+        raise SystemExit("[bench] --job: resnet50, inception_v3, bert_graph or widedeep")
     from flink_tensorflow_amd.batching.timed import TimedWindow
-    from flink_tensorflow_amd.models.zoo.image_classifier import ResNet50Model
-    from flink_tensorflow_amd.models.zoo.resnet import resnet50_flops_per_image
     from flink_tensorflow_amd.runtime import StreamExecutionEnvironment
     from flink_tensorflow_amd.runtime.sources import DiscardingSink
 
-    class JobResNet50(TimedWindow, ResNet50Model):
-        pass
-
     B, W, K, P = args.batch, args.warmup, args.steps, args.gpus
-    HW = args.image_hw or 256
-    lanes = args.lanes or 2
     pool_n = args.pool
     out_dir = tempfile.mkdtemp(prefix="ftm-bench-job-")
     t0 = time.perf_counter()
+    seq = None
     try:
+        if args.model in ("resnet50", "inception_v3"):
+            from flink_tensorflow_amd.models.zoo.image_classifier import InceptionV3Model, ResNet50Model
+
+            inc = args.model == "inception_v3"
+            HW = args.image_hw or (299 if inc else 256)
+            lanes = args.lanes or (3 if inc else 2)
+            base = InceptionV3Model if inc else ResNet50Model
+
+            class JobModel(TimedWindow, base):
+                pass
+
+            extra = {}
+            if inc:  # one calibration set for every subtask: the same fp8 scales on every rank
+                extra["calibration_images"] = np.random.default_rng(1234).integers(0, 256, size=(64, HW, HW, 3),
+                                                                                   dtype=np.uint8)
+            model = JobModel(image_hw=(HW, HW), buckets=(B,), distributed_weights=True, lanes=lanes,
+                             depth=args.depth, lane_offset_us=args.lane_offset_us, **extra)
+
+            def records(idx, par, start):  # runs in the subtask's worker process
+                pool = np.random.default_rng(1234 + idx).integers(0, 256, size=(pool_n, HW, HW, 3), dtype=np.uint8)
+                for i in range(start, (W + K) * B):
+                    yield pool[i % pool_n]
+
+            if inc:
+                from flink_tensorflow_amd.models.zoo.inception_v3 import inception_v3_flops_per_image
+
+                metric, name, flops = METRIC_INCEPTION, "Inception-v3", inception_v3_flops_per_image(299)
+                dtype = "fp8 (e4m3 weights+activations, fp32 accumulate)"
+            else:
+                from flink_tensorflow_amd.models.zoo.resnet import resnet50_flops_per_image
+
+                metric, name, flops, dtype = METRIC, "ResNet-50 v1.5", resnet50_flops_per_image(224), "bf16"
+            data = f"synthetic decoded uint8 {HW}x{HW}x3 images generated in each worker, random-init weights"
+            input_hw = 299 if inc else 224
+        else:  # the BERT-base classifier as a TF SavedModel (modeling.py GraphDef, weights as variables)
+            from flink_tensorflow_amd.models.batched import SignatureBatchedModel
+            from flink_tensorflow_amd.models.zoo.bert import BertConfig
+            from flink_tensorflow_amd.models.zoo.bert_graph import export_bert_saved_model
+
+            class JobModel(TimedWindow, SignatureBatchedModel):
+                pass
+
+            cfg = BertConfig.base()
+            seq = args.seq_len
+            lanes = args.lanes or 3
+            sm = export_bert_saved_model(os.path.join(out_dir, "bert_savedmodel"), cfg, seq, seed=0,
+                                         mask_from_ids=True)
+            model = JobModel(sm, output_keys=["logits"], buckets=(B,), lanes=lanes, depth=args.depth,
+                             distributed_weights=True)
+            vocab = cfg.vocab_size
+
+            def records(idx, par, start):
+                rng = np.random.default_rng(1234 + idx)
+                pool = rng.integers(1000, vocab, size=(pool_n, seq), dtype=np.int32)
+                lens = rng.integers(seq // 2, seq + 1, size=pool_n)
+                for i, n in enumerate(lens):
+                    pool[i, n:] = 0
+                pool[:, 0] = 101
+                for i in range(start, (W + K) * B):
+                    yield pool[i % pool_n]
+
+            metric, name, flops, dtype = METRIC_BERT, "BERT-base (seq classification), TF SavedModel", None, "bf16"
+            data = (f"synthetic token ids generated in each worker, seq {seq} (real lengths U[{seq // 2},{seq}]), "
+                    "random-init weights, padding-free (token-packed) compiled plans")
+            input_hw = None
+        model.timed_window(W, K, os.path.join(out_dir, "ranks"))
         env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(P)
         env.enable_job_communicator(True)  # one RCCL group for the operator, P = 1 included
-
-        def images(idx, par, start):  # runs in the subtask's worker process
-            pool = np.random.default_rng(1234 + idx).integers(0, 256, size=(pool_n, HW, HW, 3), dtype=np.uint8)
-            for i in range(start, (W + K) * B):
-                yield pool[i % pool_n]
-
-        model = JobResNet50(image_hw=(HW, HW), buckets=(B,), distributed_weights=True, lanes=lanes,
-                            depth=args.depth, lane_offset_us=args.lane_offset_us).timed_window(W, K, out_dir)
-        src = env.generate(images).run_in_processes()
-        src.map_with_model_batched(model, None, max_batch=B, max_delay_ms=60_000.0, name="resnet50") \
+        src = env.generate(records).run_in_processes()
+        src.map_with_model_batched(model, None, max_batch=B, max_delay_ms=60_000.0, name=args.model) \
             .run_in_processes().add_sink(DiscardingSink()).run_in_processes()  # results stay in the worker
         res = env.execute("bench-job")
         wall = time.perf_counter() - t0
         ranks = []
         for r in range(P):
-            with open(os.path.join(out_dir, f"rank{r}.json")) as f:
+            with open(os.path.join(out_dir, "ranks", f"rank{r}.json")) as f:
                 ranks.append(json.load(f))
     finally:
         shutil.rmtree(out_dir, ignore_errors=True)
@@ -498,20 +551,19 @@ def run_job(args):
     lat = np.concatenate([np.asarray(r["latencies_s"]) for r in ranks]) if ranks else np.zeros(1)
     total = n_rec / elapsed
     print(json.dumps({
-        "metric": METRIC, "value": round(total, 1), "unit": "records/s", "n_gpus": P, "steps": K, "warmup": W,
+        "metric": metric, "value": round(total, 1), "unit": "records/s", "n_gpus": P, "steps": K, "warmup": W,
         "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "bf16",
-        "data": f"synthetic decoded uint8 {HW}x{HW}x3 images generated in each worker, random-init weights",
-        "config": {"model": "ResNet-50 v1.5", "global_batch": B * P, "seq_len": None, "parallelism": f"dp{P}",
-                   "micro_batch_per_gpu": B, "input_hw": 224, "batch_buckets": [B], "compute_lanes": lanes,
-                   "lane_offset_us": args.lane_offset_us,
+        "vs_baseline": None, "dtype": dtype, "data": data,
+        "config": {"model": name, "global_batch": B * P, "seq_len": seq, "parallelism": f"dp{P}",
+                   "micro_batch_per_gpu": B, "input_hw": input_hw, "batch_buckets": [B], "compute_lanes": lanes,
+                   "lane_offset_us": args.lane_offset_us if seq is None else None,
                    "mode": "job: one DataStream job, P worker-process GPU subtasks, chained sources, "
                            "distributed_weights over the operator's communicator"},
         "p50_latency_ms": round(float(np.percentile(lat, 50)) * 1e3, 3) if lat.size else None,
         "p99_latency_ms": round(float(np.percentile(lat, 99)) * 1e3, 3) if lat.size else None,
         "per_rank_records_per_s": [round(r["records"] / r["elapsed_s"], 1) for r in ranks],
         "communicator": ranks[0]["communicator"], "comm_world_size": ranks[0]["world"],
-        "model_tflops_per_s": round(resnet50_flops_per_image(224) * total / 1e12, 1),
+        "model_tflops_per_s": round(flops * total / 1e12, 1) if flops else None,
         "job_wall_s": round(wall, 2), "job_attempts": res.attempts}), flush=True)
 
 

@@ -109,6 +109,8 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
     # ------------------------------------------------------------------ batched GPU API
     @staticmethod
     def _as_array(r) -> np.ndarray:
+        if isinstance(r, tuple) and len(r) == 2 and isinstance(r[0], str):
+            r = r[1]  # an ``ImageInputFormat`` record: (file name, decoded image)
         if isinstance(r, TensorValue):
             r = r.to_numpy()
         elif isinstance(r, torch.Tensor):

@@ -562,8 +562,8 @@ def pack_click_records(records, cfg: WideDeepConfig, n_cross: int = 8) -> np.nda
     """``(label, dense, cats, cross)`` tuples -> uint8 rows ``[n, row_bytes]``."""
     lay = click_record_layout(cfg, n_cross)
     arr = np.zeros(len(records), lay)
-    for i, (lab, dense, cats, cross) in enumerate(records):
-        arr[i] = (lab, dense, cats, cross)
+    for i, r in enumerate(records):  # (label, dense, cats, cross[, anything else])
+        arr[i] = tuple(r[:4])
     return arr.view(np.uint8).reshape(len(records), lay.itemsize)
 
 

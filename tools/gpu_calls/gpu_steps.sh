@@ -10,6 +10,7 @@ export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {
   local name=$1 t=$2; shift 2
   local t0=$(date +%s)
+  mkdir -p "$(dirname "$OUT/$name.log")"
   timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "[step] $name rc=$rc $(( $(date +%s) - t0 ))s"
