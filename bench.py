@@ -487,8 +487,8 @@ def run_job(args):
 
             def records(idx, par, start):  # runs in the subtask's worker process
                 pool = np.random.default_rng(1234 + idx).integers(0, 256, size=(pool_n, HW, HW, 3), dtype=np.uint8)
-                for i in range(start, (W + K) * B):
-                    yield pool[i % pool_n]
+                for i in range(start, (W + K) * B, 64):  # bulk: runs of 64 records per hand-over
+                    yield [pool[(i + k) % pool_n] for k in range(min(64, (W + K) * B - i))]
 
             if inc:
                 from flink_tensorflow_amd.models.zoo.inception_v3 import inception_v3_flops_per_image
@@ -515,7 +515,7 @@ def run_job(args):
             sm = export_bert_saved_model(os.path.join(out_dir, "bert_savedmodel"), cfg, seq, seed=0,
                                          mask_from_ids=True)
             model = JobModel(sm, output_keys=["logits"], buckets=(B,), lanes=lanes, depth=args.depth,
-                             distributed_weights=True)
+                             distributed_weights=True, lane_offset_us=args.lane_offset_us)
             vocab = cfg.vocab_size
 
             def records(idx, par, start):
@@ -525,8 +525,8 @@ def run_job(args):
                 for i, n in enumerate(lens):
                     pool[i, n:] = 0
                 pool[:, 0] = 101
-                for i in range(start, (W + K) * B):
-                    yield pool[i % pool_n]
+                for i in range(start, (W + K) * B, 64):
+                    yield [pool[(i + k) % pool_n] for k in range(min(64, (W + K) * B - i))]
 
             metric, name, flops, dtype = METRIC_BERT, "BERT-base (seq classification), TF SavedModel", None, "bf16"
             data = (f"synthetic token ids generated in each worker, seq {seq} (real lengths U[{seq // 2},{seq}]), "
@@ -535,7 +535,7 @@ def run_job(args):
         model.timed_window(W, K, os.path.join(out_dir, "ranks"))
         env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(P)
         env.enable_job_communicator(True)  # one RCCL group for the operator, P = 1 included
-        src = env.generate(records).run_in_processes()
+        src = env.generate(records, bulk=True).run_in_processes()
         src.map_with_model_batched(model, None, max_batch=B, max_delay_ms=60_000.0, name=args.model) \
             .run_in_processes().add_sink(DiscardingSink()).run_in_processes()  # results stay in the worker
         res = env.execute("bench-job")
@@ -556,7 +556,7 @@ def run_job(args):
         "vs_baseline": None, "dtype": dtype, "data": data,
         "config": {"model": name, "global_batch": B * P, "seq_len": seq, "parallelism": f"dp{P}",
                    "micro_batch_per_gpu": B, "input_hw": input_hw, "batch_buckets": [B], "compute_lanes": lanes,
-                   "lane_offset_us": args.lane_offset_us if seq is None else None,
+                   "lane_offset_us": args.lane_offset_us,
                    "mode": "job: one DataStream job, P worker-process GPU subtasks, chained sources, "
                            "distributed_weights over the operator's communicator"},
         "p50_latency_ms": round(float(np.percentile(lat, 50)) * 1e3, 3) if lat.size else None,

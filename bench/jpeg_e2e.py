@@ -63,6 +63,11 @@ def main():
     ap.add_argument("--lanes", type=int, default=2)
     ap.add_argument("--gpu-rate", type=float, default=77500.0, help="GPU-bound records/s (SPMD bench)")
     ap.add_argument("--max-delay-ms", type=float, default=20.0)
+    ap.add_argument("--decode", default="staged", choices=["staged", "reader"],
+                    help="staged: the reader emits the JPEG bytes and the model's host stage decodes them with the "
+                         "native pool into the pinned slot (reader chained into the model worker); reader: Pillow "
+                         "decode in --readers reader processes (the reference's placement)")
+    ap.add_argument("--decode-threads", type=int, default=16)
     a = ap.parse_args()
 
     from flink_tensorflow_amd.batching.timed import TimedWindow
@@ -80,7 +85,7 @@ def main():
         t0 = time.perf_counter()
         mean_bytes = make_jpegs(d, a.files, a.hw)
         gen_s = time.perf_counter() - t0
-        # single-thread decode cost of the format's read_record
+        # single-thread decode cost of the format's read_record (Pillow)
         fmt = ImageInputFormat()
         files = sorted(os.listdir(d))[:400]
         datas = [open(os.path.join(d, f), "rb").read() for f in files]
@@ -95,7 +100,13 @@ def main():
         model = TimedResNet(image_hw=(a.hw, a.hw), buckets=(B,), lanes=a.lanes, depth=3,
                             lane_offset_us=1500.0).timed_window(a.warmup, K, out_dir)
         env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(1)
-        readers = env.read_file(ImageInputFormat(), d, PROCESS_ONCE, parallelism=a.readers).run_in_processes()
+        staged = a.decode == "staged"
+        model.decode_threads = a.decode_threads
+        fmt_job = ImageInputFormat(defer_decode=staged)
+        if staged:  # one reader, chained into the model's worker process: only paths cross
+            readers = env.read_file(fmt_job, d, PROCESS_ONCE, parallelism=1)
+        else:
+            readers = env.read_file(fmt_job, d, PROCESS_ONCE, parallelism=a.readers).run_in_processes()
         readers.map_with_model_batched(model, None, max_batch=B, max_delay_ms=a.max_delay_ms, name="resnet50",
                                        parallelism=1).run_in_processes() \
             .add_sink(DiscardingSink()).run_in_processes()
@@ -108,11 +119,13 @@ def main():
         lat = np.asarray(r0["latencies_s"])
         print(json.dumps({
             "bench": "jpeg_e2e", "files": a.files, "hw": a.hw, "mean_jpeg_bytes": round(mean_bytes),
-            "readers": a.readers, "reader_processes": True, "gpus": 1, "model": "ResNet-50 v1.5 (bf16, compiled plan)",
+            "decode": ("native baseline decoder on the model's host pool, into the pinned slot "
+                       f"({a.decode_threads} threads)" if staged else f"Pillow in {a.readers} reader processes"),
+            "readers": 1 if staged else a.readers, "gpus": 1, "model": "ResNet-50 v1.5 (bf16, compiled plan)",
             "records_per_s": round(rate, 1), "job_records_per_s": round(a.files / wall, 1),
             "job_wall_s": round(wall, 2), "timed_batches": K, "timed_records": r0["records"],
             "decode_ms_per_record_1thread": round(decode_ms, 3),
-            "decode_bound_records_per_s": round(a.readers * 1e3 / decode_ms, 1),
+            "pillow_decode_bound_records_per_s": round(a.readers * 1e3 / decode_ms, 1),
             "gpu_rate_records_per_s": a.gpu_rate, "gpu_idle_share": round(max(0.0, 1 - rate / a.gpu_rate), 3),
             "p50_latency_ms": round(float(np.percentile(lat, 50)) * 1e3, 2) if lat.size else None,
             "allowed_cpus": len(os.sched_getaffinity(0)), "generate_s": round(gen_s, 1),

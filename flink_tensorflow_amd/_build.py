@@ -79,7 +79,7 @@ def hip_lib_path() -> Path:
 def build_native(force: bool = False, verbose: bool = False) -> Path:
     srcs = sorted(CSRC.glob("*.cpp"))
     hdrs = sorted(CSRC.glob("*.h"))
-    flags = ["-O3", "-std=c++17", "-shared", "-fPIC", "-msse4.2", "-pthread", "-fvisibility=hidden"]
+    flags = ["-O3", "-std=c++17", "-shared", "-fPIC", "-msse4.2", "-mavx2", "-mfma", "-pthread", "-fvisibility=hidden"]
     extra = os.environ.get("FTM_NATIVE_CFLAGS", "").split()  # e.g. sanitizer builds
     lib = native_lib_path()
     dig = _digest(srcs + hdrs, flags + extra)

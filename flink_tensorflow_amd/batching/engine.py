@@ -82,7 +82,7 @@ class PipelinedGpuRunner:
     def __init__(self, plans, feed: str, fetch_bufs: Callable[[Any], Sequence[torch.Tensor]],
                  record_shape, record_dtype=torch.uint8, depth: int = 3, device=None, gather_threads: int = 8,
                  stage_chunk: int = 64, lane_offset_us: float = 0.0, freeze_gc: bool = True, timeline: bool = False,
-                 interleave_head: bool = True):
+                 interleave_head: bool = True, decode_threads: int = 16):
         lanes = plans if isinstance(plans, (list, tuple)) else [plans]
         self.lanes = [dict(sorted(p.items())) for p in lanes]
         self.plans = self.lanes[0]
@@ -102,6 +102,10 @@ class PipelinedGpuRunner:
         self.compute_streams = [dedicated_stream(self.device, owner=self) for _ in self.lanes]
         self.compute_stream = self.compute_streams[0]
         self.gather_threads = gather_threads
+        # records that arrive as compressed JPEG bytes (``ImageInputFormat(defer_decode=True)``)
+        # are decoded by the native pool straight into the pinned rows (csrc/jpeg.cpp)
+        self.decode_threads = decode_threads
+        self.decode_fallbacks = 0
         self.stage_chunk = stage_chunk  # records per gather + H2D piece (0: whole batch at once)
         self.interleave_head = interleave_head  # launch each piece's head kernel inside the gather loop
         self._native = _ext.native()
@@ -183,9 +187,14 @@ class PipelinedGpuRunner:
                       and plan.head_pieces_ok(self.feed, slot.dev_in))
         if interleave:
             self._begin_lane(slot, lane, stream)
+        jpeg = isinstance(payloads[0], (bytes, bytearray, memoryview)) and len(self.record_shape) == 3 \
+            and self.record_shape[2] == 3 and self.record_dtype == torch.uint8
         with trace_range(f"gather[{n}/{b}]"):
             for i, (lo, hi) in enumerate(pieces):
-                self._native.gather_into(base + lo * rb, cap - lo * rb, payloads[lo:hi], rb, self.gather_threads)
+                if jpeg:
+                    self._decode_into(slot, base, cap, lo, payloads[lo:hi])
+                else:
+                    self._native.gather_into(base + lo * rb, cap - lo * rb, payloads[lo:hi], rb, self.gather_threads)
                 if n < b and hi == n:  # the padding rows of a short batch travel with the last piece
                     slot.pinned_in[n:].zero_()
                     hi = b
@@ -242,6 +251,17 @@ class PipelinedGpuRunner:
         hs["launch"] += t4 - t3
         self.batches += 1
         return finished
+
+    def _decode_into(self, slot: _Slot, base: int, cap: int, lo: int, blobs: list) -> None:
+        """JPEG byte strings -> RGB rows ``lo ..`` of the pinned slot: the native baseline
+        decoder on the host pool, GIL released; what it does not take (progressive, another
+        size, not a JPEG) goes through Pillow, resized to the record shape."""
+        from ..graph.ops_io import decode_jpegs_into
+
+        H, W, _ = self.record_shape
+        rb = self.record_bytes
+        self.decode_fallbacks += decode_jpegs_into(base + lo * rb, cap - lo * rb, blobs, rb, H, W,
+                                                   self.decode_threads, rows=slot.pinned_in[lo:])
 
     def _begin_lane(self, slot: _Slot, lane: int, stream) -> None:
         """The lane's stream work that precedes a batch: the phase delay of a restarting
@@ -336,6 +356,19 @@ class MicroBatcher:
         if len(self.items) >= self.max_batch:
             return self.flush()
         return None
+
+    def add_many(self, items: list, ts: float) -> list:
+        """``add`` for a run of items arriving together: the full batches it completes."""
+        out = []
+        i = 0
+        while i < len(items):
+            k = min(len(items) - i, self.max_batch - len(self.items))
+            self.items.extend(items[i:i + k])
+            self.ts.extend([ts] * k)
+            i += k
+            if len(self.items) >= self.max_batch:
+                out.append(self.flush())
+        return out
 
     def due(self, now: float | None = None) -> bool:
         if not self.items:

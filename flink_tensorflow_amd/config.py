@@ -44,6 +44,7 @@ class EngineConfig:
     fuse_preprocess_stem: bool = True  # resize-free preprocess folded into the s2d RGB stem conv
     fuse_block_tails: bool = True      # ResNet block boundary: expand + next reduce in one kernel
     decimate_tails: bool = True        # stage-1 tail output stored at the stride-2 reader's pixels
+    recompute_tails: bool = True       # stage-1 residual stream recomputed from 64-ch sources, not re-read
     pw_res_kernel: bool = True         # identity-residual expand convs on the persistent kernel
     conv3x3c64_kernel: bool = True     # 64-channel 3x3 convs with the filter bank in LDS
     # cache-resident batch slices: the plan's leading run of large-activation layers (every

@@ -1067,6 +1067,8 @@ void gather_into(uintptr_t dst, size_t dst_bytes, const py::list& srcs, size_t s
 
 }  // namespace
 
+void pool_run(int n, int threads, const std::function<void(int)>& fn) { CopyPool::get().run(n, threads, fn); }
+
 PYBIND11_MODULE(_native, m) {
   m.doc() = "flink_tensorflow_amd host runtime: wire codecs, protobuf, Example, bundle I/O";
   m.def("crc32c", [](const py::buffer& b, uint32_t init) {
@@ -1101,6 +1103,7 @@ PYBIND11_MODULE(_native, m) {
         py::arg("nthreads") = 4);
   register_arena(m);
   register_shm_ring(m);
+  register_jpeg(m);
   m.attr("has_sse42") =
 #if defined(__SSE4_2__)
       true;

@@ -119,6 +119,50 @@ def decode_image_bytes(data: bytes, channels: int = 3) -> np.ndarray:
     return arr
 
 
+def fit_image_bytes(data: bytes, h: int, w: int) -> np.ndarray:
+    """Pillow decode to RGB ``[h, w, 3]`` (bilinear resize when the file has another size):
+    the fallback for what the native baseline decoder declines (progressive, PNG, ...)."""
+    from PIL import Image
+
+    img = Image.open(_io.BytesIO(data)).convert("RGB")
+    if img.size != (w, h):
+        img = img.resize((w, h), Image.BILINEAR)
+    return np.asarray(img, dtype=np.uint8)
+
+
+def decode_jpegs_into(ptr: int, nbytes: int, blobs: list, stride: int, h: int, w: int, threads: int = 8,
+                      rows=None) -> int:
+    """Decode ``blobs`` (JPEG byte strings) into consecutive ``stride``-byte rows at host
+    address ``ptr`` as RGB ``[h, w, 3]`` uint8: the native baseline decoder on the host
+    pool (``csrc/jpeg.cpp``, GIL released); every image it reports as not taken goes through
+    :func:`fit_image_bytes`.  ``rows`` (indexable ``[n] -> writable [h, w, 3]``) receives the
+    fallbacks; when None a numpy view over ``ptr`` is used.  Returns the fallback count."""
+    from .. import _ext
+
+    st = _ext.native().jpeg_decode_into(ptr, nbytes, blobs, stride, h, w, threads)
+    bad = [k for k, code in enumerate(st) if code]
+    if bad and rows is None:
+        import ctypes
+
+        buf = (ctypes.c_uint8 * (len(blobs) * stride)).from_address(ptr)
+        rows = np.frombuffer(buf, np.uint8).reshape(len(blobs), stride)[:, : h * w * 3].reshape(-1, h, w, 3)
+    for k in bad:
+        img = fit_image_bytes(bytes(blobs[k]), h, w)
+        if isinstance(rows, np.ndarray):
+            rows[k] = img
+        else:
+            rows[k].copy_(__import__("torch").from_numpy(img))
+    return len(bad)
+
+
+def decode_jpegs(blobs: list, h: int, w: int, threads: int = 8) -> np.ndarray:
+    """``[n, h, w, 3]`` uint8 from JPEG byte strings (see :func:`decode_jpegs_into`)."""
+    out = np.empty((len(blobs), h, w, 3), np.uint8)
+    if len(blobs):
+        decode_jpegs_into(out.ctypes.data, out.nbytes, list(blobs), h * w * 3, h, w, threads, rows=out)
+    return out
+
+
 @register("DecodeJpeg", "DecodePng", "DecodeImage", "DecodeBmp")
 def _decode_jpeg(ctx, node, contents):
     ch = node.attr("channels", 0) or 3

@@ -19,6 +19,7 @@ void register_dconv(pybind11::module_& m);
 void register_elementwise(pybind11::module_& m);
 void register_conv3x3c64(pybind11::module_& m);
 void register_bottleneck(pybind11::module_& m);
+void register_bottleneck_chain(pybind11::module_& m);
 void register_gemm_pp(pybind11::module_& m);
 void register_conv_pp(pybind11::module_& m);
 void register_widedeep(pybind11::module_& m);
@@ -39,6 +40,7 @@ PYBIND11_MODULE(_hip, m) {
   register_elementwise(m);
   register_conv3x3c64(m);
   register_bottleneck(m);
+  register_bottleneck_chain(m);
   register_gemm_pp(m);
   register_conv_pp(m);
   register_widedeep(m);

@@ -43,8 +43,10 @@ class SignatureBatchedModel(SavedModel_, BatchedGpuModel):
                  input_key: str | None = None, output_keys: Sequence[str] | None = None,
                  record_shape: Sequence[int] | None = None, buckets: Sequence[int] = (64, 256), lanes: int = 2,
                  depth: int = 3, precision: str = "bf16", tags: Sequence[str] = (TAG_SERVE,), device=None,
-                 distributed_weights: bool = False, pack_tokens: bool | None = None):
+                 distributed_weights: bool = False, pack_tokens: bool | None = None, lane_offset_us: float = 0.0):
         super().__init__(path, tags, device, distributed_weights)
+        # staggered start of the compute lanes (batching/engine.py ``lane_offset_us``)
+        self.lane_offset_us = float(lane_offset_us)
         # token-id signatures (BERT-style, mask computed from the ids): padding-free plans
         # (graph/packed.py).  None = whenever the graph allows it, False = padded plans
         self.pack_tokens = pack_tokens
@@ -119,7 +121,8 @@ class SignatureBatchedModel(SavedModel_, BatchedGpuModel):
         if glue:
             LOG.info("signature %s: ops run as PyTorch glue in the compiled plans: %s", self.signature, glue)
         self._runner = PipelinedGpuRunner(lanes, self._feed, lambda p: p.output_tensors(), self._shape,
-                                          self._dtype.torch, depth=self.depth, device=dev)
+                                          self._dtype.torch, depth=self.depth, device=dev,
+                                          lane_offset_us=getattr(self, "lane_offset_us", 0.0))
         self._version = getattr(sess.variables, "version", 0)
 
     def close(self) -> None:

@@ -86,7 +86,8 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
                 comm.broadcast_tensors([t for ln in lanes for p in ln.values() for t in p.params], src=0)
             self._runner = PipelinedGpuRunner(lanes, self.feed, lambda p: p.output_tensors(), (H, W, 3),
                                               torch.uint8, depth=self.depth, device=dev,
-                                              lane_offset_us=getattr(self, "lane_offset_us", 0.0))
+                                              lane_offset_us=getattr(self, "lane_offset_us", 0.0),
+                                              decode_threads=getattr(self, "decode_threads", 16))
 
     def _calibration(self, b: int):
         if self.precision != "fp8" or self.calibration_images is None:
@@ -110,7 +111,9 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
     @staticmethod
     def _as_array(r) -> np.ndarray:
         if isinstance(r, tuple) and len(r) == 2 and isinstance(r[0], str):
-            r = r[1]  # an ``ImageInputFormat`` record: (file name, decoded image)
+            r = r[1]  # an ``ImageInputFormat`` record: (file name, decoded image or JPEG bytes)
+        if isinstance(r, (bytes, bytearray)):
+            return r  # compressed: decoded by the runner straight into the staging slot
         if isinstance(r, TensorValue):
             r = r.to_numpy()
         elif isinstance(r, torch.Tensor):
@@ -151,7 +154,15 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
     def label(self, images) -> list[list[tuple[float, str]]]:
         """Top-k ``(probability, label)`` per image (``InceptionModel.label`` +
         ``toTextLabels``)."""
-        arrs = np.stack([self._as_array(r) for r in images])
+        arrs = [self._as_array(r) for r in images]
+        if any(isinstance(a, (bytes, bytearray)) for a in arrs):
+            from ...graph.ops_io import decode_jpegs
+
+            H, W = self.image_hw
+            blobs = [a for a in arrs if isinstance(a, (bytes, bytearray))]
+            dec = iter(decode_jpegs(blobs, H, W, getattr(self, "decode_threads", 16)))
+            arrs = [next(dec) if isinstance(a, (bytes, bytearray)) else a for a in arrs]
+        arrs = np.stack(arrs)
         sess = self.session()
         if self._plans is not None:
             n = len(arrs)

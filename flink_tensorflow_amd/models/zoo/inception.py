@@ -176,11 +176,17 @@ class ImageInputFormat(WholeFileInputFormat):
     with ``normalize_on_host`` a float ``TensorValue`` [1,224,224,3] from
     ``ImageNormalization`` (the reference's behaviour)."""
 
-    def __init__(self, include=None, exclude=None, normalize_on_host: bool = False, resize_to=None):
+    def __init__(self, include=None, exclude=None, normalize_on_host: bool = False, resize_to=None,
+                 defer_decode: bool = False):
         super().__init__(include, exclude)
         self.configure(include=["*.jpg", "*.jpeg"], exclude=["*.crdownload"])
         self.normalize_on_host = normalize_on_host
         self.resize_to = resize_to
+        # defer_decode: records carry the compressed bytes; a GPU image model decodes them
+        # with the native pool straight into its staging slot (csrc/jpeg.cpp), so a ~20 KB
+        # record crosses the job instead of a 196 KB decoded image and no per-image Python
+        # decode runs in the reader
+        self.defer_decode = defer_decode
         self.model = ImageNormalization() if normalize_on_host else None
 
     def open_input_format(self):
@@ -196,6 +202,8 @@ class ImageInputFormat(WholeFileInputFormat):
             return None
         if self.normalize_on_host:
             return os.path.basename(path), TensorValue.from_tensor(self.model.normalize(data))
+        if self.defer_decode:
+            return os.path.basename(path), data
         from ...graph.ops_io import decode_image_bytes
 
         img = decode_image_bytes(data, 3)

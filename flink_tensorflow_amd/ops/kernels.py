@@ -284,6 +284,67 @@ def bottleneck_tail(x2: torch.Tensor, res: torch.Tensor | None, w3: torch.Tensor
     return y3, y1
 
 
+def bottleneck_chain(links, w1: torch.Tensor, b1: torch.Tensor, y1: torch.Tensor | None = None,
+                     y3: torch.Tensor | None = None, y3_decimated: bool = False, store_y3: bool = True):
+    """ResNet stage 1's residual stream recomputed instead of re-read (kernels/bottleneck_chain.hip):
+    ``links`` = [(c1, x0, w_a, b_a), (c2, None, w_b, b_b), ...] (1 to 3), ``y = relu([c1|x0] .
+    w_a^T + b_a)`` then ``y = relu(c_j . w_j^T + b_j + y)`` per further link — each link rounded
+    exactly as ``bottleneck_tail`` rounds it (acc + b -> bf16, + residual, relu -> bf16) — then
+    ``y1 = relu(y . w1^T + b1)``.  The last ``y`` is stored into ``y3`` only with
+    ``store_y3`` (``y3_decimated``: the even-(h, w) pixels, compact).  Returns ``(y3 or None, y1)``.
+    All sources [..., 64] of one pixel count; w_a [256, 128], the others [256, 64]; w1 [cn, 256]."""
+    x0 = links[0][0]
+    lead = x0.shape[:-1]
+    M = x0.numel() // 64
+    cn = w1.shape[0]
+    if not 1 <= len(links) <= 3 or links[0][1] is None or any(l[1] is not None for l in links[1:]):
+        raise ValueError("bottleneck_chain: 1 to 3 links, the first dual ([x | xs]), the others plain")
+    for j, (x, xs, w, b) in enumerate(links):
+        if x.shape[-1] != 64 or x.numel() != M * 64 or (xs is not None and tuple(xs.shape) != tuple(x.shape)):
+            raise ValueError("bottleneck_chain: every source is [..., 64] over the same pixels")
+        if tuple(w.reshape(w.shape[0], -1).shape) != (256, 128 if j == 0 else 64) or b.numel() != 256:
+            raise ValueError(f"bottleneck_chain: link {j} weights must be [256, {128 if j == 0 else 64}]")
+    if cn not in (64, 128) or tuple(w1.reshape(cn, -1).shape) != (cn, 256) or b1.numel() != cn:
+        raise ValueError("bottleneck_chain: w1 must be [64 or 128, 256]")
+    dec_hw = (0, 0)
+    if y3_decimated:
+        if x0.dim() != 4 or x0.shape[1] % 2 or x0.shape[2] % 2:
+            raise ValueError("bottleneck_chain: decimated y3 needs [N, H, W, 64] sources with even H, W")
+        dec_hw = (x0.shape[1], x0.shape[2])
+    odt = x0.dtype if x0.is_cuda else torch.float32
+    lead3 = (lead[0], dec_hw[0] // 2, dec_hw[1] // 2) if y3_decimated else lead
+    if store_y3 and y3 is None:
+        y3 = torch.empty((*lead3, 256), dtype=odt, device=x0.device)
+    y1 = torch.empty((*lead, cn), dtype=odt, device=x0.device) if y1 is None else y1
+    if (store_y3 and tuple(y3.shape) != (*lead3, 256)) or tuple(y1.shape) != (*lead, cn):
+        raise ValueError("bottleneck_chain: output buffers do not fit")
+    if x0.is_cuda:
+        for j, (x, xs, w, b) in enumerate(links):
+            for t, n in ((x, "x"), (w, "w")) + (((xs, "xs"),) if xs is not None else ()):
+                _check(t, f"link {j} {n}", device=x0.device)
+            _check(b, f"link {j} bias", torch.float32, x0.device)
+        _check(w1, "w1", device=x0.device)
+        _check(b1, "b1", torch.float32, x0.device)
+        _check(y1, "y1", device=x0.device)
+        if store_y3:
+            _check(y3, "y3", device=x0.device)
+        dev = x0.device.index if x0.device.index is not None else torch.cuda.current_device()
+        _hip().bottleneck_chain_bf16([(x.data_ptr(), _ptr(xs), w.data_ptr(), b.data_ptr()) for x, xs, w, b in links],
+                                     w1.data_ptr(), b1.data_ptr(), y3.data_ptr() if store_y3 else 0, y1.data_ptr(), M,
+                                     cn, _NUM_CU[dev], _stream(), dec_hw[0], dec_hw[1])
+        return (y3 if store_y3 else None), y1
+    y = None
+    rdt = y1.dtype  # each link's y3 rounded as the unfused tail's y3 buffer would hold it
+    for x, xs, w, b in links:
+        xin = torch.cat([x.reshape(M, 64), xs.reshape(M, 64)], 1) if xs is not None else x.reshape(M, 64)
+        a = (xin.float() @ w.reshape(256, -1).float().t() + b.float()).to(odt).float()
+        y = torch.relu(a if y is None else a + y).to(rdt).float()
+    if store_y3:
+        y3.copy_(y.reshape(*lead, 256)[:, ::2, ::2] if y3_decimated else y.reshape(y3.shape))
+    y1.copy_(torch.relu(y @ w1.reshape(cn, 256).float().t() + b1.float()).reshape(y1.shape).to(y1.dtype))
+    return (y3 if store_y3 else None), y1
+
+
 def gemm(x: torch.Tensor, w_nk: torch.Tensor, bias: torch.Tensor | None = None, residual: torch.Tensor | None = None,
          act=None, out: torch.Tensor | None = None, cfg: int = -1) -> torch.Tensor:
     """``act(x[M,K] @ w[N,K]^T + bias + residual)``; leading dims of x are flattened."""

@@ -226,7 +226,8 @@ class _Task:
                              self.job.config, self.job)
         ctx.global_index = self.job.rank * self.node.parallelism + self.subtask
         ctx.global_parallelism = self.job.world_size * self.node.parallelism
-        ctx.restart_attempts = self.job.env.restart_strategy.attempts
+        env = getattr(self.job, "env", None)
+        ctx.restart_attempts = env.restart_strategy.attempts if env is not None else 0
         return ctx
 
     def start(self):

@@ -216,6 +216,13 @@ class SourceContext:
     def collect(self, value, timestamp: float | None = None) -> None:
         raise NotImplementedError
 
+    def collect_many(self, values, timestamp: float | None = None) -> None:
+        """Emits ``values`` in order (one lock hold; a chained micro-batching consumer takes
+        them as one run — ``process_many`` — instead of one call chain per record)."""
+        with self.checkpoint_lock:
+            for v in values:
+                self.collect(v, timestamp)
+
     def emit_watermark(self, ts: float) -> None:
         raise NotImplementedError
 

@@ -131,6 +131,11 @@ class BatchedModelOperator(Operator):
         if b is not None:
             self._run(*b)
 
+    def process_many(self, values: list, ts=None):
+        """A run of records from a chained bulk source (``SourceContext.collect_many``)."""
+        for b in self.batcher.add_many([Record(v, ts) for v in values], time.perf_counter()):
+            self._run(*b)
+
     def _run(self, recs, ts):
         m = self.ctx.metrics
         if m is not None:

@@ -386,21 +386,31 @@ class _GroupBound:
     open, broadcasts, collective training steps, snapshots — see this operator's group,
     whichever thread makes the call (task loop, chain timer)."""
 
-    _CALLS = ("setup", "initialize", "open", "close", "process", "process_watermark", "on_idle", "next_deadline",
-              "end_input", "prepare_snapshot", "snapshot_state", "notify_checkpoint_complete")
+    _CALLS = ("setup", "initialize", "open", "close", "process", "process_many", "process_watermark", "on_idle",
+              "next_deadline", "end_input", "prepare_snapshot", "snapshot_state", "notify_checkpoint_complete")
 
     def __init__(self, op, group):
         self.__dict__["_op"], self.__dict__["_group"] = op, group
+        self.__dict__["_calls"] = {}
 
     def __getattr__(self, name):
         a = getattr(self._op, name)
         if name not in self._CALLS or self._group is None:
             return a
-        from ..parallel import comm
+        c = self._calls.get(name)
+        if c is not None and c[0] is a:
+            return c[1]
+        from ..parallel.comm import _BOUND
 
-        def call(*args, **kw):
-            with comm.bound(self._group):
+        group = self._group
+
+        def call(*args, **kw):  # the per-record path: a plain context-variable set / reset
+            tok = _BOUND.set(group)
+            try:
                 return a(*args, **kw)
+            finally:
+                _BOUND.reset(tok)
+        self._calls[name] = (a, call)
         return call
 
     def __setattr__(self, name, value):
@@ -438,7 +448,17 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
             if not parent_alive():
                 return  # coordinator gone
         if msg[0] == "init_chain":
-            _run_source_chain(msg, inp, out, emit, flush, parent_alive)
+            prof = os.environ.get("FTM_WORKER_PROFILE")  # diagnostics: cProfile of the chain's thread
+            if prof:
+                import cProfile
+
+                pr = cProfile.Profile()
+                try:
+                    pr.runcall(_run_source_chain, msg, inp, out, emit, flush, parent_alive)
+                finally:
+                    pr.dump_stats(f"{prof}.{os.getpid()}")
+            else:
+                _run_source_chain(msg, inp, out, emit, flush, parent_alive)
             op = None
             return
         kind, factory, spec, restore, restore_dir = msg
@@ -573,7 +593,7 @@ def _run_source_chain(msg, inp, out, emit, flush, parent_alive):
     def into(nxt):
         def e(elem):
             if type(elem) is Record:
-                nxt.process(elem, 0)
+                nxt.process(elem, 0)  # (_GroupBound caches the bound call: no per-record closure)
             elif isinstance(elem, Watermark):
                 nxt.process_watermark(elem, 0)
             else:
@@ -596,6 +616,7 @@ def _run_source_chain(msg, inp, out, emit, flush, parent_alive):
     for op in reversed(ops):
         op.open()
     head = into(ops[1]) if len(ops) > 1 else emit
+    bulk_head = getattr(ops[1], "process_many", None) if len(ops) > 1 else None
     src, fn = ops[0], ops[0].fn
     lock = threading.RLock()
     last = [time.perf_counter()]
@@ -646,6 +667,16 @@ def _run_source_chain(msg, inp, out, emit, flush, parent_alive):
                 poll()
                 head(Record(value, timestamp))
             recs_out[0] += 1
+
+        def collect_many(self, values, timestamp=None):
+            with lock:
+                poll()
+                if bulk_head is not None:  # a micro-batching first member takes the run at once
+                    bulk_head(values, timestamp)
+                else:
+                    for v in values:
+                        head(Record(v, timestamp))
+            recs_out[0] += len(values)
 
         def emit_watermark(self, ts):
             with lock:

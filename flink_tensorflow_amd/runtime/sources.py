@@ -86,10 +86,13 @@ class GeneratorSource(SourceFunction, CheckpointedFunction):
 
     relocatable = True
 
-    def __init__(self, factory: Callable[[int, int, int], Iterable], limit: int | None = None):
+    def __init__(self, factory: Callable[[int, int, int], Iterable], limit: int | None = None, bulk: bool = False):
         super().__init__()
         self.factory = factory
         self.limit = limit
+        # bulk: the factory yields LISTS of records, each emitted as one run
+        # (``SourceContext.collect_many``); offsets still count records
+        self.bulk = bulk
         self.offset = 0
         self._running = True
 
@@ -108,8 +111,14 @@ class GeneratorSource(SourceFunction, CheckpointedFunction):
             if not self._running or (self.limit is not None and self.offset >= self.limit):
                 break
             with ctx.checkpoint_lock:
-                ctx.collect(v)
-                self.offset += 1
+                if self.bulk:
+                    if self.limit is not None:
+                        v = v[:self.limit - self.offset]
+                    ctx.collect_many(v)
+                    self.offset += len(v)
+                else:
+                    ctx.collect(v)
+                    self.offset += 1
 
     def cancel(self):
         self._running = False

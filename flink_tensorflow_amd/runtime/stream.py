@@ -165,8 +165,10 @@ class StreamExecutionEnvironment:
         return self.from_collection(items)
 
     def generate(self, factory: Callable[[int, int, int], Iterable], limit: int | None = None,
-                 parallelism: int | None = None) -> "DataStream":
-        return self.add_source(GeneratorSource(factory, limit), "generator", parallelism)
+                 parallelism: int | None = None, bulk: bool = False) -> "DataStream":
+        """``factory(subtask, parallelism, start_record)`` yields the subtask's records — or,
+        with ``bulk``, lists of records, each handed to the chained consumer as one run."""
+        return self.add_source(GeneratorSource(factory, limit, bulk), "generator", parallelism)
 
     def read_file(self, fmt: WholeFileInputFormat, path: str, mode=PROCESS_ONCE, interval_s: float = 1.0,
                   parallelism: int | None = None, max_polls: int | None = None) -> "DataStream":

@@ -112,3 +112,76 @@ def test_decimated_tail_reference():
 @pytest.mark.gpu
 def test_decimated_tail_gpu():
     _decimated_case(torch.device("cuda", 0))
+
+
+def _chain_case(dev, M_hw=(2, 6, 10)):
+    """Three stage-1 tails unfused (``bottleneck_tail``: dual, then two identity-residual
+    ones reading the previous y3) against the recomputing chains (``bottleneck_chain``
+    with 1, 2 and 3 links): the same y1 of every tail and the same (decimated) last y3."""
+    g = torch.Generator().manual_seed(9)
+    N, H, W = M_hw
+
+    def bf(*shape, s=1.0):
+        return (torch.randn(*shape, generator=g) * s).bfloat16().float()
+
+    x0, c1, c2, c3 = (bf(N, H, W, 64) for _ in range(4))
+    wa, wb, wc = bf(256, 128, s=1 / 11), bf(256, 64, s=1 / 8), bf(256, 64, s=1 / 8)
+    ba, bb, bc = (torch.randn(256, generator=g) * 0.1 for _ in range(3))
+    w1a, w1b, w1c = bf(64, 256, s=1 / 16), bf(64, 256, s=1 / 16), bf(128, 256, s=1 / 16)
+    b1a, b1b, b1c = torch.randn(64, generator=g), torch.randn(64, generator=g), torch.randn(128, generator=g)
+    cast = (lambda t: t.to(dev, torch.bfloat16)) if dev.type == "cuda" else (lambda t: t)
+    fp = (lambda t: t.to(dev)) if dev.type == "cuda" else (lambda t: t)
+    # unfused: three tails, y3 round-tripping
+    y3a, y1a = K.bottleneck_tail(cast(c1), None, cast(wa), fp(ba), cast(w1a), fp(b1a), xs=cast(x0))
+    y3b, y1b = K.bottleneck_tail(cast(c2), y3a, cast(wb), fp(bb), cast(w1b), fp(b1b))
+    y3c, y1c = K.bottleneck_tail(cast(c3), y3b, cast(wc), fp(bc), cast(w1c), fp(b1c), y3_decimated=True)
+    la = (cast(c1), cast(x0), cast(wa), fp(ba))
+    lb = (cast(c2), None, cast(wb), fp(bb))
+    lc = (cast(c3), None, cast(wc), fp(bc))
+    n1, z1 = K.bottleneck_chain([la], cast(w1a), fp(b1a), store_y3=False)
+    n2, z2 = K.bottleneck_chain([la, lb], cast(w1b), fp(b1b), store_y3=False)
+    z3c, z3 = K.bottleneck_chain([la, lb, lc], cast(w1c), fp(b1c), y3_decimated=True)
+    assert n1 is None and n2 is None and tuple(z3c.shape) == (N, H // 2, W // 2, 256)
+    # the chain rounds every link exactly as the tails do: bit-identical
+    for a, b in ((z1, y1a), (z2, y1b), (z3, y1c), (z3c, y3c)):
+        assert torch.equal(a.float().cpu(), b.float().cpu())
+
+
+def test_chain_reference_equals_unfused_tails():
+    _chain_case(torch.device("cpu"))
+    with pytest.raises(ValueError):  # the first link must be the dual one
+        K.bottleneck_chain([(torch.zeros(2, 64), None, torch.zeros(256, 64), torch.zeros(256))], torch.zeros(64, 256),
+                           torch.zeros(64))
+
+
+@pytest.mark.gpu
+def test_chain_kernel_equals_unfused_tails_gpu():
+    _chain_case(torch.device("cuda", 0))
+    _chain_case(torch.device("cuda", 0), (3, 8, 14))  # a partial last tile
+
+
+def _compile_chain(g, dev, on):
+    from flink_tensorflow_amd.config import override
+
+    with override(recompute_tails=on):
+        return CompiledFunction(g, {"images:0": ((2, 64, 64, 3), "UINT8")}, ["logits:0"], dev, strict=True)
+
+
+def _check_chain(r50, dev):
+    on, off = _compile_chain(r50, dev, True), _compile_chain(r50, dev, False)
+    assert on.summary()["chained_tails"] == 2 and off.summary()["chained_tails"] == 0
+    assert on.summary()["fused_tails"] == off.summary()["fused_tails"] == 3
+    assert on.activation_bytes <= off.activation_bytes * 1.25
+    imgs = torch.randint(0, 256, (2, 64, 64, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(2))
+    a = on({"images:0": imgs.to(dev)})[0].float().cpu()
+    b = off({"images:0": imgs.to(dev)})[0].float().cpu()
+    assert torch.equal(a, b)  # the recomputed residual stream is bit-identical
+
+
+def test_compiled_resnet50_recomputes_the_stage1_residual_stream_cpu(r50):
+    _check_chain(r50, torch.device("cpu"))
+
+
+@pytest.mark.gpu
+def test_compiled_resnet50_recomputes_the_stage1_residual_stream_gpu(r50):
+    _check_chain(r50, torch.device("cuda", 0))

@@ -368,3 +368,21 @@ def test_key_by_and_fan_out_break_chains():
     ex.execute()
     assert ["id", "a"] not in ex.chains and all(c[0] != "id" for c in ex.chains)
     assert len(a.results()) == 100 and len(b.results()) == 100
+
+
+def test_bulk_generator_feeds_a_chained_micro_batcher_in_order():
+    """``env.generate(factory, bulk=True)``: the factory yields runs of records; a chained
+    micro-batching operator in the worker takes each run at once (``process_many``) and
+    forms the same batches, in the same order, as record-at-a-time emission; ``limit``
+    counts records, not runs."""
+    from flink_tensorflow_amd.runtime import StreamExecutionEnvironment
+
+    def gen(idx, par, start):
+        for i in range(start, 100, 7):
+            yield list(range(i, min(i + 7, 100)))
+
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(1)
+    out = env.generate(gen, bulk=True, limit=90).run_in_processes() \
+        .map_with_model_batched(object(), lambda m, recs: [r * 2 for r in recs], max_batch=16, max_delay_ms=50,
+                                name="x2").run_in_processes().execute_and_collect()
+    assert out == [2 * i for i in range(90)]
