@@ -17,8 +17,10 @@
 #include <atomic>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -520,9 +522,49 @@ std::vector<int> jpeg_decode_into(uintptr_t dst, size_t dst_bytes, const py::lis
   return status;
 }
 
+// Whole files -> bytes, read on the host pool with the GIL released (the file reader's
+// bulk path: one Python call per run of paths instead of an open/read per record).  A file
+// that cannot be read comes back as None.
+py::list read_files(const py::list& paths, int nthreads) {
+  const size_t n = paths.size();
+  std::vector<std::string> names(n);
+  for (size_t i = 0; i < n; ++i) names[i] = paths[i].cast<std::string>();
+  std::vector<std::string> data(n);
+  std::vector<char> ok(n, 0);
+  {
+    py::gil_scoped_release nogil;
+    pool_run(int(n), std::max(1, nthreads), [&](int i) {
+      FILE* f = std::fopen(names[i].c_str(), "rb");
+      if (!f) return;
+      std::string& d = data[i];
+      if (std::fseek(f, 0, SEEK_END) == 0) {
+        long len = std::ftell(f);
+        if (len >= 0 && std::fseek(f, 0, SEEK_SET) == 0) {
+          d.resize(size_t(len));
+          size_t got = len ? std::fread(&d[0], 1, size_t(len), f) : 0;
+          d.resize(got);
+          ok[i] = got == size_t(len);
+        }
+      }
+      std::fclose(f);
+    });
+  }
+  py::list out(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (ok[i]) {
+      out[i] = py::bytes(data[i]);
+    } else {
+      out[i] = py::none();
+    }
+  }
+  return out;
+}
+
 }  // namespace
 
 void register_jpeg(py::module_& m) {
+  m.def("read_files", &read_files, py::arg("paths"), py::arg("nthreads") = 8,
+        "Reads whole files on the host pool (GIL released); bytes per path, None for a file that cannot be read.");
   m.def("jpeg_decode_into", &jpeg_decode_into, py::arg("dst"), py::arg("dst_bytes"), py::arg("images"),
         py::arg("stride"), py::arg("h"), py::arg("w"), py::arg("nthreads") = 8,
         "Decodes baseline JPEG byte strings into rows of `stride` bytes at `dst` (H x W x 3 RGB); per-image status "

@@ -47,14 +47,26 @@ END = EndOfInput()
 class Output:
     """Operator output: main stream + side outputs."""
 
-    def __init__(self, emit: Callable[[Record], None], emit_side: Callable[[OutputTag, Any], None] | None = None):
+    def __init__(self, emit: Callable[[Record], None], emit_side: Callable[[OutputTag, Any], None] | None = None,
+                 emit_many: Callable[[list, Any], None] | None = None):
         self._emit = emit
         self._side = emit_side
+        self._many = emit_many
         self.count = 0
 
     def emit(self, value, ts=None):
         self.count += 1
         self._emit(Record(value, ts))
+
+    def emit_many(self, values: list, ts=None):
+        """A run of values with one timestamp: handed over in one call where the consumer
+        takes runs (a chained ``process_many``), else one ``emit`` each."""
+        if self._many is not None:
+            self.count += len(values)
+            self._many(values, ts)
+        else:
+            for v in values:
+                self.emit(v, ts)
 
     def emit_side(self, tag, value):
         if self._side is None:
@@ -108,6 +120,12 @@ class Operator:
     # data
     def process(self, rec: Record, input_index: int = 0):
         raise NotImplementedError
+
+    def process_batch(self, recs: list, input_index: int = 0):
+        """The records of one channel message, in order (operators that gain from a run —
+        the chained file reader — override this)."""
+        for r in recs:
+            self.process(r, input_index)
 
     def process_watermark(self, wm: Watermark, input_index: int = 0):
         self.current_watermark = max(self.current_watermark, wm.ts)
@@ -479,6 +497,31 @@ class FileReaderOperator(Operator):
         self.pending.append(rec.value)
         self._drain(rec.ts)
 
+    def process_batch(self, recs: list, input_index: int = 0):
+        """A message's run of paths: the local files are read on the native host pool in
+        one call (GIL released) and the records go on as one run (``Output.emit_many``:
+        one ``process_many`` of the chained model operator)."""
+        from ..utils import fs
+
+        self.pending.extend(r.value for r in recs)
+        paths = list(self.pending)
+        local = [fs.get_fs(p) for p in paths]
+        if not all(isinstance(f, fs.LocalFS) for f, _ in local):
+            return self._drain(recs[-1].ts if recs else None)
+        from .. import _ext
+
+        blobs = _ext.native().read_files([p for _, p in local], getattr(self, "read_threads", 8))
+        outs = []
+        for path, data in zip(paths, blobs):
+            if data is None:  # unreadable: the per-file path raises with the OS error
+                data = fs.read_bytes(path)
+            out = self.fmt.read_record(path, data)
+            if out is not None:
+                outs.append(out)
+        self.pending.clear()
+        if outs:
+            self.out.emit_many(outs, recs[-1].ts)
+
     def _drain(self, ts):
         from ..utils import fs
 
@@ -520,7 +563,8 @@ class ChainOperator(Operator):
                 else:
                     b.process(elem, 0)
 
-            a.setup(ctx, Output(fwd, out._side))
+            many = getattr(b, "process_many", None)  # e.g. the batched model operator
+            a.setup(ctx, Output(fwd, out._side, many))
         self.ops[-1].setup(ctx, out)
 
     def initialize(self, snapshot, checkpoint_dir):
@@ -538,6 +582,9 @@ class ChainOperator(Operator):
 
     def process(self, rec: Record, input_index: int = 0):
         self.ops[0].process(rec, input_index)
+
+    def process_batch(self, recs: list, input_index: int = 0):
+        self.ops[0].process_batch(recs, input_index)
 
     def process_watermark(self, wm: Watermark, input_index: int = 0):
         self.ops[0].process_watermark(wm, input_index)

@@ -386,7 +386,8 @@ class _GroupBound:
     open, broadcasts, collective training steps, snapshots — see this operator's group,
     whichever thread makes the call (task loop, chain timer)."""
 
-    _CALLS = ("setup", "initialize", "open", "close", "process", "process_many", "process_watermark", "on_idle",
+    _CALLS = ("setup", "initialize", "open", "close", "process", "process_batch", "process_many", "process_watermark",
+              "on_idle",
               "next_deadline", "end_input", "prepare_snapshot", "snapshot_state", "notify_checkpoint_complete")
 
     def __init__(self, op, group):
@@ -423,6 +424,7 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
     slab = TensorSlab(slab_name, create=False) if slab_name else None
     op = None
     group = None
+    profiler = None
     pending: list = []
     parent = os.getppid()
 
@@ -466,15 +468,12 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
         from .functions import RuntimeContext
         from ..utils.metrics import MetricGroup
 
-        device = None
-        if spec["gpu"]:
-            import torch
+        device = _worker_device(spec)
+        if os.environ.get("FTM_WORKER_PROFILE"):  # diagnostics: cProfile of the operator loop
+            import cProfile
 
-            if torch.cuda.is_available():
-                from ..parallel.comm import gpu_count
-
-                device = torch.device("cuda", spec["subtask"] % max(1, gpu_count()))
-                torch.cuda.set_device(device)
+            profiler = cProfile.Profile()
+            profiler.enable()
         metrics = MetricGroup(f"{spec['name']}[{spec['subtask']}]")
         ctx = RuntimeContext(spec["name"], spec["subtask"], spec["parallelism"], device, spec["attempt"], metrics,
                              spec["config"], None)
@@ -507,11 +506,17 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
                     refs = [v for v, _, _ in items if _is_ref(v)]
                     if refs:
                         arrs = iter(slab.view_batch(refs))
-                for value, ts, idx in items:
-                    if arrs is not None and _is_ref(value):
-                        a = next(arrs)
-                        value = a if value[6] == "np" else _from_slab(value, slab, a)
-                    op.process(Record(value, ts), idx)
+                batch_fn = getattr(op, "process_batch", None) if arrs is None and items else None
+                if batch_fn is not None and all(it[2] == items[0][2] for it in items):
+                    # a plain run from one input: one call (the chained file reader reads the
+                    # run's files in one native call and hands the model one run)
+                    batch_fn([Record(v, ts) for v, ts, _ in items], items[0][2])
+                else:
+                    for value, ts, idx in items:
+                        if arrs is not None and _is_ref(value):
+                            a = next(arrs)
+                            value = a if value[6] == "np" else _from_slab(value, slab, a)
+                        op.process(Record(value, ts), idx)
                 metrics.inc("records_in", len(items))
             elif kind == "wm":
                 op.process_watermark(Watermark(msg[1]))
@@ -551,6 +556,9 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
             except Exception:  # noqa: BLE001
                 pass
         _close_group(group, abort=True)
+        if profiler is not None:
+            profiler.disable()
+            profiler.dump_stats(f"{os.environ['FTM_WORKER_PROFILE']}.{os.getpid()}")
         out.close()
 
 
@@ -570,6 +578,12 @@ def _worker_device(spec):
 
     device = torch.device("cuda", spec["subtask"] % max(1, gpu_count()))
     torch.cuda.set_device(device)
+    if os.environ.get("FT_NUMA_BIND", "1") != "0":
+        from ..parallel.comm import bind_to_gpu_numa
+
+        # the subtask's host staging (gather / decode pools started after this) runs on its
+        # GPU's socket, as the SPMD ranks do (bench.py)
+        bind_to_gpu_numa(device)
     return device
 
 

@@ -129,3 +129,55 @@ def test_deferred_decode_job_matches_decoded_records(tmp_path):
         assert np.allclose([r[0][0] for r in ld], [r[0][0] for r in le], rtol=1e-5)
     finally:
         m.close()
+
+
+def test_chained_reader_bulk_run_matches_per_record(tmp_path):
+    """The chained file reader's bulk path (``process_batch``: the run's files read by the
+    native pool, one ``emit_many`` into the consumer's ``process_many``) yields the same
+    records, in order, as the per-record path; an unreadable file still raises."""
+    from flink_tensorflow_amd.models.zoo.inception import ImageInputFormat
+    from flink_tensorflow_amd.runtime.operators import ChainOperator, FileReaderOperator, Operator, Record
+
+    blobs = [_jpeg(_img(32, 32, s), quality=90) for s in range(7)]
+    paths = []
+    for i, b in enumerate(blobs):
+        p = tmp_path / f"f{i}.jpg"
+        p.write_bytes(b)
+        paths.append(str(p))
+
+    class Sink(Operator):
+        def __init__(self):
+            super().__init__(None, "sink")
+            self.got, self.runs = [], 0
+
+        def process(self, rec, input_index=0):
+            self.got.append(rec.value)
+
+        def process_many(self, values, ts=None):
+            self.runs += 1
+            self.got.extend(values)
+
+    def run(bulk):
+        sink = Sink()
+        chain = ChainOperator([FileReaderOperator(ImageInputFormat(defer_decode=True)), sink])
+        from flink_tensorflow_amd.runtime.operators import Output
+
+        chain.setup(None, Output(lambda r: None))
+        recs = [Record(p, 0.0) for p in paths]
+        if bulk:
+            chain.process_batch(recs, 0)
+        else:
+            for r in recs:
+                chain.process(r, 0)
+        return sink
+
+    a, b = run(False), run(True)
+    assert a.got == b.got and [n for n, _ in b.got] == [f"f{i}.jpg" for i in range(7)]
+    assert b.runs == 1 and a.runs == 0
+    assert [d for _, d in b.got] == blobs
+    sink_chain = ChainOperator([FileReaderOperator(ImageInputFormat(defer_decode=True)), Operator(None, "x")])
+    from flink_tensorflow_amd.runtime.operators import Output
+
+    sink_chain.setup(None, Output(lambda r: None))
+    with pytest.raises(FileNotFoundError):
+        sink_chain.process_batch([Record(str(tmp_path / "missing.jpg"), 0.0)], 0)
