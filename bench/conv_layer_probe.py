@@ -2,7 +2,7 @@
 incumbent implicit-GEMM conv (``igemm``) and the ping-pong conv (``pp``) on the stage 2/3/4
 3x3 layers at B=256, --reps launches each, plus a µs line per kernel on stdout.
 
-    python bench/conv_layer_probe.py --layers s3_3x3 --impls igemm,lite:2,lite:3 --reps 10
+    python bench/conv_layer_probe.py --layers s3_3x3 --impls igemm,lite:2,lite:4,lite:5,lite:6 --reps 10
 
 (``lite:4`` / ``5`` / ``6``: tile 2 without MFMAs / without DMA after the first K-tile /
 MFMAs only — a decomposition of where its time goes; outputs meaningless.)
@@ -54,7 +54,7 @@ def main():
             if impl == "igemm":
                 def fn():
                     K.conv2d_nhwc(x, w, b, res, (s, s), (pad, pad, pad, pad), (1, 1), K.ACT_RELU, out=y)
-            else:  # lite[:tile]: the 128x128 LDS-DMA tile (2 = 4 waves, 3 = 2 waves, 4..6 diagnostics)
+            else:  # lite[:tile]: the 128x128 LDS-DMA tile (2; 4..6 diagnostics)
                 tile = int(impl.split(":")[1]) if ":" in impl else None
                 cp = K.ConvPP([((B, H, W, Cin), (k, k), (s, s), (pad, pad), (1, 1))], Cout, (OH, OW), dev, tile=tile)
                 w2 = w.reshape(Cout, -1)

@@ -1,11 +1,17 @@
 #!/usr/bin/env python3
 """The reference's own workload end to end on the GPU: a directory of JPEG
-files -> ``env.read_file(ImageInputFormat)`` (one file monitor, R reader subtasks that read
-and DECODE in their own worker processes) -> the compiled ResNet-50 operator
+files -> ``env.read_file(ImageInputFormat)`` -> the compiled ResNet-50 operator
 (``map_with_model_batched``, one GPU subtask, the fused resize + normalise preprocess in the
 plan) -> discarding sink.  Reference pipeline: ``inception.scala:33-46``
 (``readFile(ImageInputFormat, dir, PROCESS_ONCE)`` -> ``mapWithModel``),
 ``ImageInputFormat.scala:63-80`` (decode per file), ``ImageNormalization.scala:42-77``.
+
+Decode placements (``--decode``): ``staged`` (default) — the reader emits the compressed
+bytes (``ImageInputFormat(defer_decode=True)``) and the model's host stage decodes them with
+the native baseline decoder on its thread pool straight into the pinned staging slot
+(``csrc/jpeg.cpp``); the reader runs in the model's worker, with the directory listing too
+under ``--monitor partitioned`` (``sources.PartitionedFileSource``).  ``reader`` — Pillow
+decode in R reader worker processes, the reference's placement (``ImageInputFormat.scala``).
 
 Reports, as one JSON line:
 * records/s of the timed window on the model operator (W + K micro-batches,
@@ -67,7 +73,10 @@ def main():
                     help="staged: the reader emits the JPEG bytes and the model's host stage decodes them with the "
                          "native pool into the pinned slot (reader chained into the model worker); reader: Pillow "
                          "decode in --readers reader processes (the reference's placement)")
-    ap.add_argument("--decode-threads", type=int, default=16)
+    ap.add_argument("--decode-threads", type=int, default=32)
+    ap.add_argument("--monitor", default="partitioned", choices=["partitioned", "coordinator"],
+                    help="partitioned: the listing + reading source runs inside the model's worker (nothing crosses "
+                         "the coordinator); coordinator: Flink's monitor in the coordinator forwarding paths")
     a = ap.parse_args()
 
     from flink_tensorflow_amd.batching.timed import TimedWindow
@@ -95,6 +104,25 @@ def main():
             fmt.read_record(f, b)
         decode_ms = (time.perf_counter() - t0) / len(files) * 1e3
 
+        # native decode capacity in this process: 256 images into one buffer, 1 thread and
+        # --decode-threads threads, in 64-image pieces as the runner stages them
+        from flink_tensorflow_amd import _ext
+
+        nat = _ext.native()
+        blobs = (datas * (256 // len(datas) + 1))[:256]
+        buf = np.empty((256, a.hw, a.hw, 3), np.uint8)
+        rb = a.hw * a.hw * 3
+        native_ms = {}
+        for th in (1, a.decode_threads):
+            nat.jpeg_decode_into(buf.ctypes.data, buf.nbytes, blobs[:64], rb, a.hw, a.hw, th)
+            t0 = time.perf_counter()
+            reps = 2 if th == 1 else 10
+            for _ in range(reps):
+                for lo in range(0, 256, 64):
+                    nat.jpeg_decode_into(buf.ctypes.data + lo * rb, buf.nbytes - lo * rb, blobs[lo:lo + 64], rb,
+                                         a.hw, a.hw, th)
+            native_ms[th] = (time.perf_counter() - t0) / reps * 1e3
+
         B = a.batch
         K = a.files // B - a.warmup - 1  # the last, partial batch is not timed
         model = TimedResNet(image_hw=(a.hw, a.hw), buckets=(B,), lanes=a.lanes, depth=3,
@@ -103,8 +131,8 @@ def main():
         staged = a.decode == "staged"
         model.decode_threads = a.decode_threads
         fmt_job = ImageInputFormat(defer_decode=staged)
-        if staged:  # one reader, chained into the model's worker process: only paths cross
-            readers = env.read_file(fmt_job, d, PROCESS_ONCE, parallelism=1)
+        if staged:  # one reader in the model's worker process (partitioned: the listing too)
+            readers = env.read_file(fmt_job, d, PROCESS_ONCE, parallelism=1, monitor=a.monitor)
         else:
             readers = env.read_file(fmt_job, d, PROCESS_ONCE, parallelism=a.readers).run_in_processes()
         readers.map_with_model_batched(model, None, max_batch=B, max_delay_ms=a.max_delay_ms, name="resnet50",
@@ -121,13 +149,17 @@ def main():
             "bench": "jpeg_e2e", "files": a.files, "hw": a.hw, "mean_jpeg_bytes": round(mean_bytes),
             "decode": ("native baseline decoder on the model's host pool, into the pinned slot "
                        f"({a.decode_threads} threads)" if staged else f"Pillow in {a.readers} reader processes"),
-            "readers": 1 if staged else a.readers, "gpus": 1, "model": "ResNet-50 v1.5 (bf16, compiled plan)",
+            "readers": 1 if staged else a.readers, "monitor": a.monitor if staged else "coordinator", "gpus": 1, "model": "ResNet-50 v1.5 (bf16, compiled plan)",
             "records_per_s": round(rate, 1), "job_records_per_s": round(a.files / wall, 1),
             "job_wall_s": round(wall, 2), "timed_batches": K, "timed_records": r0["records"],
             "decode_ms_per_record_1thread": round(decode_ms, 3),
+            "native_decode_ms_per_record_1thread": round(native_ms[1] / 256, 3),
+            f"native_decode_ms_per_256_batch_{a.decode_threads}threads": round(native_ms[a.decode_threads], 3),
             "pillow_decode_bound_records_per_s": round(a.readers * 1e3 / decode_ms, 1),
             "gpu_rate_records_per_s": a.gpu_rate, "gpu_idle_share": round(max(0.0, 1 - rate / a.gpu_rate), 3),
             "p50_latency_ms": round(float(np.percentile(lat, 50)) * 1e3, 2) if lat.size else None,
+            "host_ms_per_batch": r0.get("host_ms_per_batch"),
+            "batch_interval_ms": round(r0["elapsed_s"] / max(1, K) * 1e3, 3),
             "allowed_cpus": len(os.sched_getaffinity(0)), "generate_s": round(gen_s, 1),
             "attempts": res.attempts}), flush=True)
     finally:

@@ -55,6 +55,7 @@ class TimedWindow:
         if i == tw["w"]:
             out += self._fence()  # warm-up results: not timed
             tw["t0"] = time.perf_counter()
+            tw["host0"] = self._host_s()
         if tw["w"] <= i < tw["w"] + tw["k"]:
             tw["records"] += len(records)
         out += self._keep(super().submit(records, ingest_ts, tags))
@@ -68,6 +69,12 @@ class TimedWindow:
     def poll(self):
         return self._keep(super().poll())
 
+    def _host_s(self) -> dict:
+        """The GPU runner's cumulative host seconds per phase (gather / decode, select,
+        launch, wait), when the model has one."""
+        r = getattr(self, "_runner", None)
+        return dict(getattr(r, "host_s", {}) or {})
+
     def _write(self, elapsed: float) -> None:
         from ..parallel import comm
 
@@ -77,8 +84,10 @@ class TimedWindow:
         os.makedirs(tw["dir"], exist_ok=True)
         tmp = os.path.join(tw["dir"], f".rank{rank}.json")
         with open(tmp, "w") as f:
+            h0, h1 = tw.get("host0") or {}, self._host_s()
+            host = {k: round((v - h0.get(k, 0.0)) * 1e3 / max(1, tw["k"]), 3) for k, v in h1.items()}
             json.dump({"rank": rank, "world": comm.rank_size()[1], "elapsed_s": elapsed, "records": tw["records"],
-                       "latencies_s": lat.tolist(), "pid": os.getpid(),
+                       "latencies_s": lat.tolist(), "pid": os.getpid(), "host_ms_per_batch": host,
                        "communicator": type(comm.get()).__name__ if comm.is_dist() else None}, f)
         os.replace(tmp, os.path.join(tw["dir"], f"rank{rank}.json"))
 

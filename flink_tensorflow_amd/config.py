@@ -47,7 +47,6 @@ class EngineConfig:
     recompute_tails: bool = True       # stage-1 residual stream recomputed from 64-ch sources, not re-read
     pw_res_kernel: bool = True         # identity-residual expand convs on the persistent kernel
     conv3x3c64_kernel: bool = True     # 64-channel 3x3 convs with the filter bank in LDS
-    conv_lite_waves: int = 4           # single-source conv_lite tile: 4 waves of 64x64 or 2 of 128x64 outputs
     # cache-resident batch slices: the plan's leading run of large-activation layers (every
     # tensor >= chain_min_hw pixels per image: Inception-v3's 149x149 .. 71x71 stem) runs once
     # per slice of chain_batch images, its intermediates in slice-sized buffers that stay in
@@ -152,8 +151,6 @@ class EngineConfig:
             raise ValueError("arena_fraction must be in (0, 1]")
         if self.wd_sparse_exchange not in ("bucketed", "owner", "allgather"):
             raise ValueError("wd_sparse_exchange must be bucketed, owner or allgather")
-        if self.conv_lite_waves not in (2, 4):
-            raise ValueError("conv_lite_waves must be 2 or 4")
         if self.wd_bucket_slack <= 0:
             raise ValueError("wd_bucket_slack must be positive")
         if self.batch_buckets and sorted(self.batch_buckets) != list(self.batch_buckets):

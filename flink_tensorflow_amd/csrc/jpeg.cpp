@@ -19,6 +19,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <immintrin.h>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -112,6 +113,9 @@ struct Idct {
     const int i = int(v + 128.5f);  // v + 128, rounded (v > -128.5 for the cast to floor)
     return uint8_t(i < 0 ? 0 : i > 255 ? 255 : i);
   }
+#if defined(__AVX2__) && defined(__FMA__)
+  static void run_avx2(const int32_t* F, uint8_t* out, int stride);
+#endif
   void run(const int32_t* F, uint8_t* out, int stride) const {
     bool ac = false;
     for (int k = 1; k < 64; ++k) ac |= F[k] != 0;
@@ -120,6 +124,10 @@ struct Idct {
       for (int x = 0; x < 8; ++x) std::memset(out + x * stride, v, 8);
       return;
     }
+#if defined(__AVX2__) && defined(__FMA__)
+    run_avx2(F, out, stride);
+    return;
+#endif
     float f[64], g[64];
     for (int k = 0; k < 64; ++k) f[k] = float(F[k]);
     for (int u = 0; u < 8; ++u) {  // rows: f[u][v] over v -> g[u][y]
@@ -140,6 +148,82 @@ struct Idct {
     }
   }
 };
+
+#if defined(__AVX2__) && defined(__FMA__)
+// The same factorisation on 8 lanes: a vector holds one coefficient index of 8 rows (or
+// columns), the 1-D transform runs on 8 of them at once, and two 8x8 transposes put the
+// row pass's outputs into the column pass's layout and its outputs back into rows.
+static inline void transpose8(__m256* r) {
+  const __m256 t0 = _mm256_unpacklo_ps(r[0], r[1]), t1 = _mm256_unpackhi_ps(r[0], r[1]);
+  const __m256 t2 = _mm256_unpacklo_ps(r[2], r[3]), t3 = _mm256_unpackhi_ps(r[2], r[3]);
+  const __m256 t4 = _mm256_unpacklo_ps(r[4], r[5]), t5 = _mm256_unpackhi_ps(r[4], r[5]);
+  const __m256 t6 = _mm256_unpacklo_ps(r[6], r[7]), t7 = _mm256_unpackhi_ps(r[6], r[7]);
+  const __m256 u0 = _mm256_shuffle_ps(t0, t2, 0x44), u1 = _mm256_shuffle_ps(t0, t2, 0xEE);
+  const __m256 u2 = _mm256_shuffle_ps(t1, t3, 0x44), u3 = _mm256_shuffle_ps(t1, t3, 0xEE);
+  const __m256 u4 = _mm256_shuffle_ps(t4, t6, 0x44), u5 = _mm256_shuffle_ps(t4, t6, 0xEE);
+  const __m256 u6 = _mm256_shuffle_ps(t5, t7, 0x44), u7 = _mm256_shuffle_ps(t5, t7, 0xEE);
+  r[0] = _mm256_permute2f128_ps(u0, u4, 0x20);
+  r[1] = _mm256_permute2f128_ps(u1, u5, 0x20);
+  r[2] = _mm256_permute2f128_ps(u2, u6, 0x20);
+  r[3] = _mm256_permute2f128_ps(u3, u7, 0x20);
+  r[4] = _mm256_permute2f128_ps(u0, u4, 0x31);
+  r[5] = _mm256_permute2f128_ps(u1, u5, 0x31);
+  r[6] = _mm256_permute2f128_ps(u2, u6, 0x31);
+  r[7] = _mm256_permute2f128_ps(u3, u7, 0x31);
+}
+
+static inline void pass8(__m256* v) {
+  const auto k = [](float c) { return _mm256_set1_ps(c); };
+  const __m256 z1 = _mm256_mul_ps(_mm256_add_ps(v[2], v[6]), k(0.541196100f));
+  const __m256 t2 = _mm256_fnmadd_ps(v[6], k(1.847759065f), z1);
+  const __m256 t3 = _mm256_fmadd_ps(v[2], k(0.765366865f), z1);
+  const __m256 t0 = _mm256_add_ps(v[0], v[4]), t1 = _mm256_sub_ps(v[0], v[4]);
+  const __m256 t10 = _mm256_add_ps(t0, t3), t13 = _mm256_sub_ps(t0, t3);
+  const __m256 t11 = _mm256_add_ps(t1, t2), t12 = _mm256_sub_ps(t1, t2);
+  __m256 o0 = v[7], o1 = v[5], o2 = v[3], o3 = v[1];
+  const __m256 q1 = _mm256_add_ps(o0, o3), q2 = _mm256_add_ps(o1, o2);
+  const __m256 q3 = _mm256_add_ps(o0, o2), q4 = _mm256_add_ps(o1, o3);
+  const __m256 q5 = _mm256_mul_ps(_mm256_add_ps(q3, q4), k(1.175875602f));
+  const __m256 r1 = _mm256_mul_ps(q1, k(-0.899976223f)), r2 = _mm256_mul_ps(q2, k(-2.562915447f));
+  const __m256 r3 = _mm256_fmadd_ps(q3, k(-1.961570560f), q5), r4 = _mm256_fmadd_ps(q4, k(-0.390180644f), q5);
+  o0 = _mm256_fmadd_ps(o0, k(0.298631336f), _mm256_add_ps(r1, r3));
+  o1 = _mm256_fmadd_ps(o1, k(2.053119869f), _mm256_add_ps(r2, r4));
+  o2 = _mm256_fmadd_ps(o2, k(3.072711026f), _mm256_add_ps(r2, r3));
+  o3 = _mm256_fmadd_ps(o3, k(1.501321110f), _mm256_add_ps(r1, r4));
+  v[0] = _mm256_add_ps(t10, o3);
+  v[7] = _mm256_sub_ps(t10, o3);
+  v[1] = _mm256_add_ps(t11, o2);
+  v[6] = _mm256_sub_ps(t11, o2);
+  v[2] = _mm256_add_ps(t12, o1);
+  v[5] = _mm256_sub_ps(t12, o1);
+  v[3] = _mm256_add_ps(t13, o0);
+  v[4] = _mm256_sub_ps(t13, o0);
+}
+
+void Idct::run_avx2(const int32_t* F, uint8_t* out, int stride) {
+  __m256 v[8];
+  for (int u = 0; u < 8; ++u) v[u] = _mm256_cvtepi32_ps(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(F + 8 * u)));
+  transpose8(v);  // v[k]: coefficient k of every row u
+  pass8(v);       // v[y]: row pass output y of every row u
+  transpose8(v);  // v[u]: row u's outputs over y
+  pass8(v);       // v[x]: output row x over y
+  const __m256 sc = _mm256_set1_ps(0.125f), off = _mm256_set1_ps(128.5f);
+  __m256i q[8];
+  for (int x = 0; x < 8; ++x) {  // v / 8 + 128, rounded as the scalar path (truncation of v + 128.5)
+    const __m256i i = _mm256_cvttps_epi32(_mm256_fmadd_ps(v[x], sc, off));
+    q[x] = _mm256_min_epi32(_mm256_max_epi32(i, _mm256_setzero_si256()), _mm256_set1_epi32(255));
+  }
+  const __m256i perm = _mm256_setr_epi32(0, 4, 1, 5, 2, 6, 3, 7);
+  for (int h = 0; h < 2; ++h) {  // rows 4h .. 4h + 3
+    const __m256i p01 = _mm256_packus_epi32(q[4 * h], q[4 * h + 1]);
+    const __m256i p23 = _mm256_packus_epi32(q[4 * h + 2], q[4 * h + 3]);
+    const __m256i b = _mm256_permutevar8x32_epi32(_mm256_packus_epi16(p01, p23), perm);
+    alignas(32) uint8_t rows[32];
+    _mm256_store_si256(reinterpret_cast<__m256i*>(rows), b);
+    for (int r = 0; r < 4; ++r) std::memcpy(out + (4 * h + r) * stride, rows + 8 * r, 8);
+  }
+}
+#endif
 
 const Idct& idct() {
   static const Idct k;
@@ -282,10 +366,28 @@ class Decoder {
     return kOk;
   }
 
-  // ---- entropy-coded segment: bit reader over the stuffed byte stream
+  // ---- entropy-coded segment: bit reader over the stuffed byte stream.  64-bit buffer,
+  // MSB first; refill() tops it up to >= 32 valid bits — four bytes at once when none of
+  // them is 0xFF (no stuffing, no marker), byte by byte otherwise — so one refill covers a
+  // Huffman code (<= 16 bits) plus its magnitude bits (<= 15).
+  static bool has_ff(uint32_t w) {
+    const uint32_t v = ~w;
+    return ((v - 0x01010101u) & ~v & 0x80808080u) != 0;
+  }
   void refill() {
-    while (nbits_ <= 24) {
-      uint32_t byte = 0;
+    if (nbits_ >= 32) return;
+    if (!marker_ && end_ - p_ >= 4) {
+      uint32_t w;
+      std::memcpy(&w, p_, 4);
+      if (!has_ff(w)) {
+        bitbuf_ |= uint64_t(__builtin_bswap32(w)) << (32 - nbits_);
+        nbits_ += 32;
+        p_ += 4;
+        return;
+      }
+    }
+    while (nbits_ <= 56) {
+      uint64_t byte = 0;
       if (!marker_ && p_ < end_) {
         byte = *p_;
         if (byte == 0xFF) {
@@ -300,33 +402,32 @@ class Decoder {
           ++p_;
         }
       }
-      bitbuf_ |= byte << (24 - nbits_);
+      bitbuf_ |= byte << (56 - nbits_);
       nbits_ += 8;
     }
   }
+  // callers refill() first
   int getbits(int n) {
     if (n == 0) return 0;
-    refill();
-    const int v = int(bitbuf_ >> (32 - n));
+    const int v = int(bitbuf_ >> (64 - n));
     bitbuf_ <<= n;
     nbits_ -= n;
     return v;
   }
   static int extend(int v, int t) { return v < (1 << (t - 1)) ? v - (1 << t) + 1 : v; }
   int huff(const Huff& h) {
-    refill();
-    const uint16_t f = h.fast[bitbuf_ >> 23];
+    const uint16_t f = h.fast[bitbuf_ >> 55];
     if (f) {
       const int len = f >> 8;
       bitbuf_ <<= len;
       nbits_ -= len;
       return f & 0xFF;
     }
-    int code = int(bitbuf_ >> 23);  // 9 bits
+    int code = int(bitbuf_ >> 55);  // 9 bits
     int len = 9;
-    uint32_t rest = bitbuf_ << 9;
+    uint64_t rest = bitbuf_ << 9;
     while (len < 16 && code > h.maxcode[len]) {
-      code = (code << 1) | int(rest >> 31);
+      code = (code << 1) | int(rest >> 63);
       rest <<= 1;
       ++len;
     }
@@ -338,12 +439,14 @@ class Decoder {
   bool block(Component& c, int32_t* F) {
     std::memset(F, 0, 64 * sizeof(int32_t));
     const uint16_t* q = qt_[c.tq];
+    refill();
     const int t = huff(dc_[c.td]);
     if (t < 0 || t > 11) return false;
     c.pred += t ? extend(getbits(t), t) : 0;
     F[0] = c.pred * q[0];
     const Huff& ac = ac_[c.ta];
     for (int k = 1; k < 64;) {
+      refill();
       const int rs = huff(ac);
       if (rs < 0) return false;
       const int r = rs >> 4, s = rs & 15;
@@ -482,7 +585,7 @@ class Decoder {
   Huff dc_[4], ac_[4];
   Component c_[3];
   int h_ = 0, w_ = 0, nc_ = 0, hmax_ = 1, vmax_ = 1, mcux_ = 0, mcuy_ = 0, restart_ = 0;
-  uint32_t bitbuf_ = 0;
+  uint64_t bitbuf_ = 0;
   int nbits_ = 0;
   bool marker_ = false;
 };

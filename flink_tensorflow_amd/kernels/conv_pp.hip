@@ -84,33 +84,31 @@ FTM_DEVICE int lite_slot(int row, int chunk) {
 // for Cout >= 256, so one workgroup stages the input tile once for 256 channels where two
 // 128-wide tiles stage it twice: 24 KiB per 32-deep K-tile for 128 x 256 outputs, 25 % fewer
 // bytes per MAC than the 128x128 / 64-deep tile (the fp8 192-wide tile's gain: r04_ac).
-// NW = 2 (tile 3): the same 128 x 128 workgroup tile on TWO waves, each 128 pixels x 64
-// channels (8 pixel x 4 channel fragments, 128 accumulator registers), on 32-deep K-tiles
-// (2 x 16 KiB stages: four workgroups = eight waves per CU).  Per MFMA a wave reads 12 KiB
-// of fragments per 32 MFMAs instead of 8 KiB per 16: 27 % fewer LDS bytes per FLOP on the
-// read side, the DMA fill per FLOP unchanged.
 // MODE (diagnostics, bench/conv_layer_probe.py lite:4..6; outputs meaningless): 1 = no
 // MFMA (the fragments are folded by one VALU op so the LDS reads stay), 2 = no DMA after
 // the first K-tile, 3 = MFMAs only (fragments read once, no DMA or LDS reads in the loop).
-template <int ACT, bool HAS_RES, int BK, bool DUAL = false, bool STAMP = false, int BN_ = 128, int NW = 4,
-          int MODE = 0>
-__global__ __launch_bounds__(NW * 64, 2) void conv_lite_kernel(CPParams p) {
+// Measured on the stage-3 3x3 (profiles/r06_conv_probe): 68.7 µs whole, 45.0 µs MFMAs only
+// (1.32 PF/s: the tile's ceiling at 784 tiles on 512 resident workgroups), 55.4 µs without
+// the DMA.  Deeper DMA prefetch (32-deep K-tiles on four stages: 87 µs; 64-deep on three,
+// one workgroup per CU: 110 µs) and a two-wave 128x64-per-wave tile (27 % fewer LDS
+// fragment bytes per MFMA: 78 µs) were measured slower and removed.
+template <int ACT, bool HAS_RES, int BK, bool DUAL = false, bool STAMP = false, int BN_ = 128, int MODE = 0>
+__global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
   // BK = 64: 128-B LDS rows, 2 x 32 KiB stages, 2 MFMA steps per K-tile.
   // BK = 32: 64-B rows, 2 x 16 KiB stages (the igemm's footprint: four workgroups per CU),
   //          1 MFMA step per K-tile; 16-B chunk slot = chunk ^ ((row >> 2) & 3) keeps the
   //          16-lane ds_read_b128 groups on distinct banks.
   constexpr int BM = 128, BN = BN_;
-  constexpr int NT = NW * 64;              // threads
+  constexpr int NT = 256;                  // threads
   constexpr int ROWB = BK * 2;             // LDS row bytes
   constexpr int CPR = ROWB / 16;           // 16-B chunks per row
   constexpr int RPI = 1024 / ROWB;         // rows per DMA wave-instruction
-  constexpr int QX = BM / RPI / NW;        // DMA instructions per wave for the pixel image
-  constexpr int QW = BN / RPI / NW;        // ... for the weight image
+  constexpr int QX = BM / RPI / 4;         // DMA instructions per wave for the pixel image
+  constexpr int QW = BN / RPI / 4;         // ... for the weight image
   constexpr int QM = QX > QW ? QX : QW;
   constexpr int NI = BN / 32;              // channel fragments per wave (BN / 2 channels)
-  constexpr int PJ = NW == 2 ? 8 : 4;      // pixel fragments per wave
+  constexpr int PJ = 4;                    // pixel fragments per wave
   static_assert(QX <= 4 && QW <= 4 && (BN == 128 || BN == 256), "channel tile 128 or 256");
-  static_assert(NW == 4 || (NW == 2 && BN == 128 && !DUAL), "two-wave tile: 128 channels, one source");
   constexpr int XB = BM * ROWB, WB = BN * ROWB, STG = XB + WB;
   constexpr int OPITCH = BN * 2 + 16;
   constexpr int LDS = 2 * STG > BM * OPITCH ? 2 * STG : BM * OPITCH;
@@ -124,8 +122,8 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_lite_kernel(CPParams p) {
   const int n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = NW == 2 ? 0 : wave & 1;      // pixel half of the tile (two waves: all 128)
-  const int wn = NW == 2 ? wave : wave >> 1;  // channel half
+  const int wm = wave & 1;   // pixel half of the tile
+  const int wn = wave >> 1;  // channel half
 
   // DMA roles: wave w stages image rows RPI * (QX w + q) + lane / CPR of both the X (pixel)
   // and W (channel) images; the lane's 16-B chunk is pre-swizzled on the source
@@ -329,26 +327,10 @@ template <int ACT>
 void launch_lite(const CPParams& p, hipStream_t s, bool dual, int tile) {
   const dim3 grid(p.tiles_m * p.tiles_n), block(256);
   if (tile >= 4 && tile <= 6 && !p.res) {  // diagnostics (outputs meaningless)
-    if (tile == 4) hipLaunchKernelGGL((conv_lite_kernel<ACT, false, 64, false, false, 128, 4, 1>), grid, block, 0, s, p);
-    if (tile == 5) hipLaunchKernelGGL((conv_lite_kernel<ACT, false, 64, false, false, 128, 4, 2>), grid, block, 0, s, p);
-    if (tile == 6) hipLaunchKernelGGL((conv_lite_kernel<ACT, false, 64, false, false, 128, 4, 3>), grid, block, 0, s, p);
+    if (tile == 4) hipLaunchKernelGGL((conv_lite_kernel<ACT, false, 64, false, false, 128, 1>), grid, block, 0, s, p);
+    if (tile == 5) hipLaunchKernelGGL((conv_lite_kernel<ACT, false, 64, false, false, 128, 2>), grid, block, 0, s, p);
+    if (tile == 6) hipLaunchKernelGGL((conv_lite_kernel<ACT, false, 64, false, false, 128, 3>), grid, block, 0, s, p);
     return;
-  }
-  if (tile == 3) {  // two waves, 128 x 64 each, 32-deep K-tiles
-    if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, 32, false, false, 128, 2>), grid, dim3(128), 0, s, p);
-    else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, 32, false, false, 128, 2>), grid, dim3(128), 0, s, p);
-    return;
-  }
-  if (dual) {
-    if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, 64, true>), grid, block, 0, s, p);
-    else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, 64, true>), grid, block, 0, s, p);
-    return;
-  }
-  if constexpr (ACT == ACT_RELU) {
-    if (p.stamp && !p.res) {  // diagnostics only (conv_lite_stamp)
-      hipLaunchKernelGGL((conv_lite_kernel<ACT, false, 64, false, true>), grid, block, 0, s, p);
-      return;
-    }
   }
   if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, 64>), grid, block, 0, s, p);
   else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, 64>), grid, block, 0, s, p);
@@ -419,8 +401,8 @@ void conv_pp(pybind11::list srcs, uintptr_t ktab, uintptr_t w, uintptr_t bias, u
   p.OH = OH; p.OW = OW;
   p.ldw = (int)K; p.ldy = ldy; p.y_coff = y_coff; p.ldr = ldr;
   p.stamp = g_lite_stamp;
-  need(tile == 2 || (tile >= 3 && tile <= 6 && ns == 1), "tile must be 2 (conv_lite 128x128, 4 waves, K-tile 64) or 3 "
-       "(2 waves, K-tile 32, one source); 4..6 are diagnostics");
+  need(tile == 2 || (tile >= 4 && tile <= 6 && ns == 1),
+       "tile must be 2 (conv_lite: 4 waves, K-tile 64, 2 stages); 4..6 are diagnostics");
   need(splits <= 1, "conv_lite takes no split-K");
   (void)ws;
   p.tiles_m = (p.M + 127) / 128;

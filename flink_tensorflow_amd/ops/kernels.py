@@ -598,10 +598,9 @@ def conv_pp_ktab(srcs) -> torch.Tensor:
 
 class ConvPP:
     """A planned ``conv_lite`` launch (kernels/conv_pp.hip): implicit-GEMM NHWC convolution
-    of one or two sources into one accumulator on the 128x128 LDS-DMA tile: ``tile`` 2 =
-    four waves of 64x64 outputs on 64-deep K-tiles, ``tile`` 3 = two waves of 128x64 on
-    32-deep K-tiles (one source; ``EngineConfig.conv_lite_waves``).  The ping-pong / wide /
-    wave-split tiles measured slower and were removed.
+    of one or two sources into one accumulator on the 4-wave 128x128 LDS-DMA tile (``tile``
+    2; 4..6 are diagnostic variants).  The ping-pong / wide / wave-split / two-wave /
+    deeper-prefetch tiles measured slower and were removed (``kernels/conv_pp.hip``).
 
     ``srcs``: [(x_shape NHWC, (KH, KW), (sh, sw), (pt, pl), (dh, dw))]; the weight is the
     concatenation of the sources' OHWI filters, [Cout, sum KH*KW*C] bf16; a second source
@@ -620,14 +619,10 @@ class ConvPP:
         if Cout % 8:
             raise ValueError("conv_pp: Cout % 8")
         self.M = self.N * self.OH * self.OW
-        if tile is None:
-            from ..config import current
-
-            tile = 3 if current().conv_lite_waves == 2 and len(self.srcs) == 1 else 2
-        self.tile = tile
-        # (4..6: diagnostic variants of tile 2 for bench/conv_layer_probe.py, outputs meaningless)
-        if self.tile not in (2, 3, 4, 5, 6) or (splits or 1) != 1 or (self.tile != 2 and len(self.srcs) != 1):
-            raise ValueError("conv_pp: conv_lite tile 2 (4 waves) or 3 (2 waves, one source), no split-K")
+        self.tile = 2 if tile is None else tile
+        # (4..6: diagnostic variants for bench/conv_layer_probe.py, outputs meaningless)
+        if self.tile not in (2, 4, 5, 6) or (splits or 1) != 1 or (self.tile != 2 and len(self.srcs) != 1):
+            raise ValueError("conv_pp: only the conv_lite tile (2) without split-K remains")
         if len(self.srcs) == 2:
             (xs1, k1, st1, pd1, dl1) = self.srcs[1]
             if tuple(k1) != (1, 1) or tuple(pd1) != (0, 0) or (self.OH - 1) * st1[0] >= xs1[1] \

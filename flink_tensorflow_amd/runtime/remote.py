@@ -538,6 +538,10 @@ def _worker_main(in_name: str, out_name: str, slab_name: str | None = None):
                 op = None
                 _close_group(group, abort=False)
                 group = None
+                if profiler is not None:  # before "closed": the coordinator may reap us after it
+                    profiler.disable()
+                    profiler.dump_stats(f"{os.environ['FTM_WORKER_PROFILE']}.{os.getpid()}")
+                    profiler = None
                 flush()
                 out.send(("closed", metrics.snapshot()), alive=parent_alive)
                 break

@@ -255,6 +255,85 @@ class FileMonitorFunction(SourceFunction, CheckpointedFunction):
         self._running = False
 
 
+class PartitionedFileSource(SourceFunction, CheckpointedFunction):
+    """``read_file(..., monitor="partitioned")``: the monitor and the reader in one source
+    subtask per reader, each listing the directory itself and taking the files whose path
+    hashes to its index (``crc32(path) % parallelism``), reading a run of them at once on the
+    native host pool (``read_files``) and handing the run's records on as one run
+    (``SourceContext.collect_many``).  Relocatable, so a subtask runs inside the worker
+    process of the GPU operator it feeds: no path and no record crosses the coordinator,
+    where the Flink-shaped monitor + readers (``FileMonitorFunction`` ->
+    ``FileReaderOperator``) forward every path through it.  State: the paths already
+    emitted by this subtask (as the monitor's), so a restore re-reads none of them."""
+
+    relocatable = True
+
+    def __init__(self, fmt: WholeFileInputFormat, path: str, mode: FileProcessingMode = PROCESS_ONCE,
+                 interval_s: float = 1.0, max_polls: int | None = None, run: int = 64, read_threads: int = 8):
+        super().__init__()
+        self.fmt = fmt
+        self.path = path
+        self.mode = mode
+        self.interval = interval_s
+        self.max_polls = max_polls
+        self.run_size = max(1, int(run))
+        self.read_threads = read_threads
+        self.seen: set[str] = set()
+        self._running = True
+
+    def initialize_state(self, ctx):
+        self._state = ctx.operator_state.get_list_state(ListStateDescriptor("seen"))
+        if ctx.is_restored():
+            self.seen = set(self._state.get())
+
+    def snapshot_state(self, ctx):
+        self._state.update(sorted(self.seen))
+
+    def open(self, parameters=None):
+        self.fmt.open_input_format()
+
+    def close(self):
+        self.fmt.close_input_format()
+
+    def _read(self, paths: list) -> list:
+        blobs = [None] * len(paths)
+        if isinstance(fs.get_fs(self.path)[0], fs.LocalFS):  # the listing's children are local too
+            from .. import _ext
+
+            blobs = _ext.native().read_files([fs.get_fs(p)[1] if "://" in p else p for p in paths],
+                                             self.read_threads)
+        # not local, or unreadable: the per-file path (raises with the OS error)
+        return [b if b is not None else fs.read_bytes(p) for p, b in zip(paths, blobs)]
+
+    def run(self, ctx):
+        import zlib
+
+        idx, par = _partition(self.get_runtime_context())
+        polls = 0
+        while self._running:
+            mine = sorted((f for f in self.fmt.files(self.path)
+                           if f not in self.seen and zlib.crc32(f.encode()) % par == idx), key=_mtime_then_name)
+            for lo in range(0, len(mine), self.run_size):
+                if not self._running:
+                    return
+                paths = mine[lo:lo + self.run_size]
+                outs = [o for o in (self.fmt.read_record(p, d) for p, d in zip(paths, self._read(paths)))
+                        if o is not None]
+                with ctx.checkpoint_lock:
+                    if outs:
+                        ctx.collect_many(outs)
+                    self.seen.update(paths)
+            polls += 1
+            if self.mode == PROCESS_ONCE or (self.max_polls is not None and polls >= self.max_polls):
+                break
+            t_end = time.time() + self.interval
+            while self._running and time.time() < t_end:
+                time.sleep(min(0.05, self.interval))
+
+    def cancel(self):
+        self._running = False
+
+
 def _mtime_then_name(path: str):
     import os
 

@@ -171,16 +171,27 @@ class StreamExecutionEnvironment:
         return self.add_source(GeneratorSource(factory, limit, bulk), "generator", parallelism)
 
     def read_file(self, fmt: WholeFileInputFormat, path: str, mode=PROCESS_ONCE, interval_s: float = 1.0,
-                  parallelism: int | None = None, max_polls: int | None = None) -> "DataStream":
+                  parallelism: int | None = None, max_polls: int | None = None,
+                  monitor: str = "coordinator") -> "DataStream":
         """``StreamExecutionEnvironment.readFile`` (``EX/inception/inception.scala:33-34``)
         as Flink builds it: one monitor (parallelism 1, in the coordinator) forwarding the
         new files' paths round-robin to ``parallelism`` readers (default: the
         environment's) that read and decode them.  A reader feeding a worker-process GPU
         operator of its parallelism is chained into that worker, so decoding happens where
-        the records are consumed and only paths cross the coordinator."""
+        the records are consumed and only paths cross the coordinator.  ``monitor=
+        "partitioned"``: each reader lists the directory itself and takes its hash share of the
+        files (``sources.PartitionedFileSource``) — nothing crosses the coordinator."""
         from .operators import FileReaderOperator
-        from .sources import FileMonitorFunction
+        from .sources import FileMonitorFunction, PartitionedFileSource
 
+        if monitor == "partitioned":
+            # one listing + reading source subtask per reader (``PartitionedFileSource``):
+            # relocated into the worker process of the operator it feeds, so nothing
+            # crosses the coordinator
+            return self.add_source(PartitionedFileSource(fmt, path, mode, interval_s, max_polls), "file-source",
+                                   parallelism or self.parallelism)
+        if monitor != "coordinator":
+            raise ValueError("read_file: monitor must be 'coordinator' or 'partitioned'")
         mon = self.add_source(FileMonitorFunction(fmt, path, mode, interval_s, max_polls), "file-monitor", 1)
         proto = fmt
         readers = mon._add("file-reader", lambda: FileReaderOperator(clone_function(proto), "file-reader"),

@@ -201,3 +201,64 @@ def test_read_file_rebalance_then_workers_still_chains(tmp_path):
     recs = sum(v["records"] for v in stats)
     longest = max(len(str(p)) for p in imgs.iterdir())
     assert recs == 6 and sum(v["ring_bytes"] for v in stats) / recs <= longest + 32
+
+
+def test_partitioned_monitor_runs_inside_the_workers(tmp_path):
+    """``read_file(..., monitor="partitioned")``: each of the 3 model workers lists the
+    directory itself and takes its hash share of the files — every file labelled exactly
+    once, in the worker that read it, and nothing crosses the coordinator on the way in."""
+    from flink_tensorflow_amd.runtime.remote import TRANSPORT_STATS
+
+    imgs = tmp_path / "imgs"
+    imgs.mkdir()
+    for i in range(24):
+        (imgs / f"img{i:02d}.jpg").write_bytes(_jpeg(seed=i))
+    (imgs / "partial.crdownload").write_bytes(b"junk")
+    TRANSPORT_STATS.clear()
+    env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(3)
+    sink = (env.read_file(ImageInputFormat(), str(imgs), PROCESS_ONCE, monitor="partitioned")
+            .map_with_model(_ColorModel(), lambda rec, m: (rec[0], os.getpid(), m.label([rec[1]])[0][0][1]))
+            .run_in_processes().collect_into())
+    env.execute("read-file-partitioned")
+    out = sink.results()
+    assert sorted(n for n, _, _ in out) == [f"img{i:02d}.jpg" for i in range(24)]
+    pids = {p for _, p, _ in out}
+    assert len(pids) == 3 and os.getpid() not in pids
+    inbound = [v for k, v in TRANSPORT_STATS.items() if k[0] == "map-with-model"]
+    assert sum(v.get("records", 0) for v in inbound) == 0  # the sources ran in the workers
+
+
+def test_partitioned_source_splits_files_disjointly(tmp_path):
+    """The hash split: subtasks of one ``PartitionedFileSource`` see disjoint file sets
+    that together cover the directory, each emitted in runs (``collect_many``)."""
+    import zlib
+
+    from flink_tensorflow_amd.runtime.sources import BytesInputFormat, PartitionedFileSource
+
+    d = tmp_path / "in"
+    d.mkdir()
+    for i in range(50):
+        (d / f"f{i:02d}.bin").write_bytes(bytes([i]) * 3)
+
+    class Ctx:
+        def __init__(self, idx, par):
+            self.subtask_index, self.parallelism = idx, par
+            self.runs = []
+            self.checkpoint_lock = threading.RLock()
+
+        def collect_many(self, values, timestamp=None):
+            self.runs.append(list(values))
+
+    got = []
+    for idx in range(3):
+        src = PartitionedFileSource(BytesInputFormat(), str(d), PROCESS_ONCE, run=8)
+        ctx = Ctx(idx, 3)
+        src.set_runtime_context(ctx)
+        src.open()
+        src.run(ctx)
+        names = [os.path.basename(p) for r in ctx.runs for p, _ in r]
+        assert all(len(r) <= 8 for r in ctx.runs)
+        assert all(zlib.crc32(str(d / n).encode()) % 3 == idx for n in names)
+        assert all(data == bytes([int(n[1:3])]) * 3 for r in ctx.runs for p, data in r for n in [os.path.basename(p)])
+        got += names
+    assert sorted(got) == [f"f{i:02d}.bin" for i in range(50)]
