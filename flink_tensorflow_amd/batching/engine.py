@@ -82,7 +82,7 @@ class PipelinedGpuRunner:
     def __init__(self, plans, feed: str, fetch_bufs: Callable[[Any], Sequence[torch.Tensor]],
                  record_shape, record_dtype=torch.uint8, depth: int = 3, device=None, gather_threads: int = 8,
                  stage_chunk: int = 64, lane_offset_us: float = 0.0, freeze_gc: bool = True, timeline: bool = False,
-                 interleave_head: bool = True, decode_threads: int = 16):
+                 interleave_head: bool = True, decode_threads: int = 16, async_decode: bool = True):
         lanes = plans if isinstance(plans, (list, tuple)) else [plans]
         self.lanes = [dict(sorted(p.items())) for p in lanes]
         self.plans = self.lanes[0]
@@ -106,6 +106,8 @@ class PipelinedGpuRunner:
         # are decoded by the native pool straight into the pinned rows (csrc/jpeg.cpp)
         self.decode_threads = decode_threads
         self.decode_fallbacks = 0
+        self.async_decode = async_decode
+        self._pending = None  # (DecodeJob, slot, bucket, payloads, ingest_ts, tags)
         self.stage_chunk = stage_chunk  # records per gather + H2D piece (0: whole batch at once)
         self.interleave_head = interleave_head  # launch each piece's head kernel inside the gather loop
         self._native = _ext.native()
@@ -148,10 +150,13 @@ class PipelinedGpuRunner:
         return self.buckets[i]
 
     # ------------------------------------------------------------------ submission
-    def submit(self, payloads: Sequence, ingest_ts: np.ndarray, tags: list | None = None) -> list[BatchResult]:
-        """Stages ``payloads`` (buffer-protocol records of ``record_shape``) and launches the
-        batch.  Returns results of earlier batches that completed (slot reuse)."""
-        n = len(payloads)
+    def _is_jpeg(self, payloads) -> bool:
+        return (isinstance(payloads[0], (bytes, bytearray, memoryview)) and len(self.record_shape) == 3
+                and self.record_shape[2] == 3 and self.record_dtype == torch.uint8)
+
+    def _reserve(self, n: int):
+        """The bucket and ring slot of an n-record batch, with the slot's previous batch
+        (and anything beyond the in-flight cap) harvested."""
         b = self.bucket_for(n)
         slots = self.slots[b]
         slot = slots[self._next[b]]
@@ -160,6 +165,56 @@ class PipelinedGpuRunner:
         finished = self._harvest_through(slot) if slot.busy else []
         while len(self._inflight) >= self.max_inflight:
             finished.append(self._harvest(self._inflight[0]))
+        self.host_s["wait"] += time.perf_counter() - t0
+        return b, slot, finished
+
+    def submit(self, payloads: Sequence, ingest_ts: np.ndarray, tags: list | None = None) -> list[BatchResult]:
+        """Stages ``payloads`` (buffer-protocol records of ``record_shape``) and launches the
+        batch.  Returns results of earlier batches that completed (slot reuse).
+
+        JPEG byte strings (``ImageInputFormat(defer_decode=True)``) are decoded by the
+        native pool into the pinned slot; with ``async_decode`` that decode runs in the
+        background and the batch is launched by the next ``submit`` / ``poll`` / ``drain``
+        once it has landed, so the caller reads and batches the next records meanwhile."""
+        payloads = list(payloads)
+        finished = self._finish_pending(block=True)
+        if self.async_decode and self._is_jpeg(payloads):
+            b, slot, more = self._reserve(len(payloads))
+            H, W, _ = self.record_shape
+            base, cap = slot.pinned_in.data_ptr(), slot.pinned_in.numel() * slot.pinned_in.element_size()
+            job = self._native.jpeg_decode_start(base, cap, payloads, self.record_bytes, H, W, self.decode_threads)
+            self._pending = (job, slot, b, payloads, ingest_ts, tags)
+            return finished + more
+        b, slot, more = self._reserve(len(payloads))
+        self._stage_launch(slot, b, payloads, ingest_ts, tags, decoded=False)
+        return finished + more
+
+    def _finish_pending(self, block: bool) -> list[BatchResult]:
+        """Launches the batch whose JPEG decode runs in the background, once it has landed
+        (waiting for it when ``block``); images the native decoder declined go through
+        Pillow first."""
+        if self._pending is None:
+            return []
+        job, slot, b, payloads, ingest_ts, tags = self._pending
+        if not block and not job.done():
+            return []
+        self._pending = None
+        t0 = time.perf_counter()
+        st = job.wait()
+        self.host_s["decode_wait"] = self.host_s.get("decode_wait", 0.0) + time.perf_counter() - t0
+        bad = [k for k, code in enumerate(st) if code]
+        if bad:
+            from ..graph.ops_io import fit_image_bytes
+
+            H, W, _ = self.record_shape
+            for k in bad:
+                slot.pinned_in[k].copy_(torch.from_numpy(np.ascontiguousarray(fit_image_bytes(bytes(payloads[k]), H, W))))
+            self.decode_fallbacks += len(bad)
+        self._stage_launch(slot, b, payloads, ingest_ts, tags, decoded=True)
+        return []
+
+    def _stage_launch(self, slot: _Slot, b: int, payloads: list, ingest_ts, tags, decoded: bool) -> None:
+        n = len(payloads)
         t1 = time.perf_counter()
         # host gather into the pinned slot in pieces, each piece's H2D issued as soon as it is
         # staged (the DMA of piece i overlaps the gather of piece i+1: a batch reaches the GPU
@@ -168,7 +223,6 @@ class PipelinedGpuRunner:
         rb = self.record_bytes
         base, cap = slot.pinned_in.data_ptr(), slot.pinned_in.numel() * slot.pinned_in.element_size()
         step = self.stage_chunk if 0 < self.stage_chunk < n else n
-        payloads = list(payloads)
         pieces = [(lo, min(n, lo + step)) for lo in range(0, n, step)]
         while len(slot.h2d_parts) < len(pieces):
             slot.h2d_parts.append(torch.cuda.Event())
@@ -187,11 +241,12 @@ class PipelinedGpuRunner:
                       and plan.head_pieces_ok(self.feed, slot.dev_in))
         if interleave:
             self._begin_lane(slot, lane, stream)
-        jpeg = isinstance(payloads[0], (bytes, bytearray, memoryview)) and len(self.record_shape) == 3 \
-            and self.record_shape[2] == 3 and self.record_dtype == torch.uint8
+        jpeg = self._is_jpeg(payloads)
         with trace_range(f"gather[{n}/{b}]"):
             for i, (lo, hi) in enumerate(pieces):
-                if jpeg:
+                if decoded:
+                    pass  # the rows are in the slot already (background decode)
+                elif jpeg:
                     self._decode_into(slot, base, cap, lo, payloads[lo:hi])
                 else:
                     self._native.gather_into(base + lo * rb, cap - lo * rb, payloads[lo:hi], rb, self.gather_threads)
@@ -245,12 +300,10 @@ class PipelinedGpuRunner:
         self._inflight.append(slot)
         t4 = time.perf_counter()
         hs = self.host_s
-        hs["wait"] += t1 - t0
         hs["gather"] += t2 - t1
         hs["select"] += t3 - t2
         hs["launch"] += t4 - t3
         self.batches += 1
-        return finished
 
     def _decode_into(self, slot: _Slot, base: int, cap: int, lo: int, blobs: list) -> None:
         """JPEG byte strings -> RGB rows ``lo ..`` of the pinned slot: the native baseline
@@ -318,9 +371,9 @@ class PipelinedGpuRunner:
         self.timeline.clear()
 
     def poll(self) -> list[BatchResult]:
-        """Harvests completed batches without blocking, oldest first, stopping at the
-        first one still running."""
-        out = []
+        """Launches a background-decoded batch that has landed, then harvests completed
+        batches without blocking, oldest first, stopping at the first one still running."""
+        out = self._finish_pending(block=False)
         while self._inflight:
             with capture_lock():
                 ready = self._inflight[0].done.query()
@@ -330,7 +383,7 @@ class PipelinedGpuRunner:
         return out
 
     def drain(self) -> list[BatchResult]:
-        out = []
+        out = self._finish_pending(block=True)
         while self._inflight:
             out.append(self._harvest(self._inflight[0]))
         return out

@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstring>
 #include <immintrin.h>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -39,10 +40,28 @@ enum Status : int { kOk = 0, kNotJpeg = 1, kUnsupported = 2, kCorrupt = 3, kSize
 struct Huff {
   // canonical table: lookup of the first 9 bits, then the classic maxcode walk
   uint16_t fast[512];  // (length << 8) | symbol, 0 = longer code
+  // AC tables: when a 9-bit prefix holds a whole (code, magnitude bits) pair of a nonzero
+  // coefficient, its run, value and total length in one lookup (0 length = not there)
+  int16_t fast_val[512];
+  uint8_t fast_run[512], fast_len[512];
   int32_t maxcode[18];
   int32_t valoff[17];
   uint8_t vals[256];
   bool ok = false;
+
+  void build_fast_ac() {
+    for (int p = 0; p < 512; ++p) {
+      fast_len[p] = 0;
+      const uint16_t f = fast[p];
+      if (!f) continue;
+      const int len = f >> 8, rs = f & 0xFF, r = rs >> 4, sz = rs & 15;
+      if (sz == 0 || len + sz > 9) continue;
+      const int v = (p >> (9 - len - sz)) & ((1 << sz) - 1);
+      fast_val[p] = int16_t(v < (1 << (sz - 1)) ? v - (1 << sz) + 1 : v);
+      fast_run[p] = uint8_t(r);
+      fast_len[p] = uint8_t(len + sz);
+    }
+  }
 
   bool build(const uint8_t* counts, const uint8_t* symbols, int nsym) {
     std::memset(fast, 0, sizeof(fast));
@@ -116,9 +135,9 @@ struct Idct {
 #if defined(__AVX2__) && defined(__FMA__)
   static void run_avx2(const int32_t* F, uint8_t* out, int stride);
 #endif
-  void run(const int32_t* F, uint8_t* out, int stride) const {
-    bool ac = false;
-    for (int k = 1; k < 64; ++k) ac |= F[k] != 0;
+  // ac: whether the entropy decoder stored any AC coefficient (a zero one may still have
+  // been coded: the DC-only shortcut then just does not fire)
+  void run(const int32_t* F, uint8_t* out, int stride, bool ac) const {
     if (!ac) {  // DC only: IDCT = F[0] / 8 everywhere
       const uint8_t v = clamp8(float(F[0]) * 0.125f);
       for (int x = 0; x < 8; ++x) std::memset(out + x * stride, v, 8);
@@ -305,6 +324,7 @@ class Decoder {
       if (n > 256 || s + 17 + n > e) return kCorrupt;
       Huff& h = tc ? ac_[th] : dc_[th];
       if (!h.build(s + 1, s + 17, n)) return kCorrupt;
+      if (tc) h.build_fast_ac();
       s += 17 + n;
     }
     return kOk;
@@ -436,8 +456,9 @@ class Decoder {
     nbits_ -= len;
     return h.vals[h.valoff[len] + code];
   }
-  bool block(Component& c, int32_t* F) {
+  bool block(Component& c, int32_t* F, bool& any_ac) {
     std::memset(F, 0, 64 * sizeof(int32_t));
+    any_ac = false;
     const uint16_t* q = qt_[c.tq];
     refill();
     const int t = huff(dc_[c.td]);
@@ -447,6 +468,17 @@ class Decoder {
     const Huff& ac = ac_[c.ta];
     for (int k = 1; k < 64;) {
       refill();
+      const int p9 = int(bitbuf_ >> 55);
+      if (const int fl = ac.fast_len[p9]) {  // code + magnitude in the first 9 bits
+        k += ac.fast_run[p9];
+        if (k > 63) return false;
+        F[kZigzag[k]] = ac.fast_val[p9] * q[k];
+        any_ac = true;
+        ++k;
+        bitbuf_ <<= fl;
+        nbits_ -= fl;
+        continue;
+      }
       const int rs = huff(ac);
       if (rs < 0) return false;
       const int r = rs >> 4, s = rs & 15;
@@ -454,6 +486,7 @@ class Decoder {
         k += r;
         if (k > 63) return false;
         F[kZigzag[k]] = extend(getbits(s), s) * q[k];
+        any_ac = true;
         ++k;
       } else if (r == 15) {
         k += 16;
@@ -490,9 +523,10 @@ class Decoder {
           const int stride = c.bw * 8;
           for (int by = 0; by < c.v; ++by)
             for (int bx = 0; bx < c.h; ++bx) {
-              if (!block(c, F)) return kCorrupt;
+              bool any_ac;
+              if (!block(c, F, any_ac)) return kCorrupt;
               const int row = (my * c.v + by) * 8, col = (mx * c.h + bx) * 8;
-              id.run(F, c.plane.data() + size_t(row) * stride + col, stride);
+              id.run(F, c.plane.data() + size_t(row) * stride + col, stride, any_ac);
             }
         }
       }
@@ -530,7 +564,11 @@ class Decoder {
       const uint8_t* cb = pl[1] ? pl[1] + size_t(y) * W : c_[1].plane.data() + size_t(y) * c_[1].bw * 8;
       const uint8_t* cr = pl[2] ? pl[2] + size_t(y) * W : c_[2].plane.data() + size_t(y) * c_[2].bw * 8;
       uint8_t* d = dst + size_t(y) * W * 3;
-      for (int x = 0; x < W; ++x) {  // JFIF YCbCr -> RGB in 16.16 fixed point
+      int x0 = 0;
+#if defined(__AVX2__)
+      x0 = ycc_rgb16(ys, cb, cr, d, W);
+#endif
+      for (int x = x0; x < W; ++x) {  // JFIF YCbCr -> RGB in 16.16 fixed point
         const int Y = ys[x] << 16, B = cb[x] - 128, R = cr[x] - 128;
         const int r = (Y + 91881 * R + 32768) >> 16;
         const int g = (Y - 22554 * B - 46802 * R + 32768) >> 16;
@@ -542,13 +580,48 @@ class Decoder {
     }
     return kOk;
   }
+#if defined(__AVX2__)
+  // 16 pixels per step: YCbCr -> RGB in Q15 16-bit lanes (R = Y + Cr' + 0.402 Cr', G = Y -
+  // 0.344 Cb' - 0.714 Cr', B = Y + Cb' + 0.772 Cb', each product rounded by mulhrs), packed
+  // with saturation and interleaved to RGB by byte shuffles.  Returns the pixels done.
+  static int ycc_rgb16(const uint8_t* ys, const uint8_t* cb, const uint8_t* cr, uint8_t* d, int W) {
+    const __m256i c128 = _mm256_set1_epi16(128);
+    const __m256i kr = _mm256_set1_epi16(13173), kgb = _mm256_set1_epi16(11277), kgr = _mm256_set1_epi16(23401),
+                  kb = _mm256_set1_epi16(25297);
+    const __m128i m_rg0 = _mm_setr_epi8(0, 8, -1, 1, 9, -1, 2, 10, -1, 3, 11, -1, 4, 12, -1, 5);
+    const __m128i m_b0 = _mm_setr_epi8(-1, -1, 0, -1, -1, 1, -1, -1, 2, -1, -1, 3, -1, -1, 4, -1);
+    const __m128i m_rg1 = _mm_setr_epi8(13, -1, 6, 14, -1, 7, 15, -1, -1, -1, -1, -1, -1, -1, -1, -1);
+    const __m128i m_b1 = _mm_setr_epi8(-1, 5, -1, -1, 6, -1, -1, 7, -1, -1, -1, -1, -1, -1, -1, -1);
+    int x = 0;
+    for (; x + 16 <= W; x += 16) {
+      const __m256i Y = _mm256_cvtepu8_epi16(_mm_loadu_si128(reinterpret_cast<const __m128i*>(ys + x)));
+      const __m256i B_ = _mm256_sub_epi16(_mm256_cvtepu8_epi16(_mm_loadu_si128(reinterpret_cast<const __m128i*>(cb + x))), c128);
+      const __m256i R_ = _mm256_sub_epi16(_mm256_cvtepu8_epi16(_mm_loadu_si128(reinterpret_cast<const __m128i*>(cr + x))), c128);
+      const __m256i R = _mm256_add_epi16(_mm256_add_epi16(Y, R_), _mm256_mulhrs_epi16(R_, kr));
+      const __m256i G = _mm256_sub_epi16(_mm256_sub_epi16(Y, _mm256_mulhrs_epi16(B_, kgb)), _mm256_mulhrs_epi16(R_, kgr));
+      const __m256i B = _mm256_add_epi16(_mm256_add_epi16(Y, B_), _mm256_mulhrs_epi16(B_, kb));
+      const __m256i rg = _mm256_packus_epi16(R, G);                         // lane h: r(8h..8h+7), g(..)
+      const __m256i bb = _mm256_packus_epi16(B, _mm256_setzero_si256());   // lane h: b(8h..8h+7), 0
+      for (int h = 0; h < 2; ++h) {
+        const __m128i RG = h ? _mm256_extracti128_si256(rg, 1) : _mm256_castsi256_si128(rg);
+        const __m128i BB = h ? _mm256_extracti128_si256(bb, 1) : _mm256_castsi256_si128(bb);
+        uint8_t* o = d + 3 * (x + 8 * h);
+        _mm_storeu_si128(reinterpret_cast<__m128i*>(o),
+                         _mm_or_si128(_mm_shuffle_epi8(RG, m_rg0), _mm_shuffle_epi8(BB, m_b0)));
+        _mm_storel_epi64(reinterpret_cast<__m128i*>(o + 16),
+                         _mm_or_si128(_mm_shuffle_epi8(RG, m_rg1), _mm_shuffle_epi8(BB, m_b1)));
+      }
+    }
+    return x;
+  }
+#endif
   // triangle ("fancy") upsampling by 2 in x and / or y: each output sample weighs its
   // nearer input sample 3/4 and the farther 1/4 per upsampled axis (edges replicate), in
   // integers: a vertical 3:1 column sum, then a horizontal 3:1 blend, one rounding
   void upsample(const Component& c, int sx, int sy, uint8_t* out, int W, int H) const {
     const int cw = c.bw * 8;
     const int vw = (W + sx - 1) / sx, vh = (H + sy - 1) / sy;  // valid source samples
-    std::vector<int> col(size_t(vw) + 2);
+    std::vector<int16_t> col(size_t(vw) + 18);  // + edge replicas and a 16-lane overrun
     for (int y = 0; y < H; ++y) {
       const uint8_t *r0, *r1;
       int wv;  // vertical weights (wv : 4 - wv), scale 4
@@ -562,13 +635,32 @@ class Decoder {
         r0 = r1 = c.plane.data() + size_t(y) * cw;
         wv = 4;
       }
-      int* cs = col.data() + 1;  // cs[-1], cs[vw] replicate the edges
-      for (int x = 0; x < vw; ++x) cs[x] = wv * r0[x] + (4 - wv) * r1[x];
+      int16_t* cs = col.data() + 1;  // cs[-1], cs[vw] replicate the edges
+      for (int x = 0; x < vw; ++x) cs[x] = int16_t(wv * r0[x] + (4 - wv) * r1[x]);
       cs[-1] = cs[0];
       cs[vw] = cs[vw - 1];
       uint8_t* o = out + size_t(y) * W;
       if (sx == 2) {
-        for (int x = 0; x < W; ++x) {
+        int x = 0;
+#if defined(__AVX2__)
+        // 16 source columns -> 32 outputs: even 3 cs[j] + cs[j-1], odd 3 cs[j] + cs[j+1]
+        // (scale 16, + 8, >> 4), packed and interleaved byte-wise
+        const __m256i eight = _mm256_set1_epi16(8);
+        for (int j = 0; 2 * j + 32 <= W && j + 16 <= vw; j += 16, x += 32) {
+          const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(cs + j));
+          const __m256i cm = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(cs + j - 1));
+          const __m256i cp = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(cs + j + 1));
+          const __m256i c3 = _mm256_add_epi16(_mm256_add_epi16(c, c), c);
+          const __m256i e = _mm256_srli_epi16(_mm256_add_epi16(_mm256_add_epi16(c3, cm), eight), 4);
+          const __m256i od = _mm256_srli_epi16(_mm256_add_epi16(_mm256_add_epi16(c3, cp), eight), 4);
+          // interleave e / od as 16-bit pairs, then pack to bytes: lane h holds j + 8h ..
+          const __m256i lo = _mm256_unpacklo_epi16(e, od), hi = _mm256_unpackhi_epi16(e, od);
+          const __m256i b = _mm256_packus_epi16(lo, hi);  // lane0: j0..3 pairs, j4..7 pairs; lane1: j8..
+          _mm_storeu_si128(reinterpret_cast<__m128i*>(o + x), _mm256_castsi256_si128(b));
+          _mm_storeu_si128(reinterpret_cast<__m128i*>(o + x + 16), _mm256_extracti128_si256(b, 1));
+        }
+#endif
+        for (; x < W; ++x) {
           const int xc = x >> 1;
           const int v = 3 * cs[xc] + ((x & 1) ? cs[xc + 1] : cs[xc - 1]);  // scale 16
           o[x] = uint8_t((v + 8) >> 4);
@@ -625,6 +717,67 @@ std::vector<int> jpeg_decode_into(uintptr_t dst, size_t dst_bytes, const py::lis
   return status;
 }
 
+// A decode running in the background (jpeg_decode_start): a host thread drives the pool
+// over the batch while the caller goes on (the model worker keeps reading and batching the
+// next records); wait() joins it and returns the per-image statuses.  The job holds the
+// byte strings (and their buffer views) until then.
+struct DecodeJob {
+  py::list keep;
+  std::vector<Py_buffer> views;
+  size_t held = 0;
+  std::vector<int> status;
+  std::thread th;
+  std::atomic<bool> finished{false};
+  bool joined = false;
+
+  void release() {
+    for (size_t i = 0; i < held; ++i) PyBuffer_Release(&views[i]);
+    held = 0;
+  }
+  void join() {  // GIL held on entry
+    if (joined) return;
+    {
+      py::gil_scoped_release nogil;
+      th.join();
+    }
+    joined = true;
+    release();
+  }
+  ~DecodeJob() {
+    if (th.joinable()) join();
+    release();
+  }
+};
+
+std::shared_ptr<DecodeJob> jpeg_decode_start(uintptr_t dst, size_t dst_bytes, const py::list& images, size_t stride,
+                                             int H, int W, int nthreads) {
+  const size_t n = images.size();
+  if (size_t(H) * W * 3 > stride) throw std::invalid_argument("jpeg_decode_start: stride smaller than H*W*3");
+  if (n * stride > dst_bytes) throw std::invalid_argument("jpeg_decode_start: slot too small for the batch");
+  auto job = std::make_shared<DecodeJob>();
+  job->keep = images;
+  job->views.resize(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (PyObject_GetBuffer(images[i].ptr(), &job->views[i], PyBUF_SIMPLE) != 0) throw py::error_already_set();
+    ++job->held;
+  }
+  job->status.assign(n, kOk);
+  DecodeJob* j = job.get();
+  uint8_t* d = reinterpret_cast<uint8_t*>(dst);
+  job->th = std::thread([j, d, stride, H, W, nthreads, n]() {
+    pool_run(int(n), std::max(1, nthreads), [&](int i) {
+      Decoder dec(static_cast<const uint8_t*>(j->views[i].buf), size_t(j->views[i].len));
+      try {
+        j->status[i] = dec.decode(d + size_t(i) * stride, H, W);
+      } catch (...) {
+        j->status[i] = kCorrupt;
+      }
+    });
+    j->finished.store(true, std::memory_order_release);
+  });
+  return job;
+}
+
 // Whole files -> bytes, read on the host pool with the GIL released (the file reader's
 // bulk path: one Python call per run of paths instead of an open/read per record).  A file
 // that cannot be read comes back as None.
@@ -666,6 +819,15 @@ py::list read_files(const py::list& paths, int nthreads) {
 }  // namespace
 
 void register_jpeg(py::module_& m) {
+  py::class_<DecodeJob, std::shared_ptr<DecodeJob>>(m, "DecodeJob")
+      .def("done", [](DecodeJob& j) { return j.finished.load(std::memory_order_acquire); })
+      .def("wait", [](DecodeJob& j) {
+        j.join();
+        return j.status;
+      });
+  m.def("jpeg_decode_start", &jpeg_decode_start, py::arg("dst"), py::arg("dst_bytes"), py::arg("images"),
+        py::arg("stride"), py::arg("h"), py::arg("w"), py::arg("nthreads") = 8,
+        "jpeg_decode_into in the background: returns a DecodeJob (done() / wait() -> statuses).");
   m.def("read_files", &read_files, py::arg("paths"), py::arg("nthreads") = 8,
         "Reads whole files on the host pool (GIL released); bytes per path, None for a file that cannot be read.");
   m.def("jpeg_decode_into", &jpeg_decode_into, py::arg("dst"), py::arg("dst_bytes"), py::arg("images"),

@@ -181,3 +181,44 @@ def test_chained_reader_bulk_run_matches_per_record(tmp_path):
     sink_chain.setup(None, Output(lambda r: None))
     with pytest.raises(FileNotFoundError):
         sink_chain.process_batch([Record(str(tmp_path / "missing.jpg"), 0.0)], 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("async_decode", [True, False])
+def test_runner_decodes_jpeg_payloads_gpu(async_decode):
+    """JPEG byte strings through the compiled ResNet operator's runner: decoded by the
+    native pool into the pinned slot (in the background when ``async_decode``: launched by
+    the next submit / drain), a progressive file through Pillow — the same top-k as the
+    records decoded on the host first."""
+    import numpy as np
+    import torch
+
+    from flink_tensorflow_amd.graph.ops_io import decode_jpegs
+    from flink_tensorflow_amd.models.zoo.image_classifier import ResNet50Model
+
+    blobs = [_jpeg(_img(64, 64, s), quality=90) for s in range(11)]
+    blobs.append(_jpeg(_img(64, 64, 99), quality=90, progressive=True))
+    m = ResNet50Model(image_hw=(64, 64), buckets=(8,), depth_layers=26, lanes=1)
+    m.open()
+    try:
+        m._runner.async_decode = async_decode
+        dec = decode_jpegs(blobs, 64, 64)
+
+        def run(recs):
+            out = []
+            for lo in range(0, len(recs), 6):  # 6-record batches (bucket 8: padded)
+                chunk = recs[lo:lo + 6]
+                for res, _, _ in m.submit(chunk, np.zeros(len(chunk)), list(range(lo, lo + len(chunk)))):
+                    out += res
+            for res, _, _ in m.drain():
+                out += res
+            return out
+
+        got = run([(f"f{i}.jpg", b) for i, b in enumerate(blobs)])
+        ref = run([(f"f{i}.jpg", d) for i, d in enumerate(dec)])
+        assert len(got) == len(ref) == len(blobs)
+        assert got == ref  # identical staged bytes -> identical replays
+        assert m._runner.decode_fallbacks >= 1
+        torch.cuda.synchronize()
+    finally:
+        m.close()
