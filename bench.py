@@ -563,7 +563,7 @@ def run_job(args):
         "p99_latency_ms": round(float(np.percentile(lat, 99)) * 1e3, 3) if lat.size else None,
         "per_rank_records_per_s": [round(r["records"] / r["elapsed_s"], 1) for r in ranks],
         "communicator": ranks[0]["communicator"], "comm_world_size": ranks[0]["world"],
-        "host_ms_per_batch_rank0": ranks[0].get("host_ms_per_batch"),
+        "host_ms_per_batch_rank0": ranks[0].get("host_ms_per_batch"), "plan": ranks[0].get("plan"),
         "model_tflops_per_s": round(flops * total / 1e12, 1) if flops else None,
         "job_wall_s": round(wall, 2), "job_attempts": res.attempts}), flush=True)
 

@@ -86,9 +86,14 @@ class TimedWindow:
         with open(tmp, "w") as f:
             h0, h1 = tw.get("host0") or {}, self._host_s()
             host = {k: round((v - h0.get(k, 0.0)) * 1e3 / max(1, tw["k"]), 3) for k, v in h1.items()}
+            ps = getattr(self, "plan_summary", None)
+            try:
+                plan = ps() if callable(ps) else None
+            except Exception:  # noqa: BLE001  (diagnostics only)
+                plan = None
             json.dump({"rank": rank, "world": comm.rank_size()[1], "elapsed_s": elapsed, "records": tw["records"],
-                       "latencies_s": lat.tolist(), "pid": os.getpid(), "host_ms_per_batch": host,
-                       "communicator": type(comm.get()).__name__ if comm.is_dist() else None}, f)
+                       "latencies_s": lat.tolist(), "pid": os.getpid(), "host_ms_per_batch": host, "plan": plan,
+                       "communicator": type(comm.get()).__name__ if comm.is_dist() else None}, f, default=str)
         os.replace(tmp, os.path.join(tw["dir"], f"rank{rank}.json"))
 
 

@@ -26,7 +26,7 @@ from ..core import DefaultGraphLoader, GenericModel, GraphDefGraphLoader, GraphL
 
 
 class ImageClassifierModel(GenericModel, BatchedGpuModel):
-    _TRANSIENT = ("_graph", "_session", "_plans", "_runner", "_arena")
+    _TRANSIENT = ("_graph", "_session", "_plans", "_runner", "_arena", "_labels_cache")
 
     def __init__(self, graph_source: Callable[[], GraphDef] | str, image_hw: tuple[int, int],
                  buckets: Sequence[int] = (64, 256), top_k: int = 5, labels: Sequence[str] | None = None,
@@ -104,6 +104,9 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
         self._arena = None
         super().close()
 
+    def plan_summary(self) -> dict | None:
+        return next(iter(self._plans.values())).summary() if self._plans else None
+
     def label_of(self, i: int) -> str:
         return self.labels[i] if self.labels and i < len(self.labels) else f"class_{i}"
 
@@ -123,9 +126,20 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
             a = a[0]
         return np.ascontiguousarray(a, dtype=np.uint8)
 
+    def _label_table(self, n: int) -> list:
+        """``label_of`` for every class index below ``n``, built once (the per-batch result
+        conversion is 256 x top-k lookups on the worker's hot path)."""
+        t = self.__dict__.get("_labels_cache")
+        if t is None or len(t) < n:
+            t = self.__dict__["_labels_cache"] = [self.label_of(i) for i in range(max(n, 1024))]
+        return t
+
     def _results(self, br):
         vals, idxs = br.outputs[0][: br.n], br.outputs[1][: br.n]
-        res = [[(float(v), self.label_of(int(i))) for v, i in zip(vr, ir)] for vr, ir in zip(vals.tolist(), idxs.tolist())]
+        il = idxs.tolist()
+        lab = self._label_table(max((max(r) for r in il), default=0) + 1)
+        # tolist() already yields Python floats / ints
+        res = [list(zip(vr, [lab[i] for i in ir])) for vr, ir in zip(vals.tolist(), il)]
         return res, br.tags, br.latencies
 
     def submit(self, records, ingest_ts, tags):
