@@ -558,8 +558,11 @@ def click_record_layout(cfg: WideDeepConfig, n_cross: int = 8) -> np.dtype:
                      ("cross", "<i4", (n_cross,))])
 
 
-def pack_click_records(records, cfg: WideDeepConfig, n_cross: int = 8) -> np.ndarray:
-    """``(label, dense, cats, cross)`` tuples -> uint8 rows ``[n, row_bytes]``."""
+def pack_click_records(records, cfg: WideDeepConfig, n_cross: int | None = None) -> np.ndarray:
+    """``(label, dense, cats, cross)`` tuples -> uint8 rows ``[n, row_bytes]`` (``n_cross``
+    defaults to the first record's crossed-feature count, 8 for an empty list)."""
+    if n_cross is None:
+        n_cross = len(records[0][3]) if len(records) else 8
     lay = click_record_layout(cfg, n_cross)
     arr = np.zeros(len(records), lay)
     for i, r in enumerate(records):  # (label, dense, cats, cross[, anything else])

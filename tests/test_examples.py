@@ -138,17 +138,22 @@ def test_bert_stream_over_a_savedmodel(tmp_path):
     m.close()
 
 
-def test_widedeep_online_example_cpu():
-    """examples/widedeep_online.py on the host: the co-process job trains every click
-    record in micro-batches and answers the control stream's eval ticks."""
+@pytest.mark.parametrize("args", [[], ["--parallelism", "2"], ["--control-stream", "--eval-every", "0.5"]],
+                         ids=["generated", "generated-p2", "control-stream"])
+def test_widedeep_online_example_cpu(args):
+    """examples/widedeep_online.py on the host: the lockstep trainer job trains every click
+    record in agreed micro-batch steps — clicks generated in each rank's worker (P = 1, 2)
+    or, in the reference's co-process shape, from one coordinator source with a control
+    stream of eval ticks — and reports held-out losses."""
     import json
     import os
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    p = subprocess.run([sys.executable, os.path.join(root, "examples", "widedeep_online.py"), "--cpu",
-                        "--eval-every", "0.5"], capture_output=True, text=True, timeout=300, cwd=root)
+    p = subprocess.run([sys.executable, os.path.join(root, "examples", "widedeep_online.py"), "--cpu", *args],
+                       capture_output=True, text=True, timeout=300, cwd=root)
     assert p.returncode == 0, p.stderr[-2000:]
     out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
-    assert out["records_trained"] == 2048 and out["steps"] >= 8 and out["eval_losses"]
+    assert out["records_trained"] == 2048 and out["steps"] >= 4 and out["eval_losses"]
+    assert out["last_loss"] < out["first_loss"]
