@@ -66,26 +66,34 @@ def main():
     ap.add_argument("--readers", type=int, default=12, help="reader (decode) subtasks, each a worker process")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--warmup", type=int, default=4, help="untimed micro-batches")
-    ap.add_argument("--lanes", type=int, default=2)
-    ap.add_argument("--gpu-rate", type=float, default=77500.0, help="GPU-bound records/s (SPMD bench)")
+    ap.add_argument("--lanes", type=int, default=0, help="compute lanes (0: 2 for resnet50, 3 for inception_v3)")
+    ap.add_argument("--gpu-rate", type=float, default=0.0,
+                    help="GPU-bound records/s (SPMD bench; 0: 77.5k ResNet-50, 84.5k Inception-v3)")
     ap.add_argument("--max-delay-ms", type=float, default=20.0)
     ap.add_argument("--decode", default="staged", choices=["staged", "reader"],
                     help="staged: the reader emits the JPEG bytes and the model's host stage decodes them with the "
                          "native pool into the pinned slot (reader chained into the model worker); reader: Pillow "
                          "decode in --readers reader processes (the reference's placement)")
     ap.add_argument("--decode-threads", type=int, default=32)
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "inception_v3"],
+                    help="resnet50: bf16, 2 lanes, 256x256 files (the headline model); inception_v3: the reference "
+                         "example's model, fp8, 3 lanes, 299x299 files")
     ap.add_argument("--monitor", default="partitioned", choices=["partitioned", "coordinator"],
                     help="partitioned: the listing + reading source runs inside the model's worker (nothing crosses "
                          "the coordinator); coordinator: Flink's monitor in the coordinator forwarding paths")
     a = ap.parse_args()
 
     from flink_tensorflow_amd.batching.timed import TimedWindow
-    from flink_tensorflow_amd.models.zoo.image_classifier import ResNet50Model
+    from flink_tensorflow_amd.models.zoo.image_classifier import InceptionV3Model, ResNet50Model
     from flink_tensorflow_amd.models.zoo.inception import ImageInputFormat
     from flink_tensorflow_amd.runtime import PROCESS_ONCE, StreamExecutionEnvironment
     from flink_tensorflow_amd.runtime.sources import DiscardingSink
 
-    class TimedResNet(TimedWindow, ResNet50Model):
+    inc = a.model == "inception_v3"
+    if inc and a.hw == 256:
+        a.hw = 299
+
+    class TimedModel(TimedWindow, InceptionV3Model if inc else ResNet50Model):
         pass
 
     d = tempfile.mkdtemp(prefix="ftm-jpeg-")
@@ -125,8 +133,13 @@ def main():
 
         B = a.batch
         K = a.files // B - a.warmup - 1  # the last, partial batch is not timed
-        model = TimedResNet(image_hw=(a.hw, a.hw), buckets=(B,), lanes=a.lanes, depth=3,
-                            lane_offset_us=1500.0).timed_window(a.warmup, K, out_dir)
+        extra = {}
+        if inc:  # fp8 scales from the bench's own images (decoded once here)
+            from flink_tensorflow_amd.graph.ops_io import decode_jpegs
+
+            extra["calibration_images"] = decode_jpegs(datas[:64], a.hw, a.hw)
+        model = TimedModel(image_hw=(a.hw, a.hw), buckets=(B,), lanes=a.lanes or (3 if inc else 2), depth=3,
+                           lane_offset_us=1500.0, **extra).timed_window(a.warmup, K, out_dir)
         env = StreamExecutionEnvironment.get_execution_environment().set_parallelism(1)
         staged = a.decode == "staged"
         model.decode_threads = a.decode_threads
@@ -138,6 +151,8 @@ def main():
         readers.map_with_model_batched(model, None, max_batch=B, max_delay_ms=a.max_delay_ms, name="resnet50",
                                        parallelism=1).run_in_processes() \
             .add_sink(DiscardingSink()).run_in_processes()
+        if not a.gpu_rate:
+            a.gpu_rate = 84500.0 if inc else 77500.0
         t0 = time.perf_counter()
         res = env.execute("jpeg-e2e")
         wall = time.perf_counter() - t0
@@ -149,7 +164,8 @@ def main():
             "bench": "jpeg_e2e", "files": a.files, "hw": a.hw, "mean_jpeg_bytes": round(mean_bytes),
             "decode": ("native baseline decoder on the model's host pool, into the pinned slot "
                        f"({a.decode_threads} threads)" if staged else f"Pillow in {a.readers} reader processes"),
-            "readers": 1 if staged else a.readers, "monitor": a.monitor if staged else "coordinator", "gpus": 1, "model": "ResNet-50 v1.5 (bf16, compiled plan)",
+            "readers": 1 if staged else a.readers, "monitor": a.monitor if staged else "coordinator", "gpus": 1,
+            "model": "Inception-v3 (fp8, compiled plan)" if inc else "ResNet-50 v1.5 (bf16, compiled plan)",
             "records_per_s": round(rate, 1), "job_records_per_s": round(a.files / wall, 1),
             "job_wall_s": round(wall, 2), "timed_batches": K, "timed_records": r0["records"],
             "decode_ms_per_record_1thread": round(decode_ms, 3),
