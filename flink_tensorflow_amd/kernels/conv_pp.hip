@@ -326,6 +326,17 @@ __global__ __launch_bounds__(256, 2) void conv_lite_kernel(CPParams p) {
 template <int ACT>
 void launch_lite(const CPParams& p, hipStream_t s, bool dual, int tile) {
   const dim3 grid(p.tiles_m * p.tiles_n), block(256);
+  if (dual) {
+    if (p.res) hipLaunchKernelGGL((conv_lite_kernel<ACT, true, 64, true>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((conv_lite_kernel<ACT, false, 64, true>), grid, block, 0, s, p);
+    return;
+  }
+  if constexpr (ACT == ACT_RELU) {
+    if (p.stamp && !p.res) {  // diagnostics only (conv_lite_stamp)
+      hipLaunchKernelGGL((conv_lite_kernel<ACT, false, 64, false, true>), grid, block, 0, s, p);
+      return;
+    }
+  }
   if (tile >= 4 && tile <= 6 && !p.res) {  // diagnostics (outputs meaningless)
     if (tile == 4) hipLaunchKernelGGL((conv_lite_kernel<ACT, false, 64, false, false, 128, 1>), grid, block, 0, s, p);
     if (tile == 5) hipLaunchKernelGGL((conv_lite_kernel<ACT, false, 64, false, false, 128, 2>), grid, block, 0, s, p);
