@@ -23,6 +23,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <vector>
 
@@ -778,6 +779,36 @@ std::shared_ptr<DecodeJob> jpeg_decode_start(uintptr_t dst, size_t dst_bytes, co
   return job;
 }
 
+// (height, width, components, baseline) from the frame header, or (0, 0, 0, false) when
+// the bytes are not a JPEG / carry no frame header
+py::tuple jpeg_info(const py::bytes& b) {
+  const std::string_view v(b);
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(v.data());
+  const uint8_t* e = p + v.size();
+  if (e - p < 4 || p[0] != 0xFF || p[1] != 0xD8) return py::make_tuple(0, 0, 0, false);
+  p += 2;
+  while (p + 4 <= e) {
+    if (p[0] != 0xFF) break;
+    const uint8_t mk = p[1];
+    if (mk == 0xFF) {
+      ++p;
+      continue;
+    }
+    p += 2;
+    if (mk == 0xD8 || (mk >= 0xD0 && mk <= 0xD7) || mk == 0x01) continue;
+    if (mk == 0xD9 || mk == 0xDA) break;
+    const int len = (p[0] << 8) | p[1];
+    if (len < 2 || p + len > e) break;
+    if (mk >= 0xC0 && mk <= 0xCF && mk != 0xC4 && mk != 0xC8 && mk != 0xCC) {
+      if (len < 8) break;
+      const int h = (p[3] << 8) | p[4], w = (p[5] << 8) | p[6], nc = p[7];
+      return py::make_tuple(h, w, nc, (mk == 0xC0 || mk == 0xC1) && p[2] == 8);
+    }
+    p += len;
+  }
+  return py::make_tuple(0, 0, 0, false);
+}
+
 // Whole files -> bytes, read on the host pool with the GIL released (the file reader's
 // bulk path: one Python call per run of paths instead of an open/read per record).  A file
 // that cannot be read comes back as None.
@@ -819,6 +850,8 @@ py::list read_files(const py::list& paths, int nthreads) {
 }  // namespace
 
 void register_jpeg(py::module_& m) {
+  m.def("jpeg_info", &jpeg_info, py::arg("data"),
+        "(height, width, components, baseline) of a JPEG's frame header; zeros when there is none.");
   py::class_<DecodeJob, std::shared_ptr<DecodeJob>>(m, "DecodeJob")
       .def("done", [](DecodeJob& j) { return j.finished.load(std::memory_order_acquire); })
       .def("wait", [](DecodeJob& j) {

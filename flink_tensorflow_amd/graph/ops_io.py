@@ -155,6 +155,20 @@ def decode_jpegs_into(ptr: int, nbytes: int, blobs: list, stride: int, h: int, w
     return len(bad)
 
 
+def decode_rgb(data: bytes) -> np.ndarray:
+    """One image file -> RGB ``[h, w, 3]`` uint8 at its own size: the native baseline decoder
+    for baseline JPEGs (``csrc/jpeg.cpp``, GIL released), Pillow for everything else."""
+    from .. import _ext
+
+    nat = _ext.native()
+    h, w, nc, baseline = nat.jpeg_info(bytes(data))
+    if baseline and nc in (1, 3) and h > 0 and w > 0:
+        out = np.empty((h, w, 3), np.uint8)
+        if nat.jpeg_decode_into(out.ctypes.data, out.nbytes, [data], h * w * 3, h, w, 1)[0] == 0:
+            return out
+    return decode_image_bytes(bytes(data), 3)
+
+
 def decode_jpegs(blobs: list, h: int, w: int, threads: int = 8) -> np.ndarray:
     """``[n, h, w, 3]`` uint8 from JPEG byte strings (see :func:`decode_jpegs_into`)."""
     out = np.empty((len(blobs), h, w, 3), np.uint8)

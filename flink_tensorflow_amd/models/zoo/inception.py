@@ -204,9 +204,9 @@ class ImageInputFormat(WholeFileInputFormat):
             return os.path.basename(path), TensorValue.from_tensor(self.model.normalize(data))
         if self.defer_decode:
             return os.path.basename(path), data
-        from ...graph.ops_io import decode_image_bytes
+        from ...graph.ops_io import decode_rgb
 
-        img = decode_image_bytes(data, 3)
+        img = decode_rgb(data)  # native baseline decoder, Pillow for the rest
         if self.resize_to is not None and img.shape[:2] != tuple(self.resize_to):
             from PIL import Image
 

@@ -222,3 +222,25 @@ def test_runner_decodes_jpeg_payloads_gpu(async_decode):
         torch.cuda.synchronize()
     finally:
         m.close()
+
+
+def test_decode_rgb_any_size_and_fallbacks():
+    """``decode_rgb`` (ImageInputFormat's decode): the native decoder at the file's own size
+    for baseline JPEGs, Pillow for progressive files and PNGs."""
+    from PIL import Image
+
+    from flink_tensorflow_amd import _ext
+    from flink_tensorflow_amd.graph.ops_io import decode_rgb
+
+    a = _img(77, 123, 5)
+    b = _jpeg(a, quality=92)
+    assert _ext.native().jpeg_info(b) == (77, 123, 3, True)
+    out = decode_rgb(b)
+    assert out.shape == (77, 123, 3) and np.abs(out.astype(int) - _pil(b).astype(int)).max() <= 6
+    prog = _jpeg(a, quality=92, progressive=True)
+    assert _ext.native().jpeg_info(prog)[3] is False
+    assert np.array_equal(decode_rgb(prog), _pil(prog))
+    png = io.BytesIO()
+    Image.fromarray(a).save(png, format="PNG")
+    assert _ext.native().jpeg_info(png.getvalue()) == (0, 0, 0, False)
+    assert np.array_equal(decode_rgb(png.getvalue()), a)
