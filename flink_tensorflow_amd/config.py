@@ -45,6 +45,7 @@ class EngineConfig:
     fuse_block_tails: bool = True      # ResNet block boundary: expand + next reduce in one kernel
     decimate_tails: bool = True        # stage-1 tail output stored at the stride-2 reader's pixels
     recompute_tails: bool = True       # stage-1 residual stream recomputed from 64-ch sources, not re-read
+    chain_max_links: int = 2           # ... over at most this many links (3: -2 %, profiles/r06_chain)
     pw_res_kernel: bool = True         # identity-residual expand convs on the persistent kernel
     conv3x3c64_kernel: bool = True     # 64-channel 3x3 convs with the filter bank in LDS
     # cache-resident batch slices: the plan's leading run of large-activation layers (every

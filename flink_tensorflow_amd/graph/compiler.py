@@ -280,8 +280,9 @@ class CompiledFunction(TransformerLowering):
         that y3 again from the previous tails' 64-channel sources (the 3x3 outputs and the
         stem output, kept alive until it) instead of reading the 256-channel tensor, and the
         previous tail stops storing it.  Chains start at the dual (projection) tail and hold
-        up to three links: at micro-batch 256, ~1.4 GB less HBM traffic per batch for ~130
-        GFLOP of K = 64 MFMA work."""
+        up to ``chain_max_links`` links (2: tail 1 -> tail 2, the third tail reads y3 again;
+        three links recompute more than the saved traffic buys: 77.6-77.8k vs 79.3-79.6k,
+        profiles/r06_chain)."""
         self.chained_tails = 0
         if not _cfg().recompute_tails:
             return
@@ -301,7 +302,7 @@ class CompiledFunction(TransformerLowering):
                 continue
             prev = prods[0]
             prev_links = links_of[id(prev)]
-            if len(prev_links) >= 3 or id(res) in fetched or res.alias_of is not None or res.concat_slot is not None \
+            if len(prev_links) >= _cfg().chain_max_links or id(res) in fetched or res.alias_of is not None or res.concat_slot is not None \
                     or getattr(res, "buf_shape", None) is not None \
                     or any(v is not res and _root(v) is res for v in self.vals.values()):
                 continue

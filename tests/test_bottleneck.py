@@ -160,16 +160,17 @@ def test_chain_kernel_equals_unfused_tails_gpu():
     _chain_case(torch.device("cuda", 0), (3, 8, 14))  # a partial last tile
 
 
-def _compile_chain(g, dev, on):
+def _compile_chain(g, dev, on, links=2):
     from flink_tensorflow_amd.config import override
 
-    with override(recompute_tails=on):
+    with override(recompute_tails=on, chain_max_links=links):
         return CompiledFunction(g, {"images:0": ((2, 64, 64, 3), "UINT8")}, ["logits:0"], dev, strict=True)
 
 
-def _check_chain(r50, dev):
-    on, off = _compile_chain(r50, dev, True), _compile_chain(r50, dev, False)
-    assert on.summary()["chained_tails"] == 2 and off.summary()["chained_tails"] == 0
+def _check_chain(r50, dev, links=2):
+    on, off = _compile_chain(r50, dev, True, links), _compile_chain(r50, dev, False)
+    # links 2 (default): tail 1 -> tail 2 chained, tail 3 reads y3; links 3: all three
+    assert on.summary()["chained_tails"] == links - 1 and off.summary()["chained_tails"] == 0
     assert on.summary()["fused_tails"] == off.summary()["fused_tails"] == 3
     assert on.activation_bytes <= off.activation_bytes * 1.25
     imgs = torch.randint(0, 256, (2, 64, 64, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(2))
@@ -178,10 +179,12 @@ def _check_chain(r50, dev):
     assert torch.equal(a, b)  # the recomputed residual stream is bit-identical
 
 
-def test_compiled_resnet50_recomputes_the_stage1_residual_stream_cpu(r50):
-    _check_chain(r50, torch.device("cpu"))
+@pytest.mark.parametrize("links", [2, 3])
+def test_compiled_resnet50_recomputes_the_stage1_residual_stream_cpu(r50, links):
+    _check_chain(r50, torch.device("cpu"), links)
 
 
 @pytest.mark.gpu
-def test_compiled_resnet50_recomputes_the_stage1_residual_stream_gpu(r50):
-    _check_chain(r50, torch.device("cuda", 0))
+@pytest.mark.parametrize("links", [2, 3])
+def test_compiled_resnet50_recomputes_the_stage1_residual_stream_gpu(r50, links):
+    _check_chain(r50, torch.device("cuda", 0), links)
