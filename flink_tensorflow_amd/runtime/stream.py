@@ -172,7 +172,7 @@ class StreamExecutionEnvironment:
 
     def read_file(self, fmt: WholeFileInputFormat, path: str, mode=PROCESS_ONCE, interval_s: float = 1.0,
                   parallelism: int | None = None, max_polls: int | None = None,
-                  monitor: str = "coordinator") -> "DataStream":
+                  monitor: str = "coordinator", read_threads: int = 8) -> "DataStream":
         """``StreamExecutionEnvironment.readFile`` (``EX/inception/inception.scala:33-34``)
         as Flink builds it: one monitor (parallelism 1, in the coordinator) forwarding the
         new files' paths round-robin to ``parallelism`` readers (default: the
@@ -188,7 +188,8 @@ class StreamExecutionEnvironment:
             # one listing + reading source subtask per reader (``PartitionedFileSource``):
             # relocated into the worker process of the operator it feeds, so nothing
             # crosses the coordinator
-            return self.add_source(PartitionedFileSource(fmt, path, mode, interval_s, max_polls), "file-source",
+            return self.add_source(PartitionedFileSource(fmt, path, mode, interval_s, max_polls,
+                                                         read_threads=read_threads), "file-source",
                                    parallelism or self.parallelism)
         if monitor != "coordinator":
             raise ValueError("read_file: monitor must be 'coordinator' or 'partitioned'")
