@@ -140,9 +140,9 @@ def main():
                          "of this script where there is one GPU; numbers from such runs are not results")
     ap.add_argument("--lanes", type=int, default=None,
                     help="compute lanes: independent plan instances on their own HIP streams, batches round-robin "
-                         "(default: 3 for bert / bert_graph and inception_v3, 2 otherwise; measured in "
-                         "profiles/r01_lanes, r05_m: Inception-v3 fp8 +3.7 %% static / +7.6 %% dynamic at 3, "
-                         "ResNet-50 no better)")
+                         "(default: 3 for inception_v3, 2 otherwise; measured in profiles/r01_lanes, r05_m, "
+                         "r06_lanes: Inception-v3 fp8 +3.7 %% static / +7.6 %% dynamic at 3, -12 %% at 4; "
+                         "ResNet-50 -2 %% at 3; BERT-base +0.4 %% and p50 26.5 -> 20.5 ms at 2 instead of 3)")
     ap.add_argument("--no-interleave", action="store_true",
                     help="A/B: launch a batch's per-piece head kernels after the whole host gather instead of "
                          "interleaved with it")
@@ -212,7 +212,7 @@ def main():
     from flink_tensorflow_amd.batching.arena import DeviceArena
     from flink_tensorflow_amd.config import EngineConfig
 
-    lanes = args.lanes or (3 if args.model in ("bert", "bert_graph", "inception_v3") else 2)
+    lanes = args.lanes or (3 if args.model == "inception_v3" else 2)
     budget = EngineConfig().arena_bytes(dev) // lanes  # this subtask's HBM share, split over its lanes
     lane_plans, params = [], []
     if args.model == "inception_v3":
@@ -511,7 +511,7 @@ def run_job(args):
 
             cfg = BertConfig.base()
             seq = args.seq_len
-            lanes = args.lanes or 3
+            lanes = args.lanes or 2
             sm = export_bert_saved_model(os.path.join(out_dir, "bert_savedmodel"), cfg, seq, seed=0,
                                          mask_from_ids=True)
             model = JobModel(sm, output_keys=["logits"], buckets=(B,), lanes=lanes, depth=args.depth,
