@@ -387,8 +387,8 @@ class _GroupBound:
     whichever thread makes the call (task loop, chain timer)."""
 
     _CALLS = ("setup", "initialize", "open", "close", "process", "process_batch", "process_many", "process_watermark",
-              "on_idle",
-              "next_deadline", "end_input", "prepare_snapshot", "snapshot_state", "notify_checkpoint_complete")
+              "on_idle", "next_deadline", "end_input", "prepare_snapshot", "snapshot_state",
+              "notify_checkpoint_complete")
 
     def __init__(self, op, group):
         self.__dict__["_op"], self.__dict__["_group"] = op, group
