@@ -82,7 +82,7 @@ class PipelinedGpuRunner:
     def __init__(self, plans, feed: str, fetch_bufs: Callable[[Any], Sequence[torch.Tensor]],
                  record_shape, record_dtype=torch.uint8, depth: int = 3, device=None, gather_threads: int = 8,
                  stage_chunk: int = 64, lane_offset_us: float = 0.0, freeze_gc: bool = True, timeline: bool = False,
-                 interleave_head: bool = True, decode_threads: int = 16, async_decode: bool = True):
+                 interleave_head: bool = True, decode_threads: int | None = None, async_decode: bool = True):
         lanes = plans if isinstance(plans, (list, tuple)) else [plans]
         self.lanes = [dict(sorted(p.items())) for p in lanes]
         self.plans = self.lanes[0]
@@ -104,6 +104,12 @@ class PipelinedGpuRunner:
         self.gather_threads = gather_threads
         # records that arrive as compressed JPEG bytes (``ImageInputFormat(defer_decode=True)``)
         # are decoded by the native pool straight into the pinned rows (csrc/jpeg.cpp)
+        # (None: 32, at most the CPUs this process may run on — 32 measured best on the
+        # MI355X box, 64 oversubscribed it: profiles/r06_jpeg)
+        if decode_threads is None:
+            import os
+
+            decode_threads = max(1, min(32, len(os.sched_getaffinity(0))))
         self.decode_threads = decode_threads
         self.decode_fallbacks = 0
         self.async_decode = async_decode

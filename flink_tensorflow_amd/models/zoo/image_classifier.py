@@ -87,7 +87,7 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
             self._runner = PipelinedGpuRunner(lanes, self.feed, lambda p: p.output_tensors(), (H, W, 3),
                                               torch.uint8, depth=self.depth, device=dev,
                                               lane_offset_us=getattr(self, "lane_offset_us", 0.0),
-                                              decode_threads=getattr(self, "decode_threads", 16))
+                                              decode_threads=getattr(self, "decode_threads", None))
 
     def _calibration(self, b: int):
         if self.precision != "fp8" or self.calibration_images is None:
@@ -174,7 +174,7 @@ class ImageClassifierModel(GenericModel, BatchedGpuModel):
 
             H, W = self.image_hw
             blobs = [a for a in arrs if isinstance(a, (bytes, bytearray))]
-            dec = iter(decode_jpegs(blobs, H, W, getattr(self, "decode_threads", 16)))
+            dec = iter(decode_jpegs(blobs, H, W, getattr(self, "decode_threads", None) or 8))
             arrs = [next(dec) if isinstance(a, (bytes, bytearray)) else a for a in arrs]
         arrs = np.stack(arrs)
         sess = self.session()
