@@ -288,3 +288,32 @@ def test_partitioned_monitor_restart_reads_every_file_once(tmp_path):
         got[name] = max(got.get(name, 0), count)
     assert sorted(got) == [f"f{i:02d}.bin" for i in range(40)]
     assert set(got.values()) == {1}
+
+
+def test_partitioned_source_reads_non_local_filesystems():
+    """A ``mem://`` directory: the partitioned source lists and reads through the file-system
+    registry (no native bulk read), same split rule."""
+    from flink_tensorflow_amd.runtime.sources import BytesInputFormat, PartitionedFileSource
+    from flink_tensorflow_amd.utils import fs
+
+    for i in range(12):
+        fs.write_bytes(f"mem://ptest/in/f{i:02d}.bin", bytes([i]) * 2)
+
+    class Ctx:
+        def __init__(self, idx, par):
+            self.subtask_index, self.parallelism = idx, par
+            self.checkpoint_lock = threading.RLock()
+            self.got = []
+
+        def collect_many(self, values, timestamp=None):
+            self.got += values
+
+    got = []
+    for idx in range(2):
+        src = PartitionedFileSource(BytesInputFormat(), "mem://ptest/in", PROCESS_ONCE, run=5)
+        ctx = Ctx(idx, 2)
+        src.set_runtime_context(ctx)
+        src.open()
+        src.run(ctx)
+        got += [(p.rsplit("/", 1)[1], d) for p, d in ctx.got]
+    assert sorted(got) == [(f"f{i:02d}.bin", bytes([i]) * 2) for i in range(12)]
